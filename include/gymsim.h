@@ -1,0 +1,147 @@
+/*
+ * gymsim.h -- C ABI of libgymsim.so, the MI355X-native simulator behind the
+ * `isaacgym.gymapi` / `gymtorch` surface.
+ *
+ * The reference reaches its (closed, CUDA/PhysX) simulator only through the
+ * Isaac Gym Python binding; every entry point below replaces one call the
+ * reference's task layer makes on `self.gym`.  The
+ * Python shim in isaacgymenv_amd/isaacgym/gymapi.py binds these with ctypes
+ * (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - plain pointers and sizes; no torch types.  Device pointers are HIP
+ *     device addresses (torch.Tensor.data_ptr() on cuda:k); `stream` is a
+ *     hipStream_t passed as void* (0 = default stream).
+ *   - every function returns int status, 0 = ok; on error gs_last_error()
+ *     returns a message.  gs_sim_create returns NULL on failure, the caller's
+ *     `create_sim` returns None (vec_task.py:338-340).
+ *   - a gs_sim is not thread safe; all work is stream ordered (no host sync)
+ *     except gs_sim_create / gs_sim_set_model / gs_sim_prepare.
+ *   - tensor layouts are the reference's (AoS, float32):
+ *       root state  [num_envs][13]  pos(3) quat xyzw(4) lin vel of COM(3) ang vel(3)
+ *       dof state   [num_envs*num_dofs][2] (pos, vel)
+ *       dof force   [num_envs*num_dofs]
+ *       net contact [num_envs*num_bodies][3]
+ *     (one articulation actor per env; actor index == env index)
+ */
+#ifndef GYMSIM_H
+#define GYMSIM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_ABI_VERSION 1
+
+typedef struct gs_sim gs_sim;
+
+/* Articulation description after asset import (double precision on the host).
+ * Built by isaacgymenv_amd/isaacgym/_model.py:flatten(). */
+typedef struct gs_model_desc {
+    int32_t num_bodies, num_dofs, num_candidates, num_shapes, fixed_base;
+    const int32_t *parent;        /* [nb] body parent, -1 root                          */
+    const int32_t *joint_kind;    /* [nb] 1 revolute, 2 prismatic, root 3 free / 0 fixed */
+    const int32_t *body_dof;      /* [nb] dof moved by the body's joint, -1 root        */
+    const double *joint_origin;   /* [nb][12] parent frame -> joint frame: R (9) t (3)  */
+    const double *joint_axis;     /* [nb][3] in the joint frame                         */
+    const double *mass;           /* [nb]                                               */
+    const double *com;            /* [nb][3] body frame                                 */
+    const double *inertia;        /* [nb][9] about COM, body axes                       */
+    const int32_t *cand_body;     /* [nc] contact candidate: body                       */
+    const double *cand_point;     /* [nc][3] body frame                                 */
+    const double *cand_radius;    /* [nc]                                               */
+    const int32_t *cand_shape;    /* [nc] shape index (friction lookup)                 */
+    const double *dof_effort;     /* [nd] max |force|, <= 0 unlimited                   */
+    const double *dof_velocity;   /* [nd] max |vel|, <= 0 unlimited                     */
+    const double *dof_armature;   /* [nd]                                               */
+} gs_model_desc;
+
+/* gymapi.SimParams subset the reference sets (vec_task.py:514-562). */
+typedef struct gs_sim_params {
+    double dt;
+    int32_t substeps;
+    double gravity[3];
+    int32_t num_position_iterations;
+    int32_t num_velocity_iterations;
+    double contact_offset;
+    double rest_offset;
+    double bounce_threshold_velocity;   /* accepted, restitution is 0 in every in-scope task */
+    double max_depenetration_velocity;
+    int32_t contact_collection;         /* 0 never, 1 last substep (2 treated as 1)        */
+} gs_sim_params;
+
+/* Fused PD decimation step (AnymalTerrain.pre_physics_step + VecTask.step's
+ * simulate loop, anymal_terrain.py:441-451 + vec_task.py:379-382):
+ *   repeat `decimation` times:
+ *     torque = clip(kp*(action_scale*a + default_pos - q) - kd*qd, +-torque_limit)
+ *     simulate()                                  (sim dt, `substeps`)
+ *   then `extra_simulates` more simulate() with the last torque.
+ *   Outputs mirror the refresh calls the reference makes: dof state after the
+ *   decimation loop (refresh_dof_state_tensor inside the loop), root state and
+ *   contact forces after the extra simulates (post_physics_step refreshes). */
+typedef struct gs_pd_args {
+    const float *actions;        /* [N][nd]                      */
+    const float *default_pos;    /* [nd]  (device)               */
+    float kp, kd, action_scale, torque_limit;
+    int32_t decimation;
+    int32_t extra_simulates;
+    float *torques_out;          /* [N][nd]  last applied torque */
+    float *dof_state_out;        /* [N*nd][2] or NULL            */
+    float *root_state_out;       /* [N][13]   or NULL            */
+    float *contact_out;          /* [N*nb][3] or NULL            */
+} gs_pd_args;
+
+int gs_abi_version(void);
+const char *gs_last_error(void);
+
+/* 1 if libgymsim was compiled with a specialised kernel for this topology. */
+int gs_topology_supported(const gs_model_desc *model);
+
+/* gym.create_sim(compute_device, graphics_device, SIM_PHYSX, sim_params)   vec_task.py:337 */
+gs_sim *gs_sim_create(int device, const gs_sim_params *params);
+void gs_sim_destroy(gs_sim *sim);
+
+/* gym.add_ground(sim, PlaneParams)   anymal_terrain.py:188-194 (z-up plane only) */
+int gs_sim_add_ground(gs_sim *sim, double static_friction, double dynamic_friction, double restitution);
+
+/* gym.load_asset + create_actor for every env (one articulation type per sim)
+ * anymal_terrain.py:231,282  cartpole.py:88,106 */
+int gs_sim_set_model(gs_sim *sim, const gs_model_desc *model);
+
+/* gym.prepare_sim(sim)   vec_task.py:262.
+ * Binds caller-owned device buffers:
+ *   state   [13 + 2*nd][N]  SoA sim state: pos(3) quat(4) v_origin(3) w(3) q(nd) qd(nd)
+ *   shape_friction [ns][N]  per-env shape friction (anymal_terrain.py:279-281)
+ *   contact [3*nb][N]       SoA net contact force of the last collected substep
+ * The initial state must already be in `state`. */
+int gs_sim_prepare(gs_sim *sim, int num_envs, float *state, const float *shape_friction, float *contact);
+
+/* gym.simulate(sim) with dof actuation forces [N*nd] (set_dof_actuation_force_tensor,
+ * anymal_terrain.py:446-448, vec_task.py:382).  `dof_force` may be NULL (zero). */
+int gs_sim_simulate(gs_sim *sim, const float *dof_force, void *stream);
+
+/* refresh_*_tensor: sim state -> reference-layout tensors (anymal_terrain.py:451,455,456) */
+int gs_sim_refresh_root(gs_sim *sim, float *root_state, void *stream);
+int gs_sim_refresh_dof(gs_sim *sim, float *dof_state, void *stream);
+int gs_sim_refresh_contact(gs_sim *sim, float *net_contact, void *stream);
+
+/* set_actor_root_state_tensor(_indexed) / set_dof_state_tensor(_indexed):
+ * rows `idx[0..n_idx)` (int32 actor ids) of the full source tensor; idx NULL = all envs.
+ * anymal_terrain.py:401-407, 439 */
+int gs_sim_set_root(gs_sim *sim, const float *root_state, const int32_t *idx, int n_idx, void *stream);
+int gs_sim_set_dof(gs_sim *sim, const float *dof_state, const int32_t *idx, int n_idx, void *stream);
+
+/* Fused decimation step, see gs_pd_args. */
+int gs_sim_pd_step(gs_sim *sim, const gs_pd_args *args, void *stream);
+
+/* Kernel time of the last gs_sim_pd_step / gs_sim_simulate launch measured with
+ * HIP events on `stream` (ms); -1 if not recorded.  Used by bench.py. */
+int gs_sim_enable_timing(gs_sim *sim, int enable);
+float gs_sim_last_kernel_ms(gs_sim *sim);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GYMSIM_H */

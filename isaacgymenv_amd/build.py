@@ -1,0 +1,66 @@
+"""Build the native libraries in-tree (hipcc, gfx950).
+
+    python -m isaacgymenv_amd.build          # all libraries
+Outputs ``isaacgymenv_amd/_lib/libgymsim.so`` (physics + tensor API) and
+``isaacgymenv_amd/_lib/libgymtask.so`` (fused task kernels).  Built .so files
+are git-ignored but travel to the GPU box with the repo snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "_lib")
+ARCH = os.environ.get("GS_OFFLOAD_ARCH", "gfx950")
+
+LIBS = {
+    "libgymsim.so": ["gs_physics.hip", "gs_capi.hip"],
+    "libgymtask.so": ["gt_anymal.hip", "gt_capi.hip"],
+}
+HEADERS = ["gs_internal.h", "gs_topologies.h", "gt_internal.h"]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _stale(out: str, srcs) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    deps = [os.path.join(CSRC, s) for s in srcs] + [os.path.join(CSRC, h) for h in HEADERS]
+    deps.append(os.path.join(os.path.dirname(HERE), "include", "gymsim.h"))
+    deps.append(os.path.join(os.path.dirname(HERE), "include", "gymtask.h"))
+    return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = True) -> None:
+    os.makedirs(LIBDIR, exist_ok=True)
+    cc = hipcc()
+    for lib, srcs in LIBS.items():
+        if not all(os.path.exists(os.path.join(CSRC, s)) for s in srcs):
+            raise RuntimeError(f"missing sources for {lib}: {srcs}")
+        out = os.path.join(LIBDIR, lib)
+        if not force and not _stale(out, srcs):
+            continue
+        cmd = [cc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-I", os.path.join(os.path.dirname(HERE), "include"), "-I", CSRC, "-o", out]
+        cmd += [os.path.join(CSRC, s) for s in srcs]
+        if verbose:
+            print("[build]", " ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {lib}:\n{r.stdout}\n{r.stderr}")
+        if verbose and r.stderr.strip():
+            print(r.stderr[-4000:], file=sys.stderr)
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,263 @@
+// gs_capi.hip -- the C ABI of libgymsim.so (include/gymsim.h).
+//
+// Host-side object that replaces the Isaac Gym `sim` handle: it owns the
+// float32 device copy of the articulation model, the parsed SimParams and the
+// selected kernel specialisation, and binds the caller-owned (torch) device
+// buffers that hold the sim state.  All launches are stream ordered; nothing
+// here synchronises the host except create/set_model/prepare.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gs_internal.h"
+#include "../../include/gymsim.h"
+
+namespace {
+thread_local std::string g_err;
+
+int fail(const char* fmt, const char* arg = nullptr) {
+  char buf[512];
+  std::snprintf(buf, sizeof(buf), fmt, arg ? arg : "");
+  g_err = buf;
+  return -1;
+}
+int hip_fail(hipError_t e, const char* where) {
+  char buf[512];
+  std::snprintf(buf, sizeof(buf), "%s: %s", where, hipGetErrorString(e));
+  g_err = buf;
+  return -1;
+}
+
+std::string signature(const gs_model_desc* m) {
+  std::string s = "fb" + std::to_string(m->fixed_base) + "_p";
+  for (int i = 0; i < m->num_bodies; ++i) s += (i ? "-" : "") + std::to_string(m->parent[i]);
+  s += "_c";
+  for (int i = 0; i < m->num_candidates; ++i) s += (i ? "-" : "") + std::to_string(m->cand_body[i]);
+  return s;
+}
+
+const TopoEntry* find_topology(const gs_model_desc* m) {
+  const std::string sig = signature(m);
+  for (int i = 0; i < g_num_topologies; ++i)
+    if (sig == g_topologies[i].sig) return &g_topologies[i];
+  return nullptr;
+}
+}  // namespace
+
+struct gs_sim {
+  int device = 0;
+  gs_sim_params params{};
+  DevParams dp{};
+  bool has_ground = false;
+  float ground_mu = 1.f;
+  const TopoEntry* topo = nullptr;
+  DevModel* d_model = nullptr;
+  int nb = 0, nd = 0, nc = 0, ns = 0;
+  int N = 0;
+  float* state = nullptr;
+  const float* mu = nullptr;
+  float* cf = nullptr;
+  bool timing = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+};
+
+extern "C" {
+
+int gs_abi_version(void) { return GS_ABI_VERSION; }
+const char* gs_last_error(void) { return g_err.c_str(); }
+
+int gs_topology_supported(const gs_model_desc* model) { return find_topology(model) != nullptr; }
+
+gs_sim* gs_sim_create(int device, const gs_sim_params* p) {
+  if (!p) { fail("gs_sim_create: null params"); return nullptr; }
+  if (!(p->dt > 0)) { fail("gs_sim_create: dt must be > 0"); return nullptr; }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+    fail("gs_sim_create: no HIP device %s", std::to_string(device).c_str());
+    return nullptr;
+  }
+  hipSetDevice(device);
+  gs_sim* s = new gs_sim();
+  s->device = device;
+  s->params = *p;
+  const int sub = p->substeps > 0 ? p->substeps : 1;
+  s->dp.h = (float)(p->dt / sub);
+  s->dp.substeps = sub;
+  for (int k = 0; k < 3; ++k) s->dp.g[k] = (float)p->gravity[k];
+  s->dp.pos_iters = p->num_position_iterations;
+  s->dp.vel_iters = p->num_velocity_iterations;
+  s->dp.contact_offset = (float)p->contact_offset;
+  s->dp.rest_offset = (float)p->rest_offset;
+  s->dp.max_depen_vel = (float)p->max_depenetration_velocity;
+  s->dp.collect = p->contact_collection != 0;
+  s->dp.has_ground = 0;
+  s->dp.ground_mu = 1.f;
+  return s;
+}
+
+void gs_sim_destroy(gs_sim* s) {
+  if (!s) return;
+  hipSetDevice(s->device);
+  if (s->d_model) hipFree(s->d_model);
+  if (s->ev0) hipEventDestroy(s->ev0);
+  if (s->ev1) hipEventDestroy(s->ev1);
+  delete s;
+}
+
+int gs_sim_add_ground(gs_sim* s, double static_friction, double dynamic_friction, double restitution) {
+  if (!s) return fail("gs_sim_add_ground: null sim");
+  (void)dynamic_friction;
+  (void)restitution;
+  s->has_ground = true;
+  s->dp.has_ground = 1;
+  s->dp.ground_mu = (float)static_friction;
+  return 0;
+}
+
+int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
+  if (!s || !m) return fail("gs_sim_set_model: null argument");
+  if (m->num_bodies > GS_MAXB || m->num_dofs > GS_MAXD || m->num_candidates > GS_MAXC)
+    return fail("gs_sim_set_model: articulation exceeds compiled maxima (bodies/dofs/candidates)");
+  const TopoEntry* t = find_topology(m);
+  if (!t)
+    return fail("gs_sim_set_model: no compiled kernel for topology %s (add it to tools/gen_topologies.py)",
+                signature(m).c_str());
+  DevModel h;
+  std::memset(&h, 0, sizeof(h));
+  for (int i = 0; i < m->num_bodies; ++i) {
+    for (int k = 0; k < 9; ++k) h.jR[i][k] = (float)m->joint_origin[12 * i + k];
+    for (int k = 0; k < 3; ++k) h.jt[i][k] = (float)m->joint_origin[12 * i + 9 + k];
+    for (int k = 0; k < 3; ++k) h.jaxis[i][k] = (float)m->joint_axis[3 * i + k];
+    h.mass[i] = (float)m->mass[i];
+    for (int k = 0; k < 3; ++k) h.com[i][k] = (float)m->com[3 * i + k];
+    const double* I = m->inertia + 9 * i;
+    h.inertia[i][0] = (float)I[0]; h.inertia[i][1] = (float)I[4]; h.inertia[i][2] = (float)I[8];
+    h.inertia[i][3] = (float)I[1]; h.inertia[i][4] = (float)I[2]; h.inertia[i][5] = (float)I[5];
+  }
+  for (int c = 0; c < m->num_candidates; ++c) {
+    for (int k = 0; k < 3; ++k) h.cpoint[c][k] = (float)m->cand_point[3 * c + k];
+    h.cradius[c] = (float)m->cand_radius[c];
+  }
+  for (int j = 0; j < m->num_dofs; ++j) {
+    h.effort[j] = (float)m->dof_effort[j];
+    h.vmax[j] = (float)m->dof_velocity[j];
+    h.armature[j] = (float)m->dof_armature[j];
+  }
+  hipSetDevice(s->device);
+  if (!s->d_model) {
+    hipError_t e = hipMalloc(&s->d_model, sizeof(DevModel));
+    if (e != hipSuccess) return hip_fail(e, "gs_sim_set_model hipMalloc");
+  }
+  hipError_t e = hipMemcpy(s->d_model, &h, sizeof(DevModel), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "gs_sim_set_model hipMemcpy");
+  s->topo = t;
+  s->nb = m->num_bodies;
+  s->nd = m->num_dofs;
+  s->nc = m->num_candidates;
+  s->ns = m->num_shapes;
+  return 0;
+}
+
+int gs_sim_prepare(gs_sim* s, int num_envs, float* state, const float* shape_friction, float* contact) {
+  if (!s || !s->topo) return fail("gs_sim_prepare: model not set");
+  if (num_envs <= 0 || !state || !shape_friction || !contact) return fail("gs_sim_prepare: bad buffers");
+  s->N = num_envs;
+  s->state = state;
+  s->mu = shape_friction;
+  s->cf = contact;
+  return 0;
+}
+
+static SimBuffers buffers(gs_sim* s) { return SimBuffers{s->state, s->mu, s->cf, s->N}; }
+
+static int ready(gs_sim* s, const char* where) {
+  if (!s || !s->topo || !s->state) return fail("%s: sim not prepared", where);
+  return 0;
+}
+
+static void timing_begin(gs_sim* s, hipStream_t st) {
+  if (!s->timing) return;
+  if (!s->ev0) { hipEventCreate(&s->ev0); hipEventCreate(&s->ev1); }
+  hipEventRecord(s->ev0, st);
+}
+static void timing_end(gs_sim* s, hipStream_t st) {
+  if (!s->timing) return;
+  hipEventRecord(s->ev1, st);
+  s->timed = true;
+}
+
+int gs_sim_simulate(gs_sim* s, const float* dof_force, void* stream) {
+  if (ready(s, "gs_sim_simulate")) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  timing_begin(s, st);
+  hipError_t e = s->topo->sim(s->d_model, s->dp, buffers(s), dof_force, st);
+  timing_end(s, st);
+  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_simulate");
+}
+
+int gs_sim_pd_step(gs_sim* s, const gs_pd_args* a, void* stream) {
+  if (ready(s, "gs_sim_pd_step")) return -1;
+  if (!a || !a->actions || !a->default_pos || !a->torques_out || !a->dof_state_out)
+    return fail("gs_sim_pd_step: actions/default_pos/torques_out/dof_state_out required");
+  PdDev d;
+  d.actions = a->actions;
+  d.dof_state_in = a->dof_state_out;
+  d.default_pos = a->default_pos;
+  d.kp = a->kp; d.kd = a->kd; d.scale = a->action_scale; d.tlim = a->torque_limit;
+  d.decimation = a->decimation;
+  d.extra = a->extra_simulates;
+  d.torques_out = a->torques_out;
+  d.dof_out = a->dof_state_out;
+  d.root_out = a->root_state_out;
+  d.cf_out = a->contact_out;
+  hipStream_t st = (hipStream_t)stream;
+  timing_begin(s, st);
+  hipError_t e = s->topo->pd(s->d_model, s->dp, buffers(s), d, st);
+  timing_end(s, st);
+  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_pd_step");
+}
+
+int gs_sim_refresh_root(gs_sim* s, float* out, void* stream) {
+  if (ready(s, "gs_sim_refresh_root")) return -1;
+  hipError_t e = launch_refresh_root(s->state, s->N, s->nd, &s->d_model->com[0][0], out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_root");
+}
+int gs_sim_refresh_dof(gs_sim* s, float* out, void* stream) {
+  if (ready(s, "gs_sim_refresh_dof")) return -1;
+  hipError_t e = launch_refresh_dof(s->state, s->N, s->nd, out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_dof");
+}
+int gs_sim_refresh_contact(gs_sim* s, float* out, void* stream) {
+  if (ready(s, "gs_sim_refresh_contact")) return -1;
+  hipError_t e = launch_refresh_contact(s->cf, s->N, s->nb, out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_contact");
+}
+int gs_sim_set_root(gs_sim* s, const float* src, const int32_t* idx, int n_idx, void* stream) {
+  if (ready(s, "gs_sim_set_root")) return -1;
+  hipError_t e = launch_set_root(s->state, s->N, s->nd, &s->d_model->com[0][0], src, idx, n_idx,
+                                 (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_set_root");
+}
+int gs_sim_set_dof(gs_sim* s, const float* src, const int32_t* idx, int n_idx, void* stream) {
+  if (ready(s, "gs_sim_set_dof")) return -1;
+  hipError_t e = launch_set_dof(s->state, s->N, s->nd, src, idx, n_idx, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_set_dof");
+}
+
+int gs_sim_enable_timing(gs_sim* s, int enable) {
+  if (!s) return fail("gs_sim_enable_timing: null sim");
+  s->timing = enable != 0;
+  return 0;
+}
+float gs_sim_last_kernel_ms(gs_sim* s) {
+  if (!s || !s->timed) return -1.f;
+  float ms = -1.f;
+  if (hipEventSynchronize(s->ev1) != hipSuccess) return -1.f;
+  if (hipEventElapsedTime(&ms, s->ev0, s->ev1) != hipSuccess) return -1.f;
+  return ms;
+}
+
+}  // extern "C"

@@ -1,0 +1,83 @@
+// Internal (non-ABI) declarations shared by the kernels and the C-ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#define GS_MAXB 32   // bodies per articulation
+#define GS_MAXD 32   // dofs per articulation
+#define GS_MAXC 64   // plane-contact candidates per articulation
+#define GS_WAVE 64
+
+// Model constants shared by every env, float32, one copy in device memory.
+// Kernels index it with compile-time body / candidate indices from a uniform
+// pointer, so every read lowers to a scalar (SGPR) load.
+struct DevModel {
+  float jR[GS_MAXB][9];      // parent frame -> joint frame rotation, row major
+  float jt[GS_MAXB][3];      // parent frame -> joint frame translation
+  float jaxis[GS_MAXB][3];   // joint axis in the joint frame
+  float mass[GS_MAXB];
+  float com[GS_MAXB][3];     // body frame
+  float inertia[GS_MAXB][6]; // about COM, body axes: xx yy zz xy xz yz
+  float cpoint[GS_MAXC][3];  // contact candidate, body frame
+  float cradius[GS_MAXC];
+  float effort[GS_MAXD];     // <= 0 : unlimited
+  float vmax[GS_MAXD];       // <= 0 : unlimited
+  float armature[GS_MAXD];
+};
+
+struct DevParams {
+  float h;               // substep length = dt / substeps
+  int substeps;
+  float g[3];
+  int pos_iters, vel_iters;
+  float contact_offset, rest_offset, max_depen_vel;
+  float ground_mu;       // ground plane friction (0.5*(mu_shape + mu_ground) is the pair friction)
+  int has_ground;
+  int collect;           // contact_collection != 0
+};
+
+// SoA state: field f of env e at state[f*N + e]
+//   0..2 root pos, 3..6 quat xyzw, 7..9 root ORIGIN lin vel, 10..12 ang vel,
+//   13..13+nd-1 dof pos, 13+nd..13+2nd-1 dof vel
+struct SimBuffers {
+  float* state;
+  const float* mu;       // [ns][N]
+  float* cf;             // [3*nb][N]
+  int N;
+};
+
+struct PdDev {
+  const float* actions;      // [N][nd]
+  const float* dof_state_in; // [N*nd][2] dof tensor as the task sees it (first PD uses it)
+  const float* default_pos;  // [nd]
+  float kp, kd, scale, tlim;
+  int decimation, extra;
+  float* torques_out;        // [N][nd]
+  float* dof_out;            // [N*nd][2] or null
+  float* root_out;           // [N][13]   or null
+  float* cf_out;             // [N*nb][3] or null
+};
+
+typedef hipError_t (*launch_sim_fn)(const DevModel*, const DevParams&, const SimBuffers&, const float* tau,
+                                    hipStream_t);
+typedef hipError_t (*launch_pd_fn)(const DevModel*, const DevParams&, const SimBuffers&, const PdDev&,
+                                   hipStream_t);
+
+struct TopoEntry {
+  const char* sig;
+  const char* name;
+  launch_sim_fn sim;
+  launch_pd_fn pd;
+  int nb, nd, nc, ns;
+};
+
+extern TopoEntry g_topologies[];
+extern const int g_num_topologies;
+
+// generic (runtime-sized) tensor API kernels
+hipError_t launch_refresh_root(const float* state, int N, int nd, const float* com0, float* out, hipStream_t s);
+hipError_t launch_refresh_dof(const float* state, int N, int nd, float* out, hipStream_t s);
+hipError_t launch_refresh_contact(const float* cf, int N, int nb, float* out, hipStream_t s);
+hipError_t launch_set_root(float* state, int N, int nd, const float* com0, const float* src, const int* idx,
+                           int n_idx, hipStream_t s);
+hipError_t launch_set_dof(float* state, int N, int nd, const float* src, const int* idx, int n_idx,
+                          hipStream_t s);

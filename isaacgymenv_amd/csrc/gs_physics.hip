@@ -1,0 +1,810 @@
+// gs_physics.hip -- articulation dynamics + plane contact solve for gfx950.
+//
+// Replaces the PhysX GPU articulation/contact pipeline that the reference runs
+// inside `gym.simulate` (vec_task.py:382, anymal_terrain.py:448).  The solver
+// specification is shared with the fp64 CPU oracle in
+// oracle/physics_oracle.c, which is written independently (dense Cholesky,
+// joint-space impulses); this file is the MI355X form:
+//
+//   * one env per lane, 64 envs per wave / workgroup; state loads and stores
+//     are SoA so every wave-instruction moves 256 contiguous bytes;
+//   * the articulation topology is a template parameter (gs_topologies.h), all
+//     tree walks unroll at compile time and the per-body quantities (poses,
+//     motion subspaces, composite inertias, the L^T D L factor of the mass
+//     matrix) live in VGPRs;
+//   * contact rows are staged in LDS ([slot][lane], conflict-free) because
+//     their count (3 per candidate) would not fit the register file;
+//   * model constants are read through a uniform pointer -> SGPR loads.
+//
+// Per substep (h = dt / substeps):
+//   FK -> spatial inertias at the root origin O -> RNEA bias (gravity as base
+//   acceleration) -> CRBA mass matrix -> tree-sparse L^T D L -> free velocity
+//   -> plane contact candidates (contact_offset) -> per row scaled
+//   Z = J L^-1 D^-1/2 -> projected Gauss-Seidel in w-space
+//   (pos iterations with depenetration bias, then velocity iterations without)
+//   -> velocity limits -> semi-implicit integration with the position-phase
+//   velocity; the velocity-phase velocity is kept as state.
+#include "gs_internal.h"
+#include "gs_topologies.h"
+
+namespace {
+
+__device__ __forceinline__ void cross3(const float* a, const float* b, float* o) {
+  const float x = a[1] * b[2] - a[2] * b[1];
+  const float y = a[2] * b[0] - a[0] * b[2];
+  const float z = a[0] * b[1] - a[1] * b[0];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+__device__ __forceinline__ void mat3vec(const float* R, const float* v, float* o) {
+  const float x = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
+  const float y = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
+  const float z = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
+  o[0] = x; o[1] = y; o[2] = z;
+}
+__device__ __forceinline__ void mat3mul(const float* A, const float* B, float* C) {
+  float T[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) T[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) C[k] = T[k];
+}
+__device__ __forceinline__ void quat_to_mat(const float* q, float* R) {
+  const float x = q[0], y = q[1], z = q[2], w = q[3];
+  R[0] = 1.f - 2.f * (y * y + z * z); R[1] = 2.f * (x * y - z * w);       R[2] = 2.f * (x * z + y * w);
+  R[3] = 2.f * (x * y + z * w);       R[4] = 1.f - 2.f * (x * x + z * z); R[5] = 2.f * (y * z - x * w);
+  R[6] = 2.f * (x * z - y * w);       R[7] = 2.f * (y * z + x * w);       R[8] = 1.f - 2.f * (x * x + y * y);
+}
+
+// spatial inertia about O in world axes: f = (I w + h x v, m v - h x w)
+struct SpI {
+  float m, h[3], I[6];  // I: xx yy zz xy xz yz
+};
+__device__ __forceinline__ void spi_mul(const SpI& I, const float* mv, float* f) {
+  const float n0 = I.I[0] * mv[0] + I.I[3] * mv[1] + I.I[4] * mv[2];
+  const float n1 = I.I[3] * mv[0] + I.I[1] * mv[1] + I.I[5] * mv[2];
+  const float n2 = I.I[4] * mv[0] + I.I[5] * mv[1] + I.I[2] * mv[2];
+  float hv[3], hw[3];
+  cross3(I.h, mv + 3, hv);
+  cross3(I.h, mv, hw);
+  f[0] = n0 + hv[0]; f[1] = n1 + hv[1]; f[2] = n2 + hv[2];
+  f[3] = I.m * mv[3] - hw[0]; f[4] = I.m * mv[4] - hw[1]; f[5] = I.m * mv[5] - hw[2];
+}
+// motion x motion
+__device__ __forceinline__ void crm(const float* a, const float* b, float* o) {
+  float t1[3], t2[3], t3[3];
+  cross3(a, b, t1); cross3(a, b + 3, t2); cross3(a + 3, b, t3);
+  o[0] = t1[0]; o[1] = t1[1]; o[2] = t1[2];
+  o[3] = t2[0] + t3[0]; o[4] = t2[1] + t3[1]; o[5] = t2[2] + t3[2];
+}
+// motion x* force
+__device__ __forceinline__ void crf(const float* a, const float* b, float* o) {
+  float t1[3], t2[3], t3[3];
+  cross3(a, b, t1); cross3(a + 3, b + 3, t2); cross3(a, b + 3, t3);
+  o[0] = t1[0] + t2[0]; o[1] = t1[1] + t2[1]; o[2] = t1[2] + t2[2];
+  o[3] = t3[0]; o[4] = t3[1]; o[5] = t3[2];
+}
+__device__ __forceinline__ float dot6(const float* a, const float* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+
+// k-th node of the support path of a contact on the body moved by generalized dof
+// `leaf`: the leaf itself, then its ancestors towards the root.
+template <class T>
+__device__ __forceinline__ constexpr int supp_node(int leaf, int si) {
+  return si == 0 ? leaf : T::anc[leaf][si > 0 ? si - 1 : 0];
+}
+
+// Register-resident env state.
+template <class T>
+struct EnvState {
+  float p[3], quat[4], vo[3], w[3];
+  float q[T::ND > 0 ? T::ND : 1], qd[T::ND > 0 ? T::ND : 1];
+};
+
+template <class T>
+__device__ __forceinline__ void load_state(const float* __restrict__ st, int N, int e, EnvState<T>& s) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s.p[k] = st[k * N + e];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) s.quat[k] = st[(3 + k) * N + e];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s.vo[k] = st[(7 + k) * N + e];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s.w[k] = st[(10 + k) * N + e];
+#pragma unroll
+  for (int j = 0; j < T::ND; ++j) s.q[j] = st[(13 + j) * N + e];
+#pragma unroll
+  for (int j = 0; j < T::ND; ++j) s.qd[j] = st[(13 + T::ND + j) * N + e];
+}
+template <class T>
+__device__ __forceinline__ void store_state(float* __restrict__ st, int N, int e, const EnvState<T>& s) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) st[k * N + e] = s.p[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) st[(3 + k) * N + e] = s.quat[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) st[(7 + k) * N + e] = s.vo[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) st[(10 + k) * N + e] = s.w[k];
+#pragma unroll
+  for (int j = 0; j < T::ND; ++j) st[(13 + j) * N + e] = s.q[j];
+#pragma unroll
+  for (int j = 0; j < T::ND; ++j) st[(13 + T::ND + j) * N + e] = s.qd[j];
+}
+
+// One substep for one env.  `lds` points at this lane's column of the
+// workgroup's [NSLOT][64] contact-row staging area.
+//
+// Register budget: the tree is walked ONCE in DFS order.  Kinematics,
+// velocities, RNEA forces and composite inertias are accumulated post-order,
+// so only the bodies on the current root->leaf path are live at any time; a
+// body's bias force and its mass-matrix row are emitted the moment its subtree
+// is complete (T::subend).  Contact Jacobian rows are written to LDS during the
+// same walk (they need the path's motion subspaces) and turned into scaled
+// Z rows after the factorisation.
+template <class T>
+__device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvState<T>& s,
+                                        const float* tau, const float* mu, float* lds, float (*cf)[3],
+                                        bool collect) {
+  constexpr int NB = T::NB, NV = T::NV, NB6 = T::NBASE, NC = T::NC;
+  constexpr int MS = T::MAXDEP + 1;
+  // Keep the model pointer opaque per substep: the constants are re-read with
+  // scalar loads (K$ hits) instead of being hoisted out of the substep loop
+  // into hundreds of SGPRs.
+  uintptr_t mp = reinterpret_cast<uintptr_t>(Min);
+  asm volatile("" : "+s"(mp));
+  const DevModel* __restrict__ M = reinterpret_cast<const DevModel*>(mp);
+  const float h = P.h;
+
+  float nu[NV];
+  if (NB6) {
+    nu[0] = s.w[0]; nu[1] = s.w[1]; nu[2] = s.w[2];
+    nu[3] = s.vo[0]; nu[4] = s.vo[1]; nu[5] = s.vo[2];
+  }
+#pragma unroll
+  for (int j = 0; j < T::ND; ++j) nu[NB6 + j] = s.qd[j];
+
+  float R[NB][9], X[NB][3], S[NB][6], V[NB][6], A[NB][6], Fc[NB][6];
+  SpI Ic[NB];
+  float Mm[NV][NV], bias[NV];
+  bool act[NC];
+  float sep[NC], cmu[NC];
+
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    // ---- kinematics of body i (positions relative to the root origin)
+    if (i == 0) {
+      float qn[4];
+      const float inv = rsqrtf(s.quat[0] * s.quat[0] + s.quat[1] * s.quat[1] + s.quat[2] * s.quat[2] +
+                               s.quat[3] * s.quat[3]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) qn[k] = s.quat[k] * inv;
+      quat_to_mat(qn, R[0]);
+      X[0][0] = X[0][1] = X[0][2] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) V[0][k] = NB6 ? nu[k] : 0.f;
+      A[0][0] = A[0][1] = A[0][2] = 0.f;
+      A[0][3] = -P.g[0]; A[0][4] = -P.g[1]; A[0][5] = -P.g[2];
+    } else {
+      const int pa = T::parent[i];
+      float RJ[9], t[3], aw[3];
+      mat3mul(R[pa], M->jR[i], RJ);
+      mat3vec(R[pa], M->jt[i], t);
+      X[i][0] = X[pa][0] + t[0]; X[i][1] = X[pa][1] + t[1]; X[i][2] = X[pa][2] + t[2];
+      mat3vec(RJ, M->jaxis[i], aw);
+      const float qj = s.q[T::bdof[i]];
+      if (T::jkind[i] == 1) {
+        float sn, cs;
+        sincosf(qj, &sn, &cs);
+        const float* a = M->jaxis[i];
+        const float C = 1.f - cs;
+        float Rq[9];
+        Rq[0] = cs + a[0] * a[0] * C;        Rq[1] = a[0] * a[1] * C - a[2] * sn; Rq[2] = a[0] * a[2] * C + a[1] * sn;
+        Rq[3] = a[1] * a[0] * C + a[2] * sn; Rq[4] = cs + a[1] * a[1] * C;        Rq[5] = a[1] * a[2] * C - a[0] * sn;
+        Rq[6] = a[2] * a[0] * C - a[1] * sn; Rq[7] = a[2] * a[1] * C + a[0] * sn; Rq[8] = cs + a[2] * a[2] * C;
+        mat3mul(RJ, Rq, R[i]);
+        S[i][0] = aw[0]; S[i][1] = aw[1]; S[i][2] = aw[2];
+        cross3(X[i], aw, &S[i][3]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R[i][k] = RJ[k];
+        X[i][0] += aw[0] * qj; X[i][1] += aw[1] * qj; X[i][2] += aw[2] * qj;
+        S[i][0] = S[i][1] = S[i][2] = 0.f;
+        S[i][3] = aw[0]; S[i][4] = aw[1]; S[i][5] = aw[2];
+      }
+      const float qd = nu[NB6 + T::bdof[i]];
+      float c6[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) V[i][k] = V[pa][k] + S[i][k] * qd;
+      crm(V[i], S[i], c6);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) A[i][k] = A[pa][k] + c6[k] * qd;
+    }
+
+    // ---- spatial inertia of body i at O; RNEA force
+    {
+      float c[3];
+      mat3vec(R[i], M->com[i], c);
+      c[0] += X[i][0]; c[1] += X[i][1]; c[2] += X[i][2];
+      const float* Il = M->inertia[i];  // xx yy zz xy xz yz
+      const float* Rm = R[i];
+      float Am[9];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        Am[3 * r + 0] = Rm[3 * r] * Il[0] + Rm[3 * r + 1] * Il[3] + Rm[3 * r + 2] * Il[4];
+        Am[3 * r + 1] = Rm[3 * r] * Il[3] + Rm[3 * r + 1] * Il[1] + Rm[3 * r + 2] * Il[5];
+        Am[3 * r + 2] = Rm[3 * r] * Il[4] + Rm[3 * r + 1] * Il[5] + Rm[3 * r + 2] * Il[2];
+      }
+      const float m = M->mass[i];
+      const float cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+      SpI& I = Ic[i];
+      I.m = m;
+      I.h[0] = m * c[0]; I.h[1] = m * c[1]; I.h[2] = m * c[2];
+      I.I[0] = Am[0] * Rm[0] + Am[1] * Rm[1] + Am[2] * Rm[2] + m * (cc - c[0] * c[0]);
+      I.I[1] = Am[3] * Rm[3] + Am[4] * Rm[4] + Am[5] * Rm[5] + m * (cc - c[1] * c[1]);
+      I.I[2] = Am[6] * Rm[6] + Am[7] * Rm[7] + Am[8] * Rm[8] + m * (cc - c[2] * c[2]);
+      I.I[3] = Am[0] * Rm[3] + Am[1] * Rm[4] + Am[2] * Rm[5] - m * c[0] * c[1];
+      I.I[4] = Am[0] * Rm[6] + Am[1] * Rm[7] + Am[2] * Rm[8] - m * c[0] * c[2];
+      I.I[5] = Am[3] * Rm[6] + Am[4] * Rm[7] + Am[5] * Rm[8] - m * c[1] * c[2];
+      float ia[6], iv[6], x6[6];
+      spi_mul(I, A[i], ia);
+      spi_mul(I, V[i], iv);
+      crf(V[i], iv, x6);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) Fc[i][k] = ia[k] + x6[k];
+    }
+
+    // ---- contact candidates on body i: activity test + Jacobian rows -> LDS
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (T::cbody[c] == i) {
+        float x[3];
+        mat3vec(R[i], M->cpoint[c], x);
+        x[0] += X[i][0]; x[1] += X[i][1]; x[2] += X[i][2];
+        const float r = M->cradius[c];
+        const float dist = s.p[2] + x[2] - r;
+        act[c] = P.has_ground && (dist < P.contact_offset);
+        sep[c] = dist - P.rest_offset;
+        cmu[c] = 0.5f * (mu[T::cshape[c]] + P.ground_mu);
+        if (act[c]) {
+          const float xc[3] = {x[0], x[1], x[2] - r};
+          const int SUP = T::csupp[c];
+          const int leaf = T::cleaf[c];
+          float* slot = lds + T::cslot[c] * GS_WAVE;
+#pragma unroll
+          for (int rr = 0; rr < 3; ++rr) {
+            const int ax = (rr == 0) ? 2 : (rr == 1 ? 0 : 1);  // normal z, tangent x, tangent y
+#pragma unroll
+            for (int si = 0; si < MS; ++si) {
+              if (si < SUP) {
+                const int k = supp_node<T>(leaf, si);
+                float v;
+                if (k < NB6) {
+                  if (k < 3) {
+                    const float m3[3][3] = {{0.f, xc[2], -xc[1]}, {-xc[2], 0.f, xc[0]}, {xc[1], -xc[0], 0.f}};
+                    v = m3[ax][k];  // d(w x xc)/dw = -[xc]x
+                  } else {
+                    v = (ax == k - 3) ? 1.f : 0.f;
+                  }
+                } else {
+                  const float* Sk = S[T::gbody[k]];
+                  float t[3];
+                  cross3(Sk, xc, t);
+                  v = Sk[3 + ax] + t[ax];
+                }
+                slot[(rr * SUP + si) * GS_WAVE] = v;
+              }
+            }
+          }
+        }
+      }
+    }
+
+    // ---- subtrees completed at body i: bias + mass-matrix rows, then fold into the parent
+#pragma unroll
+    for (int a = NB - 1; a >= 0; --a) {
+      if (a <= i && T::subend[a] == i && (a == i || true)) {
+        bool on_path = false;
+        // a must be i or an ancestor of i (subend == i implies that)
+        on_path = true;
+        if (on_path) {
+          if (a > 0) {
+            const int ga = NB6 + T::bdof[a];
+            bias[ga] = dot6(S[a], Fc[a]);
+            float F[6];
+            spi_mul(Ic[a], S[a], F);
+            Mm[ga][ga] = dot6(S[a], F) + M->armature[T::bdof[a]];
+#pragma unroll
+            for (int k = 0; k < T::MAXDEP; ++k) {
+              if (k < T::depth[ga]) {
+                const int an = T::anc[ga][k];
+                if (an >= NB6) Mm[ga][an] = dot6(S[T::gbody[an]], F);
+                else Mm[ga][an] = F[an];
+              }
+            }
+            const int pa = T::parent[a];
+            Ic[pa].m += Ic[a].m;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) Ic[pa].h[k] += Ic[a].h[k];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) Ic[pa].I[k] += Ic[a].I[k];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) Fc[pa][k] += Fc[a][k];
+          } else if (NB6) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) bias[k] = Fc[0][k];
+            const SpI& I0 = Ic[0];
+            Mm[0][0] = I0.I[0]; Mm[1][1] = I0.I[1]; Mm[2][2] = I0.I[2];
+            Mm[1][0] = I0.I[3]; Mm[2][0] = I0.I[4]; Mm[2][1] = I0.I[5];
+            Mm[3][0] = 0.f;       Mm[3][1] = I0.h[2];  Mm[3][2] = -I0.h[1];
+            Mm[4][0] = -I0.h[2];  Mm[4][1] = 0.f;      Mm[4][2] = I0.h[0];
+            Mm[5][0] = I0.h[1];   Mm[5][1] = -I0.h[0]; Mm[5][2] = 0.f;
+            Mm[3][3] = I0.m; Mm[4][4] = I0.m; Mm[5][5] = I0.m;
+            Mm[4][3] = 0.f; Mm[5][3] = 0.f; Mm[5][4] = 0.f;
+          }
+        }
+      }
+    }
+  }
+
+  // ---------------- L^T D L (Featherstone, tree-sparse, in place)
+#pragma unroll
+  for (int kk = 0; kk < NV; ++kk) {
+    const int k = NV - 1 - kk;
+    const float dinv = 1.f / Mm[k][k];
+#pragma unroll
+    for (int ai = 0; ai < T::MAXDEP; ++ai) {
+      if (ai < T::depth[k]) {
+        const int i = T::anc[k][ai];
+        const float a = Mm[k][i] * dinv;
+#pragma unroll
+        for (int aj = ai; aj < T::MAXDEP; ++aj) {
+          if (aj < T::depth[k]) {
+            const int j = T::anc[k][aj];
+            Mm[i][j] -= a * Mm[k][j];
+          }
+        }
+        Mm[k][i] = a;
+      }
+    }
+  }
+  float sD[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) sD[k] = rsqrtf(Mm[k][k]);
+
+  // ---------------- free velocity: nu_f = nu + h M^-1 (tau - c) (+ mixed-frame term)
+  float nuf[NV];
+  {
+    float r[NV];
+    if (NB6) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) r[k] = -bias[k];
+    }
+#pragma unroll
+    for (int j = 0; j < T::ND; ++j) {
+      float t = tau[j];
+      const float e = M->effort[j];
+      if (e > 0.f) t = clampf(t, -e, e);
+      r[NB6 + j] = t - bias[NB6 + j];
+    }
+#pragma unroll
+    for (int kk = 0; kk < NV; ++kk) {
+      const int k = NV - 1 - kk;
+#pragma unroll
+      for (int ai = 0; ai < T::MAXDEP; ++ai)
+        if (ai < T::depth[k]) r[T::anc[k][ai]] -= Mm[k][T::anc[k][ai]] * r[k];
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) r[k] *= sD[k] * sD[k];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+#pragma unroll
+      for (int ai = 0; ai < T::MAXDEP; ++ai)
+        if (ai < T::depth[k]) r[k] -= Mm[k][T::anc[k][ai]] * r[T::anc[k][ai]];
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) nuf[k] = nu[k] + h * r[k];
+    if (NB6) {
+      float wxp[3];
+      cross3(&nu[0], &nu[3], wxp);
+      nuf[3] += h * wxp[0]; nuf[4] += h * wxp[1]; nuf[5] += h * wxp[2];
+    }
+  }
+
+  // ---------------- contact rows: J (LDS) -> c = J nu_f, scaled Z = (L^-T J^T) D^-1/2, 1/diag
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (act[c]) {
+      const int SUP = T::csupp[c];
+      const int leaf = T::cleaf[c];
+      float* slot = lds + T::cslot[c] * GS_WAVE;
+#pragma unroll
+      for (int rr = 0; rr < 3; ++rr) {
+        float jv[MS];
+        float cj = 0.f;
+#pragma unroll
+        for (int si = 0; si < MS; ++si) {
+          if (si < SUP) {
+            jv[si] = slot[(rr * SUP + si) * GS_WAVE];
+            cj += jv[si] * nuf[supp_node<T>(leaf, si)];
+          }
+        }
+#pragma unroll
+        for (int si = 0; si < MS; ++si) {
+          if (si < SUP) {
+            const int k = supp_node<T>(leaf, si);
+#pragma unroll
+            for (int sj = si + 1; sj < MS; ++sj)
+              if (sj < SUP) jv[sj] -= Mm[k][supp_node<T>(leaf, sj)] * jv[si];
+          }
+        }
+        float d = 0.f;
+#pragma unroll
+        for (int si = 0; si < MS; ++si) {
+          if (si < SUP) {
+            const float zh = jv[si] * sD[supp_node<T>(leaf, si)];
+            d += zh * zh;
+            slot[(rr * SUP + si) * GS_WAVE] = zh;
+          }
+        }
+        slot[(3 * SUP + rr) * GS_WAVE] = cj;
+        slot[(3 * SUP + 3 + rr) * GS_WAVE] = 1.f / d;
+      }
+    }
+  }
+
+  // ---------------- projected Gauss-Seidel in w-space
+  float wt[NV], lam[NC][3], wpos[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) wt[k] = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) lam[c][0] = lam[c][1] = lam[c][2] = 0.f;
+  const float inv_h = 1.f / h;
+  const int iters = P.pos_iters + P.vel_iters;
+  for (int it = 0; it < iters; ++it) {
+    const bool pos_phase = it < P.pos_iters;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (act[c]) {
+        const int SUP = T::csupp[c];
+        const int leaf = T::cleaf[c];
+        const float* slot = lds + T::cslot[c] * GS_WAVE;
+        const float sc = sep[c];
+        float target = -sc * inv_h;
+        if (sc < 0.f) target = pos_phase ? fminf(target, P.max_depen_vel) : 0.f;
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) {
+          float z[MS];
+          float u = slot[(3 * SUP + rr) * GS_WAVE];
+#pragma unroll
+          for (int si = 0; si < MS; ++si) {
+            if (si < SUP) {
+              z[si] = slot[(rr * SUP + si) * GS_WAVE];
+              u += z[si] * wt[supp_node<T>(leaf, si)];
+            }
+          }
+          const float dinv = slot[(3 * SUP + 3 + rr) * GS_WAVE];
+          float nl;
+          if (rr == 0) {
+            nl = fmaxf(lam[c][0] + (target - u) * dinv, 0.f);
+          } else {
+            const float lim = cmu[c] * lam[c][0];
+            nl = clampf(lam[c][rr] - u * dinv, -lim, lim);
+          }
+          const float dl = nl - lam[c][rr];
+          lam[c][rr] = nl;
+#pragma unroll
+          for (int si = 0; si < MS; ++si)
+            if (si < SUP) wt[supp_node<T>(leaf, si)] += z[si] * dl;
+        }
+      }
+    }
+    if (it == P.pos_iters - 1) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) wpos[k] = wt[k];
+    }
+  }
+  if (P.pos_iters <= 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) wpos[k] = wt[k];
+  }
+  // dnu = L^-1 D^-1/2 w  for the velocity-phase (state) and position-phase (integration) solutions
+  float nun[NV], nupos[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    float v = wt[k] * sD[k], vp = wpos[k] * sD[k];
+#pragma unroll
+    for (int ai = 0; ai < T::MAXDEP; ++ai) {
+      if (ai < T::depth[k]) {
+        const float l = Mm[k][T::anc[k][ai]];
+        v -= l * nun[T::anc[k][ai]];
+        vp -= l * nupos[T::anc[k][ai]];
+      }
+    }
+    nun[k] = v;
+    nupos[k] = vp;
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    nun[k] += nuf[k];
+    nupos[k] += nuf[k];
+  }
+
+  // ---------------- joint velocity limits
+#pragma unroll
+  for (int j = 0; j < T::ND; ++j) {
+    const float vm = M->vmax[j];
+    if (vm > 0.f) {
+      nun[NB6 + j] = clampf(nun[NB6 + j], -vm, vm);
+      nupos[NB6 + j] = clampf(nupos[NB6 + j], -vm, vm);
+    }
+  }
+
+  // ---------------- integrate positions with nu_pos; keep nu_new
+  if (NB6) {
+    s.p[0] += h * nupos[3]; s.p[1] += h * nupos[4]; s.p[2] += h * nupos[5];
+    const float wx = nupos[0], wy = nupos[1], wz = nupos[2];
+    float x = s.quat[0], y = s.quat[1], z = s.quat[2], w = s.quat[3];
+    const float hh = 0.5f * h;
+    const float dx = hh * (w * wx + wy * z - wz * y);
+    const float dy = hh * (w * wy + wz * x - wx * z);
+    const float dz = hh * (w * wz + wx * y - wy * x);
+    const float dw = -hh * (wx * x + wy * y + wz * z);
+    x += dx; y += dy; z += dz; w += dw;
+    const float n = rsqrtf(x * x + y * y + z * z + w * w);
+    s.quat[0] = x * n; s.quat[1] = y * n; s.quat[2] = z * n; s.quat[3] = w * n;
+    s.w[0] = nun[0]; s.w[1] = nun[1]; s.w[2] = nun[2];
+    s.vo[0] = nun[3]; s.vo[1] = nun[4]; s.vo[2] = nun[5];
+  }
+#pragma unroll
+  for (int j = 0; j < T::ND; ++j) {
+    s.q[j] += h * nupos[NB6 + j];
+    s.qd[j] = nun[NB6 + j];
+  }
+  if (collect) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) cf[b][0] = cf[b][1] = cf[b][2] = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int b = T::cbody[c];
+      cf[b][0] += lam[c][1] * inv_h;
+      cf[b][1] += lam[c][2] * inv_h;
+      cf[b][2] += lam[c][0] * inv_h;
+    }
+  }
+}
+
+template <class T>
+__device__ __forceinline__ void com_velocity(const DevModel* __restrict__ M, const EnvState<T>& s, float* v) {
+  float R[9], c[3], wc[3];
+  quat_to_mat(s.quat, R);
+  mat3vec(R, M->com[0], c);
+  cross3(s.w, c, wc);
+  v[0] = s.vo[0] + wc[0]; v[1] = s.vo[1] + wc[1]; v[2] = s.vo[2] + wc[2];
+}
+
+// ---------------------------------------------------------------- kernels
+template <class T>
+__global__ __launch_bounds__(GS_WAVE, 1) void k_simulate(const DevModel* __restrict__ M, DevParams P,
+                                                          SimBuffers B, const float* __restrict__ tau_aos) {
+  __shared__ float lds[T::NSLOT * GS_WAVE];
+  const int e = blockIdx.x * GS_WAVE + threadIdx.x;
+  if (e >= B.N) return;
+  const int N = B.N;
+  EnvState<T> s;
+  load_state<T>(B.state, N, e, s);
+  float tau[T::ND > 0 ? T::ND : 1], mu[T::NS > 0 ? T::NS : 1];
+#pragma unroll
+  for (int j = 0; j < T::ND; ++j) tau[j] = tau_aos ? tau_aos[(size_t)e * T::ND + j] : 0.f;
+#pragma unroll
+  for (int k = 0; k < T::NS; ++k) mu[k] = B.mu[k * N + e];
+  float cf[T::NB][3];
+  for (int sstep = 0; sstep < P.substeps; ++sstep) {
+    const bool last = (sstep == P.substeps - 1) && P.collect;
+    substep<T>(M, P, s, tau, mu, lds + threadIdx.x, cf, last);
+  }
+  store_state<T>(B.state, N, e, s);
+  if (P.collect) {
+#pragma unroll
+    for (int b = 0; b < T::NB; ++b)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) B.cf[(3 * b + k) * N + e] = cf[b][k];
+  }
+}
+
+template <class T>
+__global__ __launch_bounds__(GS_WAVE, 1) void k_pd_step(const DevModel* __restrict__ M, DevParams P, SimBuffers B,
+                                                         PdDev A) {
+  __shared__ float lds[T::NSLOT * GS_WAVE];
+  const int e = blockIdx.x * GS_WAVE + threadIdx.x;
+  if (e >= B.N) return;
+  const int N = B.N;
+  constexpr int ND = T::ND;
+  EnvState<T> s;
+  load_state<T>(B.state, N, e, s);
+  float act[ND], mu[T::NS > 0 ? T::NS : 1], tau[ND];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) act[j] = A.actions[(size_t)e * ND + j];
+#pragma unroll
+  for (int k = 0; k < T::NS; ++k) mu[k] = B.mu[k * N + e];
+  float cf[T::NB][3];
+  // the first PD evaluation reads the dof tensor the task holds (refreshed after the
+  // previous step's decimation loop or written by reset_idx): anymal_terrain.py:444
+  float q0[ND], qd0[ND];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    q0[j] = A.dof_state_in[((size_t)e * ND + j) * 2 + 0];
+    qd0[j] = A.dof_state_in[((size_t)e * ND + j) * 2 + 1];
+  }
+  // one call site for the substep so it is inlined once
+  const int sub = P.substeps;
+  const int n_pd = A.decimation * sub;
+  const int total = (A.decimation + A.extra) * sub;
+  for (int it = 0; it < total; ++it) {
+    if (it < n_pd && (it % sub) == 0) {
+      const bool first = it == 0;
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        const float qj = first ? q0[j] : s.q[j];
+        const float qdj = first ? qd0[j] : s.qd[j];
+        tau[j] = clampf(A.kp * (A.scale * act[j] + A.default_pos[j] - qj) - A.kd * qdj, -A.tlim, A.tlim);
+      }
+    }
+    const bool last = ((it % sub) == sub - 1) && P.collect;
+    substep<T>(M, P, s, tau, mu, lds + threadIdx.x, cf, last);
+    if (it == n_pd - 1 && A.dof_out) {
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        A.dof_out[((size_t)e * ND + j) * 2 + 0] = s.q[j];
+        A.dof_out[((size_t)e * ND + j) * 2 + 1] = s.qd[j];
+      }
+    }
+  }
+  store_state<T>(B.state, N, e, s);
+#pragma unroll
+  for (int j = 0; j < ND; ++j) A.torques_out[(size_t)e * ND + j] = tau[j];
+  if (A.root_out) {
+    float* o = A.root_out + (size_t)e * 13;
+    o[0] = s.p[0]; o[1] = s.p[1]; o[2] = s.p[2];
+    o[3] = s.quat[0]; o[4] = s.quat[1]; o[5] = s.quat[2]; o[6] = s.quat[3];
+    float v[3];
+    com_velocity<T>(M, s, v);
+    o[7] = v[0]; o[8] = v[1]; o[9] = v[2];
+    o[10] = s.w[0]; o[11] = s.w[1]; o[12] = s.w[2];
+  }
+  if (P.collect) {
+#pragma unroll
+    for (int b = 0; b < T::NB; ++b)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) B.cf[(3 * b + k) * N + e] = cf[b][k];
+    if (A.cf_out) {
+#pragma unroll
+      for (int b = 0; b < T::NB; ++b)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) A.cf_out[((size_t)e * T::NB + b) * 3 + k] = cf[b][k];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- tensor API kernels
+__global__ void k_refresh_root(const float* __restrict__ st, int N, const float* __restrict__ com0,
+                               float* __restrict__ out) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N) return;
+  float q[4], R[9], c[3], w[3], wc[3];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) q[k] = st[(3 + k) * N + e];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) w[k] = st[(10 + k) * N + e];
+  quat_to_mat(q, R);
+  mat3vec(R, com0, c);
+  cross3(w, c, wc);
+  float* o = out + (size_t)e * 13;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) o[k] = st[k * N + e];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) o[3 + k] = q[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) o[7 + k] = st[(7 + k) * N + e] + wc[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) o[10 + k] = w[k];
+}
+__global__ void k_refresh_dof(const float* __restrict__ st, int N, int nd, float* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;  // t = e*nd + j
+  if (t >= N * nd) return;
+  const int e = t / nd, j = t - e * nd;
+  out[2 * (size_t)t + 0] = st[(13 + j) * N + e];
+  out[2 * (size_t)t + 1] = st[(13 + nd + j) * N + e];
+}
+__global__ void k_refresh_contact(const float* __restrict__ cf, int N, int nb, float* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;  // t = (e*nb + b)*3 + k
+  if (t >= N * nb * 3) return;
+  const int k = t % 3, eb = t / 3, b = eb % nb, e = eb / nb;
+  out[t] = cf[(3 * b + k) * N + e];
+}
+__global__ void k_set_root(float* __restrict__ st, int N, const float* __restrict__ com0,
+                           const float* __restrict__ src, const int* __restrict__ idx, int n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int e = idx ? idx[t] : t;
+  if (e < 0 || e >= N) return;
+  const float* r = src + (size_t)e * 13;
+  float q[4], R[9], c[3], wc[3];
+  const float inv = rsqrtf(r[3] * r[3] + r[4] * r[4] + r[5] * r[5] + r[6] * r[6]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) q[k] = r[3 + k] * inv;
+  quat_to_mat(q, R);
+  mat3vec(R, com0, c);
+  cross3(r + 10, c, wc);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) st[k * N + e] = r[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) st[(3 + k) * N + e] = q[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) st[(7 + k) * N + e] = r[7 + k] - wc[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) st[(10 + k) * N + e] = r[10 + k];
+}
+__global__ void k_set_dof(float* __restrict__ st, int N, int nd, const float* __restrict__ src,
+                          const int* __restrict__ idx, int n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;  // t over n*nd
+  if (t >= n * nd) return;
+  const int r = t / nd, j = t - r * nd;
+  const int e = idx ? idx[r] : r;
+  if (e < 0 || e >= N) return;
+  st[(13 + j) * N + e] = src[((size_t)e * nd + j) * 2 + 0];
+  st[(13 + nd + j) * N + e] = src[((size_t)e * nd + j) * 2 + 1];
+}
+
+inline int nblk(long n, int b) { return (int)((n + b - 1) / b); }
+
+}  // namespace
+
+hipError_t launch_refresh_root(const float* state, int N, int nd, const float* com0, float* out, hipStream_t s) {
+  (void)nd;
+  hipLaunchKernelGGL(k_refresh_root, dim3(nblk(N, 256)), dim3(256), 0, s, state, N, com0, out);
+  return hipGetLastError();
+}
+hipError_t launch_refresh_dof(const float* state, int N, int nd, float* out, hipStream_t s) {
+  if (nd == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_refresh_dof, dim3(nblk((long)N * nd, 256)), dim3(256), 0, s, state, N, nd, out);
+  return hipGetLastError();
+}
+hipError_t launch_refresh_contact(const float* cf, int N, int nb, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_refresh_contact, dim3(nblk((long)N * nb * 3, 256)), dim3(256), 0, s, cf, N, nb, out);
+  return hipGetLastError();
+}
+hipError_t launch_set_root(float* state, int N, int nd, const float* com0, const float* src, const int* idx, int n_idx,
+                           hipStream_t s) {
+  (void)nd;
+  const int n = idx ? n_idx : N;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_set_root, dim3(nblk(n, 256)), dim3(256), 0, s, state, N, com0, src, idx, n);
+  return hipGetLastError();
+}
+hipError_t launch_set_dof(float* state, int N, int nd, const float* src, const int* idx, int n_idx, hipStream_t s) {
+  const int n = idx ? n_idx : N;
+  if (n <= 0 || nd == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_set_dof, dim3(nblk((long)n * nd, 256)), dim3(256), 0, s, state, N, nd, src, idx, n);
+  return hipGetLastError();
+}
+
+template <class T>
+hipError_t launch_sim(const DevModel* M, const DevParams& P, const SimBuffers& B, const float* tau, hipStream_t st) {
+  const int blocks = (B.N + GS_WAVE - 1) / GS_WAVE;
+  hipLaunchKernelGGL(k_simulate<T>, dim3(blocks), dim3(GS_WAVE), 0, st, M, P, B, tau);
+  return hipGetLastError();
+}
+template <class T>
+hipError_t launch_pd(const DevModel* M, const DevParams& P, const SimBuffers& B, const PdDev& A, hipStream_t st) {
+  const int blocks = (B.N + GS_WAVE - 1) / GS_WAVE;
+  hipLaunchKernelGGL(k_pd_step<T>, dim3(blocks), dim3(GS_WAVE), 0, st, M, P, B, A);
+  return hipGetLastError();
+}
+
+#define GS_TOPO_ENTRY(T, SIG) {SIG, T::kName, &launch_sim<T>, &launch_pd<T>, T::NB, T::ND, T::NC, T::NS},
+TopoEntry g_topologies[] = {GS_FOR_EACH_TOPOLOGY(GS_TOPO_ENTRY)};
+const int g_num_topologies = sizeof(g_topologies) / sizeof(g_topologies[0]);

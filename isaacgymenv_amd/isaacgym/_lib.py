@@ -1,0 +1,110 @@
+"""ctypes binding of libgymsim.so (include/gymsim.h).
+
+There is no fallback: if the HIP library or a GPU is missing, every call that
+needs it raises.  (The CPU oracle under oracle/ is test infrastructure and is
+never loaded from here.)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_HERE, "_lib", "libgymsim.so")
+
+
+class GsModelDesc(C.Structure):
+    _fields_ = [("num_bodies", C.c_int32), ("num_dofs", C.c_int32), ("num_candidates", C.c_int32),
+                ("num_shapes", C.c_int32), ("fixed_base", C.c_int32)] + [
+        (n, C.c_void_p) for n in ("parent", "joint_kind", "body_dof", "joint_origin", "joint_axis", "mass",
+                                  "com", "inertia", "cand_body", "cand_point", "cand_radius", "cand_shape",
+                                  "dof_effort", "dof_velocity", "dof_armature")]
+
+
+class GsSimParams(C.Structure):
+    _fields_ = [("dt", C.c_double), ("substeps", C.c_int32), ("gravity", C.c_double * 3),
+                ("num_position_iterations", C.c_int32), ("num_velocity_iterations", C.c_int32),
+                ("contact_offset", C.c_double), ("rest_offset", C.c_double),
+                ("bounce_threshold_velocity", C.c_double), ("max_depenetration_velocity", C.c_double),
+                ("contact_collection", C.c_int32)]
+
+
+class GsPdArgs(C.Structure):
+    _fields_ = [("actions", C.c_void_p), ("default_pos", C.c_void_p), ("kp", C.c_float), ("kd", C.c_float),
+                ("action_scale", C.c_float), ("torque_limit", C.c_float), ("decimation", C.c_int32),
+                ("extra_simulates", C.c_int32), ("torques_out", C.c_void_p), ("dof_state_out", C.c_void_p),
+                ("root_state_out", C.c_void_p), ("contact_out", C.c_void_p)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m isaacgymenv_amd.build` "
+                               "(hipcc, gfx950). There is no CPU fallback.")
+        L = C.CDLL(LIB_PATH)
+        vp, i, f, d = C.c_void_p, C.c_int, C.c_float, C.c_double
+        sig = {
+            "gs_abi_version": (i, []),
+            "gs_last_error": (C.c_char_p, []),
+            "gs_topology_supported": (i, [C.POINTER(GsModelDesc)]),
+            "gs_sim_create": (vp, [i, C.POINTER(GsSimParams)]),
+            "gs_sim_destroy": (None, [vp]),
+            "gs_sim_add_ground": (i, [vp, d, d, d]),
+            "gs_sim_set_model": (i, [vp, C.POINTER(GsModelDesc)]),
+            "gs_sim_prepare": (i, [vp, i, vp, vp, vp]),
+            "gs_sim_simulate": (i, [vp, vp, vp]),
+            "gs_sim_refresh_root": (i, [vp, vp, vp]),
+            "gs_sim_refresh_dof": (i, [vp, vp, vp]),
+            "gs_sim_refresh_contact": (i, [vp, vp, vp]),
+            "gs_sim_set_root": (i, [vp, vp, vp, i, vp]),
+            "gs_sim_set_dof": (i, [vp, vp, vp, i, vp]),
+            "gs_sim_pd_step": (i, [vp, C.POINTER(GsPdArgs), vp]),
+            "gs_sim_enable_timing": (i, [vp, i]),
+            "gs_sim_last_kernel_ms": (f, [vp]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {lib().gs_last_error().decode()}")
+
+
+EXPORTED_SYMBOLS = [
+    "gs_abi_version", "gs_last_error", "gs_topology_supported", "gs_sim_create", "gs_sim_destroy",
+    "gs_sim_add_ground", "gs_sim_set_model", "gs_sim_prepare", "gs_sim_simulate", "gs_sim_refresh_root",
+    "gs_sim_refresh_dof", "gs_sim_refresh_contact", "gs_sim_set_root", "gs_sim_set_dof", "gs_sim_pd_step",
+    "gs_sim_enable_timing", "gs_sim_last_kernel_ms",
+]
+
+
+def model_desc(flat: dict):
+    """Build a GsModelDesc over the numpy arrays of ``_model.flatten``; returns (desc, keepalive)."""
+    import numpy as np
+    keep = {}
+    m = GsModelDesc()
+    m.num_bodies, m.num_dofs, m.num_candidates = flat["nb"], flat["nd"], flat["nc"]
+    m.num_shapes, m.fixed_base = flat["ns"], flat["fixed_base"]
+    pairs = [("parent", "parent", np.int32), ("joint_kind", "jkind", np.int32), ("body_dof", "bdof", np.int32),
+             ("joint_origin", "jorigin", np.float64), ("joint_axis", "jaxis", np.float64),
+             ("mass", "mass", np.float64), ("com", "com", np.float64), ("inertia", "inertia", np.float64),
+             ("cand_body", "cbody", np.int32), ("cand_point", "cpoint", np.float64),
+             ("cand_radius", "cradius", np.float64), ("cand_shape", "cshape", np.int32),
+             ("dof_effort", "effort", np.float64), ("dof_velocity", "vmax", np.float64),
+             ("dof_armature", "armature", np.float64)]
+    for field, key, dt in pairs:
+        a = np.ascontiguousarray(flat[key], dtype=dt)
+        if a.size == 0:
+            a = np.zeros(1, dtype=dt)
+        keep[field] = a
+        setattr(m, field, a.ctypes.data)
+    return m, keep

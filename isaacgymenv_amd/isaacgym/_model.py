@@ -1,0 +1,64 @@
+"""Flat (C-ABI) form of an :class:`Articulation`.
+
+The same flat arrays feed the product library (``gs_sim_set_model`` in
+``include/gymsim.h``) and, in tests, the CPU oracle.  Layout:
+
+* ``parent[nb]``, ``jkind[nb]``, ``bdof[nb]`` (int32)
+* ``jorigin[nb][12]`` -- parent body frame -> joint frame, R row-major then t
+* ``jaxis[nb][3]``, ``mass[nb]``, ``com[nb][3]``, ``inertia[nb][9]`` (about COM)
+* contact candidates ``cbody[nc]``, ``cpoint[nc][3]``, ``cradius[nc]``, ``cshape[nc]``
+* per dof ``effort``, ``vmax``, ``armature``, ``lower``, ``upper``, ``has_limits``
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ._assets import Articulation, JOINT_FREE, JOINT_FIXED
+
+
+def flatten(art: Articulation, armature: float | None = None) -> dict:
+    nb, nd = art.num_bodies, art.num_dofs
+    parent = np.array([b.parent for b in art.bodies], dtype=np.int32)
+    jkind = np.array([b.joint_kind for b in art.bodies], dtype=np.int32)
+    bdof = np.full(nb, -1, dtype=np.int32)
+    for di, d in enumerate(art.dofs):
+        bdof[d.body] = di
+    jorigin = np.zeros((nb, 12))
+    jaxis = np.zeros((nb, 3))
+    mass = np.zeros(nb)
+    com = np.zeros((nb, 3))
+    inertia = np.zeros((nb, 9))
+    for i, b in enumerate(art.bodies):
+        jorigin[i, :9] = b.origin.R.reshape(-1)
+        jorigin[i, 9:] = b.origin.t
+        jaxis[i] = b.axis
+        mass[i] = b.mass
+        com[i] = b.com
+        inertia[i] = b.inertia.reshape(-1)
+    cands = art.contact_candidates()
+    if art.fixed_base:
+        # a body welded to the world cannot take a contact impulse: drop its candidates
+        cands = [c for c in cands if c[0] != 0]
+    nc = len(cands)
+    cbody = np.array([c[0] for c in cands], dtype=np.int32).reshape(nc)
+    cpoint = np.array([c[1] for c in cands], dtype=np.float64).reshape(nc, 3)
+    cradius = np.array([c[2] for c in cands], dtype=np.float64).reshape(nc)
+    cshape = np.array([c[3] for c in cands], dtype=np.int32).reshape(nc)
+    arm = art.options.get("armature", 0.0) if armature is None else armature
+    return dict(
+        nb=nb, nd=nd, nc=nc, ns=art.num_shapes, fixed_base=int(art.fixed_base),
+        parent=parent, jkind=jkind, bdof=bdof, jorigin=jorigin, jaxis=jaxis, mass=mass, com=com,
+        inertia=inertia, cbody=cbody, cpoint=cpoint, cradius=cradius, cshape=cshape,
+        effort=np.array([d.effort for d in art.dofs], dtype=np.float64).reshape(nd),
+        vmax=np.array([d.velocity for d in art.dofs], dtype=np.float64).reshape(nd),
+        armature=np.full(nd, float(arm)),
+        lower=np.array([d.lower for d in art.dofs], dtype=np.float64).reshape(nd),
+        upper=np.array([d.upper for d in art.dofs], dtype=np.float64).reshape(nd),
+        has_limits=np.array([int(d.has_limits) for d in art.dofs], dtype=np.int32).reshape(nd),
+    )
+
+
+def topology_signature(flat: dict) -> str:
+    """Compile-time shape of a model: what selects a specialised kernel."""
+    return "fb{}_p{}_c{}".format(flat["fixed_base"], "-".join(str(int(p)) for p in flat["parent"]),
+                                  "-".join(str(int(b)) for b in flat["cbody"]))

@@ -1,0 +1,745 @@
+"""Drop-in ``isaacgym.gymapi`` for the MI355X simulator.
+
+The reference imports the closed Isaac Gym binding as
+``from isaacgym import gymapi, gymtorch`` (vec_task.py:37) and drives the
+simulator only through ``self.gym = gymapi.acquire_gym()`` (vec_task.py:247).
+This module keeps that Python surface -- the constants, parameter classes and
+``Gym`` methods the reference's task layer calls -- and
+implements it over libgymsim.so (include/gymsim.h).  Env/actor bookkeeping is
+host Python (cold path); everything per step is a HIP launch on the torch
+stream of the sim device.
+
+Scope notes:
+  * one articulation actor per env, every env the same asset;
+  * z-up ground plane contacts (trimesh/heightfield terrain is the next row);
+  * ``pipeline=cpu`` keeps host-side tensors, the physics still runs on the GPU
+    (there is no CPU physics in the product).
+"""
+from __future__ import annotations
+
+import enum
+import math
+import os
+from typing import List, Optional
+
+import numpy as np
+
+from . import _assets
+from ._assets import build_articulation, load_raw, mat_to_quat_xyzw, quat_xyzw_to_mat
+from ._model import flatten
+from . import _lib
+
+# ------------------------------------------------------------------ constants
+SIM_PHYSX = 0
+SIM_FLEX = 1
+UP_AXIS_Y = 0
+UP_AXIS_Z = 1
+DOF_MODE_NONE = 0
+DOF_MODE_POS = 1
+DOF_MODE_VEL = 2
+DOF_MODE_EFFORT = 3
+DOF_INVALID = 0
+DOF_ROTATION = 1
+DOF_TRANSLATION = 2
+STATE_NONE, STATE_POS, STATE_VEL, STATE_ALL = 0, 1, 2, 3
+DOMAIN_SIM, DOMAIN_ENV, DOMAIN_ACTOR = 0, 1, 2
+MESH_NONE, MESH_COLLISION, MESH_VISUAL, MESH_VISUAL_AND_COLLISION = 0, 1, 2, 3
+IMAGE_COLOR, IMAGE_DEPTH = 0, 1
+KEY_ESCAPE, KEY_V, KEY_R = 0, 1, 2
+INVALID_HANDLE = -1
+
+
+class ContactCollection(enum.IntEnum):
+    CC_NEVER = 0
+    CC_LAST_SUBSTEP = 1
+    CC_ALL_SUBSTEPS = 2
+
+
+# ------------------------------------------------------------------ value types
+class Vec3:
+    __slots__ = ("x", "y", "z")
+
+    def __init__(self, x=0.0, y=0.0, z=0.0):
+        self.x, self.y, self.z = float(x), float(y), float(z)
+
+    def __iter__(self):
+        return iter((self.x, self.y, self.z))
+
+    def __repr__(self):
+        return f"Vec3({self.x}, {self.y}, {self.z})"
+
+
+class Quat:
+    __slots__ = ("x", "y", "z", "w")
+
+    def __init__(self, x=0.0, y=0.0, z=0.0, w=1.0):
+        self.x, self.y, self.z, self.w = float(x), float(y), float(z), float(w)
+
+    def __iter__(self):
+        return iter((self.x, self.y, self.z, self.w))
+
+    @staticmethod
+    def from_axis_angle(axis: Vec3, angle: float) -> "Quat":
+        s = math.sin(angle / 2)
+        n = math.sqrt(axis.x ** 2 + axis.y ** 2 + axis.z ** 2) or 1.0
+        return Quat(axis.x / n * s, axis.y / n * s, axis.z / n * s, math.cos(angle / 2))
+
+    @staticmethod
+    def from_euler_zyx(roll, pitch, yaw) -> "Quat":
+        q = mat_to_quat_xyzw(_assets.rpy_to_mat([roll, pitch, yaw]))
+        return Quat(*q)
+
+
+class Transform:
+    def __init__(self, p: Optional[Vec3] = None, r: Optional[Quat] = None):
+        self.p = p if p is not None else Vec3()
+        self.r = r if r is not None else Quat()
+
+
+class PlaneParams:
+    def __init__(self):
+        self.normal = Vec3(0.0, 0.0, 1.0)
+        self.distance = 0.0
+        self.static_friction = 1.0
+        self.dynamic_friction = 1.0
+        self.restitution = 0.0
+        self.segmentation_id = 0
+
+
+class TriangleMeshParams:
+    def __init__(self):
+        self.nb_vertices = 0
+        self.nb_triangles = 0
+        self.transform = Transform()
+        self.static_friction = 1.0
+        self.dynamic_friction = 1.0
+        self.restitution = 0.0
+
+
+class PhysXParams:
+    def __init__(self):
+        self.num_threads = 4
+        self.solver_type = 1
+        self.use_gpu = True
+        self.num_position_iterations = 4
+        self.num_velocity_iterations = 1
+        self.contact_offset = 0.02
+        self.rest_offset = 0.001
+        self.bounce_threshold_velocity = 0.2
+        self.max_depenetration_velocity = 100.0
+        self.default_buffer_size_multiplier = 2.0
+        self.max_gpu_contact_pairs = 1024 * 1024
+        self.num_subscenes = 0
+        self.contact_collection = ContactCollection.CC_LAST_SUBSTEP
+        self.friction_offset_threshold = 0.04
+        self.friction_correlation_distance = 0.025
+        self.always_use_articulations = False
+
+
+class FlexParams:
+    def __init__(self):
+        self.__dict__["_values"] = {}
+
+    def __setattr__(self, k, v):
+        self._values[k] = v
+
+    def __getattr__(self, k):
+        try:
+            return self.__dict__["_values"][k]
+        except KeyError:
+            raise AttributeError(k)
+
+
+class SimParams:
+    def __init__(self):
+        self.dt = 1.0 / 60.0
+        self.substeps = 2
+        self.up_axis = UP_AXIS_Y
+        self.gravity = Vec3(0.0, -9.8, 0.0)
+        self.use_gpu_pipeline = False
+        self.num_client_threads = 0
+        self.enable_actor_creation_warning = False
+        self.physx = PhysXParams()
+        self.flex = FlexParams()
+
+
+class AssetOptions:
+    def __init__(self):
+        d = _assets.DEFAULT_ASSET_OPTIONS
+        self.default_dof_drive_mode = DOF_MODE_POS
+        self.collapse_fixed_joints = d["collapse_fixed_joints"]
+        self.replace_cylinder_with_capsule = d["replace_cylinder_with_capsule"]
+        self.flip_visual_attachments = False
+        self.fix_base_link = False
+        self.density = d["density"]
+        self.angular_damping = d["angular_damping"]
+        self.linear_damping = d["linear_damping"]
+        self.max_angular_velocity = d["max_angular_velocity"]
+        self.max_linear_velocity = d["max_linear_velocity"]
+        self.armature = 0.0
+        self.thickness = d["thickness"]
+        self.disable_gravity = False
+        self.use_mesh_materials = False
+        self.override_com = False
+        self.override_inertia = False
+        self.vhacd_enabled = False
+        self.use_physx_armature = True
+        self.slices_per_cylinder = 20
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k in vars(self)}
+
+
+class CameraProperties:
+    def __init__(self):
+        self.width, self.height, self.horizontal_fov, self.enable_tensors = 1920, 1080, 90.0, False
+
+
+class RigidShapeProperties:
+    def __init__(self, friction=1.0):
+        self.friction = friction
+        self.rolling_friction = 0.0
+        self.torsion_friction = 0.0
+        self.restitution = 0.0
+        self.compliance = 0.0
+        self.thickness = 0.0
+        self.contact_offset = 0.0
+        self.rest_offset = 0.0
+        self.filter = 0
+
+
+class ActuatorProperties:
+    def __init__(self, motor_effort=0.0):
+        self.motor_effort = motor_effort
+        self.control_limited = False
+        self.lower_control_limit = 0.0
+        self.upper_control_limit = 0.0
+        self.lower_force_limit = 0.0
+        self.upper_force_limit = 0.0
+        self.kp = 0.0
+        self.kv = 0.0
+
+
+DofPropertiesDtype = np.dtype([("hasLimits", "?"), ("lower", "<f4"), ("upper", "<f4"), ("driveMode", "<i4"),
+                               ("velocity", "<f4"), ("effort", "<f4"), ("stiffness", "<f4"),
+                               ("damping", "<f4"), ("friction", "<f4"), ("armature", "<f4")])
+
+
+# ------------------------------------------------------------------ handles
+class Asset:
+    def __init__(self, art: _assets.Articulation, options: AssetOptions):
+        self.art = art
+        self.options = options
+        self.flat = flatten(art, armature=options.armature)
+        self.shape_props = [RigidShapeProperties() for _ in range(art.num_shapes)]
+        self.dof_props = self._default_dof_props()
+        self.sensors = []
+
+    def _default_dof_props(self):
+        p = np.zeros(self.art.num_dofs, dtype=DofPropertiesDtype)
+        for i, d in enumerate(self.art.dofs):
+            p[i]["hasLimits"] = d.has_limits
+            p[i]["lower"] = d.lower if d.has_limits else -3.4028235e38
+            p[i]["upper"] = d.upper if d.has_limits else 3.4028235e38
+            p[i]["driveMode"] = self.options.default_dof_drive_mode
+            p[i]["velocity"] = d.velocity
+            p[i]["effort"] = d.effort
+            p[i]["friction"] = d.friction
+            p[i]["damping"] = d.damping
+            p[i]["armature"] = self.options.armature
+        return p
+
+
+class Env:
+    def __init__(self, sim: "Sim", index: int, origin):
+        self.sim = sim
+        self.index = index
+        self.origin = np.asarray(origin, dtype=np.float64)
+        self.actors: List["Actor"] = []
+
+
+class Actor:
+    def __init__(self, env: Env, asset: Asset, pose: Transform, name: str, group: int, filter: int):
+        self.env = env
+        self.asset = asset
+        self.pose = pose
+        self.name = name
+        self.group = group
+        self.filter = filter
+        self.shape_friction = np.array([sp.friction for sp in asset.shape_props], dtype=np.float32)
+        self.dof_props = asset.dof_props.copy()
+
+
+class GymTensor:
+    """Descriptor handed out by ``acquire_*_tensor`` / ``gymtorch.unwrap_tensor``."""
+
+    def __init__(self, tensor, kind: str = "user"):
+        self.tensor = tensor
+        self.kind = kind
+
+
+# ------------------------------------------------------------------ the sim
+class Sim:
+    def __init__(self, gym: "Gym", compute_device: int, params: SimParams):
+        import torch
+        self.gym = gym
+        self.params = params
+        self.compute_device = compute_device
+        self.gpu_pipeline = bool(params.use_gpu_pipeline)
+        self.sim_device = torch.device("cuda", compute_device)
+        self.tensor_device = self.sim_device if self.gpu_pipeline else torch.device("cpu")
+        self.envs: List[Env] = []
+        self.asset: Optional[Asset] = None
+        self.ground: Optional[PlaneParams] = None
+        self.prepared = False
+        self.handle = None
+        px = params.physx
+        p = _lib.GsSimParams()
+        p.dt = params.dt
+        p.substeps = max(1, int(params.substeps))
+        g = params.gravity
+        p.gravity[0], p.gravity[1], p.gravity[2] = g.x, g.y, g.z
+        p.num_position_iterations = int(px.num_position_iterations)
+        p.num_velocity_iterations = int(px.num_velocity_iterations)
+        p.contact_offset = float(px.contact_offset)
+        p.rest_offset = float(px.rest_offset)
+        p.bounce_threshold_velocity = float(px.bounce_threshold_velocity)
+        p.max_depenetration_velocity = float(px.max_depenetration_velocity)
+        p.contact_collection = int(px.contact_collection)
+        self.cparams = p
+        L = _lib.lib()
+        h = L.gs_sim_create(int(compute_device), p)
+        if not h:
+            raise RuntimeError(L.gs_last_error().decode())
+        self.handle = h
+
+    def __del__(self):
+        try:
+            if self.handle:
+                _lib.lib().gs_sim_destroy(self.handle)
+        except Exception:
+            pass
+
+    # -------- stream of the sim device
+    def stream(self):
+        import torch
+        return torch.cuda.current_stream(self.sim_device).cuda_stream
+
+    # -------- prepare: allocate + bind tensors, initial state
+    def prepare(self):
+        import torch
+        if self.asset is None or not self.envs:
+            raise RuntimeError("prepare_sim: no actors were created")
+        for e in self.envs:
+            if len(e.actors) != 1 or e.actors[0].asset is not self.asset:
+                raise RuntimeError("prepare_sim: the MI355X simulator supports exactly one actor of one asset "
+                                   "per env (DESIGN.md section 6)")
+        art, flat = self.asset.art, self.asset.flat
+        L = _lib.lib()
+        desc, keep = _lib.model_desc(flat)
+        _lib.check(L.gs_sim_set_model(self.handle, desc), "gs_sim_set_model")
+        if self.ground is not None:
+            _lib.check(L.gs_sim_add_ground(self.handle, self.ground.static_friction, self.ground.dynamic_friction,
+                                           self.ground.restitution), "gs_sim_add_ground")
+        N, nd, nb, ns = len(self.envs), art.num_dofs, art.num_bodies, max(1, art.num_shapes)
+        self.num_envs, self.num_dofs, self.num_bodies = N, nd, nb
+        dev, tdev = self.sim_device, self.tensor_device
+        f32 = torch.float32
+        # SoA sim state (device), initial values from the actors' start poses
+        st = np.zeros((13 + 2 * nd, N), dtype=np.float32)
+        for i, e in enumerate(self.envs):
+            a = e.actors[0]
+            st[0:3, i] = e.origin + np.array(list(a.pose.p))
+            q = np.array(list(a.pose.r), dtype=np.float64)
+            st[3:7, i] = q / np.linalg.norm(q)
+            # dof positions start at 0, clamped into their limits
+            lo = a.dof_props["lower"].astype(np.float64)
+            hi = a.dof_props["upper"].astype(np.float64)
+            st[13:13 + nd, i] = np.clip(0.0, lo, hi)
+        self.state = torch.from_numpy(st).to(dev)
+        mu = np.ones((ns, N), dtype=np.float32)
+        for i, e in enumerate(self.envs):
+            mu[:art.num_shapes, i] = e.actors[0].shape_friction
+        self.shape_mu = torch.from_numpy(mu).to(dev)
+        self.cf_soa = torch.zeros(3 * nb, N, dtype=f32, device=dev)
+        _lib.check(L.gs_sim_prepare(self.handle, N, self.state.data_ptr(), self.shape_mu.data_ptr(),
+                                    self.cf_soa.data_ptr()), "gs_sim_prepare")
+        self._keep = keep
+        # reference-layout tensors (sim owned; wrap_tensor shares them)
+        self.root_tensor = torch.zeros(N, 13, dtype=f32, device=tdev)
+        self.dof_tensor = torch.zeros(N * nd, 2, dtype=f32, device=tdev)
+        self.contact_tensor = torch.zeros(N * nb, 3, dtype=f32, device=tdev)
+        self.dof_force = torch.zeros(N * nd, dtype=f32, device=dev)
+        # device mirrors used when the pipeline is on the CPU
+        if not self.gpu_pipeline:
+            self._root_dev = torch.zeros(N, 13, dtype=f32, device=dev)
+            self._dof_dev = torch.zeros(N * nd, 2, dtype=f32, device=dev)
+            self._cf_dev = torch.zeros(N * nb, 3, dtype=f32, device=dev)
+        self.prepared = True
+        self.refresh("root")
+        self.refresh("dof")
+        self.refresh("contact")
+
+    # -------- tensor API
+    def refresh(self, kind: str):
+        L, s = _lib.lib(), self.stream()
+        dst = {"root": self.root_tensor, "dof": self.dof_tensor, "contact": self.contact_tensor}[kind]
+        out = dst if self.gpu_pipeline else {"root": self._root_dev, "dof": self._dof_dev,
+                                             "contact": self._cf_dev}[kind]
+        fn = {"root": L.gs_sim_refresh_root, "dof": L.gs_sim_refresh_dof, "contact": L.gs_sim_refresh_contact}[kind]
+        _lib.check(fn(self.handle, out.data_ptr(), s), f"refresh {kind}")
+        if not self.gpu_pipeline:
+            dst.copy_(out.cpu())
+
+    def set_state(self, kind: str, src, idx=None, n: int = 0):
+        import torch
+        L, s = _lib.lib(), self.stream()
+        src = src.to(self.sim_device, dtype=torch.float32).contiguous()
+        idx_ptr = None
+        if idx is not None:
+            idx = idx.to(self.sim_device, dtype=torch.int32).contiguous()
+            n = int(n) if n else idx.numel()
+            idx_ptr = idx.data_ptr()
+            if n == 0:
+                return
+        fn = L.gs_sim_set_root if kind == "root" else L.gs_sim_set_dof
+        _lib.check(fn(self.handle, src.data_ptr(), idx_ptr, n, s), f"set {kind}")
+        self._hold = (src, idx)  # keep alive until the launch consumed them (stream ordered)
+
+    def simulate(self):
+        L = _lib.lib()
+        _lib.check(L.gs_sim_simulate(self.handle, self.dof_force.data_ptr(), self.stream()), "gs_sim_simulate")
+
+
+# ------------------------------------------------------------------ Gym
+class Gym:
+    """The object returned by ``acquire_gym()`` (vec_task.py:247)."""
+
+    # ---- sim lifecycle
+    def create_sim(self, compute_device: int = 0, graphics_device: int = -1, type: int = SIM_PHYSX,
+                   params: Optional[SimParams] = None):
+        if type != SIM_PHYSX:
+            raise ValueError("only SIM_PHYSX semantics are implemented")
+        try:
+            return Sim(self, compute_device, params or SimParams())
+        except Exception as exc:  # reference callers test for None (vec_task.py:338)
+            print(f"*** gs_sim_create failed: {exc}")
+            return None
+
+    def destroy_sim(self, sim: Sim):
+        sim.__del__()
+        sim.handle = None
+
+    def get_sim_params(self, sim: Sim) -> SimParams:
+        return sim.params
+
+    def set_sim_params(self, sim: Sim, params: SimParams):
+        sim.params = params
+
+    def prepare_sim(self, sim: Sim) -> bool:
+        sim.prepare()
+        return True
+
+    def simulate(self, sim: Sim):
+        sim.simulate()
+
+    def fetch_results(self, sim: Sim, wait: bool = True):
+        if wait and not sim.gpu_pipeline:
+            import torch
+            torch.cuda.synchronize(sim.sim_device)
+
+    def get_sim_time(self, sim: Sim) -> float:
+        return 0.0
+
+    # ---- world geometry
+    def add_ground(self, sim: Sim, params: PlaneParams):
+        n = params.normal
+        if abs(n.z - 1.0) > 1e-6 or abs(n.x) > 1e-6 or abs(n.y) > 1e-6 or params.distance != 0.0:
+            raise NotImplementedError("only the z-up ground plane through the origin is supported")
+        sim.ground = params
+
+    def add_triangle_mesh(self, sim: Sim, vertices, triangles, params: TriangleMeshParams):
+        raise NotImplementedError("trimesh terrain is the next row of SURVEY.md section 8f (not built yet)")
+
+    # ---- assets
+    def load_asset(self, sim: Sim, root: str, filename: str, options: Optional[AssetOptions] = None) -> Asset:
+        options = options or AssetOptions()
+        raw = load_raw(root, filename)
+        art = build_articulation(raw, options.as_dict())
+        return Asset(art, options)
+
+    def get_asset_dof_count(self, asset: Asset) -> int:
+        return asset.art.num_dofs
+
+    def get_asset_rigid_body_count(self, asset: Asset) -> int:
+        return asset.art.num_bodies
+
+    def get_asset_rigid_shape_count(self, asset: Asset) -> int:
+        return asset.art.num_shapes
+
+    def get_asset_joint_count(self, asset: Asset) -> int:
+        return asset.art.num_dofs
+
+    def get_asset_rigid_body_names(self, asset: Asset) -> List[str]:
+        return asset.art.body_names()
+
+    def get_asset_rigid_body_name(self, asset: Asset, index: int) -> str:
+        return asset.art.body_names()[index]
+
+    def get_asset_dof_names(self, asset: Asset) -> List[str]:
+        return asset.art.dof_names()
+
+    def get_asset_dof_name(self, asset: Asset, index: int) -> str:
+        return asset.art.dof_names()[index]
+
+    def find_asset_rigid_body_index(self, asset: Asset, name: str) -> int:
+        names = asset.art.body_names()
+        return names.index(name) if name in names else INVALID_HANDLE
+
+    def find_asset_dof_index(self, asset: Asset, name: str) -> int:
+        names = asset.art.dof_names()
+        return names.index(name) if name in names else INVALID_HANDLE
+
+    def get_asset_dof_properties(self, asset: Asset):
+        return asset.dof_props.copy()
+
+    def get_asset_rigid_shape_properties(self, asset: Asset):
+        return [RigidShapeProperties(p.friction) for p in asset.shape_props]
+
+    def set_asset_rigid_shape_properties(self, asset: Asset, props) -> bool:
+        for dst, src in zip(asset.shape_props, props):
+            dst.friction = float(src.friction)
+            dst.restitution = float(getattr(src, "restitution", 0.0))
+        return True
+
+    def get_asset_actuator_properties(self, asset: Asset):
+        return [ActuatorProperties(d.effort) for d in asset.art.dofs]
+
+    def get_asset_actuator_count(self, asset: Asset) -> int:
+        return asset.art.num_dofs
+
+    def create_asset_force_sensor(self, asset: Asset, body_idx: int, pose: Transform, props=None):
+        raise NotImplementedError("force sensors belong to the Ant row (SURVEY.md 8f rank 4), not built yet")
+
+    # ---- envs / actors
+    def create_env(self, sim: Sim, lower: Vec3, upper: Vec3, num_per_row: int) -> Env:
+        i = len(sim.envs)
+        num_per_row = max(1, int(num_per_row))
+        row, col = divmod(i, num_per_row)
+        sx, sy = upper.x - lower.x, upper.y - lower.y
+        env = Env(sim, i, (col * sx, row * sy, 0.0))
+        sim.envs.append(env)
+        return env
+
+    def get_env_origin(self, env: Env) -> Vec3:
+        return Vec3(*env.origin)
+
+    def get_env_count(self, sim: Sim) -> int:
+        return len(sim.envs)
+
+    def create_actor(self, env: Env, asset: Asset, pose: Transform, name: str = "", group: int = -1,
+                     filter: int = -1, segmentation_id: int = 0) -> int:
+        a = Actor(env, asset, pose, name, group, filter)
+        env.actors.append(a)
+        owner = env.sim
+        if owner.asset is None:
+            owner.asset = asset
+        elif owner.asset is not asset:
+            raise NotImplementedError("one asset type per sim (DESIGN.md section 6)")
+        return len(env.actors) - 1
+
+    def get_actor_count(self, env: Env) -> int:
+        return len(env.actors)
+
+    def get_sim_actor_count(self, sim: Sim) -> int:
+        return sum(len(e.actors) for e in sim.envs)
+
+    def get_actor_dof_properties(self, env: Env, actor: int):
+        return env.actors[actor].dof_props.copy()
+
+    def set_actor_dof_properties(self, env: Env, actor: int, props) -> bool:
+        env.actors[actor].dof_props = np.array(props, dtype=DofPropertiesDtype).copy()
+        return True
+
+    def get_actor_rigid_shape_properties(self, env: Env, actor: int):
+        return [RigidShapeProperties(float(f)) for f in env.actors[actor].shape_friction]
+
+    def set_actor_rigid_shape_properties(self, env: Env, actor: int, props) -> bool:
+        env.actors[actor].shape_friction = np.array([p.friction for p in props], dtype=np.float32)
+        return True
+
+    def find_actor_rigid_body_handle(self, env: Env, actor: int, name: str) -> int:
+        names = env.actors[actor].asset.art.body_names()
+        return names.index(name) if name in names else INVALID_HANDLE
+
+    def find_actor_rigid_body_index(self, env: Env, actor: int, name: str, domain: int = DOMAIN_ENV) -> int:
+        return self.find_actor_rigid_body_handle(env, actor, name)
+
+    def find_actor_dof_handle(self, env: Env, actor: int, name: str) -> int:
+        names = env.actors[actor].asset.art.dof_names()
+        return names.index(name) if name in names else INVALID_HANDLE
+
+    def get_actor_dof_count(self, env: Env, actor: int) -> int:
+        return env.actors[actor].asset.art.num_dofs
+
+    def get_actor_rigid_body_count(self, env: Env, actor: int) -> int:
+        return env.actors[actor].asset.art.num_bodies
+
+    def get_actor_rigid_body_names(self, env: Env, actor: int):
+        return env.actors[actor].asset.art.body_names()
+
+    def get_actor_dof_names(self, env: Env, actor: int):
+        return env.actors[actor].asset.art.dof_names()
+
+    def get_actor_joint_dict(self, env: Env, actor: int):
+        return {n: i for i, n in enumerate(env.actors[actor].asset.art.dof_names())}
+
+    def get_actor_dof_dict(self, env: Env, actor: int):
+        return self.get_actor_joint_dict(env, actor)
+
+    def get_actor_rigid_body_dict(self, env: Env, actor: int):
+        return {n: i for i, n in enumerate(env.actors[actor].asset.art.body_names())}
+
+    def enable_actor_dof_force_sensors(self, env: Env, actor: int):
+        return True
+
+    def set_rigid_body_color(self, *args, **kwargs):
+        return None
+
+    # ---- tensor acquire (sim owned, zero copy)
+    def acquire_actor_root_state_tensor(self, sim: Sim) -> GymTensor:
+        return GymTensor(sim.root_tensor, "root")
+
+    def acquire_dof_state_tensor(self, sim: Sim) -> GymTensor:
+        return GymTensor(sim.dof_tensor, "dof")
+
+    def acquire_net_contact_force_tensor(self, sim: Sim) -> GymTensor:
+        return GymTensor(sim.contact_tensor, "contact")
+
+    def acquire_rigid_body_state_tensor(self, sim: Sim):
+        raise NotImplementedError("rigid body state tensor belongs to the UsefulHound row (not built yet)")
+
+    def acquire_force_sensor_tensor(self, sim: Sim):
+        raise NotImplementedError("force sensor tensor belongs to the Ant row (not built yet)")
+
+    def acquire_jacobian_tensor(self, sim: Sim, name: str):
+        raise NotImplementedError("jacobian tensor belongs to the UsefulHound row (not built yet)")
+
+    def acquire_mass_matrix_tensor(self, sim: Sim, name: str):
+        raise NotImplementedError("mass matrix tensor belongs to the UsefulHound row (not built yet)")
+
+    # ---- refresh (sim -> tensors)
+    def refresh_actor_root_state_tensor(self, sim: Sim):
+        sim.refresh("root")
+
+    def refresh_dof_state_tensor(self, sim: Sim):
+        sim.refresh("dof")
+
+    def refresh_net_contact_force_tensor(self, sim: Sim):
+        sim.refresh("contact")
+
+    def refresh_rigid_body_state_tensor(self, sim: Sim):
+        raise NotImplementedError("rigid body state tensor belongs to the UsefulHound row (not built yet)")
+
+    def refresh_force_sensor_tensor(self, sim: Sim):
+        raise NotImplementedError("force sensor tensor belongs to the Ant row (not built yet)")
+
+    def refresh_dof_force_tensor(self, sim: Sim):
+        return None
+
+    # ---- set (caller -> sim)
+    def set_dof_actuation_force_tensor(self, sim: Sim, t: GymTensor) -> bool:
+        sim.dof_force.copy_(t.tensor.reshape(-1).to(sim.sim_device))
+        return True
+
+    def set_dof_actuation_force_tensor_indexed(self, sim: Sim, t: GymTensor, idx: GymTensor, n: int) -> bool:
+        import torch
+        ids = idx.tensor[:n].to(sim.sim_device, dtype=torch.long)
+        src = t.tensor.reshape(sim.num_envs, sim.num_dofs).to(sim.sim_device)
+        sim.dof_force.view(sim.num_envs, sim.num_dofs)[ids] = src[ids]
+        return True
+
+    def set_actor_root_state_tensor(self, sim: Sim, t: GymTensor) -> bool:
+        sim.set_state("root", t.tensor)
+        return True
+
+    def set_actor_root_state_tensor_indexed(self, sim: Sim, t: GymTensor, idx: GymTensor, n: int) -> bool:
+        sim.set_state("root", t.tensor, idx.tensor, n)
+        return True
+
+    def set_dof_state_tensor(self, sim: Sim, t: GymTensor) -> bool:
+        sim.set_state("dof", t.tensor)
+        return True
+
+    def set_dof_state_tensor_indexed(self, sim: Sim, t: GymTensor, idx: GymTensor, n: int) -> bool:
+        sim.set_state("dof", t.tensor, idx.tensor, n)
+        return True
+
+    # ---- viewer / rendering (headless build: no-ops)
+    def create_viewer(self, sim: Sim, props: CameraProperties):
+        return None
+
+    def subscribe_viewer_keyboard_event(self, *args, **kwargs):
+        return None
+
+    def viewer_camera_look_at(self, *args, **kwargs):
+        return None
+
+    def query_viewer_has_closed(self, viewer) -> bool:
+        return False
+
+    def query_viewer_action_events(self, viewer):
+        return []
+
+    def step_graphics(self, sim: Sim):
+        return None
+
+    def draw_viewer(self, *args, **kwargs):
+        return None
+
+    def sync_frame_time(self, sim: Sim):
+        return None
+
+    def poll_viewer_events(self, viewer):
+        return None
+
+    def clear_lines(self, viewer):
+        return None
+
+    def destroy_viewer(self, viewer):
+        return None
+
+    # ---- MI355X extensions (not part of the Isaac Gym API)
+    def amd_pd_decimation_step(self, sim: Sim, actions, default_pos, kp: float, kd: float, action_scale: float,
+                               torque_limit: float, decimation: int, extra_simulates: int, torques_out,
+                               write_root: bool = True, write_contacts: bool = True):
+        """Fused ``for i in decimation: PD torque; simulate; refresh dof`` + ``extra_simulates`` more
+        simulates, + the root/contact refreshes of post_physics_step, in ONE kernel launch."""
+        L = _lib.lib()
+        a = _lib.GsPdArgs()
+        assert sim.gpu_pipeline, "the fused step needs the GPU pipeline"
+        a.actions = actions.data_ptr()
+        a.default_pos = default_pos.data_ptr()
+        a.kp, a.kd, a.action_scale, a.torque_limit = kp, kd, action_scale, torque_limit
+        a.decimation, a.extra_simulates = int(decimation), int(extra_simulates)
+        a.torques_out = torques_out.data_ptr()
+        a.dof_state_out = sim.dof_tensor.data_ptr()
+        a.root_state_out = sim.root_tensor.data_ptr() if write_root else None
+        a.contact_out = sim.contact_tensor.data_ptr() if write_contacts else None
+        _lib.check(L.gs_sim_pd_step(sim.handle, a, sim.stream()), "gs_sim_pd_step")
+
+    def amd_enable_kernel_timing(self, sim: Sim, enable: bool = True):
+        _lib.check(_lib.lib().gs_sim_enable_timing(sim.handle, int(enable)), "gs_sim_enable_timing")
+
+    def amd_last_kernel_ms(self, sim: Sim) -> float:
+        return float(_lib.lib().gs_sim_last_kernel_ms(sim.handle))
+
+
+_GYM = None
+
+
+def acquire_gym() -> Gym:
+    global _GYM
+    if _GYM is None:
+        _GYM = Gym()
+    return _GYM

@@ -1,0 +1,99 @@
+"""ctypes wrapper of the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline leg
+may import this module.  It never backs a product code path.
+
+Physics parity vs the reference (PhysX inside Isaac Gym) is UNPINNED; see the
+header of physics_oracle.c and DESIGN.md section 4.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+class OModel(C.Structure):
+    _fields_ = [("nb", C.c_int32), ("nd", C.c_int32), ("nc", C.c_int32), ("ns", C.c_int32),
+                ("fixed_base", C.c_int32)] + [
+        (n, C.c_void_p) for n in ("parent", "jkind", "bdof", "jorigin", "jaxis", "mass", "com", "inertia",
+                                  "cbody", "cpoint", "cradius", "cshape", "effort", "vmax", "armature")]
+
+
+class OParams(C.Structure):
+    _fields_ = [("dt", C.c_double), ("substeps", C.c_int32), ("gravity", C.c_double * 3),
+                ("pos_iters", C.c_int32), ("vel_iters", C.c_int32), ("contact_offset", C.c_double),
+                ("rest_offset", C.c_double), ("max_depen_vel", C.c_double), ("collect_contacts", C.c_int32),
+                ("has_ground", C.c_int32), ("ground_friction", C.c_double)]
+
+
+def build(quiet: bool = True) -> None:
+    out = subprocess.run(["make", "-C", HERE], capture_output=True, text=True)
+    if out.returncode != 0:
+        raise RuntimeError("oracle build failed:\n" + out.stdout + out.stderr)
+
+
+_LIBS = {}
+
+
+def _lib(real_bits: int):
+    if real_bits not in _LIBS:
+        path = os.path.join(HERE, f"liboracle{real_bits}.so")
+        if not os.path.exists(path):
+            build()
+        lib = C.CDLL(path)
+        lib.oracle_simulate.restype = C.c_int
+        lib.oracle_simulate.argtypes = [C.POINTER(OModel), C.POINTER(OParams), C.c_int] + [C.c_void_p] * 5 + [C.c_int]
+        _LIBS[real_bits] = lib
+    return _LIBS[real_bits]
+
+
+class OracleSim:
+    """Holds the model arrays alive and steps numpy state in place."""
+
+    def __init__(self, flat: dict, params: dict, real_bits: int = 64):
+        self.flat = flat
+        self.real = np.float64 if real_bits == 64 else np.float32
+        self.lib = _lib(real_bits)
+        keep = {}
+        m = OModel()
+        for k in ("nb", "nd", "nc", "ns", "fixed_base"):
+            setattr(m, k, int(flat[k]))
+        for k in ("parent", "jkind", "bdof", "cbody", "cshape"):
+            a = np.ascontiguousarray(flat[k], dtype=np.int32)
+            keep[k] = a
+            setattr(m, k, a.ctypes.data)
+        for k in ("jorigin", "jaxis", "mass", "com", "inertia", "cpoint", "cradius", "effort", "vmax", "armature"):
+            a = np.ascontiguousarray(flat[k], dtype=np.float64)
+            keep[k] = a
+            setattr(m, k, a.ctypes.data)
+        self._keep = keep
+        self.model = m
+        p = OParams()
+        p.dt = params["dt"]
+        p.substeps = params["substeps"]
+        for i in range(3):
+            p.gravity[i] = params["gravity"][i]
+        p.pos_iters = params["pos_iters"]
+        p.vel_iters = params["vel_iters"]
+        p.contact_offset = params["contact_offset"]
+        p.rest_offset = params["rest_offset"]
+        p.max_depen_vel = params["max_depen_vel"]
+        p.collect_contacts = params.get("collect_contacts", 1)
+        p.has_ground = params.get("has_ground", 1)
+        p.ground_friction = params.get("ground_friction", 1.0)
+        self.params = p
+
+    def simulate(self, root, dof, tau, mu, cf=None, num_threads: int = 1) -> None:
+        for a in (root, dof, tau, mu) + ((cf,) if cf is not None else ()):
+            assert a.dtype == self.real and a.flags.c_contiguous
+        n = root.shape[0]
+        rc = self.lib.oracle_simulate(C.byref(self.model), C.byref(self.params), n, root.ctypes.data,
+                                      dof.ctypes.data, tau.ctypes.data, mu.ctypes.data,
+                                      cf.ctypes.data if cf is not None else None, num_threads)
+        if rc != 0:
+            raise RuntimeError(f"oracle_simulate failed rc={rc}")

@@ -1,0 +1,476 @@
+/*
+ * physics_oracle.c -- TEST INFRASTRUCTURE ONLY (never linked into the product).
+ *
+ * CPU restatement, in plain C, of one `gym.simulate()` call of the build's
+ * articulation + plane-contact solver.  It is the checker the HIP kernels in
+ * isaacgymenv_amd/csrc/ are compared against; only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it.
+ *
+ * PARITY STATUS vs the reference: UNPINNED.  The reference's physics is the
+ * closed Isaac Gym / PhysX binary called at vec_task.py:382 and
+ * anymal_terrain.py:448; it is neither in
+ * /root/reference nor installable here.  This file restates the *solver
+ * specification written in DESIGN.md section 3*, which follows the config
+ * semantics the reference hands PhysX:
+ *   dt / substeps                     AnymalTerrain.yaml:129-131, vec_task.py:532-535
+ *   num_position/velocity_iterations  AnymalTerrain.yaml:138-139
+ *   contact_offset / rest_offset      AnymalTerrain.yaml:140-141
+ *   max_depenetration_velocity        AnymalTerrain.yaml:143
+ *   contact_collection (last substep) AnymalTerrain.yaml:146
+ *   ground friction / restitution     anymal_terrain.py:188-194
+ *   per-shape friction buckets        anymal_terrain.py:236-281
+ *   effort limit / velocity limit     anymal_minimal.urdf <limit effort velocity>
+ *
+ * The formulation here is deliberately different from the kernels: generic
+ * runtime topology, dense CRBA mass matrix, dense Cholesky, joint-space
+ * sequential impulses with W = M^-1 J^T.  The kernels use compile-time
+ * topology, the tree-sparse L^T D L factorisation and a w-space PGS.  Both
+ * produce the same iterates in exact arithmetic.
+ *
+ * REAL is double by default (the oracle); -DREAL=float builds the fp32
+ * CPU baseline (bench.py cpu_baseline, kind "port").
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#ifndef REAL
+#define REAL double
+#endif
+typedef REAL real;
+
+#define MAXB 32
+#define MAXV 40
+#define MAXC 96
+
+typedef struct {
+    int32_t nb, nd, nc, ns, fixed_base;
+    const int32_t *parent;      /* [nb] */
+    const int32_t *jkind;       /* [nb] 1 revolute 2 prismatic (root: 3 free / 0 fixed) */
+    const int32_t *bdof;        /* [nb] dof index of the body's joint, -1 for the root */
+    const double *jorigin;      /* [nb][12] R row-major (9) + t (3) */
+    const double *jaxis;        /* [nb][3] */
+    const double *mass;         /* [nb] */
+    const double *com;          /* [nb][3] */
+    const double *inertia;      /* [nb][9] about COM */
+    const int32_t *cbody;       /* [nc] */
+    const double *cpoint;       /* [nc][3] */
+    const double *cradius;      /* [nc] */
+    const int32_t *cshape;      /* [nc] */
+    const double *effort;       /* [nd] <= 0 : unlimited */
+    const double *vmax;         /* [nd] <= 0 : unlimited */
+    const double *armature;     /* [nd] */
+} OModel;
+
+typedef struct {
+    double dt;
+    int32_t substeps;
+    double gravity[3];
+    int32_t pos_iters, vel_iters;
+    double contact_offset, rest_offset, max_depen_vel;
+    int32_t collect_contacts;
+    int32_t has_ground;
+    double ground_friction;
+} OParams;
+
+/* ---------------------------------------------------------------- helpers */
+static inline void cross3(const real *a, const real *b, real *o) {
+    real x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+static inline real dot3(const real *a, const real *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static inline void matvec3(const real *R, const real *v, real *o) {
+    real x = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
+    real y = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
+    real z = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+static inline void matmul3(const real *A, const real *B, real *C) {
+    real T[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) T[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+    memcpy(C, T, sizeof(T));
+}
+/* Rodrigues rotation about unit axis a by angle t */
+static void axis_angle(const real *a, real t, real *R) {
+    real c = cos(t), s = sin(t), C = 1 - c;
+    real x = a[0], y = a[1], z = a[2];
+    R[0] = c + x * x * C;     R[1] = x * y * C - z * s; R[2] = x * z * C + y * s;
+    R[3] = y * x * C + z * s; R[4] = c + y * y * C;     R[5] = y * z * C - x * s;
+    R[6] = z * x * C - y * s; R[7] = z * y * C + x * s; R[8] = c + z * z * C;
+}
+static void quat_to_mat(const real *q, real *R) { /* xyzw */
+    real x = q[0], y = q[1], z = q[2], w = q[3];
+    R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w);     R[2] = 2 * (x * z + y * w);
+    R[3] = 2 * (x * y + z * w);     R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - x * w);
+    R[6] = 2 * (x * z - y * w);     R[7] = 2 * (y * z + x * w);     R[8] = 1 - 2 * (x * x + y * y);
+}
+
+/* spatial inertia at O (world axes): m, h = m c, I_O (3x3) */
+typedef struct { real m, h[3], I[9]; } SpI;
+
+/* f = I * (w, v) = (I_O w + h x v, m v - h x w) */
+static void spi_mul(const SpI *I, const real *mv, real *f) {
+    real hv[3], hw[3], n[3];
+    matvec3(I->I, mv, n);
+    cross3(I->h, mv + 3, hv);
+    cross3(I->h, mv, hw);
+    for (int k = 0; k < 3; ++k) { f[k] = n[k] + hv[k]; f[3 + k] = I->m * mv[3 + k] - hw[k]; }
+}
+/* motion cross motion: (w,v) x (w',v') = (w x w', w x v' + v x w') */
+static void crm(const real *a, const real *b, real *o) {
+    real t1[3], t2[3], t3[3];
+    cross3(a, b, t1); cross3(a, b + 3, t2); cross3(a + 3, b, t3);
+    for (int k = 0; k < 3; ++k) { o[k] = t1[k]; o[3 + k] = t2[k] + t3[k]; }
+}
+/* motion cross force: (w,v) x* (n,f) = (w x n + v x f, w x f) */
+static void crf(const real *a, const real *b, real *o) {
+    real t1[3], t2[3], t3[3];
+    cross3(a, b, t1); cross3(a + 3, b + 3, t2); cross3(a, b + 3, t3);
+    for (int k = 0; k < 3; ++k) { o[k] = t1[k] + t2[k]; o[3 + k] = t3[k]; }
+}
+static inline real dot6(const real *a, const real *b) {
+    real s = 0; for (int k = 0; k < 6; ++k) s += a[k] * b[k]; return s;
+}
+
+/* dense Cholesky M = L L^T in place (lower), n x n, row stride MAXV */
+static void chol(real *A, int n) {
+    for (int j = 0; j < n; ++j) {
+        real s = A[j * MAXV + j];
+        for (int k = 0; k < j; ++k) s -= A[j * MAXV + k] * A[j * MAXV + k];
+        real d = sqrt(s > 0 ? s : (real)1e-30);
+        A[j * MAXV + j] = d;
+        for (int i = j + 1; i < n; ++i) {
+            real t = A[i * MAXV + j];
+            for (int k = 0; k < j; ++k) t -= A[i * MAXV + k] * A[j * MAXV + k];
+            A[i * MAXV + j] = t / d;
+        }
+    }
+}
+static void chol_solve(const real *L, int n, const real *b, real *x) {
+    real y[MAXV];
+    for (int i = 0; i < n; ++i) {
+        real t = b[i];
+        for (int k = 0; k < i; ++k) t -= L[i * MAXV + k] * y[k];
+        y[i] = t / L[i * MAXV + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        real t = y[i];
+        for (int k = i + 1; k < n; ++k) t -= L[k * MAXV + i] * x[k];
+        x[i] = t / L[i * MAXV + i];
+    }
+}
+
+/* ------------------------------------------------------------- one env */
+static void env_substep(const OModel *m, const OParams *p, real h,
+                        real *root, real *dq, const real *tau_in, const real *mu_shape,
+                        real *cforce /* nb*3 or NULL */)
+{
+    const int nb = m->nb, nd = m->nd, fb = m->fixed_base;
+    const int nbase = fb ? 0 : 6, nv = nbase + nd;
+    real R[MAXB][9], P[MAXB][3], S[MAXB][6], V[MAXB][6];
+    SpI Ib[MAXB], Ic[MAXB];
+
+    /* ---- forward kinematics (positions relative to the root origin) */
+    {
+        real q4[4] = {root[3], root[4], root[5], root[6]};
+        quat_to_mat(q4, R[0]);
+        P[0][0] = P[0][1] = P[0][2] = 0;
+    }
+    for (int i = 1; i < nb; ++i) {
+        const int pa = m->parent[i];
+        real Ro[9], to[3], RJ[9], a[3], tt[3];
+        for (int k = 0; k < 9; ++k) Ro[k] = (real)m->jorigin[12 * i + k];
+        for (int k = 0; k < 3; ++k) { to[k] = (real)m->jorigin[12 * i + 9 + k]; a[k] = (real)m->jaxis[3 * i + k]; }
+        matmul3(R[pa], Ro, RJ);
+        matvec3(R[pa], to, tt);
+        for (int k = 0; k < 3; ++k) P[i][k] = P[pa][k] + tt[k];
+        real aw[3];
+        matvec3(RJ, a, aw);
+        const real qj = dq[2 * m->bdof[i]];
+        if (m->jkind[i] == 1) {
+            real Rq[9];
+            axis_angle(a, qj, Rq);
+            matmul3(RJ, Rq, R[i]);
+            S[i][0] = aw[0]; S[i][1] = aw[1]; S[i][2] = aw[2];
+            cross3(P[i], aw, S[i] + 3);
+        } else {
+            memcpy(R[i], RJ, sizeof(RJ));
+            for (int k = 0; k < 3; ++k) P[i][k] += aw[k] * qj;
+            S[i][0] = S[i][1] = S[i][2] = 0;
+            S[i][3] = aw[0]; S[i][4] = aw[1]; S[i][5] = aw[2];
+        }
+    }
+    /* ---- spatial inertias at O */
+    for (int i = 0; i < nb; ++i) {
+        real c[3], cl[3], Il[9], T[9], RT[9], Iw[9];
+        for (int k = 0; k < 3; ++k) cl[k] = (real)m->com[3 * i + k];
+        for (int k = 0; k < 9; ++k) Il[k] = (real)m->inertia[9 * i + k];
+        matvec3(R[i], cl, c);
+        for (int k = 0; k < 3; ++k) c[k] += P[i][k];
+        for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) RT[3 * a + b] = R[i][3 * b + a];
+        matmul3(R[i], Il, T);
+        matmul3(T, RT, Iw);
+        const real mm = (real)m->mass[i];
+        const real cc = dot3(c, c);
+        Ib[i].m = mm;
+        for (int k = 0; k < 3; ++k) Ib[i].h[k] = mm * c[k];
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b)
+                Ib[i].I[3 * a + b] = Iw[3 * a + b] + mm * ((a == b ? cc : 0) - c[a] * c[b]);
+        Ic[i] = Ib[i];
+    }
+    for (int i = nb - 1; i > 0; --i) {
+        const int pa = m->parent[i];
+        Ic[pa].m += Ic[i].m;
+        for (int k = 0; k < 3; ++k) Ic[pa].h[k] += Ic[i].h[k];
+        for (int k = 0; k < 9; ++k) Ic[pa].I[k] += Ic[i].I[k];
+    }
+
+    /* ---- generalized velocity nu = (w, pdot, qd) */
+    real nu[MAXV];
+    if (!fb) { for (int k = 0; k < 3; ++k) { nu[k] = root[10 + k]; nu[3 + k] = root[7 + k]; } }
+    for (int j = 0; j < nd; ++j) nu[nbase + j] = dq[2 * j + 1];
+
+    /* ---- RNEA bias with gravity (A_0 = (0, -g)) */
+    real A[MAXB][6], F[MAXB][6];
+    for (int k = 0; k < 6; ++k) V[0][k] = 0;
+    if (!fb) { for (int k = 0; k < 6; ++k) V[0][k] = nu[k]; }
+    A[0][0] = A[0][1] = A[0][2] = 0;
+    for (int k = 0; k < 3; ++k) A[0][3 + k] = -(real)p->gravity[k];
+    for (int i = 1; i < nb; ++i) {
+        const int pa = m->parent[i];
+        const real qd = nu[nbase + m->bdof[i]];
+        for (int k = 0; k < 6; ++k) V[i][k] = V[pa][k] + S[i][k] * qd;
+        real c[6];
+        crm(V[i], S[i], c);
+        for (int k = 0; k < 6; ++k) A[i][k] = A[pa][k] + c[k] * qd;
+    }
+    for (int i = 0; i < nb; ++i) {
+        real ia[6], iv[6], x[6];
+        spi_mul(&Ib[i], A[i], ia);
+        spi_mul(&Ib[i], V[i], iv);
+        crf(V[i], iv, x);
+        for (int k = 0; k < 6; ++k) F[i][k] = ia[k] + x[k];
+    }
+    for (int i = nb - 1; i > 0; --i)
+        for (int k = 0; k < 6; ++k) F[m->parent[i]][k] += F[i][k];
+    real bias[MAXV];
+    if (!fb) for (int k = 0; k < 6; ++k) bias[k] = F[0][k];
+    for (int i = 1; i < nb; ++i) bias[nbase + m->bdof[i]] = dot6(S[i], F[i]);
+
+    /* ---- CRBA dense mass matrix */
+    real M[MAXV * MAXV];
+    memset(M, 0, sizeof(M));
+    if (!fb) {
+        const SpI *I0 = &Ic[0];
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) {
+                M[a * MAXV + b] = I0->I[3 * a + b];
+                M[(3 + a) * MAXV + (3 + b)] = (a == b) ? I0->m : 0;
+            }
+        /* upper-right block [h]x, lower-left [h]x^T */
+        const real *hh = I0->h;
+        real hx[9] = {0, -hh[2], hh[1], hh[2], 0, -hh[0], -hh[1], hh[0], 0};
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) {
+                M[a * MAXV + 3 + b] = hx[3 * a + b];
+                M[(3 + b) * MAXV + a] = hx[3 * a + b];
+            }
+    }
+    for (int i = 1; i < nb; ++i) {
+        const int di = nbase + m->bdof[i];
+        real Fi[6];
+        spi_mul(&Ic[i], S[i], Fi);
+        M[di * MAXV + di] = dot6(S[i], Fi) + (real)m->armature[m->bdof[i]];
+        for (int j = m->parent[i]; j > 0; j = m->parent[j]) {
+            const int dj = nbase + m->bdof[j];
+            const real v = dot6(S[j], Fi);
+            M[di * MAXV + dj] = v; M[dj * MAXV + di] = v;
+        }
+        if (!fb) for (int k = 0; k < 6; ++k) { M[di * MAXV + k] = Fi[k]; M[k * MAXV + di] = Fi[k]; }
+    }
+    chol(M, nv);
+
+    /* ---- free velocity */
+    real rhs[MAXV], acc[MAXV], nuf[MAXV];
+    for (int k = 0; k < nbase; ++k) rhs[k] = -bias[k];
+    for (int j = 0; j < nd; ++j) {
+        real t = tau_in[j];
+        const real e = (real)m->effort[j];
+        if (e > 0) t = t > e ? e : (t < -e ? -e : t);
+        rhs[nbase + j] = t - bias[nbase + j];
+    }
+    chol_solve(M, nv, rhs, acc);
+    for (int k = 0; k < nv; ++k) nuf[k] = nu[k] + h * acc[k];
+    if (!fb) {
+        real wxp[3];
+        cross3(nu, nu + 3, wxp);
+        for (int k = 0; k < 3; ++k) nuf[3 + k] += h * wxp[k];
+    }
+
+    /* ---- contacts vs the ground plane z = 0 */
+    int nact = 0;
+    int ck[MAXC];
+    real cs[MAXC], cmu[MAXC];
+    static const int row_axis[3] = {2, 0, 1}; /* normal z, tangent x, tangent y */
+    const int ncap = m->nc > 0 ? m->nc : 1;
+    real J[3 * ncap * MAXV], W[3 * ncap * MAXV];
+    real Dr[3 * MAXC];
+    if (p->has_ground) {
+        for (int c = 0; c < m->nc; ++c) {
+            const int b = m->cbody[c];
+            real xl[3], x[3];
+            for (int k = 0; k < 3; ++k) xl[k] = (real)m->cpoint[3 * c + k];
+            matvec3(R[b], xl, x);
+            for (int k = 0; k < 3; ++k) x[k] += P[b][k];
+            const real r = (real)m->cradius[c];
+            const real dist = root[2] + x[2] - r;
+            if (!(dist < (real)p->contact_offset)) continue;
+            real xc[3] = {x[0], x[1], x[2] - r};
+            real Jp[3][MAXV];
+            for (int a = 0; a < 3; ++a) for (int k = 0; k < nv; ++k) Jp[a][k] = 0;
+            if (!fb) {
+                /* d(w x xc)/dw = -[xc]x */
+                Jp[0][0] = 0;      Jp[0][1] = xc[2];  Jp[0][2] = -xc[1];
+                Jp[1][0] = -xc[2]; Jp[1][1] = 0;      Jp[1][2] = xc[0];
+                Jp[2][0] = xc[1];  Jp[2][1] = -xc[0]; Jp[2][2] = 0;
+                Jp[0][3] = 1; Jp[1][4] = 1; Jp[2][5] = 1;
+            }
+            for (int i = b; i > 0; i = m->parent[i]) {
+                real t[3];
+                cross3(S[i], xc, t);
+                const int di = nbase + m->bdof[i];
+                for (int a = 0; a < 3; ++a) Jp[a][di] = S[i][3 + a] + t[a];
+            }
+            for (int rr = 0; rr < 3; ++rr) {
+                real *Jr = J + (3 * nact + rr) * MAXV;
+                real *Wr = W + (3 * nact + rr) * MAXV;
+                for (int k = 0; k < nv; ++k) Jr[k] = Jp[row_axis[rr]][k];
+                chol_solve(M, nv, Jr, Wr);
+                real d = 0;
+                for (int k = 0; k < nv; ++k) d += Jr[k] * Wr[k];
+                Dr[3 * nact + rr] = d;
+            }
+            ck[nact] = c;
+            cs[nact] = dist - (real)p->rest_offset;
+            cmu[nact] = (real)0.5 * (mu_shape[m->cshape[c]] + (real)p->ground_friction);
+            ++nact;
+        }
+    }
+
+    /* ---- sequential impulses (joint space) */
+    real v[MAXV], lam[3 * MAXC], nupos[MAXV];
+    memcpy(v, nuf, sizeof(real) * nv);
+    for (int k = 0; k < 3 * nact; ++k) lam[k] = 0;
+    const int iters = p->pos_iters + p->vel_iters;
+    for (int it = 0; it < iters; ++it) {
+        const int pos_phase = it < p->pos_iters;
+        for (int a = 0; a < nact; ++a) {
+            const real s = cs[a];
+            /* normal */
+            {
+                const int r = 3 * a;
+                const real *Jr = J + r * MAXV, *Wr = W + r * MAXV;
+                real u = 0;
+                for (int k = 0; k < nv; ++k) u += Jr[k] * v[k];
+                real target;
+                if (s >= 0) target = -s / h;
+                else if (pos_phase) { target = -s / h; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
+                else target = 0;
+                real ln = lam[r] + (target - u) / Dr[r];
+                if (ln < 0) ln = 0;
+                const real dl = ln - lam[r];
+                lam[r] = ln;
+                for (int k = 0; k < nv; ++k) v[k] += Wr[k] * dl;
+            }
+            for (int t = 1; t < 3; ++t) {
+                const int r = 3 * a + t;
+                const real *Jr = J + r * MAXV, *Wr = W + r * MAXV;
+                real u = 0;
+                for (int k = 0; k < nv; ++k) u += Jr[k] * v[k];
+                const real lim = cmu[a] * lam[3 * a];
+                real lt = lam[r] - u / Dr[r];
+                if (lt > lim) lt = lim;
+                if (lt < -lim) lt = -lim;
+                const real dl = lt - lam[r];
+                lam[r] = lt;
+                for (int k = 0; k < nv; ++k) v[k] += Wr[k] * dl;
+            }
+        }
+        if (it == p->pos_iters - 1) memcpy(nupos, v, sizeof(real) * nv);
+    }
+    if (p->pos_iters == 0) memcpy(nupos, v, sizeof(real) * nv);
+
+    /* ---- joint velocity limits */
+    for (int j = 0; j < nd; ++j) {
+        const real vm = (real)m->vmax[j];
+        if (vm > 0) {
+            real *a = &v[nbase + j], *b = &nupos[nbase + j];
+            if (*a > vm) *a = vm; if (*a < -vm) *a = -vm;
+            if (*b > vm) *b = vm; if (*b < -vm) *b = -vm;
+        }
+    }
+
+    /* ---- integrate positions with nu_pos, keep velocities nu_new */
+    if (!fb) {
+        for (int k = 0; k < 3; ++k) root[k] += h * nupos[3 + k];
+        const real *w = nupos;
+        real x = root[3], y = root[4], z = root[5], qw = root[6];
+        real dx = 0.5 * h * (qw * w[0] + w[1] * z - w[2] * y);
+        real dy = 0.5 * h * (qw * w[1] + w[2] * x - w[0] * z);
+        real dz = 0.5 * h * (qw * w[2] + w[0] * y - w[1] * x);
+        real dw = 0.5 * h * (-(w[0] * x + w[1] * y + w[2] * z));
+        x += dx; y += dy; z += dz; qw += dw;
+        const real n = 1 / sqrt(x * x + y * y + z * z + qw * qw);
+        root[3] = x * n; root[4] = y * n; root[5] = z * n; root[6] = qw * n;
+        for (int k = 0; k < 3; ++k) { root[10 + k] = v[k]; root[7 + k] = v[3 + k]; }
+    }
+    for (int j = 0; j < nd; ++j) {
+        dq[2 * j] += h * nupos[nbase + j];
+        dq[2 * j + 1] = v[nbase + j];
+    }
+    if (cforce) {
+        for (int k = 0; k < 3 * nb; ++k) cforce[k] = 0;
+        for (int a = 0; a < nact; ++a) {
+            const int b = m->cbody[ck[a]];
+            cforce[3 * b + 0] += lam[3 * a + 1] / h;
+            cforce[3 * b + 1] += lam[3 * a + 2] / h;
+            cforce[3 * b + 2] += lam[3 * a + 0] / h;
+        }
+    }
+}
+
+/*
+ * One gym.simulate() for n_envs environments.
+ * root  : [N][13] pos(3) quat xyzw(4) v_origin(3) w(3)   (internal: root ORIGIN velocity)
+ * dof   : [N][nd][2] (q, qd)
+ * tau   : [N][nd]
+ * mu    : [N][ns]     per-env shape friction
+ * cf    : [N][nb][3]  net contact force (written when collect_contacts), may be NULL
+ */
+int oracle_simulate(const OModel *m, const OParams *p, int n_envs, real *root, real *dof,
+                    const real *tau, const real *mu, real *cf, int num_threads)
+{
+    if (m->nb > MAXB || m->nd + 6 > MAXV || m->nc > MAXC) return -1;
+    const real h = (real)(p->dt / (p->substeps > 0 ? p->substeps : 1));
+#ifdef _OPENMP
+    if (num_threads > 0) omp_set_num_threads(num_threads);
+#pragma omp parallel for schedule(static)
+#endif
+    for (int e = 0; e < n_envs; ++e) {
+        for (int s = 0; s < p->substeps; ++s) {
+            const int last = (s == p->substeps - 1);
+            env_substep(m, p, h, root + 13 * e, dof + 2 * m->nd * e, tau + m->nd * e, mu + m->ns * e,
+                        (cf && p->collect_contacts && last) ? cf + 3 * m->nb * e : NULL);
+        }
+    }
+    (void)num_threads;
+    return 0;
+}
+
+int oracle_real_size(void) { return (int)sizeof(real); }

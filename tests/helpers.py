@@ -1,0 +1,122 @@
+"""Shared test helpers (test infrastructure)."""
+import json
+import os
+
+import numpy as np
+
+from isaacgymenv_amd.isaacgym._assets import PACKED_DIR, RawModel, build_articulation
+from isaacgymenv_amd.isaacgym._model import flatten
+
+ANYMAL_OPTS = dict(collapse_fixed_joints=True, replace_cylinder_with_capsule=True)
+CARTPOLE_OPTS = dict(fix_base_link=True)
+ANYMAL_DEFAULT = {"LF_HAA": 0.03, "LH_HAA": 0.03, "RF_HAA": -0.03, "RH_HAA": -0.03, "LF_HFE": 0.4,
+                  "LH_HFE": -0.4, "RF_HFE": 0.4, "RH_HFE": -0.4, "LF_KFE": -0.8, "LH_KFE": 0.8,
+                  "RF_KFE": -0.8, "RH_KFE": 0.8}
+# AnymalTerrain.yaml:129-146
+ANYMAL_PARAMS = dict(dt=0.005, substeps=1, gravity=[0.0, 0.0, -9.81], pos_iters=4, vel_iters=1,
+                     contact_offset=0.02, rest_offset=0.0, max_depen_vel=100.0, collect_contacts=1,
+                     has_ground=1, ground_friction=1.0)
+# Cartpole.yaml:23-42
+CARTPOLE_PARAMS = dict(dt=0.0166, substeps=2, gravity=[0.0, 0.0, -9.81], pos_iters=4, vel_iters=0,
+                       contact_offset=0.02, rest_offset=0.001, max_depen_vel=100.0, collect_contacts=0,
+                       has_ground=1, ground_friction=1.0)
+
+
+def load_art(name, opts):
+    with open(os.path.join(PACKED_DIR, name)) as f:
+        return build_articulation(RawModel.from_json(json.load(f)), opts)
+
+
+def anymal():
+    art = load_art("anymal_c.model.json", ANYMAL_OPTS)
+    return art, flatten(art)
+
+
+def cartpole():
+    art = load_art("cartpole.model.json", CARTPOLE_OPTS)
+    return art, flatten(art)
+
+
+def anymal_states(n, seed=0, spread=1.0):
+    """Random but physically plausible ANYmal states: standing, airborne, penetrating, tilted."""
+    rng = np.random.RandomState(seed)
+    art, flat = anymal()
+    q0 = np.array([ANYMAL_DEFAULT[d] for d in art.dof_names()])
+    root = np.zeros((n, 13))
+    root[:, 0:2] = rng.uniform(-2, 2, (n, 2))
+    root[:, 2] = rng.uniform(0.45, 0.65, n)
+    axis = rng.normal(size=(n, 3))
+    axis /= np.linalg.norm(axis, axis=1, keepdims=True)
+    ang = rng.uniform(0, 0.25 * spread, n)
+    root[:, 3:6] = axis * np.sin(ang / 2)[:, None]
+    root[:, 6] = np.cos(ang / 2)
+    root[:, 7:10] = rng.normal(0, 0.3 * spread, (n, 3))
+    root[:, 10:13] = rng.normal(0, 0.5 * spread, (n, 3))
+    dof = np.zeros((n, 12, 2))
+    dof[:, :, 0] = q0 * rng.uniform(0.5, 1.5, (n, 12))
+    dof[:, :, 1] = rng.normal(0, 1.0 * spread, (n, 12))
+    tau = rng.uniform(-80, 80, (n, 12))
+    mu = np.repeat(rng.uniform(0.5, 1.25, (n, 1)), flat["ns"], axis=1)
+    return root, dof, tau, mu
+
+
+def make_gpu_sim(kind: str, n: int, params: dict):
+    """A libgymsim sim built through the drop-in gymapi (GPU pipeline)."""
+    from isaacgymenv_amd.isaacgym import gymapi
+    gym = gymapi.acquire_gym()
+    sp = gymapi.SimParams()
+    sp.dt = params["dt"]
+    sp.substeps = params["substeps"]
+    sp.up_axis = gymapi.UP_AXIS_Z
+    sp.gravity = gymapi.Vec3(*params["gravity"])
+    sp.use_gpu_pipeline = True
+    sp.physx.num_position_iterations = params["pos_iters"]
+    sp.physx.num_velocity_iterations = params["vel_iters"]
+    sp.physx.contact_offset = params["contact_offset"]
+    sp.physx.rest_offset = params["rest_offset"]
+    sp.physx.max_depenetration_velocity = params["max_depen_vel"]
+    sp.physx.contact_collection = gymapi.ContactCollection(params["collect_contacts"])
+    sim = gym.create_sim(0, -1, gymapi.SIM_PHYSX, sp)
+    assert sim is not None
+    if params.get("has_ground", 1):
+        plane = gymapi.PlaneParams()
+        plane.static_friction = params.get("ground_friction", 1.0)
+        gym.add_ground(sim, plane)
+    opts = gymapi.AssetOptions()
+    if kind == "anymal":
+        opts.collapse_fixed_joints = True
+        opts.replace_cylinder_with_capsule = True
+        opts.default_dof_drive_mode = gymapi.DOF_MODE_EFFORT
+        asset = gym.load_asset(sim, "/nonexistent", "urdf/anymal_c/urdf/anymal_minimal.urdf", opts)
+    else:
+        opts.fix_base_link = True
+        asset = gym.load_asset(sim, "/nonexistent", "urdf/cartpole.urdf", opts)
+    for i in range(n):
+        env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 1), 8)
+        pose = gymapi.Transform()
+        pose.p = gymapi.Vec3(0, 0, 0.62 if kind == "anymal" else 2.0)
+        gym.create_actor(env, asset, pose, kind, i, 0, 0)
+    gym.prepare_sim(sim)
+    return gym, sim
+
+
+def load_state_into(sim, root, dof, mu):
+    """Write oracle-layout numpy state ([N,13] internal root, [N,nd,2]) into the SoA sim state."""
+    import torch
+    n, nd = root.shape[0], dof.shape[1]
+    st = np.zeros((13 + 2 * nd, n), dtype=np.float32)
+    st[0:13] = root.T
+    st[13:13 + nd] = dof[:, :, 0].T
+    st[13 + nd:] = dof[:, :, 1].T
+    sim.state.copy_(torch.from_numpy(st))
+    m = np.ones(tuple(sim.shape_mu.shape), dtype=np.float32)
+    m[:mu.shape[1]] = mu.T
+    sim.shape_mu.copy_(torch.from_numpy(m))
+
+
+def read_state(sim, nd):
+    st = sim.state.cpu().numpy().astype(np.float64)
+    n = st.shape[1]
+    root = st[0:13].T.copy()
+    dof = np.stack([st[13:13 + nd].T, st[13 + nd:].T], axis=-1)
+    return root, dof
