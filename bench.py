@@ -1,0 +1,191 @@
+#!/usr/bin/env python3
+"""Benchmark: AnymalTerrain VecTask.step throughput (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--num-envs 4096] [--no-cpu-baseline]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One "step" = one ``VecTask.step(actions)`` of AnymalTerrain (default config:
+terrainType plane, 4096 envs per GPU, seed 42 + rank) with synthetic uniform
+actions in [-1, 1): 5 physics substeps (decimation 4 + controlFrequencyInv 1),
+the post-physics tail, resets, observation noise.  Envs shard across ranks with
+no data-path collective (weak scaling); the only collectives are the barrier and
+the max-over-ranks of the timed region.
+
+The rank-0 JSON line carries:
+  roofline     -- the fused physics kernel (gs_sim_pd_step): algorithmic HBM bytes
+                  per launch / its average HIP-event duration on the launch stream;
+  cpu_baseline -- the fp32 build of the CPU oracle (oracle/, kind "port") stepping
+                  a bounded sample of the same workload on the host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured float4 copy
+
+
+def physics_kernel_bytes_per_env(nd=12, nb=13, ns=9):
+    """Algorithmic HBM bytes one env moves through gs_sim_pd_step.
+
+    reads : SoA state (13 + 2 nd) f32, actions nd, dof tensor (q, qd) 2 nd, shape friction ns
+    writes: SoA state (13 + 2 nd), torques nd, dof tensor 2 nd, root tensor 13,
+            contact forces SoA 3 nb + AoS 3 nb
+    """
+    state = 13 + 2 * nd
+    reads = state + nd + 2 * nd + ns
+    writes = state + nd + 2 * nd + 13 + 6 * nb
+    return 4 * (reads + writes)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--num-envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall budget of the CPU baseline sample")
+    ap.add_argument("--kernel-launches", type=int, default=50, help="launches timed for the roofline figure")
+    return ap.parse_args()
+
+
+def cpu_baseline(num_envs: int, seconds: float):
+    """fp32 CPU oracle on the same per-env work: PD (decimation 4) + 5 substeps per env step."""
+    import numpy as np
+    from oracle.oracle import OracleSim
+    from tests import helpers as H
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    art, flat = H.anymal()
+    sim = OracleSim(flat, H.ANYMAL_PARAMS, real_bits=32)
+    n = min(num_envs, 4096)
+    q0 = np.array([H.ANYMAL_DEFAULT[d] for d in art.dof_names()], dtype=np.float32)
+    root = np.zeros((n, 13), dtype=np.float32); root[:, 2] = 0.62; root[:, 6] = 1.0
+    dof = np.zeros((n, 12, 2), dtype=np.float32); dof[:, :, 0] = q0
+    mu = np.ones((n, flat["ns"]), dtype=np.float32)
+    rng = np.random.RandomState(0)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        a = (2 * rng.rand(n, 12) - 1).astype(np.float32)
+        for sub in range(5):
+            if sub < 4:
+                tau = np.clip(80.0 * (0.5 * a + q0 - dof[:, :, 0]) - 2.0 * dof[:, :, 1], -80, 80).astype(np.float32)
+            sim.simulate(root, dof, np.ascontiguousarray(tau), mu, num_threads=threads)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and steps >= 2:
+            break
+    return {"value": n * steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"fp32 oracle (oracle/physics_oracle.c) physics only: {n} envs x {steps} env steps "
+                      f"(PD decimation 4 + 5 substeps each) in {el:.1f} s on {threads} threads; the reference's "
+                      f"Python tail (8.9-12.5 ms/step at 4096 envs, SURVEY.md section 6) is not included"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+    device = f"cuda:{local_rank}"
+
+    import isaacgymenvs
+    from isaacgymenv_amd.isaacgymenvs.utils.utils import set_seed
+    set_seed(42, rank=rank)
+    env = isaacgymenvs.make(seed=42 + rank, task="AnymalTerrain", num_envs=args.num_envs, sim_device=device,
+                            rl_device=device, graphics_device_id=-1, headless=True, force_render=False)
+    N, A = env.num_envs, env.num_actions
+    gen = torch.Generator(device=device)
+    gen.manual_seed(1234 + rank)
+    env.reset()
+
+    def step():
+        actions = 2.0 * torch.rand((N, A), device=device, generator=gen) - 1.0
+        env.step(actions)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- roofline of the dominant kernel: HIP events on the launch stream around the fused physics launches
+    stream = torch.cuda.current_stream(device)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    actions = 2.0 * torch.rand((N, A), device=device, generator=gen) - 1.0
+    env.actions = actions.clone()
+    stream.synchronize()
+    ev0.record(stream)
+    for _ in range(args.kernel_launches):
+        env.fused_physics_step(actions)
+    ev1.record(stream)
+    ev1.synchronize()
+    kernel_ms = ev0.elapsed_time(ev1) / args.kernel_launches
+    bytes_per_launch = physics_kernel_bytes_per_env() * N
+    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_pd_step.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                d = json.load(f)
+            if d.get("num_envs") == N:
+                traffic = d.get("hbm_bytes_per_launch")
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(N, args.cpu_seconds)
+        total_env_steps = N * world * args.steps
+        line = {
+            "metric": "env-steps/sec AnymalTerrain 4096 envs/GPU",
+            "value": total_env_steps / elapsed,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (uniform random actions in [-1,1), seed 42+rank; random-init sim state via reset_idx)",
+            "config": {"workload": "AnymalTerrain VecTask.step, terrainType plane (AnymalTerrain.yaml default), "
+                                   "5 physics substeps/step, obs noise on",
+                       "num_envs_per_gpu": N, "global_num_envs": N * world, "parallelism": f"dp{world}"},
+            "roofline": {"bound": "hbm", "kernel": "gs_sim_pd_step (k_pd_step<Topo_anymal_c>)",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic, "kernel_ms": kernel_ms, "bytes_per_launch": bytes_per_launch},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

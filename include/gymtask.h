@@ -1,0 +1,92 @@
+/*
+ * gymtask.h -- C ABI of libgymtask.so: fused task-layer kernels for the
+ * post-physics tail of VecTask.step (reference tasks/anymal_terrain.py).
+ *
+ * The reference computes this tail as ~790 small torch/TorchScript ops per
+ * step; these entry points replace, for AnymalTerrain:
+ *   gt_anymal_post_physics_a : anymal_terrain.py:458-475 minus the push
+ *       progress/randomize counters, base-frame velocities and gravity
+ *       (quat_rotate_inverse x3), heading command (quat_apply, atan2,
+ *       wrap_to_pi), check_termination (:294-300), compute_reward (:315-382)
+ *       incl. feet air time and episode sums.
+ *   gt_anymal_reset : reset_idx (:384-425) given the random draws the host made
+ *       with torch in the reference's order (bit-exact resets).
+ *   gt_anymal_post_physics_b : compute_observations (:302-313) + noise
+ *       (:481-482) + last_actions / last_dof_vel (:484-485).
+ * All tensors are the reference's (float32 AoS unless stated); all calls are
+ * stream ordered and return 0 on success (gt_last_error() otherwise).
+ */
+#ifndef GYMTASK_H
+#define GYMTASK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GT_ABI_VERSION 1
+#define GT_ANYMAL_NUM_TERMS 13  /* lin_vel_xy lin_vel_z ang_vel_z ang_vel_xy orient torques joint_acc
+                                   base_height air_time collision stumble action_rate hip */
+
+typedef struct gt_anymal_params {
+    int32_t num_envs, num_dofs, num_bodies, num_obs;
+    int32_t base_index;
+    int32_t num_feet, feet_idx[4];
+    int32_t num_knees, knee_idx[4];
+    int32_t hip_dofs[4];
+    int32_t allow_knee_contacts;
+    int64_t max_episode_length;
+    float dt;                        /* policy dt = decimation * sim dt */
+    /* reward scales already multiplied by dt (anymal_terrain.py:104-105) */
+    float s_termination, s_lin_vel_xy, s_lin_vel_z, s_ang_vel_z, s_ang_vel_xy, s_orient, s_torque,
+          s_joint_acc, s_base_height, s_air_time, s_collision, s_stumble, s_action_rate, s_hip;
+    float lin_vel_scale, ang_vel_scale, dof_pos_scale, dof_vel_scale, height_meas_scale;
+    float default_dof_pos[16];
+    float base_init_state[13];
+} gt_anymal_params;
+
+typedef struct gt_anymal_buffers {
+    float *root_states;          /* [N][13]                                   */
+    const float *contact_forces; /* [N*nb][3]                                 */
+    float *dof_state;            /* [N*nd][2]                                 */
+    const float *torques;        /* [N][nd]                                   */
+    const float *actions;        /* [N][nd]                                   */
+    float *last_actions;         /* [N][nd]                                   */
+    float *last_dof_vel;         /* [N][nd]                                   */
+    float *commands;             /* [N][4]                                    */
+    float *feet_air_time;        /* [N][4]                                    */
+    int64_t *progress_buf;       /* [N]                                       */
+    int64_t *randomize_buf;      /* [N]                                       */
+    uint8_t *reset_buf;          /* [N] bool                                  */
+    const void *timeout_buf;     /* [N] bool (timeout_is_int64 = 0) or int64  */
+    int32_t timeout_is_int64;    /* the first step sees VecTask's int64 zeros */
+    float *rew_buf;              /* [N]                                       */
+    float *episode_sums;         /* [13][N]                                   */
+    float *base_lin_vel;         /* [N][3]                                    */
+    float *base_ang_vel;         /* [N][3]                                    */
+    float *projected_gravity;    /* [N][3]                                    */
+    float *obs_buf;              /* [N][num_obs]                              */
+    const float *noise_scale;    /* [num_obs]                                 */
+} gt_anymal_buffers;
+
+int gt_abi_version(void);
+const char *gt_last_error(void);
+
+int gt_anymal_post_physics_a(const gt_anymal_params *p, const gt_anymal_buffers *b, void *stream);
+
+/* env_ids int32[k]; pos_offset/dof_vel [k][nd]; cmd_x/cmd_y/cmd_heading [k];
+ * episode_out[13] receives the per-term sums over env_ids (then zeroed in
+ * episode_sums); the caller divides by k * episodeLength_s. */
+int gt_anymal_reset(const gt_anymal_params *p, const gt_anymal_buffers *b, const int32_t *env_ids, int k,
+                    const float *pos_offset, const float *dof_vel, const float *cmd_x, const float *cmd_y,
+                    const float *cmd_heading, float *episode_out, void *stream);
+
+/* noise [N][num_obs] uniform(0,1) draws (torch.rand_like) or NULL when addNoise is false */
+int gt_anymal_post_physics_b(const gt_anymal_params *p, const gt_anymal_buffers *b, const float *noise,
+                             void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GYMTASK_H */

@@ -19,9 +19,11 @@ ARCH = os.environ.get("GS_OFFLOAD_ARCH", "gfx950")
 
 LIBS = {
     "libgymsim.so": ["gs_physics.hip", "gs_capi.hip"],
-    "libgymtask.so": ["gt_anymal.hip", "gt_capi.hip"],
+    "libgymtask.so": ["gt_anymal.hip"],
 }
-HEADERS = ["gs_internal.h", "gs_topologies.h", "gt_internal.h"]
+# the task kernels mirror torch's unfused elementwise arithmetic
+EXTRA_FLAGS = {"libgymtask.so": ["-ffp-contract=off"]}
+HEADERS = ["gs_internal.h", "gs_topologies.h"]
 
 
 def hipcc() -> str:
@@ -52,6 +54,7 @@ def build(force: bool = False, verbose: bool = True) -> None:
             continue
         cmd = [cc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-I", os.path.join(os.path.dirname(HERE), "include"), "-I", CSRC, "-o", out]
+        cmd += EXTRA_FLAGS.get(lib, [])
         cmd += [os.path.join(CSRC, s) for s in srcs]
         if verbose:
             print("[build]", " ".join(cmd), flush=True)

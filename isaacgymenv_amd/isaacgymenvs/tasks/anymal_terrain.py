@@ -322,33 +322,38 @@ class AnymalTerrain(VecTask):
                                  device=self.device).squeeze()
         env_ids_int32 = env_ids.to(dtype=torch.int32)
         if self._kernels is not None and not self.custom_origins:
+            # one kernel applies the draws; it also fills extras["episode"] (episode sums over env_ids)
             self._kernels.reset(env_ids_int32, positions_offset, velocities, cmd_x, cmd_y, cmd_h)
-        else:
-            self.dof_pos[env_ids] = self.default_dof_pos[env_ids] * positions_offset
-            self.dof_vel[env_ids] = velocities
-            self.root_states[env_ids] = self.base_init_state
-            if self.custom_origins:
-                self.root_states[env_ids, :3] += self.env_origins[env_ids]
-                self.root_states[env_ids, :2] += root_xy
-            self.commands[env_ids, 0] = cmd_x
-            self.commands[env_ids, 1] = cmd_y
-            self.commands[env_ids, 3] = cmd_h
-            self.commands[env_ids] *= (torch.norm(self.commands[env_ids, :2], dim=1) > 0.25).unsqueeze(1)
-            self.last_actions[env_ids] = 0.0
-            self.last_dof_vel[env_ids] = 0.0
-            self.feet_air_time[env_ids] = 0.0
-            self.progress_buf[env_ids] = 0
-            self.reset_buf[env_ids] = 1
-        self.gym.set_actor_root_state_tensor_indexed(self.sim, gymtorch.unwrap_tensor(self.root_states),
-                                                     gymtorch.unwrap_tensor(env_ids_int32), len(env_ids_int32))
-        self.gym.set_dof_state_tensor_indexed(self.sim, gymtorch.unwrap_tensor(self.dof_state),
-                                              gymtorch.unwrap_tensor(env_ids_int32), len(env_ids_int32))
+            self._set_reset_state(env_ids_int32)
+            return
+        self.dof_pos[env_ids] = self.default_dof_pos[env_ids] * positions_offset
+        self.dof_vel[env_ids] = velocities
+        self.root_states[env_ids] = self.base_init_state
+        if self.custom_origins:
+            self.root_states[env_ids, :3] += self.env_origins[env_ids]
+            self.root_states[env_ids, :2] += root_xy
+        self._set_reset_state(env_ids_int32)
+        self.commands[env_ids, 0] = cmd_x
+        self.commands[env_ids, 1] = cmd_y
+        self.commands[env_ids, 3] = cmd_h
+        self.commands[env_ids] *= (torch.norm(self.commands[env_ids, :2], dim=1) > 0.25).unsqueeze(1)
+        self.last_actions[env_ids] = 0.0
+        self.last_dof_vel[env_ids] = 0.0
+        self.feet_air_time[env_ids] = 0.0
+        self.progress_buf[env_ids] = 0
+        self.reset_buf[env_ids] = 1
         self.extras["episode"] = {}
         for key in self.episode_sums:
             self.extras["episode"]["rew_" + key] = torch.mean(self.episode_sums[key][env_ids]) / \
                 self.max_episode_length_s
             self.episode_sums[key][env_ids] = 0.0
         self.extras["episode"]["terrain_level"] = torch.mean(self.terrain_levels.float())
+
+    def _set_reset_state(self, env_ids_int32):
+        self.gym.set_actor_root_state_tensor_indexed(self.sim, gymtorch.unwrap_tensor(self.root_states),
+                                                     gymtorch.unwrap_tensor(env_ids_int32), len(env_ids_int32))
+        self.gym.set_dof_state_tensor_indexed(self.sim, gymtorch.unwrap_tensor(self.dof_state),
+                                              gymtorch.unwrap_tensor(env_ids_int32), len(env_ids_int32))
 
     def update_terrain_level(self, env_ids):
         if not self.init_done or not self.curriculum:
