@@ -88,6 +88,33 @@ def cpu_baseline(num_envs: int, seconds: float):
                       f"Python tail (8.9-12.5 ms/step at 4096 envs, SURVEY.md section 6) is not included"}
 
 
+def timed_region(step, steps: int, warmup: int, world: int, sync=lambda: None) -> float:
+    """W untimed steps, then exactly K timed steps bracketed by barrier + device sync on both
+    sides; returns the MAX over ranks of the elapsed wall time (seconds)."""
+    import torch
+    import torch.distributed as dist
+    for _ in range(warmup):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
 def main():
     args = parse()
     import torch
@@ -115,24 +142,7 @@ def main():
         actions = 2.0 * torch.rand((N, A), device=device, generator=gen) - 1.0
         env.step(actions)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed_region(step, args.steps, args.warmup, world, sync=torch.cuda.synchronize)
 
     # ---- roofline of the dominant kernel: HIP events on the launch stream around the fused physics launches
     stream = torch.cuda.current_stream(device)

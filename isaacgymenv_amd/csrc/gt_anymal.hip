@@ -30,12 +30,6 @@ __device__ __forceinline__ void quat_rotate_inverse(const float* q, const float*
   o[2] = (v[2] * s - (cz * w) * 2.0f) + (q[2] * d) * 2.0f;
 }
 
-// torch float remainder (floored): fmod then shift into the divisor's sign
-__device__ __forceinline__ float py_mod(float a, float b) {
-  float m = fmodf(a, b);
-  if (m != 0.0f && ((b < 0.0f) != (m < 0.0f))) m += b;
-  return m;
-}
 
 __device__ __forceinline__ float sq(float x) { return x * x; }
 __device__ __forceinline__ float norm3(const float* v) { return sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
@@ -69,7 +63,9 @@ __global__ void k_post_a(gt_anymal_params p, gt_anymal_buffers b) {
   const float fy = (0.0f + q[3] * ty) + (q[2] * tx - q[0] * tz);
   const float heading = atan2f(fy, fx);
   float* cmd = b.commands + (size_t)e * 4;
-  float ang = py_mod(cmd[3] - heading, kTwoPi);
+  // wrap_to_pi (anymal_terrain.py:684-687) is TorchScript: `%=` there is C fmod, not a floored
+  // remainder, so negative angles stay negative (pinned by tests/golden/anymal_terrain.npz)
+  float ang = fmodf(cmd[3] - heading, kTwoPi);
   ang = ang - kTwoPi * (ang > kPi ? 1.0f : 0.0f);
   const float c2 = fminf(fmaxf(0.5f * ang, -1.0f), 1.0f);
   cmd[2] = c2;

@@ -458,6 +458,9 @@ def quat_apply_yaw(quat, vec):
 
 
 def wrap_to_pi(angles):
-    angles %= 2 * np.pi
+    """anymal_terrain.py:684-687.  The reference function is TorchScript, where ``angles %= 2*pi``
+    lowers to C fmod (result has the sign of the dividend), so negative angles are left in
+    (-2pi, 0] and only angles > pi are shifted.  Reproduced as is (tests/test_golden_tasks.py)."""
+    angles = torch.fmod(angles, 2 * np.pi)
     angles -= 2 * np.pi * (angles > np.pi)
     return angles

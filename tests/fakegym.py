@@ -1,0 +1,137 @@
+"""FakeGym -- TEST INFRASTRUCTURE: a deterministic stand-in physics backend.
+
+Isaac Gym/PhysX is closed and absent, so the reference's
+task layer (everything above ``gym.simulate``) is exercised through this fake:
+asset/env/actor bookkeeping comes from our gymapi's pure-Python parts, and
+``simulate`` advances the state with a fixed, seeded rule that does NOT use the
+torch RNG (so the task layer's torch RNG stream is untouched).  The same fake
+drives (a) the reference's own Python in tests/golden/make_golden.py and (b) our
+task layer in tests/test_golden_*.py, so any difference in observations,
+rewards, resets, RNG call order or quirks shows up as a fixture mismatch.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from isaacgymenv_amd.isaacgym import gymapi as _g
+
+
+class FakeSim:
+    def __init__(self, params):
+        self.params = params
+        self.envs = []
+        self.asset = None
+        self.ground = None
+        self.t = 0
+
+
+class FakeGym(_g.Gym):
+    """Pure-python Gym whose simulate() is a seeded deterministic rule."""
+
+    def __init__(self, seed: int = 12345, dof_drift: float = 0.0):
+        self.seed = seed
+        self.dof_drift = dof_drift  # pushes joints out of range over time (exercises limit resets)
+
+    # ---- sim lifecycle
+    def create_sim(self, compute_device=0, graphics_device=-1, type=_g.SIM_PHYSX, params=None):
+        return FakeSim(params or _g.SimParams())
+
+    def add_ground(self, sim, params):
+        sim.ground = params
+
+    def prepare_sim(self, sim):
+        art = sim.asset.art
+        N, nd, nb = len(sim.envs), art.num_dofs, art.num_bodies
+        sim.N, sim.nd, sim.nb = N, nd, nb
+        f = torch.float32
+        root = torch.zeros(N, 13, dtype=f)
+        for i, e in enumerate(sim.envs):
+            a = e.actors[0]
+            root[i, 0:3] = torch.tensor(list(a.pose.p), dtype=f) + torch.tensor(e.origin, dtype=f)
+            root[i, 3:7] = torch.tensor(list(a.pose.r), dtype=f)
+        sim.root = root
+        sim.dof = torch.zeros(N * nd, 2, dtype=f)
+        sim.cf = torch.zeros(N * nb, 3, dtype=f)
+        sim.force = torch.zeros(N * nd, dtype=f)
+        sim.root_t = torch.zeros(N, 13, dtype=f)
+        sim.dof_t = torch.zeros(N * nd, 2, dtype=f)
+        sim.cf_t = torch.zeros(N * nb, 3, dtype=f)
+        names = art.body_names()
+        self.feet = [i for i, n in enumerate(names) if ("SHANK" in n or "foot" in n) and i > 0]
+        self.knees = [i for i, n in enumerate(names) if ("THIGH" in n or "thigh" in n) and i > 0]
+        return True
+
+    def simulate(self, sim):
+        sim.t += 1
+        rng = np.random.RandomState(self.seed + sim.t)
+        N, nd, nb = sim.N, sim.nd, sim.nb
+        t32 = lambda a: torch.from_numpy(np.asarray(a, dtype=np.float32))  # noqa: E731
+        q = sim.dof[:, 0].view(N, nd)
+        qd = sim.dof[:, 1].view(N, nd)
+        qd.mul_(0.9).add_(sim.force.view(N, nd) * 0.002).add_(t32(rng.normal(0, 0.05, (N, nd))))
+        if self.dof_drift:
+            qd.add_(self.dof_drift)
+        q.add_(qd * 0.005)
+        sim.root[:, 7:13].mul_(0.9).add_(t32(rng.normal(0, 0.1, (N, 6))))
+        sim.root[:, 0:3].add_(sim.root[:, 7:10] * 0.005)
+        quat = sim.root[:, 3:7] + t32(rng.normal(0, 0.01, (N, 4)))
+        sim.root[:, 3:7] = quat / quat.norm(dim=1, keepdim=True)
+        cf = np.zeros((N, nb, 3), dtype=np.float32)
+        cf[:, 0, 2] = np.where(rng.rand(N) < 0.01, 5.0, 0.0)
+        for k in self.knees:
+            cf[:, k, :] = np.where(rng.rand(N, 1) < 0.05, np.array([[2.0, 1.0, 3.0]]), 0.0)
+        for k in self.feet:
+            cf[:, k, 2] = np.where(rng.rand(N) < 0.6, 50.0, 0.0)
+            cf[:, k, :2] = rng.normal(0, 3.0, (N, 2))
+        sim.cf.copy_(torch.from_numpy(cf.reshape(N * nb, 3)))
+
+    def fetch_results(self, sim, wait=True):
+        return None
+
+    # ---- tensors
+    def acquire_actor_root_state_tensor(self, sim):
+        return _g.GymTensor(sim.root_t, "root")
+
+    def acquire_dof_state_tensor(self, sim):
+        return _g.GymTensor(sim.dof_t, "dof")
+
+    def acquire_net_contact_force_tensor(self, sim):
+        return _g.GymTensor(sim.cf_t, "contact")
+
+    def refresh_actor_root_state_tensor(self, sim):
+        sim.root_t.copy_(sim.root)
+
+    def refresh_dof_state_tensor(self, sim):
+        sim.dof_t.copy_(sim.dof)
+
+    def refresh_net_contact_force_tensor(self, sim):
+        sim.cf_t.copy_(sim.cf)
+
+    def set_dof_actuation_force_tensor(self, sim, t):
+        sim.force.copy_(t.tensor.reshape(-1))
+        return True
+
+    def set_actor_root_state_tensor(self, sim, t):
+        sim.root.copy_(t.tensor)
+        return True
+
+    def set_actor_root_state_tensor_indexed(self, sim, t, idx, n):
+        ids = idx.tensor[:n].long()
+        sim.root[ids] = t.tensor[ids]
+        return True
+
+    def set_dof_state_tensor_indexed(self, sim, t, idx, n):
+        ids = idx.tensor[:n].long()
+        nd = sim.nd
+        d = sim.dof.view(sim.N, nd, 2)
+        d[ids] = t.tensor.view(sim.N, nd, 2)[ids]
+        return True
+
+    def set_dof_state_tensor(self, sim, t):
+        sim.dof.copy_(t.tensor)
+        return True
+
+    # fused extension must not be used with the fake
+    def amd_pd_decimation_step(self, *a, **k):
+        raise AssertionError("the fused path needs the real simulator")

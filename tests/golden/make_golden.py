@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Generate golden fixtures from the REFERENCE's own task code (run in the dev container only).
+
+The reference (read-only at /root/reference) is imported with stub
+``isaacgym``/``gym`` modules and driven through tests/fakegym.FakeGym, the
+deterministic stand-in for the closed simulator.  Its
+outputs pin everything above ``gym.simulate``: observations, rewards, done
+masks, timeouts, episode extras, command resampling, feet air time, and the
+torch RNG call order (friction buckets, terrain levels, reset draws, push, obs
+noise).  Only the resulting arrays are committed (tests/golden/*.npz); the
+reference never travels to the GPU box.
+
+    python tests/golden/make_golden.py            # writes anymal_terrain.npz, cartpole.npz
+"""
+from __future__ import annotations
+
+import copy
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import yaml
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, ROOT)
+
+N_ANYMAL, STEPS_ANYMAL = 32, 30
+N_CARTPOLE, STEPS_CARTPOLE = 16, 40
+
+
+def anymal_cfg(num_envs: int) -> dict:
+    """AnymalTerrain.yaml (sim/env blocks resolved for the CPU pipeline) with a short episode and a
+    frequent push so a 30-step fixture covers pushes, terminations and timeouts."""
+    from isaacgymenv_amd.isaacgymenvs.config import compose
+    cfg = compose("config", ["task=AnymalTerrain", f"num_envs={num_envs}", "sim_device=cpu", "pipeline=cpu"])["task"]
+    cfg["env"]["learn"]["pushInterval_s"] = 0.1      # push every 5 env steps
+    cfg["env"]["learn"]["episodeLength_s"] = 0.4     # max_episode_length 20 -> timeouts inside the fixture
+    return cfg
+
+
+def cartpole_cfg(num_envs: int) -> dict:
+    from isaacgymenv_amd.isaacgymenvs.config import compose
+    return compose("config", ["task=Cartpole", f"num_envs={num_envs}", "sim_device=cpu", "pipeline=cpu"])["task"]
+
+
+def install_reference_stubs(fake):
+    """Make the reference importable here without Isaac Gym, gym, hydra or omegaconf."""
+    np.Inf = np.inf  # numpy 2 removed np.Inf; vec_task.py:107 uses it
+    from isaacgymenv_amd.isaacgym import gymapi as ours
+    from isaacgymenv_amd.isaacgym.gymapi import GymTensor
+    gymapi = types.ModuleType("isaacgym.gymapi")
+    gymapi.__dict__.update({k: v for k, v in ours.__dict__.items() if not k.startswith("__")})
+    gymapi.acquire_gym = lambda: fake
+    gymtorch = types.ModuleType("isaacgym.gymtorch")
+    gymtorch.wrap_tensor = lambda d: d.tensor
+    gymtorch.unwrap_tensor = lambda t: GymTensor(t)
+    gymutil = types.ModuleType("isaacgym.gymutil")
+    terrain_utils = types.ModuleType("isaacgym.terrain_utils")
+    terrain_utils.__all__ = []
+    pkg = types.ModuleType("isaacgym")
+    pkg.__path__ = []
+    pkg.gymapi, pkg.gymtorch, pkg.gymutil, pkg.terrain_utils = gymapi, gymtorch, gymutil, terrain_utils
+    for name, mod in (("isaacgym", pkg), ("isaacgym.gymapi", gymapi), ("isaacgym.gymtorch", gymtorch),
+                      ("isaacgym.gymutil", gymutil), ("isaacgym.terrain_utils", terrain_utils)):
+        sys.modules[name] = mod
+    gym = types.ModuleType("gym")
+    spaces = types.ModuleType("gym.spaces")
+
+    class Box:
+        def __init__(self, low, high, shape=None, dtype=np.float32):
+            self.low, self.high = np.asarray(low), np.asarray(high)
+            self.shape = self.low.shape
+
+    spaces.Box = Box
+    gym.spaces = spaces
+    gym.Space = object
+    sys.modules["gym"], sys.modules["gym.spaces"] = gym, spaces
+    # namespace packages so isaacgymenvs/__init__.py (hydra) is not executed
+    for name, sub in (("isaacgymenvs", ""), ("isaacgymenvs.tasks", "tasks"), ("isaacgymenvs.tasks.base", "tasks/base"),
+                      ("isaacgymenvs.utils", "utils")):
+        m = types.ModuleType(name)
+        m.__path__ = [os.path.join(REF, "isaacgymenvs", sub)]
+        sys.modules[name] = m
+
+
+def _np(t):
+    return t.detach().cpu().numpy().copy()
+
+
+def record_anymal(num_envs=N_ANYMAL, steps=STEPS_ANYMAL):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fakegym import FakeGym
+    fake = FakeGym()
+    install_reference_stubs(fake)
+    import importlib
+    ref = importlib.import_module("isaacgymenvs.tasks.anymal_terrain")
+    cfg = anymal_cfg(num_envs)
+    torch.manual_seed(42)
+    env = ref.AnymalTerrain(copy.deepcopy(cfg), "cpu", "cpu", -1, True, False, False)
+    out = {"init_commands": _np(env.commands), "init_dof_state": _np(env.dof_state),
+           "init_root_states": _np(env.root_states), "feet_indices": _np(env.feet_indices),
+           "knee_indices": _np(env.knee_indices), "noise_scale_vec": _np(env.noise_scale_vec)}
+    rng = np.random.RandomState(7)
+    actions = (2 * rng.rand(steps, num_envs, 12) - 1).astype(np.float32)
+    recs = {k: [] for k in ("obs", "rew", "reset", "time_outs", "commands", "feet_air_time", "progress",
+                            "episode_sums", "ep_extras", "ep_mask",
+                            # tail inputs (state at post_physics_step entry, after its refreshes)
+                            "in_root", "in_contact", "in_dof", "in_torques", "in_actions", "in_last_actions",
+                            "in_last_dof_vel", "in_commands", "in_feet_air_time", "in_progress", "in_episode_sums",
+                            "in_timeout", "in_timeout_is_long", "in_rng_state", "in_push",
+                            # tail outputs
+                            "out_root", "out_dof", "out_last_actions", "out_last_dof_vel", "out_base_lin_vel",
+                            "out_base_ang_vel", "out_projected_gravity", "out_obs_prenoise_free")}
+    terms = list(env.episode_sums.keys())
+    orig_post = env.post_physics_step
+
+    def traced_post():
+        g, sim = env.gym, env.sim
+        recs["in_root"].append(_np(sim.root))
+        recs["in_contact"].append(_np(sim.cf).reshape(num_envs, -1, 3))
+        recs["in_dof"].append(_np(env.dof_state))
+        recs["in_torques"].append(_np(env.torques))
+        recs["in_actions"].append(_np(env.actions))
+        recs["in_last_actions"].append(_np(env.last_actions))
+        recs["in_last_dof_vel"].append(_np(env.last_dof_vel))
+        recs["in_commands"].append(_np(env.commands))
+        recs["in_feet_air_time"].append(_np(env.feet_air_time))
+        recs["in_progress"].append(_np(env.progress_buf))
+        recs["in_episode_sums"].append(np.stack([_np(env.episode_sums[k]) for k in terms]))
+        recs["in_timeout"].append(_np(env.timeout_buf).astype(np.int64))
+        recs["in_timeout_is_long"].append(int(env.timeout_buf.dtype == torch.int64))
+        recs["in_rng_state"].append(torch.get_rng_state().numpy().copy())
+        recs["in_push"].append(int((env.common_step_counter + 1) % env.push_interval == 0))
+        env.extras.pop("episode", None)
+        orig_post()
+        recs["out_root"].append(_np(env.root_states))
+        recs["out_dof"].append(_np(env.dof_state))
+        recs["out_last_actions"].append(_np(env.last_actions))
+        recs["out_last_dof_vel"].append(_np(env.last_dof_vel))
+        recs["out_base_lin_vel"].append(_np(env.base_lin_vel))
+        recs["out_base_ang_vel"].append(_np(env.base_ang_vel))
+        recs["out_projected_gravity"].append(_np(env.projected_gravity))
+
+    env.post_physics_step = traced_post
+    for t in range(steps):
+        obs, rew, reset, extras = env.step(torch.from_numpy(actions[t]))
+        recs["obs"].append(_np(obs["obs"]))
+        recs["rew"].append(_np(rew))
+        recs["reset"].append(_np(reset).astype(np.int64))
+        recs["time_outs"].append(_np(extras["time_outs"]).astype(np.int64))
+        recs["commands"].append(_np(env.commands))
+        recs["feet_air_time"].append(_np(env.feet_air_time))
+        recs["progress"].append(_np(env.progress_buf))
+        recs["episode_sums"].append(np.stack([_np(env.episode_sums[k]) for k in terms]))
+        ep = extras.get("episode")
+        recs["ep_mask"].append(int(ep is not None))
+        recs["ep_extras"].append(np.array([float(ep["rew_" + k]) for k in terms] + [float(ep["terrain_level"])])
+                                 if ep is not None else np.zeros(len(terms) + 1))
+        assert reset.dtype == torch.bool, "AnymalTerrain reset_buf must be bool (anymal_terrain.py:295)"
+    recs.pop("out_obs_prenoise_free")
+    for k, v in recs.items():
+        out[k] = np.stack([np.asarray(x) for x in v])
+    out["actions"] = actions
+    out["terms"] = np.array(terms)
+    out["cfg_yaml"] = np.array(yaml.safe_dump(cfg))
+    return out
+
+
+def record_cartpole(num_envs=N_CARTPOLE, steps=STEPS_CARTPOLE):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fakegym import FakeGym
+    fake = FakeGym(seed=777, dof_drift=1.0)
+    install_reference_stubs(fake)
+    import importlib
+    ref = importlib.import_module("isaacgymenvs.tasks.cartpole")
+    cfg = cartpole_cfg(num_envs)
+    torch.manual_seed(42)
+    env = ref.Cartpole(copy.deepcopy(cfg), "cpu", "cpu", -1, True, False, False)
+    rng = np.random.RandomState(11)
+    actions = (2 * rng.rand(steps, num_envs, 1) - 1).astype(np.float32)
+    obs_l, rew_l, reset_l, to_l = [], [], [], []
+    for t in range(steps):
+        obs, rew, reset, extras = env.step(torch.from_numpy(actions[t]))
+        obs_l.append(_np(obs["obs"]))
+        rew_l.append(_np(rew))
+        reset_l.append(_np(reset))
+        to_l.append(_np(extras["time_outs"]).astype(np.int64))
+        assert reset.dtype == torch.int64
+    return {"actions": actions, "obs": np.stack(obs_l), "rew": np.stack(rew_l), "reset": np.stack(reset_l),
+            "time_outs": np.stack(to_l), "cfg_yaml": np.array(yaml.safe_dump(cfg))}
+
+
+def main():
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which in ("all", "anymal"):
+        d = record_anymal()
+        np.savez_compressed(os.path.join(HERE, "anymal_terrain.npz"), **d)
+        print("anymal_terrain.npz:", {k: v.shape for k, v in d.items() if hasattr(v, "shape")})
+    if which in ("all", "cartpole"):
+        # a fresh interpreter per task keeps the stubbed module graph simple
+        if which == "all":
+            import subprocess
+            subprocess.check_call([sys.executable, __file__, "cartpole"])
+        else:
+            d = record_cartpole()
+            np.savez_compressed(os.path.join(HERE, "cartpole.npz"), **d)
+            print("cartpole.npz:", {k: v.shape for k, v in d.items() if hasattr(v, "shape")})
+
+
+if __name__ == "__main__":
+    main()
