@@ -147,8 +147,8 @@ __device__ __forceinline__ void store_state(float* __restrict__ st, int N, int e
 // Z rows after the factorisation.
 template <class T>
 __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvState<T>& s,
-                                        const float* tau, const float* mu, float* lds, float (*cf)[3],
-                                        bool collect) {
+                                        const float* tau, const float* __restrict__ mu_g, int N, int e, float* lds,
+                                        float* __restrict__ cf_soa, bool collect) {
   constexpr int NB = T::NB, NV = T::NV, NB6 = T::NBASE, NC = T::NC;
   constexpr int MS = T::MAXDEP + 1;
   // Keep the model pointer opaque per substep: the constants are re-read with
@@ -268,7 +268,7 @@ __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const 
         const float dist = s.p[2] + x[2] - r;
         act[c] = P.has_ground && (dist < P.contact_offset);
         sep[c] = dist - P.rest_offset;
-        cmu[c] = 0.5f * (mu[T::cshape[c]] + P.ground_mu);
+        cmu[c] = 0.5f * (mu_g[T::cshape[c] * N + e] + P.ground_mu);
         if (act[c]) {
           const float xc[3] = {x[0], x[1], x[2] - r};
           const int SUP = T::csupp[c];
@@ -565,14 +565,21 @@ __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const 
     s.qd[j] = nun[NB6 + j];
   }
   if (collect) {
+    // net contact force per body of this (collecting) substep, SoA [3*nb][N]
 #pragma unroll
-    for (int b = 0; b < NB; ++b) cf[b][0] = cf[b][1] = cf[b][2] = 0.f;
+    for (int b = 0; b < NB; ++b) {
+      float f0 = 0.f, f1 = 0.f, f2 = 0.f;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int b = T::cbody[c];
-      cf[b][0] += lam[c][1] * inv_h;
-      cf[b][1] += lam[c][2] * inv_h;
-      cf[b][2] += lam[c][0] * inv_h;
+      for (int c = 0; c < NC; ++c) {
+        if (T::cbody[c] == b) {
+          f0 += lam[c][1] * inv_h;
+          f1 += lam[c][2] * inv_h;
+          f2 += lam[c][0] * inv_h;
+        }
+      }
+      cf_soa[(3 * b + 0) * N + e] = f0;
+      cf_soa[(3 * b + 1) * N + e] = f1;
+      cf_soa[(3 * b + 2) * N + e] = f2;
     }
   }
 }
@@ -596,23 +603,14 @@ __global__ __launch_bounds__(GS_WAVE, 1) void k_simulate(const DevModel* __restr
   const int N = B.N;
   EnvState<T> s;
   load_state<T>(B.state, N, e, s);
-  float tau[T::ND > 0 ? T::ND : 1], mu[T::NS > 0 ? T::NS : 1];
+  float tau[T::ND > 0 ? T::ND : 1];
 #pragma unroll
   for (int j = 0; j < T::ND; ++j) tau[j] = tau_aos ? tau_aos[(size_t)e * T::ND + j] : 0.f;
-#pragma unroll
-  for (int k = 0; k < T::NS; ++k) mu[k] = B.mu[k * N + e];
-  float cf[T::NB][3];
   for (int sstep = 0; sstep < P.substeps; ++sstep) {
     const bool last = (sstep == P.substeps - 1) && P.collect;
-    substep<T>(M, P, s, tau, mu, lds + threadIdx.x, cf, last);
+    substep<T>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last);
   }
   store_state<T>(B.state, N, e, s);
-  if (P.collect) {
-#pragma unroll
-    for (int b = 0; b < T::NB; ++b)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) B.cf[(3 * b + k) * N + e] = cf[b][k];
-  }
 }
 
 template <class T>
@@ -625,36 +623,26 @@ __global__ __launch_bounds__(GS_WAVE, 1) void k_pd_step(const DevModel* __restri
   constexpr int ND = T::ND;
   EnvState<T> s;
   load_state<T>(B.state, N, e, s);
-  float act[ND], mu[T::NS > 0 ? T::NS : 1], tau[ND];
-#pragma unroll
-  for (int j = 0; j < ND; ++j) act[j] = A.actions[(size_t)e * ND + j];
-#pragma unroll
-  for (int k = 0; k < T::NS; ++k) mu[k] = B.mu[k * N + e];
-  float cf[T::NB][3];
-  // the first PD evaluation reads the dof tensor the task holds (refreshed after the
-  // previous step's decimation loop or written by reset_idx): anymal_terrain.py:444
-  float q0[ND], qd0[ND];
-#pragma unroll
-  for (int j = 0; j < ND; ++j) {
-    q0[j] = A.dof_state_in[((size_t)e * ND + j) * 2 + 0];
-    qd0[j] = A.dof_state_in[((size_t)e * ND + j) * 2 + 1];
-  }
+  float tau[ND];
   // one call site for the substep so it is inlined once
   const int sub = P.substeps;
   const int n_pd = A.decimation * sub;
   const int total = (A.decimation + A.extra) * sub;
   for (int it = 0; it < total; ++it) {
     if (it < n_pd && (it % sub) == 0) {
+      // the first PD evaluation reads the dof tensor the task holds (refreshed after the previous
+      // step's decimation loop, or written by reset_idx): anymal_terrain.py:444
       const bool first = it == 0;
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
-        const float qj = first ? q0[j] : s.q[j];
-        const float qdj = first ? qd0[j] : s.qd[j];
-        tau[j] = clampf(A.kp * (A.scale * act[j] + A.default_pos[j] - qj) - A.kd * qdj, -A.tlim, A.tlim);
+        const float qj = first ? A.dof_state_in[((size_t)e * ND + j) * 2 + 0] : s.q[j];
+        const float qdj = first ? A.dof_state_in[((size_t)e * ND + j) * 2 + 1] : s.qd[j];
+        const float aj = A.actions[(size_t)e * ND + j];
+        tau[j] = clampf(A.kp * (A.scale * aj + A.default_pos[j] - qj) - A.kd * qdj, -A.tlim, A.tlim);
       }
     }
     const bool last = ((it % sub) == sub - 1) && P.collect;
-    substep<T>(M, P, s, tau, mu, lds + threadIdx.x, cf, last);
+    substep<T>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last);
     if (it == n_pd - 1 && A.dof_out) {
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
@@ -675,17 +663,11 @@ __global__ __launch_bounds__(GS_WAVE, 1) void k_pd_step(const DevModel* __restri
     o[7] = v[0]; o[8] = v[1]; o[9] = v[2];
     o[10] = s.w[0]; o[11] = s.w[1]; o[12] = s.w[2];
   }
-  if (P.collect) {
+  if (P.collect && A.cf_out) {
 #pragma unroll
     for (int b = 0; b < T::NB; ++b)
 #pragma unroll
-      for (int k = 0; k < 3; ++k) B.cf[(3 * b + k) * N + e] = cf[b][k];
-    if (A.cf_out) {
-#pragma unroll
-      for (int b = 0; b < T::NB; ++b)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) A.cf_out[((size_t)e * T::NB + b) * 3 + k] = cf[b][k];
-    }
+      for (int k = 0; k < 3; ++k) A.cf_out[((size_t)e * T::NB + b) * 3 + k] = B.cf[(3 * b + k) * N + e];
   }
 }
 
