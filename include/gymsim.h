@@ -70,6 +70,7 @@ typedef struct gs_sim_params {
     double bounce_threshold_velocity;   /* accepted, restitution is 0 in every in-scope task */
     double max_depenetration_velocity;
     int32_t contact_collection;         /* 0 never, 1 last substep (2 treated as 1)        */
+    int32_t kernel_variant;             /* 0 auto, 1 one env per lane, 2 lane team (4 lanes/env) */
 } gs_sim_params;
 
 /* Fused PD decimation step (AnymalTerrain.pre_physics_step + VecTask.step's
@@ -135,6 +136,9 @@ int gs_sim_set_dof(gs_sim *sim, const float *dof_state, const int32_t *idx, int 
 
 /* Fused decimation step, see gs_pd_args. */
 int gs_sim_pd_step(gs_sim *sim, const gs_pd_args *args, void *stream);
+
+/* Physics kernel selected by gs_sim_set_model: 1 one env per lane, 2 lane team; -1 on error. */
+int gs_sim_kernel_variant(gs_sim *sim);
 
 /* Kernel time of the last gs_sim_pd_step / gs_sim_simulate launch measured with
  * HIP events on `stream` (ms); -1 if not recorded.  Used by bench.py. */

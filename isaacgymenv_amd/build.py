@@ -18,12 +18,12 @@ LIBDIR = os.path.join(HERE, "_lib")
 ARCH = os.environ.get("GS_OFFLOAD_ARCH", "gfx950")
 
 LIBS = {
-    "libgymsim.so": ["gs_physics.hip", "gs_capi.hip"],
+    "libgymsim.so": ["gs_physics.hip", "gs_team.hip", "gs_capi.hip"],
     "libgymtask.so": ["gt_anymal.hip"],
 }
 # the task kernels mirror torch's unfused elementwise arithmetic
 EXTRA_FLAGS = {"libgymtask.so": ["-ffp-contract=off"]}
-HEADERS = ["gs_internal.h", "gs_topologies.h"]
+HEADERS = ["gs_internal.h", "gs_topologies.h", "gs_math.h"]
 
 
 def hipcc() -> str:

@@ -53,6 +53,9 @@ struct gs_sim {
   bool has_ground = false;
   float ground_mu = 1.f;
   const TopoEntry* topo = nullptr;
+  launch_sim_fn sim_fn = nullptr;
+  launch_pd_fn pd_fn = nullptr;
+  int variant = 0;  // kernel actually selected: 1 lane, 2 team
   DevModel* d_model = nullptr;
   int nb = 0, nd = 0, nc = 0, ns = 0;
   int N = 0;
@@ -154,6 +157,20 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   hipError_t e = hipMemcpy(s->d_model, &h, sizeof(DevModel), hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_fail(e, "gs_sim_set_model hipMemcpy");
   s->topo = t;
+  const TeamEntry* te = nullptr;
+  for (int i = 0; i < g_num_team_kernels; ++i)
+    if (std::strcmp(g_team_kernels[i].sig, t->sig) == 0 && g_team_kernels[i].sim) te = &g_team_kernels[i];
+  const int want = s->params.kernel_variant;
+  if (want == 2 && !te) return fail("gs_sim_set_model: no lane-team kernel for this topology");
+  if (te && want != 1) {
+    s->sim_fn = te->sim;
+    s->pd_fn = te->pd;
+    s->variant = 2;
+  } else {
+    s->sim_fn = t->sim;
+    s->pd_fn = t->pd;
+    s->variant = 1;
+  }
   s->nb = m->num_bodies;
   s->nd = m->num_dofs;
   s->nc = m->num_candidates;
@@ -193,7 +210,7 @@ int gs_sim_simulate(gs_sim* s, const float* dof_force, void* stream) {
   if (ready(s, "gs_sim_simulate")) return -1;
   hipStream_t st = (hipStream_t)stream;
   timing_begin(s, st);
-  hipError_t e = s->topo->sim(s->d_model, s->dp, buffers(s), dof_force, st);
+  hipError_t e = s->sim_fn(s->d_model, s->dp, buffers(s), dof_force, st);
   timing_end(s, st);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_simulate");
 }
@@ -215,7 +232,7 @@ int gs_sim_pd_step(gs_sim* s, const gs_pd_args* a, void* stream) {
   d.cf_out = a->contact_out;
   hipStream_t st = (hipStream_t)stream;
   timing_begin(s, st);
-  hipError_t e = s->topo->pd(s->d_model, s->dp, buffers(s), d, st);
+  hipError_t e = s->pd_fn(s->d_model, s->dp, buffers(s), d, st);
   timing_end(s, st);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_pd_step");
 }
@@ -246,6 +263,8 @@ int gs_sim_set_dof(gs_sim* s, const float* src, const int32_t* idx, int n_idx, v
   hipError_t e = launch_set_dof(s->state, s->N, s->nd, src, idx, n_idx, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_set_dof");
 }
+
+int gs_sim_kernel_variant(gs_sim* s) { return s ? s->variant : -1; }
 
 int gs_sim_enable_timing(gs_sim* s, int enable) {
   if (!s) return fail("gs_sim_enable_timing: null sim");

@@ -73,6 +73,15 @@ struct TopoEntry {
 extern TopoEntry g_topologies[];
 extern const int g_num_topologies;
 
+// lane-team kernels (gs_team.hip) for "uniform star" topologies; null when not applicable
+struct TeamEntry {
+  const char* sig;
+  launch_sim_fn sim;
+  launch_pd_fn pd;
+};
+extern TeamEntry g_team_kernels[];
+extern const int g_num_team_kernels;
+
 // generic (runtime-sized) tensor API kernels
 hipError_t launch_refresh_root(const float* state, int N, int nd, const float* com0, float* out, hipStream_t s);
 hipError_t launch_refresh_dof(const float* state, int N, int nd, float* out, hipStream_t s);

@@ -1,0 +1,873 @@
+// gs_team.hip -- lane-team form of the articulation + plane-contact substep (gfx950).
+//
+// Same solver specification as gs_physics.hip / oracle/physics_oracle.c,
+// mapped for MI355X occupancy: at 4096 envs the one-env-per-lane kernel has 64 waves for 256
+// CUs and spills (VGPR+AGPR+scratch).  Here an env is a TEAM of T::T_LANES consecutive lanes (a
+// DPP quad); lane c owns serial chain c of a "uniform star" articulation (ANYmal: 4 legs x 3
+// joints).  Chain kinematics, RNEA, composite inertias, the chain rows of the mass matrix, their
+// L^T D L elimination, the chain's contact rows and its joint state live in lane c; the 6
+// floating-base dofs are REPLICATED in every lane of the team (bit-identical: same inputs, same
+// instruction stream, commutative DPP reductions).  Cross-lane traffic is DPP quad_perm only:
+//   * sums of chain contributions to the base (composite inertia, RNEA force, Schur
+//     complement of the base block, back-substitution residuals);
+//   * per Gauss-Seidel row of chain c: broadcast of the row's impulse and activity from lane c,
+//     the row itself read from lane c's LDS column (16 teams read 16 addresses, 4-way broadcast).
+// Rows are processed in the oracle's global order (root candidates, then chain 0, 1, ...), so
+// the iterates are the same projected Gauss-Seidel sequence, only the rounding order of the base
+// sums differs.  4096 envs -> 256 waves; per-chain model constants are staged in LDS.
+#include "gs_internal.h"
+#include "gs_topologies.h"
+#include "gs_math.h"
+
+namespace {
+
+template <int CTRL>
+__device__ __forceinline__ float qperm(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int qperm_i(int x) {
+  return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, false);
+}
+// sum over the 4 lanes of the quad; every lane receives the same bits
+__device__ __forceinline__ float quad_sum(float x) {
+  x = x + qperm<0xB1>(x);  // quad_perm(1,0,3,2)
+  return x + qperm<0x4E>(x);  // quad_perm(2,3,0,1)
+}
+// broadcast lane L of the quad to all four lanes; L is a constant after unrolling, the switch folds
+__device__ __forceinline__ float bcast(float x, int L) {
+  switch (L) {
+    case 0: return qperm<0x00>(x);
+    case 1: return qperm<0x55>(x);
+    case 2: return qperm<0xAA>(x);
+    default: return qperm<0xFF>(x);
+  }
+}
+__device__ __forceinline__ int bcast_i(int x, int L) {
+  switch (L) {
+    case 0: return qperm_i<0x00>(x);
+    case 1: return qperm_i<0x55>(x);
+    case 2: return qperm_i<0xAA>(x);
+    default: return qperm_i<0xFF>(x);
+  }
+}
+
+// per-chain model constants in LDS, layout [param][lane]
+template <class T>
+struct CM {
+  static constexpr int CL = T::T_CL, CC = T::T_CC;
+  static constexpr int BODY = 25;  // jR 9 | jt 3 | axis 3 | mass 1 | com 3 | inertia 6
+  static constexpr int CAND = BODY * CL;  // point 3 | radius 1
+  static constexpr int DOF = CAND + 4 * CC;  // effort | vmax | armature
+  static constexpr int NP = DOF + 3 * CL;
+  static constexpr int LANES = T::T_LANES;
+};
+
+// LDS slots of the contact rows: chain candidate rows (owner column), then root candidate rows (own column)
+template <class T>
+struct RowSlots {
+  static constexpr int CL = T::T_CL;
+  static constexpr int PER_ROW = 6 + CL + 2;  // Zb 6 | Zc CL | c | 1/d
+  static constexpr int CHAIN = 3 * PER_ROW * T::T_CC;
+  static constexpr int ROOT_PER_ROW = 6 + 2;
+  static constexpr int ROOT = 3 * ROOT_PER_ROW * (T::T_RC > 0 ? T::T_RC : 1);
+  static constexpr int TOTAL = CHAIN + ROOT;
+  __device__ static constexpr int chain(int j, int rr) { return (j * 3 + rr) * PER_ROW; }
+  __device__ static constexpr int root(int j, int rr) { return CHAIN + (j * 3 + rr) * ROOT_PER_ROW; }
+};
+
+template <class T>
+struct TeamState {
+  float p[3], quat[4], vo[3], w[3];  // replicated root
+  float q[T::T_CL], qd[T::T_CL];     // this lane's chain
+};
+
+template <class T>
+__device__ __forceinline__ void stage_chain_model(const DevModel* __restrict__ M, float* mdl) {
+  using C = CM<T>;
+  for (int i = threadIdx.x; i < C::NP * T::T_NCH; i += blockDim.x) {
+    const int p = i / T::T_NCH, c = i - p * T::T_NCH;
+    float v;
+    if (p < C::CAND) {
+      const int k = p / C::BODY, f = p - k * C::BODY;
+      const int b = 1 + c * C::CL + k;
+      if (f < 9) v = M->jR[b][f];
+      else if (f < 12) v = M->jt[b][f - 9];
+      else if (f < 15) v = M->jaxis[b][f - 12];
+      else if (f < 16) v = M->mass[b];
+      else if (f < 19) v = M->com[b][f - 16];
+      else v = M->inertia[b][f - 19];
+    } else if (p < C::DOF) {
+      const int j = (p - C::CAND) / 4, f = (p - C::CAND) - 4 * j;
+      const int cand = T::T_RC + c * C::CC + j;
+      v = f < 3 ? M->cpoint[cand][f] : M->cradius[cand];
+    } else {
+      const int k = (p - C::DOF) / 3, f = (p - C::DOF) - 3 * k;
+      const int d = c * C::CL + k;
+      v = f == 0 ? M->effort[d] : (f == 1 ? M->vmax[d] : M->armature[d]);
+    }
+    mdl[p * C::LANES + c] = v;
+  }
+}
+
+template <class T>
+__device__ __forceinline__ void team_load(const float* __restrict__ st, int N, int e, int lc, TeamState<T>& s) {
+  constexpr int ND = T::ND, CL = T::T_CL;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s.p[k] = st[k * N + e];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) s.quat[k] = st[(3 + k) * N + e];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s.vo[k] = st[(7 + k) * N + e];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s.w[k] = st[(10 + k) * N + e];
+#pragma unroll
+  for (int k = 0; k < CL; ++k) {
+    s.q[k] = st[(13 + lc * CL + k) * N + e];
+    s.qd[k] = st[(13 + ND + lc * CL + k) * N + e];
+  }
+}
+template <class T>
+__device__ __forceinline__ void team_store(float* __restrict__ st, int N, int e, int lc, const TeamState<T>& s) {
+  constexpr int ND = T::ND, CL = T::T_CL;
+  if (lc == 0) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) st[k * N + e] = s.p[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st[(3 + k) * N + e] = s.quat[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) st[(7 + k) * N + e] = s.vo[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) st[(10 + k) * N + e] = s.w[k];
+  }
+#pragma unroll
+  for (int k = 0; k < CL; ++k) {
+    st[(13 + lc * CL + k) * N + e] = s.q[k];
+    st[(13 + ND + lc * CL + k) * N + e] = s.qd[k];
+  }
+}
+
+// spatial inertia of a body at O from its pose and local mass properties
+__device__ __forceinline__ void body_inertia(const float* R, const float* X, float m, const float* com,
+                                             const float* Il, SpI& I) {
+  float c[3];
+  mat3vec(R, com, c);
+  c[0] += X[0]; c[1] += X[1]; c[2] += X[2];
+  float Am[9];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    Am[3 * r + 0] = R[3 * r] * Il[0] + R[3 * r + 1] * Il[3] + R[3 * r + 2] * Il[4];
+    Am[3 * r + 1] = R[3 * r] * Il[3] + R[3 * r + 1] * Il[1] + R[3 * r + 2] * Il[5];
+    Am[3 * r + 2] = R[3 * r] * Il[4] + R[3 * r + 1] * Il[5] + R[3 * r + 2] * Il[2];
+  }
+  const float cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
+  I.m = m;
+  I.h[0] = m * c[0]; I.h[1] = m * c[1]; I.h[2] = m * c[2];
+  I.I[0] = Am[0] * R[0] + Am[1] * R[1] + Am[2] * R[2] + m * (cc - c[0] * c[0]);
+  I.I[1] = Am[3] * R[3] + Am[4] * R[4] + Am[5] * R[5] + m * (cc - c[1] * c[1]);
+  I.I[2] = Am[6] * R[6] + Am[7] * R[7] + Am[8] * R[8] + m * (cc - c[2] * c[2]);
+  I.I[3] = Am[0] * R[3] + Am[1] * R[4] + Am[2] * R[5] - m * c[0] * c[1];
+  I.I[4] = Am[0] * R[6] + Am[1] * R[7] + Am[2] * R[8] - m * c[0] * c[2];
+  I.I[5] = Am[3] * R[6] + Am[4] * R[7] + Am[5] * R[8] - m * c[1] * c[2];
+}
+
+// Jacobian rows of a contact point xc (relative to O) for the base dofs: row ax of [-[xc]x | I]
+__device__ __forceinline__ float base_jac(const float* xc, int ax, int k) {
+  if (k < 3) {
+    const float m3[3][3] = {{0.f, xc[2], -xc[1]}, {-xc[2], 0.f, xc[0]}, {xc[1], -xc[0], 0.f}};
+    return m3[ax][k];
+  }
+  return (ax == k - 3) ? 1.f : 0.f;
+}
+
+template <class T>
+__device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, const float* __restrict__ mdl,
+                                             const DevParams& P, TeamState<T>& s, const float* tau,
+                                             const float* __restrict__ mu_g, int N, int e, int lc,
+                                             float* __restrict__ rows_own, const float* __restrict__ rows_team,
+                                             float* __restrict__ cf_soa, bool collect) {
+  constexpr int CL = T::T_CL, CC = T::T_CC, RC = T::T_RC, NCH = T::T_NCH, LN = T::T_LANES;
+  static_assert(NCH == LN && LN == 4, "lane teams are DPP quads with one chain per lane");
+  using C = CM<T>;
+  using RS = RowSlots<T>;
+  uintptr_t mp = reinterpret_cast<uintptr_t>(Min);
+  asm volatile("" : "+s"(mp));
+  const DevModel* __restrict__ M = reinterpret_cast<const DevModel*>(mp);
+  const float* cm = mdl + lc;  // this lane's chain constants: cm[p * LN]
+  const float h = P.h;
+
+  // ================= root (replicated)
+  float R0[9];
+  {
+    const float inv = rsqrtf(s.quat[0] * s.quat[0] + s.quat[1] * s.quat[1] + s.quat[2] * s.quat[2] +
+                             s.quat[3] * s.quat[3]);
+    const float qn[4] = {s.quat[0] * inv, s.quat[1] * inv, s.quat[2] * inv, s.quat[3] * inv};
+    quat_to_mat(qn, R0);
+  }
+  const float X0[3] = {0.f, 0.f, 0.f};
+  float nub[6] = {s.w[0], s.w[1], s.w[2], s.vo[0], s.vo[1], s.vo[2]};
+  const float A0[6] = {0.f, 0.f, 0.f, -P.g[0], -P.g[1], -P.g[2]};
+  SpI I0;
+  body_inertia(R0, X0, M->mass[0], M->com[0], M->inertia[0], I0);
+  float F0[6];
+  {
+    float ia[6], iv[6], x6[6];
+    spi_mul(I0, A0, ia);
+    spi_mul(I0, nub, iv);
+    crf(nub, iv, x6);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) F0[k] = ia[k] + x6[k];
+  }
+
+  // ================= chain forward pass (lane-local)
+  float R[CL][9], X[CL][3], S[CL][6], V[CL][6], A[CL][6], Fc[CL][6];
+  SpI Ic[CL];
+  bool act[CC];
+  float sep[CC], cmu[CC];
+#pragma unroll
+  for (int k = 0; k < CL; ++k) {
+    const float* Rp = k == 0 ? R0 : R[k - 1];
+    const float* Xp = k == 0 ? X0 : X[k - 1];
+    const float* Vp = k == 0 ? nub : V[k - 1];
+    const float* Ap = k == 0 ? A0 : A[k - 1];
+    const float* bp = cm + (k * C::BODY) * LN;
+    float jR[9], jt[3], ax[3];
+#pragma unroll
+    for (int f = 0; f < 9; ++f) jR[f] = bp[f * LN];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) { jt[f] = bp[(9 + f) * LN]; ax[f] = bp[(12 + f) * LN]; }
+    float RJ[9], t[3], aw[3];
+    mat3mul(Rp, jR, RJ);
+    mat3vec(Rp, jt, t);
+    X[k][0] = Xp[0] + t[0]; X[k][1] = Xp[1] + t[1]; X[k][2] = Xp[2] + t[2];
+    mat3vec(RJ, ax, aw);
+    const float qj = s.q[k];
+    if (T::jkind[1 + k] == 1) {
+      float sn, cs;
+      sincosf(qj, &sn, &cs);
+      const float Cc = 1.f - cs;
+      float Rq[9];
+      Rq[0] = cs + ax[0] * ax[0] * Cc;         Rq[1] = ax[0] * ax[1] * Cc - ax[2] * sn; Rq[2] = ax[0] * ax[2] * Cc + ax[1] * sn;
+      Rq[3] = ax[1] * ax[0] * Cc + ax[2] * sn; Rq[4] = cs + ax[1] * ax[1] * Cc;         Rq[5] = ax[1] * ax[2] * Cc - ax[0] * sn;
+      Rq[6] = ax[2] * ax[0] * Cc - ax[1] * sn; Rq[7] = ax[2] * ax[1] * Cc + ax[0] * sn; Rq[8] = cs + ax[2] * ax[2] * Cc;
+      mat3mul(RJ, Rq, R[k]);
+      S[k][0] = aw[0]; S[k][1] = aw[1]; S[k][2] = aw[2];
+      cross3(X[k], aw, &S[k][3]);
+    } else {
+#pragma unroll
+      for (int f = 0; f < 9; ++f) R[k][f] = RJ[f];
+      X[k][0] += aw[0] * qj; X[k][1] += aw[1] * qj; X[k][2] += aw[2] * qj;
+      S[k][0] = S[k][1] = S[k][2] = 0.f;
+      S[k][3] = aw[0]; S[k][4] = aw[1]; S[k][5] = aw[2];
+    }
+    const float qd = s.qd[k];
+    float c6[6];
+#pragma unroll
+    for (int f = 0; f < 6; ++f) V[k][f] = Vp[f] + S[k][f] * qd;
+    crm(V[k], S[k], c6);
+#pragma unroll
+    for (int f = 0; f < 6; ++f) A[k][f] = Ap[f] + c6[f] * qd;
+    float com[3], Il[6];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) com[f] = bp[(16 + f) * LN];
+#pragma unroll
+    for (int f = 0; f < 6; ++f) Il[f] = bp[(19 + f) * LN];
+    body_inertia(R[k], X[k], bp[15 * LN], com, Il, Ic[k]);
+    {
+      float ia[6], iv[6], x6[6];
+      spi_mul(Ic[k], A[k], ia);
+      spi_mul(Ic[k], V[k], iv);
+      crf(V[k], iv, x6);
+#pragma unroll
+      for (int f = 0; f < 6; ++f) Fc[k][f] = ia[f] + x6[f];
+    }
+    // ---- chain contact candidates on body k: activity + Jacobian rows into this lane's LDS column
+#pragma unroll
+    for (int j = 0; j < CC; ++j) {
+      if (T::T_ccb[j] == k) {
+        const float* cp = cm + (C::CAND + 4 * j) * LN;
+        const float pl[3] = {cp[0], cp[LN], cp[2 * LN]};
+        const float r = cp[3 * LN];
+        float x[3];
+        mat3vec(R[k], pl, x);
+        x[0] += X[k][0]; x[1] += X[k][1]; x[2] += X[k][2];
+        const float dist = s.p[2] + x[2] - r;
+        act[j] = P.has_ground && (dist < P.contact_offset);
+        sep[j] = dist - P.rest_offset;
+        const int shape = T::T_RS + lc * T::T_SPC + T::T_ccs[j];
+        cmu[j] = 0.5f * (mu_g[shape * N + e] + P.ground_mu);
+        if (act[j]) {
+          const float xc[3] = {x[0], x[1], x[2] - r};
+#pragma unroll
+          for (int rr = 0; rr < 3; ++rr) {
+            const int ax3 = (rr == 0) ? 2 : (rr == 1 ? 0 : 1);
+            float* row = rows_own + RS::chain(j, rr) * GS_WAVE;
+#pragma unroll
+            for (int b = 0; b < 6; ++b) row[b * GS_WAVE] = base_jac(xc, ax3, b);
+#pragma unroll
+            for (int kk = 0; kk < CL; ++kk) {
+              float v = 0.f;
+              if (kk <= k) {
+                float tt[3];
+                cross3(S[kk], xc, tt);
+                v = S[kk][3 + ax3] + tt[ax3];
+              }
+              row[(6 + kk) * GS_WAVE] = v;
+            }
+          }
+        }
+      }
+    }
+  }
+
+  // ================= chain backward pass: composite inertia / force, bias, chain rows of M
+  float Mcc[CL][CL], Mcb[CL][6], biasc[CL];
+#pragma unroll
+  for (int kk = 0; kk < CL; ++kk) {
+    const int k = CL - 1 - kk;
+    if (k < CL - 1) {
+      Ic[k].m += Ic[k + 1].m;
+#pragma unroll
+      for (int f = 0; f < 3; ++f) Ic[k].h[f] += Ic[k + 1].h[f];
+#pragma unroll
+      for (int f = 0; f < 6; ++f) Ic[k].I[f] += Ic[k + 1].I[f];
+#pragma unroll
+      for (int f = 0; f < 6; ++f) Fc[k][f] += Fc[k + 1][f];
+    }
+    biasc[k] = dot6(S[k], Fc[k]);
+    float Fk[6];
+    spi_mul(Ic[k], S[k], Fk);
+    Mcc[k][k] = dot6(S[k], Fk) + cm[(C::DOF + 3 * k + 2) * LN];
+#pragma unroll
+    for (int j = 0; j < k; ++j) Mcc[k][j] = dot6(S[j], Fk);
+#pragma unroll
+    for (int b = 0; b < 6; ++b) Mcb[k][b] = Fk[b];
+  }
+  // ================= root sums over the team
+  float Fb[6], Mbb[6][6];
+  SpI Ir;
+  {
+#pragma unroll
+    for (int f = 0; f < 6; ++f) Fb[f] = F0[f] + quad_sum(Fc[0][f]);
+    Ir.m = I0.m + quad_sum(Ic[0].m);
+#pragma unroll
+    for (int f = 0; f < 3; ++f) Ir.h[f] = I0.h[f] + quad_sum(Ic[0].h[f]);
+#pragma unroll
+    for (int f = 0; f < 6; ++f) Ir.I[f] = I0.I[f] + quad_sum(Ic[0].I[f]);
+    Mbb[0][0] = Ir.I[0]; Mbb[1][1] = Ir.I[1]; Mbb[2][2] = Ir.I[2];
+    Mbb[1][0] = Ir.I[3]; Mbb[2][0] = Ir.I[4]; Mbb[2][1] = Ir.I[5];
+    Mbb[3][0] = 0.f;       Mbb[3][1] = Ir.h[2];  Mbb[3][2] = -Ir.h[1];
+    Mbb[4][0] = -Ir.h[2];  Mbb[4][1] = 0.f;      Mbb[4][2] = Ir.h[0];
+    Mbb[5][0] = Ir.h[1];   Mbb[5][1] = -Ir.h[0]; Mbb[5][2] = 0.f;
+    Mbb[3][3] = Ir.m; Mbb[4][4] = Ir.m; Mbb[5][5] = Ir.m;
+    Mbb[4][3] = 0.f; Mbb[5][3] = 0.f; Mbb[5][4] = 0.f;
+  }
+
+  // ================= L^T D L: chain dofs (lane-local) with the base Schur complement summed over the team
+  {
+    float corr[6][6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int b = 0; b <= a; ++b) corr[a][b] = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < CL; ++kk) {
+      const int k = CL - 1 - kk;
+      const float dinv = 1.f / Mcc[k][k];
+#pragma unroll
+      for (int jj = 0; jj < CL; ++jj) {
+        const int j = k - 1 - jj;
+        if (j >= 0) {
+          const float a = Mcc[k][j] * dinv;
+#pragma unroll
+          for (int i = 0; i <= j; ++i) Mcc[j][i] -= a * Mcc[k][i];
+#pragma unroll
+          for (int b = 0; b < 6; ++b) Mcb[j][b] -= a * Mcb[k][b];
+          Mcc[k][j] = a;
+        }
+      }
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) {
+        const int b = 5 - bb;
+        const float a = Mcb[k][b] * dinv;
+#pragma unroll
+        for (int i = 0; i <= b; ++i) corr[b][i] -= a * Mcb[k][i];
+        Mcb[k][b] = a;
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int b = 0; b <= a; ++b) Mbb[a][b] += quad_sum(corr[a][b]);
+  }
+#pragma unroll
+  for (int kk = 0; kk < 6; ++kk) {
+    const int k = 5 - kk;
+    const float dinv = 1.f / Mbb[k][k];
+#pragma unroll
+    for (int ii = 0; ii < 6; ++ii) {
+      const int i = k - 1 - ii;
+      if (i >= 0) {
+        const float a = Mbb[k][i] * dinv;
+#pragma unroll
+        for (int j = 0; j <= i; ++j) Mbb[i][j] -= a * Mbb[k][j];
+        Mbb[k][i] = a;
+      }
+    }
+  }
+  float sDc[CL], sDb[6];
+#pragma unroll
+  for (int k = 0; k < CL; ++k) sDc[k] = rsqrtf(Mcc[k][k]);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) sDb[k] = rsqrtf(Mbb[k][k]);
+
+  // ================= free velocity
+  float nufc[CL], nufb[6];
+  {
+    float rc[CL], rb[6], rcorr[6];
+#pragma unroll
+    for (int k = 0; k < CL; ++k) {
+      float t = tau[k];
+      const float ef = cm[(C::DOF + 3 * k + 0) * LN];
+      if (ef > 0.f) t = clampf(t, -ef, ef);
+      rc[k] = t - biasc[k];
+    }
+#pragma unroll
+    for (int b = 0; b < 6; ++b) { rb[b] = -Fb[b]; rcorr[b] = 0.f; }
+#pragma unroll
+    for (int kk = 0; kk < CL; ++kk) {
+      const int k = CL - 1 - kk;
+#pragma unroll
+      for (int j = 0; j < k; ++j) rc[j] -= Mcc[k][j] * rc[k];
+#pragma unroll
+      for (int b = 0; b < 6; ++b) rcorr[b] -= Mcb[k][b] * rc[k];
+    }
+#pragma unroll
+    for (int b = 0; b < 6; ++b) rb[b] += quad_sum(rcorr[b]);
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) {
+      const int k = 5 - kk;
+#pragma unroll
+      for (int b = 0; b < k; ++b) rb[b] -= Mbb[k][b] * rb[k];
+    }
+#pragma unroll
+    for (int b = 0; b < 6; ++b) rb[b] *= sDb[b] * sDb[b];
+#pragma unroll
+    for (int k = 0; k < CL; ++k) rc[k] *= sDc[k] * sDc[k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+#pragma unroll
+      for (int b = 0; b < k; ++b) rb[k] -= Mbb[k][b] * rb[b];
+#pragma unroll
+    for (int k = 0; k < CL; ++k) {
+#pragma unroll
+      for (int b = 0; b < 6; ++b) rc[k] -= Mcb[k][b] * rb[b];
+#pragma unroll
+      for (int j = 0; j < k; ++j) rc[k] -= Mcc[k][j] * rc[j];
+    }
+#pragma unroll
+    for (int b = 0; b < 6; ++b) nufb[b] = nub[b] + h * rb[b];
+#pragma unroll
+    for (int k = 0; k < CL; ++k) nufc[k] = s.qd[k] + h * rc[k];
+    float wxp[3];
+    cross3(&nub[0], &nub[3], wxp);
+    nufb[3] += h * wxp[0]; nufb[4] += h * wxp[1]; nufb[5] += h * wxp[2];
+  }
+
+  // ================= contact rows: scaled Z = (L^-T J^T) D^-1/2, c = J nu_f, 1/diag
+  // chain candidates (owner lane)
+#pragma unroll
+  for (int j = 0; j < CC; ++j) {
+    if (act[j]) {
+      const int kb = T::T_ccb[j];
+#pragma unroll
+      for (int rr = 0; rr < 3; ++rr) {
+        float* row = rows_own + RS::chain(j, rr) * GS_WAVE;
+        float zb[6], zc[CL];
+        float cj = 0.f;
+#pragma unroll
+        for (int b = 0; b < 6; ++b) { zb[b] = row[b * GS_WAVE]; cj += zb[b] * nufb[b]; }
+#pragma unroll
+        for (int k = 0; k < CL; ++k) { zc[k] = row[(6 + k) * GS_WAVE]; if (k <= kb) cj += zc[k] * nufc[k]; }
+        // leaf -> root: chain nodes kb..0 then base 5..0
+#pragma unroll
+        for (int kk = 0; kk < CL; ++kk) {
+          const int k = kb - kk;
+          if (k >= 0) {
+#pragma unroll
+            for (int i = 0; i < k; ++i) zc[i] -= Mcc[k][i] * zc[k];
+#pragma unroll
+            for (int b = 0; b < 6; ++b) zb[b] -= Mcb[k][b] * zc[k];
+          }
+        }
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) {
+          const int k = 5 - kk;
+#pragma unroll
+          for (int b = 0; b < k; ++b) zb[b] -= Mbb[k][b] * zb[k];
+        }
+        float d = 0.f;
+#pragma unroll
+        for (int b = 0; b < 6; ++b) { zb[b] *= sDb[b]; d += zb[b] * zb[b]; row[b * GS_WAVE] = zb[b]; }
+#pragma unroll
+        for (int k = 0; k < CL; ++k) {
+          const float z = k <= kb ? zc[k] * sDc[k] : 0.f;
+          d += z * z;
+          row[(6 + k) * GS_WAVE] = z;
+        }
+        row[(6 + CL) * GS_WAVE] = cj;
+        row[(7 + CL) * GS_WAVE] = 1.f / d;
+      }
+    }
+  }
+  // root candidates (replicated in every lane, own column)
+  bool ract[RC > 0 ? RC : 1];
+  float rsep[RC > 0 ? RC : 1], rmu[RC > 0 ? RC : 1];
+#pragma unroll
+  for (int j = 0; j < RC; ++j) {
+    float x[3];
+    mat3vec(R0, M->cpoint[j], x);
+    const float r = M->cradius[j];
+    const float dist = s.p[2] + x[2] - r;
+    ract[j] = P.has_ground && (dist < P.contact_offset);
+    rsep[j] = dist - P.rest_offset;
+    rmu[j] = 0.5f * (mu_g[T::T_rcs[j] * N + e] + P.ground_mu);
+    if (ract[j]) {
+      const float xc[3] = {x[0], x[1], x[2] - r};
+#pragma unroll
+      for (int rr = 0; rr < 3; ++rr) {
+        const int ax3 = (rr == 0) ? 2 : (rr == 1 ? 0 : 1);
+        float* row = rows_own + RS::root(j, rr) * GS_WAVE;
+        float zb[6], cj = 0.f;
+#pragma unroll
+        for (int b = 0; b < 6; ++b) { zb[b] = base_jac(xc, ax3, b); cj += zb[b] * nufb[b]; }
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) {
+          const int k = 5 - kk;
+#pragma unroll
+          for (int b = 0; b < k; ++b) zb[b] -= Mbb[k][b] * zb[k];
+        }
+        float d = 0.f;
+#pragma unroll
+        for (int b = 0; b < 6; ++b) { zb[b] *= sDb[b]; d += zb[b] * zb[b]; row[b * GS_WAVE] = zb[b]; }
+        row[6 * GS_WAVE] = cj;
+        row[7 * GS_WAVE] = 1.f / d;
+      }
+    }
+  }
+
+  // ================= projected Gauss-Seidel, global row order: root candidates, chain 0, 1, ...
+  float wb[6], wc[CL], wbp[6], wcp[CL];
+  float lamc[CC][3], lamr[RC > 0 ? RC : 1][3];
+#pragma unroll
+  for (int b = 0; b < 6; ++b) wb[b] = 0.f;
+#pragma unroll
+  for (int k = 0; k < CL; ++k) wc[k] = 0.f;
+#pragma unroll
+  for (int j = 0; j < CC; ++j) lamc[j][0] = lamc[j][1] = lamc[j][2] = 0.f;
+#pragma unroll
+  for (int j = 0; j < RC; ++j) lamr[j][0] = lamr[j][1] = lamr[j][2] = 0.f;
+  const float inv_h = 1.f / h;
+  const int iters = P.pos_iters + P.vel_iters;
+  for (int it = 0; it < iters; ++it) {
+    const bool pos_phase = it < P.pos_iters;
+    // root candidates: every lane runs the identical update
+#pragma unroll
+    for (int j = 0; j < RC; ++j) {
+      if (ract[j]) {
+        float target = -rsep[j] * inv_h;
+        if (rsep[j] < 0.f) target = pos_phase ? fminf(target, P.max_depen_vel) : 0.f;
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) {
+          const float* row = rows_own + RS::root(j, rr) * GS_WAVE;
+          float z[6], u = row[6 * GS_WAVE];
+#pragma unroll
+          for (int b = 0; b < 6; ++b) { z[b] = row[b * GS_WAVE]; u += z[b] * wb[b]; }
+          const float dinv = row[7 * GS_WAVE];
+          float nl;
+          if (rr == 0) {
+            nl = fmaxf(lamr[j][0] + (target - u) * dinv, 0.f);
+          } else {
+            const float lim = rmu[j] * lamr[j][0];
+            nl = clampf(lamr[j][rr] - u * dinv, -lim, lim);
+          }
+          const float dl = nl - lamr[j][rr];
+          lamr[j][rr] = nl;
+#pragma unroll
+          for (int b = 0; b < 6; ++b) wb[b] += z[b] * dl;
+        }
+      }
+    }
+    // chain candidates: owner lane cc computes the impulse, the team applies it to the shared base
+#pragma unroll
+    for (int cc = 0; cc < NCH; ++cc) {
+      const bool owner = lc == cc;
+      const float* col = rows_team + cc;
+#pragma unroll
+      for (int j = 0; j < CC; ++j) {
+        const int a_o = bcast_i(act[j] ? 1 : 0, cc);
+        if (a_o) {
+          const float sc = sep[j];
+          float target = -sc * inv_h;
+          if (sc < 0.f) target = pos_phase ? fminf(target, P.max_depen_vel) : 0.f;
+#pragma unroll
+          for (int rr = 0; rr < 3; ++rr) {
+            const float* row = col + RS::chain(j, rr) * GS_WAVE;
+            float zb[6], zc[CL], u = row[(6 + CL) * GS_WAVE];
+#pragma unroll
+            for (int b = 0; b < 6; ++b) { zb[b] = row[b * GS_WAVE]; u += zb[b] * wb[b]; }
+#pragma unroll
+            for (int k = 0; k < CL; ++k) { zc[k] = row[(6 + k) * GS_WAVE]; u += zc[k] * wc[k]; }
+            const float dinv = row[(7 + CL) * GS_WAVE];
+            float nl;
+            if (rr == 0) {
+              nl = fmaxf(lamc[j][0] + (target - u) * dinv, 0.f);
+            } else {
+              const float lim = cmu[j] * lamc[j][0];
+              nl = clampf(lamc[j][rr] - u * dinv, -lim, lim);
+            }
+            const float dl_own = nl - lamc[j][rr];
+            if (owner) lamc[j][rr] = nl;
+            const float dl = bcast(dl_own, cc);
+#pragma unroll
+            for (int b = 0; b < 6; ++b) wb[b] += zb[b] * dl;
+            if (owner) {
+#pragma unroll
+              for (int k = 0; k < CL; ++k) wc[k] += zc[k] * dl;
+            }
+          }
+        }
+      }
+    }
+    if (it == P.pos_iters - 1) {
+#pragma unroll
+      for (int b = 0; b < 6; ++b) wbp[b] = wb[b];
+#pragma unroll
+      for (int k = 0; k < CL; ++k) wcp[k] = wc[k];
+    }
+  }
+  if (P.pos_iters <= 0) {
+#pragma unroll
+    for (int b = 0; b < 6; ++b) wbp[b] = wb[b];
+#pragma unroll
+    for (int k = 0; k < CL; ++k) wcp[k] = wc[k];
+  }
+
+  // ================= dnu = L^-1 D^-1/2 w (base first, then the chain)
+  float nunb[6], nupb[6], nunc[CL], nupc[CL];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    float v = wb[k] * sDb[k], vp = wbp[k] * sDb[k];
+#pragma unroll
+    for (int b = 0; b < k; ++b) { v -= Mbb[k][b] * nunb[b]; vp -= Mbb[k][b] * nupb[b]; }
+    nunb[k] = v;
+    nupb[k] = vp;
+  }
+#pragma unroll
+  for (int k = 0; k < CL; ++k) {
+    float v = wc[k] * sDc[k], vp = wcp[k] * sDc[k];
+#pragma unroll
+    for (int b = 0; b < 6; ++b) { v -= Mcb[k][b] * nunb[b]; vp -= Mcb[k][b] * nupb[b]; }
+#pragma unroll
+    for (int j = 0; j < k; ++j) { v -= Mcc[k][j] * nunc[j]; vp -= Mcc[k][j] * nupc[j]; }
+    nunc[k] = v;
+    nupc[k] = vp;
+  }
+#pragma unroll
+  for (int b = 0; b < 6; ++b) { nunb[b] += nufb[b]; nupb[b] += nufb[b]; }
+#pragma unroll
+  for (int k = 0; k < CL; ++k) {
+    float vn = nunc[k] + nufc[k], vp = nupc[k] + nufc[k];
+    const float vm = cm[(C::DOF + 3 * k + 1) * LN];
+    if (vm > 0.f) { vn = clampf(vn, -vm, vm); vp = clampf(vp, -vm, vm); }
+    nunc[k] = vn;
+    nupc[k] = vp;
+  }
+
+  // ================= integrate
+  s.p[0] += h * nupb[3]; s.p[1] += h * nupb[4]; s.p[2] += h * nupb[5];
+  {
+    const float wx = nupb[0], wy = nupb[1], wz = nupb[2];
+    float x = s.quat[0], y = s.quat[1], z = s.quat[2], w = s.quat[3];
+    const float hh = 0.5f * h;
+    const float dx = hh * (w * wx + wy * z - wz * y);
+    const float dy = hh * (w * wy + wz * x - wx * z);
+    const float dz = hh * (w * wz + wx * y - wy * x);
+    const float dw = -hh * (wx * x + wy * y + wz * z);
+    x += dx; y += dy; z += dz; w += dw;
+    const float n = rsqrtf(x * x + y * y + z * z + w * w);
+    s.quat[0] = x * n; s.quat[1] = y * n; s.quat[2] = z * n; s.quat[3] = w * n;
+  }
+  s.w[0] = nunb[0]; s.w[1] = nunb[1]; s.w[2] = nunb[2];
+  s.vo[0] = nunb[3]; s.vo[1] = nunb[4]; s.vo[2] = nunb[5];
+#pragma unroll
+  for (int k = 0; k < CL; ++k) {
+    s.q[k] += h * nupc[k];
+    s.qd[k] = nunc[k];
+  }
+  if (collect) {
+#pragma unroll
+    for (int k = 0; k < CL; ++k) {
+      float f0 = 0.f, f1 = 0.f, f2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < CC; ++j) {
+        if (T::T_ccb[j] == k) {
+          f0 += lamc[j][1] * inv_h;
+          f1 += lamc[j][2] * inv_h;
+          f2 += lamc[j][0] * inv_h;
+        }
+      }
+      const int b = 1 + lc * CL + k;
+      cf_soa[(3 * b + 0) * N + e] = f0;
+      cf_soa[(3 * b + 1) * N + e] = f1;
+      cf_soa[(3 * b + 2) * N + e] = f2;
+    }
+    if (lc == 0) {
+      float f0 = 0.f, f1 = 0.f, f2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < RC; ++j) {
+        f0 += lamr[j][1] * inv_h;
+        f1 += lamr[j][2] * inv_h;
+        f2 += lamr[j][0] * inv_h;
+      }
+      cf_soa[0 * N + e] = f0;
+      cf_soa[1 * N + e] = f1;
+      cf_soa[2 * N + e] = f2;
+    }
+  }
+}
+
+template <class T>
+__device__ __forceinline__ void team_com_velocity(const DevModel* __restrict__ M, const TeamState<T>& s, float* v) {
+  float R[9], c[3], wc[3];
+  quat_to_mat(s.quat, R);
+  mat3vec(R, M->com[0], c);
+  cross3(s.w, c, wc);
+  v[0] = s.vo[0] + wc[0]; v[1] = s.vo[1] + wc[1]; v[2] = s.vo[2] + wc[2];
+}
+
+constexpr int kTeamBlock = 64;  // one wave per workgroup: 16 envs
+
+template <class T>
+__global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel* __restrict__ M, DevParams P,
+                                                                 SimBuffers B, const float* __restrict__ tau_aos) {
+  constexpr int LN = T::T_LANES, CL = T::T_CL, ND = T::ND;
+  __shared__ float mdl[CM<T>::NP * LN];
+  __shared__ float rows[RowSlots<T>::TOTAL * GS_WAVE];
+  stage_chain_model<T>(M, mdl);
+  __syncthreads();
+  const int lc = threadIdx.x & (LN - 1);
+  const int e = (blockIdx.x * kTeamBlock + threadIdx.x) / LN;
+  if (e >= B.N) return;
+  const int N = B.N;
+  TeamState<T> s;
+  team_load<T>(B.state, N, e, lc, s);
+  float tau[CL];
+#pragma unroll
+  for (int k = 0; k < CL; ++k) tau[k] = tau_aos ? tau_aos[(size_t)e * ND + lc * CL + k] : 0.f;
+  float* own = rows + threadIdx.x;
+  const float* team = rows + (threadIdx.x & ~(LN - 1));
+  for (int sstep = 0; sstep < P.substeps; ++sstep) {
+    const bool last = (sstep == P.substeps - 1) && P.collect;
+    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last);
+  }
+  team_store<T>(B.state, N, e, lc, s);
+}
+
+template <class T>
+__global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* __restrict__ M, DevParams P,
+                                                                SimBuffers B, PdDev A) {
+  constexpr int LN = T::T_LANES, CL = T::T_CL, ND = T::ND, NB = T::NB;
+  __shared__ float mdl[CM<T>::NP * LN];
+  __shared__ float rows[RowSlots<T>::TOTAL * GS_WAVE];
+  stage_chain_model<T>(M, mdl);
+  __syncthreads();
+  const int lc = threadIdx.x & (LN - 1);
+  const int e = (blockIdx.x * kTeamBlock + threadIdx.x) / LN;
+  if (e >= B.N) return;
+  const int N = B.N;
+  TeamState<T> s;
+  team_load<T>(B.state, N, e, lc, s);
+  float tau[CL];
+  float* own = rows + threadIdx.x;
+  const float* team = rows + (threadIdx.x & ~(LN - 1));
+  const int sub = P.substeps;
+  const int n_pd = A.decimation * sub;
+  const int total = (A.decimation + A.extra) * sub;
+  const size_t d0 = (size_t)e * ND + lc * CL;  // this lane's first dof in the AoS tensors
+  for (int it = 0; it < total; ++it) {
+    if (it < n_pd && (it % sub) == 0) {
+      const bool first = it == 0;
+#pragma unroll
+      for (int k = 0; k < CL; ++k) {
+        const float qj = first ? A.dof_state_in[(d0 + k) * 2 + 0] : s.q[k];
+        const float qdj = first ? A.dof_state_in[(d0 + k) * 2 + 1] : s.qd[k];
+        const float aj = A.actions[d0 + k];
+        tau[k] = clampf(A.kp * (A.scale * aj + A.default_pos[lc * CL + k] - qj) - A.kd * qdj, -A.tlim, A.tlim);
+      }
+    }
+    const bool last = ((it % sub) == sub - 1) && P.collect;
+    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last);
+    if (it == n_pd - 1 && A.dof_out) {
+#pragma unroll
+      for (int k = 0; k < CL; ++k) {
+        A.dof_out[(d0 + k) * 2 + 0] = s.q[k];
+        A.dof_out[(d0 + k) * 2 + 1] = s.qd[k];
+      }
+    }
+  }
+  team_store<T>(B.state, N, e, lc, s);
+#pragma unroll
+  for (int k = 0; k < CL; ++k) A.torques_out[d0 + k] = tau[k];
+  if (A.root_out && lc == 0) {
+    float* o = A.root_out + (size_t)e * 13;
+    o[0] = s.p[0]; o[1] = s.p[1]; o[2] = s.p[2];
+    o[3] = s.quat[0]; o[4] = s.quat[1]; o[5] = s.quat[2]; o[6] = s.quat[3];
+    float v[3];
+    team_com_velocity<T>(M, s, v);
+    o[7] = v[0]; o[8] = v[1]; o[9] = v[2];
+    o[10] = s.w[0]; o[11] = s.w[1]; o[12] = s.w[2];
+  }
+  if (P.collect && A.cf_out) {
+#pragma unroll
+    for (int k = 0; k < CL; ++k) {
+      const int b = 1 + lc * CL + k;
+#pragma unroll
+      for (int f = 0; f < 3; ++f) A.cf_out[((size_t)e * NB + b) * 3 + f] = B.cf[(3 * b + f) * N + e];
+    }
+    if (lc == 0) {
+#pragma unroll
+      for (int f = 0; f < 3; ++f) A.cf_out[((size_t)e * NB) * 3 + f] = B.cf[f * N + e];
+    }
+  }
+}
+
+}  // namespace
+
+template <class T>
+hipError_t launch_sim_team(const DevModel* M, const DevParams& P, const SimBuffers& B, const float* tau,
+                           hipStream_t st) {
+  if constexpr (T::HAS_TEAM) {
+    const long lanes = (long)B.N * T::T_LANES;
+    const int blocks = (int)((lanes + kTeamBlock - 1) / kTeamBlock);
+    hipLaunchKernelGGL(k_simulate_team<T>, dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, tau);
+    return hipGetLastError();
+  } else {
+    return hipErrorInvalidConfiguration;
+  }
+}
+template <class T>
+hipError_t launch_pd_team(const DevModel* M, const DevParams& P, const SimBuffers& B, const PdDev& A, hipStream_t st) {
+  if constexpr (T::HAS_TEAM) {
+    const long lanes = (long)B.N * T::T_LANES;
+    const int blocks = (int)((lanes + kTeamBlock - 1) / kTeamBlock);
+    hipLaunchKernelGGL(k_pd_step_team<T>, dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, A);
+    return hipGetLastError();
+  } else {
+    return hipErrorInvalidConfiguration;
+  }
+}
+
+#define GS_TEAM_ENTRY(T, SIG) {SIG, T::HAS_TEAM ? &launch_sim_team<T> : nullptr, T::HAS_TEAM ? &launch_pd_team<T> : nullptr},
+TeamEntry g_team_kernels[] = {GS_FOR_EACH_TOPOLOGY(GS_TEAM_ENTRY)};
+const int g_num_team_kernels = sizeof(g_team_kernels) / sizeof(g_team_kernels[0]);

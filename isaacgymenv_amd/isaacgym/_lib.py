@@ -26,7 +26,7 @@ class GsSimParams(C.Structure):
                 ("num_position_iterations", C.c_int32), ("num_velocity_iterations", C.c_int32),
                 ("contact_offset", C.c_double), ("rest_offset", C.c_double),
                 ("bounce_threshold_velocity", C.c_double), ("max_depenetration_velocity", C.c_double),
-                ("contact_collection", C.c_int32)]
+                ("contact_collection", C.c_int32), ("kernel_variant", C.c_int32)]
 
 
 class GsPdArgs(C.Structure):
@@ -63,6 +63,7 @@ def lib():
             "gs_sim_set_root": (i, [vp, vp, vp, i, vp]),
             "gs_sim_set_dof": (i, [vp, vp, vp, i, vp]),
             "gs_sim_pd_step": (i, [vp, C.POINTER(GsPdArgs), vp]),
+            "gs_sim_kernel_variant": (i, [vp]),
             "gs_sim_enable_timing": (i, [vp, i]),
             "gs_sim_last_kernel_ms": (f, [vp]),
         }
@@ -83,7 +84,7 @@ EXPORTED_SYMBOLS = [
     "gs_abi_version", "gs_last_error", "gs_topology_supported", "gs_sim_create", "gs_sim_destroy",
     "gs_sim_add_ground", "gs_sim_set_model", "gs_sim_prepare", "gs_sim_simulate", "gs_sim_refresh_root",
     "gs_sim_refresh_dof", "gs_sim_refresh_contact", "gs_sim_set_root", "gs_sim_set_dof", "gs_sim_pd_step",
-    "gs_sim_enable_timing", "gs_sim_last_kernel_ms",
+    "gs_sim_kernel_variant", "gs_sim_enable_timing", "gs_sim_last_kernel_ms",
 ]
 
 

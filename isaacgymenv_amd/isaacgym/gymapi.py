@@ -306,6 +306,8 @@ class Sim:
         p.bounce_threshold_velocity = float(px.bounce_threshold_velocity)
         p.max_depenetration_velocity = float(px.max_depenetration_velocity)
         p.contact_collection = int(px.contact_collection)
+        # GS_PHYSICS_KERNEL=auto|lane|team selects the physics kernel form
+        p.kernel_variant = {"auto": 0, "lane": 1, "team": 2}[os.environ.get("GS_PHYSICS_KERNEL", "auto")]
         self.cparams = p
         L = _lib.lib()
         h = L.gs_sim_create(int(compute_device), p)
@@ -365,6 +367,7 @@ class Sim:
         _lib.check(L.gs_sim_prepare(self.handle, N, self.state.data_ptr(), self.shape_mu.data_ptr(),
                                     self.cf_soa.data_ptr()), "gs_sim_prepare")
         self._keep = keep
+        self.kernel_variant = L.gs_sim_kernel_variant(self.handle)
         # reference-layout tensors (sim owned; wrap_tensor shares them)
         self.root_tensor = torch.zeros(N, 13, dtype=f32, device=tdev)
         self.dof_tensor = torch.zeros(N * nd, 2, dtype=f32, device=tdev)

@@ -26,11 +26,17 @@ def _oracle_step(flat, params, root, dof, tau, mu, steps=1):
     return r, d, cf
 
 
-def test_anymal_one_simulate_matches_oracle():
+KERNELS = {"lane": 1, "team": 2}
+
+
+@pytest.mark.parametrize("kernel", sorted(KERNELS))
+def test_anymal_one_simulate_matches_oracle(kernel, monkeypatch):
+    monkeypatch.setenv("GS_PHYSICS_KERNEL", kernel)
     n = 256
     art, flat = H.anymal()
     root, dof, tau, mu = H.anymal_states(n, seed=1)
     gym, sim = H.make_gpu_sim("anymal", n, H.ANYMAL_PARAMS)
+    assert sim.kernel_variant == KERNELS[kernel]
     H.load_state_into(sim, root, dof, mu)
     sim.dof_force.copy_(torch.from_numpy(tau.astype(np.float32).reshape(-1)))
     gym.simulate(sim)
@@ -46,8 +52,10 @@ def test_anymal_one_simulate_matches_oracle():
     np.testing.assert_allclose(g_cf, o_cf, atol=1.0, rtol=2e-2)
 
 
-def test_anymal_standing_rollout_tracks_oracle():
+@pytest.mark.parametrize("kernel", sorted(KERNELS))
+def test_anymal_standing_rollout_tracks_oracle(kernel, monkeypatch):
     """50 env steps of PD standing (5 simulates each): trajectories stay within 1e-3."""
+    monkeypatch.setenv("GS_PHYSICS_KERNEL", kernel)
     n = 64
     art, flat = H.anymal()
     q0 = np.array([H.ANYMAL_DEFAULT[d] for d in art.dof_names()])
@@ -90,3 +98,25 @@ def test_cartpole_matches_oracle():
     g_root, g_dof = H.read_state(sim, 2)
     o_root, o_dof, _ = _oracle_step(flat, H.CARTPOLE_PARAMS, root, dof, tau, mu)
     np.testing.assert_allclose(g_dof, o_dof, atol=1e-4, rtol=1e-4)
+
+
+def test_team_and_lane_kernels_agree_on_random_states(monkeypatch):
+    """Both kernel forms from the same 1024 random states (incl. penetrating, airborne, tilted)."""
+    n = 1024
+    art, flat = H.anymal()
+    root, dof, tau, mu = H.anymal_states(n, seed=21, spread=2.0)
+    out = {}
+    for kernel in ("lane", "team"):
+        monkeypatch.setenv("GS_PHYSICS_KERNEL", kernel)
+        gym, sim = H.make_gpu_sim("anymal", n, H.ANYMAL_PARAMS)
+        H.load_state_into(sim, root, dof, mu)
+        sim.dof_force.copy_(torch.from_numpy(tau.astype(np.float32).reshape(-1)))
+        for _ in range(5):
+            gym.simulate(sim)
+        torch.cuda.synchronize()
+        out[kernel] = H.read_state(sim, 12) + (sim.cf_soa.cpu().numpy(),)
+    (r1, d1, c1), (r2, d2, c2) = out["lane"], out["team"]
+    np.testing.assert_allclose(r2[:, :7], r1[:, :7], atol=1e-3)
+    np.testing.assert_allclose(d2[:, :, 0], d1[:, :, 0], atol=1e-3)
+    np.testing.assert_allclose(r2[:, 7:], r1[:, 7:], atol=2e-2)
+    np.testing.assert_allclose(d2[:, :, 1], d1[:, :, 1], atol=5e-2)

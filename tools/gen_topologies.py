@@ -74,10 +74,65 @@ def topo_tables(flat: dict) -> dict:
         subend[parent[b]] = max(subend[parent[b]], subend[b])
     cshape = [int(s) for s in flat["cshape"]]
     jkind = [int(k) for k in flat["jkind"]]
-    return dict(NB=nb, ND=nd, NC=nc, NS=int(flat["ns"]), FIXED=fixed, NBASE=nbase, NV=nv, MAXDEP=maxdep,
+    team = team_tables(flat, parent, bdof, nbase)
+    return dict(TEAM=team, NB=nb, ND=nd, NC=nc, NS=int(flat["ns"]), FIXED=fixed, NBASE=nbase, NV=nv, MAXDEP=maxdep,
                 parent=parent, bdof=bdof, jkind=jkind, dpar=dpar, depth=[len(a) for a in anc],
                 anc=[a + [-1] * (maxdep - len(a)) for a in anc], bgdof=bgdof, cbody=cbody, cleaf=cleaf,
                 csupp=csupp, cslot=cslot, NSLOT=max(off, 1), gbody=gbody, cshape=cshape, subend=subend)
+
+
+def team_tables(flat, parent, bdof, nbase):
+    """Lane-team layout for a floating 'uniform star': root + NCH identical-structure serial chains.
+
+    Returns None when the topology does not qualify (the one-env-per-lane kernel is used)."""
+    nb = len(parent)
+    if nbase != 6 or nb < 2:
+        return None
+    kids = {}
+    for b in range(1, nb):
+        kids.setdefault(parent[b], []).append(b)
+    chains = []
+    for top in kids.get(0, []):
+        ch, cur = [top], top
+        while cur in kids:
+            if len(kids[cur]) != 1:
+                return None
+            cur = kids[cur][0]
+            ch.append(cur)
+        chains.append(ch)
+    nch, cl = len(chains), len(chains[0])
+    if any(len(c) != cl for c in chains) or nch > 8:
+        return None
+    # chains must be contiguous in body order with dofs in the same order
+    for c, ch in enumerate(chains):
+        if ch != list(range(1 + c * cl, 1 + (c + 1) * cl)) or [bdof[b] for b in ch] != list(range(c * cl, (c + 1) * cl)):
+            return None
+    cbody = [int(b) for b in flat["cbody"]]
+    cshape = [int(s) for s in flat["cshape"]]
+    rc = sum(1 for b in cbody if b == 0)
+    if cbody[:rc] != [0] * rc:
+        return None
+    rest = list(zip(cbody[rc:], cshape[rc:]))
+    if len(rest) % nch:
+        return None
+    cc = len(rest) // nch
+    per = [rest[c * cc:(c + 1) * cc] for c in range(nch)]
+    loc_b = [b - 1 - 0 * cl for b, _ in per[0]]
+    root_shapes = max(cshape[:rc]) + 1 if rc else 0
+    shapes_per_chain = (max(s for _, s in rest) + 1 - root_shapes) // nch if rest else 0
+    loc_s = [s - root_shapes for _, s in per[0]]
+    for c in range(nch):
+        if [b - 1 - c * cl for b, _ in per[c]] != loc_b:
+            return None
+        if [s - root_shapes - c * shapes_per_chain for _, s in per[c]] != loc_s:
+            return None
+    lanes = 1
+    while lanes < nch:
+        lanes *= 2
+    if lanes > 4:  # quad-DPP reductions: up to 4 lanes per env
+        return None
+    return dict(LANES=lanes, NCH=nch, CL=cl, RC=rc, CC=cc, RS=root_shapes, SPC=shapes_per_chain,
+                ccb=loc_b, ccs=loc_s, rcs=cshape[:rc] or [0])
 
 
 def carr(v) -> str:
@@ -110,6 +165,17 @@ def emit() -> str:
             dim = n if len(t[k]) else "1"
             lines.append(f"  static constexpr int {k}[{dim}] = {carr(vals)};")
         lines.append(f"  static constexpr int anc[NV][MAXDEP] = {carr(t['anc'])};")
+        tm = t["TEAM"]
+        if tm:
+            lines.append("  // lane-team layout (gs_team.hip): LANES lanes per env, lane c owns chain c")
+            lines.append("  static constexpr bool HAS_TEAM = true;")
+            for k in ("LANES", "NCH", "CL", "RC", "CC", "RS", "SPC"):
+                lines.append(f"  static constexpr int T_{k} = {tm[k]};")
+            for k in ("ccb", "ccs", "rcs"):
+                vals = tm[k] if tm[k] else [0]
+                lines.append(f"  static constexpr int T_{k}[{len(vals)}] = {carr(vals)};")
+        else:
+            lines.append("  static constexpr bool HAS_TEAM = false;")
         lines.append("};")
         lines.append("")
         reg.append((sig, name))
