@@ -92,6 +92,8 @@ typedef struct gs_pd_args {
     float *dof_state_out;        /* [N*nd][2] or NULL            */
     float *root_state_out;       /* [N][13]   or NULL            */
     float *contact_out;          /* [N*nb][3] or NULL            */
+    float *actions_copy_out;     /* [N][nd] or NULL: receives `actions` (the task's
+                                    `self.actions = actions.clone()`, anymal_terrain.py:442) */
 } gs_pd_args;
 
 int gs_abi_version(void);

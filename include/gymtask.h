@@ -29,6 +29,15 @@ extern "C" {
 #define GT_ANYMAL_NUM_TERMS 13  /* lin_vel_xy lin_vel_z ang_vel_z ang_vel_xy orient torques joint_acc
                                    base_height air_time collision stumble action_rate hip */
 
+/* One torch.rand(n) call on the device generator, evaluated in-kernel instead of launched
+ * (isaacgymenv_amd/csrc/torch_philox.h): seed and offset are the generator's before the call,
+ * threads = 256 * min(CUs * maxThreadsPerCU / 256, ceil(n / 256)); the host advances the
+ * generator offset by ((n - 1) / (4 * threads) + 1) * 4 as torch does. */
+typedef struct gt_torch_rand_plan {
+    uint64_t seed, offset;
+    uint32_t threads, numel;
+} gt_torch_rand_plan;
+
 typedef struct gt_anymal_params {
     int32_t num_envs, num_dofs, num_bodies, num_obs;
     int32_t base_index;
@@ -68,6 +77,17 @@ typedef struct gt_anymal_buffers {
     float *projected_gravity;    /* [N][3]                                    */
     float *obs_buf;              /* [N][num_obs]                              */
     const float *noise_scale;    /* [num_obs]                                 */
+    int32_t *reset_count;        /* [3] device, zero-initialised: post_a's accumulator and
+                                    workgroup counter (re-armed by post_a itself), and [2] =
+                                    the number of envs post_a flagged for reset               */
+    int32_t *host_count;         /* [2] host-mapped words (gt_host_alloc) or NULL: post_a's last
+                                    workgroup stores {count, seq} with system scope            */
+    int32_t seq;                 /* sequence number post_a publishes in host_count[1]        */
+    uint64_t *reset_masks;       /* [ceil(N/64)] post_a's per-wave reset ballots (bit l of word w =
+                                    env 64w+l), read by gt_anymal_reset_flagged                */
+    float *obs_out;              /* [N][num_obs] or NULL: VecTask's clamped obs copy (vec_task.py:402) */
+    uint8_t *time_outs;          /* [N] bool or NULL: (progress >= T-1) & reset (vec_task.py:394)     */
+    float clip_obs;              /* clipObservations (inf -> plain copy)                    */
 } gt_anymal_buffers;
 
 int gt_abi_version(void);
@@ -82,9 +102,41 @@ int gt_anymal_reset(const gt_anymal_params *p, const gt_anymal_buffers *b, const
                     const float *pos_offset, const float *dof_vel, const float *cmd_x, const float *cmd_y,
                     const float *cmd_heading, float *episode_out, void *stream);
 
-/* noise [N][num_obs] uniform(0,1) draws (torch.rand_like) or NULL when addNoise is false */
+/* torch.rand draws (uniform [0,1), float32) made by the host in the reference's order
+ * (anymal_terrain.py:385-398); the kernel applies torch_rand_float's map
+ * `range * u + lower` in float32 (range = float(upper - lower)). */
+typedef struct gt_anymal_reset_draws {
+    const float *u_pos, *u_vel;              /* [k][nd] drawn buffers, or NULL: use the plan */
+    const float *u_cmd_x, *u_cmd_y, *u_cmd_h; /* [k]     */
+    gt_torch_rand_plan plan_pos, plan_vel, plan_cmd_x, plan_cmd_y, plan_cmd_h;
+    float pos_range, pos_lower, vel_range, vel_lower;
+    float cmd_x_range, cmd_x_lower, cmd_y_range, cmd_y_lower, cmd_h_range, cmd_h_lower;
+} gt_anymal_reset_draws;
+
+/* reset_idx (plane terrain) for the k envs the last post_a flagged, without the host knowing
+ * which: envs are ranked by index from reset_masks (torch.nonzero's order), row t of the draws
+ * goes to the t-th flagged env.  env_ids_out int32[k] receives the flagged ids ascending (for
+ * set_*_tensor_indexed); episode_out[13] = mean over the flagged envs of each episode sum /
+ * episode_length_s (extras["episode"], :416-420), sums then zeroed.  scratch: 16 words of
+ * zero-initialised device memory the kernel re-arms. */
+int gt_anymal_reset_flagged(const gt_anymal_params *p, const gt_anymal_buffers *b, int k,
+                            const gt_anymal_reset_draws *draws, int32_t *env_ids_out, float *episode_out,
+                            float episode_length_s, void *scratch, void *stream);
+
+/* Pinned, device-mapped, coherent host memory for host_count (hipHostMalloc). */
+int gt_host_alloc(uint64_t bytes, void **host_ptr, void **device_ptr);
+int gt_host_free(void *host_ptr);
+/* Spin until words[1] == seq (post_a published), then *value = words[0].  Returns -1 after
+ * timeout_ms (a kernel that never finished): the caller raises instead of hanging. */
+int gt_wait_host_seq(const int32_t *words, int32_t seq, int32_t timeout_ms, int32_t *value);
+
+/* noise [N][num_obs] uniform draws (torch.rand_like(obs_buf)), or NULL and noise_plan for the
+ * same draws evaluated in-kernel, or both NULL when addNoise is false */
 int gt_anymal_post_physics_b(const gt_anymal_params *p, const gt_anymal_buffers *b, const float *noise,
-                             void *stream);
+                             const gt_torch_rand_plan *noise_plan, void *stream);
+
+/* out[plan.numel] = torch.rand(plan.numel) for the given plan (checks torch_philox.h against torch) */
+int gt_torch_rand(const gt_torch_rand_plan *plan, float *out, void *stream);
 
 #ifdef __cplusplus
 }

@@ -23,7 +23,7 @@ LIBS = {
 }
 # the task kernels mirror torch's unfused elementwise arithmetic
 EXTRA_FLAGS = {"libgymtask.so": ["-ffp-contract=off"]}
-HEADERS = ["gs_internal.h", "gs_topologies.h", "gs_math.h"]
+HEADERS = ["gs_internal.h", "gs_topologies.h", "gs_math.h", "torch_philox.h"]
 
 
 def hipcc() -> str:

@@ -230,6 +230,7 @@ int gs_sim_pd_step(gs_sim* s, const gs_pd_args* a, void* stream) {
   d.dof_out = a->dof_state_out;
   d.root_out = a->root_state_out;
   d.cf_out = a->contact_out;
+  d.actions_copy = a->actions_copy_out;
   hipStream_t st = (hipStream_t)stream;
   timing_begin(s, st);
   hipError_t e = s->pd_fn(s->d_model, s->dp, buffers(s), d, st);

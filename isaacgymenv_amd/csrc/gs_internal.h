@@ -55,6 +55,7 @@ struct PdDev {
   float* dof_out;            // [N*nd][2] or null
   float* root_out;           // [N][13]   or null
   float* cf_out;             // [N*nb][3] or null
+  float* actions_copy;       // [N][nd]   or null
 };
 
 typedef hipError_t (*launch_sim_fn)(const DevModel*, const DevParams&, const SimBuffers&, const float* tau,

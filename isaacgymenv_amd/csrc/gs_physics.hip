@@ -594,6 +594,10 @@ __global__ __launch_bounds__(GS_WAVE, 1) void k_pd_step(const DevModel* __restri
   store_state<T>(B.state, N, e, s);
 #pragma unroll
   for (int j = 0; j < ND; ++j) A.torques_out[(size_t)e * ND + j] = tau[j];
+  if (A.actions_copy) {
+#pragma unroll
+    for (int j = 0; j < ND; ++j) A.actions_copy[(size_t)e * ND + j] = A.actions[(size_t)e * ND + j];
+  }
   if (A.root_out) {
     float* o = A.root_out + (size_t)e * 13;
     o[0] = s.p[0]; o[1] = s.p[1]; o[2] = s.p[2];

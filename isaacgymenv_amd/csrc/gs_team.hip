@@ -819,6 +819,10 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
   team_store<T>(B.state, N, e, lc, s);
 #pragma unroll
   for (int k = 0; k < CL; ++k) A.torques_out[d0 + k] = tau[k];
+  if (A.actions_copy) {
+#pragma unroll
+    for (int k = 0; k < CL; ++k) A.actions_copy[d0 + k] = A.actions[d0 + k];
+  }
   if (A.root_out && lc == 0) {
     float* o = A.root_out + (size_t)e * 13;
     o[0] = s.p[0]; o[1] = s.p[1]; o[2] = s.p[2];

@@ -6,10 +6,15 @@
 // so results track the reference's elementwise torch ops to float rounding.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <cstring>
+#include <cstdint>
 #include <cstdio>
 #include <string>
+#include <thread>
 
 #include "../../include/gymtask.h"
+#include "torch_philox.h"
 
 namespace {
 thread_local std::string g_err;
@@ -34,27 +39,91 @@ __device__ __forceinline__ void quat_rotate_inverse(const float* q, const float*
 __device__ __forceinline__ float sq(float x) { return x * x; }
 __device__ __forceinline__ float norm3(const float* v) { return sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
 
-__global__ void k_post_a(gt_anymal_params p, gt_anymal_buffers b) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= p.num_envs) return;
-  const int nd = p.num_dofs, nb = p.num_bodies;
-  const int64_t prog = b.progress_buf[e] + 1;
-  b.progress_buf[e] = prog;
-  b.randomize_buf[e] += 1;
+// 16-float rows (nd <= 16) as float4 loads when the row is 16-B aligned (nd % 4 == 0 and the
+// tensor base is aligned; the host checks): AoS rows of 48 B per env are otherwise 12 dword
+// loads that each touch 64 cache lines per wave.
+template <bool VEC>
+__device__ __forceinline__ void load_row16(const float* __restrict__ src, int n, float* dst) {
+  if (VEC) {
+#pragma unroll
+    for (int j = 0; j < 16; j += 4)
+      if (j < n) {
+        const float4 v = *reinterpret_cast<const float4*>(src + j);
+        dst[j] = v.x; dst[j + 1] = v.y; dst[j + 2] = v.z; dst[j + 3] = v.w;
+      }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j < n) dst[j] = src[j];
+  }
+}
+// dof_state row [nd][2] -> q, qd
+template <bool VEC>
+__device__ __forceinline__ void load_dof_row(const float* __restrict__ src, int n, float* q, float* qd) {
+  if (VEC) {
+#pragma unroll
+    for (int j = 0; j < 16; j += 2)
+      if (j < n) {
+        const float4 v = *reinterpret_cast<const float4*>(src + 2 * j);
+        q[j] = v.x; qd[j] = v.y; q[j + 1] = v.z; qd[j + 1] = v.w;
+      }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j < n) { q[j] = src[2 * j]; qd[j] = src[2 * j + 1]; }
+  }
+}
 
-  const float* root = b.root_states + (size_t)e * 13;
-  float q[4] = {root[3], root[4], root[5], root[6]};
+// One env: every input is loaded first (one memory round trip), then computed, then stored:
+// the buffers may alias as far as the compiler knows, so interleaved loads and stores would
+// serialise into one round trip per statement group.
+template <bool VEC>
+__device__ __forceinline__ bool post_a_env(const gt_anymal_params& p, const gt_anymal_buffers& b, const int e) {
+  const int nd = p.num_dofs, nb = p.num_bodies;
+  const size_t N = p.num_envs;
+  // ---- loads
+  const int64_t prog = b.progress_buf[e] + 1;
+  const int64_t rnd = b.randomize_buf[e] + 1;
+  float root[13];
+#pragma unroll
+  for (int k = 0; k < 13; ++k) root[k] = b.root_states[(size_t)e * 13 + k];
+  float cmd[4], air[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    cmd[k] = b.commands[(size_t)e * 4 + k];
+    air[k] = b.feet_air_time[(size_t)e * 4 + k];
+  }
+  const float* cf = b.contact_forces + (size_t)e * nb * 3;
+  float fbase[3], fknee[4][3], ffoot[4][3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) fbase[c] = cf[3 * p.base_index + c];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      fknee[k][c] = k < p.num_knees ? cf[3 * p.knee_idx[k] + c] : 0.0f;
+      ffoot[k][c] = k < p.num_feet ? cf[3 * p.feet_idx[k] + c] : 0.0f;
+    }
+  float tq[16], act[16], lact[16], lqd[16], dq[16], dqd[16];
+  load_row16<VEC>(b.torques + (size_t)e * nd, nd, tq);
+  load_row16<VEC>(b.actions + (size_t)e * nd, nd, act);
+  load_row16<VEC>(b.last_actions + (size_t)e * nd, nd, lact);
+  load_row16<VEC>(b.last_dof_vel + (size_t)e * nd, nd, lqd);
+  load_dof_row<VEC>(b.dof_state + (size_t)e * nd * 2, nd, dq, dqd);
+  float not_timeout;
+  if (b.timeout_is_int64) not_timeout = (float)(~((const int64_t*)b.timeout_buf)[e]);
+  else not_timeout = ((const uint8_t*)b.timeout_buf)[e] ? 0.0f : 1.0f;
+  float sums[GT_ANYMAL_NUM_TERMS];
+#pragma unroll
+  for (int t = 0; t < GT_ANYMAL_NUM_TERMS; ++t) sums[t] = b.episode_sums[t * N + e];
+
+  // ---- base-frame quantities (anymal_terrain.py:461-463)
+  const float q[4] = {root[3], root[4], root[5], root[6]};
   float blv[3], bav[3], pg[3];
   quat_rotate_inverse(q, root + 7, blv);
   quat_rotate_inverse(q, root + 10, bav);
   const float gv[3] = {0.0f, 0.0f, -1.0f};
   quat_rotate_inverse(q, gv, pg);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    b.base_lin_vel[e * 3 + k] = blv[k];
-    b.base_ang_vel[e * 3 + k] = bav[k];
-    b.projected_gravity[e * 3 + k] = pg[k];
-  }
   // heading: quat_apply(q, (1,0,0)) -> t = 2 u x f ; f + w t + u x t
   const float tx = (q[1] * 0.0f - q[2] * 0.0f) * 2.0f;
   const float ty = (q[2] * 1.0f - q[0] * 0.0f) * 2.0f;
@@ -62,24 +131,21 @@ __global__ void k_post_a(gt_anymal_params p, gt_anymal_buffers b) {
   const float fx = (1.0f + q[3] * tx) + (q[1] * tz - q[2] * ty);
   const float fy = (0.0f + q[3] * ty) + (q[2] * tx - q[0] * tz);
   const float heading = atan2f(fy, fx);
-  float* cmd = b.commands + (size_t)e * 4;
   // wrap_to_pi (anymal_terrain.py:684-687) is TorchScript: `%=` there is C fmod, not a floored
   // remainder, so negative angles stay negative (pinned by tests/golden/anymal_terrain.npz)
   float ang = fmodf(cmd[3] - heading, kTwoPi);
   ang = ang - kTwoPi * (ang > kPi ? 1.0f : 0.0f);
   const float c2 = fminf(fmaxf(0.5f * ang, -1.0f), 1.0f);
-  cmd[2] = c2;
 
-  // ---- check_termination
-  const float* cf = b.contact_forces + (size_t)e * nb * 3;
-  bool reset = norm3(cf + 3 * p.base_index) > 1.0f;
+  // ---- check_termination (:294-300)
+  bool reset = norm3(fbase) > 1.0f;
   int knee_count = 0;
-  for (int k = 0; k < p.num_knees; ++k) knee_count += norm3(cf + 3 * p.knee_idx[k]) > 1.0f ? 1 : 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) knee_count += (k < p.num_knees && norm3(fknee[k]) > 1.0f) ? 1 : 0;
   if (!p.allow_knee_contacts && knee_count > 0) reset = true;
   if (prog >= p.max_episode_length - 1) reset = true;
-  b.reset_buf[e] = reset ? 1 : 0;
 
-  // ---- compute_reward (reference order)
+  // ---- compute_reward (:315-382, reference order)
   const float lin_err = sq(cmd[0] - blv[0]) + sq(cmd[1] - blv[1]);
   const float ang_err = sq(c2 - bav[2]);
   const float r_lin_xy = expf(-lin_err / 0.25f) * p.s_lin_vel_xy;
@@ -88,65 +154,95 @@ __global__ void k_post_a(gt_anymal_params p, gt_anymal_buffers b) {
   const float r_ang_xy = (sq(bav[0]) + sq(bav[1])) * p.s_ang_vel_xy;
   const float r_orient = (sq(pg[0]) + sq(pg[1])) * p.s_orient;
   const float r_height = sq(root[2] - 0.52f) * p.s_base_height;
-  const float* tq = b.torques + (size_t)e * nd;
-  const float* act = b.actions + (size_t)e * nd;
-  const float* lact = b.last_actions + (size_t)e * nd;
-  const float* lqd = b.last_dof_vel + (size_t)e * nd;
-  const float* ds = b.dof_state + (size_t)e * nd * 2;
   float s_tq = 0.f, s_acc = 0.f, s_rate = 0.f;
-  for (int j = 0; j < nd; ++j) {
-    s_tq += sq(tq[j]);
-    s_acc += sq(lqd[j] - ds[2 * j + 1]);
-    s_rate += sq(lact[j] - act[j]);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    if (j < nd) {
+      s_tq += sq(tq[j]);
+      s_acc += sq(lqd[j] - dqd[j]);
+      s_rate += sq(lact[j] - act[j]);
+    }
   }
   const float r_torque = s_tq * p.s_torque;
   const float r_jacc = s_acc * p.s_joint_acc;
   const float r_coll = (float)knee_count * p.s_collision;
   int stumble = 0;
-  float* air = b.feet_air_time + (size_t)e * 4;
   float air_sum = 0.f;
-  for (int k = 0; k < p.num_feet; ++k) {
-    const float* f = cf + 3 * p.feet_idx[k];
-    stumble += (sqrtf(f[0] * f[0] + f[1] * f[1]) > 5.0f && fabsf(f[2]) < 1.0f) ? 1 : 0;
-    const bool contact = f[2] > 1.0f;
-    const bool first = (air[k] > 0.0f) && contact;
-    const float a = air[k] + p.dt;
-    air_sum += (a - 0.5f) * (first ? 1.0f : 0.0f);
-    air[k] = a * (contact ? 0.0f : 1.0f);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (k < p.num_feet) {
+      const float* f = ffoot[k];
+      stumble += (sqrtf(f[0] * f[0] + f[1] * f[1]) > 5.0f && fabsf(f[2]) < 1.0f) ? 1 : 0;
+      const bool contact = f[2] > 1.0f;
+      const bool first = (air[k] > 0.0f) && contact;
+      const float a = air[k] + p.dt;
+      air_sum += (a - 0.5f) * (first ? 1.0f : 0.0f);
+      air[k] = a * (contact ? 0.0f : 1.0f);
+    }
   }
   const float r_stumble = (float)stumble * p.s_stumble;
   const float r_rate = s_rate * p.s_action_rate;
   float r_air = air_sum * p.s_air_time;
   r_air = r_air * (sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]) > 0.1f ? 1.0f : 0.0f);
   float hip = 0.f;
-  for (int k = 0; k < 4; ++k) {
-    const int j = p.hip_dofs[k];
-    hip += fabsf(ds[2 * j] - p.default_dof_pos[j]);
-  }
+  // hip dofs are 0, 3, 6, 9 (anymal_terrain.py:378); constant indices keep dq in registers
+#pragma unroll
+  for (int k = 0; k < 4; ++k) hip += fabsf(dq[3 * k] - p.default_dof_pos[3 * k]);
   const float r_hip = hip * p.s_hip;
   float rew = r_lin_xy + r_ang_z + r_lin_z + r_ang_xy + r_orient + r_height + r_torque + r_jacc + r_coll + r_rate +
               r_air + r_hip + r_stumble;
   rew = fmaxf(rew, 0.0f);
-  float not_timeout;
-  if (b.timeout_is_int64) not_timeout = (float)(~((const int64_t*)b.timeout_buf)[e]);
-  else not_timeout = ((const uint8_t*)b.timeout_buf)[e] ? 0.0f : 1.0f;
   rew += p.s_termination * ((reset ? 1.0f : 0.0f) * not_timeout);
+  const float terms[GT_ANYMAL_NUM_TERMS] = {r_lin_xy, r_lin_z,  r_ang_z,    r_ang_xy, r_orient, r_torque, r_jacc,
+                                            r_height, r_air,    r_coll,     r_stumble, r_rate,  r_hip};
+
+  // ---- stores
+  b.progress_buf[e] = prog;
+  b.randomize_buf[e] = rnd;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    b.base_lin_vel[e * 3 + k] = blv[k];
+    b.base_ang_vel[e * 3 + k] = bav[k];
+    b.projected_gravity[e * 3 + k] = pg[k];
+  }
+  b.commands[(size_t)e * 4 + 2] = c2;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (k < p.num_feet) b.feet_air_time[(size_t)e * 4 + k] = air[k];
+  b.reset_buf[e] = reset ? 1 : 0;
   b.rew_buf[e] = rew;
-  const size_t N = p.num_envs;
-  float* es = b.episode_sums;
-  es[0 * N + e] += r_lin_xy;
-  es[1 * N + e] += r_lin_z;
-  es[2 * N + e] += r_ang_z;
-  es[3 * N + e] += r_ang_xy;
-  es[4 * N + e] += r_orient;
-  es[5 * N + e] += r_torque;
-  es[6 * N + e] += r_jacc;
-  es[7 * N + e] += r_height;
-  es[8 * N + e] += r_air;
-  es[9 * N + e] += r_coll;
-  es[10 * N + e] += r_stumble;
-  es[11 * N + e] += r_rate;
-  es[12 * N + e] += r_hip;
+#pragma unroll
+  for (int t = 0; t < GT_ANYMAL_NUM_TERMS; ++t) b.episode_sums[t * N + e] = sums[t] + terms[t];
+  return reset;
+}
+
+// One lane per env, one wave per workgroup (4096 envs -> 64 workgroups on 64 CUs: the tail is
+// latency bound, so spreading it over CUs beats packing 4 waves per CU).
+template <bool VEC>
+__global__ void __launch_bounds__(64) k_post_a(gt_anymal_params p, gt_anymal_buffers b) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  bool reset = false;
+  if (e < p.num_envs) reset = post_a_env<VEC>(p, b, e);
+  // reset count: one 64-bit atomic per wave carries {waves done << 32 | count}; the wave that
+  // completes the grid publishes the total (device word reset_count[2], and {count, seq} into
+  // host memory for the host's spin wait) and re-arms the accumulator for the next launch
+  const unsigned long long m = __ballot(reset);
+  if ((threadIdx.x & 63) == 0) {
+    if (b.reset_masks) b.reset_masks[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = m;
+    const unsigned nwaves = (gridDim.x * blockDim.x + 63) / 64;
+    unsigned long long* acc = reinterpret_cast<unsigned long long*>(b.reset_count);
+    const unsigned long long add = (1ull << 32) | (unsigned long long)__popcll(m);
+    const unsigned long long old = atomicAdd(acc, add);
+    if ((unsigned)(old >> 32) == nwaves - 1) {
+      const int total = (int)((old + add) & 0xffffffffull);
+      *acc = 0ull;
+      b.reset_count[2] = total;
+      if (b.host_count) {
+        __hip_atomic_store(&b.host_count[0], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&b.host_count[1], b.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
 }
 
 __global__ void k_reset(gt_anymal_params p, gt_anymal_buffers b, const int32_t* __restrict__ ids, int k,
@@ -184,40 +280,182 @@ __global__ void k_reset(gt_anymal_params p, gt_anymal_buffers b, const int32_t* 
   }
 }
 
-// one thread per observation element: coalesced obs / noise traffic
-__global__ void k_post_b(gt_anymal_params p, gt_anymal_buffers b, const float* __restrict__ noise) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int no = p.num_obs;
-  if (t >= (long)p.num_envs * no) return;
-  const int e = (int)(t / no), k = (int)(t - (long)e * no);
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// reset_idx for the envs post_a flagged (anymal_terrain.py:384-425, plane terrain).  One lane
+// per env, one wave per workgroup; the rank of a flagged env among all flagged envs comes from
+// post_a's per-wave ballots (exclusive prefix of popcounts), so no compaction pass is needed.
+__global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_anymal_buffers b, int k,
+                                                      gt_anymal_reset_draws d, int32_t* __restrict__ ids_out,
+                                                      float* __restrict__ ep_out, float len_s,
+                                                      float* __restrict__ acc, unsigned* __restrict__ done) {
+  const int lane = threadIdx.x;
+  const int w = blockIdx.x;
+  const int e = w * 64 + lane;
+  int base = 0;
+  for (int c = 0; c < w; c += 64) {
+    const int i = c + lane;
+    base += wave_sum(i < w ? (int)__popcll(b.reset_masks[i]) : 0);
+  }
+  const unsigned long long mine = b.reset_masks[w];
+  const bool flagged = (mine >> lane) & 1ull;
   const int nd = p.num_dofs;
-  float v;
+  const size_t N = p.num_envs;
+  // The wave's draws (2*nd + 3 per flagged env) are evaluated by all 64 lanes and exchanged
+  // through LDS: one Philox chain per lane instead of 2*nd + 3 serial ones per flagged lane.
+  constexpr int kMaxDraws = 2 * 16 + 3;
+  __shared__ float u_lds[64 * kMaxDraws];
+  const int m = (int)__popcll(mine);
+  const int D = 2 * nd + 3;
+  for (int s = lane; s < m * D; s += 64) {
+    const int r = s / D, c = s - (s / D) * D;
+    const int t = base + r;
+    float u;
+    if (c < nd) u = d.u_pos ? d.u_pos[(size_t)t * nd + c] : torch_philox::rand_at(d.plan_pos, (size_t)t * nd + c);
+    else if (c < 2 * nd) {
+      const size_t q = (size_t)t * nd + (c - nd);
+      u = d.u_vel ? d.u_vel[q] : torch_philox::rand_at(d.plan_vel, q);
+    } else if (c == 2 * nd) u = d.u_cmd_x ? d.u_cmd_x[t] : torch_philox::rand_at(d.plan_cmd_x, t);
+    else if (c == 2 * nd + 1) u = d.u_cmd_y ? d.u_cmd_y[t] : torch_philox::rand_at(d.plan_cmd_y, t);
+    else u = d.u_cmd_h ? d.u_cmd_h[t] : torch_philox::rand_at(d.plan_cmd_h, t);
+    u_lds[s] = u;
+  }
+  __syncthreads();
+  float term[GT_ANYMAL_NUM_TERMS];
+#pragma unroll
+  for (int i = 0; i < GT_ANYMAL_NUM_TERMS; ++i) term[i] = 0.0f;
+  if (flagged) {
+    const int r = (int)__popcll(mine & ((1ull << lane) - 1ull));
+    const int t = base + r;
+    const float* u = u_lds + r * D;
+    float* ds = b.dof_state + (size_t)e * nd * 2;
+    for (int j = 0; j < nd; ++j) {
+      const float off = d.pos_range * u[j] + d.pos_lower;
+      const float vel = d.vel_range * u[nd + j] + d.vel_lower;
+      ds[2 * j] = p.default_dof_pos[j] * off;
+      ds[2 * j + 1] = vel;
+    }
+    float* root = b.root_states + (size_t)e * 13;
+    for (int j = 0; j < 13; ++j) root[j] = p.base_init_state[j];
+    float cmd[4];
+    const float ux = u[2 * nd], uy = u[2 * nd + 1], uh = u[2 * nd + 2];
+    cmd[0] = d.cmd_x_range * ux + d.cmd_x_lower;
+    cmd[1] = d.cmd_y_range * uy + d.cmd_y_lower;
+    cmd[2] = b.commands[(size_t)e * 4 + 2];
+    cmd[3] = d.cmd_h_range * uh + d.cmd_h_lower;
+    const float m = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]) > 0.25f ? 1.0f : 0.0f;
+    for (int j = 0; j < 4; ++j) b.commands[(size_t)e * 4 + j] = cmd[j] * m;
+    for (int j = 0; j < nd; ++j) {
+      b.last_actions[(size_t)e * nd + j] = 0.0f;
+      b.last_dof_vel[(size_t)e * nd + j] = 0.0f;
+    }
+    for (int j = 0; j < 4; ++j) b.feet_air_time[(size_t)e * 4 + j] = 0.0f;
+    b.progress_buf[e] = 0;
+    b.reset_buf[e] = 1;
+#pragma unroll
+    for (int i = 0; i < GT_ANYMAL_NUM_TERMS; ++i) {
+      term[i] = b.episode_sums[i * N + e];
+      b.episode_sums[i * N + e] = 0.0f;
+    }
+    ids_out[t] = e;
+  }
+  if (mine) {
+#pragma unroll
+    for (int i = 0; i < GT_ANYMAL_NUM_TERMS; ++i) {
+      const float s = wave_sum(term[i]);
+      if (lane == 0) atomicAdd(&acc[i], s);
+    }
+  }
+  unsigned old = 0;
+  if (lane == 0) {
+    __threadfence();
+    old = atomicAdd(done, 1u);
+  }
+  old = __shfl(old, 0, 64);
+  if (old == gridDim.x - 1) {  // last wave: finalise the 13 terms in parallel lanes
+    __threadfence();
+    if (lane < GT_ANYMAL_NUM_TERMS) {
+      const float v = atomicExch(&acc[lane], 0.0f);
+      ep_out[lane] = (v / (float)k) / len_s;  // torch.mean(sums[env_ids]) / max_episode_length_s
+    }
+    if (lane == 0) *done = 0u;
+  }
+}
+
+// One workgroup per env, one lane per observation element (compute_observations, :302-313).
+// Each lane selects its source address and scale first and then issues ONE load, so the
+// ragged segments of the obs row do not serialise into one memory round trip per segment.
+template <int NOISE>  // 0 none, 1 drawn buffer, 2 in-kernel torch.rand stream
+__global__ void __launch_bounds__(256) k_post_b(gt_anymal_params p, gt_anymal_buffers b,
+                                                const float* __restrict__ noise, gt_torch_rand_plan plan) {
+  const int e = blockIdx.x;
+  const int k = threadIdx.x;
+  const int no = p.num_obs;
+  if (k >= no) return;
+  const int nd = p.num_dofs;
+  const size_t t = (size_t)e * no + k;
+  // side outputs: last_actions / last_dof_vel (:484-485) and VecTask's time_outs (vec_task.py:394)
+  float la = 0.0f, lq = 0.0f;
+  if (k < nd) {
+    la = b.actions[(size_t)e * nd + k];
+    lq = b.dof_state[((size_t)e * nd + k) * 2 + 1];
+  }
+  int64_t prog = 0;
+  uint8_t rst = 0;
+  if (k == 0 && b.time_outs) {
+    prog = b.progress_buf[e];
+    rst = b.reset_buf[e];
+  }
+  const float* src;
+  float sc = 1.0f;
+  bool height = false;
   if (k < 3) {
-    v = b.base_lin_vel[e * 3 + k] * p.lin_vel_scale;
+    src = b.base_lin_vel + e * 3 + k; sc = p.lin_vel_scale;
   } else if (k < 6) {
-    v = b.base_ang_vel[e * 3 + k - 3] * p.ang_vel_scale;
+    src = b.base_ang_vel + e * 3 + k - 3; sc = p.ang_vel_scale;
   } else if (k < 9) {
-    v = b.projected_gravity[e * 3 + k - 6];
+    src = b.projected_gravity + e * 3 + k - 6;
   } else if (k < 12) {
-    const float sc = k < 11 ? p.lin_vel_scale : p.ang_vel_scale;
-    v = b.commands[(size_t)e * 4 + k - 9] * sc;
+    src = b.commands + (size_t)e * 4 + k - 9; sc = k < 11 ? p.lin_vel_scale : p.ang_vel_scale;
   } else if (k < 12 + nd) {
-    v = b.dof_state[((size_t)e * nd + (k - 12)) * 2] * p.dof_pos_scale;
+    src = b.dof_state + ((size_t)e * nd + (k - 12)) * 2; sc = p.dof_pos_scale;
   } else if (k < 12 + 2 * nd) {
-    v = b.dof_state[((size_t)e * nd + (k - 12 - nd)) * 2 + 1] * p.dof_vel_scale;
+    src = b.dof_state + ((size_t)e * nd + (k - 12 - nd)) * 2 + 1; sc = p.dof_vel_scale;
   } else if (k < no - nd) {
     // plane terrain: measured heights are 0 (anymal_terrain.py:516-517)
-    const float h = b.root_states[(size_t)e * 13 + 2] - 0.5f - 0.0f;
-    v = fminf(fmaxf(h, -1.0f), 1.0f) * p.height_meas_scale;
+    src = b.root_states + (size_t)e * 13 + 2; height = true;
   } else {
-    v = b.actions[(size_t)e * nd + (k - (no - nd))];
+    src = b.actions + (size_t)e * nd + (k - (no - nd));
   }
-  if (noise) v = v + (2.0f * noise[t] - 1.0f) * b.noise_scale[k];
+  const float x = *src;
+  const float nz = NOISE == 1 ? noise[t] : NOISE == 2 ? torch_philox::rand_at(plan, t) : 0.0f;
+  const float ns = b.noise_scale[k];
+  float v;
+  if (height) v = fminf(fmaxf(x - 0.5f - 0.0f, -1.0f), 1.0f) * p.height_meas_scale;
+  else if (k < 12 + 2 * nd && !(k >= 6 && k < 9)) v = x * sc;
+  else v = x;
+  if (NOISE) v = v + (2.0f * nz - 1.0f) * ns;
   b.obs_buf[t] = v;
+  if (b.obs_out) b.obs_out[t] = fminf(fmaxf(v, -b.clip_obs), b.clip_obs);
+  if (k == 0 && b.time_outs) b.time_outs[e] = (prog >= p.max_episode_length - 1) && (rst != 0);
   if (k < nd) {
-    b.last_actions[(size_t)e * nd + k] = b.actions[(size_t)e * nd + k];
-    b.last_dof_vel[(size_t)e * nd + k] = b.dof_state[((size_t)e * nd + k) * 2 + 1];
+    b.last_actions[(size_t)e * nd + k] = la;
+    b.last_dof_vel[(size_t)e * nd + k] = lq;
   }
+}
+
+__global__ void k_torch_rand(gt_torch_rand_plan plan, float* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < plan.numel) out[i] = torch_philox::rand_at(plan, i);
 }
 
 int fail(const char* what, hipError_t e) {
@@ -243,8 +481,17 @@ const char* gt_last_error(void) { return g_err.c_str(); }
 
 int gt_anymal_post_physics_a(const gt_anymal_params* p, const gt_anymal_buffers* b, void* stream) {
   if (check_params(p)) return -1;
-  const int blk = 256;
-  hipLaunchKernelGGL(k_post_a, dim3((p->num_envs + blk - 1) / blk), dim3(blk), 0, (hipStream_t)stream, *p, *b);
+  if (!b->reset_count) {
+    g_err = "gt_anymal_post_physics_a: reset_count (int32[3], zero-initialised) is required";
+    return -1;
+  }
+  const int blk = 64;
+  const dim3 grid((p->num_envs + blk - 1) / blk);
+  auto aligned = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
+  const bool vec = p->num_dofs % 4 == 0 && aligned(b->torques) && aligned(b->actions) && aligned(b->last_actions) &&
+                   aligned(b->last_dof_vel) && aligned(b->dof_state);
+  if (vec) hipLaunchKernelGGL(k_post_a<true>, grid, dim3(blk), 0, (hipStream_t)stream, *p, *b);
+  else hipLaunchKernelGGL(k_post_a<false>, grid, dim3(blk), 0, (hipStream_t)stream, *p, *b);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("gt_anymal_post_physics_a", e);
 }
@@ -265,14 +512,107 @@ int gt_anymal_reset(const gt_anymal_params* p, const gt_anymal_buffers* b, const
 }
 
 int gt_anymal_post_physics_b(const gt_anymal_params* p, const gt_anymal_buffers* b, const float* noise,
-                             void* stream) {
+                             const gt_torch_rand_plan* noise_plan, void* stream) {
   if (check_params(p)) return -1;
-  const long n = (long)p->num_envs * p->num_obs;
-  const int blk = 256;
-  hipLaunchKernelGGL(k_post_b, dim3((unsigned)((n + blk - 1) / blk)), dim3(blk), 0, (hipStream_t)stream, *p, *b,
-                     noise);
+  if (p->num_obs > 256) {
+    g_err = "gt_anymal_post_physics_b: num_obs > 256";
+    return -1;
+  }
+  const int blk = (p->num_obs + 63) / 64 * 64;
+  gt_torch_rand_plan plan{};
+  hipStream_t st = (hipStream_t)stream;
+  if (noise) {
+    hipLaunchKernelGGL(k_post_b<1>, dim3(p->num_envs), dim3(blk), 0, st, *p, *b, noise, plan);
+  } else if (noise_plan) {
+    if ((uint64_t)noise_plan->numel != (uint64_t)p->num_envs * p->num_obs || noise_plan->threads == 0) {
+      g_err = "gt_anymal_post_physics_b: noise plan does not cover obs_buf";
+      return -1;
+    }
+    hipLaunchKernelGGL(k_post_b<2>, dim3(p->num_envs), dim3(blk), 0, st, *p, *b, nullptr, *noise_plan);
+  } else {
+    hipLaunchKernelGGL(k_post_b<0>, dim3(p->num_envs), dim3(blk), 0, st, *p, *b, nullptr, plan);
+  }
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("gt_anymal_post_physics_b", e);
+}
+
+int gt_anymal_reset_flagged(const gt_anymal_params* p, const gt_anymal_buffers* b, int k,
+                            const gt_anymal_reset_draws* d, int32_t* env_ids_out, float* episode_out,
+                            float episode_length_s, void* scratch, void* stream) {
+  if (check_params(p)) return -1;
+  if (!b->reset_masks || !d || !env_ids_out || !episode_out || !scratch || k < 0 || k > p->num_envs) {
+    g_err = "gt_anymal_reset_flagged: invalid arguments";
+    return -1;
+  }
+  if (k == 0) return 0;
+  float* acc = static_cast<float*>(scratch);
+  unsigned* done = reinterpret_cast<unsigned*>(acc + GT_ANYMAL_NUM_TERMS);
+  hipLaunchKernelGGL(k_reset_flagged, dim3((p->num_envs + 63) / 64), dim3(64), 0, (hipStream_t)stream, *p, *b, k,
+                     *d, env_ids_out, episode_out, episode_length_s, acc, done);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail("gt_anymal_reset_flagged", e);
+}
+
+int gt_torch_rand(const gt_torch_rand_plan* plan, float* out, void* stream) {
+  if (!plan || !out || plan->threads == 0) {
+    g_err = "gt_torch_rand: invalid arguments";
+    return -1;
+  }
+  if (plan->numel == 0) return 0;
+  const int blk = 256;
+  hipLaunchKernelGGL(k_torch_rand, dim3((plan->numel + blk - 1) / blk), dim3(blk), 0, (hipStream_t)stream, *plan,
+                     out);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail("gt_torch_rand", e);
+}
+
+int gt_host_alloc(uint64_t bytes, void** host_ptr, void** device_ptr) {
+  if (!host_ptr || !device_ptr || bytes == 0) {
+    g_err = "gt_host_alloc: invalid arguments";
+    return -1;
+  }
+  void* h = nullptr;
+  hipError_t e = hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return fail("gt_host_alloc hipHostMalloc", e);
+  std::memset(h, 0, bytes);
+  void* d = nullptr;
+  e = hipHostGetDevicePointer(&d, h, 0);
+  if (e != hipSuccess) {
+    (void)hipHostFree(h);
+    return fail("gt_host_alloc hipHostGetDevicePointer", e);
+  }
+  *host_ptr = h;
+  *device_ptr = d;
+  return 0;
+}
+
+int gt_host_free(void* host_ptr) {
+  if (!host_ptr) return 0;
+  hipError_t e = hipHostFree(host_ptr);
+  return e == hipSuccess ? 0 : fail("gt_host_free", e);
+}
+
+int gt_wait_host_seq(const int32_t* words, int32_t seq, int32_t timeout_ms, int32_t* value) {
+  if (!words || !value) {
+    g_err = "gt_wait_host_seq: invalid arguments";
+    return -1;
+  }
+  // Busy-poll: the count lands a few microseconds after post_a finishes, much sooner than an
+  // event wake-up.  Yield after the first ~50k polls (~1 ms) so a long wait does not hog a core.
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t i = 0;; ++i) {
+    if (__atomic_load_n(&words[1], __ATOMIC_ACQUIRE) == seq) {
+      *value = __atomic_load_n(&words[0], __ATOMIC_RELAXED);
+      return 0;
+    }
+    if ((i & 4095) == 4095) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) {
+        g_err = "gt_wait_host_seq: timed out waiting for post_a (kernel not finished)";
+        return -1;
+      }
+      if (i > 50000) std::this_thread::yield();
+    }
+  }
 }
 
 }  // extern "C"

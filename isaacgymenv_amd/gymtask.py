@@ -13,6 +13,40 @@ import torch
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libgymtask.so")
 
 
+class GtTorchRandPlan(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("offset", C.c_uint64), ("threads", C.c_uint32), ("numel", C.c_uint32)]
+
+
+class TorchRandPlanner:
+    """Reserves torch.rand(n) draws on a device generator without launching torch's kernel.
+
+    Mirrors ATen's calc_execution_policy + philox_cuda_state (DistributionTemplates.h): the
+    kernel-side evaluation is isaacgymenv_amd/csrc/torch_philox.h.  After ``plan(n)`` the
+    generator is exactly where ``torch.rand(n, device=...)`` would have left it."""
+
+    def __init__(self, device):
+        dev = torch.device(device)
+        self.index = dev.index if dev.index is not None else torch.cuda.current_device()
+        self.gen = torch.cuda.default_generators[self.index]
+        props = torch.cuda.get_device_properties(self.index)
+        self.grid_cap = props.multi_processor_count * (props.max_threads_per_multi_processor // 256)
+
+    def plan(self, n: int) -> GtTorchRandPlan:
+        return self.plan_many((n,))[0]
+
+    def plan_many(self, sizes):
+        """Plans for consecutive torch.rand calls of the given sizes (one generator update)."""
+        g = self.gen
+        seed, off = g.initial_seed(), g.get_offset()
+        plans = []
+        for n in sizes:
+            threads = 256 * min(self.grid_cap, (n + 255) // 256)
+            plans.append(GtTorchRandPlan(seed, off, threads, n))
+            off += ((n - 1) // (4 * threads) + 1) * 4
+        g.set_offset(off)
+        return plans
+
+
 class GtAnymalParams(C.Structure):
     _fields_ = [("num_envs", C.c_int32), ("num_dofs", C.c_int32), ("num_bodies", C.c_int32), ("num_obs", C.c_int32),
                 ("base_index", C.c_int32), ("num_feet", C.c_int32), ("feet_idx", C.c_int32 * 4),
@@ -31,7 +65,16 @@ class GtAnymalBuffers(C.Structure):
                                           "progress_buf", "randomize_buf", "reset_buf", "timeout_buf")] + [
         ("timeout_is_int64", C.c_int32)] + [
         (n, C.c_void_p) for n in ("rew_buf", "episode_sums", "base_lin_vel", "base_ang_vel", "projected_gravity",
-                                  "obs_buf", "noise_scale")]
+                                  "obs_buf", "noise_scale", "reset_count", "host_count")] + [
+        ("seq", C.c_int32), ("reset_masks", C.c_void_p), ("obs_out", C.c_void_p), ("time_outs", C.c_void_p),
+        ("clip_obs", C.c_float)]
+
+
+class GtAnymalResetDraws(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("u_pos", "u_vel", "u_cmd_x", "u_cmd_y", "u_cmd_h")] + [
+        (n, GtTorchRandPlan) for n in ("plan_pos", "plan_vel", "plan_cmd_x", "plan_cmd_y", "plan_cmd_h")] + [
+        (n, C.c_float) for n in ("pos_range", "pos_lower", "vel_range", "vel_lower", "cmd_x_range", "cmd_x_lower",
+                                 "cmd_y_range", "cmd_y_lower", "cmd_h_range", "cmd_h_lower")]
 
 
 _lib = None
@@ -47,7 +90,13 @@ def lib():
         P, B, vp, i = C.POINTER(GtAnymalParams), C.POINTER(GtAnymalBuffers), C.c_void_p, C.c_int
         for name, args in {"gt_anymal_post_physics_a": [P, B, vp],
                            "gt_anymal_reset": [P, B, vp, i, vp, vp, vp, vp, vp, vp, vp],
-                           "gt_anymal_post_physics_b": [P, B, vp, vp]}.items():
+                           "gt_anymal_post_physics_b": [P, B, vp, C.POINTER(GtTorchRandPlan), vp],
+                           "gt_torch_rand": [C.POINTER(GtTorchRandPlan), vp, vp],
+                           "gt_anymal_reset_flagged": [P, B, i, C.POINTER(GtAnymalResetDraws), vp, vp, C.c_float,
+                                                       vp, vp],
+                           "gt_host_alloc": [C.c_uint64, C.POINTER(vp), C.POINTER(vp)],
+                           "gt_host_free": [vp],
+                           "gt_wait_host_seq": [vp, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]}.items():
             fn = getattr(L, name)
             fn.restype = C.c_int
             fn.argtypes = args
@@ -58,7 +107,8 @@ def lib():
 
 
 EXPORTED_SYMBOLS = ["gt_abi_version", "gt_last_error", "gt_anymal_post_physics_a", "gt_anymal_reset",
-                    "gt_anymal_post_physics_b"]
+                    "gt_anymal_post_physics_b", "gt_anymal_reset_flagged", "gt_torch_rand", "gt_host_alloc",
+                    "gt_host_free", "gt_wait_host_seq"]
 
 
 def _check(rc, what):
@@ -121,24 +171,59 @@ class AnymalTailKernels:
             t.episode_sums[name] = self.sums[k]
         self.ep_out = z(len(self.TERMS))
         self.noise_scale = t.noise_scale_vec.contiguous()
+        self.reset_count = torch.zeros(3, dtype=torch.int32, device=dev)  # accumulator, wg counter, last count
+        self.reset_masks = torch.zeros((N + 63) // 64, dtype=torch.int64, device=dev)
+        self.reset_scratch = torch.zeros(16, dtype=torch.float32, device=dev)
+        # {count, seq} published by post_a straight into pinned host memory (gt_wait_host_seq)
+        h, d = C.c_void_p(), C.c_void_p()
+        _check(L.gt_host_alloc(8, C.byref(h), C.byref(d)), "gt_host_alloc")
+        self._host_words, self._host_words_dev = h.value, d.value
+        self._seq = 0
+        self._count_out = C.c_int32(0)
+        # reference draws (reset offsets/commands, obs noise) evaluated inside the kernels from the
+        # device generator's Philox stream (bit-identical to torch.rand); False: torch draws buffers
+        self.inkernel_rng = True
+        self.planner = TorchRandPlanner(dev)
+        self._draws = None
+        self._ep_keys = ["rew_" + name for name in self.TERMS]
         self._terrain_level = None
+        self._b = None
+        self._bound = None
+
+    def __del__(self):
+        if getattr(self, "_host_words", None) and _lib is not None:
+            _lib.gt_host_free(self._host_words)
+            self._host_words = None
+
+    # task attributes whose storage the kernels use; rebuilt only when one of them is rebound
+    _STABLE = ("root_states", "contact_forces", "dof_state", "last_actions", "last_dof_vel", "commands",
+               "feet_air_time", "progress_buf", "randomize_buf", "rew_buf", "base_lin_vel", "base_ang_vel",
+               "projected_gravity", "obs_buf")
 
     def _buffers(self):
+        """The gt_anymal_buffers struct; rebuilt only if the task rebound a buffer (cheap on the hot path)."""
         t = self.task
-        b = GtAnymalBuffers()
-        for name in ("root_states", "dof_state", "torques", "actions", "last_actions", "last_dof_vel", "commands",
-                     "feet_air_time", "progress_buf", "randomize_buf", "rew_buf", "base_lin_vel", "base_ang_vel",
-                     "projected_gravity", "obs_buf"):
-            v = getattr(t, name)
-            assert v.is_contiguous() and v.device.type == "cuda", name
-            setattr(b, name, v.data_ptr())
-        b.contact_forces = t.contact_forces.data_ptr()
-        b.reset_buf = self.reset_bool.data_ptr()
+        cur = tuple(getattr(t, n) for n in self._STABLE)
+        b = self._b
+        if b is None or any(x is not y for x, y in zip(cur, self._bound)):
+            b = GtAnymalBuffers()
+            for name, v in zip(self._STABLE, cur):
+                assert v.is_contiguous() and v.device.type == "cuda", name
+                setattr(b, name, v.data_ptr())
+            b.reset_buf = self.reset_bool.data_ptr()
+            b.episode_sums = self.sums.data_ptr()
+            b.noise_scale = self.noise_scale.data_ptr()
+            b.reset_count = self.reset_count.data_ptr()
+            b.host_count = self._host_words_dev
+            b.reset_masks = self.reset_masks.data_ptr()
+            self._b, self._bound = b, cur
+        b.torques = t.torques.data_ptr()
+        b.actions = t.actions.data_ptr()
         tb = t.timeout_buf
         b.timeout_buf = tb.data_ptr()
         b.timeout_is_int64 = int(tb.dtype == torch.int64)
-        b.episode_sums = self.sums.data_ptr()
-        b.noise_scale = self.noise_scale.data_ptr()
+        b.obs_out = None
+        b.time_outs = None
         return b
 
     def _stream(self):
@@ -148,8 +233,53 @@ class AnymalTailKernels:
         t = self.task
         if not t.torques.is_contiguous():
             t.torques = t.torques.contiguous()
-        _check(lib().gt_anymal_post_physics_a(self.p, self._buffers(), self._stream()), "gt_anymal_post_physics_a")
+        if not t.actions.is_contiguous():
+            t.actions = t.actions.contiguous()
+        b = self._buffers()
+        self._seq = (self._seq + 1) & 0x7FFFFFFF
+        b.seq = self._seq
+        _check(lib().gt_anymal_post_physics_a(self.p, b, self._stream()), "gt_anymal_post_physics_a")
         t.reset_buf = self.reset_bool  # check_termination makes reset_buf a bool tensor (anymal_terrain.py:295)
+
+    def num_resets(self) -> int:
+        """Envs the last post_a flagged for reset, read back through the stream (synchronising)."""
+        return int(self.reset_count[2].item())
+
+    # The host learns the reset count from post_a's last workgroup, which stores it into pinned
+    # host memory; meanwhile the GPU already builds the observations of the common no-reset step
+    # (see AnymalTerrain.post_physics_step).
+    WAIT_TIMEOUT_MS = 60000
+
+    def wait_reset_count(self) -> int:
+        _check(lib().gt_wait_host_seq(self._host_words, self._seq, self.WAIT_TIMEOUT_MS, C.byref(self._count_out)),
+               "gt_wait_host_seq")
+        self.last_reset_count = int(self._count_out.value)
+        return self.last_reset_count
+
+    def rng_snapshot(self):
+        """Host-side generator position (the device generator's Philox offset; with torch-drawn
+        buffers also the CPU generator, for callers that draw there).  Restoring it discards the
+        draws made after the snapshot."""
+        g = self.planner.gen
+        return g.get_offset(), (None if self.inkernel_rng else torch.get_rng_state())
+
+    def rng_restore(self, snap):
+        off, cpu = snap
+        self.planner.gen.set_offset(off)
+        if cpu is not None:
+            torch.set_rng_state(cpu)
+
+    def observe(self, rand_like=None):
+        """compute_observations + noise + history (anymal_terrain.py:477-485), one kernel.  The
+        noise is torch.rand_like(obs_buf): evaluated in-kernel (inkernel_rng) or drawn by
+        ``rand_like`` into a buffer; either way the generator advances as the reference's."""
+        t = self.task
+        if not t.add_noise:
+            self.post_b(None)
+        elif self.inkernel_rng:
+            self.post_b(None, self.planner.plan(t.obs_buf.numel()))
+        else:
+            self.post_b((rand_like or torch.rand_like)(t.obs_buf))
 
     def reset(self, env_ids_int32, pos_offset, vel, cmd_x, cmd_y, cmd_h):
         t = self.task
@@ -168,6 +298,53 @@ class AnymalTailKernels:
         t.extras["episode"]["terrain_level"] = self._terrain_level
         self._keep = (ids, pos_offset, vel, cx, cy, ch)
 
-    def post_b(self, noise):
-        _check(lib().gt_anymal_post_physics_b(self.p, self._buffers(), _ptr(noise), self._stream()),
+    def reset_flagged(self, k: int, rand_unit=None):
+        """reset_idx for the k envs the last post_a flagged (plane terrain), in one kernel.
+
+        Draws u ~ U[0,1) with ``rand_unit(shape, device)`` in the reference's order and shapes
+        (anymal_terrain.py:385-398: dof offsets, dof velocities, cmd x, cmd y, cmd heading), so the
+        RNG stream advances exactly as torch_rand_float's would; the kernel applies the affine
+        maps, ranks the flagged envs (nonzero order) and fills extras["episode"]."""
+        t = self.task
+        dev, nd = t.device, t.num_dof
+        d = self._draws
+        if d is None:  # the affine maps are fixed per task
+            d = self._draws = GtAnymalResetDraws()
+            for name, (lo, hi) in (("pos", (0.5, 1.5)), ("vel", (-0.1, 0.1)), ("cmd_x", t.command_x_range),
+                                   ("cmd_y", t.command_y_range), ("cmd_h", t.command_yaw_range)):
+                setattr(d, name + "_range", float(hi - lo))
+                setattr(d, name + "_lower", float(lo))
+        if self.inkernel_rng:
+            u = None
+            d.u_pos = d.u_vel = d.u_cmd_x = d.u_cmd_y = d.u_cmd_h = None
+            d.plan_pos, d.plan_vel, d.plan_cmd_x, d.plan_cmd_y, d.plan_cmd_h = self.planner.plan_many(
+                (k * nd, k * nd, k, k, k))
+        else:
+            u = [rand_unit((k, nd), dev), rand_unit((k, nd), dev)]
+            u += [rand_unit((k, 1), dev) for _ in range(3)]
+            d.u_pos, d.u_vel, d.u_cmd_x, d.u_cmd_y, d.u_cmd_h = (x.data_ptr() for x in u)
+        ids = torch.empty(k, dtype=torch.int32, device=dev)
+        ep = torch.empty(len(self.TERMS), dtype=torch.float32, device=dev)
+        _check(lib().gt_anymal_reset_flagged(self.p, self._buffers(), k, d, ids.data_ptr(), ep.data_ptr(),
+                                             float(t.max_episode_length_s), self.reset_scratch.data_ptr(),
+                                             self._stream()), "gt_anymal_reset_flagged")
+        t._set_reset_state(ids)
+        t.extras["episode"] = dict(zip(self._ep_keys, ep.unbind()))
+        if self._terrain_level is None:
+            self._terrain_level = torch.mean(t.terrain_levels.float())
+        t.extras["episode"]["terrain_level"] = self._terrain_level
+        self._keep = (u, ids)
+
+    def post_b(self, noise, noise_plan=None):
+        """Observations (+noise), history buffers, and VecTask's time_outs / clamped obs (vec_task.py:393-402)."""
+        t = self.task
+        b = self._buffers()
+        fuse_outputs = not t.dr_randomizations.get("observations", None)
+        if fuse_outputs:
+            obs = torch.empty_like(t.obs_buf)
+            time_outs = torch.empty(t.num_envs, dtype=torch.bool, device=t.device)
+            b.obs_out, b.time_outs, b.clip_obs = obs.data_ptr(), time_outs.data_ptr(), float(t.clip_obs)
+        _check(lib().gt_anymal_post_physics_b(self.p, b, _ptr(noise), noise_plan, self._stream()),
                "gt_anymal_post_physics_b")
+        if fuse_outputs:
+            t._fused_outputs = (time_outs, obs)

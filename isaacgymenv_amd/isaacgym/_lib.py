@@ -33,7 +33,7 @@ class GsPdArgs(C.Structure):
     _fields_ = [("actions", C.c_void_p), ("default_pos", C.c_void_p), ("kp", C.c_float), ("kd", C.c_float),
                 ("action_scale", C.c_float), ("torque_limit", C.c_float), ("decimation", C.c_int32),
                 ("extra_simulates", C.c_int32), ("torques_out", C.c_void_p), ("dof_state_out", C.c_void_p),
-                ("root_state_out", C.c_void_p), ("contact_out", C.c_void_p)]
+                ("root_state_out", C.c_void_p), ("contact_out", C.c_void_p), ("actions_copy_out", C.c_void_p)]
 
 
 _lib = None

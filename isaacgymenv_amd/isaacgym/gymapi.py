@@ -715,7 +715,7 @@ class Gym:
     # ---- MI355X extensions (not part of the Isaac Gym API)
     def amd_pd_decimation_step(self, sim: Sim, actions, default_pos, kp: float, kd: float, action_scale: float,
                                torque_limit: float, decimation: int, extra_simulates: int, torques_out,
-                               write_root: bool = True, write_contacts: bool = True):
+                               write_root: bool = True, write_contacts: bool = True, actions_copy_out=None):
         """Fused ``for i in decimation: PD torque; simulate; refresh dof`` + ``extra_simulates`` more
         simulates, + the root/contact refreshes of post_physics_step, in ONE kernel launch."""
         L = _lib.lib()
@@ -729,10 +729,15 @@ class Gym:
         a.dof_state_out = sim.dof_tensor.data_ptr()
         a.root_state_out = sim.root_tensor.data_ptr() if write_root else None
         a.contact_out = sim.contact_tensor.data_ptr() if write_contacts else None
+        a.actions_copy_out = actions_copy_out.data_ptr() if actions_copy_out is not None else None
         _lib.check(L.gs_sim_pd_step(sim.handle, a, sim.stream()), "gs_sim_pd_step")
 
     def amd_enable_kernel_timing(self, sim: Sim, enable: bool = True):
         _lib.check(_lib.lib().gs_sim_enable_timing(sim.handle, int(enable)), "gs_sim_enable_timing")
+
+    def amd_kernel_variant(self, sim: Sim) -> int:
+        """1: one env per lane, 2: lane team (4 lanes per env); see gs_sim_kernel_variant."""
+        return int(_lib.lib().gs_sim_kernel_variant(sim.handle))
 
     def amd_last_kernel_ms(self, sim: Sim) -> float:
         return float(_lib.lib().gs_sim_last_kernel_ms(sim.handle))

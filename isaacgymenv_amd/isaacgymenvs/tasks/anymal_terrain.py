@@ -38,6 +38,12 @@ from ..utils.torch_jit_utils import (get_axis_params, normalize, quat_apply, qua
                                      torch_rand_float)
 from .base.vec_task import VecTask
 
+
+def torch_rand_unit(shape, device):
+    """The torch.rand draw inside torch_rand_float (torch_jit_utils.py); the fused reset applies
+    torch_rand_float's affine map on the GPU, so the RNG stream advances identically."""
+    return torch.rand(*shape, device=device)
+
 REWARD_TERMS = ["lin_vel_xy", "lin_vel_z", "ang_vel_z", "ang_vel_xy", "orient", "torques", "joint_acc",
                 "base_height", "air_time", "collision", "stumble", "action_rate", "hip"]
 
@@ -234,10 +240,12 @@ class AnymalTerrain(VecTask):
         upper = gymapi.Vec3(spacing, spacing, spacing)
         self.anymal_handles = []
         self.envs = []
+        # one device->host copy instead of one blocking read per shape per env (same values)
+        friction_host = friction_buckets.cpu().numpy()[:, 0]
         for i in range(self.num_envs):
             env_handle = self.gym.create_env(self.sim, lower, upper, num_per_row)
             for sp in shape_props:
-                sp.friction = friction_buckets[i % num_buckets]
+                sp.friction = friction_host[i % num_buckets]
             self.gym.set_asset_rigid_shape_properties(asset, shape_props)
             handle = self.gym.create_actor(env_handle, asset, start_pose, "anymal", i, 0, 0)
             self.gym.set_actor_dof_properties(env_handle, handle, dof_props)
@@ -379,10 +387,17 @@ class AnymalTerrain(VecTask):
 
     def fused_physics_step(self, actions):
         """pre_physics_step + VecTask's simulate loop + post_physics_step's refreshes, one kernel."""
-        self.actions = actions.clone().to(self.device)
-        self.gym.amd_pd_decimation_step(self.sim, self.actions, self._default_pos_row(), float(self.Kp),
-                                        float(self.Kd), float(self.action_scale), 80.0, self.decimation,
-                                        self.control_freq_inv, self.torques)
+        if actions.device == self.torques.device and actions.dtype == torch.float32 and actions.is_contiguous():
+            # self.actions = actions.clone() (anymal_terrain.py:442), written by the physics kernel
+            self.actions = torch.empty_like(actions)
+            self.gym.amd_pd_decimation_step(self.sim, actions, self._default_pos_row(), float(self.Kp),
+                                            float(self.Kd), float(self.action_scale), 80.0, self.decimation,
+                                            self.control_freq_inv, self.torques, actions_copy_out=self.actions)
+        else:
+            self.actions = actions.clone().to(self.device)
+            self.gym.amd_pd_decimation_step(self.sim, self.actions, self._default_pos_row(), float(self.Kp),
+                                            float(self.Kd), float(self.action_scale), 80.0, self.decimation,
+                                            self.control_freq_inv, self.torques)
         self._fused_refreshed = True
 
     def _default_pos_row(self):
@@ -400,12 +415,22 @@ class AnymalTerrain(VecTask):
         if self._kernels is not None:
             if push:
                 self.push_robots()
-            self._kernels.post_a()  # counters, base quantities, heading command, termination, reward
-            env_ids = self.reset_buf.nonzero(as_tuple=False).flatten()
-            if len(env_ids) > 0:
-                self.reset_idx(env_ids)
-            noise = torch.rand_like(self.obs_buf) if self.add_noise else None
-            self._kernels.post_b(noise)  # observations (+ noise), action / dof-velocity history
+            kern = self._kernels
+            kern.post_a()  # counters, base quantities, heading command, termination, reward
+            # Optimistic: most steps reset nobody, so draw the noise and build the observations before
+            # the host knows the count.  On a reset step, roll the RNG back and redo both after
+            # reset_idx: the draws, their order and the results are the reference's either way.
+            snap = kern.rng_snapshot() if self.add_noise else None
+            kern.observe()
+            if kern.wait_reset_count() > 0:
+                k = kern.last_reset_count
+                if snap is not None:
+                    kern.rng_restore(snap)
+                if self.custom_origins:
+                    self.reset_idx(self.reset_buf.nonzero(as_tuple=False).flatten())
+                else:
+                    kern.reset_flagged(k, torch_rand_unit)  # reset_idx without nonzero / host sync
+                kern.observe()
             return
         self.progress_buf += 1
         self.randomize_buf += 1

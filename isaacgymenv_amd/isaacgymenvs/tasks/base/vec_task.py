@@ -16,7 +16,10 @@ subclasses depend on it:
 MI355X addition: a task may implement ``fused_physics_step(actions)``; when it
 does (and the sim runs the GPU pipeline), ``step`` calls it INSTEAD of
 ``pre_physics_step`` + the simulate loop.  The fused call must have exactly the
-observable effect of the unfused sequence (tests/test_fused_equivalence.py).
+observable effect of the unfused sequence (tests/test_task_gpu.py).  A task's
+fused tail may also hand ``step`` its ``(time_outs, clamped obs)`` pair through
+``self._fused_outputs`` (computed by the same kernel that writes ``obs_buf``),
+which replaces the three torch ops of vec_task.py:393-402.
 """
 from __future__ import annotations
 
@@ -210,6 +213,7 @@ class VecTask(Env):
 
     # the fused path is optional; tasks that provide it set this to True
     supports_fused_physics = False
+    _fused_outputs = None
 
     def _use_fused(self) -> bool:
         return (self.supports_fused_physics and self.device != "cpu" and not self.force_render
@@ -219,7 +223,10 @@ class VecTask(Env):
                                                    Dict[str, Any]]:
         if self.dr_randomizations.get("actions", None):
             actions = self.dr_randomizations["actions"]["noise_lambda"](actions)
-        action_tensor = torch.clamp(actions, -self.clip_actions, self.clip_actions)
+        if np.isinf(self.clip_actions):
+            action_tensor = actions  # clamp(+-inf) is an identity copy; pre_physics_step clones anyway
+        else:
+            action_tensor = torch.clamp(actions, -self.clip_actions, self.clip_actions)
         if self._use_fused():
             self.fused_physics_step(action_tensor)
         else:
@@ -232,12 +239,18 @@ class VecTask(Env):
             self.gym.fetch_results(self.sim, True)
         self.post_physics_step()
         self.control_steps += 1
-        # set to 1 only when the episode length is reached AND the env is being reset (vec_task.py:393-394)
-        self.timeout_buf = (self.progress_buf >= self.max_episode_length - 1) & (self.reset_buf != 0)
-        if self.dr_randomizations.get("observations", None):
-            self.obs_buf = self.dr_randomizations["observations"]["noise_lambda"](self.obs_buf)
-        self.extras["time_outs"] = self.timeout_buf.to(self.rl_device)
-        self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
+        fused_out, self._fused_outputs = self._fused_outputs, None
+        if fused_out is not None:
+            self.timeout_buf, obs = fused_out
+            self.extras["time_outs"] = self.timeout_buf.to(self.rl_device)
+            self.obs_dict["obs"] = obs.to(self.rl_device)
+        else:
+            # set to 1 only when the episode length is reached AND the env is being reset (vec_task.py:393-394)
+            self.timeout_buf = (self.progress_buf >= self.max_episode_length - 1) & (self.reset_buf != 0)
+            if self.dr_randomizations.get("observations", None):
+                self.obs_buf = self.dr_randomizations["observations"]["noise_lambda"](self.obs_buf)
+            self.extras["time_outs"] = self.timeout_buf.to(self.rl_device)
+            self.obs_dict["obs"] = torch.clamp(self.obs_buf, -self.clip_obs, self.clip_obs).to(self.rl_device)
         if self.num_states > 0:
             self.obs_dict["states"] = self.get_state()
         return self.obs_dict, self.rew_buf.to(self.rl_device), self.reset_buf.to(self.rl_device), self.extras

@@ -66,3 +66,35 @@ def test_sim_create_fails_cleanly_without_device():
 def test_topology_header_is_current():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_topologies.py"), "--check"])
     assert r.returncode == 0, "run tools/gen_topologies.py"
+
+
+def test_ctypes_struct_layouts_match_the_headers(tmp_path):
+    """Every ctypes mirror has the C struct's size and field offsets (gcc on include/*.h)."""
+    import shutil
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    from isaacgymenv_amd.isaacgym import _lib
+    from isaacgymenv_amd import gymtask
+    mirrors = {"gs_model_desc": _lib.GsModelDesc, "gs_sim_params": _lib.GsSimParams, "gs_pd_args": _lib.GsPdArgs,
+               "gt_torch_rand_plan": gymtask.GtTorchRandPlan, "gt_anymal_params": gymtask.GtAnymalParams,
+               "gt_anymal_buffers": gymtask.GtAnymalBuffers, "gt_anymal_reset_draws": gymtask.GtAnymalResetDraws}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gymsim.h"', '#include "gymtask.h"',
+             "int main(void) {"]
+    expect = []
+    for cname, py in mirrors.items():
+        lines.append(f'  printf("%zu\\n", sizeof({cname}));')
+        expect.append(C_sizeof(py))
+        for f in py._fields_:
+            lines.append(f'  printf("%zu\\n", offsetof({cname}, {f[0]}));')
+            expect.append(getattr(py, f[0]).offset)
+    lines.append("  return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got == expect
+
+
+def C_sizeof(py):
+    return ctypes.sizeof(py)

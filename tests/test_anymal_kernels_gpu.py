@@ -34,6 +34,7 @@ def test_fused_tail_kernels_match_reference_golden(monkeypatch):
     dev = "cuda:0"
     env = at.AnymalTerrain(copy.deepcopy(cfg), dev, dev, -1, True, False, False)
     assert env._kernels is not None, "GPU pipeline must use the fused tail kernels"
+    env._kernels.inkernel_rng = False  # draws come from the replayed CPU stream below
 
     # replay the reference's CPU RNG stream
     def cpu_rand_float(lower, upper, shape, device):
@@ -41,7 +42,12 @@ def test_fused_tail_kernels_match_reference_golden(monkeypatch):
 
     real_rand_like = torch.rand_like
     monkeypatch.setattr(at, "torch_rand_float", cpu_rand_float)
+    monkeypatch.setattr(at, "torch_rand_unit", lambda shape, device: torch.rand(*shape).to(device))
     monkeypatch.setattr(torch, "rand_like", lambda t: real_rand_like(t, device="cpu").to(t.device))
+
+    counts = []
+    real_wait = env._kernels.wait_reset_count
+    env._kernels.wait_reset_count = lambda: counts.append(real_wait()) or counts[-1]
 
     terms = [str(t) for t in d["terms"]]
     T = d["actions"].shape[0]
@@ -78,6 +84,14 @@ def test_fused_tail_kernels_match_reference_golden(monkeypatch):
         _close(np.stack([env.episode_sums[k].cpu().numpy() for k in terms]), d["episode_sums"][t],
                f"episode sums step {t}")
         _close(env.obs_buf.cpu().numpy(), d["obs"][t], f"obs step {t}")
+        # reset count from the post_a ballot, and VecTask's time_outs / obs clamp fused into post_b
+        assert counts[-1] == int(d["reset"][t].sum()), f"reset count step {t}"
+        rc = env._kernels.reset_count.tolist()
+        assert rc[0] == 0 and rc[1] == 0 and rc[2] == counts[-1], rc  # re-armed; device copy of the count
+        time_outs, obs_out = env._fused_outputs
+        env._fused_outputs = None
+        assert torch.equal(obs_out, torch.clamp(env.obs_buf, -env.clip_obs, env.clip_obs))
+        assert torch.equal(time_outs, (env.progress_buf >= env.max_episode_length - 1) & (env.reset_buf != 0))
         _close(env.base_lin_vel.cpu().numpy(), d["out_base_lin_vel"][t], f"base_lin_vel step {t}")
         _close(env.projected_gravity.cpu().numpy(), d["out_projected_gravity"][t], f"gravity step {t}")
         _close(env.root_states.cpu().numpy(), d["out_root"][t], f"root states step {t}")

@@ -101,7 +101,12 @@ def test_cartpole_matches_oracle():
 
 
 def test_team_and_lane_kernels_agree_on_random_states(monkeypatch):
-    """Both kernel forms from the same 1024 random states (incl. penetrating, airborne, tilted)."""
+    """Both kernel forms from the same 1024 random states (incl. penetrating, airborne, tilted).
+
+    The two forms sum the same terms in different orders (quad DPP reductions vs
+    serial loops); over 5 substeps of 4+1 PGS sweeps that rounding difference
+    moves velocities near the +-20 rad/s clamp by up to ~0.5 %, hence the
+    relative term on velocities.  Each form is pinned to the fp64 oracle above."""
     n = 1024
     art, flat = H.anymal()
     root, dof, tau, mu = H.anymal_states(n, seed=21, spread=2.0)
@@ -118,5 +123,5 @@ def test_team_and_lane_kernels_agree_on_random_states(monkeypatch):
     (r1, d1, c1), (r2, d2, c2) = out["lane"], out["team"]
     np.testing.assert_allclose(r2[:, :7], r1[:, :7], atol=1e-3)
     np.testing.assert_allclose(d2[:, :, 0], d1[:, :, 0], atol=1e-3)
-    np.testing.assert_allclose(r2[:, 7:], r1[:, 7:], atol=2e-2)
-    np.testing.assert_allclose(d2[:, :, 1], d1[:, :, 1], atol=5e-2)
+    np.testing.assert_allclose(r2[:, 7:], r1[:, 7:], atol=2e-2, rtol=1e-2)
+    np.testing.assert_allclose(d2[:, :, 1], d1[:, :, 1], atol=5e-2, rtol=1e-2)

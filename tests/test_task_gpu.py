@@ -74,14 +74,56 @@ def test_fused_step_equals_unfused_sequence(monkeypatch):
     for (o1, r1, d1, q1, x1), (o2, r2, d2, q2, x2) in zip(out["1"], out["0"]):
         # the fused kernel evaluates the PD torque with FMAs, the unfused path with separate torch
         # ops; that last-bit difference passes through the PGS friction clamp, so velocities agree
-        # to the solver's resolution (~1e-2 rad/s) while positions agree to ~1e-5.
+        # to the solver's resolution (~1e-2 rad/s) while positions agree to ~1e-4.
         assert torch.equal(d1, d2)
-        torch.testing.assert_close(q2[:, 0], q1[:, 0], rtol=0, atol=1e-4)
+        torch.testing.assert_close(q2[:, 0], q1[:, 0], rtol=0, atol=5e-4)
         torch.testing.assert_close(q2[:, 1], q1[:, 1], rtol=0, atol=2e-2)
-        torch.testing.assert_close(x2[:, :7], x1[:, :7], rtol=0, atol=1e-4)
+        torch.testing.assert_close(x2[:, :7], x1[:, :7], rtol=0, atol=5e-4)
         torch.testing.assert_close(x2[:, 7:], x1[:, 7:], rtol=0, atol=2e-2)
         torch.testing.assert_close(o2, o1, rtol=0, atol=2e-2)
         torch.testing.assert_close(r2, r1, rtol=1e-2, atol=1e-4)
+
+
+def test_kernel_tail_equals_torch_tail_across_resets(monkeypatch):
+    """The fused tail (post_a -> optimistic noise/post_b -> RNG rollback + reset_idx + post_b on
+    reset steps) against the reference's torch statements, same physics kernel and same CUDA
+    RNG stream, over 5-step episodes so that most steps reset someone."""
+    n = 256
+    env = _make("AnymalTerrain", n, monkeypatch, **{"task.env.learn.episodeLength_s": 0.1})
+    assert env.max_episode_length in (5, 6)
+    gen = torch.Generator(device="cuda:0").manual_seed(9)
+    acts = [2 * torch.rand((n, 12), device="cuda:0", generator=gen) - 1 for _ in range(12)]
+    env.step(acts[0])
+    snap = _snapshot(env)
+    kernels = env._kernels
+    out = {}
+    for mode in ("kernels", "torch"):
+        _restore(env, snap)
+        env._kernels = kernels if mode == "kernels" else None
+        env.extras.pop("episode", None)
+        res = []
+        for a in acts:
+            obs, rew, reset, extras = env.step(a)
+            ep = extras.get("episode")
+            res.append((obs["obs"].clone(), rew.clone(), reset.clone(), extras["time_outs"].clone(),
+                        None if ep is None else torch.stack([torch.as_tensor(v, device="cuda:0").float()
+                                                             for v in ep.values()]),
+                        env.root_states.clone()))
+            env.extras.pop("episode", None)
+        out[mode] = res
+    env._kernels = kernels
+    n_reset_steps = 0
+    for t, (a, b) in enumerate(zip(out["kernels"], out["torch"])):
+        assert torch.equal(a[2], b[2]), f"reset mask step {t}"
+        n_reset_steps += int(bool(a[2].any()))
+        assert torch.equal(a[3], b[3]), f"time_outs step {t}"
+        torch.testing.assert_close(a[0], b[0], rtol=1e-5, atol=1e-5, msg=f"obs step {t}")
+        torch.testing.assert_close(a[1], b[1], rtol=1e-5, atol=1e-6, msg=f"reward step {t}")
+        assert (a[4] is None) == (b[4] is None)
+        if a[4] is not None:
+            torch.testing.assert_close(a[4], b[4], rtol=1e-4, atol=1e-7, msg=f"episode extras step {t}")
+        torch.testing.assert_close(a[5], b[5], rtol=1e-5, atol=1e-5, msg=f"root states step {t}")
+    assert n_reset_steps >= 2
 
 
 def test_anymal_full_episode(monkeypatch):

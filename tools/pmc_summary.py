@@ -1,0 +1,92 @@
+"""Summarise rocprofv3 PMC passes for the physics kernel into profiles/pmc_pd_step.json.
+
+Usage (after two separate `rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE --kernel-trace` runs of bench.py):
+    python tools/pmc_summary.py --fetch <fetch counter_collection.csv> --write <write csv> \
+        --round 2 --num-envs 4096 [--copy-prefix profiles/r02]
+
+FETCH_SIZE / WRITE_SIZE are KB per dispatch; FETCH_SIZE is doubled on gfx950
+(MI355X_MICROARCH.md, HBM section: 128-B requests are tallied at 64 B).
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import os
+import re
+import shutil
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+KERNEL_KEY = "k_pd_step"
+
+
+def _rows(path, counter):
+    out = []
+    with open(path, newline="") as f:
+        for r in csv.DictReader(f):
+            r["Kernel"] = r.get("Kernel", r.get("Kernel_Name", ""))
+            if KERNEL_KEY in r["Kernel"] and r["Counter_Name"] == counter:
+                out.append(r)
+    if not out:
+        raise SystemExit(f"no {KERNEL_KEY} {counter} rows in {path}")
+    return out
+
+
+def _trim(src, dst):
+    """Keep only our kernels' rows (the rocprof CSV also lists torch's)."""
+    with open(src, newline="") as f, open(dst, "w", newline="") as g:
+        rd = csv.reader(f)
+        wr = csv.writer(g)
+        head = next(rd)
+        col = head.index("Kernel_Name") if "Kernel_Name" in head else head.index("Kernel")
+        wr.writerow(head)
+        for r in rd:
+            if any(k in r[col] for k in ("k_pd_step", "k_simulate", "k_post_", "k_reset", "k_refresh", "k_set_")):
+                wr.writerow(r)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--round", type=int, required=True)
+    ap.add_argument("--num-envs", type=int, default=4096)
+    ap.add_argument("--copy-prefix", default=None)
+    args = ap.parse_args()
+    import bench
+    fr = _rows(args.fetch, "FETCH_SIZE")
+    wr = _rows(args.write, "WRITE_SIZE")
+    fetch_kb = statistics.median(float(r["Counter_Value"]) for r in fr)
+    write_kb = statistics.median(float(r["Counter_Value"]) for r in wr)
+    scratch = int(fr[0]["Scratch_Size"])
+    hbm = (2.0 * fetch_kb + write_kb) * 1024.0
+    alg = bench.physics_kernel_bytes_per_env() * args.num_envs
+    out = {
+        "kernel": re.search(r"k_pd_step\w*<\w+>", fr[0]["Kernel"]).group(0) + " (gs_sim_pd_step)",
+        "num_envs": args.num_envs,
+        "round": args.round,
+        "counters": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, --kernel-trace",
+        "dispatches": len(fr),
+        "fetch_size_kb_per_launch": fetch_kb,
+        "write_size_kb_per_launch": write_kb,
+        "gfx950_correction": "FETCH_SIZE x2 (MI355X_MICROARCH.md HBM section: 128-B requests tallied at 64 B)",
+        "hbm_bytes_per_launch": hbm,
+        "algorithmic_bytes_per_launch": alg,
+        "scratch_bytes_per_lane": scratch,
+        "vgpr": int(fr[0]["VGPR_Count"]), "agpr": int(fr[0]["Accum_VGPR_Count"]),
+        "lds_bytes_per_block": int(fr[0]["LDS_Block_Size"]),
+    }
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "profiles", "pmc_pd_step.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    if args.copy_prefix:
+        _trim(args.fetch, args.copy_prefix + "_pmc_fetch_size.csv")
+        _trim(args.write, args.copy_prefix + "_pmc_write_size.csv")
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
