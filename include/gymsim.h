@@ -147,6 +147,10 @@ int gs_sim_kernel_variant(gs_sim *sim);
 int gs_sim_enable_timing(gs_sim *sim, int enable);
 float gs_sim_last_kernel_ms(gs_sim *sim);
 
+/* Profiling build only (libgymsim_prof.so, -DGS_PHASE_PROFILE): per-phase cycle sums of the
+ * lane-team kernel over all waves since the last reset (tools/phase_profile.py); -1 otherwise. */
+int gs_debug_phase_cycles(unsigned long long *out, int n, int reset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,9 +20,15 @@ ARCH = os.environ.get("GS_OFFLOAD_ARCH", "gfx950")
 LIBS = {
     "libgymsim.so": ["gs_physics.hip", "gs_team.hip", "gs_capi.hip"],
     "libgymtask.so": ["gt_anymal.hip"],
+    # phase-profiling build of the simulator (tools/phase_profile.py); never loaded by default
+    "libgymsim_prof.so": ["gs_physics.hip", "gs_team.hip", "gs_capi.hip"],
 }
 # the task kernels mirror torch's unfused elementwise arithmetic
-EXTRA_FLAGS = {"libgymtask.so": ["-ffp-contract=off"]}
+# -fno-slp-vectorize: the SLP vectorizer packs the scalar spatial algebra into v_pk_* pairs and
+# then spends ~1700 v_mov_b32 (and AGPR copies) arranging register pairs in the physics kernels
+SIM_FLAGS = ["-fno-slp-vectorize"]
+EXTRA_FLAGS = {"libgymtask.so": ["-ffp-contract=off"], "libgymsim.so": SIM_FLAGS,
+               "libgymsim_prof.so": SIM_FLAGS + ["-DGS_PHASE_PROFILE"]}
 HEADERS = ["gs_internal.h", "gs_topologies.h", "gs_math.h", "torch_philox.h"]
 
 
@@ -40,6 +46,7 @@ def _stale(out: str, srcs) -> bool:
     deps = [os.path.join(CSRC, s) for s in srcs] + [os.path.join(CSRC, h) for h in HEADERS]
     deps.append(os.path.join(os.path.dirname(HERE), "include", "gymsim.h"))
     deps.append(os.path.join(os.path.dirname(HERE), "include", "gymtask.h"))
+    deps.append(os.path.abspath(__file__))  # flags live here
     return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
 
 

@@ -19,11 +19,34 @@
 #include "gs_topologies.h"
 #include "gs_math.h"
 
+// Phase profiler (profiling build only, -DGS_PHASE_PROFILE -> libgymsim_prof.so): per-wave
+// s_memtime deltas per solver phase, summed over waves into gs_phase_cycles (gs_capi.hip).
+#ifdef GS_PHASE_PROFILE
+__device__ unsigned long long gs_phase_cycles[16];
+#define GS_PROF_DECL long long gs_t_ = clock64(); long long gs_acc_[16] = {0};
+#define GS_PROF(i) { const long long t_ = clock64(); gs_acc_[i] += t_ - gs_t_; gs_t_ = t_; }
+#define GS_PROF_COUNT(i, n) { gs_acc_[i] += (n); }
+#define GS_PROF_PARAM , long long &gs_t_, long long *gs_acc_
+#define GS_PROF_ARGS , gs_t_, gs_acc_
+#define GS_PROF_FLUSH                                                   \
+  if ((threadIdx.x & 63) == 0) {                                        \
+    for (int i_ = 0; i_ < 16; ++i_) atomicAdd(&gs_phase_cycles[i_], (unsigned long long)gs_acc_[i_]); \
+  }
+#else
+#define GS_PROF_DECL
+#define GS_PROF_PARAM
+#define GS_PROF_ARGS
+#define GS_PROF(i)
+#define GS_PROF_COUNT(i, n)
+#define GS_PROF_FLUSH
+#endif
+
 namespace {
 
 template <int CTRL>
 __device__ __forceinline__ float qperm(float x) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+  // bound_ctrl: quad_perm never reads out of range; it lets the DPP fold into the consuming VALU op
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
 }
 template <int CTRL>
 __device__ __forceinline__ int qperm_i(int x) {
@@ -63,18 +86,81 @@ struct CM {
   static constexpr int LANES = T::T_LANES;
 };
 
-// LDS slots of the contact rows: chain candidate rows (owner column), then root candidate rows (own column)
+// LDS row stride: one float per lane plus a pad, so the 4 lanes of a team reading 4 different slots
+// of one column land in 4 different banks
+constexpr int RW = GS_WAVE + 1;
+
+// LDS contact records, layout [slot][lane]: chain candidates in the owner lane's column, then root
+// candidates (replicated, every lane its own column).  A record holds everything a lane needs
+// to run the contact's three Gauss-Seidel rows without cross-lane traffic:
+//   Z rows (3 x [Zb 6 | Zc CL]) | c (3) | 1/G_rr (3) | G10 G20 G21 | target pos/vel phase | mu | active
+// where G = Z Z^T is the contact's 3x3 Delassus block (couples its rows within one GS pass).
 template <class T>
 struct RowSlots {
   static constexpr int CL = T::T_CL;
-  static constexpr int PER_ROW = 6 + CL + 2;  // Zb 6 | Zc CL | c | 1/d
-  static constexpr int CHAIN = 3 * PER_ROW * T::T_CC;
-  static constexpr int ROOT_PER_ROW = 6 + 2;
-  static constexpr int ROOT = 3 * ROOT_PER_ROW * (T::T_RC > 0 ? T::T_RC : 1);
+  // A Z row's 9 components (base 6 | chain 3) in PGS-owner order: lane l's three components
+  // (l, l+4, 8 or a zero pad) are consecutive slots, so a lane reads them with paired LDS loads
+  // and the four lanes of a team hit four different banks (stride RW).
+  static constexpr int ZROW = 12;
+  static constexpr int RZROW = 12;
+  __device__ static constexpr int zslot(int comp) { return comp < 4 ? 3 * comp : comp < 8 ? 3 * (comp - 4) + 1 : 2; }
+  static constexpr int C_C = 3 * ZROW, C_DI = C_C + 3, C_G = C_DI + 3, C_TP = C_G + 3, C_TV = C_TP + 1,
+                       C_MU = C_TV + 1, C_ACT = C_MU + 1, PER_CONTACT = C_ACT + 1;
+  static constexpr int R_C = 3 * RZROW, R_DI = R_C + 3, R_G = R_DI + 3, R_TP = R_G + 3, R_TV = R_TP + 1,
+                       R_MU = R_TV + 1, PER_ROOT = R_MU + 1;
+  static constexpr int CHAIN = PER_CONTACT * T::T_CC;
+  static constexpr int ROOT = PER_ROOT * (T::T_RC > 0 ? T::T_RC : 1);
   static constexpr int TOTAL = CHAIN + ROOT;
-  __device__ static constexpr int chain(int j, int rr) { return (j * 3 + rr) * PER_ROW; }
-  __device__ static constexpr int root(int j, int rr) { return CHAIN + (j * 3 + rr) * ROOT_PER_ROW; }
+  __device__ static constexpr int chain(int j) { return j * PER_CONTACT; }
+  __device__ static constexpr int chain_row(int j, int rr) { return j * PER_CONTACT + rr * ZROW; }
+  __device__ static constexpr int root(int j) { return CHAIN + j * PER_ROOT; }
 };
+
+// x[lc][k] for the lane's own chain lc (runtime) out of a replicated [NCH][K] register array
+template <int NCH, int K>
+__device__ __forceinline__ float sel_chain(const float (&x)[NCH][K], int lc, int k) {
+  float v = x[0][k];
+#pragma unroll
+  for (int c = 1; c < NCH; ++c) v = lc == c ? x[c][k] : v;
+  return v;
+}
+
+// Distributed PGS velocity -> replicated base w (6) and this lane's chain w (3).  Owners: base b<4
+// lane b (wA), base 4,5 lanes 0,1 (wBb), chain c comps 0,1 lanes 2,3 (wB[c]), comp 2 lane 0 (wC[c]).
+template <class T>
+__device__ __forceinline__ void gather_w(int lc, float wA, float wBb, const float (&wB)[T::T_NCH],
+                                         const float (&wC)[T::T_NCH], float* wb, float* wc) {
+  wb[0] = bcast(wA, 0); wb[1] = bcast(wA, 1); wb[2] = bcast(wA, 2); wb[3] = bcast(wA, 3);
+  wb[4] = bcast(wBb, 0); wb[5] = bcast(wBb, 1);
+  wc[0] = wc[1] = wc[2] = 0.f;
+#pragma unroll
+  for (int c = 0; c < T::T_NCH; ++c) {
+    const float c0 = bcast(wB[c], 2), c1 = bcast(wB[c], 3), c2 = bcast(wC[c], 0);
+    wc[0] = lc == c ? c0 : wc[0];
+    wc[1] = lc == c ? c1 : wc[1];
+    wc[2] = lc == c ? c2 : wc[2];
+  }
+}
+
+// One contact's three projected Gauss-Seidel rows (normal, friction x2, box friction cone) given
+// u = c + Z w before the pass; the in-pass coupling of its rows goes through G.  Returns the
+// impulse increments and updates lam.  Same iterate as three scalar GS rows.
+__device__ __forceinline__ void contact_block(float u0, float u1, float u2, float di0, float di1, float di2,
+                                              float g10, float g20, float g21, float target, float mu,
+                                              float* lam, float& dl0, float& dl1, float& dl2) {
+  const float n0 = fmaxf(lam[0] + (target - u0) * di0, 0.f);
+  dl0 = n0 - lam[0];
+  lam[0] = n0;
+  const float lim = mu * n0;
+  u1 += g10 * dl0;
+  const float n1 = clampf(lam[1] - u1 * di1, -lim, lim);
+  dl1 = n1 - lam[1];
+  lam[1] = n1;
+  u2 += g20 * dl0 + g21 * dl1;
+  const float n2 = clampf(lam[2] - u2 * di2, -lim, lim);
+  dl2 = n2 - lam[2];
+  lam[2] = n2;
+}
 
 template <class T>
 struct TeamState {
@@ -185,7 +271,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
                                              const DevParams& P, TeamState<T>& s, const float* tau,
                                              const float* __restrict__ mu_g, int N, int e, int lc,
                                              float* __restrict__ rows_own, const float* __restrict__ rows_team,
-                                             float* __restrict__ cf_soa, bool collect) {
+                                             float* __restrict__ cf_soa, bool collect GS_PROF_PARAM) {
   constexpr int CL = T::T_CL, CC = T::T_CC, RC = T::T_RC, NCH = T::T_NCH, LN = T::T_LANES;
   static_assert(NCH == LN && LN == 4, "lane teams are DPP quads with one chain per lane");
   using C = CM<T>;
@@ -301,9 +387,9 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
 #pragma unroll
           for (int rr = 0; rr < 3; ++rr) {
             const int ax3 = (rr == 0) ? 2 : (rr == 1 ? 0 : 1);
-            float* row = rows_own + RS::chain(j, rr) * GS_WAVE;
+            float* row = rows_own + RS::chain_row(j, rr) * RW;
 #pragma unroll
-            for (int b = 0; b < 6; ++b) row[b * GS_WAVE] = base_jac(xc, ax3, b);
+            for (int b = 0; b < 6; ++b) row[RS::zslot(b) * RW] = base_jac(xc, ax3, b);
 #pragma unroll
             for (int kk = 0; kk < CL; ++kk) {
               float v = 0.f;
@@ -312,7 +398,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
                 cross3(S[kk], xc, tt);
                 v = S[kk][3 + ax3] + tt[ax3];
               }
-              row[(6 + kk) * GS_WAVE] = v;
+              row[RS::zslot(6 + kk) * RW] = v;
             }
           }
         }
@@ -320,6 +406,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     }
   }
 
+  GS_PROF(0)  // root + chain forward pass + contact Jacobians
   // ================= chain backward pass: composite inertia / force, bias, chain rows of M
   float Mcc[CL][CL], Mcb[CL][6], biasc[CL];
 #pragma unroll
@@ -421,6 +508,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
 #pragma unroll
   for (int k = 0; k < 6; ++k) sDb[k] = rsqrtf(Mbb[k][k]);
 
+  GS_PROF(1)  // backward pass, team sums, L^T D L
   // ================= free velocity
   float nufc[CL], nufb[6];
   {
@@ -474,21 +562,26 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     nufb[3] += h * wxp[0]; nufb[4] += h * wxp[1]; nufb[5] += h * wxp[2];
   }
 
-  // ================= contact rows: scaled Z = (L^-T J^T) D^-1/2, c = J nu_f, 1/diag
-  // chain candidates (owner lane)
+  GS_PROF(2)  // free velocity
+  // ================= contact records: scaled Z = (L^-T J^T) D^-1/2, c = J nu_f, Delassus block
+  const float inv_h = 1.f / h;
+  // chain candidates (owner lane writes its column; the whole team reads it in the sweeps)
 #pragma unroll
   for (int j = 0; j < CC; ++j) {
+    float* rec = rows_own + RS::chain(j) * RW;
+    rec[RS::C_ACT * RW] = act[j] ? 1.f : 0.f;
     if (act[j]) {
       const int kb = T::T_ccb[j];
+      float zr[3][6 + CL];
 #pragma unroll
       for (int rr = 0; rr < 3; ++rr) {
-        float* row = rows_own + RS::chain(j, rr) * GS_WAVE;
+        float* row = rows_own + RS::chain_row(j, rr) * RW;
         float zb[6], zc[CL];
         float cj = 0.f;
 #pragma unroll
-        for (int b = 0; b < 6; ++b) { zb[b] = row[b * GS_WAVE]; cj += zb[b] * nufb[b]; }
+        for (int b = 0; b < 6; ++b) { zb[b] = row[RS::zslot(b) * RW]; cj += zb[b] * nufb[b]; }
 #pragma unroll
-        for (int k = 0; k < CL; ++k) { zc[k] = row[(6 + k) * GS_WAVE]; if (k <= kb) cj += zc[k] * nufc[k]; }
+        for (int k = 0; k < CL; ++k) { zc[k] = row[RS::zslot(6 + k) * RW]; if (k <= kb) cj += zc[k] * nufc[k]; }
         // leaf -> root: chain nodes kb..0 then base 5..0
 #pragma unroll
         for (int kk = 0; kk < CL; ++kk) {
@@ -508,21 +601,44 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         }
         float d = 0.f;
 #pragma unroll
-        for (int b = 0; b < 6; ++b) { zb[b] *= sDb[b]; d += zb[b] * zb[b]; row[b * GS_WAVE] = zb[b]; }
+        for (int b = 0; b < 6; ++b) {
+          zb[b] *= sDb[b];
+          d += zb[b] * zb[b];
+          row[RS::zslot(b) * RW] = zb[b];
+          zr[rr][b] = zb[b];
+        }
 #pragma unroll
         for (int k = 0; k < CL; ++k) {
           const float z = k <= kb ? zc[k] * sDc[k] : 0.f;
           d += z * z;
-          row[(6 + k) * GS_WAVE] = z;
+          row[RS::zslot(6 + k) * RW] = z;
+          zr[rr][6 + k] = z;
         }
-        row[(6 + CL) * GS_WAVE] = cj;
-        row[(7 + CL) * GS_WAVE] = 1.f / d;
+        row[5 * RW] = 0.f;  // zero pads read as lanes 1-3's third component
+        row[8 * RW] = 0.f;
+        row[11 * RW] = 0.f;
+        rec[(RS::C_C + rr) * RW] = cj;
+        rec[(RS::C_DI + rr) * RW] = 1.f / d;
       }
+      float g10 = 0.f, g20 = 0.f, g21 = 0.f;
+#pragma unroll
+      for (int f = 0; f < 6 + CL; ++f) {
+        g10 += zr[1][f] * zr[0][f];
+        g20 += zr[2][f] * zr[0][f];
+        g21 += zr[2][f] * zr[1][f];
+      }
+      rec[(RS::C_G + 0) * RW] = g10;
+      rec[(RS::C_G + 1) * RW] = g20;
+      rec[(RS::C_G + 2) * RW] = g21;
+      const float sc = sep[j];
+      const float tgt = -sc * inv_h;
+      rec[RS::C_TP * RW] = sc < 0.f ? fminf(tgt, P.max_depen_vel) : tgt;
+      rec[RS::C_TV * RW] = sc < 0.f ? 0.f : tgt;
+      rec[RS::C_MU * RW] = cmu[j];
     }
   }
   // root candidates (replicated in every lane, own column)
   bool ract[RC > 0 ? RC : 1];
-  float rsep[RC > 0 ? RC : 1], rmu[RC > 0 ? RC : 1];
 #pragma unroll
   for (int j = 0; j < RC; ++j) {
     float x[3];
@@ -530,14 +646,13 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     const float r = M->cradius[j];
     const float dist = s.p[2] + x[2] - r;
     ract[j] = P.has_ground && (dist < P.contact_offset);
-    rsep[j] = dist - P.rest_offset;
-    rmu[j] = 0.5f * (mu_g[T::T_rcs[j] * N + e] + P.ground_mu);
     if (ract[j]) {
+      float* rec = rows_own + RS::root(j) * RW;
       const float xc[3] = {x[0], x[1], x[2] - r};
+      float zr[3][6];
 #pragma unroll
       for (int rr = 0; rr < 3; ++rr) {
         const int ax3 = (rr == 0) ? 2 : (rr == 1 ? 0 : 1);
-        float* row = rows_own + RS::root(j, rr) * GS_WAVE;
         float zb[6], cj = 0.f;
 #pragma unroll
         for (int b = 0; b < 6; ++b) { zb[b] = base_jac(xc, ax3, b); cj += zb[b] * nufb[b]; }
@@ -549,110 +664,132 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         }
         float d = 0.f;
 #pragma unroll
-        for (int b = 0; b < 6; ++b) { zb[b] *= sDb[b]; d += zb[b] * zb[b]; row[b * GS_WAVE] = zb[b]; }
-        row[6 * GS_WAVE] = cj;
-        row[7 * GS_WAVE] = 1.f / d;
+        for (int b = 0; b < 6; ++b) {
+          zb[b] *= sDb[b];
+          d += zb[b] * zb[b];
+          rec[(rr * RS::RZROW + RS::zslot(b)) * RW] = zb[b];
+          zr[rr][b] = zb[b];
+        }
+        rec[(rr * RS::RZROW + RS::zslot(6)) * RW] = 0.f;  // lanes 2, 3: second component is chain-only
+        rec[(rr * RS::RZROW + RS::zslot(7)) * RW] = 0.f;
+        rec[(RS::R_C + rr) * RW] = cj;
+        rec[(RS::R_DI + rr) * RW] = 1.f / d;
       }
+      float g10 = 0.f, g20 = 0.f, g21 = 0.f;
+#pragma unroll
+      for (int f = 0; f < 6; ++f) {
+        g10 += zr[1][f] * zr[0][f];
+        g20 += zr[2][f] * zr[0][f];
+        g21 += zr[2][f] * zr[1][f];
+      }
+      rec[(RS::R_G + 0) * RW] = g10;
+      rec[(RS::R_G + 1) * RW] = g20;
+      rec[(RS::R_G + 2) * RW] = g21;
+      const float sc = dist - P.rest_offset;
+      const float tgt = -sc * inv_h;
+      rec[RS::R_TP * RW] = sc < 0.f ? fminf(tgt, P.max_depen_vel) : tgt;
+      rec[RS::R_TV * RW] = sc < 0.f ? 0.f : tgt;
+      rec[RS::R_MU * RW] = 0.5f * (mu_g[T::T_rcs[j] * N + e] + P.ground_mu);
     }
   }
+  // the sweeps read other lanes' records: make this wave's LDS writes visible (one-wave block)
+  __syncthreads();
 
-  // ================= projected Gauss-Seidel, global row order: root candidates, chain 0, 1, ...
-  float wb[6], wc[CL], wbp[6], wcp[CL];
-  float lamc[CC][3], lamr[RC > 0 ? RC : 1][3];
+  GS_PROF(3)  // contact records
+  // ================= projected Gauss-Seidel, global contact order: root candidates, chain 0, 1, ...
+  // The 9 velocity components a chain contact row touches (base 6 | its chain's 3) are spread over
+  // the team: lane l owns components l, l+4 and (lane 0 only) 8, i.e. base l, base 4+l / chain
+  // comp l-2, chain comp 2.  Each lane forms its partial of the 3 rows' u = c + Z w, a DPP quad
+  // sum completes them (bit-identical in the 4 lanes), the 3-row projection through the
+  // contact's Delassus couplings runs replicated, and each lane updates only what it owns.
+  static_assert(CL == 3, "component distribution assumes 3-dof chains");
+  const bool low = lc < 2;            // component l+4 is a base component (else chain comp l-2)
+  float wA = 0.f, wBb = 0.f, wB[NCH], wC[NCH];
 #pragma unroll
-  for (int b = 0; b < 6; ++b) wb[b] = 0.f;
+  for (int c = 0; c < NCH; ++c) wB[c] = wC[c] = 0.f;
+  float lamc[NCH][CC][3], lamr[RC > 0 ? RC : 1][3];
 #pragma unroll
-  for (int k = 0; k < CL; ++k) wc[k] = 0.f;
+  for (int c = 0; c < NCH; ++c)
 #pragma unroll
-  for (int j = 0; j < CC; ++j) lamc[j][0] = lamc[j][1] = lamc[j][2] = 0.f;
+    for (int j = 0; j < CC; ++j) lamc[c][j][0] = lamc[c][j][1] = lamc[c][j][2] = 0.f;
 #pragma unroll
   for (int j = 0; j < RC; ++j) lamr[j][0] = lamr[j][1] = lamr[j][2] = 0.f;
-  const float inv_h = 1.f / h;
+  float wbp[6], wcp[CL];
   const int iters = P.pos_iters + P.vel_iters;
   for (int it = 0; it < iters; ++it) {
-    const bool pos_phase = it < P.pos_iters;
-    // root candidates: every lane runs the identical update
+    const int tsel = it < P.pos_iters ? RS::C_TP : RS::C_TV;
+    const int rsel = it < P.pos_iters ? RS::R_TP : RS::R_TV;
 #pragma unroll
     for (int j = 0; j < RC; ++j) {
       if (ract[j]) {
-        float target = -rsep[j] * inv_h;
-        if (rsep[j] < 0.f) target = pos_phase ? fminf(target, P.max_depen_vel) : 0.f;
+        const float* rec = rows_own + RS::root(j) * RW;
+        const float* recl = rec + 3 * lc * RW;
+        float za[3], zb2[3], u[3];
 #pragma unroll
         for (int rr = 0; rr < 3; ++rr) {
-          const float* row = rows_own + RS::root(j, rr) * GS_WAVE;
-          float z[6], u = row[6 * GS_WAVE];
-#pragma unroll
-          for (int b = 0; b < 6; ++b) { z[b] = row[b * GS_WAVE]; u += z[b] * wb[b]; }
-          const float dinv = row[7 * GS_WAVE];
-          float nl;
-          if (rr == 0) {
-            nl = fmaxf(lamr[j][0] + (target - u) * dinv, 0.f);
-          } else {
-            const float lim = rmu[j] * lamr[j][0];
-            nl = clampf(lamr[j][rr] - u * dinv, -lim, lim);
-          }
-          const float dl = nl - lamr[j][rr];
-          lamr[j][rr] = nl;
-#pragma unroll
-          for (int b = 0; b < 6; ++b) wb[b] += z[b] * dl;
+          za[rr] = recl[(rr * RS::RZROW) * RW];
+          zb2[rr] = recl[(rr * RS::RZROW + 1) * RW];
+          u[rr] = rec[(RS::R_C + rr) * RW] + quad_sum(za[rr] * wA + zb2[rr] * wBb);
         }
+        float dl0, dl1, dl2;
+        contact_block(u[0], u[1], u[2], rec[RS::R_DI * RW], rec[(RS::R_DI + 1) * RW], rec[(RS::R_DI + 2) * RW],
+                      rec[RS::R_G * RW], rec[(RS::R_G + 1) * RW], rec[(RS::R_G + 2) * RW], rec[rsel * RW],
+                      rec[RS::R_MU * RW], lamr[j], dl0, dl1, dl2);
+        wA += za[0] * dl0 + za[1] * dl1 + za[2] * dl2;
+        wBb += zb2[0] * dl0 + zb2[1] * dl1 + zb2[2] * dl2;  // lanes 2, 3 read the zero pads
       }
     }
-    // chain candidates: owner lane cc computes the impulse, the team applies it to the shared base
 #pragma unroll
     for (int cc = 0; cc < NCH; ++cc) {
-      const bool owner = lc == cc;
       const float* col = rows_team + cc;
 #pragma unroll
       for (int j = 0; j < CC; ++j) {
-        const int a_o = bcast_i(act[j] ? 1 : 0, cc);
+        const float* rec = col + RS::chain(j) * RW;
+        const bool a_o = rec[RS::C_ACT * RW] != 0.f;
+#ifdef GS_PHASE_PROFILE
+        if (__ballot(a_o) != 0ull) GS_PROF_COUNT(8, 1)  // chain contacts the wave executes
+#endif
         if (a_o) {
-          const float sc = sep[j];
-          float target = -sc * inv_h;
-          if (sc < 0.f) target = pos_phase ? fminf(target, P.max_depen_vel) : 0.f;
+          const float wBv = low ? wBb : wB[cc];
+          const float* recl = rec + 3 * lc * RW;
+          float za[3], zb2[3], zc2[3], u[3];
 #pragma unroll
           for (int rr = 0; rr < 3; ++rr) {
-            const float* row = col + RS::chain(j, rr) * GS_WAVE;
-            float zb[6], zc[CL], u = row[(6 + CL) * GS_WAVE];
-#pragma unroll
-            for (int b = 0; b < 6; ++b) { zb[b] = row[b * GS_WAVE]; u += zb[b] * wb[b]; }
-#pragma unroll
-            for (int k = 0; k < CL; ++k) { zc[k] = row[(6 + k) * GS_WAVE]; u += zc[k] * wc[k]; }
-            const float dinv = row[(7 + CL) * GS_WAVE];
-            float nl;
-            if (rr == 0) {
-              nl = fmaxf(lamc[j][0] + (target - u) * dinv, 0.f);
-            } else {
-              const float lim = cmu[j] * lamc[j][0];
-              nl = clampf(lamc[j][rr] - u * dinv, -lim, lim);
-            }
-            const float dl_own = nl - lamc[j][rr];
-            if (owner) lamc[j][rr] = nl;
-            const float dl = bcast(dl_own, cc);
-#pragma unroll
-            for (int b = 0; b < 6; ++b) wb[b] += zb[b] * dl;
-            if (owner) {
-#pragma unroll
-              for (int k = 0; k < CL; ++k) wc[k] += zc[k] * dl;
-            }
+            const float* row = recl + rr * RS::ZROW * RW;
+            za[rr] = row[0];
+            zb2[rr] = row[RW];
+            zc2[rr] = row[2 * RW];
+            u[rr] = rec[(RS::C_C + rr) * RW] + quad_sum(za[rr] * wA + zb2[rr] * wBv + zc2[rr] * wC[cc]);
           }
+          float dl0, dl1, dl2;
+          contact_block(u[0], u[1], u[2], rec[RS::C_DI * RW], rec[(RS::C_DI + 1) * RW], rec[(RS::C_DI + 2) * RW],
+                        rec[RS::C_G * RW], rec[(RS::C_G + 1) * RW], rec[(RS::C_G + 2) * RW], rec[tsel * RW],
+                        rec[RS::C_MU * RW], lamc[cc][j], dl0, dl1, dl2);
+          wA += za[0] * dl0 + za[1] * dl1 + za[2] * dl2;
+          const float nB = wBv + (zb2[0] * dl0 + zb2[1] * dl1 + zb2[2] * dl2);
+          wBb = low ? nB : wBb;
+          wB[cc] = low ? wB[cc] : nB;
+          wC[cc] += zc2[0] * dl0 + zc2[1] * dl1 + zc2[2] * dl2;
         }
       }
     }
-    if (it == P.pos_iters - 1) {
-#pragma unroll
-      for (int b = 0; b < 6; ++b) wbp[b] = wb[b];
-#pragma unroll
-      for (int k = 0; k < CL; ++k) wcp[k] = wc[k];
-    }
+#ifdef GS_PHASE_PROFILE
+    for (int j = 0; j < RC; ++j)
+      if (__ballot(ract[j]) != 0ull) GS_PROF_COUNT(9, 1)  // root contacts the wave executes
+#endif
+    if (it == P.pos_iters - 1) gather_w<T>(lc, wA, wBb, wB, wC, wbp, wcp);
   }
+  float wb[6], wc[CL];
+  gather_w<T>(lc, wA, wBb, wB, wC, wb, wc);
   if (P.pos_iters <= 0) {
 #pragma unroll
     for (int b = 0; b < 6; ++b) wbp[b] = wb[b];
 #pragma unroll
     for (int k = 0; k < CL; ++k) wcp[k] = wc[k];
   }
+  __syncthreads();  // the next substep rewrites the records other lanes just read
 
+  GS_PROF(4)  // PGS
   // ================= dnu = L^-1 D^-1/2 w (base first, then the chain)
   float nunb[6], nupb[6], nunc[CL], nupc[CL];
 #pragma unroll
@@ -712,9 +849,16 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
 #pragma unroll
       for (int j = 0; j < CC; ++j) {
         if (T::T_ccb[j] == k) {
-          f0 += lamc[j][1] * inv_h;
-          f1 += lamc[j][2] * inv_h;
-          f2 += lamc[j][0] * inv_h;
+          float l0 = lamc[0][j][0], l1 = lamc[0][j][1], l2 = lamc[0][j][2];
+#pragma unroll
+          for (int c = 1; c < NCH; ++c) {
+            l0 = lc == c ? lamc[c][j][0] : l0;
+            l1 = lc == c ? lamc[c][j][1] : l1;
+            l2 = lc == c ? lamc[c][j][2] : l2;
+          }
+          f0 += l1 * inv_h;
+          f1 += l2 * inv_h;
+          f2 += l0 * inv_h;
         }
       }
       const int b = 1 + lc * CL + k;
@@ -735,6 +879,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       cf_soa[2 * N + e] = f2;
     }
   }
+  GS_PROF(5)  // back-substitution + integrate + contact forces
 }
 
 template <class T>
@@ -753,7 +898,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel*
                                                                  SimBuffers B, const float* __restrict__ tau_aos) {
   constexpr int LN = T::T_LANES, CL = T::T_CL, ND = T::ND;
   __shared__ float mdl[CM<T>::NP * LN];
-  __shared__ float rows[RowSlots<T>::TOTAL * GS_WAVE];
+  __shared__ float rows[RowSlots<T>::TOTAL * RW];
   stage_chain_model<T>(M, mdl);
   __syncthreads();
   const int lc = threadIdx.x & (LN - 1);
@@ -767,11 +912,13 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel*
   for (int k = 0; k < CL; ++k) tau[k] = tau_aos ? tau_aos[(size_t)e * ND + lc * CL + k] : 0.f;
   float* own = rows + threadIdx.x;
   const float* team = rows + (threadIdx.x & ~(LN - 1));
+  GS_PROF_DECL
   for (int sstep = 0; sstep < P.substeps; ++sstep) {
     const bool last = (sstep == P.substeps - 1) && P.collect;
-    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last);
+    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last GS_PROF_ARGS);
   }
   team_store<T>(B.state, N, e, lc, s);
+  GS_PROF_FLUSH
 }
 
 template <class T>
@@ -779,7 +926,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
                                                                 SimBuffers B, PdDev A) {
   constexpr int LN = T::T_LANES, CL = T::T_CL, ND = T::ND, NB = T::NB;
   __shared__ float mdl[CM<T>::NP * LN];
-  __shared__ float rows[RowSlots<T>::TOTAL * GS_WAVE];
+  __shared__ float rows[RowSlots<T>::TOTAL * RW];
   stage_chain_model<T>(M, mdl);
   __syncthreads();
   const int lc = threadIdx.x & (LN - 1);
@@ -795,6 +942,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
   const int n_pd = A.decimation * sub;
   const int total = (A.decimation + A.extra) * sub;
   const size_t d0 = (size_t)e * ND + lc * CL;  // this lane's first dof in the AoS tensors
+  GS_PROF_DECL
   for (int it = 0; it < total; ++it) {
     if (it < n_pd && (it % sub) == 0) {
       const bool first = it == 0;
@@ -807,7 +955,8 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
       }
     }
     const bool last = ((it % sub) == sub - 1) && P.collect;
-    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last);
+    GS_PROF(6)  // PD torque
+    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last GS_PROF_ARGS);
     if (it == n_pd - 1 && A.dof_out) {
 #pragma unroll
       for (int k = 0; k < CL; ++k) {
@@ -844,6 +993,8 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
       for (int f = 0; f < 3; ++f) A.cf_out[((size_t)e * NB) * 3 + f] = B.cf[f * N + e];
     }
   }
+  GS_PROF(7)  // outputs
+  GS_PROF_FLUSH
 }
 
 }  // namespace
@@ -875,3 +1026,20 @@ hipError_t launch_pd_team(const DevModel* M, const DevParams& P, const SimBuffer
 #define GS_TEAM_ENTRY(T, SIG) {SIG, T::HAS_TEAM ? &launch_sim_team<T> : nullptr, T::HAS_TEAM ? &launch_pd_team<T> : nullptr},
 TeamEntry g_team_kernels[] = {GS_FOR_EACH_TOPOLOGY(GS_TEAM_ENTRY)};
 const int g_num_team_kernels = sizeof(g_team_kernels) / sizeof(g_team_kernels[0]);
+
+// Phase profile readout (include/gymsim.h); -1 outside the profiling build.
+extern "C" int gs_debug_phase_cycles(unsigned long long* out, int n, int reset) {
+#ifdef GS_PHASE_PROFILE
+  if (!out || n <= 0 || n > 16) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gs_phase_cycles), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(gs_phase_cycles), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+#else
+  (void)out; (void)n; (void)reset;
+  return -1;
+#endif
+}

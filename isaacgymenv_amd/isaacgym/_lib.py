@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_HERE, "_lib", "libgymsim.so")
+# GS_LIBGYMSIM=libgymsim_prof.so selects the phase-profiling build (tools/phase_profile.py)
+LIB_PATH = os.path.join(_HERE, "_lib", os.environ.get("GS_LIBGYMSIM", "libgymsim.so"))
 
 
 class GsModelDesc(C.Structure):
@@ -66,6 +67,7 @@ def lib():
             "gs_sim_kernel_variant": (i, [vp]),
             "gs_sim_enable_timing": (i, [vp, i]),
             "gs_sim_last_kernel_ms": (f, [vp]),
+            "gs_debug_phase_cycles": (i, [vp, i, i]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -84,7 +86,7 @@ EXPORTED_SYMBOLS = [
     "gs_abi_version", "gs_last_error", "gs_topology_supported", "gs_sim_create", "gs_sim_destroy",
     "gs_sim_add_ground", "gs_sim_set_model", "gs_sim_prepare", "gs_sim_simulate", "gs_sim_refresh_root",
     "gs_sim_refresh_dof", "gs_sim_refresh_contact", "gs_sim_set_root", "gs_sim_set_dof", "gs_sim_pd_step",
-    "gs_sim_kernel_variant", "gs_sim_enable_timing", "gs_sim_last_kernel_ms",
+    "gs_sim_kernel_variant", "gs_sim_enable_timing", "gs_sim_last_kernel_ms", "gs_debug_phase_cycles",
 ]
 
 

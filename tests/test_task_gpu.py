@@ -77,9 +77,9 @@ def test_fused_step_equals_unfused_sequence(monkeypatch):
         # to the solver's resolution (~1e-2 rad/s) while positions agree to ~1e-4.
         assert torch.equal(d1, d2)
         torch.testing.assert_close(q2[:, 0], q1[:, 0], rtol=0, atol=5e-4)
-        torch.testing.assert_close(q2[:, 1], q1[:, 1], rtol=0, atol=2e-2)
+        torch.testing.assert_close(q2[:, 1], q1[:, 1], rtol=1e-2, atol=2e-2)
         torch.testing.assert_close(x2[:, :7], x1[:, :7], rtol=0, atol=5e-4)
-        torch.testing.assert_close(x2[:, 7:], x1[:, 7:], rtol=0, atol=2e-2)
+        torch.testing.assert_close(x2[:, 7:], x1[:, 7:], rtol=1e-2, atol=2e-2)
         torch.testing.assert_close(o2, o1, rtol=0, atol=2e-2)
         torch.testing.assert_close(r2, r1, rtol=1e-2, atol=1e-4)
 

@@ -1,0 +1,56 @@
+"""Per-phase cycle breakdown of the lane-team physics kernel (profiling build).
+
+    python -m isaacgymenv_amd.build && python tools/phase_profile.py [--steps 100]
+
+Loads libgymsim_prof.so (-DGS_PHASE_PROFILE) instead of libgymsim.so, runs AnymalTerrain
+steps and prints, per kernel launch and wave, the s_memtime cycles of each solver phase and the
+number of contacts each wave executes in the PGS sweeps (wave-uniform control flow: a contact
+costs a wave its full latency if ANY of its 16 envs has it active).
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+os.environ["GS_LIBGYMSIM"] = "libgymsim_prof.so"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+PHASES = ["forward pass + contact Jacobians", "backward pass + L^T D L", "free velocity", "contact rows (Z, c)",
+          "PGS sweeps", "back-substitution + integrate", "PD torque", "kernel outputs"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--num-envs", type=int, default=4096)
+    a = ap.parse_args()
+    import torch
+    import isaacgymenvs
+    from isaacgymenv_amd.isaacgym import _lib
+    L = _lib.lib()
+    env = isaacgymenvs.make(seed=42, task="AnymalTerrain", num_envs=a.num_envs, sim_device="cuda:0",
+                            rl_device="cuda:0", headless=True, force_render=False)
+    N, A = env.num_envs, env.num_actions
+    pool = torch.empty((64, N, A), device="cuda:0").uniform_(-1, 1)
+    for i in range(a.warmup):
+        env.step(pool[i % 64])
+    buf = (C.c_ulonglong * 16)()
+    assert L.gs_debug_phase_cycles(buf, 16, 1) == 0, "not the profiling build"
+    for i in range(a.steps):
+        env.step(pool[i % 64])
+    assert L.gs_debug_phase_cycles(buf, 16, 1) == 0
+    waves = (N * 4 + 63) // 64
+    substeps = 5
+    per = [buf[i] / (a.steps * waves) for i in range(16)]
+    total = sum(per[:8])
+    print(f"cycles per launch per wave (s_memtime), {waves} waves, {a.steps} launches:")
+    for i, name in enumerate(PHASES):
+        print(f"  {name:36s} {per[i]:10.0f}  {100 * per[i] / total:5.1f} %")
+    print(f"  {'total':36s} {total:10.0f}")
+    print(f"chain contacts executed per wave per PGS sweep: {per[8] / (substeps * 5):.2f} of 12")
+    print(f"root contacts executed per wave per PGS sweep:  {per[9] / (substeps * 5):.2f} of 2")
+
+
+if __name__ == "__main__":
+    main()
