@@ -93,8 +93,11 @@ constexpr int RW = GS_WAVE + 1;
 // LDS contact records, layout [slot][lane]: chain candidates in the owner lane's column, then root
 // candidates (replicated, every lane its own column).  A record holds everything a lane needs
 // to run the contact's three Gauss-Seidel rows without cross-lane traffic:
-//   Z rows (3 x [Zb 6 | Zc CL]) | c (3) | 1/G_rr (3) | G10 G20 G21 | target pos/vel phase | mu | active
-// where G = Z Z^T is the contact's 3x3 Delassus block (couples its rows within one GS pass).
+//   Z rows (3 x [Zb 6 | Zc CL]) | c (3) | 1/G_rr (3) | G10/G11 G20/G22 G21/G22 | target/G00 (pos, vel
+//   phase) | mu | active
+// where G = Z Z^T is the contact's 3x3 Delassus block (couples its rows within one GS pass); the
+// couplings and the target are stored pre-scaled by the row's 1/G_rr so that the serial part of a
+// contact's Gauss-Seidel update is as short as possible (contact_block).
 template <class T>
 struct RowSlots {
   static constexpr int CL = T::T_CL;
@@ -142,22 +145,25 @@ __device__ __forceinline__ void gather_w(int lc, float wA, float wBb, const floa
   }
 }
 
-// One contact's three projected Gauss-Seidel rows (normal, friction x2, box friction cone) given
-// u = c + Z w before the pass; the in-pass coupling of its rows goes through G.  Returns the
-// impulse increments and updates lam.  Same iterate as three scalar GS rows.
+// One contact's three projected Gauss-Seidel rows (normal, then the two box-friction rows bounded by
+// mu * normal impulse) given u = c + Z w before the pass; the in-pass coupling of its rows goes
+// through the Delassus block.  Arguments are pre-scaled: tdi = target/G00, s10 = G10/G11,
+// s20 = G20/G22, s21 = G21/G22.  Algebraically the iterate of three scalar GS rows
+// with the dependent chain cut to: max, sub | fma, med3, sub | fma, med3, sub.
 __device__ __forceinline__ void contact_block(float u0, float u1, float u2, float di0, float di1, float di2,
-                                              float g10, float g20, float g21, float target, float mu,
+                                              float s10, float s20, float s21, float tdi, float mu,
                                               float* lam, float& dl0, float& dl1, float& dl2) {
-  const float n0 = fmaxf(lam[0] + (target - u0) * di0, 0.f);
+  const float n0 = fmaxf(fmaf(-u0, di0, lam[0] + tdi), 0.f);
+  const float a1 = fmaf(-u1, di1, lam[1]);  // row 1 before the in-pass coupling to row 0
+  const float a2 = fmaf(-u2, di2, lam[2]);
   dl0 = n0 - lam[0];
   lam[0] = n0;
   const float lim = mu * n0;
-  u1 += g10 * dl0;
-  const float n1 = clampf(lam[1] - u1 * di1, -lim, lim);
+  const float n1 = __builtin_amdgcn_fmed3f(fmaf(-s10, dl0, a1), -lim, lim);
+  const float b2 = fmaf(-s20, dl0, a2);
   dl1 = n1 - lam[1];
   lam[1] = n1;
-  u2 += g20 * dl0 + g21 * dl1;
-  const float n2 = clampf(lam[2] - u2 * di2, -lim, lim);
+  const float n2 = __builtin_amdgcn_fmed3f(fmaf(-s21, dl1, b2), -lim, lim);
   dl2 = n2 - lam[2];
   lam[2] = n2;
 }
@@ -572,7 +578,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     rec[RS::C_ACT * RW] = act[j] ? 1.f : 0.f;
     if (act[j]) {
       const int kb = T::T_ccb[j];
-      float zr[3][6 + CL];
+      float zr[3][6 + CL], dir[3];
 #pragma unroll
       for (int rr = 0; rr < 3; ++rr) {
         float* row = rows_own + RS::chain_row(j, rr) * RW;
@@ -618,7 +624,8 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         row[8 * RW] = 0.f;
         row[11 * RW] = 0.f;
         rec[(RS::C_C + rr) * RW] = cj;
-        rec[(RS::C_DI + rr) * RW] = 1.f / d;
+        dir[rr] = 1.f / d;
+        rec[(RS::C_DI + rr) * RW] = dir[rr];
       }
       float g10 = 0.f, g20 = 0.f, g21 = 0.f;
 #pragma unroll
@@ -627,13 +634,13 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         g20 += zr[2][f] * zr[0][f];
         g21 += zr[2][f] * zr[1][f];
       }
-      rec[(RS::C_G + 0) * RW] = g10;
-      rec[(RS::C_G + 1) * RW] = g20;
-      rec[(RS::C_G + 2) * RW] = g21;
+      rec[(RS::C_G + 0) * RW] = g10 * dir[1];
+      rec[(RS::C_G + 1) * RW] = g20 * dir[2];
+      rec[(RS::C_G + 2) * RW] = g21 * dir[2];
       const float sc = sep[j];
       const float tgt = -sc * inv_h;
-      rec[RS::C_TP * RW] = sc < 0.f ? fminf(tgt, P.max_depen_vel) : tgt;
-      rec[RS::C_TV * RW] = sc < 0.f ? 0.f : tgt;
+      rec[RS::C_TP * RW] = (sc < 0.f ? fminf(tgt, P.max_depen_vel) : tgt) * dir[0];
+      rec[RS::C_TV * RW] = (sc < 0.f ? 0.f : tgt) * dir[0];
       rec[RS::C_MU * RW] = cmu[j];
     }
   }
@@ -649,7 +656,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     if (ract[j]) {
       float* rec = rows_own + RS::root(j) * RW;
       const float xc[3] = {x[0], x[1], x[2] - r};
-      float zr[3][6];
+      float zr[3][6], dir[3];
 #pragma unroll
       for (int rr = 0; rr < 3; ++rr) {
         const int ax3 = (rr == 0) ? 2 : (rr == 1 ? 0 : 1);
@@ -673,7 +680,8 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         rec[(rr * RS::RZROW + RS::zslot(6)) * RW] = 0.f;  // lanes 2, 3: second component is chain-only
         rec[(rr * RS::RZROW + RS::zslot(7)) * RW] = 0.f;
         rec[(RS::R_C + rr) * RW] = cj;
-        rec[(RS::R_DI + rr) * RW] = 1.f / d;
+        dir[rr] = 1.f / d;
+        rec[(RS::R_DI + rr) * RW] = dir[rr];
       }
       float g10 = 0.f, g20 = 0.f, g21 = 0.f;
 #pragma unroll
@@ -682,13 +690,13 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         g20 += zr[2][f] * zr[0][f];
         g21 += zr[2][f] * zr[1][f];
       }
-      rec[(RS::R_G + 0) * RW] = g10;
-      rec[(RS::R_G + 1) * RW] = g20;
-      rec[(RS::R_G + 2) * RW] = g21;
+      rec[(RS::R_G + 0) * RW] = g10 * dir[1];
+      rec[(RS::R_G + 1) * RW] = g20 * dir[2];
+      rec[(RS::R_G + 2) * RW] = g21 * dir[2];
       const float sc = dist - P.rest_offset;
       const float tgt = -sc * inv_h;
-      rec[RS::R_TP * RW] = sc < 0.f ? fminf(tgt, P.max_depen_vel) : tgt;
-      rec[RS::R_TV * RW] = sc < 0.f ? 0.f : tgt;
+      rec[RS::R_TP * RW] = (sc < 0.f ? fminf(tgt, P.max_depen_vel) : tgt) * dir[0];
+      rec[RS::R_TV * RW] = (sc < 0.f ? 0.f : tgt) * dir[0];
       rec[RS::R_MU * RW] = 0.5f * (mu_g[T::T_rcs[j] * N + e] + P.ground_mu);
     }
   }
@@ -704,6 +712,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
   // contact's Delassus couplings runs replicated, and each lane updates only what it owns.
   static_assert(CL == 3, "component distribution assumes 3-dof chains");
   const bool low = lc < 2;            // component l+4 is a base component (else chain comp l-2)
+  const float lane0 = lc == 0 ? 1.f : 0.f;
   float wA = 0.f, wBb = 0.f, wB[NCH], wC[NCH];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) wB[c] = wC[c] = 0.f;
@@ -729,7 +738,8 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         for (int rr = 0; rr < 3; ++rr) {
           za[rr] = recl[(rr * RS::RZROW) * RW];
           zb2[rr] = recl[(rr * RS::RZROW + 1) * RW];
-          u[rr] = rec[(RS::R_C + rr) * RW] + quad_sum(za[rr] * wA + zb2[rr] * wBb);
+          const float c0 = rec[(RS::R_C + rr) * RW] * lane0;  // c joins lane 0's partial
+          u[rr] = quad_sum(fmaf(za[rr], wA, fmaf(zb2[rr], wBb, c0)));
         }
         float dl0, dl1, dl2;
         contact_block(u[0], u[1], u[2], rec[RS::R_DI * RW], rec[(RS::R_DI + 1) * RW], rec[(RS::R_DI + 2) * RW],
@@ -739,38 +749,54 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         wBb += zb2[0] * dl0 + zb2[1] * dl1 + zb2[2] * dl2;  // lanes 2, 3 read the zero pads
       }
     }
+    // software-pipelined over the NCH*CC chain contacts: the next contact's activity, Z components
+    // and c are loaded before this contact's (divergent) block, so their LDS latency overlaps it
+    float nact, nz[9], nc[3];
+    auto fetch = [&](int n, float& act_o, float* z_o, float* c_o) {
+      const int cc = n / CC, j = n - (n / CC) * CC;
+      const float* rec = rows_team + cc + RS::chain(j) * RW;
+      const float* recl = rec + 3 * lc * RW;
+      act_o = rec[RS::C_ACT * RW];
 #pragma unroll
-    for (int cc = 0; cc < NCH; ++cc) {
-      const float* col = rows_team + cc;
+      for (int rr = 0; rr < 3; ++rr) {
+        const float* row = recl + rr * RS::ZROW * RW;
+        z_o[3 * rr + 0] = row[0];
+        z_o[3 * rr + 1] = row[RW];
+        z_o[3 * rr + 2] = row[2 * RW];
+        c_o[rr] = rec[(RS::C_C + rr) * RW] * lane0;  // multiply, not select: no divergent load
+      }
+    };
+    fetch(0, nact, nz, nc);
 #pragma unroll
-      for (int j = 0; j < CC; ++j) {
-        const float* rec = col + RS::chain(j) * RW;
-        const bool a_o = rec[RS::C_ACT * RW] != 0.f;
+    for (int n = 0; n < NCH * CC; ++n) {
+      const int cc = n / CC, j = n - (n / CC) * CC;
+      const float* rec = rows_team + cc + RS::chain(j) * RW;
+      float z[9], c3[3];
+      const float act_n = nact;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) z[i] = nz[i];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) c3[i] = nc[i];
+      if (n + 1 < NCH * CC) fetch(n + 1, nact, nz, nc);
+      const bool a_o = act_n != 0.f;
 #ifdef GS_PHASE_PROFILE
-        if (__ballot(a_o) != 0ull) GS_PROF_COUNT(8, 1)  // chain contacts the wave executes
+      if (__ballot(a_o) != 0ull) GS_PROF_COUNT(8, 1)  // chain contacts the wave executes
 #endif
-        if (a_o) {
-          const float wBv = low ? wBb : wB[cc];
-          const float* recl = rec + 3 * lc * RW;
-          float za[3], zb2[3], zc2[3], u[3];
+      if (a_o) {
+        const float wBv = low ? wBb : wB[cc];
+        float u[3];
 #pragma unroll
-          for (int rr = 0; rr < 3; ++rr) {
-            const float* row = recl + rr * RS::ZROW * RW;
-            za[rr] = row[0];
-            zb2[rr] = row[RW];
-            zc2[rr] = row[2 * RW];
-            u[rr] = rec[(RS::C_C + rr) * RW] + quad_sum(za[rr] * wA + zb2[rr] * wBv + zc2[rr] * wC[cc]);
-          }
-          float dl0, dl1, dl2;
-          contact_block(u[0], u[1], u[2], rec[RS::C_DI * RW], rec[(RS::C_DI + 1) * RW], rec[(RS::C_DI + 2) * RW],
-                        rec[RS::C_G * RW], rec[(RS::C_G + 1) * RW], rec[(RS::C_G + 2) * RW], rec[tsel * RW],
-                        rec[RS::C_MU * RW], lamc[cc][j], dl0, dl1, dl2);
-          wA += za[0] * dl0 + za[1] * dl1 + za[2] * dl2;
-          const float nB = wBv + (zb2[0] * dl0 + zb2[1] * dl1 + zb2[2] * dl2);
-          wBb = low ? nB : wBb;
-          wB[cc] = low ? wB[cc] : nB;
-          wC[cc] += zc2[0] * dl0 + zc2[1] * dl1 + zc2[2] * dl2;
-        }
+        for (int rr = 0; rr < 3; ++rr)  // c joins lane 0's partial; the w terms last (they carry the chain)
+          u[rr] = quad_sum(fmaf(z[3 * rr], wA, fmaf(z[3 * rr + 1], wBv, fmaf(z[3 * rr + 2], wC[cc], c3[rr]))));
+        float dl0, dl1, dl2;
+        contact_block(u[0], u[1], u[2], rec[RS::C_DI * RW], rec[(RS::C_DI + 1) * RW], rec[(RS::C_DI + 2) * RW],
+                      rec[RS::C_G * RW], rec[(RS::C_G + 1) * RW], rec[(RS::C_G + 2) * RW], rec[tsel * RW],
+                      rec[RS::C_MU * RW], lamc[cc][j], dl0, dl1, dl2);
+        wA += z[0] * dl0 + z[3] * dl1 + z[6] * dl2;
+        const float nB = wBv + (z[1] * dl0 + z[4] * dl1 + z[7] * dl2);
+        wBb = low ? nB : wBb;
+        wB[cc] = low ? wB[cc] : nB;
+        wC[cc] += z[2] * dl0 + z[5] * dl1 + z[8] * dl2;
       }
     }
 #ifdef GS_PHASE_PROFILE

@@ -120,3 +120,20 @@ def read_state(sim, nd):
     root = st[0:13].T.copy()
     dof = np.stack([st[13:13 + nd].T, st[13 + nd:].T], axis=-1)
     return root, dof
+
+
+def assert_mostly_close(actual, desired, atol, rtol=0.0, max_frac=1e-3, hard=None, what=""):
+    """Two float implementations of a contact solver from the same state agree elementwise except
+    where a contact's activity or friction-cone clamp switched on a last-bit difference (the
+    dynamics is discontinuous there): at most `max_frac` of the elements may exceed
+    atol + rtol*|desired|, and none may exceed `hard` (default 50x the tolerance)."""
+    import numpy as np
+    a = np.asarray(actual, dtype=np.float64)
+    d = np.asarray(desired, dtype=np.float64)
+    tol = atol + rtol * np.abs(d)
+    err = np.abs(a - d)
+    bad = err > tol
+    frac = bad.mean() if bad.size else 0.0
+    hard_tol = 50 * tol if hard is None else hard
+    assert frac <= max_frac, f"{what}: {bad.sum()} of {bad.size} elements off (max err {err.max():.3g})"
+    assert np.all(err <= hard_tol), f"{what}: max err {err.max():.3g} beyond the hard bound"

@@ -12,7 +12,7 @@ import ctypes as C
 import os
 import sys
 
-os.environ["GS_LIBGYMSIM"] = "libgymsim_prof.so"
+os.environ.setdefault("GS_LIBGYMSIM", "libgymsim_prof.so")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 PHASES = ["forward pass + contact Jacobians", "backward pass + L^T D L", "free velocity", "contact rows (Z, c)",
