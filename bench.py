@@ -30,6 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured float4 copy
+FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector)
 
 
 def physics_kernel_bytes_per_env(nd=12, nb=13, ns=9):
@@ -174,6 +175,19 @@ def main():
                 d = json.load(f)
             if d.get("num_envs") == N:
                 traffic = d.get("hbm_bytes_per_launch")
+        # secondary roofline (SURVEY.md 8d "report both"): counted FP32 VALU FLOPs of the same kernel
+        valu = None
+        vj = os.path.join(ROOT, "profiles", "valu_pd_step.json")
+        if os.path.exists(vj):
+            with open(vj) as f:
+                d = json.load(f)
+            if d.get("num_envs") == N:
+                fl = d["fp32_flops_per_launch"]
+                ach = fl / (kernel_ms * 1e-3) / 1e12
+                valu = {"bound": "valu", "achieved": ach, "peak": FP32_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": ach / FP32_VECTOR_PEAK_TFLOPS, "flops_per_launch": fl,
+                        "flops_per_env_step": d["fp32_flops_per_env_step"],
+                        "valu_busy_frac": d["busy_frac_valu"], "wait_frac": d["wait_frac"]}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(N, args.cpu_seconds)
@@ -196,7 +210,8 @@ def main():
                        "num_envs_per_gpu": N, "global_num_envs": N * world, "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "kernel": f"gs_sim_pd_step ({kernel_name})",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "kernel_ms": kernel_ms, "bytes_per_launch": bytes_per_launch},
+                         "traffic": traffic, "kernel_ms": kernel_ms, "bytes_per_launch": bytes_per_launch,
+                         "valu": valu},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

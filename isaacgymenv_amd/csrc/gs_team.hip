@@ -277,7 +277,8 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
                                              const DevParams& P, TeamState<T>& s, const float* tau,
                                              const float* __restrict__ mu_g, int N, int e, int lc,
                                              float* __restrict__ rows_own, const float* __restrict__ rows_team,
-                                             float* __restrict__ cf_soa, bool collect GS_PROF_PARAM) {
+                                             float* __restrict__ cf_soa, bool collect,
+                                             float* __restrict__ cf_aos GS_PROF_PARAM) {
   constexpr int CL = T::T_CL, CC = T::T_CC, RC = T::T_RC, NCH = T::T_NCH, LN = T::T_LANES;
   static_assert(NCH == LN && LN == 4, "lane teams are DPP quads with one chain per lane");
   using C = CM<T>;
@@ -466,7 +467,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
 #pragma unroll
     for (int kk = 0; kk < CL; ++kk) {
       const int k = CL - 1 - kk;
-      const float dinv = 1.f / Mcc[k][k];
+      const float dinv = __builtin_amdgcn_rcpf(Mcc[k][k]);
 #pragma unroll
       for (int jj = 0; jj < CL; ++jj) {
         const int j = k - 1 - jj;
@@ -496,7 +497,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
 #pragma unroll
   for (int kk = 0; kk < 6; ++kk) {
     const int k = 5 - kk;
-    const float dinv = 1.f / Mbb[k][k];
+    const float dinv = __builtin_amdgcn_rcpf(Mbb[k][k]);
 #pragma unroll
     for (int ii = 0; ii < 6; ++ii) {
       const int i = k - 1 - ii;
@@ -624,7 +625,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         row[8 * RW] = 0.f;
         row[11 * RW] = 0.f;
         rec[(RS::C_C + rr) * RW] = cj;
-        dir[rr] = 1.f / d;
+        dir[rr] = __builtin_amdgcn_rcpf(d);
         rec[(RS::C_DI + rr) * RW] = dir[rr];
       }
       float g10 = 0.f, g20 = 0.f, g21 = 0.f;
@@ -680,7 +681,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         rec[(rr * RS::RZROW + RS::zslot(6)) * RW] = 0.f;  // lanes 2, 3: second component is chain-only
         rec[(rr * RS::RZROW + RS::zslot(7)) * RW] = 0.f;
         rec[(RS::R_C + rr) * RW] = cj;
-        dir[rr] = 1.f / d;
+        dir[rr] = __builtin_amdgcn_rcpf(d);
         rec[(RS::R_DI + rr) * RW] = dir[rr];
       }
       float g10 = 0.f, g20 = 0.f, g21 = 0.f;
@@ -891,6 +892,10 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       cf_soa[(3 * b + 0) * N + e] = f0;
       cf_soa[(3 * b + 1) * N + e] = f1;
       cf_soa[(3 * b + 2) * N + e] = f2;
+      if (cf_aos) {  // net contact force tensor [N*nb][3] (the launch's last collecting substep)
+        float* o = cf_aos + ((size_t)e * T::NB + b) * 3;
+        o[0] = f0; o[1] = f1; o[2] = f2;
+      }
     }
     if (lc == 0) {
       float f0 = 0.f, f1 = 0.f, f2 = 0.f;
@@ -903,6 +908,10 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       cf_soa[0 * N + e] = f0;
       cf_soa[1 * N + e] = f1;
       cf_soa[2 * N + e] = f2;
+      if (cf_aos) {
+        float* o = cf_aos + (size_t)e * T::NB * 3;
+        o[0] = f0; o[1] = f1; o[2] = f2;
+      }
     }
   }
   GS_PROF(5)  // back-substitution + integrate + contact forces
@@ -941,7 +950,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel*
   GS_PROF_DECL
   for (int sstep = 0; sstep < P.substeps; ++sstep) {
     const bool last = (sstep == P.substeps - 1) && P.collect;
-    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last GS_PROF_ARGS);
+    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, nullptr GS_PROF_ARGS);
   }
   team_store<T>(B.state, N, e, lc, s);
   GS_PROF_FLUSH
@@ -982,7 +991,8 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
     }
     const bool last = ((it % sub) == sub - 1) && P.collect;
     GS_PROF(6)  // PD torque
-    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last GS_PROF_ARGS);
+    float* cf_aos = (it == total - 1) ? A.cf_out : nullptr;
+    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, cf_aos GS_PROF_ARGS);
     if (it == n_pd - 1 && A.dof_out) {
 #pragma unroll
       for (int k = 0; k < CL; ++k) {
@@ -1006,18 +1016,6 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
     team_com_velocity<T>(M, s, v);
     o[7] = v[0]; o[8] = v[1]; o[9] = v[2];
     o[10] = s.w[0]; o[11] = s.w[1]; o[12] = s.w[2];
-  }
-  if (P.collect && A.cf_out) {
-#pragma unroll
-    for (int k = 0; k < CL; ++k) {
-      const int b = 1 + lc * CL + k;
-#pragma unroll
-      for (int f = 0; f < 3; ++f) A.cf_out[((size_t)e * NB + b) * 3 + f] = B.cf[(3 * b + f) * N + e];
-    }
-    if (lc == 0) {
-#pragma unroll
-      for (int f = 0; f < 3; ++f) A.cf_out[((size_t)e * NB) * 3 + f] = B.cf[f * N + e];
-    }
   }
   GS_PROF(7)  // outputs
   GS_PROF_FLUSH
