@@ -56,6 +56,9 @@ typedef struct gs_model_desc {
     const double *dof_effort;     /* [nd] max |force|, <= 0 unlimited                   */
     const double *dof_velocity;   /* [nd] max |vel|, <= 0 unlimited                     */
     const double *dof_armature;   /* [nd]                                               */
+    const double *dof_lower;      /* [nd] joint limits (rad or m), used where has_limits */
+    const double *dof_upper;      /* [nd]                                               */
+    const int32_t *dof_has_limits;/* [nd] 0/1 (URDF <limit>, MJCF limited="true")     */
 } gs_model_desc;
 
 /* gymapi.SimParams subset the reference sets (vec_task.py:514-562). */
@@ -71,6 +74,7 @@ typedef struct gs_sim_params {
     double max_depenetration_velocity;
     int32_t contact_collection;         /* 0 never, 1 last substep (2 treated as 1)        */
     int32_t kernel_variant;             /* 0 auto, 1 one env per lane, 2 lane team (4 lanes/env) */
+    double joint_limit_margin;          /* a limit row is active within this distance of the limit */
 } gs_sim_params;
 
 /* Fused PD decimation step (AnymalTerrain.pre_physics_step + VecTask.step's
@@ -138,6 +142,17 @@ int gs_sim_set_dof(gs_sim *sim, const float *dof_state, const int32_t *idx, int 
 
 /* Fused decimation step, see gs_pd_args. */
 int gs_sim_pd_step(gs_sim *sim, const gs_pd_args *args, void *stream);
+
+/* Force sensors (gym.create_asset_force_sensor, ant.py:174-178): one per listed body, identity
+ * sensor pose, leaf bodies only.  Call after gs_sim_set_model and before gs_sim_prepare.  A sensor
+ * reads the wrench its body receives through its parent joint (Newton-Euler of the body with the
+ * substep's solved accelerations, minus gravity and contact), force then torque at the body origin
+ * in body axes, from the last substep of every simulate call. */
+int gs_sim_set_force_sensors(gs_sim *sim, int n, const int32_t *bodies);
+/* Caller-owned SoA readings [6*n][N], bound after gs_sim_prepare. */
+int gs_sim_bind_force_sensors(gs_sim *sim, float *sensor_soa);
+/* refresh_force_sensor_tensor: SoA -> [N*n][6] (ant.py:233-235) */
+int gs_sim_refresh_force_sensor(gs_sim *sim, float *out, void *stream);
 
 /* Physics kernel selected by gs_sim_set_model: 1 one env per lane, 2 lane team; -1 on error. */
 int gs_sim_kernel_variant(gs_sim *sim);

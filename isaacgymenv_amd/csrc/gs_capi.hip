@@ -57,6 +57,9 @@ struct gs_sim {
   launch_pd_fn pd_fn = nullptr;
   int variant = 0;  // kernel actually selected: 1 lane, 2 team
   DevModel* d_model = nullptr;
+  DevModel h_model{};             // host copy (sensors are added after set_model)
+  std::vector<int> parent;
+  float* sens = nullptr;          // [6*nsens][N]
   int nb = 0, nd = 0, nc = 0, ns = 0;
   int N = 0;
   float* state = nullptr;
@@ -96,6 +99,8 @@ gs_sim* gs_sim_create(int device, const gs_sim_params* p) {
   s->dp.rest_offset = (float)p->rest_offset;
   s->dp.max_depen_vel = (float)p->max_depenetration_velocity;
   s->dp.collect = p->contact_collection != 0;
+  s->dp.limit_margin = (float)(p->joint_limit_margin > 0 ? p->joint_limit_margin : 0.0);
+  s->dp.any_limits = 0;
   s->dp.has_ground = 0;
   s->dp.ground_mu = 1.f;
   return s;
@@ -144,11 +149,19 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
     for (int k = 0; k < 3; ++k) h.cpoint[c][k] = (float)m->cand_point[3 * c + k];
     h.cradius[c] = (float)m->cand_radius[c];
   }
+  int any_lim = 0;
   for (int j = 0; j < m->num_dofs; ++j) {
     h.effort[j] = (float)m->dof_effort[j];
     h.vmax[j] = (float)m->dof_velocity[j];
     h.armature[j] = (float)m->dof_armature[j];
+    h.has_lim[j] = m->dof_has_limits && m->dof_has_limits[j] && m->dof_upper[j] > m->dof_lower[j];
+    h.lower[j] = h.has_lim[j] ? (float)m->dof_lower[j] : 0.f;
+    h.upper[j] = h.has_lim[j] ? (float)m->dof_upper[j] : 0.f;
+    any_lim |= h.has_lim[j];
   }
+  h.nsens = 0;
+  for (int b = 0; b < GS_MAXB; ++b) h.sens_of_body[b] = -1;
+  s->h_model = h;
   hipSetDevice(s->device);
   if (!s->d_model) {
     hipError_t e = hipMalloc(&s->d_model, sizeof(DevModel));
@@ -161,7 +174,10 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   for (int i = 0; i < g_num_team_kernels; ++i)
     if (std::strcmp(g_team_kernels[i].sig, t->sig) == 0 && g_team_kernels[i].sim) te = &g_team_kernels[i];
   const int want = s->params.kernel_variant;
-  if (want == 2 && !te) return fail("gs_sim_set_model: no lane-team kernel for this topology");
+  if (te && any_lim) te = nullptr;  // the lane team has no joint-limit rows: the one-env-per-lane kernel runs
+  if (want == 2 && !te) return fail("gs_sim_set_model: no lane-team kernel for this topology / joint limits");
+  s->dp.any_limits = any_lim;
+  s->parent.assign(m->parent, m->parent + m->num_bodies);
   if (te && want != 1) {
     s->sim_fn = te->sim;
     s->pd_fn = te->pd;
@@ -188,7 +204,7 @@ int gs_sim_prepare(gs_sim* s, int num_envs, float* state, const float* shape_fri
   return 0;
 }
 
-static SimBuffers buffers(gs_sim* s) { return SimBuffers{s->state, s->mu, s->cf, s->N}; }
+static SimBuffers buffers(gs_sim* s) { return SimBuffers{s->state, s->mu, s->cf, s->N, s->sens}; }
 
 static int ready(gs_sim* s, const char* where) {
   if (!s || !s->topo || !s->state) return fail("%s: sim not prepared", where);
@@ -263,6 +279,43 @@ int gs_sim_set_dof(gs_sim* s, const float* src, const int32_t* idx, int n_idx, v
   if (ready(s, "gs_sim_set_dof")) return -1;
   hipError_t e = launch_set_dof(s->state, s->N, s->nd, src, idx, n_idx, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_set_dof");
+}
+
+int gs_sim_set_force_sensors(gs_sim* s, int n, const int32_t* bodies) {
+  if (!s || !s->topo) return fail("gs_sim_set_force_sensors: model not set");
+  if (s->state) return fail("gs_sim_set_force_sensors: call before gs_sim_prepare");
+  if (n < 0 || n > GS_MAXS || (n > 0 && !bodies)) return fail("gs_sim_set_force_sensors: at most 8 sensors");
+  if (n > 0 && s->variant == 2)
+    return fail("gs_sim_set_force_sensors: the lane-team kernel has no force sensors (use kernel_variant 1)");
+  DevModel& h = s->h_model;
+  for (int b = 0; b < GS_MAXB; ++b) h.sens_of_body[b] = -1;
+  for (int i = 0; i < n; ++i) {
+    const int b = bodies[i];
+    if (b <= 0 || b >= s->nb) return fail("gs_sim_set_force_sensors: sensor body out of range (or the root)");
+    for (int c = 0; c < s->nb; ++c)
+      if (s->parent[c] == b) return fail("gs_sim_set_force_sensors: sensors on non-leaf bodies are not supported");
+    if (h.sens_of_body[b] >= 0) return fail("gs_sim_set_force_sensors: two sensors on one body");
+    h.sens_of_body[b] = i;
+  }
+  h.nsens = n;
+  hipSetDevice(s->device);
+  hipError_t e = hipMemcpy(s->d_model, &h, sizeof(DevModel), hipMemcpyHostToDevice);
+  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_set_force_sensors hipMemcpy");
+}
+
+int gs_sim_bind_force_sensors(gs_sim* s, float* soa) {
+  if (ready(s, "gs_sim_bind_force_sensors")) return -1;
+  if (s->h_model.nsens > 0 && !soa) return fail("gs_sim_bind_force_sensors: buffer required");
+  s->sens = soa;
+  return 0;
+}
+
+int gs_sim_refresh_force_sensor(gs_sim* s, float* out, void* stream) {
+  if (ready(s, "gs_sim_refresh_force_sensor")) return -1;
+  if (s->h_model.nsens == 0) return 0;
+  if (!s->sens) return fail("gs_sim_refresh_force_sensor: sensors not bound");
+  hipError_t e = launch_refresh_sensor(s->sens, s->N, s->h_model.nsens, out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_force_sensor");
 }
 
 int gs_sim_kernel_variant(gs_sim* s) { return s ? s->variant : -1; }

@@ -5,6 +5,7 @@
 #define GS_MAXB 32   // bodies per articulation
 #define GS_MAXD 32   // dofs per articulation
 #define GS_MAXC 64   // plane-contact candidates per articulation
+#define GS_MAXS 8    // force sensors per articulation
 #define GS_WAVE 64
 
 // Model constants shared by every env, float32, one copy in device memory.
@@ -22,6 +23,10 @@ struct DevModel {
   float effort[GS_MAXD];     // <= 0 : unlimited
   float vmax[GS_MAXD];       // <= 0 : unlimited
   float armature[GS_MAXD];
+  float lower[GS_MAXD], upper[GS_MAXD];  // joint limits where has_lim
+  int has_lim[GS_MAXD];
+  int nsens;                    // force sensors (leaf bodies)
+  int sens_of_body[GS_MAXB];    // sensor index of body b, -1 if none
 };
 
 struct DevParams {
@@ -33,6 +38,8 @@ struct DevParams {
   float ground_mu;       // ground plane friction (0.5*(mu_shape + mu_ground) is the pair friction)
   int has_ground;
   int collect;           // contact_collection != 0
+  float limit_margin;    // joint-limit rows are active within this distance
+  int any_limits;        // some dof has limits (uniform: skips the limit rows entirely)
 };
 
 // SoA state: field f of env e at state[f*N + e]
@@ -43,6 +50,7 @@ struct SimBuffers {
   const float* mu;       // [ns][N]
   float* cf;             // [3*nb][N]
   int N;
+  float* sens;           // [6*nsens][N] force-sensor readings or null
 };
 
 struct PdDev {
@@ -87,6 +95,7 @@ extern const int g_num_team_kernels;
 hipError_t launch_refresh_root(const float* state, int N, int nd, const float* com0, float* out, hipStream_t s);
 hipError_t launch_refresh_dof(const float* state, int N, int nd, float* out, hipStream_t s);
 hipError_t launch_refresh_contact(const float* cf, int N, int nb, float* out, hipStream_t s);
+hipError_t launch_refresh_sensor(const float* soa, int N, int ns, float* out, hipStream_t s);
 hipError_t launch_set_root(float* state, int N, int nd, const float* com0, const float* src, const int* idx,
                            int n_idx, hipStream_t s);
 hipError_t launch_set_dof(float* state, int N, int nd, const float* src, const int* idx, int n_idx,

@@ -37,6 +37,21 @@ __device__ __forceinline__ constexpr int supp_node(int leaf, int si) {
   return si == 0 ? leaf : T::anc[leaf][si > 0 ? si - 1 : 0];
 }
 
+// body kk is b or one of its ancestors
+template <class T>
+__device__ __forceinline__ constexpr bool body_on_path(int kk, int b) {
+  for (int x = b; x > 0; x = T::parent[x])
+    if (x == kk) return true;
+  return kk == 0;
+}
+
+// Lanes (= envs) per workgroup: a full wave unless the topology's LDS rows would exceed the
+// 160 KB of LDS per CU (nv_ant: 25 candidates -> 748 slots -> 32 lanes).
+template <class T>
+struct LaneCfg {
+  static constexpr int LB = (T::NSLOT * 64 * 4 <= 160 * 1024) ? 64 : (T::NSLOT * 32 * 4 <= 160 * 1024) ? 32 : 16;
+};
+
 // Register-resident env state.
 template <class T>
 struct EnvState {
@@ -88,8 +103,9 @@ __device__ __forceinline__ void store_state(float* __restrict__ st, int N, int e
 template <class T>
 __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvState<T>& s,
                                         const float* tau, const float* __restrict__ mu_g, int N, int e, float* lds,
-                                        float* __restrict__ cf_soa, bool collect) {
-  constexpr int NB = T::NB, NV = T::NV, NB6 = T::NBASE, NC = T::NC;
+                                        float* __restrict__ cf_soa, bool collect, float* __restrict__ sens_soa) {
+  constexpr int NB = T::NB, NV = T::NV, NB6 = T::NBASE, NC = T::NC, ND = T::ND;
+  constexpr int LB = LaneCfg<T>::LB;
   constexpr int MS = T::MAXDEP + 1;
   // Keep the model pointer opaque per substep: the constants are re-read with
   // scalar loads (K$ hits) instead of being hoisted out of the substep loop
@@ -213,7 +229,7 @@ __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const 
           const float xc[3] = {x[0], x[1], x[2] - r};
           const int SUP = T::csupp[c];
           const int leaf = T::cleaf[c];
-          float* slot = lds + T::cslot[c] * GS_WAVE;
+          float* slot = lds + T::cslot[c] * LB;
 #pragma unroll
           for (int rr = 0; rr < 3; ++rr) {
             const int ax = (rr == 0) ? 2 : (rr == 1 ? 0 : 1);  // normal z, tangent x, tangent y
@@ -235,7 +251,7 @@ __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const 
                   cross3(Sk, xc, t);
                   v = Sk[3 + ax] + t[ax];
                 }
-                slot[(rr * SUP + si) * GS_WAVE] = v;
+                slot[(rr * SUP + si) * LB] = v;
               }
             }
           }
@@ -286,6 +302,22 @@ __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const 
             Mm[4][3] = 0.f; Mm[5][3] = 0.f; Mm[5][4] = 0.f;
           }
         }
+      }
+    }
+  }
+
+  // ---------------- joint-limit activity (substep start): one unilateral row per dof within
+  // limit_margin of a limit; sign +1 pushes q up (lower limit), -1 down (upper limit)
+  float lsgn[ND > 0 ? ND : 1], lsep[ND > 0 ? ND : 1];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    lsgn[j] = 0.f;
+    lsep[j] = 0.f;
+    if (P.any_limits && M->has_lim[j]) {
+      const float lo = s.q[j] - M->lower[j], hi = M->upper[j] - s.q[j];
+      if (lo < P.limit_margin || hi < P.limit_margin) {
+        lsgn[j] = lo <= hi ? 1.f : -1.f;
+        lsep[j] = lo <= hi ? lo : hi;
       }
     }
   }
@@ -360,7 +392,7 @@ __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const 
     if (act[c]) {
       const int SUP = T::csupp[c];
       const int leaf = T::cleaf[c];
-      float* slot = lds + T::cslot[c] * GS_WAVE;
+      float* slot = lds + T::cslot[c] * LB;
 #pragma unroll
       for (int rr = 0; rr < 3; ++rr) {
         float jv[MS];
@@ -368,7 +400,7 @@ __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const 
 #pragma unroll
         for (int si = 0; si < MS; ++si) {
           if (si < SUP) {
-            jv[si] = slot[(rr * SUP + si) * GS_WAVE];
+            jv[si] = slot[(rr * SUP + si) * LB];
             cj += jv[si] * nuf[supp_node<T>(leaf, si)];
           }
         }
@@ -387,17 +419,52 @@ __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const 
           if (si < SUP) {
             const float zh = jv[si] * sD[supp_node<T>(leaf, si)];
             d += zh * zh;
-            slot[(rr * SUP + si) * GS_WAVE] = zh;
+            slot[(rr * SUP + si) * LB] = zh;
           }
         }
-        slot[(3 * SUP + rr) * GS_WAVE] = cj;
-        slot[(3 * SUP + 3 + rr) * GS_WAVE] = 1.f / d;
+        slot[(3 * SUP + rr) * LB] = cj;
+        slot[(3 * SUP + 3 + rr) * LB] = 1.f / d;
       }
     }
   }
 
-  // ---------------- projected Gauss-Seidel in w-space
-  float wt[NV], lam[NC][3], wpos[NV];
+  // ---------------- joint-limit rows: J = sign * e_dof -> c, scaled Z, 1/diag (same elimination)
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    if (lsgn[j] != 0.f) {
+      const int SUP = T::lsupp[j];
+      const int leaf = T::lleaf[j];
+      float* slot = lds + T::lslot[j] * LB;
+      float jv[MS];
+#pragma unroll
+      for (int si = 0; si < MS; ++si) jv[si] = si == 0 ? lsgn[j] : 0.f;
+#pragma unroll
+      for (int si = 0; si < MS; ++si) {
+        if (si < SUP) {
+          const int k = supp_node<T>(leaf, si);
+#pragma unroll
+          for (int sj = si + 1; sj < MS; ++sj)
+            if (sj < SUP) jv[sj] -= Mm[k][supp_node<T>(leaf, sj)] * jv[si];
+        }
+      }
+      float d = 0.f;
+#pragma unroll
+      for (int si = 0; si < MS; ++si) {
+        if (si < SUP) {
+          const float zh = jv[si] * sD[supp_node<T>(leaf, si)];
+          d += zh * zh;
+          slot[si * LB] = zh;
+        }
+      }
+      slot[SUP * LB] = lsgn[j] * nuf[leaf];
+      slot[(SUP + 1) * LB] = 1.f / d;
+    }
+  }
+
+  // ---------------- projected Gauss-Seidel in w-space (joint limits, then contacts)
+  float wt[NV], lam[NC][3], wpos[NV], laml[ND > 0 ? ND : 1];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) laml[j] = 0.f;
 #pragma unroll
   for (int k = 0; k < NV; ++k) wt[k] = 0.f;
 #pragma unroll
@@ -407,26 +474,52 @@ __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const 
   for (int it = 0; it < iters; ++it) {
     const bool pos_phase = it < P.pos_iters;
 #pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      if (lsgn[j] != 0.f) {
+        const int SUP = T::lsupp[j];
+        const int leaf = T::lleaf[j];
+        const float* slot = lds + T::lslot[j] * LB;
+        const float sc = lsep[j];
+        float target = -sc * inv_h;
+        if (sc < 0.f) target = pos_phase ? fminf(target, P.max_depen_vel) : 0.f;
+        float z[MS];
+        float u = slot[SUP * LB];
+#pragma unroll
+        for (int si = 0; si < MS; ++si) {
+          if (si < SUP) {
+            z[si] = slot[si * LB];
+            u += z[si] * wt[supp_node<T>(leaf, si)];
+          }
+        }
+        const float nl = fmaxf(laml[j] + (target - u) * slot[(SUP + 1) * LB], 0.f);
+        const float dl = nl - laml[j];
+        laml[j] = nl;
+#pragma unroll
+        for (int si = 0; si < MS; ++si)
+          if (si < SUP) wt[supp_node<T>(leaf, si)] += z[si] * dl;
+      }
+    }
+#pragma unroll
     for (int c = 0; c < NC; ++c) {
       if (act[c]) {
         const int SUP = T::csupp[c];
         const int leaf = T::cleaf[c];
-        const float* slot = lds + T::cslot[c] * GS_WAVE;
+        const float* slot = lds + T::cslot[c] * LB;
         const float sc = sep[c];
         float target = -sc * inv_h;
         if (sc < 0.f) target = pos_phase ? fminf(target, P.max_depen_vel) : 0.f;
 #pragma unroll
         for (int rr = 0; rr < 3; ++rr) {
           float z[MS];
-          float u = slot[(3 * SUP + rr) * GS_WAVE];
+          float u = slot[(3 * SUP + rr) * LB];
 #pragma unroll
           for (int si = 0; si < MS; ++si) {
             if (si < SUP) {
-              z[si] = slot[(rr * SUP + si) * GS_WAVE];
+              z[si] = slot[(rr * SUP + si) * LB];
               u += z[si] * wt[supp_node<T>(leaf, si)];
             }
           }
-          const float dinv = slot[(3 * SUP + 3 + rr) * GS_WAVE];
+          const float dinv = slot[(3 * SUP + 3 + rr) * LB];
           float nl;
           if (rr == 0) {
             nl = fmaxf(lam[c][0] + (target - u) * dinv, 0.f);
@@ -522,6 +615,71 @@ __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const 
       cf_soa[(3 * b + 2) * N + e] = f2;
     }
   }
+  if (sens_soa && M->nsens > 0) {
+    // force sensors on leaf bodies: the wrench through the parent joint,
+    //   f_joint = I_b a_b + v_b x* I_b v_b - f_contact   (a_b with the gravity offset, RNEA form)
+    // with a_b = A_b (velocity products + gravity) + base acceleration + sum_path S_k qdd_k, where
+    // qdd = (nu_new - nu)/h and the base's spatial acceleration is (dw/h, dpdot/h - w x pdot).
+    // Fc[b] / Ic[b] of a leaf still hold the body's own RNEA force / inertia.
+    float ab[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) ab[k] = 0.f;
+    if (NB6) {
+      float wxp[3];
+      cross3(&nu[0], &nu[3], wxp);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        ab[k] = (nun[k] - nu[k]) * inv_h;
+        ab[3 + k] = (nun[3 + k] - nu[3 + k]) * inv_h - wxp[k];
+      }
+    }
+#pragma unroll
+    for (int b = 1; b < NB; ++b) {
+      const int si = M->sens_of_body[b];
+      if (si >= 0) {
+        float a[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) a[k] = ab[k];
+#pragma unroll
+        for (int kk = 0; kk < NB; ++kk) {  // path root -> b (compile-time ancestor test)
+            if (kk > 0 && body_on_path<T>(kk, b)) {
+            const int g = NB6 + T::bdof[kk];
+            const float qdd = (nun[g] - nu[g]) * inv_h;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) a[k] += S[kk][k] * qdd;
+          }
+        }
+        float ia[6], f[6];
+        spi_mul(Ic[b], a, ia);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) f[k] = Fc[b][k] + ia[k];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          if (T::cbody[c] == b && act[c]) {
+            float x[3];
+            mat3vec(R[b], M->cpoint[c], x);
+            x[0] += X[b][0]; x[1] += X[b][1]; x[2] += X[b][2] - M->cradius[c];
+            const float fc[3] = {lam[c][1] * inv_h, lam[c][2] * inv_h, lam[c][0] * inv_h};
+            float n[3];
+            cross3(x, fc, n);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { f[k] -= n[k]; f[3 + k] -= fc[k]; }
+          }
+        }
+        // torque about the body origin, then body axes
+        float xf[3], tq[3];
+        cross3(X[b], &f[3], xf);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) tq[k] = f[k] - xf[k];
+        const float* Rb = R[b];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          sens_soa[(6 * si + k) * N + e] = Rb[k] * f[3] + Rb[3 + k] * f[4] + Rb[6 + k] * f[5];
+          sens_soa[(6 * si + 3 + k) * N + e] = Rb[k] * tq[0] + Rb[3 + k] * tq[1] + Rb[6 + k] * tq[2];
+        }
+      }
+    }
+  }
 }
 
 template <class T>
@@ -535,10 +693,11 @@ __device__ __forceinline__ void com_velocity(const DevModel* __restrict__ M, con
 
 // ---------------------------------------------------------------- kernels
 template <class T>
-__global__ __launch_bounds__(GS_WAVE, 1) void k_simulate(const DevModel* __restrict__ M, DevParams P,
+__global__ __launch_bounds__(LaneCfg<T>::LB, 1) void k_simulate(const DevModel* __restrict__ M, DevParams P,
                                                           SimBuffers B, const float* __restrict__ tau_aos) {
-  __shared__ float lds[T::NSLOT * GS_WAVE];
-  const int e = blockIdx.x * GS_WAVE + threadIdx.x;
+  constexpr int LB = LaneCfg<T>::LB;
+  __shared__ float lds[T::NSLOT * LB];
+  const int e = blockIdx.x * LB + threadIdx.x;
   if (e >= B.N) return;
   const int N = B.N;
   EnvState<T> s;
@@ -548,16 +707,18 @@ __global__ __launch_bounds__(GS_WAVE, 1) void k_simulate(const DevModel* __restr
   for (int j = 0; j < T::ND; ++j) tau[j] = tau_aos ? tau_aos[(size_t)e * T::ND + j] : 0.f;
   for (int sstep = 0; sstep < P.substeps; ++sstep) {
     const bool last = (sstep == P.substeps - 1) && P.collect;
-    substep<T>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last);
+    substep<T>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last,
+               sstep == P.substeps - 1 ? B.sens : nullptr);
   }
   store_state<T>(B.state, N, e, s);
 }
 
 template <class T>
-__global__ __launch_bounds__(GS_WAVE, 1) void k_pd_step(const DevModel* __restrict__ M, DevParams P, SimBuffers B,
+__global__ __launch_bounds__(LaneCfg<T>::LB, 1) void k_pd_step(const DevModel* __restrict__ M, DevParams P, SimBuffers B,
                                                          PdDev A) {
-  __shared__ float lds[T::NSLOT * GS_WAVE];
-  const int e = blockIdx.x * GS_WAVE + threadIdx.x;
+  constexpr int LB = LaneCfg<T>::LB;
+  __shared__ float lds[T::NSLOT * LB];
+  const int e = blockIdx.x * LB + threadIdx.x;
   if (e >= B.N) return;
   const int N = B.N;
   constexpr int ND = T::ND;
@@ -582,7 +743,7 @@ __global__ __launch_bounds__(GS_WAVE, 1) void k_pd_step(const DevModel* __restri
       }
     }
     const bool last = ((it % sub) == sub - 1) && P.collect;
-    substep<T>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last);
+    substep<T>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last, it == total - 1 ? B.sens : nullptr);
     if (it == n_pd - 1 && A.dof_out) {
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
@@ -651,6 +812,15 @@ __global__ void k_refresh_contact(const float* __restrict__ cf, int N, int nb, f
   const int k = t % 3, eb = t / 3, b = eb % nb, e = eb / nb;
   out[t] = cf[(3 * b + k) * N + e];
 }
+__global__ void k_refresh_sensor(const float* __restrict__ soa, int N, int ns, float* __restrict__ out) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)N * ns * 6) return;
+  const int k = (int)(t % 6);
+  const long eb = t / 6;
+  const int sidx = (int)(eb % ns);
+  const int e = (int)(eb / ns);
+  out[t] = soa[(6 * sidx + k) * (long)N + e];
+}
 __global__ void k_set_root(float* __restrict__ st, int N, const float* __restrict__ com0,
                            const float* __restrict__ src, const int* __restrict__ idx, int n) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -703,6 +873,11 @@ hipError_t launch_refresh_contact(const float* cf, int N, int nb, float* out, hi
   hipLaunchKernelGGL(k_refresh_contact, dim3(nblk((long)N * nb * 3, 256)), dim3(256), 0, s, cf, N, nb, out);
   return hipGetLastError();
 }
+hipError_t launch_refresh_sensor(const float* soa, int N, int ns, float* out, hipStream_t s) {
+  // [6*ns][N] -> [N*ns][6]: the same transpose as the contact refresh with 6 components
+  hipLaunchKernelGGL(k_refresh_sensor, dim3(nblk((long)N * ns * 6, 256)), dim3(256), 0, s, soa, N, ns, out);
+  return hipGetLastError();
+}
 hipError_t launch_set_root(float* state, int N, int nd, const float* com0, const float* src, const int* idx, int n_idx,
                            hipStream_t s) {
   (void)nd;
@@ -720,14 +895,16 @@ hipError_t launch_set_dof(float* state, int N, int nd, const float* src, const i
 
 template <class T>
 hipError_t launch_sim(const DevModel* M, const DevParams& P, const SimBuffers& B, const float* tau, hipStream_t st) {
-  const int blocks = (B.N + GS_WAVE - 1) / GS_WAVE;
-  hipLaunchKernelGGL(k_simulate<T>, dim3(blocks), dim3(GS_WAVE), 0, st, M, P, B, tau);
+  constexpr int LB = LaneCfg<T>::LB;
+  const int blocks = (B.N + LB - 1) / LB;
+  hipLaunchKernelGGL(k_simulate<T>, dim3(blocks), dim3(LB), 0, st, M, P, B, tau);
   return hipGetLastError();
 }
 template <class T>
 hipError_t launch_pd(const DevModel* M, const DevParams& P, const SimBuffers& B, const PdDev& A, hipStream_t st) {
-  const int blocks = (B.N + GS_WAVE - 1) / GS_WAVE;
-  hipLaunchKernelGGL(k_pd_step<T>, dim3(blocks), dim3(GS_WAVE), 0, st, M, P, B, A);
+  constexpr int LB = LaneCfg<T>::LB;
+  const int blocks = (B.N + LB - 1) / LB;
+  hipLaunchKernelGGL(k_pd_step<T>, dim3(blocks), dim3(LB), 0, st, M, P, B, A);
   return hipGetLastError();
 }
 

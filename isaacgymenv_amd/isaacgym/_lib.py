@@ -19,7 +19,8 @@ class GsModelDesc(C.Structure):
                 ("num_shapes", C.c_int32), ("fixed_base", C.c_int32)] + [
         (n, C.c_void_p) for n in ("parent", "joint_kind", "body_dof", "joint_origin", "joint_axis", "mass",
                                   "com", "inertia", "cand_body", "cand_point", "cand_radius", "cand_shape",
-                                  "dof_effort", "dof_velocity", "dof_armature")]
+                                  "dof_effort", "dof_velocity", "dof_armature", "dof_lower", "dof_upper",
+                                  "dof_has_limits")]
 
 
 class GsSimParams(C.Structure):
@@ -27,7 +28,8 @@ class GsSimParams(C.Structure):
                 ("num_position_iterations", C.c_int32), ("num_velocity_iterations", C.c_int32),
                 ("contact_offset", C.c_double), ("rest_offset", C.c_double),
                 ("bounce_threshold_velocity", C.c_double), ("max_depenetration_velocity", C.c_double),
-                ("contact_collection", C.c_int32), ("kernel_variant", C.c_int32)]
+                ("contact_collection", C.c_int32), ("kernel_variant", C.c_int32),
+                ("joint_limit_margin", C.c_double)]
 
 
 class GsPdArgs(C.Structure):
@@ -68,6 +70,9 @@ def lib():
             "gs_sim_enable_timing": (i, [vp, i]),
             "gs_sim_last_kernel_ms": (f, [vp]),
             "gs_debug_phase_cycles": (i, [vp, i, i]),
+            "gs_sim_set_force_sensors": (i, [vp, i, vp]),
+            "gs_sim_bind_force_sensors": (i, [vp, vp]),
+            "gs_sim_refresh_force_sensor": (i, [vp, vp, vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -87,6 +92,7 @@ EXPORTED_SYMBOLS = [
     "gs_sim_add_ground", "gs_sim_set_model", "gs_sim_prepare", "gs_sim_simulate", "gs_sim_refresh_root",
     "gs_sim_refresh_dof", "gs_sim_refresh_contact", "gs_sim_set_root", "gs_sim_set_dof", "gs_sim_pd_step",
     "gs_sim_kernel_variant", "gs_sim_enable_timing", "gs_sim_last_kernel_ms", "gs_debug_phase_cycles",
+    "gs_sim_set_force_sensors", "gs_sim_bind_force_sensors", "gs_sim_refresh_force_sensor",
 ]
 
 
@@ -103,7 +109,8 @@ def model_desc(flat: dict):
              ("cand_body", "cbody", np.int32), ("cand_point", "cpoint", np.float64),
              ("cand_radius", "cradius", np.float64), ("cand_shape", "cshape", np.int32),
              ("dof_effort", "effort", np.float64), ("dof_velocity", "vmax", np.float64),
-             ("dof_armature", "armature", np.float64)]
+             ("dof_armature", "armature", np.float64), ("dof_lower", "lower", np.float64),
+             ("dof_upper", "upper", np.float64), ("dof_has_limits", "has_limits", np.int32)]
     for field, key, dt in pairs:
         a = np.ascontiguousarray(flat[key], dtype=dt)
         if a.size == 0:

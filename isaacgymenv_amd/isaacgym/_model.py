@@ -51,7 +51,8 @@ def flatten(art: Articulation, armature: float | None = None) -> dict:
         inertia=inertia, cbody=cbody, cpoint=cpoint, cradius=cradius, cshape=cshape,
         effort=np.array([d.effort for d in art.dofs], dtype=np.float64).reshape(nd),
         vmax=np.array([d.velocity for d in art.dofs], dtype=np.float64).reshape(nd),
-        armature=np.full(nd, float(arm)),
+        armature=np.array([float(arm) if d.armature is None else float(d.armature) for d in art.dofs],
+                          dtype=np.float64).reshape(nd),
         lower=np.array([d.lower for d in art.dofs], dtype=np.float64).reshape(nd),
         upper=np.array([d.upper for d in art.dofs], dtype=np.float64).reshape(nd),
         has_limits=np.array([int(d.has_limits) for d in art.dofs], dtype=np.int32).reshape(nd),

@@ -231,7 +231,7 @@ class Asset:
         self.art = art
         self.options = options
         self.flat = flatten(art, armature=options.armature)
-        self.shape_props = [RigidShapeProperties() for _ in range(art.num_shapes)]
+        self.shape_props = [RigidShapeProperties(art.default_friction) for _ in range(art.num_shapes)]
         self.dof_props = self._default_dof_props()
         self.sensors = []
 
@@ -246,7 +246,7 @@ class Asset:
             p[i]["effort"] = d.effort
             p[i]["friction"] = d.friction
             p[i]["damping"] = d.damping
-            p[i]["armature"] = self.options.armature
+            p[i]["armature"] = self.options.armature if d.armature is None else d.armature
         return p
 
 
@@ -276,6 +276,9 @@ class GymTensor:
     def __init__(self, tensor, kind: str = "user"):
         self.tensor = tensor
         self.kind = kind
+
+
+JOINT_LIMIT_MARGIN = 0.1
 
 
 # ------------------------------------------------------------------ the sim
@@ -308,6 +311,8 @@ class Sim:
         p.contact_collection = int(px.contact_collection)
         # GS_PHYSICS_KERNEL=auto|lane|team selects the physics kernel form
         p.kernel_variant = {"auto": 0, "lane": 1, "team": 2}[os.environ.get("GS_PHYSICS_KERNEL", "auto")]
+        # a joint-limit row is generated within this distance of a limit (rad / m)
+        p.joint_limit_margin = JOINT_LIMIT_MARGIN
         self.cparams = p
         L = _lib.lib()
         h = L.gs_sim_create(int(compute_device), p)
@@ -340,6 +345,10 @@ class Sim:
         L = _lib.lib()
         desc, keep = _lib.model_desc(flat)
         _lib.check(L.gs_sim_set_model(self.handle, desc), "gs_sim_set_model")
+        sens = [b for b, _ in self.asset.sensors]
+        if sens:
+            sb = np.ascontiguousarray(sens, dtype=np.int32)
+            _lib.check(L.gs_sim_set_force_sensors(self.handle, len(sens), sb.ctypes.data), "gs_sim_set_force_sensors")
         if self.ground is not None:
             _lib.check(L.gs_sim_add_ground(self.handle, self.ground.static_friction, self.ground.dynamic_friction,
                                            self.ground.restitution), "gs_sim_add_ground")
@@ -368,6 +377,11 @@ class Sim:
                                     self.cf_soa.data_ptr()), "gs_sim_prepare")
         self._keep = keep
         self.kernel_variant = L.gs_sim_kernel_variant(self.handle)
+        self.num_sensors = len(sens)
+        self.sens_soa = torch.zeros(max(1, 6 * len(sens)), N, dtype=f32, device=dev)
+        if sens:
+            _lib.check(L.gs_sim_bind_force_sensors(self.handle, self.sens_soa.data_ptr()), "gs_sim_bind_force_sensors")
+        self.sensor_tensor = torch.zeros(N * len(sens), 6, dtype=f32, device=tdev)
         # reference-layout tensors (sim owned; wrap_tensor shares them)
         self.root_tensor = torch.zeros(N, 13, dtype=f32, device=tdev)
         self.dof_tensor = torch.zeros(N * nd, 2, dtype=f32, device=tdev)
@@ -378,6 +392,7 @@ class Sim:
             self._root_dev = torch.zeros(N, 13, dtype=f32, device=dev)
             self._dof_dev = torch.zeros(N * nd, 2, dtype=f32, device=dev)
             self._cf_dev = torch.zeros(N * nb, 3, dtype=f32, device=dev)
+            self._sens_dev = torch.zeros(N * len(sens), 6, dtype=f32, device=dev)
         self.prepared = True
         self.refresh("root")
         self.refresh("dof")
@@ -386,10 +401,12 @@ class Sim:
     # -------- tensor API
     def refresh(self, kind: str):
         L, s = _lib.lib(), self.stream()
-        dst = {"root": self.root_tensor, "dof": self.dof_tensor, "contact": self.contact_tensor}[kind]
+        dst = {"root": self.root_tensor, "dof": self.dof_tensor, "contact": self.contact_tensor,
+               "sensor": self.sensor_tensor}[kind]
         out = dst if self.gpu_pipeline else {"root": self._root_dev, "dof": self._dof_dev,
-                                             "contact": self._cf_dev}[kind]
-        fn = {"root": L.gs_sim_refresh_root, "dof": L.gs_sim_refresh_dof, "contact": L.gs_sim_refresh_contact}[kind]
+                                             "contact": self._cf_dev, "sensor": self._sens_dev}[kind]
+        fn = {"root": L.gs_sim_refresh_root, "dof": L.gs_sim_refresh_dof, "contact": L.gs_sim_refresh_contact,
+              "sensor": L.gs_sim_refresh_force_sensor}[kind]
         _lib.check(fn(self.handle, out.data_ptr(), s), f"refresh {kind}")
         if not self.gpu_pipeline:
             dst.copy_(out.cpu())
@@ -516,13 +533,20 @@ class Gym:
         return True
 
     def get_asset_actuator_properties(self, asset: Asset):
-        return [ActuatorProperties(d.effort) for d in asset.art.dofs]
+        # MJCF motors carry their gear (ant.py:160-162 reads it as motor_effort); URDF: the effort limit
+        return [ActuatorProperties(d.motor_gear if d.motor_gear > 0 else d.effort) for d in asset.art.dofs]
 
     def get_asset_actuator_count(self, asset: Asset) -> int:
         return asset.art.num_dofs
 
-    def create_asset_force_sensor(self, asset: Asset, body_idx: int, pose: Transform, props=None):
-        raise NotImplementedError("force sensors belong to the Ant row (SURVEY.md 8f rank 4), not built yet")
+    def create_asset_force_sensor(self, asset: Asset, body_idx: int, pose: Transform, props=None) -> int:
+        """Sensor on a leaf body with identity pose (ant.py:174-178); reads the joint-reaction wrench
+        the body receives from its parent."""
+        p, r = np.array(list(pose.p)), np.array(list(pose.r))
+        if np.any(np.abs(p) > 1e-9) or np.any(np.abs(r - np.array([0, 0, 0, 1.0])) > 1e-9):
+            raise NotImplementedError("force sensors support the identity sensor pose only")
+        asset.sensors.append((int(body_idx), pose))
+        return len(asset.sensors) - 1
 
     # ---- envs / actors
     def create_env(self, sim: Sim, lower: Vec3, upper: Vec3, num_per_row: int) -> Env:
@@ -622,8 +646,9 @@ class Gym:
     def acquire_rigid_body_state_tensor(self, sim: Sim):
         raise NotImplementedError("rigid body state tensor belongs to the UsefulHound row (not built yet)")
 
-    def acquire_force_sensor_tensor(self, sim: Sim):
-        raise NotImplementedError("force sensor tensor belongs to the Ant row (not built yet)")
+    def acquire_force_sensor_tensor(self, sim: Sim) -> GymTensor:
+        """[num_envs * sensors_per_env, 6]: force (3) then torque (3) in the sensor frame (ant.py:80-83)."""
+        return GymTensor(sim.sensor_tensor, "sensor")
 
     def acquire_jacobian_tensor(self, sim: Sim, name: str):
         raise NotImplementedError("jacobian tensor belongs to the UsefulHound row (not built yet)")
@@ -645,7 +670,8 @@ class Gym:
         raise NotImplementedError("rigid body state tensor belongs to the UsefulHound row (not built yet)")
 
     def refresh_force_sensor_tensor(self, sim: Sim):
-        raise NotImplementedError("force sensor tensor belongs to the Ant row (not built yet)")
+        if sim.num_sensors:
+            sim.refresh("sensor")
 
     def refresh_dof_force_tensor(self, sim: Sim):
         return None

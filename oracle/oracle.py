@@ -21,14 +21,16 @@ class OModel(C.Structure):
     _fields_ = [("nb", C.c_int32), ("nd", C.c_int32), ("nc", C.c_int32), ("ns", C.c_int32),
                 ("fixed_base", C.c_int32)] + [
         (n, C.c_void_p) for n in ("parent", "jkind", "bdof", "jorigin", "jaxis", "mass", "com", "inertia",
-                                  "cbody", "cpoint", "cradius", "cshape", "effort", "vmax", "armature")]
+                                  "cbody", "cpoint", "cradius", "cshape", "effort", "vmax", "armature",
+                                  "lower", "upper", "has_limits")] + [
+        ("nsens", C.c_int32), ("sens_body", C.c_void_p)]
 
 
 class OParams(C.Structure):
     _fields_ = [("dt", C.c_double), ("substeps", C.c_int32), ("gravity", C.c_double * 3),
                 ("pos_iters", C.c_int32), ("vel_iters", C.c_int32), ("contact_offset", C.c_double),
                 ("rest_offset", C.c_double), ("max_depen_vel", C.c_double), ("collect_contacts", C.c_int32),
-                ("has_ground", C.c_int32), ("ground_friction", C.c_double)]
+                ("has_ground", C.c_int32), ("ground_friction", C.c_double), ("limit_margin", C.c_double)]
 
 
 def build(quiet: bool = True) -> None:
@@ -47,7 +49,7 @@ def _lib(real_bits: int):
             build()
         lib = C.CDLL(path)
         lib.oracle_simulate.restype = C.c_int
-        lib.oracle_simulate.argtypes = [C.POINTER(OModel), C.POINTER(OParams), C.c_int] + [C.c_void_p] * 5 + [C.c_int]
+        lib.oracle_simulate.argtypes = [C.POINTER(OModel), C.POINTER(OParams), C.c_int] + [C.c_void_p] * 6 + [C.c_int]
         _LIBS[real_bits] = lib
     return _LIBS[real_bits]
 
@@ -55,7 +57,7 @@ def _lib(real_bits: int):
 class OracleSim:
     """Holds the model arrays alive and steps numpy state in place."""
 
-    def __init__(self, flat: dict, params: dict, real_bits: int = 64):
+    def __init__(self, flat: dict, params: dict, real_bits: int = 64, sensor_bodies=()):
         self.flat = flat
         self.real = np.float64 if real_bits == 64 else np.float32
         self.lib = _lib(real_bits)
@@ -63,14 +65,20 @@ class OracleSim:
         m = OModel()
         for k in ("nb", "nd", "nc", "ns", "fixed_base"):
             setattr(m, k, int(flat[k]))
-        for k in ("parent", "jkind", "bdof", "cbody", "cshape"):
+        for k in ("parent", "jkind", "bdof", "cbody", "cshape", "has_limits"):
             a = np.ascontiguousarray(flat[k], dtype=np.int32)
             keep[k] = a
             setattr(m, k, a.ctypes.data)
-        for k in ("jorigin", "jaxis", "mass", "com", "inertia", "cpoint", "cradius", "effort", "vmax", "armature"):
+        for k in ("jorigin", "jaxis", "mass", "com", "inertia", "cpoint", "cradius", "effort", "vmax", "armature",
+                  "lower", "upper"):
             a = np.ascontiguousarray(flat[k], dtype=np.float64)
             keep[k] = a
             setattr(m, k, a.ctypes.data)
+        sb = np.ascontiguousarray(list(sensor_bodies) or [0], dtype=np.int32)
+        keep["sens_body"] = sb
+        m.nsens = len(sensor_bodies)
+        m.sens_body = sb.ctypes.data
+        self.nsens = len(sensor_bodies)
         self._keep = keep
         self.model = m
         p = OParams()
@@ -86,14 +94,16 @@ class OracleSim:
         p.collect_contacts = params.get("collect_contacts", 1)
         p.has_ground = params.get("has_ground", 1)
         p.ground_friction = params.get("ground_friction", 1.0)
+        p.limit_margin = params.get("limit_margin", 0.1)
         self.params = p
 
-    def simulate(self, root, dof, tau, mu, cf=None, num_threads: int = 1) -> None:
-        for a in (root, dof, tau, mu) + ((cf,) if cf is not None else ()):
+    def simulate(self, root, dof, tau, mu, cf=None, num_threads: int = 1, sens=None) -> None:
+        for a in (root, dof, tau, mu) + ((cf,) if cf is not None else ()) + ((sens,) if sens is not None else ()):
             assert a.dtype == self.real and a.flags.c_contiguous
         n = root.shape[0]
         rc = self.lib.oracle_simulate(C.byref(self.model), C.byref(self.params), n, root.ctypes.data,
                                       dof.ctypes.data, tau.ctypes.data, mu.ctypes.data,
-                                      cf.ctypes.data if cf is not None else None, num_threads)
+                                      cf.ctypes.data if cf is not None else None,
+                                      sens.ctypes.data if sens is not None else None, num_threads)
         if rc != 0:
             raise RuntimeError(f"oracle_simulate failed rc={rc}")

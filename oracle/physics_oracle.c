@@ -20,6 +20,8 @@
  *   ground friction / restitution     anymal_terrain.py:188-194
  *   per-shape friction buckets        anymal_terrain.py:236-281
  *   effort limit / velocity limit     anymal_minimal.urdf <limit effort velocity>
+ *   joint limits                      nv_ant.xml <joint range limited="true"> (Ant.yaml)
+ *   force sensors (leaf bodies)       ant.py:174-178, 233-235
  *
  * The formulation here is deliberately different from the kernels: generic
  * runtime topology, dense CRBA mass matrix, dense Cholesky, joint-space
@@ -64,6 +66,11 @@ typedef struct {
     const double *effort;       /* [nd] <= 0 : unlimited */
     const double *vmax;         /* [nd] <= 0 : unlimited */
     const double *armature;     /* [nd] */
+    const double *lower;        /* [nd] joint limits where has_limits */
+    const double *upper;        /* [nd] */
+    const int32_t *has_limits;  /* [nd] */
+    int32_t nsens;              /* force sensors */
+    const int32_t *sens_body;   /* [nsens] leaf bodies */
 } OModel;
 
 typedef struct {
@@ -75,6 +82,7 @@ typedef struct {
     int32_t collect_contacts;
     int32_t has_ground;
     double ground_friction;
+    double limit_margin;        /* joint-limit rows active within this distance of a limit */
 } OParams;
 
 /* ---------------------------------------------------------------- helpers */
@@ -168,7 +176,7 @@ static void chol_solve(const real *L, int n, const real *b, real *x) {
 /* ------------------------------------------------------------- one env */
 static void env_substep(const OModel *m, const OParams *p, real h,
                         real *root, real *dq, const real *tau_in, const real *mu_shape,
-                        real *cforce /* nb*3 or NULL */)
+                        real *cforce /* nb*3 or NULL */, real *sens /* nsens*6 or NULL */)
 {
     const int nb = m->nb, nd = m->nd, fb = m->fixed_base;
     const int nbase = fb ? 0 : 6, nv = nbase + nd;
@@ -257,6 +265,8 @@ static void env_substep(const OModel *m, const OParams *p, real h,
         crf(V[i], iv, x);
         for (int k = 0; k < 6; ++k) F[i][k] = ia[k] + x[k];
     }
+    real Fown[MAXB][6];
+    memcpy(Fown, F, sizeof(F));
     for (int i = nb - 1; i > 0; --i)
         for (int k = 0; k < 6; ++k) F[m->parent[i]][k] += F[i][k];
     real bias[MAXV];
@@ -313,6 +323,27 @@ static void env_substep(const OModel *m, const OParams *p, real h,
         for (int k = 0; k < 3; ++k) nuf[3 + k] += h * wxp[k];
     }
 
+    /* ---- joint limits: one unilateral row per dof within limit_margin of a limit,
+     * J = +e (lower) / -e (upper), solved before the contacts in dof order */
+    int nlim = 0, ldof[MAXV];
+    real lsgn[MAXV], lsep[MAXV], LJ[MAXV * MAXV], LW[MAXV * MAXV], LD[MAXV];
+    for (int j = 0; j < nd; ++j) {
+        if (!(m->has_limits && m->has_limits[j] && m->upper[j] > m->lower[j])) continue;
+        const real q = dq[2 * j];
+        const real lo = q - (real)m->lower[j], hi = (real)m->upper[j] - q;
+        if (!(lo < (real)p->limit_margin || hi < (real)p->limit_margin)) continue;
+        const real sg = lo <= hi ? 1 : -1;
+        real *Jr = LJ + nlim * MAXV, *Wr = LW + nlim * MAXV;
+        for (int k = 0; k < nv; ++k) Jr[k] = 0;
+        Jr[nbase + j] = sg;
+        chol_solve(M, nv, Jr, Wr);
+        LD[nlim] = sg * Wr[nbase + j];
+        ldof[nlim] = j;
+        lsgn[nlim] = sg;
+        lsep[nlim] = lo <= hi ? lo : hi;
+        ++nlim;
+    }
+
     /* ---- contacts vs the ground plane z = 0 */
     int nact = 0;
     int ck[MAXC];
@@ -364,12 +395,27 @@ static void env_substep(const OModel *m, const OParams *p, real h,
     }
 
     /* ---- sequential impulses (joint space) */
-    real v[MAXV], lam[3 * MAXC], nupos[MAXV];
+    real v[MAXV], lam[3 * MAXC], nupos[MAXV], laml[MAXV];
     memcpy(v, nuf, sizeof(real) * nv);
     for (int k = 0; k < 3 * nact; ++k) lam[k] = 0;
+    for (int k = 0; k < nlim; ++k) laml[k] = 0;
     const int iters = p->pos_iters + p->vel_iters;
     for (int it = 0; it < iters; ++it) {
         const int pos_phase = it < p->pos_iters;
+        for (int a = 0; a < nlim; ++a) {
+            const real s = lsep[a];
+            const real u = lsgn[a] * v[nbase + ldof[a]];
+            real target;
+            if (s >= 0) target = -s / h;
+            else if (pos_phase) { target = -s / h; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
+            else target = 0;
+            real ln = laml[a] + (target - u) / LD[a];
+            if (ln < 0) ln = 0;
+            const real dl = ln - laml[a];
+            laml[a] = ln;
+            const real *Wr = LW + a * MAXV;
+            for (int k = 0; k < nv; ++k) v[k] += Wr[k] * dl;
+        }
         for (int a = 0; a < nact; ++a) {
             const real s = cs[a];
             /* normal */
@@ -443,6 +489,47 @@ static void env_substep(const OModel *m, const OParams *p, real h,
             cforce[3 * b + 2] += lam[3 * a + 0] / h;
         }
     }
+    if (sens && m->nsens > 0) {
+        /* joint-reaction wrench of each sensor (leaf) body: I a + v x* I v - f_contact, with the
+         * substep's accelerations (RNEA form, gravity offset in A) -> body origin, body axes */
+        real ab[6] = {0, 0, 0, 0, 0, 0};
+        if (!fb) {
+            real wxp[3];
+            cross3(nu, nu + 3, wxp);
+            for (int k = 0; k < 3; ++k) { ab[k] = (v[k] - nu[k]) / h; ab[3 + k] = (v[3 + k] - nu[3 + k]) / h - wxp[k]; }
+        }
+        for (int si = 0; si < m->nsens; ++si) {
+            const int b = m->sens_body[si];
+            real a6[6], ia[6], f[6];
+            for (int k = 0; k < 6; ++k) a6[k] = ab[k];
+            for (int i = b; i > 0; i = m->parent[i]) {
+                const int g = nbase + m->bdof[i];
+                const real qdd = (v[g] - nu[g]) / h;
+                for (int k = 0; k < 6; ++k) a6[k] += S[i][k] * qdd;
+            }
+            spi_mul(&Ib[b], a6, ia);
+            for (int k = 0; k < 6; ++k) f[k] = Fown[b][k] + ia[k];
+            for (int a = 0; a < nact; ++a) {
+                const int c = ck[a];
+                if (m->cbody[c] != b) continue;
+                real xl[3], x[3], fc[3], n[3];
+                for (int k = 0; k < 3; ++k) xl[k] = (real)m->cpoint[3 * c + k];
+                matvec3(R[b], xl, x);
+                for (int k = 0; k < 3; ++k) x[k] += P[b][k];
+                x[2] -= (real)m->cradius[c];
+                fc[0] = lam[3 * a + 1] / h; fc[1] = lam[3 * a + 2] / h; fc[2] = lam[3 * a] / h;
+                cross3(x, fc, n);
+                for (int k = 0; k < 3; ++k) { f[k] -= n[k]; f[3 + k] -= fc[k]; }
+            }
+            real xf[3], tq[3];
+            cross3(P[b], f + 3, xf);
+            for (int k = 0; k < 3; ++k) tq[k] = f[k] - xf[k];
+            for (int k = 0; k < 3; ++k) {
+                sens[6 * si + k] = R[b][k] * f[3] + R[b][3 + k] * f[4] + R[b][6 + k] * f[5];
+                sens[6 * si + 3 + k] = R[b][k] * tq[0] + R[b][3 + k] * tq[1] + R[b][6 + k] * tq[2];
+            }
+        }
+    }
 }
 
 /*
@@ -452,9 +539,10 @@ static void env_substep(const OModel *m, const OParams *p, real h,
  * tau   : [N][nd]
  * mu    : [N][ns]     per-env shape friction
  * cf    : [N][nb][3]  net contact force (written when collect_contacts), may be NULL
+ * sens  : [N][nsens][6] force-sensor readings of the last substep, may be NULL
  */
 int oracle_simulate(const OModel *m, const OParams *p, int n_envs, real *root, real *dof,
-                    const real *tau, const real *mu, real *cf, int num_threads)
+                    const real *tau, const real *mu, real *cf, real *sens, int num_threads)
 {
     if (m->nb > MAXB || m->nd + 6 > MAXV || m->nc > MAXC) return -1;
     const real h = (real)(p->dt / (p->substeps > 0 ? p->substeps : 1));
@@ -466,7 +554,8 @@ int oracle_simulate(const OModel *m, const OParams *p, int n_envs, real *root, r
         for (int s = 0; s < p->substeps; ++s) {
             const int last = (s == p->substeps - 1);
             env_substep(m, p, h, root + 13 * e, dof + 2 * m->nd * e, tau + m->nd * e, mu + m->ns * e,
-                        (cf && p->collect_contacts && last) ? cf + 3 * m->nb * e : NULL);
+                        (cf && p->collect_contacts && last) ? cf + 3 * m->nb * e : NULL,
+                        (sens && last) ? sens + 6 * m->nsens * e : NULL);
         }
     }
     (void)num_threads;

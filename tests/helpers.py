@@ -22,6 +22,13 @@ CARTPOLE_PARAMS = dict(dt=0.0166, substeps=2, gravity=[0.0, 0.0, -9.81], pos_ite
                        has_ground=1, ground_friction=1.0)
 
 
+# Ant.yaml:42-61 (dt 1/60, 2 substeps, 4/0 iterations, contact collection never)
+ANT_PARAMS = dict(dt=0.0166, substeps=2, gravity=[0.0, 0.0, -9.81], pos_iters=4, vel_iters=0,
+                  contact_offset=0.02, rest_offset=0.0, max_depen_vel=10.0, collect_contacts=0,
+                  has_ground=1, ground_friction=1.0, limit_margin=0.1)
+ANT_FEET = [2, 4, 6, 8]  # bodies whose names contain "foot" (ant.py:166-173)
+
+
 def load_art(name, opts):
     with open(os.path.join(PACKED_DIR, name)) as f:
         return build_articulation(RawModel.from_json(json.load(f)), opts)
@@ -35,6 +42,34 @@ def anymal():
 def cartpole():
     art = load_art("cartpole.model.json", CARTPOLE_OPTS)
     return art, flatten(art)
+
+
+def ant():
+    art = load_art("nv_ant.model.json", dict(angular_damping=0.0))
+    return art, flatten(art)
+
+
+def ant_states(n, seed=0, spread=1.0):
+    """Random Ant states: near/on/into the ground, dofs anywhere in (and slightly beyond) their limits."""
+    rng = np.random.RandomState(seed)
+    art, flat = ant()
+    lo, hi = flat["lower"], flat["upper"]
+    root = np.zeros((n, 13))
+    root[:, 0:2] = rng.uniform(-2, 2, (n, 2))
+    root[:, 2] = rng.uniform(0.2, 0.6, n)
+    axis = rng.normal(size=(n, 3))
+    axis /= np.linalg.norm(axis, axis=1, keepdims=True)
+    ang = rng.uniform(0, 0.4 * spread, n)
+    root[:, 3:6] = axis * np.sin(ang / 2)[:, None]
+    root[:, 6] = np.cos(ang / 2)
+    root[:, 7:10] = rng.normal(0, 0.5 * spread, (n, 3))
+    root[:, 10:13] = rng.normal(0, 1.0 * spread, (n, 3))
+    dof = np.zeros((n, 8, 2))
+    dof[:, :, 0] = rng.uniform(lo - 0.05, hi + 0.05, (n, 8))
+    dof[:, :, 1] = rng.normal(0, 2.0 * spread, (n, 8))
+    tau = rng.uniform(-15, 15, (n, 8))
+    mu = np.full((n, flat["ns"]), 1.5)
+    return root, dof, tau, mu
 
 
 def anymal_states(n, seed=0, spread=1.0):
@@ -83,18 +118,25 @@ def make_gpu_sim(kind: str, n: int, params: dict):
         plane.static_friction = params.get("ground_friction", 1.0)
         gym.add_ground(sim, plane)
     opts = gymapi.AssetOptions()
+    sensors = []
     if kind == "anymal":
         opts.collapse_fixed_joints = True
         opts.replace_cylinder_with_capsule = True
         opts.default_dof_drive_mode = gymapi.DOF_MODE_EFFORT
         asset = gym.load_asset(sim, "/nonexistent", "urdf/anymal_c/urdf/anymal_minimal.urdf", opts)
+    elif kind == "ant":
+        opts.default_dof_drive_mode = gymapi.DOF_MODE_NONE
+        opts.angular_damping = 0.0
+        asset = gym.load_asset(sim, "/nonexistent", "mjcf/nv_ant.xml", opts)
+        for b in ANT_FEET:
+            gym.create_asset_force_sensor(asset, b, gymapi.Transform())
     else:
         opts.fix_base_link = True
         asset = gym.load_asset(sim, "/nonexistent", "urdf/cartpole.urdf", opts)
     for i in range(n):
         env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 1), 8)
         pose = gymapi.Transform()
-        pose.p = gymapi.Vec3(0, 0, 0.62 if kind == "anymal" else 2.0)
+        pose.p = gymapi.Vec3(0, 0, {"anymal": 0.62, "ant": 0.44}.get(kind, 2.0))
         gym.create_actor(env, asset, pose, kind, i, 0, 0)
     gym.prepare_sim(sim)
     return gym, sim

@@ -26,6 +26,7 @@ from isaacgymenv_amd.isaacgym._model import flatten, topology_signature  # noqa:
 MODELS = [
     ("anymal_c", "anymal_c.model.json", dict(collapse_fixed_joints=True, replace_cylinder_with_capsule=True)),
     ("cartpole", "cartpole.model.json", dict(fix_base_link=True)),
+    ("nv_ant", "nv_ant.model.json", dict()),
 ]
 
 OUT = os.path.join(ROOT, "isaacgymenv_amd", "csrc", "gs_topologies.h")
@@ -67,6 +68,13 @@ def topo_tables(flat: dict) -> dict:
     for s in csupp:
         cslot.append(off)
         off += 3 * s + 6
+    # joint-limit rows, one potential row per dof (node nbase + j): scaled Z (supp) + c + 1/diag
+    lleaf = [nbase + j for j in range(nd)]
+    lsupp = [len(anc[l]) + 1 for l in lleaf]
+    lslot = []
+    for s in lsupp:
+        lslot.append(off)
+        off += s + 2
     gbody = [0] * nbase + [body_of_dof[j] for j in range(nd)]
     # last body (DFS order) of each body's subtree: where its subtree sums are complete
     subend = list(range(nb))
@@ -78,7 +86,8 @@ def topo_tables(flat: dict) -> dict:
     return dict(TEAM=team, NB=nb, ND=nd, NC=nc, NS=int(flat["ns"]), FIXED=fixed, NBASE=nbase, NV=nv, MAXDEP=maxdep,
                 parent=parent, bdof=bdof, jkind=jkind, dpar=dpar, depth=[len(a) for a in anc],
                 anc=[a + [-1] * (maxdep - len(a)) for a in anc], bgdof=bgdof, cbody=cbody, cleaf=cleaf,
-                csupp=csupp, cslot=cslot, NSLOT=max(off, 1), gbody=gbody, cshape=cshape, subend=subend)
+                csupp=csupp, cslot=cslot, NSLOT=max(off, 1), gbody=gbody, cshape=cshape, subend=subend,
+                lleaf=lleaf, lsupp=lsupp, lslot=lslot)
 
 
 def team_tables(flat, parent, bdof, nbase):
@@ -101,7 +110,7 @@ def team_tables(flat, parent, bdof, nbase):
             ch.append(cur)
         chains.append(ch)
     nch, cl = len(chains), len(chains[0])
-    if any(len(c) != cl for c in chains) or nch > 8:
+    if any(len(c) != cl for c in chains) or nch > 8 or cl != 3:  # the team PGS distributes 6 + 3 components
         return None
     # chains must be contiguous in body order with dofs in the same order
     for c, ch in enumerate(chains):
@@ -160,7 +169,8 @@ def emit() -> str:
         for k in ("NB", "ND", "NC", "NS", "FIXED", "NBASE", "NV", "MAXDEP", "NSLOT"):
             lines.append(f"  static constexpr int {k} = {t[k]};")
         for k, n in (("parent", "NB"), ("bdof", "NB"), ("jkind", "NB"), ("bgdof", "NB"), ("subend", "NB"), ("dpar", "NV"),
-                     ("depth", "NV"), ("gbody", "NV"), ("cbody", "NC"), ("cshape", "NC"), ("cleaf", "NC"), ("csupp", "NC"), ("cslot", "NC")):
+                     ("depth", "NV"), ("gbody", "NV"), ("cbody", "NC"), ("cshape", "NC"), ("cleaf", "NC"), ("csupp", "NC"), ("cslot", "NC"),
+                     ("lleaf", "ND"), ("lsupp", "ND"), ("lslot", "ND")):
             vals = t[k] if len(t[k]) else [0]
             dim = n if len(t[k]) else "1"
             lines.append(f"  static constexpr int {k}[{dim}] = {carr(vals)};")

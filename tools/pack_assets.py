@@ -16,19 +16,22 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from isaacgymenv_amd.isaacgym._assets import parse_urdf, PACKED_DIR  # noqa: E402
+from isaacgymenv_amd.isaacgym._mjcf import parse_mjcf  # noqa: E402
 
 REF = "/root/reference/assets"
 SOURCES = {
     "anymal_c.model.json": "urdf/anymal_c/urdf/anymal_minimal.urdf",
     "cartpole.model.json": "urdf/cartpole.urdf",
     "hound.model.json": "urdf/UsefulHound/urdf/Hound.urdf",
+    "nv_ant.model.json": "mjcf/nv_ant.xml",
 }
 
 
 def main():
     os.makedirs(PACKED_DIR, exist_ok=True)
     for out, src in SOURCES.items():
-        raw = parse_urdf(os.path.join(REF, src))
+        path = os.path.join(REF, src)
+        raw = parse_mjcf(path) if src.endswith(".xml") else parse_urdf(path)
         with open(os.path.join(PACKED_DIR, out), "w") as f:
             json.dump(raw.to_json(), f, indent=1)
         print("packed", src, "->", out)
