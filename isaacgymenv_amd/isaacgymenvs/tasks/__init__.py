@@ -1,8 +1,10 @@
 """Task registry (reference ``tasks/__init__.py:90-119``), in-scope tasks only."""
+from .ant import Ant
 from .anymal_terrain import AnymalTerrain
 from .cartpole import Cartpole
 
 isaacgym_task_map = {
+    "Ant": Ant,
     "AnymalTerrain": AnymalTerrain,
     "Cartpole": Cartpole,
 }

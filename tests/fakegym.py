@@ -29,9 +29,10 @@ class FakeSim:
 class FakeGym(_g.Gym):
     """Pure-python Gym whose simulate() is a seeded deterministic rule."""
 
-    def __init__(self, seed: int = 12345, dof_drift: float = 0.0):
+    def __init__(self, seed: int = 12345, dof_drift: float = 0.0, z_drift: float = 0.0):
         self.seed = seed
         self.dof_drift = dof_drift  # pushes joints out of range over time (exercises limit resets)
+        self.z_drift = z_drift      # sinks random roots (exercises height terminations)
 
     # ---- sim lifecycle
     def create_sim(self, compute_device=0, graphics_device=-1, type=_g.SIM_PHYSX, params=None):
@@ -57,6 +58,9 @@ class FakeGym(_g.Gym):
         sim.root_t = torch.zeros(N, 13, dtype=f)
         sim.dof_t = torch.zeros(N * nd, 2, dtype=f)
         sim.cf_t = torch.zeros(N * nb, 3, dtype=f)
+        sim.ns = len(sim.asset.sensors)
+        sim.sens = torch.zeros(N * sim.ns, 6, dtype=f)
+        sim.sens_t = torch.zeros(N * sim.ns, 6, dtype=f)
         names = art.body_names()
         self.feet = [i for i, n in enumerate(names) if ("SHANK" in n or "foot" in n) and i > 0]
         self.knees = [i for i, n in enumerate(names) if ("THIGH" in n or "thigh" in n) and i > 0]
@@ -85,6 +89,10 @@ class FakeGym(_g.Gym):
             cf[:, k, 2] = np.where(rng.rand(N) < 0.6, 50.0, 0.0)
             cf[:, k, :2] = rng.normal(0, 3.0, (N, 2))
         sim.cf.copy_(torch.from_numpy(cf.reshape(N * nb, 3)))
+        if self.z_drift:
+            sim.root[:, 2].sub_(t32(self.z_drift * (rng.rand(N) < 0.3)))
+        if sim.ns:
+            sim.sens.copy_(t32(rng.normal(0, 20.0, (N * sim.ns, 6))))
 
     def fetch_results(self, sim, wait=True):
         return None
@@ -98,6 +106,12 @@ class FakeGym(_g.Gym):
 
     def acquire_net_contact_force_tensor(self, sim):
         return _g.GymTensor(sim.cf_t, "contact")
+
+    def acquire_force_sensor_tensor(self, sim):
+        return _g.GymTensor(sim.sens_t, "sensor")
+
+    def refresh_force_sensor_tensor(self, sim):
+        sim.sens_t.copy_(sim.sens)
 
     def refresh_actor_root_state_tensor(self, sim):
         sim.root_t.copy_(sim.root)

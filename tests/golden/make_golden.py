@@ -10,7 +10,7 @@ torch RNG call order (friction buckets, terrain levels, reset draws, push, obs
 noise).  Only the resulting arrays are committed (tests/golden/*.npz); the
 reference never travels to the GPU box.
 
-    python tests/golden/make_golden.py            # writes anymal_terrain.npz, cartpole.npz
+    python tests/golden/make_golden.py            # writes anymal_terrain.npz, cartpole.npz, ant.npz
 """
 from __future__ import annotations
 
@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 
 N_ANYMAL, STEPS_ANYMAL = 32, 30
 N_CARTPOLE, STEPS_CARTPOLE = 16, 40
+N_ANT, STEPS_ANT = 16, 40
 
 
 def anymal_cfg(num_envs: int) -> dict:
@@ -45,6 +46,14 @@ def anymal_cfg(num_envs: int) -> dict:
 def cartpole_cfg(num_envs: int) -> dict:
     from isaacgymenv_amd.isaacgymenvs.config import compose
     return compose("config", ["task=Cartpole", f"num_envs={num_envs}", "sim_device=cpu", "pipeline=cpu"])["task"]
+
+
+def ant_cfg(num_envs: int) -> dict:
+    """Ant.yaml with a 25-step episode so a 40-step fixture holds timeouts next to height terminations."""
+    from isaacgymenv_amd.isaacgymenvs.config import compose
+    cfg = compose("config", ["task=Ant", f"num_envs={num_envs}", "sim_device=cpu", "pipeline=cpu"])["task"]
+    cfg["env"]["episodeLength"] = 25
+    return cfg
 
 
 def install_reference_stubs(fake):
@@ -194,6 +203,43 @@ def record_cartpole(num_envs=N_CARTPOLE, steps=STEPS_CARTPOLE):
             "time_outs": np.stack(to_l), "cfg_yaml": np.array(yaml.safe_dump(cfg))}
 
 
+def record_ant(num_envs=N_ANT, steps=STEPS_ANT):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fakegym import FakeGym
+    fake = FakeGym(seed=4242, dof_drift=2.0, z_drift=0.02)
+    install_reference_stubs(fake)
+    import importlib
+    ref = importlib.import_module("isaacgymenvs.tasks.ant")
+    cfg = ant_cfg(num_envs)
+    torch.manual_seed(42)
+    env = ref.Ant(copy.deepcopy(cfg), "cpu", "cpu", -1, True, False, False)
+    out = {"joint_gears": _np(env.joint_gears), "dof_limits_lower": _np(env.dof_limits_lower),
+           "dof_limits_upper": _np(env.dof_limits_upper), "initial_dof_pos": _np(env.initial_dof_pos),
+           "extremities_index": _np(env.extremities_index), "initial_root_states": _np(env.initial_root_states)}
+    rng = np.random.RandomState(13)
+    actions = (2.4 * rng.rand(steps, num_envs, 8) - 1.2).astype(np.float32)  # beyond clipActions=1
+    recs = {k: [] for k in ("obs", "rew", "reset", "time_outs", "progress", "potentials", "prev_potentials",
+                            "true_objective", "dof_state", "root_states")}
+    for t in range(steps):
+        obs, rew, reset, extras = env.step(torch.from_numpy(actions[t]))
+        recs["obs"].append(_np(obs["obs"]))
+        recs["rew"].append(_np(rew))
+        recs["reset"].append(_np(reset).astype(np.int64))
+        recs["time_outs"].append(_np(extras["time_outs"]).astype(np.int64))
+        recs["progress"].append(_np(env.progress_buf))
+        recs["potentials"].append(_np(env.potentials))
+        recs["prev_potentials"].append(_np(env.prev_potentials))
+        recs["true_objective"].append(_np(extras["true_objective"]))
+        recs["dof_state"].append(_np(env.dof_state))
+        recs["root_states"].append(_np(env.root_states))
+        assert reset.dtype == torch.int64
+    for k, v in recs.items():
+        out[k] = np.stack(v)
+    out["actions"] = actions
+    out["cfg_yaml"] = np.array(yaml.safe_dump(cfg))
+    return out
+
+
 def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     if which in ("all", "anymal"):
@@ -209,6 +255,14 @@ def main():
             d = record_cartpole()
             np.savez_compressed(os.path.join(HERE, "cartpole.npz"), **d)
             print("cartpole.npz:", {k: v.shape for k, v in d.items() if hasattr(v, "shape")})
+    if which in ("all", "ant"):
+        if which == "all":
+            import subprocess
+            subprocess.check_call([sys.executable, __file__, "ant"])
+        else:
+            d = record_ant()
+            np.savez_compressed(os.path.join(HERE, "ant.npz"), **d)
+            print("ant.npz:", {k: v.shape for k, v in d.items() if hasattr(v, "shape")})
 
 
 if __name__ == "__main__":

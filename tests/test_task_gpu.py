@@ -159,3 +159,42 @@ def test_cartpole_gpu_runs(monkeypatch):
         assert reset.dtype == torch.int64
         assert torch.isfinite(obs["obs"]).all()
     assert float(obs["obs"].abs().max()) <= 5.0  # clipObservations
+
+
+def test_ant_gpu_episode(monkeypatch):
+    """Ant (A13) on the real simulator: standing still it stays upright with its weight carried by the
+    foot sensors; under random torques some ants fall (height < terminationHeight) and are reset, and
+    every env that never fell resets together at the episode end."""
+    n = 512
+    env = _make("Ant", n, monkeypatch)
+    assert env.obs_buf.shape == (n, 60) and env.reset_buf.dtype == torch.int64
+    zero = torch.zeros((n, 8), device="cuda:0")
+    env.step(zero)  # the initial all-envs reset happens on the first step
+    for _ in range(60):
+        obs, rew, reset, extras = env.step(zero)
+    o = obs["obs"]
+    assert torch.isfinite(o).all()
+    assert float((o[:, 10] > 0.93).float().mean()) > 0.95, "resting ants stay upright"
+    assert not bool(reset.any())
+    z = env.root_states[:, 2]
+    assert 0.31 < float(z.min()) and float(z.max()) < 0.7
+    # weight of everything above the feet hangs on the four foot joints (DESIGN.md 3.6)
+    from tests.helpers import ANT_FEET, ant
+    mass = ant()[1]["mass"]
+    load = 9.81 * (float(np.sum(mass)) - float(np.sum(mass[ANT_FEET])))
+    # (readings are in the tilted foot frames, so compare the sum of magnitudes, which bounds the
+    # world-frame resultant from above; a leg resting on the plane bypasses the sensors -> median)
+    f = env.vec_sensor_tensor.view(n, 4, 6)[:, :, 0:3].norm(dim=-1).sum(1)
+    assert 0.6 * load < float(f.median()) < 2.5 * load, (float(f.median()), load)
+    # random torques: falls and resets happen, the episode end resets the survivors
+    gen = torch.Generator(device="cuda:0").manual_seed(3)
+    dones = []
+    for t in range(1000):
+        a = 2 * torch.rand((n, 8), device="cuda:0", generator=gen) - 1
+        obs, rew, reset, extras = env.step(a)
+        if t % 100 == 0:
+            assert torch.isfinite(obs["obs"]).all() and torch.isfinite(rew).all()
+        dones.append(reset.clone())
+    d = torch.stack(dones)
+    assert int(d.sum()) >= n // 4
+    assert torch.isfinite(extras["true_objective"]).all()
