@@ -32,7 +32,7 @@ import os
 import numpy as np
 import torch
 
-from isaacgym import gymapi, gymtorch
+from isaacgym import gymapi, gymtorch, terrain_utils
 
 from ..utils.torch_jit_utils import (get_axis_params, normalize, quat_apply, quat_rotate_inverse, to_torch,
                                      torch_rand_float)
@@ -158,7 +158,8 @@ class AnymalTerrain(VecTask):
         if terrain_type == "plane":
             self._create_ground_plane()
         elif terrain_type == "trimesh":
-            raise NotImplementedError("terrainType=trimesh is SURVEY.md section 8f rank 1 (not built in round 1)")
+            self._create_trimesh()
+            self.custom_origins = True
         self._create_envs(self.num_envs, self.cfg["env"]["envSpacing"], int(np.sqrt(self.num_envs)))
 
     def _get_noise_scale_vec(self, cfg):
@@ -184,6 +185,25 @@ class AnymalTerrain(VecTask):
         plane.dynamic_friction = t["dynamicFriction"]
         plane.restitution = t["restitution"]
         self.gym.add_ground(self.sim, plane)
+
+    def _create_trimesh(self):
+        """anymal_terrain.py:196-209: the generated heightfield as a triangle mesh placed at
+        (-border, -border, 0), and the raw int16 samples kept on the device for get_heights."""
+        t = self.cfg["env"]["terrain"]
+        self.terrain = Terrain(t, num_robots=self.num_envs)
+        tm = gymapi.TriangleMeshParams()
+        tm.nb_vertices = self.terrain.vertices.shape[0]
+        tm.nb_triangles = self.terrain.triangles.shape[0]
+        tm.transform.p.x = -self.terrain.border_size
+        tm.transform.p.y = -self.terrain.border_size
+        tm.transform.p.z = 0.0
+        tm.static_friction = t["staticFriction"]
+        tm.dynamic_friction = t["dynamicFriction"]
+        tm.restitution = t["restitution"]
+        self.gym.add_triangle_mesh(self.sim, self.terrain.vertices.flatten(order="C"),
+                                   self.terrain.triangles.flatten(order="C"), tm)
+        self.height_samples = torch.tensor(self.terrain.heightsamples).view(
+            self.terrain.tot_rows, self.terrain.tot_cols).to(self.device)
 
     def _asset_location(self):
         here = os.path.dirname(os.path.abspath(__file__))
@@ -235,6 +255,9 @@ class AnymalTerrain(VecTask):
             tcfg["maxInitMapLevel"] = tcfg["numLevels"] - 1
         self.terrain_levels = torch.randint(0, tcfg["maxInitMapLevel"] + 1, (self.num_envs,), device=self.device)
         self.terrain_types = torch.randint(0, tcfg["numTerrains"], (self.num_envs,), device=self.device)
+        if self.custom_origins:
+            self.terrain_origins = torch.from_numpy(self.terrain.env_origins).to(self.device).to(torch.float)
+            spacing = 0.0
 
         lower = gymapi.Vec3(-spacing, -spacing, 0.0)
         upper = gymapi.Vec3(spacing, spacing, spacing)
@@ -244,6 +267,12 @@ class AnymalTerrain(VecTask):
         friction_host = friction_buckets.cpu().numpy()[:, 0]
         for i in range(self.num_envs):
             env_handle = self.gym.create_env(self.sim, lower, upper, num_per_row)
+            if self.custom_origins:
+                # spawn on the env's terrain tile, +-1 m (anymal_terrain.py:271-275)
+                self.env_origins[i] = self.terrain_origins[self.terrain_levels[i], self.terrain_types[i]]
+                pos = self.env_origins[i].clone()
+                pos[:2] += torch_rand_float(-1.0, 1.0, (2, 1), device=self.device).squeeze(1)
+                start_pose.p = gymapi.Vec3(*pos.tolist())
             for sp in shape_props:
                 sp.friction = friction_host[i % num_buckets]
             self.gym.set_asset_rigid_shape_properties(asset, shape_props)
@@ -364,9 +393,16 @@ class AnymalTerrain(VecTask):
                                               gymtorch.unwrap_tensor(env_ids_int32), len(env_ids_int32))
 
     def update_terrain_level(self, env_ids):
+        """anymal_terrain.py:427-435: an env that walked less than a quarter of its commanded
+        distance moves a level down, one that left its tile moves up (levels wrap modulo numLevels)."""
         if not self.init_done or not self.curriculum:
             return
-        raise NotImplementedError("terrain curriculum belongs to the trimesh row (not built in round 1)")
+        distance = torch.norm(self.root_states[env_ids, :2] - self.env_origins[env_ids, :2], dim=1)
+        self.terrain_levels[env_ids] -= 1 * (distance < torch.norm(self.commands[env_ids, :2]) *
+                                             self.max_episode_length_s * 0.25)
+        self.terrain_levels[env_ids] += 1 * (distance > self.terrain.env_length / 2)
+        self.terrain_levels[env_ids] = torch.clip(self.terrain_levels[env_ids], 0) % self.terrain.env_rows
+        self.env_origins[env_ids] = self.terrain_origins[self.terrain_levels[env_ids], self.terrain_types[env_ids]]
 
     def push_robots(self):
         self.root_states[:, 7:9] = torch_rand_float(-1.0, 1.0, (self.num_envs, 2), device=self.device)
@@ -472,7 +508,136 @@ class AnymalTerrain(VecTask):
             return torch.zeros(self.num_envs, self.num_height_points, device=self.device, requires_grad=False)
         if ttype == "none":
             raise NameError("Can't measure height with terrain type 'none'")
-        raise NotImplementedError("heightfield sampling belongs to the trimesh row (not built in round 1)")
+        return sample_heights(self.height_samples, self.base_quat, self.root_states, self.height_points,
+                              self.terrain.border_size, self.terrain.horizontal_scale,
+                              self.terrain.vertical_scale, env_ids)
+
+
+def sample_heights(height_samples, base_quat, root_states, height_points, border: float, hs: float, vs: float,
+                   env_ids=None):
+    """get_heights (anymal_terrain.py:515-538): the 14x10 probe grid turned by the base yaw and
+    placed at the base, truncated to heightfield cells (clipped to the second-last row/column),
+    the lower of the samples at (px, py) and (px+1, py+1), in metres."""
+    nh = height_points.shape[1]
+    if env_ids:
+        pts = quat_apply_yaw(base_quat[env_ids].repeat(1, nh), height_points[env_ids]) + \
+            root_states[env_ids, :3].unsqueeze(1)
+    else:
+        pts = quat_apply_yaw(base_quat.repeat(1, nh), height_points) + root_states[:, :3].unsqueeze(1)
+    pts += border
+    pts = (pts / hs).long()
+    px = torch.clip(pts[:, :, 0].view(-1), 0, height_samples.shape[0] - 2)
+    py = torch.clip(pts[:, :, 1].view(-1), 0, height_samples.shape[1] - 2)
+    h = torch.min(height_samples[px, py], height_samples[px + 1, py + 1])
+    return h.view(pts.shape[0], -1) * vs
+
+
+class Terrain:
+    """The terrain map of anymal_terrain.py:543-673: numLevels x numTerrains tiles of
+    mapLength x mapWidth metres inside a 20 m border, int16 heights (0.005 m units, 0.1 m cells),
+    converted to a triangle mesh with vertical walls above slopeTreshold.  Curriculum maps vary
+    difficulty along the level axis and terrain kind along the type axis (terrainProportions);
+    env origins sit at each tile's centre on top of its highest point within +-1 m."""
+
+    horizontal_scale = 0.1
+    vertical_scale = 0.005
+    border_size = 20
+
+    def __init__(self, cfg, num_robots):
+        self.type = cfg["terrainType"]
+        if self.type in ("none", "plane"):
+            return
+        self.env_length = cfg["mapLength"]
+        self.env_width = cfg["mapWidth"]
+        props = cfg["terrainProportions"]
+        self.proportions = [np.sum(props[:i + 1]) for i in range(len(props))]
+        self.env_rows = cfg["numLevels"]
+        self.env_cols = cfg["numTerrains"]
+        self.num_maps = self.env_rows * self.env_cols
+        self.num_per_env = int(num_robots / self.num_maps)
+        self.env_origins = np.zeros((self.env_rows, self.env_cols, 3))
+        self.width_per_env_pixels = int(self.env_width / self.horizontal_scale)
+        self.length_per_env_pixels = int(self.env_length / self.horizontal_scale)
+        self.border = int(self.border_size / self.horizontal_scale)
+        self.tot_cols = int(self.env_cols * self.width_per_env_pixels) + 2 * self.border
+        self.tot_rows = int(self.env_rows * self.length_per_env_pixels) + 2 * self.border
+        self.height_field_raw = np.zeros((self.tot_rows, self.tot_cols), dtype=np.int16)
+        if cfg["curriculum"]:
+            self.curiculum(num_robots, num_terrains=self.env_cols, num_levels=self.env_rows)
+        else:
+            self.randomized_terrain()
+        self.heightsamples = self.height_field_raw
+        self.vertices, self.triangles = terrain_utils.convert_heightfield_to_trimesh(
+            self.height_field_raw, self.horizontal_scale, self.vertical_scale, cfg["slopeTreshold"])
+
+    def _tile(self):
+        return terrain_utils.SubTerrain("terrain", width=self.width_per_env_pixels, length=self.width_per_env_pixels,
+                                        vertical_scale=self.vertical_scale, horizontal_scale=self.horizontal_scale)
+
+    def _place(self, i, j, tile):
+        x0 = self.border + i * self.length_per_env_pixels
+        y0 = self.border + j * self.width_per_env_pixels
+        self.height_field_raw[x0:x0 + self.length_per_env_pixels, y0:y0 + self.width_per_env_pixels] = \
+            tile.height_field_raw
+        x1 = int((self.env_length / 2.0 - 1) / self.horizontal_scale)
+        x2 = int((self.env_length / 2.0 + 1) / self.horizontal_scale)
+        y1 = int((self.env_width / 2.0 - 1) / self.horizontal_scale)
+        y2 = int((self.env_width / 2.0 + 1) / self.horizontal_scale)
+        top = np.max(tile.height_field_raw[x1:x2, y1:y2]) * self.vertical_scale
+        self.env_origins[i, j] = [(i + 0.5) * self.env_length, (j + 0.5) * self.env_width, top]
+
+    def randomized_terrain(self):
+        tu = terrain_utils
+        for k in range(self.num_maps):
+            i, j = np.unravel_index(k, (self.env_rows, self.env_cols))
+            tile = self._tile()
+            choice = np.random.uniform(0, 1)
+            if choice < 0.1:
+                if np.random.choice([0, 1]):
+                    tu.pyramid_sloped_terrain(tile, np.random.choice([-0.3, -0.2, 0, 0.2, 0.3]))
+                    tu.random_uniform_terrain(tile, min_height=-0.1, max_height=0.1, step=0.05,
+                                              downsampled_scale=0.2)
+                else:
+                    tu.pyramid_sloped_terrain(tile, np.random.choice([-0.3, -0.2, 0, 0.2, 0.3]))
+            elif choice < 0.6:
+                tu.pyramid_stairs_terrain(tile, step_width=0.31, step_height=np.random.choice([-0.15, 0.15]),
+                                          platform_size=3.0)
+            else:
+                tu.discrete_obstacles_terrain(tile, 0.15, 1.0, 2.0, 40, platform_size=3.0)
+            self._place(i, j, tile)
+
+    def curiculum(self, num_robots, num_terrains, num_levels):
+        tu = terrain_utils
+        p = self.proportions
+        for j in range(num_terrains):
+            for i in range(num_levels):
+                tile = self._tile()
+                difficulty = i / num_levels
+                choice = j / num_terrains
+                slope = difficulty * 0.4
+                step_height = 0.05 + 0.175 * difficulty
+                obstacle_height = 0.025 + difficulty * 0.15
+                stone_size = 2 - 1.8 * difficulty
+                if choice < p[0]:
+                    if choice < 0.05:
+                        slope *= -1
+                    tu.pyramid_sloped_terrain(tile, slope=slope, platform_size=3.0)
+                elif choice < p[1]:
+                    if choice < 0.15:
+                        slope *= -1
+                    tu.pyramid_sloped_terrain(tile, slope=slope, platform_size=3.0)
+                    tu.random_uniform_terrain(tile, min_height=-0.1, max_height=0.1, step=0.025,
+                                              downsampled_scale=0.2)
+                elif choice < p[3]:
+                    if choice < p[2]:
+                        step_height *= -1
+                    tu.pyramid_stairs_terrain(tile, step_width=0.31, step_height=step_height, platform_size=3.0)
+                elif choice < p[4]:
+                    tu.discrete_obstacles_terrain(tile, obstacle_height, 1.0, 2.0, 40, platform_size=3.0)
+                else:
+                    tu.stepping_stones_terrain(tile, stone_size=stone_size, stone_distance=0.1, max_height=0.0,
+                                               platform_size=3.0)
+                self._place(i, j, tile)
 
 
 def quat_apply_yaw(quat, vec):

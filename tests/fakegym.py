@@ -29,8 +29,9 @@ class FakeSim:
 class FakeGym(_g.Gym):
     """Pure-python Gym whose simulate() is a seeded deterministic rule."""
 
-    def __init__(self, seed: int = 12345, dof_drift: float = 0.0, z_drift: float = 0.0):
+    def __init__(self, seed: int = 12345, dof_drift: float = 0.0, z_drift: float = 0.0, xy_drift: float = 0.0):
         self.seed = seed
+        self.xy_drift = xy_drift    # walks even envs along +x (exercises terrain-level curriculum)
         self.dof_drift = dof_drift  # pushes joints out of range over time (exercises limit resets)
         self.z_drift = z_drift      # sinks random roots (exercises height terminations)
 
@@ -40,6 +41,10 @@ class FakeGym(_g.Gym):
 
     def add_ground(self, sim, params):
         sim.ground = params
+
+    def add_triangle_mesh(self, sim, vertices, triangles, params):
+        sim.mesh = (np.asarray(vertices).size // 3, np.asarray(triangles).size // 3)
+        return True
 
     def prepare_sim(self, sim):
         art = sim.asset.art
@@ -89,6 +94,8 @@ class FakeGym(_g.Gym):
             cf[:, k, 2] = np.where(rng.rand(N) < 0.6, 50.0, 0.0)
             cf[:, k, :2] = rng.normal(0, 3.0, (N, 2))
         sim.cf.copy_(torch.from_numpy(cf.reshape(N * nb, 3)))
+        if self.xy_drift:
+            sim.root[0::2, 0].add_(self.xy_drift)
         if self.z_drift:
             sim.root[:, 2].sub_(t32(self.z_drift * (rng.rand(N) < 0.3)))
         if sim.ns:

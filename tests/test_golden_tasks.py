@@ -112,3 +112,32 @@ def test_ant_matches_reference(fake_gym):
         _close(extras["true_objective"].numpy(), d["true_objective"][t], f"true objective step {t}")
         _close(env.dof_state.numpy(), d["dof_state"][t], f"dof state step {t}")
         _close(env.root_states.numpy(), d["root_states"][t], f"root states step {t}")
+
+
+def test_anymal_trimesh_matches_reference(fake_gym):
+    """Trimesh AnymalTerrain: terrain map, custom origins, curriculum levels,
+    height probes and the 188-wide observation against the reference's own task code (both on
+    our terrain_utils restatement, since Isaac Gym's is absent)."""
+    d = np.load(os.path.join(GOLDEN, "anymal_trimesh.npz"))
+    fake_gym(FakeGym(seed=99, xy_drift=0.25))
+    from isaacgymenv_amd.isaacgymenvs.tasks.anymal_terrain import AnymalTerrain
+    cfg = yaml.safe_load(str(d["cfg_yaml"]))
+    np.random.seed(42)
+    torch.manual_seed(42)
+    env = AnymalTerrain(copy.deepcopy(cfg), "cpu", "cpu", -1, True, False, False)
+    np.testing.assert_array_equal(env.height_samples.numpy(), d["height_samples"])
+    _close(env.terrain_origins.numpy(), d["terrain_origins"], "terrain origins")
+    _close(env.env_origins.numpy(), d["init_env_origins"], "env origins at init")
+    _close(env.root_states.numpy(), d["init_root_states"], "root states after the initial reset")
+    np.testing.assert_array_equal(env.terrain_levels.numpy(), d["init_levels"])
+    np.testing.assert_array_equal(env.terrain_types.numpy(), d["init_types"])
+    assert len(set(d["levels"][-1].tolist())) > 1 and d["reset"].sum() > 0
+    for t in range(d["actions"].shape[0]):
+        obs, rew, reset, extras = env.step(torch.from_numpy(d["actions"][t]))
+        np.testing.assert_array_equal(reset.numpy().astype(np.int64), d["reset"][t], err_msg=f"reset step {t}")
+        np.testing.assert_array_equal(env.terrain_levels.numpy(), d["levels"][t], err_msg=f"levels step {t}")
+        _close(env.env_origins.numpy(), d["env_origins"][t], f"env origins step {t}")
+        _close(env.measured_heights.numpy(), d["heights"][t], f"heights step {t}")
+        _close(env.root_states.numpy(), d["root_states"][t], f"root states step {t}")
+        _close(obs["obs"].numpy(), d["obs"][t], f"obs step {t}")
+        _close(rew.numpy(), d["rew"][t], f"reward step {t}")
