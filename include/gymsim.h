@@ -113,6 +113,17 @@ void gs_sim_destroy(gs_sim *sim);
 /* gym.add_ground(sim, PlaneParams)   anymal_terrain.py:188-194 (z-up plane only) */
 int gs_sim_add_ground(gs_sim *sim, double static_friction, double dynamic_friction, double restitution);
 
+/* gym.add_triangle_mesh(sim, vertices f32[3V], triangles u32[3T], TriangleMeshParams)
+ * anymal_terrain.py:196-208.  The mesh must be a heightfield grid as produced by
+ * terrain_utils.convert_heightfield_to_trimesh (rows x cols vertices, row-major; cell (i,j) ->
+ * triangles (v[i,j], v[i+1,j+1], v[i,j+1]), (v[i,j], v[i+1,j], v[i+1,j+1]); every vertex within
+ * one cell of its grid point); other meshes are rejected (-1, gs_last_error).  transform_p is the
+ * mesh translation (TriangleMeshParams.transform.p; rotations are not supported).  One mesh per
+ * sim; call before gs_sim_set_model.  Contacts: DESIGN.md 3.7. */
+int gs_sim_add_triangle_mesh(gs_sim *sim, const float *vertices, int64_t num_vertices, const uint32_t *triangles,
+                             int64_t num_triangles, const double *transform_p, double static_friction,
+                             double dynamic_friction, double restitution);
+
 /* gym.load_asset + create_actor for every env (one articulation type per sim)
  * anymal_terrain.py:231,282  cartpole.py:88,106 */
 int gs_sim_set_model(gs_sim *sim, const gs_model_desc *model);
@@ -165,6 +176,11 @@ float gs_sim_last_kernel_ms(gs_sim *sim);
 /* Profiling build only (libgymsim_prof.so, -DGS_PHASE_PROFILE): per-phase cycle sums of the
  * lane-team kernel over all waves since the last reset (tools/phase_profile.py); -1 otherwise. */
 int gs_debug_phase_cycles(unsigned long long *out, int n, int reset);
+
+/* Test hook: the terrain-mesh contact query of the physics kernels (gs_terrain.h)
+ * for n spheres: centres [n][3] world, radii [n] (device pointers), threshold = r + contact_offset;
+ * out [n][5] = (found, separation, normal xyz). */
+int gs_debug_terrain_query(gs_sim *sim, const float *centres, const float *radii, int n, float *out, void *stream);
 
 #ifdef __cplusplus
 }

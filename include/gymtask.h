@@ -88,6 +88,8 @@ typedef struct gt_anymal_buffers {
     float *obs_out;              /* [N][num_obs] or NULL: VecTask's clamped obs copy (vec_task.py:402) */
     uint8_t *time_outs;          /* [N] bool or NULL: (progress >= T-1) & reset (vec_task.py:394)     */
     float clip_obs;              /* clipObservations (inf -> plain copy)                    */
+    const float *measured_heights; /* [N][num_obs - 36 - nd] terrain heights under the probes
+                                    (gt_measure_heights), or NULL: plane terrain, heights 0 */
 } gt_anymal_buffers;
 
 int gt_abi_version(void);
@@ -134,6 +136,15 @@ int gt_wait_host_seq(const int32_t *words, int32_t seq, int32_t timeout_ms, int3
  * same draws evaluated in-kernel, or both NULL when addNoise is false */
 int gt_anymal_post_physics_b(const gt_anymal_params *p, const gt_anymal_buffers *b, const float *noise,
                              const gt_torch_rand_plan *noise_plan, void *stream);
+
+/* get_heights (anymal_terrain.py:515-538, trimesh terrain): for env e and probe k,
+ *   p = quat_apply_yaw(root_quat[e], points[e][k]) + root_pos[e] + border,
+ *   (px, py) = clip(trunc(p.xy / hs), 0, (rows-2, cols-2)),
+ *   heights[e][k] = vs * min(samples[px][py], samples[px+1][py+1]).
+ * samples int16 [rows][cols]; root_states [N][13]; points [N][num_points][3]; heights [N][num_points]. */
+int gt_measure_heights(const int16_t *samples, int rows, int cols, float border, float hs, float vs,
+                       const float *root_states, const float *points, int num_envs, int num_points, float *heights,
+                       void *stream);
 
 /* out[plan.numel] = torch.rand(plan.numel) for the given plan (checks torch_philox.h against torch) */
 int gt_torch_rand(const gt_torch_rand_plan *plan, float *out, void *stream);

@@ -29,7 +29,7 @@ LIBS = {
 SIM_FLAGS = ["-fno-slp-vectorize"]
 EXTRA_FLAGS = {"libgymtask.so": ["-ffp-contract=off"], "libgymsim.so": SIM_FLAGS,
                "libgymsim_prof.so": SIM_FLAGS + ["-DGS_PHASE_PROFILE"]}
-HEADERS = ["gs_internal.h", "gs_topologies.h", "gs_math.h", "torch_philox.h"]
+HEADERS = ["gs_internal.h", "gs_topologies.h", "gs_math.h", "gs_terrain.h", "torch_philox.h"]
 
 
 def hipcc() -> str:

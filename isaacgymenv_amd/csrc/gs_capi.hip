@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -68,6 +69,8 @@ struct gs_sim {
   bool timing = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
+  float4* d_tverts = nullptr;     // terrain mesh (gs_terrain.h)
+  uint2* d_tcells = nullptr;
 };
 
 extern "C" {
@@ -110,6 +113,8 @@ void gs_sim_destroy(gs_sim* s) {
   if (!s) return;
   hipSetDevice(s->device);
   if (s->d_model) hipFree(s->d_model);
+  if (s->d_tverts) hipFree(s->d_tverts);
+  if (s->d_tcells) hipFree(s->d_tcells);
   if (s->ev0) hipEventDestroy(s->ev0);
   if (s->ev1) hipEventDestroy(s->ev1);
   delete s;
@@ -122,6 +127,99 @@ int gs_sim_add_ground(gs_sim* s, double static_friction, double dynamic_friction
   s->has_ground = true;
   s->dp.has_ground = 1;
   s->dp.ground_mu = (float)static_friction;
+  return 0;
+}
+
+int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_vertices, const uint32_t* triangles,
+                             int64_t num_triangles, const double* transform_p, double static_friction,
+                             double dynamic_friction, double restitution) {
+  (void)dynamic_friction;
+  (void)restitution;
+  if (!s || !vertices || !triangles) return fail("gs_sim_add_triangle_mesh: null argument");
+  if (s->topo) return fail("gs_sim_add_triangle_mesh: call before the model is set (prepare_sim)");
+  if (s->d_tverts) return fail("gs_sim_add_triangle_mesh: one triangle mesh per sim");
+  if (num_triangles < 2) return fail("gs_sim_add_triangle_mesh: empty mesh");
+  // grid shape from the first triangle (v[0,0], v[1,1], v[0,1]) = (0, cols + 1, 1)
+  const int64_t cols = (int64_t)triangles[1] - 1;
+  if (triangles[0] != 0 || triangles[2] != 1 || cols < 2 || num_vertices % cols != 0)
+    return fail("gs_sim_add_triangle_mesh: not a heightfield grid mesh (first triangle)");
+  const int64_t rows = num_vertices / cols;
+  if (rows < 2 || num_triangles != 2 * (rows - 1) * (cols - 1))
+    return fail("gs_sim_add_triangle_mesh: triangle count does not match a %s grid",
+                (std::to_string(rows) + "x" + std::to_string(cols)).c_str());
+  if (rows > (1 << 24) || cols > (1 << 24)) return fail("gs_sim_add_triangle_mesh: grid too large");
+  for (int64_t i = 0; i + 1 < rows; ++i) {
+    for (int64_t j = 0; j + 1 < cols; ++j) {
+      const int64_t b = i * cols + j, t = 2 * (i * (cols - 1) + j);
+      const uint32_t* a = triangles + 3 * t;
+      if (a[0] != b || a[1] != b + cols + 1 || a[2] != b + 1 || a[3] != b || a[4] != b + cols || a[5] != b + cols + 1)
+        return fail("gs_sim_add_triangle_mesh: triangle %s does not follow the heightfield grid layout",
+                    std::to_string(t).c_str());
+    }
+  }
+  // spacing: the grid points are x = i*hs, y = j*hs before the transform (vertex 1 of row 0 may be moved:
+  // take the most common row step)
+  std::vector<double> steps;
+  for (int64_t i = 0; i + 1 < rows && steps.size() < 4096; i += std::max<int64_t>(1, rows / 64))
+    for (int64_t j = 0; j < cols && steps.size() < 4096; j += std::max<int64_t>(1, cols / 64))
+      steps.push_back((double)vertices[3 * ((i + 1) * cols + j)] - (double)vertices[3 * (i * cols + j)]);
+  std::sort(steps.begin(), steps.end());
+  double hs = steps[steps.size() / 2];
+  if (!(hs > 0)) return fail("gs_sim_add_triangle_mesh: cannot infer the grid spacing");
+  const double tx = transform_p ? transform_p[0] : 0.0, ty = transform_p ? transform_p[1] : 0.0,
+               tz = transform_p ? transform_p[2] : 0.0;
+  // grid point (0, 0): vertices of row 0 / column 0 can only move inward, so take the minimum
+  double x0 = vertices[0], y0 = vertices[1];
+  for (int64_t j = 0; j < cols; ++j) x0 = std::min(x0, (double)vertices[3 * j]);
+  for (int64_t i = 0; i < rows; ++i) y0 = std::min(y0, (double)vertices[3 * (i * cols) + 1]);
+  std::vector<float4> hv((size_t)(rows * cols));
+  for (int64_t i = 0; i < rows; ++i) {
+    for (int64_t j = 0; j < cols; ++j) {
+      const float* v = vertices + 3 * (i * cols + j);
+      const double gx = x0 + i * hs, gy = y0 + j * hs;
+      if (std::fabs(v[0] - gx) > 1.001 * hs || std::fabs(v[1] - gy) > 1.001 * hs)
+        return fail("gs_sim_add_triangle_mesh: a vertex lies more than one cell from its grid point");
+      hv[(size_t)(i * cols + j)] = make_float4((float)(v[0] + tx), (float)(v[1] + ty), (float)(v[2] + tz), 0.f);
+    }
+  }
+  std::vector<uint2> hc((size_t)((rows - 1) * (cols - 1)));
+  for (int64_t i = 0; i + 1 < rows; ++i) {
+    for (int64_t j = 0; j + 1 < cols; ++j) {
+      const float4 q[4] = {hv[i * cols + j], hv[i * cols + j + 1], hv[(i + 1) * cols + j], hv[(i + 1) * cols + j + 1]};
+      float zmax = q[0].z, xmin = q[0].x, xmax = q[0].x, ymin = q[0].y, ymax = q[0].y;
+      for (int k = 1; k < 4; ++k) {
+        zmax = std::max(zmax, q[k].z);
+        xmin = std::min(xmin, q[k].x); xmax = std::max(xmax, q[k].x);
+        ymin = std::min(ymin, q[k].y); ymax = std::max(ymax, q[k].y);
+      }
+      const double cx0 = x0 + tx + i * hs, cy0 = y0 + ty + j * hs;
+      uint32_t f = 0;
+      if (xmin < cx0 - 0.25 * hs) f |= TCELL_XLO;
+      if (xmax > cx0 + 1.25 * hs) f |= TCELL_XHI;
+      if (ymin < cy0 - 0.25 * hs) f |= TCELL_YLO;
+      if (ymax > cy0 + 1.25 * hs) f |= TCELL_YHI;
+      uint32_t zb;
+      std::memcpy(&zb, &zmax, 4);
+      hc[(size_t)(i * (cols - 1) + j)] = make_uint2(zb, f);
+    }
+  }
+  hipSetDevice(s->device);
+  hipError_t e = hipMalloc(&s->d_tverts, hv.size() * sizeof(float4));
+  if (e == hipSuccess) e = hipMalloc(&s->d_tcells, hc.size() * sizeof(uint2));
+  if (e == hipSuccess) e = hipMemcpy(s->d_tverts, hv.data(), hv.size() * sizeof(float4), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(s->d_tcells, hc.data(), hc.size() * sizeof(uint2), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "gs_sim_add_triangle_mesh");
+  TerrainDev& T = s->dp.terr;
+  T.v = s->d_tverts;
+  T.cell = s->d_tcells;
+  T.rows = (int)rows;
+  T.cols = (int)cols;
+  T.x0 = (float)(x0 + tx);
+  T.y0 = (float)(y0 + ty);
+  T.hs = (float)hs;
+  T.inv_hs = (float)(1.0 / hs);
+  T.mu = (float)static_friction;
+  s->dp.has_terrain = 1;
   return 0;
 }
 
@@ -174,8 +272,10 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   for (int i = 0; i < g_num_team_kernels; ++i)
     if (std::strcmp(g_team_kernels[i].sig, t->sig) == 0 && g_team_kernels[i].sim) te = &g_team_kernels[i];
   const int want = s->params.kernel_variant;
-  if (te && any_lim) te = nullptr;  // the lane team has no joint-limit rows: the one-env-per-lane kernel runs
-  if (want == 2 && !te) return fail("gs_sim_set_model: no lane-team kernel for this topology / joint limits");
+  // the lane team has no joint-limit rows and no mesh contacts: the one-env-per-lane kernel runs
+  if (te && (any_lim || s->dp.has_terrain)) te = nullptr;
+  if (want == 2 && !te)
+    return fail("gs_sim_set_model: no lane-team kernel for this topology / joint limits / terrain mesh");
   s->dp.any_limits = any_lim;
   s->parent.assign(m->parent, m->parent + m->num_bodies);
   if (te && want != 1) {
@@ -316,6 +416,13 @@ int gs_sim_refresh_force_sensor(gs_sim* s, float* out, void* stream) {
   if (!s->sens) return fail("gs_sim_refresh_force_sensor: sensors not bound");
   hipError_t e = launch_refresh_sensor(s->sens, s->N, s->h_model.nsens, out, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_force_sensor");
+}
+
+int gs_debug_terrain_query(gs_sim* s, const float* centres, const float* radii, int n, float* out, void* stream) {
+  if (!s || !s->dp.has_terrain) return fail("gs_debug_terrain_query: no terrain mesh");
+  if (n < 0 || (n > 0 && (!centres || !radii || !out))) return fail("gs_debug_terrain_query: bad buffers");
+  hipError_t e = launch_terrain_query(s->dp, centres, radii, n, out, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "gs_debug_terrain_query");
 }
 
 int gs_sim_kernel_variant(gs_sim* s) { return s ? s->variant : -1; }

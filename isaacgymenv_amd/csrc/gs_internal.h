@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "gs_terrain.h"
+
 #define GS_MAXB 32   // bodies per articulation
 #define GS_MAXD 32   // dofs per articulation
 #define GS_MAXC 64   // plane-contact candidates per articulation
@@ -40,6 +42,8 @@ struct DevParams {
   int collect;           // contact_collection != 0
   float limit_margin;    // joint-limit rows are active within this distance
   int any_limits;        // some dof has limits (uniform: skips the limit rows entirely)
+  int has_terrain;       // a heightfield triangle mesh is present (TERR kernels, gs_terrain.h)
+  TerrainDev terr;
 };
 
 // SoA state: field f of env e at state[f*N + e]
@@ -92,6 +96,7 @@ extern TeamEntry g_team_kernels[];
 extern const int g_num_team_kernels;
 
 // generic (runtime-sized) tensor API kernels
+hipError_t launch_terrain_query(const DevParams& P, const float* c, const float* r, int n, float* out, hipStream_t s);
 hipError_t launch_refresh_root(const float* state, int N, int nd, const float* com0, float* out, hipStream_t s);
 hipError_t launch_refresh_dof(const float* state, int N, int nd, float* out, hipStream_t s);
 hipError_t launch_refresh_contact(const float* cf, int N, int nb, float* out, hipStream_t s);

@@ -47,10 +47,24 @@ __device__ __forceinline__ constexpr bool body_on_path(int kk, int b) {
 
 // Lanes (= envs) per workgroup: a full wave unless the topology's LDS rows would exceed the
 // 160 KB of LDS per CU (nv_ant: 25 candidates -> 748 slots -> 32 lanes).
-template <class T>
+// TERR kernels (trimesh terrain) keep each active candidate's contact normal in 3 more slots.
+template <class T, bool TERR = false>
 struct LaneCfg {
-  static constexpr int LB = (T::NSLOT * 64 * 4 <= 160 * 1024) ? 64 : (T::NSLOT * 32 * 4 <= 160 * 1024) ? 32 : 16;
+  static constexpr int SLOTS = T::NSLOT + (TERR ? 3 * T::NC : 0);
+  static constexpr int LB = (SLOTS * 64 * 4 <= 160 * 1024) ? 64 : (SLOTS * 32 * 4 <= 160 * 1024) ? 32 : 16;
 };
+
+// World-frame force of candidate c's impulses (normal from LDS, tangents rebuilt), / h.
+template <class T, int LB>
+__device__ __forceinline__ void contact_force_world(const float* lds, int c, const float* lam, float inv_h,
+                                                    float* f) {
+  const float* nsl = lds + (T::NSLOT + 3 * c) * LB;
+  const float n[3] = {nsl[0], nsl[LB], nsl[2 * LB]};
+  float t1[3], t2[3];
+  gs_terrain::tangents(n, t1, t2);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) f[k] = (lam[0] * n[k] + lam[1] * t1[k] + lam[2] * t2[k]) * inv_h;
+}
 
 // Register-resident env state.
 template <class T>
@@ -100,12 +114,12 @@ __device__ __forceinline__ void store_state(float* __restrict__ st, int N, int e
 // is complete (T::subend).  Contact Jacobian rows are written to LDS during the
 // same walk (they need the path's motion subspaces) and turned into scaled
 // Z rows after the factorisation.
-template <class T>
+template <class T, bool TERR>
 __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvState<T>& s,
                                         const float* tau, const float* __restrict__ mu_g, int N, int e, float* lds,
                                         float* __restrict__ cf_soa, bool collect, float* __restrict__ sens_soa) {
   constexpr int NB = T::NB, NV = T::NV, NB6 = T::NBASE, NC = T::NC, ND = T::ND;
-  constexpr int LB = LaneCfg<T>::LB;
+  constexpr int LB = LaneCfg<T, TERR>::LB;
   constexpr int MS = T::MAXDEP + 1;
   // Keep the model pointer opaque per substep: the constants are re-read with
   // scalar loads (K$ hits) instead of being hoisted out of the substep loop
@@ -221,6 +235,54 @@ __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const 
         mat3vec(R[i], M->cpoint[c], x);
         x[0] += X[i][0]; x[1] += X[i][1]; x[2] += X[i][2];
         const float r = M->cradius[c];
+        if constexpr (TERR) {
+          // deepest of the ground plane and the terrain mesh (gs_terrain.h); the contact frame is
+          // (n, t1, t2) with n stored in LDS for the force outputs
+          const float cw[3] = {s.p[0] + x[0], s.p[1] + x[1], s.p[2] + x[2]};
+          float dist = P.has_ground ? cw[2] - r : 3.0e38f;
+          float nrm[3] = {0.f, 0.f, 1.f};
+          float smu = P.ground_mu;
+          float st, nt[3];
+          if (gs_terrain::sphere_contact(P.terr, cw, r, r + P.contact_offset, st, nt) && st < dist) {
+            dist = st;
+            nrm[0] = nt[0]; nrm[1] = nt[1]; nrm[2] = nt[2];
+            smu = P.terr.mu;
+          }
+          act[c] = dist < P.contact_offset;
+          sep[c] = dist - P.rest_offset;
+          cmu[c] = 0.5f * (mu_g[T::cshape[c] * N + e] + smu);
+          if (act[c]) {
+            float* nsl = lds + (T::NSLOT + 3 * c) * LB;
+            nsl[0] = nrm[0]; nsl[LB] = nrm[1]; nsl[2 * LB] = nrm[2];
+            float dir[3][3];
+            dir[0][0] = nrm[0]; dir[0][1] = nrm[1]; dir[0][2] = nrm[2];
+            gs_terrain::tangents(nrm, dir[1], dir[2]);
+            const float xc[3] = {x[0] - r * nrm[0], x[1] - r * nrm[1], x[2] - r * nrm[2]};
+            const int SUP = T::csupp[c];
+            const int leaf = T::cleaf[c];
+            float* slot = lds + T::cslot[c] * LB;
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+              const float* d = dir[rr];
+              float xd[3];  // the row's angular part: d.(w x xc) = w.(xc x d)
+              cross3(xc, d, xd);
+#pragma unroll
+              for (int si = 0; si < MS; ++si) {
+                if (si < SUP) {
+                  const int k = supp_node<T>(leaf, si);
+                  float v;
+                  if (k < NB6) {
+                    v = k < 3 ? xd[k] : d[k - 3];
+                  } else {
+                    const float* Sk = S[T::gbody[k]];
+                    v = Sk[3] * d[0] + Sk[4] * d[1] + Sk[5] * d[2] + Sk[0] * xd[0] + Sk[1] * xd[1] + Sk[2] * xd[2];
+                  }
+                  slot[(rr * SUP + si) * LB] = v;
+                }
+              }
+            }
+          }
+        } else {
         const float dist = s.p[2] + x[2] - r;
         act[c] = P.has_ground && (dist < P.contact_offset);
         sep[c] = dist - P.rest_offset;
@@ -256,6 +318,7 @@ __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const 
             }
           }
         }
+        }  // !TERR
       }
     }
 
@@ -605,9 +668,17 @@ __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const 
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         if (T::cbody[c] == b) {
-          f0 += lam[c][1] * inv_h;
-          f1 += lam[c][2] * inv_h;
-          f2 += lam[c][0] * inv_h;
+          if constexpr (TERR) {
+            if (act[c]) {
+              float fw[3];
+              contact_force_world<T, LB>(lds, c, lam[c], inv_h, fw);
+              f0 += fw[0]; f1 += fw[1]; f2 += fw[2];
+            }
+          } else {
+            f0 += lam[c][1] * inv_h;
+            f1 += lam[c][2] * inv_h;
+            f2 += lam[c][0] * inv_h;
+          }
         }
       }
       cf_soa[(3 * b + 0) * N + e] = f0;
@@ -658,8 +729,16 @@ __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const 
           if (T::cbody[c] == b && act[c]) {
             float x[3];
             mat3vec(R[b], M->cpoint[c], x);
-            x[0] += X[b][0]; x[1] += X[b][1]; x[2] += X[b][2] - M->cradius[c];
-            const float fc[3] = {lam[c][1] * inv_h, lam[c][2] * inv_h, lam[c][0] * inv_h};
+            float fc[3];
+            if constexpr (TERR) {
+              const float* nsl = lds + (T::NSLOT + 3 * c) * LB;
+              const float r = M->cradius[c];
+              x[0] += X[b][0] - r * nsl[0]; x[1] += X[b][1] - r * nsl[LB]; x[2] += X[b][2] - r * nsl[2 * LB];
+              contact_force_world<T, LB>(lds, c, lam[c], inv_h, fc);
+            } else {
+              x[0] += X[b][0]; x[1] += X[b][1]; x[2] += X[b][2] - M->cradius[c];
+              fc[0] = lam[c][1] * inv_h; fc[1] = lam[c][2] * inv_h; fc[2] = lam[c][0] * inv_h;
+            }
             float n[3];
             cross3(x, fc, n);
 #pragma unroll
@@ -692,11 +771,11 @@ __device__ __forceinline__ void com_velocity(const DevModel* __restrict__ M, con
 }
 
 // ---------------------------------------------------------------- kernels
-template <class T>
-__global__ __launch_bounds__(LaneCfg<T>::LB, 1) void k_simulate(const DevModel* __restrict__ M, DevParams P,
-                                                          SimBuffers B, const float* __restrict__ tau_aos) {
-  constexpr int LB = LaneCfg<T>::LB;
-  __shared__ float lds[T::NSLOT * LB];
+template <class T, bool TERR>
+__global__ __launch_bounds__((LaneCfg<T, TERR>::LB), 1) void k_simulate(const DevModel* __restrict__ M, DevParams P,
+                                                                SimBuffers B, const float* __restrict__ tau_aos) {
+  constexpr int LB = LaneCfg<T, TERR>::LB;
+  __shared__ float lds[LaneCfg<T, TERR>::SLOTS * LB];
   const int e = blockIdx.x * LB + threadIdx.x;
   if (e >= B.N) return;
   const int N = B.N;
@@ -707,17 +786,17 @@ __global__ __launch_bounds__(LaneCfg<T>::LB, 1) void k_simulate(const DevModel* 
   for (int j = 0; j < T::ND; ++j) tau[j] = tau_aos ? tau_aos[(size_t)e * T::ND + j] : 0.f;
   for (int sstep = 0; sstep < P.substeps; ++sstep) {
     const bool last = (sstep == P.substeps - 1) && P.collect;
-    substep<T>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last,
-               sstep == P.substeps - 1 ? B.sens : nullptr);
+    substep<T, TERR>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last,
+                     sstep == P.substeps - 1 ? B.sens : nullptr);
   }
   store_state<T>(B.state, N, e, s);
 }
 
-template <class T>
-__global__ __launch_bounds__(LaneCfg<T>::LB, 1) void k_pd_step(const DevModel* __restrict__ M, DevParams P, SimBuffers B,
-                                                         PdDev A) {
-  constexpr int LB = LaneCfg<T>::LB;
-  __shared__ float lds[T::NSLOT * LB];
+template <class T, bool TERR>
+__global__ __launch_bounds__((LaneCfg<T, TERR>::LB), 1) void k_pd_step(const DevModel* __restrict__ M, DevParams P,
+                                                               SimBuffers B, PdDev A) {
+  constexpr int LB = LaneCfg<T, TERR>::LB;
+  __shared__ float lds[LaneCfg<T, TERR>::SLOTS * LB];
   const int e = blockIdx.x * LB + threadIdx.x;
   if (e >= B.N) return;
   const int N = B.N;
@@ -743,7 +822,7 @@ __global__ __launch_bounds__(LaneCfg<T>::LB, 1) void k_pd_step(const DevModel* _
       }
     }
     const bool last = ((it % sub) == sub - 1) && P.collect;
-    substep<T>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last, it == total - 1 ? B.sens : nullptr);
+    substep<T, TERR>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last, it == total - 1 ? B.sens : nullptr);
     if (it == n_pd - 1 && A.dof_out) {
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
@@ -855,10 +934,27 @@ __global__ void k_set_dof(float* __restrict__ st, int N, int nd, const float* __
   st[(13 + nd + j) * N + e] = src[((size_t)e * nd + j) * 2 + 1];
 }
 
+__global__ void k_terrain_query(TerrainDev T, float offset, const float* __restrict__ c, const float* __restrict__ r,
+                                int n, float* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const float p[3] = {c[3 * t], c[3 * t + 1], c[3 * t + 2]};
+  float sep = 0.f, nn[3] = {0.f, 0.f, 0.f};
+  const bool f = gs_terrain::sphere_contact(T, p, r[t], r[t] + offset, sep, nn);
+  out[5 * t] = f ? 1.f : 0.f;
+  out[5 * t + 1] = sep;
+  out[5 * t + 2] = nn[0]; out[5 * t + 3] = nn[1]; out[5 * t + 4] = nn[2];
+}
+
 inline int nblk(long n, int b) { return (int)((n + b - 1) / b); }
 
 }  // namespace
 
+hipError_t launch_terrain_query(const DevParams& P, const float* c, const float* r, int n, float* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_terrain_query, dim3(nblk(n, 256)), dim3(256), 0, s, P.terr, P.contact_offset, c, r, n, out);
+  return hipGetLastError();
+}
 hipError_t launch_refresh_root(const float* state, int N, int nd, const float* com0, float* out, hipStream_t s) {
   (void)nd;
   hipLaunchKernelGGL(k_refresh_root, dim3(nblk(N, 256)), dim3(256), 0, s, state, N, com0, out);
@@ -895,16 +991,24 @@ hipError_t launch_set_dof(float* state, int N, int nd, const float* src, const i
 
 template <class T>
 hipError_t launch_sim(const DevModel* M, const DevParams& P, const SimBuffers& B, const float* tau, hipStream_t st) {
-  constexpr int LB = LaneCfg<T>::LB;
-  const int blocks = (B.N + LB - 1) / LB;
-  hipLaunchKernelGGL(k_simulate<T>, dim3(blocks), dim3(LB), 0, st, M, P, B, tau);
+  if (P.has_terrain) {
+    constexpr int LB = LaneCfg<T, true>::LB;
+    hipLaunchKernelGGL((k_simulate<T, true>), dim3((B.N + LB - 1) / LB), dim3(LB), 0, st, M, P, B, tau);
+  } else {
+    constexpr int LB = LaneCfg<T, false>::LB;
+    hipLaunchKernelGGL((k_simulate<T, false>), dim3((B.N + LB - 1) / LB), dim3(LB), 0, st, M, P, B, tau);
+  }
   return hipGetLastError();
 }
 template <class T>
 hipError_t launch_pd(const DevModel* M, const DevParams& P, const SimBuffers& B, const PdDev& A, hipStream_t st) {
-  constexpr int LB = LaneCfg<T>::LB;
-  const int blocks = (B.N + LB - 1) / LB;
-  hipLaunchKernelGGL(k_pd_step<T>, dim3(blocks), dim3(LB), 0, st, M, P, B, A);
+  if (P.has_terrain) {
+    constexpr int LB = LaneCfg<T, true>::LB;
+    hipLaunchKernelGGL((k_pd_step<T, true>), dim3((B.N + LB - 1) / LB), dim3(LB), 0, st, M, P, B, A);
+  } else {
+    constexpr int LB = LaneCfg<T, false>::LB;
+    hipLaunchKernelGGL((k_pd_step<T, false>), dim3((B.N + LB - 1) / LB), dim3(LB), 0, st, M, P, B, A);
+  }
   return hipGetLastError();
 }
 

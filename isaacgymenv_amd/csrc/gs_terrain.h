@@ -1,0 +1,180 @@
+// gs_terrain.h -- sphere vs heightfield-grid triangle mesh (the trimesh terrain of
+// anymal_terrain.py:196-208, built by terrain_utils.convert_heightfield_to_trimesh).
+//
+// Mesh layout (checked on the host by gs_sim_add_triangle_mesh): vertex (i, j) of a rows x cols
+// grid at index i*cols + j, at most one cell away from its grid point (x0 + i*hs, y0 + j*hs)
+// (the slope-threshold moves that turn steep edges into walls); cell (i, j) holds the triangles
+// (v[i,j], v[i+1,j+1], v[i,j+1]) and (v[i,j], v[i+1,j], v[i+1,j+1]).
+//
+// Contact rule (the oracle restates it in oracle/physics_oracle.c):
+//   for a candidate sphere (centre c, radius r) and threshold thr = r + contact_offset, every
+//   triangle whose closest point q to c lies within thr is a candidate surface:
+//     * q interior to the face: normal = the face normal nf, separation = nf.(c - a) - r, also
+//       when the centre is below the face by at most r + TERRAIN_BACK (penetration);
+//     * q on an edge or vertex: only from the front side (nf.(c - a) >= 0), normal = (c - q)/|c - q|,
+//       separation = |c - q| - r;
+//   the candidate keeps the surface of the triangle CLOSEST to its centre (|sd| for a face, |c - q|
+//   otherwise), first found on ties, scanning cells in (i, j) order and the two triangles of a
+//   cell in the order above (a foot pushed into a stair riser below the tread's edge is pushed
+//   back out of the riser, not lifted onto the tread, unless the tread is nearer).
+// Cells are culled by their top height (a centre more than thr above every vertex of a cell
+// cannot touch it from the front nor lie behind one of its faces) and by their (move-extended)
+// footprint widened by the horizontal reach max(thr, r + TERRAIN_BACK); both tests are
+// conservative, so the result is that of a full scan.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TERRAIN_BACK 0.1f
+
+struct TerrainDev {
+  const float4* v;     // [rows*cols] world xyz (transform applied), w unused
+  const uint2* cell;   // [(rows-1)*(cols-1)]: x = top height (float bits), y = footprint flags
+  int rows, cols;
+  float x0, y0, hs, inv_hs;
+  float mu;            // static friction of the mesh
+};
+
+// footprint flags of a cell: its triangles reach one cell further towards -x, +x, -y, +y
+#define TCELL_XLO 1u
+#define TCELL_XHI 2u
+#define TCELL_YLO 4u
+#define TCELL_YHI 8u
+
+namespace gs_terrain {
+
+__device__ __forceinline__ float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+// closest point on triangle (a, b, c) to p (Voronoi-region walk); returns true when the point is
+// interior to the face
+__device__ __forceinline__ bool closest_on_triangle(const float* p, const float* a, const float* b, const float* c,
+                                                    float* q) {
+  float ab[3], ac[3], ap[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { ab[k] = b[k] - a[k]; ac[k] = c[k] - a[k]; ap[k] = p[k] - a[k]; }
+  const float d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+  if (d1 <= 0.f && d2 <= 0.f) { q[0] = a[0]; q[1] = a[1]; q[2] = a[2]; return false; }
+  float bp[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) bp[k] = p[k] - b[k];
+  const float d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  if (d3 >= 0.f && d4 <= d3) { q[0] = b[0]; q[1] = b[1]; q[2] = b[2]; return false; }
+  const float vc = d1 * d4 - d3 * d2;
+  if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) {
+    const float t = d1 / (d1 - d3);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) q[k] = a[k] + t * ab[k];
+    return false;
+  }
+  float cp[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) cp[k] = p[k] - c[k];
+  const float d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+  if (d6 >= 0.f && d5 <= d6) { q[0] = c[0]; q[1] = c[1]; q[2] = c[2]; return false; }
+  const float vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) {
+    const float t = d2 / (d2 - d6);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) q[k] = a[k] + t * ac[k];
+    return false;
+  }
+  const float va = d3 * d6 - d5 * d4;
+  if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) {
+    const float t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+#pragma unroll
+    for (int k = 0; k < 3; ++k) q[k] = b[k] + t * (c[k] - b[k]);
+    return false;
+  }
+  const float den = 1.f / (va + vb + vc);
+  const float v = vb * den, w = vc * den;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) q[k] = a[k] + ab[k] * v + ac[k] * w;
+  return true;
+}
+
+// one triangle: update (bkey, best, n) when it is an admissible surface closer to the centre
+__device__ __forceinline__ void triangle(const float* p, float r, float thr, const float4& A, const float4& B,
+                                         const float4& C, float& bkey, float& best, float* n) {
+  const float a[3] = {A.x, A.y, A.z}, b[3] = {B.x, B.y, B.z}, c[3] = {C.x, C.y, C.z};
+  const float e1[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+  const float e2[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+  float nf[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+  const float l2 = dot3(nf, nf);
+  if (!(l2 > 1e-14f)) return;  // degenerate (collapsed by two vertex moves)
+  const float il = rsqrtf(l2);
+  nf[0] *= il; nf[1] *= il; nf[2] *= il;
+  const float ap[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
+  const float sd = dot3(nf, ap);
+  if (sd > thr || sd < -(r + TERRAIN_BACK)) return;
+  float q[3];
+  const bool face = closest_on_triangle(p, a, b, c, q);
+  if (face) {
+    const float key = fabsf(sd);
+    if (key < bkey) { bkey = key; best = sd - r; n[0] = nf[0]; n[1] = nf[1]; n[2] = nf[2]; }
+    return;
+  }
+  if (sd < 0.f) return;
+  const float d[3] = {p[0] - q[0], p[1] - q[1], p[2] - q[2]};
+  const float dd = dot3(d, d);
+  if (dd > thr * thr) return;
+  const float dist = sqrtf(dd);
+  if (dist < bkey) {
+    bkey = dist;
+    best = dist - r;
+    if (dist > 1e-7f) {
+      const float id = 1.f / dist;
+      n[0] = d[0] * id; n[1] = d[1] * id; n[2] = d[2] * id;
+    } else {
+      n[0] = nf[0]; n[1] = nf[1]; n[2] = nf[2];
+    }
+  }
+}
+
+// Closest admissible mesh surface for sphere (p, r); false when none lies within thr.
+__device__ __forceinline__ bool sphere_contact(const TerrainDev& T, const float* p, float r, float thr, float& sep,
+                                               float* n) {
+  // horizontal reach: a face can be admitted from behind up to r + TERRAIN_BACK away (walls)
+  const float reach = fmaxf(thr, r + TERRAIN_BACK);
+  const float gx = (p[0] - T.x0) * T.inv_hs, gy = (p[1] - T.y0) * T.inv_hs, gt = reach * T.inv_hs;
+  const int i0 = max((int)floorf(gx - gt) - 1, 0), i1 = min((int)floorf(gx + gt) + 1, T.rows - 2);
+  const int j0 = max((int)floorf(gy - gt) - 1, 0), j1 = min((int)floorf(gy + gt) + 1, T.cols - 2);
+  float best = 3.0e38f, bkey = 3.0e38f;
+  const float zlo = p[2] - thr;
+  for (int i = i0; i <= i1; ++i) {
+    const float cx0 = T.x0 + (float)i * T.hs;
+    for (int j = j0; j <= j1; ++j) {
+      const uint2 cinfo = T.cell[(size_t)i * (T.cols - 1) + j];
+      if (zlo > __uint_as_float(cinfo.x)) continue;
+      const uint32_t f = cinfo.y;
+      const float cy0 = T.y0 + (float)j * T.hs;
+      const float bx0 = cx0 - ((f & TCELL_XLO) ? T.hs : 0.f), bx1 = cx0 + ((f & TCELL_XHI) ? 2.f : 1.f) * T.hs;
+      const float by0 = cy0 - ((f & TCELL_YLO) ? T.hs : 0.f), by1 = cy0 + ((f & TCELL_YHI) ? 2.f : 1.f) * T.hs;
+      if (p[0] + reach < bx0 || p[0] - reach > bx1 || p[1] + reach < by0 || p[1] - reach > by1) continue;
+      const size_t v0 = (size_t)i * T.cols + j;
+      const float4 v00 = T.v[v0], v01 = T.v[v0 + 1], v10 = T.v[v0 + T.cols], v11 = T.v[v0 + T.cols + 1];
+      triangle(p, r, thr, v00, v11, v01, bkey, best, n);
+      triangle(p, r, thr, v00, v10, v11, bkey, best, n);
+    }
+  }
+  if (best >= thr - r) return false;
+  sep = best;
+  return true;
+}
+
+// tangent basis of the contact frame: t1 = world x projected onto the contact plane (world y
+// when n is along x), t2 = n x t1; for n = +z this is (x, y), the plane contact's axes
+__device__ __forceinline__ void tangents(const float* n, float* t1, float* t2) {
+  float a[3] = {1.f - n[0] * n[0], -n[0] * n[1], -n[0] * n[2]};
+  float l2 = a[0] * a[0] + a[1] * a[1] + a[2] * a[2];
+  if (l2 < 1e-6f) {
+    a[0] = -n[1] * n[0]; a[1] = 1.f - n[1] * n[1]; a[2] = -n[1] * n[2];
+    l2 = a[0] * a[0] + a[1] * a[1] + a[2] * a[2];
+  }
+  const float il = rsqrtf(l2);
+  t1[0] = a[0] * il; t1[1] = a[1] * il; t1[2] = a[2] * il;
+  t2[0] = n[1] * t1[2] - n[2] * t1[1];
+  t2[1] = n[2] * t1[0] - n[0] * t1[2];
+  t2[2] = n[0] * t1[1] - n[1] * t1[0];
+}
+
+}  // namespace gs_terrain

@@ -431,7 +431,7 @@ __global__ void __launch_bounds__(256) k_post_b(gt_anymal_params p, gt_anymal_bu
   } else if (k < 12 + 2 * nd) {
     src = b.dof_state + ((size_t)e * nd + (k - 12 - nd)) * 2 + 1; sc = p.dof_vel_scale;
   } else if (k < no - nd) {
-    // plane terrain: measured heights are 0 (anymal_terrain.py:516-517)
+    // the base height; the probe's terrain height is subtracted below
     src = b.root_states + (size_t)e * 13 + 2; height = true;
   } else {
     src = b.actions + (size_t)e * nd + (k - (no - nd));
@@ -440,7 +440,11 @@ __global__ void __launch_bounds__(256) k_post_b(gt_anymal_params p, gt_anymal_bu
   const float nz = NOISE == 1 ? noise[t] : NOISE == 2 ? torch_philox::rand_at(plan, t) : 0.0f;
   const float ns = b.noise_scale[k];
   float v;
-  if (height) v = fminf(fmaxf(x - 0.5f - 0.0f, -1.0f), 1.0f) * p.height_meas_scale;
+  if (height) {
+    // clip(z - 0.5 - measured_height, -1, 1) * scale (:303-304); plane terrain: heights are 0
+    const float mh = b.measured_heights ? b.measured_heights[(size_t)e * (no - 36 - nd) + (k - 12 - 2 * nd)] : 0.0f;
+    v = fminf(fmaxf(x - 0.5f - mh, -1.0f), 1.0f) * p.height_meas_scale;
+  }
   else if (k < 12 + 2 * nd && !(k >= 6 && k < 9)) v = x * sc;
   else v = x;
   if (NOISE) v = v + (2.0f * nz - 1.0f) * ns;
@@ -451,6 +455,44 @@ __global__ void __launch_bounds__(256) k_post_b(gt_anymal_params p, gt_anymal_bu
     b.last_actions[(size_t)e * nd + k] = la;
     b.last_dof_vel[(size_t)e * nd + k] = lq;
   }
+}
+
+// get_heights, one lane per (env, probe).  The statement order follows the reference's torch
+// expressions (normalize of the yaw-only quaternion, quat_apply = v + w t + q x t with t = 2 q x v,
+// + root position, + border, / hs, truncation) and the library is built without FMA contraction,
+// so the cell index matches the eager torch computation except on exact ties.
+__global__ void __launch_bounds__(256) k_measure_heights(const int16_t* __restrict__ hf, int rows, int cols,
+                                                         float border, float hs, float vs,
+                                                         const float* __restrict__ root,
+                                                         const float* __restrict__ pts, int N, int np_,
+                                                         float* __restrict__ out) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)N * np_) return;
+  const int e = (int)(t / np_);
+  const float* r = root + (size_t)e * 13;
+  const float qz = r[5], qw = r[6];
+  const float nrm = fmaxf(sqrtf(qz * qz + qw * qw), 1e-9f);
+  const float z = qz / nrm, w = qw / nrm;  // yaw-only quaternion (0, 0, z, w)
+  const float* pv = pts + (size_t)t * 3;
+  const float vx = pv[0], vy = pv[1], vz = pv[2];
+  // t = 2 * (q x v) with q = (0, 0, z): (-z vy, z vx, 0)
+  const float tx = (0.0f * vz - z * vy) * 2.0f;
+  const float ty = (z * vx - 0.0f * vz) * 2.0f;
+  const float tz = (0.0f * vy - 0.0f * vx) * 2.0f;
+  // q x t
+  const float cx = 0.0f * tz - z * ty;
+  const float cy = z * tx - 0.0f * tz;
+  float px = vx + w * tx + cx + r[0];
+  float py = vy + w * ty + cy + r[1];
+  (void)tz;
+  px += border;
+  py += border;
+  long ix = (long)(px / hs), iy = (long)(py / hs);
+  ix = ix < 0 ? 0 : (ix > rows - 2 ? rows - 2 : ix);
+  iy = iy < 0 ? 0 : (iy > cols - 2 ? cols - 2 : iy);
+  const int h1 = hf[(size_t)ix * cols + iy];
+  const int h2 = hf[(size_t)(ix + 1) * cols + iy + 1];
+  out[t] = (float)(h1 < h2 ? h1 : h2) * vs;
 }
 
 __global__ void k_torch_rand(gt_torch_rand_plan plan, float* __restrict__ out) {
@@ -551,6 +593,22 @@ int gt_anymal_reset_flagged(const gt_anymal_params* p, const gt_anymal_buffers* 
                      *d, env_ids_out, episode_out, episode_length_s, acc, done);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("gt_anymal_reset_flagged", e);
+}
+
+int gt_measure_heights(const int16_t* samples, int rows, int cols, float border, float hs, float vs,
+                       const float* root_states, const float* points, int num_envs, int num_points, float* heights,
+                       void* stream) {
+  if (!samples || !root_states || !points || !heights || rows < 2 || cols < 2 || num_envs < 0 || num_points < 0 ||
+      !(hs > 0.0f)) {
+    g_err = "gt_measure_heights: invalid arguments";
+    return -1;
+  }
+  const long n = (long)num_envs * num_points;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_measure_heights, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, samples,
+                     rows, cols, border, hs, vs, root_states, points, num_envs, num_points, heights);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail("gt_measure_heights", e);
 }
 
 int gt_torch_rand(const gt_torch_rand_plan* plan, float* out, void* stream) {

@@ -67,7 +67,7 @@ class GtAnymalBuffers(C.Structure):
         (n, C.c_void_p) for n in ("rew_buf", "episode_sums", "base_lin_vel", "base_ang_vel", "projected_gravity",
                                   "obs_buf", "noise_scale", "reset_count", "host_count")] + [
         ("seq", C.c_int32), ("reset_masks", C.c_void_p), ("obs_out", C.c_void_p), ("time_outs", C.c_void_p),
-        ("clip_obs", C.c_float)]
+        ("clip_obs", C.c_float), ("measured_heights", C.c_void_p)]
 
 
 class GtAnymalResetDraws(C.Structure):
@@ -96,7 +96,9 @@ def lib():
                                                        vp, vp],
                            "gt_host_alloc": [C.c_uint64, C.POINTER(vp), C.POINTER(vp)],
                            "gt_host_free": [vp],
-                           "gt_wait_host_seq": [vp, C.c_int32, C.c_int32, C.POINTER(C.c_int32)]}.items():
+                           "gt_wait_host_seq": [vp, C.c_int32, C.c_int32, C.POINTER(C.c_int32)],
+                           "gt_measure_heights": [vp, i, i, C.c_float, C.c_float, C.c_float, vp, vp, i, i, vp,
+                                                  vp]}.items():
             fn = getattr(L, name)
             fn.restype = C.c_int
             fn.argtypes = args
@@ -108,7 +110,7 @@ def lib():
 
 EXPORTED_SYMBOLS = ["gt_abi_version", "gt_last_error", "gt_anymal_post_physics_a", "gt_anymal_reset",
                     "gt_anymal_post_physics_b", "gt_anymal_reset_flagged", "gt_torch_rand", "gt_host_alloc",
-                    "gt_host_free", "gt_wait_host_seq"]
+                    "gt_host_free", "gt_wait_host_seq", "gt_measure_heights"]
 
 
 def _check(rc, what):
@@ -224,6 +226,8 @@ class AnymalTailKernels:
         b.timeout_is_int64 = int(tb.dtype == torch.int64)
         b.obs_out = None
         b.time_outs = None
+        hb = getattr(t, "_heights_dev", None)
+        b.measured_heights = hb.data_ptr() if hb is not None else None
         return b
 
     def _stream(self):
@@ -274,12 +278,29 @@ class AnymalTailKernels:
         noise is torch.rand_like(obs_buf): evaluated in-kernel (inkernel_rng) or drawn by
         ``rand_like`` into a buffer; either way the generator advances as the reference's."""
         t = self.task
+        if getattr(t, "_heights_dev", None) is not None:
+            self.measure_heights()
         if not t.add_noise:
             self.post_b(None)
         elif self.inkernel_rng:
             self.post_b(None, self.planner.plan(t.obs_buf.numel()))
         else:
             self.post_b((rand_like or torch.rand_like)(t.obs_buf))
+
+    def measure_heights(self):
+        """get_heights for the trimesh terrain (anymal_terrain.py:515-538), one kernel into
+        task._heights_dev (= task.measured_heights)."""
+        t = self.task
+        ter = t.terrain
+        hs = t.height_samples
+        pts = t.height_points
+        assert hs.dtype == torch.int16 and hs.is_contiguous() and pts.is_contiguous()
+        out = t._heights_dev
+        _check(lib().gt_measure_heights(hs.data_ptr(), hs.shape[0], hs.shape[1], float(ter.border_size),
+                                        float(ter.horizontal_scale), float(ter.vertical_scale),
+                                        t.root_states.data_ptr(), pts.data_ptr(), t.num_envs, pts.shape[1],
+                                        out.data_ptr(), self._stream()), "gt_measure_heights")
+        t.measured_heights = out
 
     def reset(self, env_ids_int32, pos_offset, vel, cmd_x, cmd_y, cmd_h):
         t = self.task

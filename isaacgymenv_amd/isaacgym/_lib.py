@@ -73,6 +73,8 @@ def lib():
             "gs_sim_set_force_sensors": (i, [vp, i, vp]),
             "gs_sim_bind_force_sensors": (i, [vp, vp]),
             "gs_sim_refresh_force_sensor": (i, [vp, vp, vp]),
+            "gs_sim_add_triangle_mesh": (i, [vp, vp, C.c_int64, vp, C.c_int64, vp, d, d, d]),
+            "gs_debug_terrain_query": (i, [vp, vp, vp, i, vp, vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -93,6 +95,7 @@ EXPORTED_SYMBOLS = [
     "gs_sim_refresh_dof", "gs_sim_refresh_contact", "gs_sim_set_root", "gs_sim_set_dof", "gs_sim_pd_step",
     "gs_sim_kernel_variant", "gs_sim_enable_timing", "gs_sim_last_kernel_ms", "gs_debug_phase_cycles",
     "gs_sim_set_force_sensors", "gs_sim_bind_force_sensors", "gs_sim_refresh_force_sensor",
+    "gs_sim_add_triangle_mesh", "gs_debug_terrain_query",
 ]
 
 

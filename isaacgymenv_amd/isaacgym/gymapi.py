@@ -17,6 +17,7 @@ Scope notes:
 """
 from __future__ import annotations
 
+import ctypes as C
 import enum
 import math
 import os
@@ -294,6 +295,7 @@ class Sim:
         self.envs: List[Env] = []
         self.asset: Optional[Asset] = None
         self.ground: Optional[PlaneParams] = None
+        self.mesh = None
         self.prepared = False
         self.handle = None
         px = params.physx
@@ -344,6 +346,11 @@ class Sim:
         art, flat = self.asset.art, self.asset.flat
         L = _lib.lib()
         desc, keep = _lib.model_desc(flat)
+        if self.mesh is not None:
+            v, t, tp, smu, dmu, rest = self.mesh
+            tpa = (C.c_double * 3)(*tp)
+            _lib.check(L.gs_sim_add_triangle_mesh(self.handle, v.ctypes.data, v.size // 3, t.ctypes.data, t.size // 3,
+                                                  tpa, smu, dmu, rest), "gs_sim_add_triangle_mesh")
         _lib.check(L.gs_sim_set_model(self.handle, desc), "gs_sim_set_model")
         sens = [b for b, _ in self.asset.sensors]
         if sens:
@@ -479,7 +486,23 @@ class Gym:
         sim.ground = params
 
     def add_triangle_mesh(self, sim: Sim, vertices, triangles, params: TriangleMeshParams):
-        raise NotImplementedError("trimesh terrain is the next row of SURVEY.md section 8f (not built yet)")
+        """A static heightfield-grid mesh (terrain_utils.convert_heightfield_to_trimesh layout,
+        anymal_terrain.py:196-208); translation-only transform.  Handed to libgymsim at prepare_sim."""
+        r = params.transform.r
+        if abs(r.x) > 1e-9 or abs(r.y) > 1e-9 or abs(r.z) > 1e-9 or abs(abs(r.w) - 1.0) > 1e-9:
+            raise NotImplementedError("add_triangle_mesh: only translated (unrotated) meshes are supported")
+        if sim.mesh is not None:
+            raise NotImplementedError("add_triangle_mesh: one triangle mesh per sim")
+        v = np.ascontiguousarray(np.asarray(vertices, dtype=np.float32).reshape(-1))
+        t = np.ascontiguousarray(np.asarray(triangles, dtype=np.uint32).reshape(-1))
+        if params.nb_vertices and v.size != 3 * params.nb_vertices:
+            raise ValueError("add_triangle_mesh: vertex count does not match nb_vertices")
+        if params.nb_triangles and t.size != 3 * params.nb_triangles:
+            raise ValueError("add_triangle_mesh: triangle count does not match nb_triangles")
+        p = params.transform.p
+        sim.mesh = (v, t, (float(p.x), float(p.y), float(p.z)), float(params.static_friction),
+                    float(params.dynamic_friction), float(params.restitution))
+        return True
 
     # ---- assets
     def load_asset(self, sim: Sim, root: str, filename: str, options: Optional[AssetOptions] = None) -> Asset:

@@ -143,6 +143,11 @@ class AnymalTerrain(VecTask):
         self.episode_sums = {k: zeros(self.num_envs) for k in REWARD_TERMS}
 
         self._kernels = None
+        self._heights_dev = None
+        if self.custom_origins and self.device != "cpu":
+            # trimesh: the fused tail measures the terrain under the probes in a kernel (gt_measure_heights)
+            self._heights_dev = zeros(self.num_envs, self.num_height_points)
+            self.height_points = self.height_points.contiguous()
         if self.device != "cpu":
             from ...gymtask import AnymalTailKernels  # fails loudly when libgymtask.so is missing
             self._kernels = AnymalTailKernels(self)

@@ -30,7 +30,9 @@ class OParams(C.Structure):
     _fields_ = [("dt", C.c_double), ("substeps", C.c_int32), ("gravity", C.c_double * 3),
                 ("pos_iters", C.c_int32), ("vel_iters", C.c_int32), ("contact_offset", C.c_double),
                 ("rest_offset", C.c_double), ("max_depen_vel", C.c_double), ("collect_contacts", C.c_int32),
-                ("has_ground", C.c_int32), ("ground_friction", C.c_double), ("limit_margin", C.c_double)]
+                ("has_ground", C.c_int32), ("ground_friction", C.c_double), ("limit_margin", C.c_double),
+                ("has_terrain", C.c_int32), ("trows", C.c_int32), ("tcols", C.c_int32), ("tverts", C.c_void_p),
+                ("tx0", C.c_double), ("ty0", C.c_double), ("ths", C.c_double), ("terrain_friction", C.c_double)]
 
 
 def build(quiet: bool = True) -> None:
@@ -50,6 +52,8 @@ def _lib(real_bits: int):
         lib = C.CDLL(path)
         lib.oracle_simulate.restype = C.c_int
         lib.oracle_simulate.argtypes = [C.POINTER(OModel), C.POINTER(OParams), C.c_int] + [C.c_void_p] * 6 + [C.c_int]
+        lib.oracle_terrain_query.restype = C.c_int
+        lib.oracle_terrain_query.argtypes = [C.POINTER(OParams), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         _LIBS[real_bits] = lib
     return _LIBS[real_bits]
 
@@ -57,7 +61,9 @@ def _lib(real_bits: int):
 class OracleSim:
     """Holds the model arrays alive and steps numpy state in place."""
 
-    def __init__(self, flat: dict, params: dict, real_bits: int = 64, sensor_bodies=()):
+    def __init__(self, flat: dict, params: dict, real_bits: int = 64, sensor_bodies=(), terrain=None):
+        """terrain: optional dict(vertices float32 [rows*cols, 3] world coordinates, rows, cols, x0, y0,
+        hs, friction) -- the heightfield-grid mesh of gym.add_triangle_mesh."""
         self.flat = flat
         self.real = np.float64 if real_bits == 64 else np.float32
         self.lib = _lib(real_bits)
@@ -95,7 +101,25 @@ class OracleSim:
         p.has_ground = params.get("has_ground", 1)
         p.ground_friction = params.get("ground_friction", 1.0)
         p.limit_margin = params.get("limit_margin", 0.1)
+        if terrain is not None:
+            tv = np.ascontiguousarray(terrain["vertices"], dtype=np.float32).reshape(-1)
+            keep["tverts"] = tv
+            p.has_terrain = 1
+            p.trows, p.tcols = int(terrain["rows"]), int(terrain["cols"])
+            p.tverts = tv.ctypes.data
+            p.tx0, p.ty0, p.ths = float(terrain["x0"]), float(terrain["y0"]), float(terrain["hs"])
+            p.terrain_friction = float(terrain.get("friction", 1.0))
         self.params = p
+
+    def terrain_query(self, centres, radii):
+        """The mesh contact query alone: [n][5] = (found, separation, normal xyz)."""
+        c = np.ascontiguousarray(centres, dtype=self.real)
+        r = np.ascontiguousarray(radii, dtype=self.real)
+        out = np.zeros((c.shape[0], 5), dtype=self.real)
+        if self.lib.oracle_terrain_query(C.byref(self.params), c.shape[0], c.ctypes.data, r.ctypes.data,
+                                         out.ctypes.data) != 0:
+            raise RuntimeError("oracle_terrain_query: no terrain")
+        return out
 
     def simulate(self, root, dof, tau, mu, cf=None, num_threads: int = 1, sens=None) -> None:
         for a in (root, dof, tau, mu) + ((cf,) if cf is not None else ()) + ((sens,) if sens is not None else ()):

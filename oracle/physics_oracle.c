@@ -83,6 +83,14 @@ typedef struct {
     int32_t has_ground;
     double ground_friction;
     double limit_margin;        /* joint-limit rows active within this distance of a limit */
+    /* heightfield-grid triangle mesh: vertex (i,j) at tverts[3*(i*tcols+j)], world
+     * coordinates; grid point (i,j) at (tx0 + i*ths, ty0 + j*ths); cell (i,j) -> triangles
+     * (v[i,j], v[i+1,j+1], v[i,j+1]), (v[i,j], v[i+1,j], v[i+1,j+1]) */
+    int32_t has_terrain;
+    int32_t trows, tcols;
+    const float *tverts;
+    double tx0, ty0, ths;
+    double terrain_friction;
 } OParams;
 
 /* ---------------------------------------------------------------- helpers */
@@ -116,6 +124,95 @@ static void quat_to_mat(const real *q, real *R) { /* xyzw */
     R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w);     R[2] = 2 * (x * z + y * w);
     R[3] = 2 * (x * y + z * w);     R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - x * w);
     R[6] = 2 * (x * z - y * w);     R[7] = 2 * (y * z + x * w);     R[8] = 1 - 2 * (x * x + y * y);
+}
+
+/* ---------------------------------------------------------------- terrain mesh
+ * Sphere vs triangle, stated with a plane projection and edge clamping (the kernel walks the
+ * Voronoi regions instead): the projection of c inside the triangle -> face contact along the face
+ * normal (also from behind, up to r + TERRAIN_BACK); otherwise the nearest point of the three
+ * edges, from the front side only.  The triangle CLOSEST to the centre gives the contact (first
+ * found on ties).  Full scan of a window 3 cells wider than any triangle of a grid cell can reach
+ * (vertices move at most one cell). */
+#define TERRAIN_BACK 0.1
+static void seg_closest(const real *p, const real *a, const real *b, real *q) {
+    real ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, ap[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
+    const real l2 = dot3(ab, ab);
+    real t = l2 > 0 ? dot3(ap, ab) / l2 : 0;
+    if (t < 0) t = 0;
+    if (t > 1) t = 1;
+    for (int k = 0; k < 3; ++k) q[k] = a[k] + t * ab[k];
+}
+/* candidate surface of one triangle: key = distance from the centre to the triangle (the closest
+ * surface wins), separation signed (negative behind a face) */
+static void tri_test(const real *p, real r, real thr, const real *a, const real *b, const real *c, real *bkey,
+                     real *bsep, real *n) {
+    real e1[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, e2[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]}, nf[3];
+    cross3(e1, e2, nf);
+    const real l = sqrt(dot3(nf, nf));
+    if (!(l * l > 1e-14)) return;
+    for (int k = 0; k < 3; ++k) nf[k] /= l;
+    const real ap[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
+    const real sd = dot3(nf, ap);
+    if (sd > thr || sd < -(r + TERRAIN_BACK)) return;
+    /* barycentric coordinates of the projection */
+    const real proj[3] = {p[0] - sd * nf[0], p[1] - sd * nf[1], p[2] - sd * nf[2]};
+    const real v0[3] = {proj[0] - a[0], proj[1] - a[1], proj[2] - a[2]};
+    const real d00 = dot3(e1, e1), d01 = dot3(e1, e2), d11 = dot3(e2, e2), d20 = dot3(v0, e1), d21 = dot3(v0, e2);
+    const real den = d00 * d11 - d01 * d01;
+    const real bv = (d11 * d20 - d01 * d21) / den, bw = (d00 * d21 - d01 * d20) / den;
+    if (bv >= 0 && bw >= 0 && bv + bw <= 1) {
+        const real key = fabs(sd);
+        if (key < *bkey) { *bkey = key; *bsep = sd - r; n[0] = nf[0]; n[1] = nf[1]; n[2] = nf[2]; }
+        return;
+    }
+    if (sd < 0) return;
+    real q[3], qq[3], dbest = 1e300;
+    const real *ends[3][2] = {{a, b}, {b, c}, {c, a}};
+    for (int k = 0; k < 3; ++k) {
+        seg_closest(p, ends[k][0], ends[k][1], qq);
+        const real d2 = (p[0] - qq[0]) * (p[0] - qq[0]) + (p[1] - qq[1]) * (p[1] - qq[1]) + (p[2] - qq[2]) * (p[2] - qq[2]);
+        if (d2 < dbest) { dbest = d2; q[0] = qq[0]; q[1] = qq[1]; q[2] = qq[2]; }
+    }
+    if (dbest > thr * thr) return;
+    const real dist = sqrt(dbest);
+    if (dist < *bkey) {
+        *bkey = dist;
+        *bsep = dist - r;
+        if (dist > 1e-7) { for (int k = 0; k < 3; ++k) n[k] = (p[k] - q[k]) / dist; }
+        else { n[0] = nf[0]; n[1] = nf[1]; n[2] = nf[2]; }
+    }
+}
+static int terrain_query(const OParams *pp, const real *p, real r, real thr, real *sep, real *n) {
+    const real hs = (real)pp->ths;
+    const int gi = (int)floor((p[0] - (real)pp->tx0) / hs), gj = (int)floor((p[1] - (real)pp->ty0) / hs);
+    const real reach = thr > r + TERRAIN_BACK ? thr : r + TERRAIN_BACK;
+    const int w = (int)ceil(reach / hs) + 3;
+    real bkey = 1e300, best = 1e300;
+    for (int i = gi - w; i <= gi + w; ++i) {
+        if (i < 0 || i > pp->trows - 2) continue;
+        for (int j = gj - w; j <= gj + w; ++j) {
+            if (j < 0 || j > pp->tcols - 2) continue;
+            real v[4][3];
+            const int64_t id[4] = {(int64_t)i * pp->tcols + j, (int64_t)i * pp->tcols + j + 1,
+                                   (int64_t)(i + 1) * pp->tcols + j, (int64_t)(i + 1) * pp->tcols + j + 1};
+            for (int k = 0; k < 4; ++k)
+                for (int a = 0; a < 3; ++a) v[k][a] = (real)pp->tverts[3 * id[k] + a];
+            tri_test(p, r, thr, v[0], v[3], v[1], &bkey, &best, n);
+            tri_test(p, r, thr, v[0], v[2], v[3], &bkey, &best, n);
+        }
+    }
+    if (!(best < thr - r)) return 0;
+    *sep = best;
+    return 1;
+}
+/* contact frame tangents: world x projected on the contact plane (world y when n ~ x), t2 = n x t1 */
+static void tangents(const real *n, real *t1, real *t2) {
+    real a[3] = {1 - n[0] * n[0], -n[0] * n[1], -n[0] * n[2]};
+    real l2 = dot3(a, a);
+    if (l2 < 1e-6) { a[0] = -n[1] * n[0]; a[1] = 1 - n[1] * n[1]; a[2] = -n[1] * n[2]; l2 = dot3(a, a); }
+    const real l = sqrt(l2);
+    for (int k = 0; k < 3; ++k) t1[k] = a[k] / l;
+    cross3(n, t1, t2);
 }
 
 /* spatial inertia at O (world axes): m, h = m c, I_O (3x3) */
@@ -344,15 +441,14 @@ static void env_substep(const OModel *m, const OParams *p, real h,
         ++nlim;
     }
 
-    /* ---- contacts vs the ground plane z = 0 */
+    /* ---- contacts vs the ground plane z = 0 and the terrain mesh (deepest of the two) */
     int nact = 0;
     int ck[MAXC];
-    real cs[MAXC], cmu[MAXC];
-    static const int row_axis[3] = {2, 0, 1}; /* normal z, tangent x, tangent y */
+    real cs[MAXC], cmu[MAXC], cn[MAXC][3];
     const int ncap = m->nc > 0 ? m->nc : 1;
     real J[3 * ncap * MAXV], W[3 * ncap * MAXV];
     real Dr[3 * MAXC];
-    if (p->has_ground) {
+    if (p->has_ground || p->has_terrain) {
         for (int c = 0; c < m->nc; ++c) {
             const int b = m->cbody[c];
             real xl[3], x[3];
@@ -360,9 +456,22 @@ static void env_substep(const OModel *m, const OParams *p, real h,
             matvec3(R[b], xl, x);
             for (int k = 0; k < 3; ++k) x[k] += P[b][k];
             const real r = (real)m->cradius[c];
-            const real dist = root[2] + x[2] - r;
+            real dist = p->has_ground ? root[2] + x[2] - r : 1e300;
+            real nrm[3] = {0, 0, 1}, smu = (real)p->ground_friction;
+            if (p->has_terrain) {
+                const real cw[3] = {root[0] + x[0], root[1] + x[1], root[2] + x[2]};
+                real st, nt[3];
+                if (terrain_query(p, cw, r, r + (real)p->contact_offset, &st, nt) && st < dist) {
+                    dist = st;
+                    nrm[0] = nt[0]; nrm[1] = nt[1]; nrm[2] = nt[2];
+                    smu = (real)p->terrain_friction;
+                }
+            }
             if (!(dist < (real)p->contact_offset)) continue;
-            real xc[3] = {x[0], x[1], x[2] - r};
+            real dir[3][3];
+            for (int k = 0; k < 3; ++k) dir[0][k] = nrm[k];
+            tangents(nrm, dir[1], dir[2]);
+            real xc[3] = {x[0] - r * nrm[0], x[1] - r * nrm[1], x[2] - r * nrm[2]};
             real Jp[3][MAXV];
             for (int a = 0; a < 3; ++a) for (int k = 0; k < nv; ++k) Jp[a][k] = 0;
             if (!fb) {
@@ -381,7 +490,7 @@ static void env_substep(const OModel *m, const OParams *p, real h,
             for (int rr = 0; rr < 3; ++rr) {
                 real *Jr = J + (3 * nact + rr) * MAXV;
                 real *Wr = W + (3 * nact + rr) * MAXV;
-                for (int k = 0; k < nv; ++k) Jr[k] = Jp[row_axis[rr]][k];
+                for (int k = 0; k < nv; ++k) Jr[k] = dir[rr][0] * Jp[0][k] + dir[rr][1] * Jp[1][k] + dir[rr][2] * Jp[2][k];
                 chol_solve(M, nv, Jr, Wr);
                 real d = 0;
                 for (int k = 0; k < nv; ++k) d += Jr[k] * Wr[k];
@@ -389,7 +498,8 @@ static void env_substep(const OModel *m, const OParams *p, real h,
             }
             ck[nact] = c;
             cs[nact] = dist - (real)p->rest_offset;
-            cmu[nact] = (real)0.5 * (mu_shape[m->cshape[c]] + (real)p->ground_friction);
+            cmu[nact] = (real)0.5 * (mu_shape[m->cshape[c]] + smu);
+            for (int k = 0; k < 3; ++k) cn[nact][k] = nrm[k];
             ++nact;
         }
     }
@@ -484,9 +594,10 @@ static void env_substep(const OModel *m, const OParams *p, real h,
         for (int k = 0; k < 3 * nb; ++k) cforce[k] = 0;
         for (int a = 0; a < nact; ++a) {
             const int b = m->cbody[ck[a]];
-            cforce[3 * b + 0] += lam[3 * a + 1] / h;
-            cforce[3 * b + 1] += lam[3 * a + 2] / h;
-            cforce[3 * b + 2] += lam[3 * a + 0] / h;
+            real t1[3], t2[3];
+            tangents(cn[a], t1, t2);
+            for (int k = 0; k < 3; ++k)
+                cforce[3 * b + k] += (lam[3 * a] * cn[a][k] + lam[3 * a + 1] * t1[k] + lam[3 * a + 2] * t2[k]) / h;
         }
     }
     if (sens && m->nsens > 0) {
@@ -516,8 +627,12 @@ static void env_substep(const OModel *m, const OParams *p, real h,
                 for (int k = 0; k < 3; ++k) xl[k] = (real)m->cpoint[3 * c + k];
                 matvec3(R[b], xl, x);
                 for (int k = 0; k < 3; ++k) x[k] += P[b][k];
-                x[2] -= (real)m->cradius[c];
-                fc[0] = lam[3 * a + 1] / h; fc[1] = lam[3 * a + 2] / h; fc[2] = lam[3 * a] / h;
+                real t1[3], t2[3];
+                tangents(cn[a], t1, t2);
+                for (int k = 0; k < 3; ++k) {
+                    x[k] -= (real)m->cradius[c] * cn[a][k];
+                    fc[k] = (lam[3 * a] * cn[a][k] + lam[3 * a + 1] * t1[k] + lam[3 * a + 2] * t2[k]) / h;
+                }
                 cross3(x, fc, n);
                 for (int k = 0; k < 3; ++k) { f[k] -= n[k]; f[3 + k] -= fc[k]; }
             }
@@ -563,3 +678,14 @@ int oracle_simulate(const OModel *m, const OParams *p, int n_envs, real *root, r
 }
 
 int oracle_real_size(void) { return (int)sizeof(real); }
+
+/* the terrain contact query alone (test hook): out[n][5] = (found, separation, normal xyz) */
+int oracle_terrain_query(const OParams *p, int n, const real *centres, const real *radii, real *out) {
+    if (!p->has_terrain) return -1;
+    for (int t = 0; t < n; ++t) {
+        real sep = 0, nn[3] = {0, 0, 0};
+        const int f = terrain_query(p, centres + 3 * t, radii[t], radii[t] + (real)p->contact_offset, &sep, nn);
+        out[5 * t] = f; out[5 * t + 1] = sep; out[5 * t + 2] = nn[0]; out[5 * t + 3] = nn[1]; out[5 * t + 4] = nn[2];
+    }
+    return 0;
+}

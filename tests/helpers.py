@@ -95,8 +95,9 @@ def anymal_states(n, seed=0, spread=1.0):
     return root, dof, tau, mu
 
 
-def make_gpu_sim(kind: str, n: int, params: dict):
-    """A libgymsim sim built through the drop-in gymapi (GPU pipeline)."""
+def make_gpu_sim(kind: str, n: int, params: dict, terrain=None):
+    """A libgymsim sim built through the drop-in gymapi (GPU pipeline); `terrain` (terrain_from_heights)
+    adds the heightfield mesh with gym.add_triangle_mesh."""
     from isaacgymenv_amd.isaacgym import gymapi
     gym = gymapi.acquire_gym()
     sp = gymapi.SimParams()
@@ -117,6 +118,13 @@ def make_gpu_sim(kind: str, n: int, params: dict):
         plane = gymapi.PlaneParams()
         plane.static_friction = params.get("ground_friction", 1.0)
         gym.add_ground(sim, plane)
+    if terrain is not None:
+        tm = gymapi.TriangleMeshParams()
+        tm.nb_vertices = terrain["vertices"].shape[0]
+        tm.nb_triangles = terrain["triangles"].shape[0]
+        tm.transform.p = gymapi.Vec3(*terrain["shift"])
+        tm.static_friction = terrain["friction"]
+        gym.add_triangle_mesh(sim, terrain["vertices"].flatten(), terrain["triangles"].flatten(), tm)
     opts = gymapi.AssetOptions()
     sensors = []
     if kind == "anymal":
@@ -179,3 +187,34 @@ def assert_mostly_close(actual, desired, atol, rtol=0.0, max_frac=1e-3, hard=Non
     hard_tol = 50 * tol if hard is None else hard
     assert frac <= max_frac, f"{what}: {bad.sum()} of {bad.size} elements off (max err {err.max():.3g})"
     assert np.all(err <= hard_tol), f"{what}: max err {err.max():.3g} beyond the hard bound"
+
+
+def terrain_from_heights(hf, hs=0.1, vs=0.005, slope_threshold=0.5, shift=(0.0, 0.0, 0.0), friction=1.0):
+    """A heightfield as the trimesh gym.add_triangle_mesh receives it (terrain_utils layout, translated by
+    `shift`) plus the oracle's terrain dict (world vertices, grid origin, spacing)."""
+    from isaacgymenv_amd.isaacgym import terrain_utils
+    v, t = terrain_utils.convert_heightfield_to_trimesh(np.asarray(hf, dtype=np.int16), hs, vs, slope_threshold)
+    return mesh_terrain(v, t, hf.shape[0], hf.shape[1], hs, shift, friction)
+
+
+def mesh_terrain(v, t, rows, cols, hs, shift=(0.0, 0.0, 0.0), friction=1.0):
+    world = (v.astype(np.float64) + np.asarray(shift)).astype(np.float32)
+    grid = v.reshape(rows, cols, 3)
+    oracle = dict(vertices=world, rows=rows, cols=cols, x0=float(grid[0, :, 0].min()) + shift[0],
+                  y0=float(grid[:, 0, 1].min()) + shift[1], hs=hs, friction=friction)
+    return dict(vertices=v, triangles=t, shift=shift, friction=friction, oracle=oracle)
+
+
+def rough_terrain(seed=0, rows=120, cols=120):
+    """Stairs, blocks and a random field around the origin (cells of 0.1 m), centred on (0, 0)."""
+    from isaacgymenv_amd.isaacgym import terrain_utils as tu
+    np.random.seed(seed)
+    hf = np.zeros((rows, cols), dtype=np.int16)
+    a = tu.SubTerrain("a", width=rows // 2, length=cols, vertical_scale=0.005, horizontal_scale=0.1)
+    tu.pyramid_stairs_terrain(a, step_width=0.31, step_height=0.08, platform_size=1.0)
+    b = tu.SubTerrain("b", width=rows - rows // 2, length=cols, vertical_scale=0.005, horizontal_scale=0.1)
+    tu.random_uniform_terrain(b, -0.06, 0.06, step=0.01, downsampled_scale=0.2)
+    tu.discrete_obstacles_terrain(b, 0.1, 0.5, 1.0, 10, platform_size=0.5)
+    hf[: rows // 2] = a.height_field_raw
+    hf[rows // 2:] = b.height_field_raw
+    return terrain_from_heights(hf, shift=(-rows * 0.05, -cols * 0.05, 0.0))
