@@ -16,7 +16,12 @@ The rank-0 JSON line carries:
   roofline     -- the fused physics kernel (gs_sim_pd_step): algorithmic HBM bytes
                   per launch / its average HIP-event duration on the launch stream;
   cpu_baseline -- the fp32 build of the CPU oracle (oracle/, kind "port") stepping
-                  a bounded sample of the same workload on the host cores.
+                  a bounded sample of the same workload on the host cores;
+  ppo          -- PPO samples/s (the metric's second half): the rl_games-compatible learner
+                  (isaacgymenv_amd/rl, AnymalTerrainPPO.yaml) over the same envs, one warm-up
+                  epoch then --ppo-epochs timed epochs (rollout + GAE kernel + 5 x 6 minibatch
+                  updates); with N ranks every minibatch all-reduces the 2.09 MB flat gradient
+                  over RCCL.  value = horizon * envs * ranks * epochs / max-over-ranks time.
 """
 from __future__ import annotations
 
@@ -55,6 +60,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--kernel-launches", type=int, default=50, help="launches timed for the roofline figure")
+    ap.add_argument("--ppo-epochs", type=int, default=5,
+                    help="timed PPO epochs (AnymalTerrainPPO.yaml: horizon 24 x envs samples each); 0 = skip")
     return ap.parse_args()
 
 
@@ -116,6 +123,43 @@ def timed_region(step, steps: int, warmup: int, world: int, sync=lambda: None) -
     return elapsed
 
 
+def ppo_leg(env, device, rank, world, epochs):
+    import torch
+    from isaacgymenv_amd.isaacgymenvs.config import compose
+    from isaacgymenv_amd.rl import A2CAgent, PpoConfig
+    train = compose("config", ["task=AnymalTerrain"])["train"]
+    pcfg = PpoConfig.from_train_cfg(train, multi_gpu=world > 1)
+    agent = A2CAgent(env, pcfg, device=device, seed=42 + rank)
+    agent.env_reset()
+    agent.train_epoch()  # warm-up: allocator, hipBLASLt heuristics, RCCL communicator
+    # phase split of one (untimed) epoch, synchronised between the phases
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    returns, values = agent.play_steps()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    agent.model.train()
+    agent.prepare_dataset(returns, values)
+    for _ in range(pcfg.mini_epochs):
+        for i in range(agent.num_minibatches):
+            out = agent.calc_gradients(agent._minibatch(i))
+            agent._update_lr(out[3])
+    agent.model.eval()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    elapsed = timed_region(agent.train_epoch, epochs, 0, world, sync=torch.cuda.synchronize)
+    samples = agent.batch_size * world * epochs
+    st = agent.epoch_stats()
+    return {"metric": "PPO samples/sec AnymalTerrain (rl_games a2c_continuous, AnymalTerrainPPO.yaml)",
+            "value": samples / elapsed, "unit": "samples/s", "epochs": epochs,
+            "ms_per_epoch": 1e3 * elapsed / epochs, "samples_per_epoch": agent.batch_size * world,
+            "rollout_ms": 1e3 * (t1 - t0), "update_ms": 1e3 * (t2 - t1),
+            "minibatches_per_epoch": pcfg.mini_epochs * agent.num_minibatches,
+            "allreduce_bytes_per_minibatch": agent.num_params * 4 if world > 1 else 0,
+            "dtype": "f32 rollout, fp16 autocast update (mixed_precision: True)",
+            "last_kl": st["kl"], "last_lr": st["lr"]}
+
+
 def main():
     args = parse()
     import torch
@@ -167,6 +211,10 @@ def main():
     bytes_per_launch = physics_kernel_bytes_per_env() * N
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
 
+    ppo = None
+    if args.ppo_epochs > 0:
+        ppo = ppo_leg(env, device, rank, world, args.ppo_epochs)
+
     if rank == 0:
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_pd_step.json")
@@ -213,6 +261,7 @@ def main():
                          "traffic": traffic, "kernel_ms": kernel_ms, "bytes_per_launch": bytes_per_launch,
                          "valu": valu},
             "cpu_baseline": cpu,
+            "ppo": ppo,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

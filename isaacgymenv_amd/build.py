@@ -20,6 +20,7 @@ ARCH = os.environ.get("GS_OFFLOAD_ARCH", "gfx950")
 LIBS = {
     "libgymsim.so": ["gs_physics.hip", "gs_team.hip", "gs_capi.hip"],
     "libgymtask.so": ["gt_anymal.hip"],
+    "libgymrl.so": ["rl_gae.hip"],
     # phase-profiling build of the simulator (tools/phase_profile.py); never loaded by default
     "libgymsim_prof.so": ["gs_physics.hip", "gs_team.hip", "gs_capi.hip"],
 }
@@ -27,7 +28,7 @@ LIBS = {
 # -fno-slp-vectorize: the SLP vectorizer packs the scalar spatial algebra into v_pk_* pairs and
 # then spends ~1700 v_mov_b32 (and AGPR copies) arranging register pairs in the physics kernels
 SIM_FLAGS = ["-fno-slp-vectorize"]
-EXTRA_FLAGS = {"libgymtask.so": ["-ffp-contract=off"], "libgymsim.so": SIM_FLAGS,
+EXTRA_FLAGS = {"libgymtask.so": ["-ffp-contract=off"], "libgymrl.so": ["-ffp-contract=off"], "libgymsim.so": SIM_FLAGS,
                "libgymsim_prof.so": SIM_FLAGS + ["-DGS_PHASE_PROFILE"]}
 HEADERS = ["gs_internal.h", "gs_topologies.h", "gs_math.h", "gs_terrain.h", "torch_philox.h"]
 
@@ -46,13 +47,17 @@ def _stale(out: str, srcs) -> bool:
     deps = [os.path.join(CSRC, s) for s in srcs] + [os.path.join(CSRC, h) for h in HEADERS]
     deps.append(os.path.join(os.path.dirname(HERE), "include", "gymsim.h"))
     deps.append(os.path.join(os.path.dirname(HERE), "include", "gymtask.h"))
+    deps.append(os.path.join(os.path.dirname(HERE), "include", "gymrl.h"))
     deps.append(os.path.abspath(__file__))  # flags live here
     return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
 
 
 def build(force: bool = False, verbose: bool = True) -> None:
+    """Compile every stale library; the libraries are independent, so hipcc runs in parallel."""
+    from concurrent.futures import ThreadPoolExecutor
     os.makedirs(LIBDIR, exist_ok=True)
     cc = hipcc()
+    jobs = []
     for lib, srcs in LIBS.items():
         if not all(os.path.exists(os.path.join(CSRC, s)) for s in srcs):
             raise RuntimeError(f"missing sources for {lib}: {srcs}")
@@ -63,13 +68,21 @@ def build(force: bool = False, verbose: bool = True) -> None:
                "-I", os.path.join(os.path.dirname(HERE), "include"), "-I", CSRC, "-o", out]
         cmd += EXTRA_FLAGS.get(lib, [])
         cmd += [os.path.join(CSRC, s) for s in srcs]
+        jobs.append((lib, cmd))
+
+    def run(job):
+        lib, cmd = job
         if verbose:
             print("[build]", " ".join(cmd), flush=True)
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f"hipcc failed for {lib}:\n{r.stdout}\n{r.stderr}")
-        if verbose and r.stderr.strip():
-            print(r.stderr[-4000:], file=sys.stderr)
+        return lib, subprocess.run(cmd, capture_output=True, text=True)
+
+    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "4") or 4)))
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        for lib, r in ex.map(run, jobs):
+            if r.returncode != 0:
+                raise RuntimeError(f"hipcc failed for {lib}:\n{r.stdout}\n{r.stderr}")
+            if verbose and r.stderr.strip():
+                print(r.stderr[-4000:], file=sys.stderr)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,423 @@
+"""PPO (rl_games ``a2c_continuous`` A2CAgent, rl-games 1.6.x semantics) over a VecTask.
+
+The reference trains every in-scope task with rl_games (isaacgymenvs/train.py:188-218,
+cfg/train/*PPO.yaml); rl_games is an external dependency absent from this image and from
+/root/reference, so the learner is restated here from its published algorithm:
+
+* rollout (A2CBase.play_steps): ``horizon_length`` steps of act -> VecTask.step; shaped
+  reward = scale * r plus ``gamma * V(s) * time_outs`` (value_bootstrap); dones stored u8;
+* GAE (A2CBase.discount_values) + returns + swap_and_flatten01: one HIP kernel (rl/gae.py);
+* prepare_dataset: advantages = returns - values; value normalisation (RunningMeanStd updated
+  with values then returns); advantage normalisation (mean / (std + 1e-8));
+* train_epoch: ``mini_epochs`` x contiguous minibatches (PPODataset does not shuffle), clipped
+  surrogate, clipped value loss (``critic_coef`` * 0.5), entropy bonus, bound loss, fp16
+  autocast + GradScaler (mixed_precision), gradient norm clipping, Adam(eps 1e-8); the
+  minibatch's new mu/sigma replace the dataset's old ones (update_mu_sigma); adaptive LR
+  (kl > 2 thr -> lr / 1.5, kl < thr / 2 -> lr * 1.5, clamped to [1e-6, 1e-2]) per minibatch.
+
+MI355X-first differences that do not change the arithmetic:
+* multi-GPU: the gradients live in ONE flat buffer (parameters' ``.grad`` are views into it),
+  so the per-minibatch data-parallel step is a single in-place RCCL all-reduce of 2.09 MB
+  (AnymalTerrain) with no concat/scatter copies -- rl_games concatenates the grads, reduces
+  and copies them back (trancate_gradients_and_step); the KL average is a device all-reduce;
+* the learning rate lives on the device (fused Adam with a tensor lr) and the adaptive schedule
+  is evaluated there, so a training epoch has no host synchronisation (rl_games calls
+  ``kl.item()`` after every minibatch);
+* experience buffers are stored env-major, so the flattened batch is a view, not a copy.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from dataclasses import dataclass, field
+from typing import Any, Dict, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .gae import discount_values
+from .network import ActorCriticNetwork, ModelA2CContinuousLogStd
+
+
+@dataclass
+class PpoConfig:
+    """``train.params.config`` keys (cfg/train/AnymalTerrainPPO.yaml:42-82) + network."""
+    name: str = "run"
+    gamma: float = 0.99
+    tau: float = 0.95
+    e_clip: float = 0.2
+    entropy_coef: float = 0.0
+    learning_rate: float = 3e-4
+    lr_schedule: Optional[str] = "adaptive"
+    kl_threshold: float = 0.008
+    truncate_grads: bool = True
+    grad_norm: float = 1.0
+    horizon_length: int = 24
+    minibatch_size: int = 16384
+    mini_epochs: int = 5
+    critic_coef: float = 2.0
+    clip_value: bool = True
+    bounds_loss_coef: float = 0.0
+    normalize_input: bool = True
+    normalize_value: bool = True
+    normalize_advantage: bool = True
+    value_bootstrap: bool = True
+    clip_actions: bool = False
+    mixed_precision: bool = True
+    reward_scale: float = 1.0
+    reward_shift: float = 0.0
+    max_epochs: int = 1500
+    multi_gpu: bool = False
+    weight_decay: float = 0.0
+    units: list = field(default_factory=lambda: [512, 256, 128])
+    activation: str = "elu"
+    separate: bool = True
+    fixed_sigma: bool = True
+    sigma_init_val: float = 0.0
+    games_to_track: int = 100
+
+    @classmethod
+    def from_train_cfg(cls, train_cfg: Dict[str, Any], **overrides) -> "PpoConfig":
+        """Build from a composed ``train`` config (cfg/train/<Task>PPO.yaml)."""
+        p = train_cfg["params"]
+        c = dict(p["config"])
+        net = p["network"]
+        mlp = net.get("mlp", {})
+        cont = net.get("space", {}).get("continuous", {})
+        shaper = c.get("reward_shaper", {}) or {}
+        kw = dict(
+            name=str(c.get("name", "run")), gamma=float(c["gamma"]), tau=float(c["tau"]),
+            e_clip=float(c["e_clip"]), entropy_coef=float(c.get("entropy_coef", 0.0)),
+            learning_rate=float(c["learning_rate"]), lr_schedule=c.get("lr_schedule"),
+            kl_threshold=float(c.get("kl_threshold", 0.008)), truncate_grads=bool(c.get("truncate_grads", False)),
+            grad_norm=float(c.get("grad_norm", 1.0)), horizon_length=int(c["horizon_length"]),
+            minibatch_size=int(c["minibatch_size"]), mini_epochs=int(c["mini_epochs"]),
+            critic_coef=float(c.get("critic_coef", 1.0)), clip_value=bool(c.get("clip_value", False)),
+            bounds_loss_coef=float(c.get("bounds_loss_coef", 0.0) or 0.0),
+            normalize_input=bool(c.get("normalize_input", False)),
+            normalize_value=bool(c.get("normalize_value", False)),
+            normalize_advantage=bool(c.get("normalize_advantage", True)),
+            value_bootstrap=bool(c.get("value_bootstrap", False)), clip_actions=bool(c.get("clip_actions", True)),
+            mixed_precision=bool(c.get("mixed_precision", False)),
+            reward_scale=float(shaper.get("scale_value", 1.0)), reward_shift=float(shaper.get("shift_value", 0.0)),
+            max_epochs=int(c.get("max_epochs", 1500) or 1500), multi_gpu=bool(c.get("multi_gpu", False)),
+            weight_decay=float(c.get("weight_decay", 0.0)), units=list(mlp.get("units", [512, 256, 128])),
+            activation=str(mlp.get("activation", "elu")), separate=bool(net.get("separate", False)),
+            fixed_sigma=bool(cont.get("fixed_sigma", True)),
+            sigma_init_val=float((cont.get("sigma_init") or {}).get("val", 0.0)),
+        )
+        kw.update(overrides)
+        return cls(**kw)
+
+
+class _AverageMeter:
+    """rl_games torch_ext.AverageMeter (running mean of the last ``max_size`` finished episodes),
+    kept on the device and fed with a done mask so no host sync is needed."""
+
+    def __init__(self, max_size: int, device):
+        self.max_size = max_size
+        self.mean = torch.zeros((), dtype=torch.float32, device=device)
+        self.current_size = torch.zeros((), dtype=torch.float32, device=device)
+
+    def update_masked(self, values: torch.Tensor, mask: torch.Tensor):
+        cnt = mask.float().sum()
+        new_mean = (values * mask).sum() / cnt.clamp(min=1.0)
+        size = cnt.clamp(max=float(self.max_size))
+        old_size = torch.minimum(self.max_size - size, self.current_size)
+        size_sum = old_size + size
+        upd = cnt > 0
+        self.mean = torch.where(upd, (self.mean * old_size + new_mean * size) / size_sum.clamp(min=1.0), self.mean)
+        self.current_size = torch.where(upd, size_sum, self.current_size)
+
+
+class A2CAgent:
+    """rl_games A2CAgent (continuous) on one rank; ``world_size`` > 1 = data-parallel PPO."""
+
+    def __init__(self, env, cfg: PpoConfig, device: Optional[str] = None, seed: Optional[int] = None):
+        self.env = env
+        self.cfg = cfg
+        self.device = torch.device(device or env.rl_device)
+        self.num_actors = env.num_envs
+        self.obs_dim = env.num_obs
+        self.actions_num = env.num_actions
+        self.horizon = cfg.horizon_length
+        self.batch_size = self.horizon * self.num_actors
+        if self.batch_size % cfg.minibatch_size != 0:
+            raise ValueError(f"batch {self.batch_size} (horizon x envs) is not divisible by minibatch "
+                             f"{cfg.minibatch_size}")
+        self.num_minibatches = self.batch_size // cfg.minibatch_size
+        self.multi_gpu = cfg.multi_gpu and dist.is_available() and dist.is_initialized() \
+            and dist.get_world_size() > 1
+        self.rank = dist.get_rank() if self.multi_gpu else 0
+        self.world_size = dist.get_world_size() if self.multi_gpu else 1
+        if seed is not None:
+            torch.manual_seed(seed)
+        net = ActorCriticNetwork(self.obs_dim, self.actions_num, cfg.units, cfg.activation, cfg.separate,
+                                 cfg.fixed_sigma, cfg.sigma_init_val)
+        self.model = ModelA2CContinuousLogStd(net, self.obs_dim, cfg.normalize_input, cfg.normalize_value)
+        self.model.to(self.device)
+        self.params = [p for p in self.model.parameters()]
+        self.num_params = sum(p.numel() for p in self.params)
+        # one flat gradient buffer; .grad of every parameter is a view into it
+        self.flat_grad = torch.zeros(self.num_params, dtype=torch.float32, device=self.device)
+        off = 0
+        for p in self.params:
+            p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        if self.multi_gpu:
+            self._broadcast_params()
+        on_gpu = self.device.type == "cuda"
+        self.lr = torch.tensor(cfg.learning_rate, dtype=torch.float64, device=self.device)
+        if on_gpu:
+            self._opt_lr = torch.tensor(cfg.learning_rate, dtype=torch.float32, device=self.device)
+            self.optimizer = torch.optim.Adam(self.params, lr=self._opt_lr, eps=1e-08,
+                                              weight_decay=cfg.weight_decay, fused=True)
+        else:
+            self._opt_lr = None
+            self.optimizer = torch.optim.Adam(self.params, lr=cfg.learning_rate, eps=1e-08,
+                                              weight_decay=cfg.weight_decay)
+        self.mixed_precision = cfg.mixed_precision and on_gpu
+        self.scaler = torch.amp.GradScaler("cuda", enabled=self.mixed_precision)
+        H, N, O, A = self.horizon, self.num_actors, self.obs_dim, self.actions_num
+        dev = self.device
+        # env-major experience (flattened batch = view); time-major GAE inputs
+        self.b_obs = torch.zeros(N, H, O, dtype=torch.float32, device=dev)
+        self.b_actions = torch.zeros(N, H, A, dtype=torch.float32, device=dev)
+        self.b_neglogp = torch.zeros(N, H, dtype=torch.float32, device=dev)
+        self.b_mu = torch.zeros(N, H, A, dtype=torch.float32, device=dev)
+        self.b_sigma = torch.zeros(N, H, A, dtype=torch.float32, device=dev)
+        self.t_values = torch.zeros(H, N, dtype=torch.float32, device=dev)
+        self.t_rewards = torch.zeros(H, N, dtype=torch.float32, device=dev)
+        self.t_dones = torch.zeros(H, N, dtype=torch.uint8, device=dev)
+        self.current_rewards = torch.zeros(N, dtype=torch.float32, device=dev)
+        self.current_lengths = torch.zeros(N, dtype=torch.float32, device=dev)
+        self.game_rewards = _AverageMeter(cfg.games_to_track, dev)
+        self.game_lengths = _AverageMeter(cfg.games_to_track, dev)
+        self.obs = None
+        self.dones = torch.zeros(N, dtype=torch.uint8, device=dev)
+        self.epoch_num = 0
+        self.frame = 0
+        self.entropy_coef = cfg.entropy_coef
+        self.last_stats: Dict[str, float] = {}
+
+    # ------------------------------------------------------------------ multi-GPU
+    def _broadcast_params(self):
+        flat = torch.cat([p.detach().reshape(-1) for p in self.params])
+        dist.broadcast(flat, 0)
+        off = 0
+        with torch.no_grad():
+            for p in self.params:
+                p.copy_(flat[off:off + p.numel()].view_as(p))
+                off += p.numel()
+
+    # ------------------------------------------------------------------ rollout
+    def _obs(self, obs):
+        return obs["obs"] if isinstance(obs, dict) else obs
+
+    @torch.no_grad()
+    def get_action_values(self, obs):
+        self.model.eval()
+        return self.model({"is_train": False, "obs": self._obs(obs)})
+
+    @torch.no_grad()
+    def get_values(self, obs):
+        """rl_games A2CBase.get_values: the full act forward (it samples, consuming RNG)."""
+        return self.get_action_values(obs)["values"]
+
+    def env_reset(self):
+        self.obs = self.env.reset()
+        return self.obs
+
+    def play_steps(self):
+        cfg = self.cfg
+        if self.obs is None:
+            self.env_reset()
+        for n in range(self.horizon):
+            res = self.get_action_values(self.obs)
+            self.b_obs[:, n] = self._obs(self.obs)
+            self.t_dones[n] = self.dones
+            self.t_values[n] = res["values"][:, 0]
+            self.b_actions[:, n] = res["actions"]
+            self.b_neglogp[:, n] = res["neglogpacs"]
+            self.b_mu[:, n] = res["mus"]
+            self.b_sigma[:, n] = res["sigmas"]
+            actions = res["actions"]
+            if cfg.clip_actions:
+                actions = torch.clamp(actions, -1.0, 1.0)  # action space is [-1, 1]: rescale is identity
+            self.obs, rewards, dones, infos = self.env.step(actions)
+            self.dones = dones.to(torch.uint8)
+            shaped = (rewards + cfg.reward_shift) * cfg.reward_scale
+            if cfg.value_bootstrap and "time_outs" in infos:
+                shaped = shaped + cfg.gamma * res["values"][:, 0] * infos["time_outs"].float()
+            self.t_rewards[n] = shaped
+            self.current_rewards += rewards
+            self.current_lengths += 1
+            done = self.dones.bool()
+            self.game_rewards.update_masked(self.current_rewards, done)
+            self.game_lengths.update_masked(self.current_lengths, done)
+            not_done = 1.0 - self.dones.float()
+            self.current_rewards *= not_done
+            self.current_lengths *= not_done
+        last_values = self.get_values(self.obs)[:, 0].contiguous()
+        returns, advs, values = discount_values(self.t_rewards, self.t_values, self.t_dones, last_values,
+                                                self.dones.contiguous(), cfg.gamma, cfg.tau)
+        self.frame += self.batch_size * self.world_size
+        return returns, values
+
+    # ------------------------------------------------------------------ update
+    def prepare_dataset(self, returns, values):
+        cfg = self.cfg
+        advantages = returns - values
+        values = values.unsqueeze(1)
+        returns = returns.unsqueeze(1)
+        if cfg.normalize_value:
+            vms = self.model.value_mean_std
+            vms.train()
+            values = vms(values)
+            returns = vms(returns)
+            vms.eval()
+        if cfg.normalize_advantage:
+            advantages = (advantages - advantages.mean()) / (advantages.std() + 1e-8)
+        B = self.batch_size
+        self.dataset = {
+            "old_values": values, "returns": returns, "advantages": advantages,
+            "old_logp_actions": self.b_neglogp.view(B), "actions": self.b_actions.view(B, -1),
+            "obs": self.b_obs.view(B, -1), "mu": self.b_mu.view(B, -1), "sigma": self.b_sigma.view(B, -1),
+        }
+
+    def _minibatch(self, i):
+        s = slice(i * self.cfg.minibatch_size, (i + 1) * self.cfg.minibatch_size)
+        return {k: v[s] for k, v in self.dataset.items()}
+
+    def calc_gradients(self, mb):
+        cfg = self.cfg
+        e = cfg.e_clip
+        with torch.autocast("cuda", dtype=torch.float16, enabled=self.mixed_precision):
+            res = self.model({"is_train": True, "prev_actions": mb["actions"], "obs": mb["obs"]})
+            action_log_probs, values, entropy = res["prev_neglogp"], res["values"], res["entropy"]
+            mu, sigma = res["mus"], res["sigmas"]
+            ratio = torch.exp(mb["old_logp_actions"] - action_log_probs)
+            surr1 = mb["advantages"] * ratio
+            surr2 = mb["advantages"] * torch.clamp(ratio, 1.0 - e, 1.0 + e)
+            a_loss = torch.max(-surr1, -surr2)
+            if cfg.clip_value:
+                vp_clipped = mb["old_values"] + (values - mb["old_values"]).clamp(-e, e)
+                c_loss = torch.max((values - mb["returns"]) ** 2, (vp_clipped - mb["returns"]) ** 2)
+            else:
+                c_loss = (mb["returns"] - values) ** 2
+            soft_bound = 1.1
+            b_loss = (torch.clamp_max(mu + soft_bound, 0.0) ** 2 + torch.clamp_min(mu - soft_bound, 0.0) ** 2).sum(-1)
+            a_loss, c_loss, entropy, b_loss = a_loss.mean(), c_loss.mean(), entropy.mean(), b_loss.mean()
+            loss = a_loss + 0.5 * c_loss * cfg.critic_coef - entropy * self.entropy_coef \
+                + b_loss * cfg.bounds_loss_coef
+        self.flat_grad.zero_()
+        self.scaler.scale(loss).backward()
+        self._truncate_gradients_and_step()
+        with torch.no_grad():
+            kl = self._policy_kl(mu.detach(), sigma.detach(), mb["mu"], mb["sigma"])
+        return a_loss.detach(), c_loss.detach(), entropy.detach(), kl, mu.detach(), sigma.detach(), b_loss.detach()
+
+    @staticmethod
+    def _policy_kl(p0_mu, p0_sigma, p1_mu, p1_sigma):
+        c1 = torch.log(p1_sigma / p0_sigma + 1e-5)
+        c2 = (p0_sigma ** 2 + (p1_mu - p0_mu) ** 2) / (2.0 * (p1_sigma ** 2 + 1e-5))
+        return (c1 + c2 - 0.5).sum(dim=-1).mean()
+
+    def _truncate_gradients_and_step(self):
+        if self.multi_gpu:
+            dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
+            self.flat_grad.div_(self.world_size)
+        if self.cfg.truncate_grads:
+            self.scaler.unscale_(self.optimizer)
+            nn.utils.clip_grad_norm_(self.params, self.cfg.grad_norm)
+        self.scaler.step(self.optimizer)
+        self.scaler.update()
+
+    def _update_lr(self, kl):
+        """AdaptiveScheduler.update on the device (rl_games schedulers.py)."""
+        if self.cfg.lr_schedule != "adaptive":
+            return
+        if self.multi_gpu:
+            kl = kl.clone()
+            dist.all_reduce(kl, op=dist.ReduceOp.SUM)
+            kl = kl / self.world_size
+        thr = self.cfg.kl_threshold
+        kl = kl.double()
+        cur = self.lr
+        lr = torch.where(kl > 2.0 * thr, torch.clamp(cur / 1.5, min=1e-6), cur)
+        lr = torch.where(kl < 0.5 * thr, torch.clamp(cur * 1.5, max=1e-2), lr)
+        self.lr.copy_(lr)
+        if self._opt_lr is not None:
+            self._opt_lr.copy_(lr)
+        else:
+            for g in self.optimizer.param_groups:
+                g["lr"] = float(lr)
+
+    def train_epoch(self):
+        t0 = time.perf_counter()
+        returns, values = self.play_steps()
+        t1 = time.perf_counter()
+        self.model.train()
+        self.prepare_dataset(returns, values)
+        kls, a_losses, c_losses = [], [], []
+        for _ in range(self.cfg.mini_epochs):
+            for i in range(self.num_minibatches):
+                mb = self._minibatch(i)
+                a_loss, c_loss, entropy, kl, cmu, csigma, b_loss = self.calc_gradients(mb)
+                s = slice(i * self.cfg.minibatch_size, (i + 1) * self.cfg.minibatch_size)
+                self.dataset["mu"][s] = cmu
+                self.dataset["sigma"][s] = csigma
+                self._update_lr(kl)
+                kls.append(kl)
+                a_losses.append(a_loss)
+                c_losses.append(c_loss)
+        self.model.eval()
+        self.epoch_num += 1
+        self._epoch_tensors = (torch.stack(kls), torch.stack(a_losses), torch.stack(c_losses))
+        return t1 - t0
+
+    def epoch_stats(self) -> Dict[str, float]:
+        """Host copy of the last epoch's diagnostics (one sync; not called inside the loop)."""
+        kls, a, c = self._epoch_tensors
+        return {"epoch": self.epoch_num, "frame": self.frame, "kl": float(kls.mean()), "a_loss": float(a.mean()),
+                "c_loss": float(c.mean()), "lr": float(self.lr), "mean_reward": float(self.game_rewards.mean),
+                "mean_length": float(self.game_lengths.mean)}
+
+    def train(self, max_epochs: Optional[int] = None, log_every: int = 10, printer=print):
+        """rl_games ContinuousA2CBase.train loop (no checkpoint cadence); returns the last stats."""
+        max_epochs = max_epochs or self.cfg.max_epochs
+        stats = {}
+        for ep in range(max_epochs):
+            t0 = time.perf_counter()
+            self.train_epoch()
+            if (ep + 1) % log_every == 0 or ep + 1 == max_epochs:
+                stats = self.epoch_stats()
+                dt = time.perf_counter() - t0
+                if self.rank == 0 and printer:
+                    printer(f"epoch {stats['epoch']} frames {stats['frame']} fps(last) "
+                            f"{self.batch_size * self.world_size / dt:.0f} reward {stats['mean_reward']:.3f} "
+                            f"len {stats['mean_length']:.1f} kl {stats['kl']:.4f} lr {stats['lr']:.2e}")
+        return stats
+
+    # ------------------------------------------------------------------ checkpoints
+    def get_full_state_weights(self):
+        return {"model": self.model.state_dict(), "epoch": self.epoch_num, "frame": self.frame,
+                "optimizer": self.optimizer.state_dict(), "last_lr": float(self.lr)}
+
+    def save(self, path: str):
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        torch.save(self.get_full_state_weights(), path)
+
+    def restore(self, path: str):
+        ckpt = torch.load(path, map_location=self.device, weights_only=True)
+        self.model.load_state_dict(ckpt["model"])
+        self.epoch_num = int(ckpt.get("epoch", 0))
+        self.frame = int(ckpt.get("frame", 0))
+        if "optimizer" in ckpt:
+            self.optimizer.load_state_dict(ckpt["optimizer"])
+        lr = float(ckpt.get("last_lr", self.cfg.learning_rate))
+        self.lr.fill_(lr)
+        if self._opt_lr is not None:
+            self._opt_lr.fill_(lr)

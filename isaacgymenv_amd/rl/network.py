@@ -1,0 +1,104 @@
+"""rl_games ``actor_critic`` network (network_builder.A2CBuilder, separate=True, fixed sigma)
+and the ``continuous_a2c_logstd`` model (models.ModelA2CContinuousLogStd), rl-games 1.6.x.
+
+Train config: isaacgymenvs/cfg/train/AnymalTerrainPPO.yaml:8-30 (mlp 512-256-128 elu,
+separate actor/critic, sigma const 0 = std 1, fixed_sigma).  Linear weights keep PyTorch's
+default init (rl_games ``default`` initializer = identity), biases are zeroed, as rl_games does.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List
+
+import torch
+import torch.nn as nn
+
+from .running_mean_std import RunningMeanStd
+
+_ACT = {"elu": nn.ELU, "relu": nn.ReLU, "tanh": nn.Tanh, "selu": nn.SELU, "None": nn.Identity, None: nn.Identity}
+
+
+def _mlp(in_size: int, units: List[int], activation: str) -> nn.Sequential:
+    layers = []
+    for u in units:
+        layers += [nn.Linear(in_size, u), _ACT[activation]()]
+        in_size = u
+    return nn.Sequential(*layers)
+
+
+class ActorCriticNetwork(nn.Module):
+    def __init__(self, obs_dim: int, actions_num: int, units: List[int], activation: str = "elu",
+                 separate: bool = True, fixed_sigma: bool = True, sigma_init_val: float = 0.0, value_size: int = 1):
+        super().__init__()
+        self.separate = separate
+        self.fixed_sigma = fixed_sigma
+        self.actor_mlp = _mlp(obs_dim, units, activation)
+        self.critic_mlp = _mlp(obs_dim, units, activation) if separate else None
+        out = units[-1] if units else obs_dim
+        self.value = nn.Linear(out, value_size)
+        self.mu = nn.Linear(out, actions_num)
+        if fixed_sigma:
+            self.sigma = nn.Parameter(torch.zeros(actions_num, dtype=torch.float32), requires_grad=True)
+        else:
+            self.sigma = nn.Linear(out, actions_num)
+        for m in self.modules():
+            if isinstance(m, nn.Linear) and m.bias is not None:
+                nn.init.zeros_(m.bias)
+        with torch.no_grad():  # const_initializer
+            if fixed_sigma:
+                self.sigma.fill_(sigma_init_val)
+            else:
+                self.sigma.weight.fill_(sigma_init_val)
+
+    def forward(self, obs):
+        a_out = self.actor_mlp(obs)
+        c_out = self.critic_mlp(obs) if self.separate else a_out
+        value = self.value(c_out)
+        mu = self.mu(a_out)
+        logstd = mu * 0.0 + self.sigma if self.fixed_sigma else self.sigma(a_out)
+        return mu, logstd, value
+
+
+class ModelA2CContinuousLogStd(nn.Module):
+    """Input/value normalisation around the network; the act / train forward of rl_games."""
+
+    def __init__(self, net: ActorCriticNetwork, obs_dim: int, normalize_input: bool = True,
+                 normalize_value: bool = True, value_size: int = 1):
+        super().__init__()
+        self.a2c_network = net
+        self.normalize_input = normalize_input
+        self.normalize_value = normalize_value
+        if normalize_value:
+            self.value_mean_std = RunningMeanStd((value_size,))
+        if normalize_input:
+            self.running_mean_std = RunningMeanStd((obs_dim,))
+
+    def norm_obs(self, obs):
+        with torch.no_grad():
+            return self.running_mean_std(obs) if self.normalize_input else obs
+
+    def denorm_value(self, value):
+        with torch.no_grad():
+            return self.value_mean_std(value, unnorm=True) if self.normalize_value else value
+
+    @staticmethod
+    def neglogp(x, mean, std, logstd):
+        return 0.5 * torch.sum(((x - mean) / std) ** 2, dim=-1) \
+            + 0.5 * math.log(2.0 * math.pi) * x.size()[-1] + torch.sum(logstd, dim=-1)
+
+    def forward(self, input_dict: Dict[str, torch.Tensor]):
+        is_train = input_dict.get("is_train", True)
+        prev_actions = input_dict.get("prev_actions", None)
+        obs = self.norm_obs(input_dict["obs"])
+        mu, logstd, value = self.a2c_network(obs)
+        sigma = torch.exp(logstd)
+        distr = torch.distributions.Normal(mu, sigma, validate_args=False)
+        if is_train:
+            entropy = distr.entropy().sum(dim=-1)
+            prev_neglogp = self.neglogp(prev_actions, mu, sigma, logstd)
+            return {"prev_neglogp": torch.squeeze(prev_neglogp), "values": value, "entropy": entropy,
+                    "mus": mu, "sigmas": sigma}
+        selected_action = distr.sample()
+        neglogp = self.neglogp(selected_action, mu, sigma, logstd)
+        return {"neglogpacs": torch.squeeze(neglogp), "values": self.denorm_value(value),
+                "actions": selected_action, "mus": mu, "sigmas": sigma}

@@ -8,13 +8,14 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIBS = {"gymsim.h": "isaacgymenv_amd/_lib/libgymsim.so", "gymtask.h": "isaacgymenv_amd/_lib/libgymtask.so"}
+LIBS = {"gymsim.h": "isaacgymenv_amd/_lib/libgymsim.so", "gymtask.h": "isaacgymenv_amd/_lib/libgymtask.so",
+        "gymrl.h": "isaacgymenv_amd/_lib/libgymrl.so"}
 
 
 def _declared(header):
     text = open(os.path.join(ROOT, "include", header)).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b((?:gs|gt)_[a-z0-9_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b((?:gs|gt|rl)_[a-z0-9_]+)\s*\(", text)))
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -38,6 +39,9 @@ def test_python_bindings_cover_the_abi():
     from isaacgymenv_amd import gymtask
     assert sorted(_lib.EXPORTED_SYMBOLS) == _declared("gymsim.h")
     assert sorted(gymtask.EXPORTED_SYMBOLS) == _declared("gymtask.h")
+    from isaacgymenv_amd.rl import gae
+    assert sorted(gae.EXPORTED_SYMBOLS) == _declared("gymrl.h")
+    assert gae.lib().rl_abi_version() == 1
 
 
 def test_abi_version_and_topology_query():
