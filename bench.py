@@ -131,7 +131,7 @@ def ppo_leg(env, device, rank, world, epochs):
     pcfg = PpoConfig.from_train_cfg(train, multi_gpu=world > 1)
     agent = A2CAgent(env, pcfg, device=device, seed=42 + rank)
     agent.env_reset()
-    agent.train_epoch()  # warm-up: allocator, hipBLASLt heuristics, RCCL communicator
+    agent.train_epoch()  # warm-up: allocator, hipBLASLt heuristics, RCCL communicator; HIP graph capture
     # phase split of one (untimed) epoch, synchronised between the phases
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -142,8 +142,7 @@ def ppo_leg(env, device, rank, world, epochs):
     agent.prepare_dataset(returns, values)
     for _ in range(pcfg.mini_epochs):
         for i in range(agent.num_minibatches):
-            out = agent.calc_gradients(agent._minibatch(i))
-            agent._update_lr(out[3])
+            agent._run_minibatch(i)
     agent.model.eval()
     torch.cuda.synchronize()
     t2 = time.perf_counter()

@@ -135,7 +135,8 @@ class _AverageMeter:
 class A2CAgent:
     """rl_games A2CAgent (continuous) on one rank; ``world_size`` > 1 = data-parallel PPO."""
 
-    def __init__(self, env, cfg: PpoConfig, device: Optional[str] = None, seed: Optional[int] = None):
+    def __init__(self, env, cfg: PpoConfig, device: Optional[str] = None, seed: Optional[int] = None,
+                 use_graphs: bool = True):
         self.env = env
         self.cfg = cfg
         self.device = torch.device(device or env.rl_device)
@@ -173,7 +174,7 @@ class A2CAgent:
         if on_gpu:
             self._opt_lr = torch.tensor(cfg.learning_rate, dtype=torch.float32, device=self.device)
             self.optimizer = torch.optim.Adam(self.params, lr=self._opt_lr, eps=1e-08,
-                                              weight_decay=cfg.weight_decay, fused=True)
+                                              weight_decay=cfg.weight_decay, fused=True, capturable=True)
         else:
             self._opt_lr = None
             self.optimizer = torch.optim.Adam(self.params, lr=cfg.learning_rate, eps=1e-08,
@@ -201,6 +202,19 @@ class A2CAgent:
         self.frame = 0
         self.entropy_coef = cfg.entropy_coef
         self.last_stats: Dict[str, float] = {}
+        B = self.batch_size
+        self.d_values = torch.zeros(B, 1, dtype=torch.float32, device=dev)
+        self.d_returns = torch.zeros(B, 1, dtype=torch.float32, device=dev)
+        self.d_adv = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.dataset = {
+            "old_values": self.d_values, "returns": self.d_returns, "advantages": self.d_adv,
+            "old_logp_actions": self.b_neglogp.view(B), "actions": self.b_actions.view(B, -1),
+            "obs": self.b_obs.view(B, -1), "mu": self.b_mu.view(B, -1), "sigma": self.b_sigma.view(B, -1),
+        }
+        self._stats_acc = torch.zeros(4, dtype=torch.float32, device=dev)
+        self.use_graphs = on_gpu and use_graphs
+        self._act_graph = None
+        self._mb_graphs = None
 
     # ------------------------------------------------------------------ multi-GPU
     def _broadcast_params(self):
@@ -218,8 +232,16 @@ class A2CAgent:
 
     @torch.no_grad()
     def get_action_values(self, obs):
+        """rl_games A2CBase.get_action_values (eval-mode act forward).  After the first epoch on a
+        GPU the forward is a replayed HIP graph: the returned tensors are the graph's static outputs,
+        valid until the next call."""
+        obs = self._obs(obs)
+        if self._act_graph is not None:
+            self._g_obs.copy_(obs)
+            self._act_graph.replay()
+            return self._g_res
         self.model.eval()
-        return self.model({"is_train": False, "obs": self._obs(obs)})
+        return self.model({"is_train": False, "obs": obs})
 
     @torch.no_grad()
     def get_values(self, obs):
@@ -268,6 +290,7 @@ class A2CAgent:
 
     # ------------------------------------------------------------------ update
     def prepare_dataset(self, returns, values):
+        """rl_games A2CBase.prepare_dataset; results land in the persistent dataset buffers."""
         cfg = self.cfg
         advantages = returns - values
         values = values.unsqueeze(1)
@@ -280,21 +303,21 @@ class A2CAgent:
             vms.eval()
         if cfg.normalize_advantage:
             advantages = (advantages - advantages.mean()) / (advantages.std() + 1e-8)
-        B = self.batch_size
-        self.dataset = {
-            "old_values": values, "returns": returns, "advantages": advantages,
-            "old_logp_actions": self.b_neglogp.view(B), "actions": self.b_actions.view(B, -1),
-            "obs": self.b_obs.view(B, -1), "mu": self.b_mu.view(B, -1), "sigma": self.b_sigma.view(B, -1),
-        }
+        self.d_values.copy_(values)
+        self.d_returns.copy_(returns)
+        self.d_adv.copy_(advantages)
 
     def _minibatch(self, i):
         s = slice(i * self.cfg.minibatch_size, (i + 1) * self.cfg.minibatch_size)
         return {k: v[s] for k, v in self.dataset.items()}
 
-    def calc_gradients(self, mb):
+    def _mb_forward_backward(self, i):
+        """Phase 1 of a minibatch (rl_games calc_gradients up to backward): loss, scaled backward
+        into the flat gradient buffer."""
         cfg = self.cfg
         e = cfg.e_clip
-        with torch.autocast("cuda", dtype=torch.float16, enabled=self.mixed_precision):
+        mb = self._minibatch(i)
+        with torch.autocast("cuda", dtype=torch.float16, enabled=self.mixed_precision, cache_enabled=False):
             res = self.model({"is_train": True, "prev_actions": mb["actions"], "obs": mb["obs"]})
             action_log_probs, values, entropy = res["prev_neglogp"], res["values"], res["entropy"]
             mu, sigma = res["mus"], res["sigmas"]
@@ -314,10 +337,30 @@ class A2CAgent:
                 + b_loss * cfg.bounds_loss_coef
         self.flat_grad.zero_()
         self.scaler.scale(loss).backward()
-        self._truncate_gradients_and_step()
+        return (a_loss.detach(), c_loss.detach(), entropy.detach(), b_loss.detach(), mu.detach(), sigma.detach())
+
+    def _mb_step(self, i, out):
+        """Phase 2 (after the gradient all-reduce): unscale, clip, Adam, scaler update; KL of the
+        new policy against the dataset's old mu/sigma."""
+        if self.cfg.truncate_grads:
+            self.scaler.unscale_(self.optimizer)
+            nn.utils.clip_grad_norm_(self.params, self.cfg.grad_norm)
+        self.scaler.step(self.optimizer)
+        self.scaler.update()
+        mb = self._minibatch(i)
         with torch.no_grad():
-            kl = self._policy_kl(mu.detach(), sigma.detach(), mb["mu"], mb["sigma"])
-        return a_loss.detach(), c_loss.detach(), entropy.detach(), kl, mu.detach(), sigma.detach(), b_loss.detach()
+            return self._policy_kl(out[4], out[5], mb["mu"], mb["sigma"])
+
+    def _mb_finish(self, i, out, kl):
+        """Phase 3 (after the KL all-reduce, which sums): dataset.update_mu_sigma, adaptive LR,
+        diagnostics."""
+        s = slice(i * self.cfg.minibatch_size, (i + 1) * self.cfg.minibatch_size)
+        with torch.no_grad():
+            self.dataset["mu"][s] = out[4]
+            self.dataset["sigma"][s] = out[5]
+            kl = kl / self.world_size if self.multi_gpu else kl
+            self._update_lr(kl)
+            self._stats_acc += torch.stack([out[0].float(), out[1].float(), kl.float(), out[2].float()])
 
     @staticmethod
     def _policy_kl(p0_mu, p0_sigma, p1_mu, p1_sigma):
@@ -325,24 +368,26 @@ class A2CAgent:
         c2 = (p0_sigma ** 2 + (p1_mu - p0_mu) ** 2) / (2.0 * (p1_sigma ** 2 + 1e-5))
         return (c1 + c2 - 0.5).sum(dim=-1).mean()
 
-    def _truncate_gradients_and_step(self):
+    def _allreduce_grads(self):
+        dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
+        self.flat_grad.div_(self.world_size)
+
+    def calc_gradients(self, mb_index):
+        """One minibatch update (rl_games calc_gradients + trancate_gradients_and_step +
+        update_mu_sigma + scheduler), eager."""
+        out = self._mb_forward_backward(mb_index)
         if self.multi_gpu:
-            dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
-            self.flat_grad.div_(self.world_size)
-        if self.cfg.truncate_grads:
-            self.scaler.unscale_(self.optimizer)
-            nn.utils.clip_grad_norm_(self.params, self.cfg.grad_norm)
-        self.scaler.step(self.optimizer)
-        self.scaler.update()
+            self._allreduce_grads()
+        kl = self._mb_step(mb_index, out)
+        if self.multi_gpu:
+            dist.all_reduce(kl, op=dist.ReduceOp.SUM)
+        self._mb_finish(mb_index, out, kl)
+        return out, kl
 
     def _update_lr(self, kl):
-        """AdaptiveScheduler.update on the device (rl_games schedulers.py)."""
+        """AdaptiveScheduler.update on the device (rl_games schedulers.py); ``kl`` is the rank average."""
         if self.cfg.lr_schedule != "adaptive":
             return
-        if self.multi_gpu:
-            kl = kl.clone()
-            dist.all_reduce(kl, op=dist.ReduceOp.SUM)
-            kl = kl / self.world_size
         thr = self.cfg.kl_threshold
         kl = kl.double()
         cur = self.lr
@@ -355,34 +400,79 @@ class A2CAgent:
             for g in self.optimizer.param_groups:
                 g["lr"] = float(lr)
 
+    # ------------------------------------------------------------------ HIP graphs
+    def _capture_graphs(self):
+        """Capture the act forward and every minibatch update as HIP graphs (after one eager epoch
+        has initialised optimizer state, scaler and BLAS handles).  Collectives stay outside the
+        graphs: with N ranks a minibatch is three graphs around the gradient and KL all-reduces."""
+        torch.cuda.synchronize(self.device)
+        self.model.eval()
+        self._g_obs = torch.zeros(self.num_actors, self.obs_dim, dtype=torch.float32, device=self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=torch.cuda.graph_pool_handle()):
+            with torch.no_grad():
+                self._g_res = self.model({"is_train": False, "obs": self._g_obs})
+        self._act_graph = g
+        self.model.train()
+        pool = torch.cuda.graph_pool_handle()
+        self._mb_graphs = []
+        for i in range(self.num_minibatches):
+            if not self.multi_gpu:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    out = self._mb_forward_backward(i)
+                    kl = self._mb_step(i, out)
+                    self._mb_finish(i, out, kl)
+                self._mb_graphs.append((g,))
+            else:
+                g1, g2, g3 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g1, pool=pool):
+                    out = self._mb_forward_backward(i)
+                with torch.cuda.graph(g2, pool=pool):
+                    self.flat_grad.div_(self.world_size)
+                    kl = self._mb_step(i, out)
+                with torch.cuda.graph(g3, pool=pool):
+                    self._mb_finish(i, out, kl)
+                self._mb_graphs.append((g1, g2, g3, kl))
+        self.model.eval()
+        torch.cuda.synchronize(self.device)
+
+    def _run_minibatch(self, i):
+        if self._mb_graphs is None:
+            self.calc_gradients(i)
+            return
+        gs = self._mb_graphs[i]
+        if len(gs) == 1:
+            gs[0].replay()
+            return
+        g1, g2, g3, kl = gs
+        g1.replay()
+        dist.all_reduce(self.flat_grad, op=dist.ReduceOp.SUM)
+        g2.replay()
+        dist.all_reduce(kl, op=dist.ReduceOp.SUM)
+        g3.replay()
+
     def train_epoch(self):
         t0 = time.perf_counter()
         returns, values = self.play_steps()
         t1 = time.perf_counter()
         self.model.train()
         self.prepare_dataset(returns, values)
-        kls, a_losses, c_losses = [], [], []
+        self._stats_acc.zero_()
         for _ in range(self.cfg.mini_epochs):
             for i in range(self.num_minibatches):
-                mb = self._minibatch(i)
-                a_loss, c_loss, entropy, kl, cmu, csigma, b_loss = self.calc_gradients(mb)
-                s = slice(i * self.cfg.minibatch_size, (i + 1) * self.cfg.minibatch_size)
-                self.dataset["mu"][s] = cmu
-                self.dataset["sigma"][s] = csigma
-                self._update_lr(kl)
-                kls.append(kl)
-                a_losses.append(a_loss)
-                c_losses.append(c_loss)
+                self._run_minibatch(i)
         self.model.eval()
         self.epoch_num += 1
-        self._epoch_tensors = (torch.stack(kls), torch.stack(a_losses), torch.stack(c_losses))
+        if self.use_graphs and self._mb_graphs is None:
+            self._capture_graphs()
         return t1 - t0
 
     def epoch_stats(self) -> Dict[str, float]:
         """Host copy of the last epoch's diagnostics (one sync; not called inside the loop)."""
-        kls, a, c = self._epoch_tensors
-        return {"epoch": self.epoch_num, "frame": self.frame, "kl": float(kls.mean()), "a_loss": float(a.mean()),
-                "c_loss": float(c.mean()), "lr": float(self.lr), "mean_reward": float(self.game_rewards.mean),
+        a, c, kl, ent = (self._stats_acc / (self.cfg.mini_epochs * self.num_minibatches)).tolist()
+        return {"epoch": self.epoch_num, "frame": self.frame, "kl": kl, "a_loss": a, "c_loss": c, "entropy": ent,
+                "lr": float(self.lr), "mean_reward": float(self.game_rewards.mean),
                 "mean_length": float(self.game_lengths.mean)}
 
     def train(self, max_epochs: Optional[int] = None, log_every: int = 10, printer=print):

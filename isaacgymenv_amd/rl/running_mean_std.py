@@ -36,8 +36,12 @@ class RunningMeanStd(nn.Module):
         if self.training:
             mean = input.mean(self.axis)
             var = input.var(self.axis)
-            self.running_mean, self.running_var, self.count = self._update_mean_var_count_from_moments(
+            new_mean, new_var, new_count = self._update_mean_var_count_from_moments(
                 self.running_mean, self.running_var, self.count, mean, var, input.size()[0])
+            # in place (rl_games rebinds the buffers): the update is then replayable in a HIP graph
+            self.running_mean.copy_(new_mean)
+            self.running_var.copy_(new_var)
+            self.count.copy_(new_count)
         current_mean, current_var = self.running_mean, self.running_var
         if unnorm:
             y = torch.clamp(input, min=-5.0, max=5.0)

@@ -167,8 +167,8 @@ def _dp_worker(rank, world, port, q):
     env = ToyEnv(32, seed=rank)
     agent = A2CAgent(env, _toy_cfg(multi_gpu=True, minibatch_size=64, lr_schedule=None, truncate_grads=False), device="cpu")
     agent.model.train()
-    mb = _dp_batch(rank)
-    agent.calc_gradients(mb)
+    _load_mb(agent, _dp_batch(rank))
+    agent.calc_gradients(0)
     flat = torch.cat([p.detach().reshape(-1) for p in agent.params])
     q.put((rank, flat.numpy(), agent.flat_grad.numpy().copy()))
     dist.destroy_process_group()
@@ -204,15 +204,16 @@ def test_data_parallel_allreduce_gloo_world2():
     np.testing.assert_allclose(out[0][1], (grads[0] + grads[1]) / 2, rtol=2e-4, atol=1e-6)
 
 
+def _load_mb(agent, mb):
+    n = len(mb["obs"])
+    for k, v in mb.items():
+        agent.dataset[k][:n] = v
+
+
 def _grad_only(agent, mb):
     """Gradient of the PPO loss on one minibatch, without stepping (same loss code path)."""
-    step = agent._truncate_gradients_and_step
-    agent._truncate_gradients_and_step = lambda: None
-    try:
-        agent.model.running_mean_std.train()
-        rms_state = {k: v.clone() for k, v in agent.model.running_mean_std.state_dict().items()}
-        agent.calc_gradients(mb)
-        agent.model.running_mean_std.load_state_dict(rms_state)
-    finally:
-        agent._truncate_gradients_and_step = step
+    _load_mb(agent, mb)
+    rms_state = {k: v.clone() for k, v in agent.model.running_mean_std.state_dict().items()}
+    agent._mb_forward_backward(0)
+    agent.model.running_mean_std.load_state_dict(rms_state)
     return agent.flat_grad.numpy().copy()

@@ -54,15 +54,14 @@ def _agent(task, num_envs, **over):
 
 
 def test_cartpole_ppo_learns():
+    # rl_games solves Cartpole (episode 500 steps) in ~100 epochs; this learner reaches ~490 mean
+    # episode length by epoch 60 (tools/ppo_probe.py); random play lasts ~3 steps
     agent = _agent("Cartpole", 512)
-    rew = []
-    for ep in range(40):
+    for ep in range(60):
         agent.train_epoch()
-        rew.append(float(agent.t_rewards.mean()))
-    early, late = np.mean(rew[:5]), np.mean(rew[-5:])
-    # reward per step: ~1 while the pole is up, -2 on a failure -> fewer failures = higher mean
-    assert late > early + 0.05, rew
-    assert np.isfinite(agent.epoch_stats()["kl"])
+    s = agent.epoch_stats()
+    assert s["mean_length"] > 250, s
+    assert np.isfinite(s["kl"])
 
 
 def test_anymal_terrain_ppo_epochs():
@@ -74,3 +73,21 @@ def test_anymal_terrain_ppo_epochs():
     assert np.isfinite(s["kl"]) and np.isfinite(s["a_loss"]) and np.isfinite(s["c_loss"])
     assert all(torch.isfinite(p).all() for p in agent.params)
     assert agent.frame == 2 * 24 * 4096
+
+
+def test_graph_replay_equals_eager_updates():
+    """The HIP-graph path (captured after epoch 1) performs the same updates as the eager path."""
+    runs = []
+    for graphs in (False, True):
+        torch.manual_seed(0)
+        agent = _agent("Cartpole", 512)
+        agent.use_graphs = graphs
+        for _ in range(3):
+            agent.train_epoch()
+        assert (agent._mb_graphs is not None) == graphs
+        runs.append((torch.cat([p.detach().reshape(-1) for p in agent.params]).cpu(), agent.epoch_stats(),
+                     agent.b_obs.cpu()))
+    (pe, se, oe), (pg, sg, og) = runs
+    torch.testing.assert_close(og, oe, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(pg, pe, rtol=1e-3, atol=1e-5)
+    assert abs(sg["lr"] - se["lr"]) <= 1e-9 + 1e-6 * se["lr"]
