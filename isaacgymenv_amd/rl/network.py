@@ -98,7 +98,9 @@ class ModelA2CContinuousLogStd(nn.Module):
             prev_neglogp = self.neglogp(prev_actions, mu, sigma, logstd)
             return {"prev_neglogp": torch.squeeze(prev_neglogp), "values": value, "entropy": entropy,
                     "mus": mu, "sigmas": sigma}
-        selected_action = distr.sample()
+        # = Normal.sample() = torch.normal(mu, sigma), whose ATen body is normal_(0, 1) * std + mean;
+        # spelled out because torch.normal's std >= 0 check syncs the host (not capturable in a graph)
+        selected_action = torch.empty_like(mu).normal_(0.0, 1.0).mul_(sigma).add_(mu)
         neglogp = self.neglogp(selected_action, mu, sigma, logstd)
         return {"neglogpacs": torch.squeeze(neglogp), "values": self.denorm_value(value),
                 "actions": selected_action, "mus": mu, "sigmas": sigma}
