@@ -37,6 +37,8 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+import isaacgymenv_amd
+
 from .gae import discount_values
 from .network import ActorCriticNetwork, ModelA2CContinuousLogStd
 
@@ -212,7 +214,8 @@ class A2CAgent:
             "obs": self.b_obs.view(B, -1), "mu": self.b_mu.view(B, -1), "sigma": self.b_sigma.view(B, -1),
         }
         self._stats_acc = torch.zeros(4, dtype=torch.float32, device=dev)
-        self.use_graphs = on_gpu and use_graphs
+        # graphs only with HIP graph packet capture off (isaacgymenv_amd/__init__.py)
+        self.use_graphs = on_gpu and use_graphs and isaacgymenv_amd.GRAPHS_SAFE
         self._act_graph = None
         self._mb_graphs = None
 

@@ -91,3 +91,26 @@ def test_graph_replay_equals_eager_updates():
     torch.testing.assert_close(og, oe, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(pg, pe, rtol=1e-3, atol=1e-5)
     assert abs(sg["lr"] - se["lr"]) <= 1e-9 + 1e-6 * se["lr"]
+
+
+def test_graph_replayed_backward_is_replay_invariant():
+    """A captured minibatch forward+backward gives the eager gradient on every replay (with HIP
+    graph packet capture on, the first hidden-layer bias gradient drifted from a later replay on;
+    isaacgymenv_amd/__init__.py turns it off)."""
+    import isaacgymenv_amd
+    assert isaacgymenv_amd.GRAPHS_SAFE
+    agent = _agent("Cartpole", 512)
+    agent.use_graphs = False
+    agent.train_epoch()
+    agent.model.train()
+    agent.model.running_mean_std.eval()  # frozen input statistics: every call sees the same batch
+    agent._mb_forward_backward(0)
+    torch.cuda.synchronize()
+    ref = agent.flat_grad.clone()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, pool=torch.cuda.graph_pool_handle()):
+        agent._mb_forward_backward(0)
+    for _ in range(4):
+        g.replay()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(agent.flat_grad, ref, rtol=1e-5, atol=1e-6)
