@@ -22,6 +22,12 @@
  *       dof state   [num_envs*num_dofs][2] (pos, vel)
  *       dof force   [num_envs*num_dofs]
  *       net contact [num_envs*num_bodies][3]
+ *       rigid body  [num_envs*num_bodies][13] pos(3) quat xyzw(4) lin vel of COM(3) ang vel(3)
+ *       jacobian    [num_envs][num_bodies][6][nv]  rows: COM lin vel (3), ang vel (3), world axes
+ *       mass matrix [num_envs][nv][nv]
+ *     num_bodies counts reported links (fixed-joint links included when
+ *     collapse_fixed_joints=False); nv = 6 + num_dofs (floating base: root COM
+ *     linear velocity, root angular velocity, then dof velocities) or num_dofs.
  *     (one articulation actor per env; actor index == env index)
  */
 #ifndef GYMSIM_H
@@ -33,7 +39,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 1
+#define GS_ABI_VERSION 2
 
 typedef struct gs_sim gs_sim;
 
@@ -59,6 +65,14 @@ typedef struct gs_model_desc {
     const double *dof_lower;      /* [nd] joint limits (rad or m), used where has_limits */
     const double *dof_upper;      /* [nd]                                               */
     const int32_t *dof_has_limits;/* [nd] 0/1 (URDF <limit>, MJCF limited="true")     */
+    /* reported links (ABI 2): the tensor API's rigid bodies.  Equal to the bodies unless
+     * fixed joints are kept (collapse_fixed_joints=False), then each fixed link is welded
+     * into a body for the dynamics but still reported (Hound.urdf: 19 bodies, 24 links). */
+    int32_t num_links;
+    const int32_t *cand_link;     /* [nc] link whose net contact force the candidate adds to */
+    const int32_t *link_body;     /* [nl] dynamic body the link is welded into          */
+    const double *link_pose;      /* [nl][12] link frame in the body frame: R (9) t (3) */
+    const double *link_com;       /* [nl][3] link COM, link frame                       */
 } gs_model_desc;
 
 /* gymapi.SimParams subset the reference sets (vec_task.py:514-562). */
@@ -144,6 +158,15 @@ int gs_sim_simulate(gs_sim *sim, const float *dof_force, void *stream);
 int gs_sim_refresh_root(gs_sim *sim, float *root_state, void *stream);
 int gs_sim_refresh_dof(gs_sim *sim, float *dof_state, void *stream);
 int gs_sim_refresh_contact(gs_sim *sim, float *net_contact, void *stream);
+
+/* refresh_rigid_body_state_tensor / refresh_jacobian_tensors / refresh_mass_matrix_tensors
+ * (useful_hound.py:440-455 acquire, :725-732 refresh).  Kinematics of the current state:
+ * link poses and COM velocities, the link COM Jacobians in the generalized velocities
+ * above, and M = sum_b J_b^T diag(m_b, I_b) J_b over the dynamic bodies (so v^T M v / 2 is
+ * the kinetic energy).  Layouts in the header comment. */
+int gs_sim_refresh_rigid_body(gs_sim *sim, float *rigid_body_state, void *stream);
+int gs_sim_refresh_jacobian(gs_sim *sim, float *jacobian, void *stream);
+int gs_sim_refresh_mass_matrix(gs_sim *sim, float *mass_matrix, void *stream);
 
 /* set_actor_root_state_tensor(_indexed) / set_dof_state_tensor(_indexed):
  * rows `idx[0..n_idx)` (int32 actor ids) of the full source tensor; idx NULL = all envs.

@@ -18,11 +18,11 @@ LIBDIR = os.path.join(HERE, "_lib")
 ARCH = os.environ.get("GS_OFFLOAD_ARCH", "gfx950")
 
 LIBS = {
-    "libgymsim.so": ["gs_physics.hip", "gs_team.hip", "gs_capi.hip"],
+    "libgymsim.so": ["gs_physics.hip", "gs_team.hip", "gs_kinematics.hip", "gs_capi.hip"],
     "libgymtask.so": ["gt_anymal.hip"],
     "libgymrl.so": ["rl_gae.hip"],
     # phase-profiling build of the simulator (tools/phase_profile.py); never loaded by default
-    "libgymsim_prof.so": ["gs_physics.hip", "gs_team.hip", "gs_capi.hip"],
+    "libgymsim_prof.so": ["gs_physics.hip", "gs_team.hip", "gs_kinematics.hip", "gs_capi.hip"],
 }
 # the task kernels mirror torch's unfused elementwise arithmetic
 # -fno-slp-vectorize: the SLP vectorizer packs the scalar spatial algebra into v_pk_* pairs and

@@ -36,6 +36,13 @@ std::string signature(const gs_model_desc* m) {
   for (int i = 0; i < m->num_bodies; ++i) s += (i ? "-" : "") + std::to_string(m->parent[i]);
   s += "_c";
   for (int i = 0; i < m->num_candidates; ++i) s += (i ? "-" : "") + std::to_string(m->cand_body[i]);
+  // kept fixed-joint links change the compiled contact-force tables (_model.topology_signature)
+  bool links_differ = m->num_links != m->num_bodies;
+  for (int i = 0; i < m->num_candidates && !links_differ; ++i) links_differ = m->cand_link[i] != m->cand_body[i];
+  if (links_differ) {
+    s += "_l" + std::to_string(m->num_links) + "_";
+    for (int i = 0; i < m->num_candidates; ++i) s += (i ? "-" : "") + std::to_string(m->cand_link[i]);
+  }
   return s;
 }
 
@@ -59,6 +66,8 @@ struct gs_sim {
   int variant = 0;  // kernel actually selected: 1 lane, 2 team
   DevModel* d_model = nullptr;
   DevModel h_model{};             // host copy (sensors are added after set_model)
+  DevLinks* d_links = nullptr;    // link kinematics tables (gs_kinematics.hip)
+  int nr = 0, nv = 0;
   std::vector<int> parent;
   float* sens = nullptr;          // [6*nsens][N]
   int nb = 0, nd = 0, nc = 0, ns = 0;
@@ -113,6 +122,7 @@ void gs_sim_destroy(gs_sim* s) {
   if (!s) return;
   hipSetDevice(s->device);
   if (s->d_model) hipFree(s->d_model);
+  if (s->d_links) hipFree(s->d_links);
   if (s->d_tverts) hipFree(s->d_tverts);
   if (s->d_tcells) hipFree(s->d_tcells);
   if (s->ev0) hipEventDestroy(s->ev0);
@@ -225,8 +235,15 @@ int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_verti
 
 int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   if (!s || !m) return fail("gs_sim_set_model: null argument");
-  if (m->num_bodies > GS_MAXB || m->num_dofs > GS_MAXD || m->num_candidates > GS_MAXC)
-    return fail("gs_sim_set_model: articulation exceeds compiled maxima (bodies/dofs/candidates)");
+  if (m->num_bodies > GS_MAXB || m->num_dofs > GS_MAXD || m->num_candidates > GS_MAXC || m->num_links > GS_MAXL)
+    return fail("gs_sim_set_model: articulation exceeds compiled maxima (bodies/dofs/candidates/links)");
+  if (m->num_links < m->num_bodies || !m->link_body || !m->link_pose || !m->link_com ||
+      (m->num_candidates > 0 && !m->cand_link))
+    return fail("gs_sim_set_model: link tables missing (gs_model_desc ABI 2: num_links >= num_bodies)");
+  for (int l = 0; l < m->num_links; ++l)
+    if (m->link_body[l] < 0 || m->link_body[l] >= m->num_bodies) return fail("gs_sim_set_model: link_body out of range");
+  for (int c = 0; c < m->num_candidates; ++c)
+    if (m->cand_link[c] < 0 || m->cand_link[c] >= m->num_links) return fail("gs_sim_set_model: cand_link out of range");
   const TopoEntry* t = find_topology(m);
   if (!t)
     return fail("gs_sim_set_model: no compiled kernel for topology %s (add it to tools/gen_topologies.py)",
@@ -242,6 +259,12 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
     const double* I = m->inertia + 9 * i;
     h.inertia[i][0] = (float)I[0]; h.inertia[i][1] = (float)I[4]; h.inertia[i][2] = (float)I[8];
     h.inertia[i][3] = (float)I[1]; h.inertia[i][4] = (float)I[2]; h.inertia[i][5] = (float)I[5];
+  }
+  {  // root link COM in the body-0 frame: link pose (identity for the root link) applied to its COM
+    const double* P = m->link_pose;
+    const double* c = m->link_com;
+    for (int k = 0; k < 3; ++k)
+      h.root_com[k] = (float)(P[9 + k] + P[3 * k] * c[0] + P[3 * k + 1] * c[1] + P[3 * k + 2] * c[2]);
   }
   for (int c = 0; c < m->num_candidates; ++c) {
     for (int k = 0; k < 3; ++k) h.cpoint[c][k] = (float)m->cand_point[3 * c + k];
@@ -287,6 +310,35 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
     s->pd_fn = t->pd;
     s->variant = 1;
   }
+  DevLinks hl;
+  std::memset(&hl, 0, sizeof(hl));
+  hl.nb = m->num_bodies;
+  hl.nd = m->num_dofs;
+  hl.nr = m->num_links;
+  hl.fixed_base = m->fixed_base;
+  for (int b = 0; b < m->num_bodies; ++b) {
+    hl.parent[b] = m->parent[b];
+    hl.jkind[b] = m->joint_kind[b];
+    hl.bdof[b] = m->body_dof[b];
+    unsigned mask = 0;
+    for (int a = b; a >= 0; a = m->parent[a]) mask |= 1u << a;
+    hl.anc_mask[b] = mask;
+    if (m->body_dof[b] >= 0) hl.dbody[m->body_dof[b]] = b;
+  }
+  for (int l = 0; l < m->num_links; ++l) {
+    hl.lbody[l] = m->link_body[l];
+    for (int k = 0; k < 9; ++k) hl.lR[l][k] = (float)m->link_pose[12 * l + k];
+    for (int k = 0; k < 3; ++k) hl.lt[l][k] = (float)m->link_pose[12 * l + 9 + k];
+    for (int k = 0; k < 3; ++k) hl.lcom[l][k] = (float)m->link_com[3 * l + k];
+  }
+  if (!s->d_links) {
+    hipError_t e2 = hipMalloc(&s->d_links, sizeof(DevLinks));
+    if (e2 != hipSuccess) return hip_fail(e2, "gs_sim_set_model hipMalloc links");
+  }
+  e = hipMemcpy(s->d_links, &hl, sizeof(DevLinks), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "gs_sim_set_model hipMemcpy links");
+  s->nr = m->num_links;
+  s->nv = (m->fixed_base ? 0 : 6) + m->num_dofs;
   s->nb = m->num_bodies;
   s->nd = m->num_dofs;
   s->nc = m->num_candidates;
@@ -356,7 +408,7 @@ int gs_sim_pd_step(gs_sim* s, const gs_pd_args* a, void* stream) {
 
 int gs_sim_refresh_root(gs_sim* s, float* out, void* stream) {
   if (ready(s, "gs_sim_refresh_root")) return -1;
-  hipError_t e = launch_refresh_root(s->state, s->N, s->nd, &s->d_model->com[0][0], out, (hipStream_t)stream);
+  hipError_t e = launch_refresh_root(s->state, s->N, s->nd, &s->d_model->root_com[0], out, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_root");
 }
 int gs_sim_refresh_dof(gs_sim* s, float* out, void* stream) {
@@ -366,12 +418,33 @@ int gs_sim_refresh_dof(gs_sim* s, float* out, void* stream) {
 }
 int gs_sim_refresh_contact(gs_sim* s, float* out, void* stream) {
   if (ready(s, "gs_sim_refresh_contact")) return -1;
-  hipError_t e = launch_refresh_contact(s->cf, s->N, s->nb, out, (hipStream_t)stream);
+  hipError_t e = launch_refresh_contact(s->cf, s->N, s->nr, out, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_contact");
+}
+int gs_sim_refresh_rigid_body(gs_sim* s, float* out, void* stream) {
+  if (ready(s, "gs_sim_refresh_rigid_body")) return -1;
+  if (!out) return fail("gs_sim_refresh_rigid_body: null output");
+  hipError_t e = launch_kinematics(s->d_model, s->d_links, s->state, s->N, s->nv, 1, out, nullptr, nullptr,
+                                   (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_rigid_body");
+}
+int gs_sim_refresh_jacobian(gs_sim* s, float* out, void* stream) {
+  if (ready(s, "gs_sim_refresh_jacobian")) return -1;
+  if (!out) return fail("gs_sim_refresh_jacobian: null output");
+  hipError_t e = launch_kinematics(s->d_model, s->d_links, s->state, s->N, s->nv, 2, nullptr, out, nullptr,
+                                   (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_jacobian");
+}
+int gs_sim_refresh_mass_matrix(gs_sim* s, float* out, void* stream) {
+  if (ready(s, "gs_sim_refresh_mass_matrix")) return -1;
+  if (!out) return fail("gs_sim_refresh_mass_matrix: null output");
+  hipError_t e = launch_kinematics(s->d_model, s->d_links, s->state, s->N, s->nv, 4, nullptr, nullptr, out,
+                                   (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_mass_matrix");
 }
 int gs_sim_set_root(gs_sim* s, const float* src, const int32_t* idx, int n_idx, void* stream) {
   if (ready(s, "gs_sim_set_root")) return -1;
-  hipError_t e = launch_set_root(s->state, s->N, s->nd, &s->d_model->com[0][0], src, idx, n_idx,
+  hipError_t e = launch_set_root(s->state, s->N, s->nd, &s->d_model->root_com[0], src, idx, n_idx,
                                  (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_set_root");
 }

@@ -6,7 +6,8 @@
 
 #define GS_MAXB 32   // bodies per articulation
 #define GS_MAXD 32   // dofs per articulation
-#define GS_MAXC 64   // plane-contact candidates per articulation
+#define GS_MAXC 96   // plane-contact candidates per articulation
+#define GS_MAXL 40   // reported links per articulation (fixed-joint links included)
 #define GS_MAXS 8    // force sensors per articulation
 #define GS_WAVE 64
 
@@ -19,6 +20,8 @@ struct DevModel {
   float jaxis[GS_MAXB][3];   // joint axis in the joint frame
   float mass[GS_MAXB];
   float com[GS_MAXB][3];     // body frame
+  float root_com[3];         // COM of the root LINK, body-0 frame (root tensor velocity point; = com[0]
+                             // unless fixed-joint links are welded into the root body)
   float inertia[GS_MAXB][6]; // about COM, body axes: xx yy zz xy xz yz
   float cpoint[GS_MAXC][3];  // contact candidate, body frame
   float cradius[GS_MAXC];
@@ -52,7 +55,7 @@ struct DevParams {
 struct SimBuffers {
   float* state;
   const float* mu;       // [ns][N]
-  float* cf;             // [3*nb][N]
+  float* cf;             // [3*nr][N]  (nr reported links)
   int N;
   float* sens;           // [6*nsens][N] force-sensor readings or null
 };
@@ -66,7 +69,7 @@ struct PdDev {
   float* torques_out;        // [N][nd]
   float* dof_out;            // [N*nd][2] or null
   float* root_out;           // [N][13]   or null
-  float* cf_out;             // [N*nb][3] or null
+  float* cf_out;             // [N*nr][3] or null
   float* actions_copy;       // [N][nd]   or null
 };
 
@@ -81,6 +84,21 @@ struct TopoEntry {
   launch_sim_fn sim;
   launch_pd_fn pd;
   int nb, nd, nc, ns;
+};
+
+// Kinematics of the reported links (gs_kinematics.hip): runtime-sized tree tables, one copy in
+// device memory next to the DevModel.
+struct DevLinks {
+  int nb, nd, nr, fixed_base;
+  int parent[GS_MAXB];
+  int jkind[GS_MAXB];
+  int bdof[GS_MAXB];
+  unsigned anc_mask[GS_MAXB];  // bit a set: body a is b or an ancestor of b
+  int dbody[GS_MAXD];          // body moved by dof j
+  int lbody[GS_MAXL];
+  float lR[GS_MAXL][9];        // link frame in the body frame
+  float lt[GS_MAXL][3];
+  float lcom[GS_MAXL][3];      // link COM, link frame
 };
 
 extern TopoEntry g_topologies[];
@@ -100,6 +118,9 @@ hipError_t launch_terrain_query(const DevParams& P, const float* c, const float*
 hipError_t launch_refresh_root(const float* state, int N, int nd, const float* com0, float* out, hipStream_t s);
 hipError_t launch_refresh_dof(const float* state, int N, int nd, float* out, hipStream_t s);
 hipError_t launch_refresh_contact(const float* cf, int N, int nb, float* out, hipStream_t s);
+// mode bits: 1 rigid body state [N*nr][13], 2 jacobian [N][nr][6][nv], 4 mass matrix [N][nv][nv]
+hipError_t launch_kinematics(const DevModel* M, const DevLinks* L, const float* state, int N, int nv, int mode,
+                             float* rb, float* jac, float* mm, hipStream_t s);
 hipError_t launch_refresh_sensor(const float* soa, int N, int ns, float* out, hipStream_t s);
 hipError_t launch_set_root(float* state, int N, int nd, const float* com0, const float* src, const int* idx,
                            int n_idx, hipStream_t s);

@@ -51,7 +51,9 @@ __device__ __forceinline__ constexpr bool body_on_path(int kk, int b) {
 template <class T, bool TERR = false>
 struct LaneCfg {
   static constexpr int SLOTS = T::NSLOT + (TERR ? 3 * T::NC : 0);
-  static constexpr int LB = (SLOTS * 64 * 4 <= 160 * 1024) ? 64 : (SLOTS * 32 * 4 <= 160 * 1024) ? 32 : 16;
+  static constexpr int LB = (SLOTS * 64 * 4 <= 160 * 1024) ? 64 : (SLOTS * 32 * 4 <= 160 * 1024) ? 32
+                           : (SLOTS * 16 * 4 <= 160 * 1024) ? 16 : 8;
+  static_assert(SLOTS * LB * 4 <= 160 * 1024, "contact rows exceed the LDS of a CU even at 8 lanes");
 };
 
 // World-frame force of candidate c's impulses (normal from LDS, tangents rebuilt), / h.
@@ -661,13 +663,14 @@ __device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const 
     s.qd[j] = nun[NB6 + j];
   }
   if (collect) {
-    // net contact force per body of this (collecting) substep, SoA [3*nb][N]
+    // net contact force per reported link of this (collecting) substep, SoA [3*nr][N]
+    // (links = bodies unless fixed-joint links are kept: then a candidate adds to its own link)
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
+    for (int b = 0; b < T::NR; ++b) {
       float f0 = 0.f, f1 = 0.f, f2 = 0.f;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        if (T::cbody[c] == b) {
+        if (T::clink[c] == b) {
           if constexpr (TERR) {
             if (act[c]) {
               float fw[3];
@@ -765,7 +768,7 @@ template <class T>
 __device__ __forceinline__ void com_velocity(const DevModel* __restrict__ M, const EnvState<T>& s, float* v) {
   float R[9], c[3], wc[3];
   quat_to_mat(s.quat, R);
-  mat3vec(R, M->com[0], c);
+  mat3vec(R, M->root_com, c);
   cross3(s.w, c, wc);
   v[0] = s.vo[0] + wc[0]; v[1] = s.vo[1] + wc[1]; v[2] = s.vo[2] + wc[2];
 }
@@ -849,9 +852,9 @@ __global__ __launch_bounds__((LaneCfg<T, TERR>::LB), 1) void k_pd_step(const Dev
   }
   if (P.collect && A.cf_out) {
 #pragma unroll
-    for (int b = 0; b < T::NB; ++b)
+    for (int b = 0; b < T::NR; ++b)
 #pragma unroll
-      for (int k = 0; k < 3; ++k) A.cf_out[((size_t)e * T::NB + b) * 3 + k] = B.cf[(3 * b + k) * N + e];
+      for (int k = 0; k < 3; ++k) A.cf_out[((size_t)e * T::NR + b) * 3 + k] = B.cf[(3 * b + k) * N + e];
   }
 }
 

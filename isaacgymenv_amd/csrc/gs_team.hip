@@ -921,7 +921,7 @@ template <class T>
 __device__ __forceinline__ void team_com_velocity(const DevModel* __restrict__ M, const TeamState<T>& s, float* v) {
   float R[9], c[3], wc[3];
   quat_to_mat(s.quat, R);
-  mat3vec(R, M->com[0], c);
+  mat3vec(R, M->root_com, c);
   cross3(s.w, c, wc);
   v[0] = s.vo[0] + wc[0]; v[1] = s.vo[1] + wc[1]; v[2] = s.vo[2] + wc[2];
 }
@@ -1027,6 +1027,7 @@ template <class T>
 hipError_t launch_sim_team(const DevModel* M, const DevParams& P, const SimBuffers& B, const float* tau,
                            hipStream_t st) {
   if constexpr (T::HAS_TEAM) {
+    static_assert(T::NR == T::NB, "the lane team reports contact forces per body (no kept fixed-joint links)");
     const long lanes = (long)B.N * T::T_LANES;
     const int blocks = (int)((lanes + kTeamBlock - 1) / kTeamBlock);
     hipLaunchKernelGGL(k_simulate_team<T>, dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, tau);

@@ -309,6 +309,19 @@ class Dof:
 
 
 @dataclass
+class Link:
+    """A rigid body as the tensor API reports it (``collapse_fixed_joints=False`` keeps links
+    hung on fixed joints).  Dynamics run on the welded :class:`Body` it belongs to."""
+    name: str
+    parent: int               # parent link, -1 for the root
+    joint_name: str           # joint to the parent link ("" for the root)
+    body: int                 # dynamic body it is welded into
+    pose: "Pose"              # link frame in the body frame
+    mass: float
+    com: np.ndarray           # link COM in the link frame
+
+
+@dataclass
 class Articulation:
     name: str
     bodies: List[Body]
@@ -316,6 +329,10 @@ class Articulation:
     fixed_base: bool
     options: dict
     default_friction: float = 1.0
+    # reported rigid bodies when they differ from the dynamic bodies (fixed joints kept), else None
+    links: Optional[List[Link]] = None
+    # link of every shape, in shape order (None: the shape's body)
+    shape_links: Optional[List[int]] = None
 
     @property
     def num_bodies(self):
@@ -327,6 +344,37 @@ class Articulation:
 
     def body_names(self):
         return [b.name for b in self.bodies]
+
+    # ---- reported rigid bodies (the tensor API's view): links when fixed joints are kept
+    @property
+    def num_links(self):
+        return len(self.links) if self.links is not None else len(self.bodies)
+
+    def link_names(self):
+        return [l.name for l in self.links] if self.links is not None else self.body_names()
+
+    def link_table(self) -> List[Link]:
+        """Every reported rigid body with its dynamic body and pose (identity when links = bodies)."""
+        if self.links is not None:
+            return self.links
+        return [Link(b.name, b.parent, b.joint_name, i, Pose(), b.mass, b.com.copy())
+                for i, b in enumerate(self.bodies)]
+
+    def joint_names(self):
+        """Joints in link order (one per non-root link, fixed joints included)."""
+        return [l.joint_name for l in self.link_table()[1:]]
+
+    def candidate_links(self) -> List[int]:
+        """Reported link of every contact candidate (same order as contact_candidates())."""
+        out = []
+        s_index = 0
+        for bi, b in enumerate(self.bodies):
+            for s in b.shapes:
+                link = self.shape_links[s_index] if self.shape_links is not None else bi
+                n = {SHAPE_SPHERE: 1, SHAPE_CAPSULE: 2, SHAPE_CYLINDER: 2, SHAPE_BOX: 8}[s.kind]
+                out += [link] * n
+                s_index += 1
+        return out
 
     def dof_names(self):
         return [d.name for d in self.dofs]
@@ -411,6 +459,13 @@ def build_articulation(raw: RawModel, options: Optional[dict] = None) -> Articul
     if len(roots) != 1:
         raise ValueError(f"asset {raw.name}: expected one root link, found {roots}")
     collapse = bool(opt["collapse_fixed_joints"])
+    # collapse_fixed_joints=False with fixed joints present: the dynamics weld every fixed link into
+    # its parent (a rigid weld has no dynamics of its own) while the tensor API keeps reporting each
+    # link (Isaac Gym's rigid-body count, names, contact forces and Jacobian rows are per link)
+    keep_links = not collapse and any(j.kind == JOINT_FIXED for j in raw.joints)
+    weld = collapse or keep_links
+    member_of: Dict[str, tuple] = {}
+    shape_link_names: List[str] = []
 
     # groups: a movable body plus everything welded to it; pose of each member in the body frame
     bodies: List[Body] = []
@@ -422,7 +477,7 @@ def build_articulation(raw: RawModel, options: Optional[dict] = None) -> Articul
         while stack:
             ln, pose = stack.pop(0)
             for j in sorted(children.get(ln, []), key=lambda jj: jj.child):
-                if j.kind == JOINT_FIXED and collapse:
+                if j.kind == JOINT_FIXED and weld:
                     p = pose.compose(j.origin)
                     members.append((j.child, p))
                     stack.append((j.child, p))
@@ -430,7 +485,9 @@ def build_articulation(raw: RawModel, options: Optional[dict] = None) -> Articul
                     movable_children.append((pose, j))
         m, c, I = 0.0, np.zeros(3), np.zeros((3, 3))
         shapes = []
+        idx = len(bodies)
         for ln, pose in members:
+            member_of[ln] = (idx, pose)
             link = raw.links[ln]
             if link.inertial is not None and link.inertial.mass > 0:
                 mi = link.inertial.mass
@@ -442,12 +499,12 @@ def build_articulation(raw: RawModel, options: Optional[dict] = None) -> Articul
                 if kind == SHAPE_CYLINDER and opt["replace_cylinder_with_capsule"]:
                     kind = SHAPE_CAPSULE
                 shapes.append(RawShape(kind, pose.compose(s.pose), list(s.size)))
+                shape_link_names.append(ln)
         if joint is None:
             kind = JOINT_FIXED if opt["fix_base_link"] else JOINT_FREE
             b = Body(link_name, -1, kind, "", Pose(), np.array([1.0, 0, 0]), m, c, I, shapes)
         else:
             b = Body(link_name, parent_idx, joint.kind, joint.name, joint.origin, joint.axis.copy(), m, c, I, shapes)
-        idx = len(bodies)
         bodies.append(b)
         # children visited depth-first, siblings sorted by body name
         for pose, j in sorted(movable_children, key=lambda pj: pj[1].child):
@@ -462,9 +519,6 @@ def build_articulation(raw: RawModel, options: Optional[dict] = None) -> Articul
             j = next(jj for jj in raw.joints if jj.name == b.joint_name)
             dofs.append(Dof(j.name, bi, j.kind, j.lower, j.upper, j.has_limits, j.effort, j.velocity,
                             j.damping, j.friction, j.armature, j.motor_gear))
-        elif b.joint_kind == JOINT_FIXED:
-            raise ValueError("fixed joints survive only with collapse_fixed_joints=False, which the "
-                             "kernels do not support yet (DESIGN.md: out of scope)")
     # bodies with no mass get a tiny inertia from density over their shapes' volume (Isaac Gym uses
     # `density` for links that declare no inertial); keep M non-singular
     for b in bodies:
@@ -476,7 +530,32 @@ def build_articulation(raw: RawModel, options: Optional[dict] = None) -> Articul
             ev = np.linalg.eigvalsh(b.inertia) if np.any(b.inertia) else np.zeros(3)
             if ev.min() <= 0.0:
                 b.inertia = b.inertia + np.eye(3) * max(1e-6, 1e-4 * b.mass * 0.01)
-    return Articulation(raw.name, bodies, dofs, bool(opt["fix_base_link"]), opt, raw.default_friction)
+    links, shape_links = None, None
+    if keep_links:
+        links = []
+        parent_joint = {j.child: j for j in raw.joints}
+
+        def visit(ln, parent_link):
+            bi, pose = member_of[ln]
+            inert = raw.links[ln].inertial
+            li = len(links)
+            j = parent_joint.get(ln)
+            links.append(Link(ln, parent_link, j.name if j is not None else "", bi, pose,
+                              float(inert.mass) if inert is not None else 0.0,
+                              inert.com.copy() if inert is not None else np.zeros(3)))
+            for jj in sorted(children.get(ln, []), key=lambda x: x.child):
+                visit(jj.child, li)
+
+        visit(roots[0], -1)
+        index = {l.name: i for i, l in enumerate(links)}
+        shape_links = [index[n] for n in shape_link_names]
+        # Isaac Gym numbers DOFs in link order: the welded tree must give the same order
+        link_dofs = [l.joint_name for l in links[1:] if parent_joint[l.name].kind != JOINT_FIXED]
+        if link_dofs != [d.name for d in dofs]:
+            raise ValueError(f"asset {raw.name}: welded DOF order {[d.name for d in dofs]} differs from the "
+                             f"link order {link_dofs}")
+    return Articulation(raw.name, bodies, dofs, bool(opt["fix_base_link"]), opt, raw.default_friction,
+                        links, shape_links)
 
 
 # --------------------------------------------------------------------------

@@ -20,7 +20,8 @@ class GsModelDesc(C.Structure):
         (n, C.c_void_p) for n in ("parent", "joint_kind", "body_dof", "joint_origin", "joint_axis", "mass",
                                   "com", "inertia", "cand_body", "cand_point", "cand_radius", "cand_shape",
                                   "dof_effort", "dof_velocity", "dof_armature", "dof_lower", "dof_upper",
-                                  "dof_has_limits")]
+                                  "dof_has_limits")] + [
+        ("num_links", C.c_int32)] + [(n, C.c_void_p) for n in ("cand_link", "link_body", "link_pose", "link_com")]
 
 
 class GsSimParams(C.Structure):
@@ -63,6 +64,9 @@ def lib():
             "gs_sim_refresh_root": (i, [vp, vp, vp]),
             "gs_sim_refresh_dof": (i, [vp, vp, vp]),
             "gs_sim_refresh_contact": (i, [vp, vp, vp]),
+            "gs_sim_refresh_rigid_body": (i, [vp, vp, vp]),
+            "gs_sim_refresh_jacobian": (i, [vp, vp, vp]),
+            "gs_sim_refresh_mass_matrix": (i, [vp, vp, vp]),
             "gs_sim_set_root": (i, [vp, vp, vp, i, vp]),
             "gs_sim_set_dof": (i, [vp, vp, vp, i, vp]),
             "gs_sim_pd_step": (i, [vp, C.POINTER(GsPdArgs), vp]),
@@ -95,7 +99,8 @@ EXPORTED_SYMBOLS = [
     "gs_sim_refresh_dof", "gs_sim_refresh_contact", "gs_sim_set_root", "gs_sim_set_dof", "gs_sim_pd_step",
     "gs_sim_kernel_variant", "gs_sim_enable_timing", "gs_sim_last_kernel_ms", "gs_debug_phase_cycles",
     "gs_sim_set_force_sensors", "gs_sim_bind_force_sensors", "gs_sim_refresh_force_sensor",
-    "gs_sim_add_triangle_mesh", "gs_debug_terrain_query",
+    "gs_sim_add_triangle_mesh", "gs_debug_terrain_query", "gs_sim_refresh_rigid_body", "gs_sim_refresh_jacobian",
+    "gs_sim_refresh_mass_matrix",
 ]
 
 
@@ -113,7 +118,10 @@ def model_desc(flat: dict):
              ("cand_radius", "cradius", np.float64), ("cand_shape", "cshape", np.int32),
              ("dof_effort", "effort", np.float64), ("dof_velocity", "vmax", np.float64),
              ("dof_armature", "armature", np.float64), ("dof_lower", "lower", np.float64),
-             ("dof_upper", "upper", np.float64), ("dof_has_limits", "has_limits", np.int32)]
+             ("dof_upper", "upper", np.float64), ("dof_has_limits", "has_limits", np.int32),
+             ("cand_link", "clink", np.int32), ("link_body", "lbody", np.int32),
+             ("link_pose", "lpose", np.float64), ("link_com", "lcom", np.float64)]
+    m.num_links = flat["nr"]
     for field, key, dt in pairs:
         a = np.ascontiguousarray(flat[key], dtype=dt)
         if a.size == 0:

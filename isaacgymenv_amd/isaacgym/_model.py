@@ -8,6 +8,9 @@ The same flat arrays feed the product library (``gs_sim_set_model`` in
 * ``jaxis[nb][3]``, ``mass[nb]``, ``com[nb][3]``, ``inertia[nb][9]`` (about COM)
 * contact candidates ``cbody[nc]``, ``cpoint[nc][3]``, ``cradius[nc]``, ``cshape[nc]``
 * per dof ``effort``, ``vmax``, ``armature``, ``lower``, ``upper``, ``has_limits``
+* reported links (the tensor API's rigid bodies): ``nr``, ``clink[nc]`` (link whose net contact
+  force a candidate adds to), ``lbody[nr]`` (dynamic body), ``lpose[nr][12]`` (link frame in the
+  body frame, R row-major then t), ``lcom[nr][3]`` (link COM, link frame), ``lmass[nr]``
 """
 from __future__ import annotations
 
@@ -44,6 +47,16 @@ def flatten(art: Articulation, armature: float | None = None) -> dict:
     cpoint = np.array([c[1] for c in cands], dtype=np.float64).reshape(nc, 3)
     cradius = np.array([c[2] for c in cands], dtype=np.float64).reshape(nc)
     cshape = np.array([c[3] for c in cands], dtype=np.int32).reshape(nc)
+    clinks = art.candidate_links()
+    if art.fixed_base:
+        clinks = [l for l, c in zip(clinks, art.contact_candidates()) if c[0] != 0]
+    clink = np.array(clinks, dtype=np.int32).reshape(nc)
+    links = art.link_table()
+    nr = len(links)
+    lpose = np.zeros((nr, 12))
+    for i, l in enumerate(links):
+        lpose[i, :9] = l.pose.R.reshape(-1)
+        lpose[i, 9:] = l.pose.t
     arm = art.options.get("armature", 0.0) if armature is None else armature
     return dict(
         nb=nb, nd=nd, nc=nc, ns=art.num_shapes, fixed_base=int(art.fixed_base),
@@ -56,10 +69,16 @@ def flatten(art: Articulation, armature: float | None = None) -> dict:
         lower=np.array([d.lower for d in art.dofs], dtype=np.float64).reshape(nd),
         upper=np.array([d.upper for d in art.dofs], dtype=np.float64).reshape(nd),
         has_limits=np.array([int(d.has_limits) for d in art.dofs], dtype=np.int32).reshape(nd),
+        nr=nr, clink=clink, lbody=np.array([l.body for l in links], dtype=np.int32), lpose=lpose,
+        lcom=np.array([l.com for l in links], dtype=np.float64).reshape(nr, 3),
+        lmass=np.array([l.mass for l in links], dtype=np.float64),
     )
 
 
 def topology_signature(flat: dict) -> str:
     """Compile-time shape of a model: what selects a specialised kernel."""
-    return "fb{}_p{}_c{}".format(flat["fixed_base"], "-".join(str(int(p)) for p in flat["parent"]),
-                                  "-".join(str(int(b)) for b in flat["cbody"]))
+    sig = "fb{}_p{}_c{}".format(flat["fixed_base"], "-".join(str(int(p)) for p in flat["parent"]),
+                                 "-".join(str(int(b)) for b in flat["cbody"]))
+    if flat["nr"] != flat["nb"] or any(int(a) != int(b) for a, b in zip(flat["clink"], flat["cbody"])):
+        sig += "_l{}_{}".format(flat["nr"], "-".join(str(int(l)) for l in flat["clink"]))
+    return sig

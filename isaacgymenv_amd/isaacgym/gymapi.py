@@ -282,6 +282,11 @@ class GymTensor:
 JOINT_LIMIT_MARGIN = 0.1
 
 
+def torch_empty_like_on(t, device):
+    import torch
+    return torch.empty(t.shape, dtype=t.dtype, device=device)
+
+
 # ------------------------------------------------------------------ the sim
 class Sim:
     def __init__(self, gym: "Gym", compute_device: int, params: SimParams):
@@ -359,8 +364,8 @@ class Sim:
         if self.ground is not None:
             _lib.check(L.gs_sim_add_ground(self.handle, self.ground.static_friction, self.ground.dynamic_friction,
                                            self.ground.restitution), "gs_sim_add_ground")
-        N, nd, nb, ns = len(self.envs), art.num_dofs, art.num_bodies, max(1, art.num_shapes)
-        self.num_envs, self.num_dofs, self.num_bodies = N, nd, nb
+        self._tensors()
+        N, nd, nb, ns = self.num_envs, self.num_dofs, self.num_bodies, max(1, art.num_shapes)
         dev, tdev = self.sim_device, self.tensor_device
         f32 = torch.float32
         # SoA sim state (device), initial values from the actors' start poses
@@ -389,10 +394,6 @@ class Sim:
         if sens:
             _lib.check(L.gs_sim_bind_force_sensors(self.handle, self.sens_soa.data_ptr()), "gs_sim_bind_force_sensors")
         self.sensor_tensor = torch.zeros(N * len(sens), 6, dtype=f32, device=tdev)
-        # reference-layout tensors (sim owned; wrap_tensor shares them)
-        self.root_tensor = torch.zeros(N, 13, dtype=f32, device=tdev)
-        self.dof_tensor = torch.zeros(N * nd, 2, dtype=f32, device=tdev)
-        self.contact_tensor = torch.zeros(N * nb, 3, dtype=f32, device=tdev)
         self.dof_force = torch.zeros(N * nd, dtype=f32, device=dev)
         # device mirrors used when the pipeline is on the CPU
         if not self.gpu_pipeline:
@@ -404,10 +405,62 @@ class Sim:
         self.refresh("root")
         self.refresh("dof")
         self.refresh("contact")
+        for kind in ("rigid_body", "jacobian", "mass_matrix"):  # acquired before prepare_sim
+            self.refresh(kind)
+
+    def _tensors(self):
+        """Reference-layout tensors (sim owned; wrap_tensor shares them), sized from the created envs.
+        Isaac Gym lets a task acquire them before prepare_sim (useful_hound.py:438-455 does, inside
+        _create_envs) and they are the same buffers afterwards, so they are allocated once, here."""
+        import torch
+        if getattr(self, "root_tensor", None) is not None:
+            return
+        if self.asset is None or not self.envs:
+            raise RuntimeError("tensors are available once the envs and actors exist")
+        art = self.asset.art
+        # num_bodies = reported rigid bodies (links); the dynamics may weld fixed-joint links (DESIGN.md 3.8)
+        N, nd, nb = len(self.envs), art.num_dofs, art.num_links
+        self.num_envs, self.num_dofs, self.num_bodies = N, nd, nb
+        self.nv = nd + (0 if art.fixed_base else 6)
+        f32, tdev = torch.float32, self.tensor_device
+        self.root_tensor = torch.zeros(N, 13, dtype=f32, device=tdev)
+        self.dof_tensor = torch.zeros(N * nd, 2, dtype=f32, device=tdev)
+        self.contact_tensor = torch.zeros(N * nb, 3, dtype=f32, device=tdev)
+        self.rb_tensor = self.jac_tensor = self.mm_tensor = None
 
     # -------- tensor API
+    def kinematics_tensor(self, kind: str):
+        """Sim-owned rigid-body-state / jacobian / mass-matrix tensors, allocated on first acquire
+        and filled once (Isaac Gym's acquired tensors hold the prepared state)."""
+        import torch
+        self._tensors()
+        f32, tdev = torch.float32, self.tensor_device
+        N, nr, nv = self.num_envs, self.num_bodies, self.nv
+        if kind == "rigid_body" and self.rb_tensor is None:
+            self.rb_tensor = torch.zeros(N * nr, 13, dtype=f32, device=tdev)
+        elif kind == "jacobian" and self.jac_tensor is None:
+            self.jac_tensor = torch.zeros(N, nr, 6, nv, dtype=f32, device=tdev)
+        elif kind == "mass_matrix" and self.mm_tensor is None:
+            self.mm_tensor = torch.zeros(N, nv, nv, dtype=f32, device=tdev)
+        else:
+            return {"rigid_body": self.rb_tensor, "jacobian": self.jac_tensor, "mass_matrix": self.mm_tensor}[kind]
+        if self.prepared:
+            self.refresh(kind)
+        return {"rigid_body": self.rb_tensor, "jacobian": self.jac_tensor, "mass_matrix": self.mm_tensor}[kind]
+
     def refresh(self, kind: str):
         L, s = _lib.lib(), self.stream()
+        if kind in ("rigid_body", "jacobian", "mass_matrix"):
+            dst = {"rigid_body": self.rb_tensor, "jacobian": self.jac_tensor, "mass_matrix": self.mm_tensor}[kind]
+            if dst is None:
+                return  # never acquired: nothing to fill
+            out = dst if self.gpu_pipeline else torch_empty_like_on(dst, self.sim_device)
+            fn = {"rigid_body": L.gs_sim_refresh_rigid_body, "jacobian": L.gs_sim_refresh_jacobian,
+                  "mass_matrix": L.gs_sim_refresh_mass_matrix}[kind]
+            _lib.check(fn(self.handle, out.data_ptr(), s), f"refresh {kind}")
+            if not self.gpu_pipeline:
+                dst.copy_(out.cpu())
+            return
         dst = {"root": self.root_tensor, "dof": self.dof_tensor, "contact": self.contact_tensor,
                "sensor": self.sensor_tensor}[kind]
         out = dst if self.gpu_pipeline else {"root": self._root_dev, "dof": self._dof_dev,
@@ -515,7 +568,7 @@ class Gym:
         return asset.art.num_dofs
 
     def get_asset_rigid_body_count(self, asset: Asset) -> int:
-        return asset.art.num_bodies
+        return asset.art.num_links
 
     def get_asset_rigid_shape_count(self, asset: Asset) -> int:
         return asset.art.num_shapes
@@ -524,10 +577,10 @@ class Gym:
         return asset.art.num_dofs
 
     def get_asset_rigid_body_names(self, asset: Asset) -> List[str]:
-        return asset.art.body_names()
+        return asset.art.link_names()
 
     def get_asset_rigid_body_name(self, asset: Asset, index: int) -> str:
-        return asset.art.body_names()[index]
+        return asset.art.link_names()[index]
 
     def get_asset_dof_names(self, asset: Asset) -> List[str]:
         return asset.art.dof_names()
@@ -536,7 +589,7 @@ class Gym:
         return asset.art.dof_names()[index]
 
     def find_asset_rigid_body_index(self, asset: Asset, name: str) -> int:
-        names = asset.art.body_names()
+        names = asset.art.link_names()
         return names.index(name) if name in names else INVALID_HANDLE
 
     def find_asset_dof_index(self, asset: Asset, name: str) -> int:
@@ -619,7 +672,7 @@ class Gym:
         return True
 
     def find_actor_rigid_body_handle(self, env: Env, actor: int, name: str) -> int:
-        names = env.actors[actor].asset.art.body_names()
+        names = env.actors[actor].asset.art.link_names()
         return names.index(name) if name in names else INVALID_HANDLE
 
     def find_actor_rigid_body_index(self, env: Env, actor: int, name: str, domain: int = DOMAIN_ENV) -> int:
@@ -633,22 +686,23 @@ class Gym:
         return env.actors[actor].asset.art.num_dofs
 
     def get_actor_rigid_body_count(self, env: Env, actor: int) -> int:
-        return env.actors[actor].asset.art.num_bodies
+        return env.actors[actor].asset.art.num_links
 
     def get_actor_rigid_body_names(self, env: Env, actor: int):
-        return env.actors[actor].asset.art.body_names()
+        return env.actors[actor].asset.art.link_names()
 
     def get_actor_dof_names(self, env: Env, actor: int):
         return env.actors[actor].asset.art.dof_names()
 
     def get_actor_joint_dict(self, env: Env, actor: int):
-        return {n: i for i, n in enumerate(env.actors[actor].asset.art.dof_names())}
+        """Joints in link order, fixed joints included (joint i connects link i + 1 to its parent)."""
+        return {n: i for i, n in enumerate(env.actors[actor].asset.art.joint_names())}
 
     def get_actor_dof_dict(self, env: Env, actor: int):
-        return self.get_actor_joint_dict(env, actor)
+        return {n: i for i, n in enumerate(env.actors[actor].asset.art.dof_names())}
 
     def get_actor_rigid_body_dict(self, env: Env, actor: int):
-        return {n: i for i, n in enumerate(env.actors[actor].asset.art.body_names())}
+        return {n: i for i, n in enumerate(env.actors[actor].asset.art.link_names())}
 
     def enable_actor_dof_force_sensors(self, env: Env, actor: int):
         return True
@@ -658,26 +712,43 @@ class Gym:
 
     # ---- tensor acquire (sim owned, zero copy)
     def acquire_actor_root_state_tensor(self, sim: Sim) -> GymTensor:
+        sim._tensors()
         return GymTensor(sim.root_tensor, "root")
 
     def acquire_dof_state_tensor(self, sim: Sim) -> GymTensor:
+        sim._tensors()
         return GymTensor(sim.dof_tensor, "dof")
 
     def acquire_net_contact_force_tensor(self, sim: Sim) -> GymTensor:
+        sim._tensors()
         return GymTensor(sim.contact_tensor, "contact")
 
-    def acquire_rigid_body_state_tensor(self, sim: Sim):
-        raise NotImplementedError("rigid body state tensor belongs to the UsefulHound row (not built yet)")
+    def acquire_rigid_body_state_tensor(self, sim: Sim) -> GymTensor:
+        """[num_envs * num_bodies, 13]: link origin, quat xyzw, COM linear velocity, angular velocity."""
+        return GymTensor(sim.kinematics_tensor("rigid_body"), "rigid_body")
 
     def acquire_force_sensor_tensor(self, sim: Sim) -> GymTensor:
         """[num_envs * sensors_per_env, 6]: force (3) then torque (3) in the sensor frame (ant.py:80-83)."""
         return GymTensor(sim.sensor_tensor, "sensor")
 
-    def acquire_jacobian_tensor(self, sim: Sim, name: str):
-        raise NotImplementedError("jacobian tensor belongs to the UsefulHound row (not built yet)")
+    def acquire_jacobian_tensor(self, sim: Sim, name: str) -> GymTensor:
+        """Floating base: [num_envs, num_bodies, 6, 6 + num_dofs]; fixed base: [num_envs, num_bodies - 1,
+        6, num_dofs] (the welded root row dropped, as Isaac Gym does).  Rows: COM linear velocity (3),
+        angular velocity (3); columns: root link COM linear / angular velocity, dof velocities."""
+        self._check_actor_name(sim, name)
+        t = sim.kinematics_tensor("jacobian")
+        return GymTensor(t[:, 1:] if sim.asset.art.fixed_base else t, "jacobian")
 
-    def acquire_mass_matrix_tensor(self, sim: Sim, name: str):
-        raise NotImplementedError("mass matrix tensor belongs to the UsefulHound row (not built yet)")
+    def acquire_mass_matrix_tensor(self, sim: Sim, name: str) -> GymTensor:
+        """[num_envs, nv, nv] in the jacobian's generalized velocities (v^T M v / 2 = kinetic energy)."""
+        self._check_actor_name(sim, name)
+        return GymTensor(sim.kinematics_tensor("mass_matrix"), "mass_matrix")
+
+    @staticmethod
+    def _check_actor_name(sim: Sim, name: str):
+        names = {a.name for e in sim.envs for a in e.actors}
+        if name not in names:
+            raise ValueError(f"no actor named {name!r} (actors: {sorted(names)})")
 
     # ---- refresh (sim -> tensors)
     def refresh_actor_root_state_tensor(self, sim: Sim):
@@ -690,7 +761,13 @@ class Gym:
         sim.refresh("contact")
 
     def refresh_rigid_body_state_tensor(self, sim: Sim):
-        raise NotImplementedError("rigid body state tensor belongs to the UsefulHound row (not built yet)")
+        sim.refresh("rigid_body")
+
+    def refresh_jacobian_tensors(self, sim: Sim):
+        sim.refresh("jacobian")
+
+    def refresh_mass_matrix_tensors(self, sim: Sim):
+        sim.refresh("mass_matrix")
 
     def refresh_force_sensor_tensor(self, sim: Sim):
         if sim.num_sensors:
@@ -725,6 +802,29 @@ class Gym:
 
     def set_dof_state_tensor_indexed(self, sim: Sim, t: GymTensor, idx: GymTensor, n: int) -> bool:
         sim.set_state("dof", t.tensor, idx.tensor, n)
+        return True
+
+    def set_dof_position_target_tensor(self, sim: Sim, t: GymTensor) -> bool:
+        return self._check_effort_mode(sim, "set_dof_position_target_tensor")
+
+    def set_dof_position_target_tensor_indexed(self, sim: Sim, t: GymTensor, idx: GymTensor, n: int) -> bool:
+        """Position targets drive DOF_MODE_POS dofs only.  The in-scope tasks drive every dof in
+        DOF_MODE_EFFORT (UsefulHound sets targets on reset, useful_hound.py:624-627, with zero PhysX
+        stiffness / damping), where a target has no effect: accepted and ignored."""
+        return self._check_effort_mode(sim, "set_dof_position_target_tensor_indexed")
+
+    def set_dof_velocity_target_tensor(self, sim: Sim, t: GymTensor) -> bool:
+        return self._check_effort_mode(sim, "set_dof_velocity_target_tensor")
+
+    @staticmethod
+    def _check_effort_mode(sim: Sim, what: str) -> bool:
+        for e in sim.envs:
+            for a in e.actors:
+                mode = a.dof_props["driveMode"]
+                stiff = a.dof_props["stiffness"]
+                damp = a.dof_props["damping"]
+                if np.any((mode == DOF_MODE_POS) & ((stiff != 0) | (damp != 0))):
+                    raise NotImplementedError(f"{what}: position-drive dofs are not simulated (DESIGN.md 6)")
         return True
 
     # ---- viewer / rendering (headless build: no-ops)

@@ -2,9 +2,11 @@
 from .ant import Ant
 from .anymal_terrain import AnymalTerrain
 from .cartpole import Cartpole
+from .useful_hound import UsefulHound
 
 isaacgym_task_map = {
     "Ant": Ant,
     "AnymalTerrain": AnymalTerrain,
     "Cartpole": Cartpole,
+    "UsefulHound": UsefulHound,
 }

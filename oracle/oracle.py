@@ -23,7 +23,7 @@ class OModel(C.Structure):
         (n, C.c_void_p) for n in ("parent", "jkind", "bdof", "jorigin", "jaxis", "mass", "com", "inertia",
                                   "cbody", "cpoint", "cradius", "cshape", "effort", "vmax", "armature",
                                   "lower", "upper", "has_limits")] + [
-        ("nsens", C.c_int32), ("sens_body", C.c_void_p)]
+        ("nsens", C.c_int32), ("sens_body", C.c_void_p), ("nr", C.c_int32), ("clink", C.c_void_p)]
 
 
 class OParams(C.Structure):
@@ -71,7 +71,8 @@ class OracleSim:
         m = OModel()
         for k in ("nb", "nd", "nc", "ns", "fixed_base"):
             setattr(m, k, int(flat[k]))
-        for k in ("parent", "jkind", "bdof", "cbody", "cshape", "has_limits"):
+        m.nr = int(flat.get("nr", flat["nb"]))
+        for k in ("parent", "jkind", "bdof", "cbody", "cshape", "has_limits", "clink"):
             a = np.ascontiguousarray(flat[k], dtype=np.int32)
             keep[k] = a
             setattr(m, k, a.ctypes.data)

@@ -71,6 +71,8 @@ typedef struct {
     const int32_t *has_limits;  /* [nd] */
     int32_t nsens;              /* force sensors */
     const int32_t *sens_body;   /* [nsens] leaf bodies */
+    int32_t nr;                 /* reported links (>= nb: fixed-joint links kept, _model.flatten) */
+    const int32_t *clink;       /* [nc] link whose net contact force a candidate adds to */
 } OModel;
 
 typedef struct {
@@ -591,9 +593,9 @@ static void env_substep(const OModel *m, const OParams *p, real h,
         dq[2 * j + 1] = v[nbase + j];
     }
     if (cforce) {
-        for (int k = 0; k < 3 * nb; ++k) cforce[k] = 0;
+        for (int k = 0; k < 3 * m->nr; ++k) cforce[k] = 0;
         for (int a = 0; a < nact; ++a) {
-            const int b = m->cbody[ck[a]];
+            const int b = m->clink[ck[a]];
             real t1[3], t2[3];
             tangents(cn[a], t1, t2);
             for (int k = 0; k < 3; ++k)
@@ -653,13 +655,13 @@ static void env_substep(const OModel *m, const OParams *p, real h,
  * dof   : [N][nd][2] (q, qd)
  * tau   : [N][nd]
  * mu    : [N][ns]     per-env shape friction
- * cf    : [N][nb][3]  net contact force (written when collect_contacts), may be NULL
+ * cf    : [N][nr][3]  net contact force per reported link (written when collect_contacts), may be NULL
  * sens  : [N][nsens][6] force-sensor readings of the last substep, may be NULL
  */
 int oracle_simulate(const OModel *m, const OParams *p, int n_envs, real *root, real *dof,
                     const real *tau, const real *mu, real *cf, real *sens, int num_threads)
 {
-    if (m->nb > MAXB || m->nd + 6 > MAXV || m->nc > MAXC) return -1;
+    if (m->nb > MAXB || m->nd + 6 > MAXV || m->nc > MAXC || m->nr < m->nb) return -1;
     const real h = (real)(p->dt / (p->substeps > 0 ? p->substeps : 1));
 #ifdef _OPENMP
     if (num_threads > 0) omp_set_num_threads(num_threads);
@@ -669,7 +671,7 @@ int oracle_simulate(const OModel *m, const OParams *p, int n_envs, real *root, r
         for (int s = 0; s < p->substeps; ++s) {
             const int last = (s == p->substeps - 1);
             env_substep(m, p, h, root + 13 * e, dof + 2 * m->nd * e, tau + m->nd * e, mu + m->ns * e,
-                        (cf && p->collect_contacts && last) ? cf + 3 * m->nb * e : NULL,
+                        (cf && p->collect_contacts && last) ? cf + 3 * m->nr * e : NULL,
                         (sens && last) ? sens + 6 * m->nsens * e : NULL);
         }
     }

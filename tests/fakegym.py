@@ -46,10 +46,25 @@ class FakeGym(_g.Gym):
         sim.mesh = (np.asarray(vertices).size // 3, np.asarray(triangles).size // 3)
         return True
 
+    @staticmethod
+    def _sizes(sim):
+        """Sizes from the created envs: Isaac Gym lets tasks acquire tensors before prepare_sim
+        (useful_hound.py:438-455 does, inside _create_envs), and the tensor is the same buffer after."""
+        if not hasattr(sim, "N"):
+            art = sim.asset.art
+            sim.N, sim.nd, sim.nb = len(sim.envs), art.num_dofs, art.num_links
+            sim.nv = sim.nd + (0 if art.fixed_base else 6)
+            f = torch.float32
+            sim.root_t = torch.zeros(sim.N, 13, dtype=f)
+            sim.dof_t = torch.zeros(sim.N * sim.nd, 2, dtype=f)
+            sim.cf_t = torch.zeros(sim.N * sim.nb, 3, dtype=f)
+            sim.rb_t = sim.jac_t = sim.mm_t = None
+        return sim
+
     def prepare_sim(self, sim):
         art = sim.asset.art
-        N, nd, nb = len(sim.envs), art.num_dofs, art.num_bodies
-        sim.N, sim.nd, sim.nb = N, nd, nb
+        self._sizes(sim)
+        N, nd, nb = sim.N, sim.nd, sim.nb
         f = torch.float32
         root = torch.zeros(N, 13, dtype=f)
         for i, e in enumerate(sim.envs):
@@ -60,13 +75,10 @@ class FakeGym(_g.Gym):
         sim.dof = torch.zeros(N * nd, 2, dtype=f)
         sim.cf = torch.zeros(N * nb, 3, dtype=f)
         sim.force = torch.zeros(N * nd, dtype=f)
-        sim.root_t = torch.zeros(N, 13, dtype=f)
-        sim.dof_t = torch.zeros(N * nd, 2, dtype=f)
-        sim.cf_t = torch.zeros(N * nb, 3, dtype=f)
         sim.ns = len(sim.asset.sensors)
         sim.sens = torch.zeros(N * sim.ns, 6, dtype=f)
         sim.sens_t = torch.zeros(N * sim.ns, 6, dtype=f)
-        names = art.body_names()
+        names = art.link_names()
         self.feet = [i for i, n in enumerate(names) if ("SHANK" in n or "foot" in n) and i > 0]
         self.knees = [i for i, n in enumerate(names) if ("THIGH" in n or "thigh" in n) and i > 0]
         return True
@@ -106,13 +118,13 @@ class FakeGym(_g.Gym):
 
     # ---- tensors
     def acquire_actor_root_state_tensor(self, sim):
-        return _g.GymTensor(sim.root_t, "root")
+        return _g.GymTensor(self._sizes(sim).root_t, "root")
 
     def acquire_dof_state_tensor(self, sim):
-        return _g.GymTensor(sim.dof_t, "dof")
+        return _g.GymTensor(self._sizes(sim).dof_t, "dof")
 
     def acquire_net_contact_force_tensor(self, sim):
-        return _g.GymTensor(sim.cf_t, "contact")
+        return _g.GymTensor(self._sizes(sim).cf_t, "contact")
 
     def acquire_force_sensor_tensor(self, sim):
         return _g.GymTensor(sim.sens_t, "sensor")
@@ -152,6 +164,49 @@ class FakeGym(_g.Gym):
     def set_dof_state_tensor(self, sim, t):
         sim.dof.copy_(t.tensor)
         return True
+
+    def set_dof_actuation_force_tensor_indexed(self, sim, t, idx, n):
+        ids = idx.tensor[:n].long()
+        sim.force.view(sim.N, sim.nd)[ids] = t.tensor.reshape(sim.N, sim.nd)[ids]
+        return True
+
+    def set_dof_position_target_tensor_indexed(self, sim, t, idx, n):
+        return True
+
+    # ---- link kinematics (UsefulHound): seeded stand-ins with the tensor API's shapes.  The
+    # rigid-body state is filled once (the reference never refreshes it); the Jacobian and the
+    # symmetric positive-definite mass matrix change with every refresh.
+    def acquire_rigid_body_state_tensor(self, sim):
+        self._sizes(sim)
+        if sim.rb_t is None:
+            rng = np.random.RandomState(self.seed + 17)
+            sim.rb_t = torch.from_numpy(rng.normal(0, 0.5, (sim.N * sim.nb, 13)).astype(np.float32))
+        return _g.GymTensor(sim.rb_t, "rigid_body")
+
+    def refresh_rigid_body_state_tensor(self, sim):
+        return None
+
+    def acquire_jacobian_tensor(self, sim, name):
+        self._sizes(sim)
+        if sim.jac_t is None:
+            sim.jac_t = torch.zeros(sim.N, sim.nb, 6, sim.nv)
+        return _g.GymTensor(sim.jac_t, "jacobian")
+
+    def acquire_mass_matrix_tensor(self, sim, name):
+        self._sizes(sim)
+        if sim.mm_t is None:
+            sim.mm_t = torch.zeros(sim.N, sim.nv, sim.nv)
+        return _g.GymTensor(sim.mm_t, "mass_matrix")
+
+    def refresh_jacobian_tensors(self, sim):
+        rng = np.random.RandomState(self.seed + 1000 + sim.t)
+        sim.jac_t.copy_(torch.from_numpy(rng.normal(0, 0.3, tuple(sim.jac_t.shape)).astype(np.float32)))
+
+    def refresh_mass_matrix_tensors(self, sim):
+        rng = np.random.RandomState(self.seed + 2000 + sim.t)
+        a = rng.normal(0, 0.3, tuple(sim.mm_t.shape))
+        m = np.einsum("nij,nkj->nik", a, a) + np.eye(sim.nv)[None] * 0.5
+        sim.mm_t.copy_(torch.from_numpy(m.astype(np.float32)))
 
     # fused extension must not be used with the fake
     def amd_pd_decimation_step(self, *a, **k):

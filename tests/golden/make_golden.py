@@ -10,7 +10,8 @@ torch RNG call order (friction buckets, terrain levels, reset draws, push, obs
 noise).  Only the resulting arrays are committed (tests/golden/*.npz); the
 reference never travels to the GPU box.
 
-    python tests/golden/make_golden.py            # writes anymal_terrain.npz, cartpole.npz, ant.npz
+    python tests/golden/make_golden.py            # writes anymal_terrain.npz, cartpole.npz, ant.npz, ...
+    python tests/golden/make_golden.py hound      # one fixture (anymal|trimesh|cartpole|ant|hound)
 """
 from __future__ import annotations
 
@@ -31,6 +32,7 @@ sys.path.insert(0, ROOT)
 N_ANYMAL, STEPS_ANYMAL = 32, 30
 N_CARTPOLE, STEPS_CARTPOLE = 16, 40
 N_ANT, STEPS_ANT = 16, 40
+N_HOUND, STEPS_HOUND = 16, 30
 
 
 def anymal_cfg(num_envs: int) -> dict:
@@ -64,6 +66,15 @@ def ant_cfg(num_envs: int) -> dict:
     from isaacgymenv_amd.isaacgymenvs.config import compose
     cfg = compose("config", ["task=Ant", f"num_envs={num_envs}", "sim_device=cpu", "pipeline=cpu"])["task"]
     cfg["env"]["episodeLength"] = 25
+    return cfg
+
+
+def hound_cfg(num_envs: int) -> dict:
+    """UsefulHound.yaml (CPU pipeline) with short episodes and a frequent push."""
+    from isaacgymenv_amd.isaacgymenvs.config import compose
+    cfg = compose("config", ["task=UsefulHound", f"num_envs={num_envs}", "sim_device=cpu", "pipeline=cpu"])["task"]
+    cfg["env"]["learn"]["pushInterval_s"] = 0.1
+    cfg["env"]["learn"]["episodeLength_s"] = 0.4
     return cfg
 
 
@@ -284,6 +295,52 @@ def record_ant(num_envs=N_ANT, steps=STEPS_ANT):
     return out
 
 
+def record_hound(num_envs=N_HOUND, steps=STEPS_HOUND):
+    """UsefulHound on the fake: legs PD + arm OSC over the fake's Jacobian / mass matrix."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fakegym import FakeGym
+    fake = FakeGym(seed=555)
+    install_reference_stubs(fake)
+    import importlib
+    ref = importlib.import_module("isaacgymenvs.tasks.useful_hound")
+    cfg = hound_cfg(num_envs)
+    torch.manual_seed(42)
+    env = ref.UsefulHound(copy.deepcopy(cfg), "cpu", "cpu", -1, True, False, False)
+    out = {"init_commands": _np(env.commands), "init_dof_state": _np(env.dof_state),
+           "init_root_states": _np(env.root_states), "feet_indices": _np(env.feet_indices),
+           "knee_indices": _np(env.knee_indices), "base_indices": _np(env.base_indices),
+           "eef_index": np.array(env.eef_index), "noise_scale_vec": _np(env.noise_scale_vec),
+           "arm_lower": _np(env.houndarm_dof_lower_limits), "arm_upper": _np(env.houndarm_dof_upper_limits),
+           "arm_effort": _np(env._houndarm_effort_limits)}
+    rng = np.random.RandomState(17)
+    actions = (2 * rng.rand(steps, num_envs, 18) - 1).astype(np.float32)
+    recs = {k: [] for k in ("obs", "rew", "reset", "time_outs", "progress", "torques", "dof_state", "commands",
+                            "feet_air_time", "ep_mask", "ep_extras")}
+    terms = list(env.episode_sums.keys())
+    for t in range(steps):
+        obs, rew, reset, extras = env.step(torch.from_numpy(actions[t]))
+        recs["obs"].append(_np(obs["obs"]))
+        recs["rew"].append(_np(rew))
+        recs["reset"].append(_np(reset).astype(np.int64))
+        recs["time_outs"].append(_np(extras["time_outs"]).astype(np.int64))
+        recs["progress"].append(_np(env.progress_buf))
+        recs["torques"].append(_np(env.torques))
+        recs["dof_state"].append(_np(env.dof_state))
+        recs["commands"].append(_np(env.commands))
+        recs["feet_air_time"].append(_np(env.feet_air_time))
+        ep = extras.get("episode")
+        recs["ep_mask"].append(int(ep is not None))
+        recs["ep_extras"].append(np.array([float(ep["rew_" + k]) for k in terms] + [float(ep["terrain_level"])])
+                                 if ep is not None else np.zeros(len(terms) + 1))
+        env.extras.pop("episode", None)
+    for k, v in recs.items():
+        out[k] = np.stack([np.asarray(x) for x in v])
+    out["actions"] = actions
+    out["terms"] = np.array(terms)
+    out["cfg_yaml"] = np.array(yaml.safe_dump(cfg))
+    return out
+
+
 def main():
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     if which in ("all", "anymal"):
@@ -315,6 +372,14 @@ def main():
             d = record_ant()
             np.savez_compressed(os.path.join(HERE, "ant.npz"), **d)
             print("ant.npz:", {k: v.shape for k, v in d.items() if hasattr(v, "shape")})
+    if which in ("all", "hound"):
+        if which == "all":
+            import subprocess
+            subprocess.check_call([sys.executable, __file__, "hound"])
+        else:
+            d = record_hound()
+            np.savez_compressed(os.path.join(HERE, "useful_hound.npz"), **d)
+            print("useful_hound.npz:", {k: v.shape for k, v in d.items() if hasattr(v, "shape")})
 
 
 if __name__ == "__main__":

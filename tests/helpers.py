@@ -28,6 +28,14 @@ ANT_PARAMS = dict(dt=0.0166, substeps=2, gravity=[0.0, 0.0, -9.81], pos_iters=4,
                   has_ground=1, ground_friction=1.0, limit_margin=0.1)
 ANT_FEET = [2, 4, 6, 8]  # bodies whose names contain "foot" (ant.py:166-173)
 
+# UsefulHound.yaml:161-180 (dt 0.005, 1 substep, 4/1 iterations, contact collection last substep);
+# asset options useful_hound.py:318-329 (fixed joints kept: 19 dynamic bodies, 24 links)
+HOUND_OPTS = dict(collapse_fixed_joints=False, replace_cylinder_with_capsule=False, fix_base_link=False,
+                  density=0.001, angular_damping=0.0, linear_damping=0.0, armature=0.0, thickness=0.01)
+HOUND_PARAMS = dict(dt=0.005, substeps=1, gravity=[0.0, 0.0, -9.81], pos_iters=4, vel_iters=1,
+                    contact_offset=0.02, rest_offset=0.0, max_depen_vel=100.0, collect_contacts=1,
+                    has_ground=1, ground_friction=1.0, limit_margin=0.1)
+
 
 def load_art(name, opts):
     with open(os.path.join(PACKED_DIR, name)) as f:
@@ -47,6 +55,35 @@ def cartpole():
 def ant():
     art = load_art("nv_ant.model.json", dict(angular_damping=0.0))
     return art, flatten(art)
+
+
+def hound():
+    art = load_art("hound.model.json", HOUND_OPTS)
+    return art, flatten(art)
+
+
+def hound_states(n, seed=0, spread=1.0):
+    """Random Hound states: legs near a stand, arm anywhere in its limits, base tilted/moving."""
+    rng = np.random.RandomState(seed)
+    art, flat = hound()
+    root = np.zeros((n, 13))
+    root[:, 0:2] = rng.uniform(-2, 2, (n, 2))
+    root[:, 2] = rng.uniform(0.45, 0.7, n)
+    axis = rng.normal(size=(n, 3))
+    axis /= np.linalg.norm(axis, axis=1, keepdims=True)
+    ang = rng.uniform(0, 0.3 * spread, n)
+    root[:, 3:6] = axis * np.sin(ang / 2)[:, None]
+    root[:, 6] = np.cos(ang / 2)
+    root[:, 7:10] = rng.normal(0, 0.3 * spread, (n, 3))
+    root[:, 10:13] = rng.normal(0, 0.5 * spread, (n, 3))
+    dof = np.zeros((n, 18, 2))
+    leg = np.tile([0.0, 0.7, -1.4], 4)
+    dof[:, :12, 0] = leg + rng.uniform(-0.3, 0.3, (n, 12)) * spread
+    dof[:, 12:, 0] = rng.uniform(-1.5, 1.5, (n, 6))
+    dof[:, :, 1] = rng.normal(0, 1.0 * spread, (n, 18))
+    tau = np.concatenate([rng.uniform(-80, 80, (n, 12)), rng.uniform(-20, 20, (n, 6))], axis=1)
+    mu = np.repeat(rng.uniform(0.5, 1.25, (n, 1)), flat["ns"], axis=1)
+    return root, dof, tau, mu
 
 
 def ant_states(n, seed=0, spread=1.0):
@@ -138,13 +175,18 @@ def make_gpu_sim(kind: str, n: int, params: dict, terrain=None):
         asset = gym.load_asset(sim, "/nonexistent", "mjcf/nv_ant.xml", opts)
         for b in ANT_FEET:
             gym.create_asset_force_sensor(asset, b, gymapi.Transform())
+    elif kind == "hound":
+        for k, v in HOUND_OPTS.items():
+            setattr(opts, k, v)
+        opts.default_dof_drive_mode = gymapi.DOF_MODE_EFFORT
+        asset = gym.load_asset(sim, "/nonexistent", "urdf/UsefulHound/urdf/Hound.urdf", opts)
     else:
         opts.fix_base_link = True
         asset = gym.load_asset(sim, "/nonexistent", "urdf/cartpole.urdf", opts)
     for i in range(n):
         env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 1), 8)
         pose = gymapi.Transform()
-        pose.p = gymapi.Vec3(0, 0, {"anymal": 0.62, "ant": 0.44}.get(kind, 2.0))
+        pose.p = gymapi.Vec3(0, 0, {"anymal": 0.62, "ant": 0.44, "hound": 0.55}.get(kind, 2.0))
         gym.create_actor(env, asset, pose, kind, i, 0, 0)
     gym.prepare_sim(sim)
     return gym, sim

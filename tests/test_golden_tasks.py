@@ -141,3 +141,45 @@ def test_anymal_trimesh_matches_reference(fake_gym):
         _close(env.root_states.numpy(), d["root_states"][t], f"root states step {t}")
         _close(obs["obs"].numpy(), d["obs"][t], f"obs step {t}")
         _close(rew.numpy(), d["rew"][t], f"reward step {t}")
+
+
+def test_useful_hound_matches_reference(fake_gym):
+    """UsefulHound: 24 links with kept fixed joints, link indices, arm OSC
+    torques over the Jacobian / mass matrix, termination on trunk, thigh and shoulder contacts, the
+    204-wide observation and the RNG order, against the reference's own task code on the fake."""
+    d = np.load(os.path.join(GOLDEN, "useful_hound.npz"))
+    fake_gym(FakeGym(seed=555))
+    from isaacgymenv_amd.isaacgymenvs.tasks.useful_hound import UsefulHound
+    cfg = yaml.safe_load(str(d["cfg_yaml"]))
+    torch.manual_seed(42)
+    env = UsefulHound(copy.deepcopy(cfg), "cpu", "cpu", -1, True, False, False)
+    _close(env.commands.numpy(), d["init_commands"], "commands after the initial reset (RNG order at init)")
+    _close(env.dof_state.numpy(), d["init_dof_state"], "dof state after the initial reset")
+    _close(env.root_states.numpy(), d["init_root_states"], "root states after the initial reset")
+    for k in ("feet_indices", "knee_indices", "base_indices"):
+        np.testing.assert_array_equal(getattr(env, k).numpy(), d[k], err_msg=k)
+    assert env.eef_index == int(d["eef_index"])
+    _close(env.noise_scale_vec.numpy(), d["noise_scale_vec"], "noise scale vector")
+    _close(env.houndarm_dof_lower_limits.numpy(), d["arm_lower"], "arm lower limits")
+    _close(env.houndarm_dof_upper_limits.numpy(), d["arm_upper"], "arm upper limits")
+    _close(env._houndarm_effort_limits.numpy(), d["arm_effort"], "arm effort limits")
+    terms = [str(t) for t in d["terms"]]
+    assert d["reset"].sum() > 0
+    for t in range(d["actions"].shape[0]):
+        obs, rew, reset, extras = env.step(torch.from_numpy(d["actions"][t]))
+        assert reset.dtype == torch.bool
+        np.testing.assert_array_equal(reset.numpy().astype(np.int64), d["reset"][t], err_msg=f"reset step {t}")
+        np.testing.assert_array_equal(extras["time_outs"].numpy().astype(np.int64), d["time_outs"][t])
+        np.testing.assert_array_equal(env.progress_buf.numpy(), d["progress"][t], err_msg=f"progress step {t}")
+        _close(env.torques.numpy(), d["torques"][t], f"torques (legs PD + arm OSC) step {t}", rtol=1e-4, atol=1e-4)
+        _close(env.dof_state.numpy(), d["dof_state"][t], f"dof state step {t}")
+        _close(env.commands.numpy(), d["commands"][t], f"commands step {t}")
+        _close(env.feet_air_time.numpy(), d["feet_air_time"][t], f"feet air time step {t}")
+        _close(obs["obs"].numpy(), d["obs"][t], f"obs step {t}")
+        _close(rew.numpy(), d["rew"][t], f"reward step {t}")
+        ep = extras.get("episode")
+        assert int(ep is not None) == int(d["ep_mask"][t])
+        if ep is not None:
+            got = [float(ep["rew_" + k]) for k in terms] + [float(ep["terrain_level"])]
+            _close(got, d["ep_extras"][t], f"episode extras step {t}")
+        env.extras.pop("episode", None)

@@ -27,6 +27,7 @@ MODELS = [
     ("anymal_c", "anymal_c.model.json", dict(collapse_fixed_joints=True, replace_cylinder_with_capsule=True)),
     ("cartpole", "cartpole.model.json", dict(fix_base_link=True)),
     ("nv_ant", "nv_ant.model.json", dict()),
+    ("hound", "hound.model.json", dict(collapse_fixed_joints=False)),
 ]
 
 OUT = os.path.join(ROOT, "isaacgymenv_amd", "csrc", "gs_topologies.h")
@@ -83,7 +84,7 @@ def topo_tables(flat: dict) -> dict:
     cshape = [int(s) for s in flat["cshape"]]
     jkind = [int(k) for k in flat["jkind"]]
     team = team_tables(flat, parent, bdof, nbase)
-    return dict(TEAM=team, NB=nb, ND=nd, NC=nc, NS=int(flat["ns"]), FIXED=fixed, NBASE=nbase, NV=nv, MAXDEP=maxdep,
+    return dict(NR=int(flat["nr"]), clink=[int(l) for l in flat["clink"]], TEAM=team, NB=nb, ND=nd, NC=nc, NS=int(flat["ns"]), FIXED=fixed, NBASE=nbase, NV=nv, MAXDEP=maxdep,
                 parent=parent, bdof=bdof, jkind=jkind, dpar=dpar, depth=[len(a) for a in anc],
                 anc=[a + [-1] * (maxdep - len(a)) for a in anc], bgdof=bgdof, cbody=cbody, cleaf=cleaf,
                 csupp=csupp, cslot=cslot, NSLOT=max(off, 1), gbody=gbody, cshape=cshape, subend=subend,
@@ -166,10 +167,10 @@ def emit() -> str:
         sig = topology_signature(flat)
         lines.append(f"struct Topo_{name} {{")
         lines.append(f'  static constexpr const char* kName = "{name}";')
-        for k in ("NB", "ND", "NC", "NS", "FIXED", "NBASE", "NV", "MAXDEP", "NSLOT"):
+        for k in ("NB", "NR", "ND", "NC", "NS", "FIXED", "NBASE", "NV", "MAXDEP", "NSLOT"):
             lines.append(f"  static constexpr int {k} = {t[k]};")
         for k, n in (("parent", "NB"), ("bdof", "NB"), ("jkind", "NB"), ("bgdof", "NB"), ("subend", "NB"), ("dpar", "NV"),
-                     ("depth", "NV"), ("gbody", "NV"), ("cbody", "NC"), ("cshape", "NC"), ("cleaf", "NC"), ("csupp", "NC"), ("cslot", "NC"),
+                     ("depth", "NV"), ("gbody", "NV"), ("cbody", "NC"), ("clink", "NC"), ("cshape", "NC"), ("cleaf", "NC"), ("csupp", "NC"), ("cslot", "NC"),
                      ("lleaf", "ND"), ("lsupp", "ND"), ("lslot", "ND")):
             vals = t[k] if len(t[k]) else [0]
             dim = n if len(t[k]) else "1"
