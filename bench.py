@@ -17,6 +17,8 @@ The rank-0 JSON line carries:
                   per launch / its average HIP-event duration on the launch stream;
   cpu_baseline -- the fp32 build of the CPU oracle (oracle/, kind "port") stepping
                   a bounded sample of the same workload on the host cores;
+  other_configs-- env-steps/s of the other BASELINE.json configs on one GPU (Ant 4096, AnymalTerrain
+                  trimesh 4096, UsefulHound 4096), same timed-region rules, --other-steps steps each;
   ppo          -- PPO samples/s (the metric's second half): the rl_games-compatible learner
                   (isaacgymenv_amd/rl, AnymalTerrainPPO.yaml) over the same envs, one warm-up
                   epoch then --ppo-epochs timed epochs (rollout + GAE kernel + 5 x 6 minibatch
@@ -62,6 +64,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--kernel-launches", type=int, default=50, help="launches timed for the roofline figure")
+    ap.add_argument("--other-steps", type=int, default=100,
+                    help="timed steps of each other BASELINE config (Ant, trimesh AnymalTerrain, UsefulHound); 0 = skip")
     ap.add_argument("--ppo-epochs", type=int, default=5,
                     help="timed PPO epochs (AnymalTerrainPPO.yaml: horizon 24 x envs samples each); 0 = skip")
     return ap.parse_args()
@@ -161,6 +165,52 @@ def ppo_leg(env, device, rank, world, epochs):
             "last_kl": st["kl"], "last_lr": st["lr"]}
 
 
+OTHER_CONFIGS = [  # BASELINE.json configs beside the headline one (one GPU, 4096 envs each)
+    ("Ant", "Ant num_envs=4096 (MJCF articulation, flat-ground contacts, 1 simulate/step)", []),
+    ("AnymalTerrain", "AnymalTerrain num_envs=4096 trimesh heightfield (5 simulates/step)",
+     ["task.env.terrain.terrainType=trimesh"]),
+    ("UsefulHound", "UsefulHound num_envs=4096 (quadruped + 6-DoF arm OSC, 18 DoF, 24 links, 5 simulates/step)", []),
+]
+
+
+def other_config_leg(task, desc, overrides, num_envs, steps, warmup, device, rank, world):
+    """env-steps/s of another BASELINE config (same timed-region rules) and the average duration of its
+    physics launch (HIP events around gym.simulate on the launch stream)."""
+    import torch
+    import isaacgymenvs
+    from isaacgymenv_amd.isaacgymenvs.tasks.base import vec_task
+    vec_task.EXISTING_SIM = None
+    env = isaacgymenvs.make(seed=42 + rank, task=task, num_envs=num_envs, sim_device=device, rl_device=device,
+                            graphics_device_id=-1, headless=True, force_render=False, overrides=overrides)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(4321 + rank)
+    n_batches = max(1, min(steps + warmup, 256))
+    pool = torch.empty((n_batches, env.num_envs, env.num_actions), device=device).uniform_(-1.0, 1.0, generator=gen)
+    env.reset()
+    it = [0]
+
+    def step():
+        env.step(pool[it[0] % n_batches])
+        it[0] += 1
+
+    elapsed = timed_region(step, steps, warmup, world, sync=torch.cuda.synchronize)
+    stream = torch.cuda.current_stream(device)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    stream.synchronize()
+    ev0.record(stream)
+    for _ in range(20):
+        env.gym.simulate(env.sim)
+    ev1.record(stream)
+    ev1.synchronize()
+    out = {"task": task, "workload": desc, "value": env.num_envs * world * steps / elapsed, "unit": "env-steps/s",
+           "steps": steps, "ms_per_step": 1e3 * elapsed / steps, "simulate_kernel_ms": ev0.elapsed_time(ev1) / 20,
+           "kernel_variant": env.gym.amd_kernel_variant(env.sim)}
+    del env, pool
+    vec_task.EXISTING_SIM = None
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -215,6 +265,11 @@ def main():
     ppo = None
     if args.ppo_epochs > 0:
         ppo = ppo_leg(env, device, rank, world, args.ppo_epochs)
+    others = []
+    if args.other_steps > 0:
+        del env
+        for task, desc, ov in OTHER_CONFIGS:
+            others.append(other_config_leg(task, desc, ov, args.num_envs, args.other_steps, 20, device, rank, world))
 
     if rank == 0:
         traffic = None
@@ -263,6 +318,7 @@ def main():
                          "valu": valu},
             "cpu_baseline": cpu,
             "ppo": ppo,
+            "other_configs": others,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

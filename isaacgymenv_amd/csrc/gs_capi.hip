@@ -167,14 +167,15 @@ int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_verti
                     std::to_string(t).c_str());
     }
   }
-  // spacing: the grid points are x = i*hs, y = j*hs before the transform (vertex 1 of row 0 may be moved:
-  // take the most common row step)
-  std::vector<double> steps;
-  for (int64_t i = 0; i + 1 < rows && steps.size() < 4096; i += std::max<int64_t>(1, rows / 64))
-    for (int64_t j = 0; j < cols && steps.size() < 4096; j += std::max<int64_t>(1, cols / 64))
-      steps.push_back((double)vertices[3 * ((i + 1) * cols + j)] - (double)vertices[3 * (i * cols + j)]);
-  std::sort(steps.begin(), steps.end());
-  double hs = steps[steps.size() / 2];
+  // spacing: the grid points are x = i*hs, y = j*hs before the transform.  Slope correction moves a
+  // vertex by up to one cell, so take the median over columns of the first-to-last-row span / (rows - 1):
+  // a median single-row step carries the float32 rounding of the coordinates (1.5e-5 m at 160 m), which
+  // accumulated over 2000 cells misplaces the far end of the 1200 x 2000 AnymalTerrain map by 0.2 cells
+  std::vector<double> spans;
+  for (int64_t j = 0; j < cols && spans.size() < 4096; j += std::max<int64_t>(1, cols / 1024))
+    spans.push_back((double)vertices[3 * ((rows - 1) * cols + j)] - (double)vertices[3 * j]);
+  std::sort(spans.begin(), spans.end());
+  double hs = spans[spans.size() / 2] / (double)(rows - 1);
   if (!(hs > 0)) return fail("gs_sim_add_triangle_mesh: cannot infer the grid spacing");
   const double tx = transform_p ? transform_p[0] : 0.0, ty = transform_p ? transform_p[1] : 0.0,
                tz = transform_p ? transform_p[2] : 0.0;
