@@ -212,6 +212,17 @@ def other_config_leg(task, desc, overrides, num_envs, steps, warmup, device, ran
 
 
 def main():
+    # the driver reads ONE JSON line from rank 0's stdout: every other print (set_seed, rank banners,
+    # the task layer) goes to stderr
+    import contextlib
+    out = sys.stdout
+    with contextlib.redirect_stdout(sys.stderr):
+        line = _main()
+    if line is not None:
+        print(json.dumps(line), file=out, flush=True)
+
+
+def _main():
     args = parse()
     import torch
     import torch.distributed as dist
@@ -320,9 +331,11 @@ def main():
             "ppo": ppo,
             "other_configs": others,
         }
-        print(json.dumps(line), flush=True)
+    else:
+        line = None
     if world > 1:
         dist.destroy_process_group()
+    return line
 
 
 if __name__ == "__main__":

@@ -146,6 +146,27 @@ int gt_measure_heights(const int16_t *samples, int rows, int cols, float border,
                        const float *root_states, const float *points, int num_envs, int num_points, float *heights,
                        void *stream);
 
+/* UsefulHound control (useful_hound.py:695-726 inner loop, fused): for every env,
+ *   legs: torques[0:12] = clip(kp * (action_scale * a[0:12] + leg_default - q[0:12]) - kd * qd[0:12], +-torque_limit)
+ *   arm : the operational-space controller of useful_hound.py:660-691 with
+ *         M = mass_matrix[e][nv-6:][nv-6:], J = jacobian[e][jac_row][:][0:6], v_eef = rigid_body[e*nl+eef_link][7:13],
+ *         dpose = a[12:18] * arm_cmd_limit / arm_action_scale,
+ *         u = J^T M_eef (arm_kp dpose - arm_kd v_eef) + (1 - J^T M_eef J M^-1) M u_null,  M_eef = (J M^-1 J^T)^-1,
+ *         u_null = -arm_kd_null qd_arm + arm_kp_null ((arm_default - q_arm + pi) mod 2 pi - pi),
+ *         clamped to +-arm_effort  -> torques[12:18] and arm_control (row stride arm_control_stride floats).
+ * The 6x6 algebra runs in float64 (Gauss-Jordan with partial pivoting) on one lane per env.
+ * actions [N][18], dof_state [N*18][2], leg_default [12] (device), mass_matrix [N][nv][nv],
+ * jacobian [N][nl][6][nv], rigid_body [N*nl][13], torques [N][18]. */
+typedef struct gt_hound_control_params {
+    int32_t num_envs, nv, num_links, jac_row, eef_link, arm_control_stride;
+    float kp, kd, action_scale, torque_limit, arm_action_scale;
+    float arm_kp[6], arm_kd[6], arm_kp_null[6], arm_kd_null[6], arm_cmd_limit[6], arm_default[6], arm_effort[6];
+} gt_hound_control_params;
+
+int gt_hound_control(const gt_hound_control_params *p, const float *actions, const float *dof_state,
+                     const float *leg_default, const float *mass_matrix, const float *jacobian,
+                     const float *rigid_body, float *torques, float *arm_control, void *stream);
+
 /* out[plan.numel] = torch.rand(plan.numel) for the given plan (checks torch_philox.h against torch) */
 int gt_torch_rand(const gt_torch_rand_plan *plan, float *out, void *stream);
 

@@ -19,7 +19,7 @@ ARCH = os.environ.get("GS_OFFLOAD_ARCH", "gfx950")
 
 LIBS = {
     "libgymsim.so": ["gs_physics.hip", "gs_team.hip", "gs_kinematics.hip", "gs_capi.hip"],
-    "libgymtask.so": ["gt_anymal.hip"],
+    "libgymtask.so": ["gt_anymal.hip", "gt_hound.hip"],
     "libgymrl.so": ["rl_gae.hip"],
     # phase-profiling build of the simulator (tools/phase_profile.py); never loaded by default
     "libgymsim_prof.so": ["gs_physics.hip", "gs_team.hip", "gs_kinematics.hip", "gs_capi.hip"],
@@ -45,9 +45,9 @@ def _stale(out: str, srcs) -> bool:
         return True
     t = os.path.getmtime(out)
     deps = [os.path.join(CSRC, s) for s in srcs] + [os.path.join(CSRC, h) for h in HEADERS]
-    deps.append(os.path.join(os.path.dirname(HERE), "include", "gymsim.h"))
-    deps.append(os.path.join(os.path.dirname(HERE), "include", "gymtask.h"))
-    deps.append(os.path.join(os.path.dirname(HERE), "include", "gymrl.h"))
+    # each library implements one public header (the others do not affect it)
+    header = {"gs_": "gymsim.h", "gt_": "gymtask.h", "rl_": "gymrl.h"}[srcs[0][:3]]
+    deps.append(os.path.join(os.path.dirname(HERE), "include", header))
     deps.append(os.path.abspath(__file__))  # flags live here
     return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
 

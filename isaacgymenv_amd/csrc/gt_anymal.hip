@@ -516,6 +516,9 @@ int check_params(const gt_anymal_params* p) {
 }
 }  // namespace
 
+// shared with the other task kernels of libgymtask (gt_hound.hip)
+void gt_set_last_error(const char* msg) { g_err = msg; }
+
 extern "C" {
 
 int gt_abi_version(void) { return GT_ABI_VERSION; }

@@ -77,6 +77,13 @@ class GtAnymalResetDraws(C.Structure):
                                  "cmd_y_range", "cmd_y_lower", "cmd_h_range", "cmd_h_lower")]
 
 
+class GtHoundControlParams(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("num_envs", "nv", "num_links", "jac_row", "eef_link", "arm_control_stride")] + [
+        (n, C.c_float) for n in ("kp", "kd", "action_scale", "torque_limit", "arm_action_scale")] + [
+        (n, C.c_float * 6) for n in ("arm_kp", "arm_kd", "arm_kp_null", "arm_kd_null", "arm_cmd_limit", "arm_default",
+                                     "arm_effort")]
+
+
 _lib = None
 
 
@@ -98,7 +105,9 @@ def lib():
                            "gt_host_free": [vp],
                            "gt_wait_host_seq": [vp, C.c_int32, C.c_int32, C.POINTER(C.c_int32)],
                            "gt_measure_heights": [vp, i, i, C.c_float, C.c_float, C.c_float, vp, vp, i, i, vp,
-                                                  vp]}.items():
+                                                  vp],
+                           "gt_hound_control": [C.POINTER(GtHoundControlParams), vp, vp, vp, vp, vp, vp, vp, vp,
+                                                vp]}.items():
             fn = getattr(L, name)
             fn.restype = C.c_int
             fn.argtypes = args
@@ -110,7 +119,44 @@ def lib():
 
 EXPORTED_SYMBOLS = ["gt_abi_version", "gt_last_error", "gt_anymal_post_physics_a", "gt_anymal_reset",
                     "gt_anymal_post_physics_b", "gt_anymal_reset_flagged", "gt_torch_rand", "gt_host_alloc",
-                    "gt_host_free", "gt_wait_host_seq", "gt_measure_heights"]
+                    "gt_host_free", "gt_wait_host_seq", "gt_measure_heights", "gt_hound_control"]
+
+
+class HoundControlKernel:
+    """gt_hound_control bound to one UsefulHound env's tensors (the fused inner step of its decimation loop)."""
+
+    def __init__(self, env):
+        import torch
+        self.env = env
+        p = GtHoundControlParams()
+        p.num_envs = env.num_envs
+        p.nv = int(env._mm_full.shape[-1])
+        p.num_links = int(env._jac_full.shape[1])
+        p.jac_row = int(env._hand_joint_index)
+        p.eef_link = int(env.eef_index)
+        p.arm_control_stride = int(env._effort_control.stride(0))
+        p.kp, p.kd = float(env.Kp), float(env.Kd)
+        p.action_scale, p.torque_limit = float(env.action_scale), 80.0
+        p.arm_action_scale = float(env.arm_action_scale)
+        for name, t in (("arm_kp", env.arm_kp), ("arm_kd", env.arm_kd), ("arm_kp_null", env.arm_kp_null),
+                        ("arm_kd_null", env.arm_kd_null), ("arm_cmd_limit", env.arm_cmd_limit.reshape(-1)),
+                        ("arm_default", env.houndarm_default_dof_pos[:6]), ("arm_effort", env._houndarm_effort_limits[:6])):
+            vals = [float(v) for v in t.detach().cpu().reshape(-1)[:6]]
+            getattr(p, name)[:] = vals
+        self.p = p
+        self.leg_default = env.hound_default_dof_pos[0].contiguous()
+        for t in (env.dof_state, env._mm_full, env._jac_full, env._rigid_body_state):
+            assert t.is_contiguous() and t.dtype == torch.float32 and t.is_cuda
+        assert env._effort_control.is_contiguous()
+
+    def __call__(self, actions, torques_out):
+        import torch
+        env = self.env
+        stream = torch.cuda.current_stream(actions.device).cuda_stream
+        _check(lib().gt_hound_control(C.byref(self.p), actions.data_ptr(), env.dof_state.data_ptr(),
+                                      self.leg_default.data_ptr(), env._mm_full.data_ptr(), env._jac_full.data_ptr(),
+                                      env._rigid_body_state.data_ptr(), torques_out.data_ptr(),
+                                      env._effort_control.data_ptr(), C.c_void_p(stream)), "gt_hound_control")
 
 
 def _check(rc, what):

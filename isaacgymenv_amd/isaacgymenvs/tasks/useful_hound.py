@@ -18,6 +18,9 @@ tensor API's link kinematics (rigid-body state, Jacobian, mass matrix) in gs_kin
 * RNG order: friction buckets, terrain levels / types at creation; per reset: leg dof offsets,
   leg dof velocities, [trimesh root xy], arm reset noise, command x, y, heading; per step: push
   draw and observation noise.
+On the GPU pipeline the leg PD + arm OSC of each decimation step is one HIP kernel (gt_hound_control,
+float64 6x6 algebra, one lane per env) instead of ~40 torch launches with two host-synchronising
+batched inverses; the torch statements remain the CPU-pipeline path (and the golden-tested spec).
 The end-effector state comes from the rigid-body state tensor, which the reference acquires but
 never refreshes outside its debug-viz branch: it holds the prepared (initial) state, and so does
 ours.
@@ -148,6 +151,12 @@ class UsefulHound(AnymalTerrain):
         self.arm_cmd_limit = to_torch([0.1, 0.1, 0.1, 0.5, 0.5, 0.5], device=dev).unsqueeze(0)
         self.arm_commands = zeros(self.num_envs, 3)
         self._fused_refreshed = False
+        self._control = None
+        if self.device != "cpu":
+            # GPU pipeline: the leg PD + arm OSC of every decimation step is one kernel (gt_hound_control)
+            from ...gymtask import HoundControlKernel  # fails loudly when libgymtask.so is missing
+            self._control = HoundControlKernel(self)
+            self._torque_buf = zeros(self.num_envs, self.num_actions)
         self.gym.refresh_actor_root_state_tensor(self.sim)
         self.gym.refresh_net_contact_force_tensor(self.sim)
         self.gym.refresh_jacobian_tensors(self.sim)
@@ -272,6 +281,7 @@ class UsefulHound(AnymalTerrain):
         self._j_eef = jacobian[:, hand_joint_index, :, :6]
         mm = gymtorch.wrap_tensor(self.gym.acquire_mass_matrix_tensor(self.sim, "UsefulHound"))
         self._mm = mm[:, -6:, -6:]
+        self._jac_full, self._mm_full, self._hand_joint_index = jacobian, mm, hand_joint_index
         self._pos_control = torch.zeros((self.num_envs, self.arm_num_dof), dtype=torch.float, device=self.device)
         self._effort_control = torch.zeros_like(self._pos_control)
         self._arm_control = self._effort_control[:, :6]
@@ -417,6 +427,15 @@ class UsefulHound(AnymalTerrain):
     # ------------------------------------------------------------------ step
     def pre_physics_step(self, actions):
         self.actions = actions.clone().to(self.device)
+        if self._control is not None:
+            a = self.actions.contiguous()
+            for _ in range(self.decimation):
+                self._control(a, self._torque_buf)  # torques [N,18] and _arm_control, as the torch loop below
+                self.gym.set_dof_actuation_force_tensor(self.sim, gymtorch.unwrap_tensor(self._torque_buf))
+                self.torques = self._torque_buf
+                self.gym.simulate(self.sim)
+                self.gym.refresh_dof_state_tensor(self.sim)
+            return
         for _ in range(self.decimation):
             u_arm = self.actions[:, 12:] * self.arm_cmd_limit / self.arm_action_scale
             u_arm = self._compute_osc_torques(dpose=u_arm)

@@ -179,3 +179,42 @@ def test_hound_task_episode(monkeypatch):
         if t % 50 == 0:
             assert torch.isfinite(obs["obs"]).all() and torch.isfinite(rew).all()
     assert resets > 0
+
+
+def _osc_reference_f64(J, M, v_eef, q, qd, dpose, kp, kd, kp_null, kd_null, default, effort):
+    """useful_hound.py:660-691 in float64 numpy (the oracle of gt_hound_control's arm half)."""
+    mm_inv = np.linalg.inv(M)
+    m_eef = np.linalg.inv(J @ mm_inv @ np.transpose(J, (0, 2, 1)))
+    u = np.transpose(J, (0, 2, 1)) @ m_eef @ (kp * dpose - kd * v_eef)[..., None]
+    j_eef_inv = m_eef @ J @ mm_inv
+    u_null = kd_null * -qd + kp_null * (np.mod(default - q + np.pi, 2 * np.pi) - np.pi)
+    u_null = M @ u_null[..., None]
+    u = u + (np.eye(6)[None] - np.transpose(J, (0, 2, 1)) @ j_eef_inv) @ u_null
+    return np.clip(u[..., 0], -effort, effort)
+
+
+def test_hound_control_kernel_matches_reference(monkeypatch):
+    """gt_hound_control (legs PD + arm OSC, one kernel) vs the reference expressions: the legs against
+    torch float32 on the same tensors (same expression order), the arm against float64 numpy."""
+    n = 512
+    env = _make(n, monkeypatch)
+    gen = torch.Generator(device="cuda:0").manual_seed(11)
+    for _ in range(20):
+        env.step(2 * torch.rand((n, 18), device="cuda:0", generator=gen) - 1)
+    torch.cuda.synchronize()
+    a = (2 * torch.rand((n, 18), device="cuda:0", generator=gen) - 1).contiguous()
+    out = torch.zeros((n, 18), device="cuda:0")
+    env._control(a, out)
+    torch.cuda.synchronize()
+    legs = torch.clip(env.Kp * (env.action_scale * a[:, :12] + env.hound_default_dof_pos - env.hound_dof_pos)
+                      - env.Kd * env.hound_dof_vel, -80.0, 80.0)
+    torch.testing.assert_close(out[:, :12], legs, rtol=0, atol=1e-5)
+    f = lambda t: t.detach().double().cpu().numpy()  # noqa: E731
+    dpose = f(a[:, 12:] * env.arm_cmd_limit / env.arm_action_scale)
+    ref = _osc_reference_f64(f(env._j_eef), f(env._mm), f(env._eef_state[:, 7:]), f(env._q[:, :6]), f(env._qd[:, :6]),
+                             dpose, f(env.arm_kp), f(env.arm_kd), f(env.arm_kp_null), f(env.arm_kd_null),
+                             f(env.houndarm_default_dof_pos[:6]), f(env._houndarm_effort_limits[:6]))
+    got = f(out[:, 12:])
+    scale = np.maximum(1.0, np.abs(ref))
+    assert np.all(np.abs(got - ref) <= 1e-4 * scale), np.abs(got - ref).max()
+    np.testing.assert_array_equal(f(env._effort_control[:, :6]), got)
