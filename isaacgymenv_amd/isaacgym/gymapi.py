@@ -408,6 +408,24 @@ class Sim:
         for kind in ("rigid_body", "jacobian", "mass_matrix"):  # acquired before prepare_sim
             self.refresh(kind)
 
+    def position_drives(self) -> bool:
+        """Some actor has a DOF_MODE_POS dof with drive gains (checked once: dof properties are fixed
+        once the sim is prepared; the reset path of UsefulHound asks on every reset)."""
+        if getattr(self, "_pos_drives", None) is None or not self.prepared:
+            found = False
+            for e in self.envs:
+                for a in e.actors:
+                    p = a.dof_props
+                    if np.any((p["driveMode"] == DOF_MODE_POS) & ((p["stiffness"] != 0) | (p["damping"] != 0))):
+                        found = True
+                        break
+                if found:
+                    break
+            if not self.prepared:
+                return found
+            self._pos_drives = found
+        return self._pos_drives
+
     def _tensors(self):
         """Reference-layout tensors (sim owned; wrap_tensor shares them), sized from the created envs.
         Isaac Gym lets a task acquire them before prepare_sim (useful_hound.py:438-455 does, inside
@@ -818,13 +836,8 @@ class Gym:
 
     @staticmethod
     def _check_effort_mode(sim: Sim, what: str) -> bool:
-        for e in sim.envs:
-            for a in e.actors:
-                mode = a.dof_props["driveMode"]
-                stiff = a.dof_props["stiffness"]
-                damp = a.dof_props["damping"]
-                if np.any((mode == DOF_MODE_POS) & ((stiff != 0) | (damp != 0))):
-                    raise NotImplementedError(f"{what}: position-drive dofs are not simulated (DESIGN.md 6)")
+        if sim.position_drives():
+            raise NotImplementedError(f"{what}: position-drive dofs are not simulated (DESIGN.md 6)")
         return True
 
     # ---- viewer / rendering (headless build: no-ops)
