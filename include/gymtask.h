@@ -167,6 +167,33 @@ int gt_hound_control(const gt_hound_control_params *p, const float *actions, con
                      const float *leg_default, const float *mass_matrix, const float *jacobian,
                      const float *rigid_body, float *torques, float *arm_control, void *stream);
 
+/* Ant post-physics tail (ant.py:299-324 compute_observations + :326-371 compute_ant_reward), fused,
+ * run after post_physics_step's resets and refreshes: per env, the 60-wide observation, potentials /
+ * previous potentials, up and heading vectors, the reward, the done mask (int64, fallen or episode
+ * end, else kept) and extras["true_objective"]; publishes the done count {count, seq} to host_count
+ * (gt_host_alloc words) so the next step's reset needs no nonzero() when nothing is done.
+ * root_states [N][13], dof_state [N*8][2], sensors [N][24], actions [N][8], targets [N][3],
+ * inv_start_rot [N][4], potentials / prev_potentials / rew_buf / true_objective [N],
+ * up_vec / heading_vec [N][3], obs_buf [N][60], reset_buf / progress_buf int64 [N]. */
+typedef struct gt_ant_params {
+    int32_t num_envs, num_dofs;
+    float dt, dof_vel_scale, contact_force_scale, heading_weight, up_weight, actions_cost_scale,
+          energy_cost_scale, joints_at_limit_cost_scale, termination_height, death_cost, max_episode_length;
+    float dof_lower[8], dof_upper[8];
+} gt_ant_params;
+
+typedef struct gt_ant_buffers {
+    const float *root_states, *dof_state, *sensors, *actions, *targets, *inv_start_rot;
+    float *potentials, *prev_potentials, *up_vec, *heading_vec, *obs_buf, *rew_buf, *true_objective;
+    int64_t *reset_buf;
+    const int64_t *progress_buf;
+    int32_t *reset_count;        /* [3] device, zero-initialised accumulator (re-armed by the kernel) */
+    int32_t *host_count;         /* [2] host-mapped {count, seq} or NULL */
+    int32_t seq;
+} gt_ant_buffers;
+
+int gt_ant_post_physics(const gt_ant_params *p, const gt_ant_buffers *b, void *stream);
+
 /* out[plan.numel] = torch.rand(plan.numel) for the given plan (checks torch_philox.h against torch) */
 int gt_torch_rand(const gt_torch_rand_plan *plan, float *out, void *stream);
 

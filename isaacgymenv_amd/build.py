@@ -19,7 +19,7 @@ ARCH = os.environ.get("GS_OFFLOAD_ARCH", "gfx950")
 
 LIBS = {
     "libgymsim.so": ["gs_physics.hip", "gs_team.hip", "gs_kinematics.hip", "gs_capi.hip"],
-    "libgymtask.so": ["gt_anymal.hip", "gt_hound.hip"],
+    "libgymtask.so": ["gt_anymal.hip", "gt_hound.hip", "gt_ant.hip"],
     "libgymrl.so": ["rl_gae.hip"],
     # phase-profiling build of the simulator (tools/phase_profile.py); never loaded by default
     "libgymsim_prof.so": ["gs_physics.hip", "gs_team.hip", "gs_kinematics.hip", "gs_capi.hip"],

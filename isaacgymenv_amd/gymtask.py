@@ -84,6 +84,21 @@ class GtHoundControlParams(C.Structure):
                                      "arm_effort")]
 
 
+class GtAntParams(C.Structure):
+    _fields_ = [("num_envs", C.c_int32), ("num_dofs", C.c_int32)] + [
+        (n, C.c_float) for n in ("dt", "dof_vel_scale", "contact_force_scale", "heading_weight", "up_weight",
+                                 "actions_cost_scale", "energy_cost_scale", "joints_at_limit_cost_scale",
+                                 "termination_height", "death_cost", "max_episode_length")] + [
+        ("dof_lower", C.c_float * 8), ("dof_upper", C.c_float * 8)]
+
+
+class GtAntBuffers(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("root_states", "dof_state", "sensors", "actions", "targets",
+                                          "inv_start_rot", "potentials", "prev_potentials", "up_vec",
+                                          "heading_vec", "obs_buf", "rew_buf", "true_objective", "reset_buf",
+                                          "progress_buf", "reset_count", "host_count")] + [("seq", C.c_int32)]
+
+
 _lib = None
 
 
@@ -107,7 +122,8 @@ def lib():
                            "gt_measure_heights": [vp, i, i, C.c_float, C.c_float, C.c_float, vp, vp, i, i, vp,
                                                   vp],
                            "gt_hound_control": [C.POINTER(GtHoundControlParams), vp, vp, vp, vp, vp, vp, vp, vp,
-                                                vp]}.items():
+                                                vp],
+                           "gt_ant_post_physics": [C.POINTER(GtAntParams), C.POINTER(GtAntBuffers), vp]}.items():
             fn = getattr(L, name)
             fn.restype = C.c_int
             fn.argtypes = args
@@ -119,7 +135,69 @@ def lib():
 
 EXPORTED_SYMBOLS = ["gt_abi_version", "gt_last_error", "gt_anymal_post_physics_a", "gt_anymal_reset",
                     "gt_anymal_post_physics_b", "gt_anymal_reset_flagged", "gt_torch_rand", "gt_host_alloc",
-                    "gt_host_free", "gt_wait_host_seq", "gt_measure_heights", "gt_hound_control"]
+                    "gt_host_free", "gt_wait_host_seq", "gt_measure_heights", "gt_hound_control",
+                    "gt_ant_post_physics"]
+
+
+class AntTailKernel:
+    """gt_ant_post_physics bound to one Ant env (GPU pipeline): observations + reward + done mask in one
+    launch, and the done count published to pinned host memory for the next step's reset."""
+
+    def __init__(self, env):
+        L = lib()
+        t = self.env = env
+        p = GtAntParams()
+        p.num_envs, p.num_dofs = t.num_envs, t.num_dof
+        p.dt, p.dof_vel_scale, p.contact_force_scale = float(t.dt), float(t.dof_vel_scale), float(t.contact_force_scale)
+        p.heading_weight, p.up_weight = float(t.heading_weight), float(t.up_weight)
+        p.actions_cost_scale, p.energy_cost_scale = float(t.actions_cost_scale), float(t.energy_cost_scale)
+        p.joints_at_limit_cost_scale = float(t.joints_at_limit_cost_scale)
+        p.termination_height, p.death_cost = float(t.termination_height), float(t.death_cost)
+        p.max_episode_length = float(t.max_episode_length)
+        p.dof_lower[:] = [float(v) for v in t.dof_limits_lower.cpu()]
+        p.dof_upper[:] = [float(v) for v in t.dof_limits_upper.cpu()]
+        self.p = p
+        self.true_objective = torch.zeros(t.num_envs, dtype=torch.float32, device=t.device)
+        self.reset_count = torch.zeros(3, dtype=torch.int32, device=t.device)
+        h, d = C.c_void_p(), C.c_void_p()
+        _check(L.gt_host_alloc(8, C.byref(h), C.byref(d)), "gt_host_alloc")
+        self._host_words, self._host_words_dev = h.value, d.value
+        self._seq = 0
+        self._launched = False
+        self._count = C.c_int32(0)
+
+    def __del__(self):
+        if getattr(self, "_host_words", None) and _lib is not None:
+            _lib.gt_host_free(self._host_words)
+            self._host_words = None
+
+    def done_count(self):
+        """Envs the previous launch flagged (None before the first launch: the caller must look)."""
+        if not self._launched:
+            return None
+        _check(lib().gt_wait_host_seq(C.c_void_p(self._host_words), self._seq, 10000, C.byref(self._count)),
+               "gt_wait_host_seq")
+        return int(self._count.value)
+
+    def __call__(self):
+        t = self.env
+        b = GtAntBuffers()
+        for name, ten in (("root_states", t.root_states), ("dof_state", t.dof_state), ("sensors", t.vec_sensor_tensor),
+                          ("actions", t.actions), ("targets", t.targets), ("inv_start_rot", t.inv_start_rot),
+                          ("potentials", t.potentials), ("prev_potentials", t.prev_potentials),
+                          ("up_vec", t.up_vec), ("heading_vec", t.heading_vec), ("obs_buf", t.obs_buf),
+                          ("rew_buf", t.rew_buf), ("true_objective", self.true_objective),
+                          ("reset_buf", t.reset_buf), ("progress_buf", t.progress_buf)):
+            assert ten.is_contiguous() and ten.is_cuda, name
+            setattr(b, name, ten.data_ptr())
+        assert t.reset_buf.dtype == torch.int64 and t.progress_buf.dtype == torch.int64
+        self._seq += 1
+        b.seq = self._seq
+        b.reset_count = self.reset_count.data_ptr()
+        b.host_count = self._host_words_dev
+        stream = torch.cuda.current_stream(t.root_states.device).cuda_stream
+        _check(lib().gt_ant_post_physics(C.byref(self.p), C.byref(b), C.c_void_p(stream)), "gt_ant_post_physics")
+        self._launched = True
 
 
 class HoundControlKernel:

@@ -12,6 +12,11 @@ reference's own code in tests/golden/ant.npz):
 * reset draws: dof offsets U(-0.2, 0.2) then dof velocities U(-0.1, 0.1), in that order,
   positions clamped into the limits (ant.py:252-279); the reset buffer is int64.
 
+On the GPU pipeline the post-reset tail (observations, reward, done mask, true objective) is one HIP
+kernel (libgymtask gt_ant_post_physics) that also publishes the done count to pinned host memory, so
+the next step looks for envs to reset only when there are some; the torch statements below stay the
+CPU-pipeline path and the golden-tested specification.
+
 Observation layout (ant.py:400-404): torso height, local linear velocity (3), local angular
 velocity (3), yaw, roll, angle to target, up projection, heading projection, scaled dof
 positions (8), dof velocities * dofVelocityScale (8), force-sensor wrenches * contactForceScale
@@ -100,6 +105,11 @@ class Ant(VecTask):
         self.dt = self.cfg["sim"]["dt"]
         self.potentials = to_torch([-1000.0 / self.dt], device=dev).repeat(n)
         self.prev_potentials = self.potentials.clone()
+        self._tail = None
+        if self.device != "cpu":
+            # GPU pipeline: observations + reward + done mask are one kernel (gt_ant_post_physics)
+            from ...gymtask import AntTailKernel  # fails loudly when libgymtask.so is missing
+            self._tail = AntTailKernel(self)
 
     # ------------------------------------------------------------------ scene
     def create_sim(self):
@@ -165,6 +175,19 @@ class Ant(VecTask):
     def post_physics_step(self):
         self.progress_buf += 1
         self.randomize_buf += 1
+        if self._tail is not None:
+            # the previous step's kernel published how many envs it flagged: look for them only then
+            k = self._tail.done_count()
+            if k is None or k > 0:
+                env_ids = self.reset_buf.nonzero(as_tuple=False).flatten()
+                if len(env_ids) > 0:
+                    self.reset_idx(env_ids)
+            self.gym.refresh_dof_state_tensor(self.sim)
+            self.gym.refresh_actor_root_state_tensor(self.sim)
+            self.gym.refresh_force_sensor_tensor(self.sim)
+            self._tail()  # compute_observations + compute_reward + compute_true_objective
+            self.extras["true_objective"] = self._tail.true_objective
+            return
         env_ids = self.reset_buf.nonzero(as_tuple=False).flatten()
         if len(env_ids) > 0:
             self.reset_idx(env_ids)

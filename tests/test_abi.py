@@ -82,7 +82,8 @@ def test_ctypes_struct_layouts_match_the_headers(tmp_path):
     mirrors = {"gs_model_desc": _lib.GsModelDesc, "gs_sim_params": _lib.GsSimParams, "gs_pd_args": _lib.GsPdArgs,
                "gt_torch_rand_plan": gymtask.GtTorchRandPlan, "gt_anymal_params": gymtask.GtAnymalParams,
                "gt_anymal_buffers": gymtask.GtAnymalBuffers, "gt_anymal_reset_draws": gymtask.GtAnymalResetDraws,
-               "gt_hound_control_params": gymtask.GtHoundControlParams}
+               "gt_hound_control_params": gymtask.GtHoundControlParams, "gt_ant_params": gymtask.GtAntParams,
+               "gt_ant_buffers": gymtask.GtAntBuffers}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gymsim.h"', '#include "gymtask.h"',
              "int main(void) {"]
     expect = []

@@ -1,0 +1,58 @@
+"""Ant's fused post-physics tail (libgymtask gt_ant_post_physics) vs the torch restatement of
+ant.py:374-406 / :326-371 on the same GPU tensors (the torch path is the golden-tested spec,
+tests/test_golden_tasks.py).  Tolerance: float32 rounding of differently fused expressions,
+rtol 1e-5 / atol 1e-5 (angles 2e-5); the done mask exactly."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _make(n, monkeypatch):
+    from isaacgymenv_amd.isaacgymenvs.tasks.base import vec_task
+    monkeypatch.setattr(vec_task, "EXISTING_SIM", None)
+    import isaacgymenvs
+    torch.manual_seed(42)
+    return isaacgymenvs.make(seed=42, task="Ant", num_envs=n, sim_device="cuda:0", rl_device="cuda:0",
+                             headless=True, force_render=False)
+
+
+def test_ant_tail_kernel_matches_torch_tail(monkeypatch):
+    from isaacgymenv_amd.isaacgymenvs.tasks.ant import compute_ant_observations, compute_ant_reward
+    n = 1024
+    env = _make(n, monkeypatch)
+    assert env._tail is not None
+    gen = torch.Generator(device="cuda:0").manual_seed(5)
+    for _ in range(40):
+        env.step(2 * torch.rand((n, 8), device="cuda:0", generator=gen) - 1)
+    env.progress_buf[: n // 8] = env.max_episode_length - 1  # exercise the episode-end branch
+    torch.cuda.synchronize()
+    pot0, reset0 = env.potentials.clone(), env.reset_buf.clone()
+    obs, pot, prev, up, heading = compute_ant_observations(
+        env.root_states, env.targets, pot0.clone(), env.inv_start_rot, env.dof_pos, env.dof_vel,
+        env.dof_limits_lower, env.dof_limits_upper, env.dof_vel_scale, env.vec_sensor_tensor, env.actions, env.dt,
+        env.contact_force_scale, env.basis_vec0, env.basis_vec1, env.up_axis_idx)
+    rew, reset = compute_ant_reward(obs, reset0.clone(), env.progress_buf, env.actions, env.up_weight,
+                                    env.heading_weight, pot, prev, env.actions_cost_scale, env.energy_cost_scale,
+                                    env.joints_at_limit_cost_scale, env.termination_height, env.death_cost,
+                                    env.max_episode_length)
+    env._tail()
+    torch.cuda.synchronize()
+    angles = [7, 8, 9]
+    other = [c for c in range(60) if c not in angles]
+    torch.testing.assert_close(env.obs_buf[:, other], obs[:, other], rtol=1e-5, atol=1e-5)
+    # yaw / roll are taken mod 2 pi: compare on the circle
+    d = torch.remainder(env.obs_buf[:, angles] - obs[:, angles] + np.pi, 2 * np.pi) - np.pi
+    assert float(d.abs().max()) < 2e-5
+    torch.testing.assert_close(env.potentials, pot, rtol=1e-6, atol=1e-4)
+    torch.testing.assert_close(env.prev_potentials, prev, rtol=0, atol=0)
+    torch.testing.assert_close(env.up_vec, up, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(env.heading_vec, heading, rtol=1e-5, atol=1e-6)
+    # progress reward = potentials - prev_potentials, two ~6e4 numbers (|target| / dt): one float32 ulp of
+    # the potential (0.0039 at 6e4; sqrt vs torch.norm) is the whole absolute error budget of the reward
+    ulp = float(torch.finfo(torch.float32).eps) * float(pot.abs().max())
+    torch.testing.assert_close(env.rew_buf, rew, rtol=1e-5, atol=2 * ulp)
+    assert torch.equal(env.reset_buf, reset) and int(reset.sum()) >= n // 8
+    assert env._tail.done_count() == int(reset.sum())
+    torch.testing.assert_close(env._tail.true_objective, env.root_states[:, 7])
