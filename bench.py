@@ -72,11 +72,22 @@ def parse():
 
 
 def cpu_baseline(num_envs: int, seconds: float):
-    """fp32 CPU oracle on the same per-env work: PD (decimation 4) + 5 substeps per env step."""
+    """fp32 CPU oracle on the same per-env work, on the host cores the box grants (OMP_NUM_THREADS) and,
+    beside it, on 4 threads (the reference CPU pipeline's num_threads: 4, config.yaml:30-32)."""
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    main = _cpu_sample(num_envs, seconds, threads)
+    four = _cpu_sample(num_envs, seconds / 2, 4) if threads != 4 else main
+    main["sample"] += (f"; on 4 threads (reference PhysX CPU num_threads 4): {four['value']:.0f} env-steps/s; "
+                       f"host: {os.cpu_count()} logical CPUs visible")
+    main["threads4_value"] = four["value"]
+    return main
+
+
+def _cpu_sample(num_envs: int, seconds: float, threads: int):
+    """PD (decimation 4) + 5 substeps per env step, AnymalTerrain standing start, uniform random actions."""
     import numpy as np
     from oracle.oracle import OracleSim
     from tests import helpers as H
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     art, flat = H.anymal()
     sim = OracleSim(flat, H.ANYMAL_PARAMS, real_bits=32)
     n = min(num_envs, 4096)
