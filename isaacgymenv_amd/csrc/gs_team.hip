@@ -926,7 +926,11 @@ __device__ __forceinline__ void team_com_velocity(const DevModel* __restrict__ M
   v[0] = s.vo[0] + wc[0]; v[1] = s.vo[1] + wc[1]; v[2] = s.vo[2] + wc[2];
 }
 
-constexpr int kTeamBlock = 64;  // one wave per workgroup: 16 envs
+#ifndef GS_TEAM_BLOCK
+#define GS_TEAM_BLOCK 64
+#endif
+constexpr int kTeamBlock = GS_TEAM_BLOCK;  // lanes per workgroup (one wave at most): 64 -> 16 envs
+static_assert(kTeamBlock % 4 == 0 && kTeamBlock <= GS_WAVE, "a workgroup holds whole teams within one wave");
 
 template <class T>
 __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel* __restrict__ M, DevParams P,
