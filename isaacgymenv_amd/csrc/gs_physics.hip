@@ -51,8 +51,12 @@ __device__ __forceinline__ constexpr bool body_on_path(int kk, int b) {
 template <class T, bool TERR = false>
 struct LaneCfg {
   static constexpr int SLOTS = T::NSLOT + (TERR ? 3 * T::NC : 0);
-  static constexpr int LB = (SLOTS * 64 * 4 <= 160 * 1024) ? 64 : (SLOTS * 32 * 4 <= 160 * 1024) ? 32
+  static constexpr int FIT = (SLOTS * 64 * 4 <= 160 * 1024) ? 64 : (SLOTS * 32 * 4 <= 160 * 1024) ? 32
                            : (SLOTS * 16 * 4 <= 160 * 1024) ? 16 : 8;
+  // Below 16 lanes the rows of two workgroups no longer share a CU, and halving again measured
+  // ~10 % faster for Hound (2745 slots; r01n, profiles/r01n_experiments_other_configs.txt) while
+  // Ant (32 lanes) got slower at 4: only the LDS-starved widths go narrower.
+  static constexpr int LB = FIT == 8 ? 4 : FIT;
   static_assert(SLOTS * LB * 4 <= 160 * 1024, "contact rows exceed the LDS of a CU even at 8 lanes");
 };
 
