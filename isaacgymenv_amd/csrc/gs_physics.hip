@@ -55,8 +55,10 @@ struct LaneCfg {
                            : (SLOTS * 16 * 4 <= 160 * 1024) ? 16 : 8;
   // Below 16 lanes the rows of two workgroups no longer share a CU, and halving again measured
   // ~10 % faster for Hound (2745 slots; r01n, profiles/r01n_experiments_other_configs.txt) while
-  // Ant (32 lanes) got slower at 4: only the LDS-starved widths go narrower.
-  static constexpr int LB = FIT == 8 ? 4 : FIT;
+  // Ant (32 lanes) got slower at 4: only the LDS-starved widths go narrower.  The mesh-contact
+  // (TERR) variant is bound by its terrain queries, which gain from spreading the envs over more
+  // CUs: 16 lanes measured ~8 % faster than 64 for ANYmal on the trimesh map.
+  static constexpr int LB = FIT == 8 ? 4 : (TERR && FIT > 16) ? 16 : FIT;
   static_assert(SLOTS * LB * 4 <= 160 * 1024, "contact rows exceed the LDS of a CU even at 8 lanes");
 };
 
