@@ -58,7 +58,13 @@ struct LaneCfg {
   // Ant (32 lanes) got slower at 4: only the LDS-starved widths go narrower.  The mesh-contact
   // (TERR) variant is bound by its terrain queries, which gain from spreading the envs over more
   // CUs: 16 lanes measured ~8 % faster than 64 for ANYmal on the trimesh map.
-  static constexpr int LB = FIT == 8 ? 4 : (TERR && FIT > 16) ? 16 : FIT;
+#ifndef GS_NARROW_LANES
+#define GS_NARROW_LANES 4
+#endif
+#ifndef GS_TERR_LANES
+#define GS_TERR_LANES 16
+#endif
+  static constexpr int LB = FIT == 8 ? GS_NARROW_LANES : (TERR && FIT > GS_TERR_LANES) ? GS_TERR_LANES : FIT;
   static_assert(SLOTS * LB * 4 <= 160 * 1024, "contact rows exceed the LDS of a CU even at 8 lanes");
 };
 
