@@ -97,7 +97,10 @@ gs_sim* gs_sim_create(int device, const gs_sim_params* p) {
     fail("gs_sim_create: no HIP device %s", std::to_string(device).c_str());
     return nullptr;
   }
-  hipSetDevice(device);
+  if (hipError_t e = hipSetDevice(device); e != hipSuccess) {
+    hip_fail(e, "gs_sim_create hipSetDevice");
+    return nullptr;
+  }
   gs_sim* s = new gs_sim();
   s->device = device;
   s->params = *p;
@@ -120,13 +123,14 @@ gs_sim* gs_sim_create(int device, const gs_sim_params* p) {
 
 void gs_sim_destroy(gs_sim* s) {
   if (!s) return;
-  hipSetDevice(s->device);
-  if (s->d_model) hipFree(s->d_model);
-  if (s->d_links) hipFree(s->d_links);
-  if (s->d_tverts) hipFree(s->d_tverts);
-  if (s->d_tcells) hipFree(s->d_tcells);
-  if (s->ev0) hipEventDestroy(s->ev0);
-  if (s->ev1) hipEventDestroy(s->ev1);
+  // Teardown is best-effort: a failed free cannot be reported through a void API.
+  (void)hipSetDevice(s->device);
+  if (s->d_model) (void)hipFree(s->d_model);
+  if (s->d_links) (void)hipFree(s->d_links);
+  if (s->d_tverts) (void)hipFree(s->d_tverts);
+  if (s->d_tcells) (void)hipFree(s->d_tcells);
+  if (s->ev0) (void)hipEventDestroy(s->ev0);
+  if (s->ev1) (void)hipEventDestroy(s->ev1);
   delete s;
 }
 
@@ -214,8 +218,8 @@ int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_verti
       hc[(size_t)(i * (cols - 1) + j)] = make_uint2(zb, f);
     }
   }
-  hipSetDevice(s->device);
-  hipError_t e = hipMalloc(&s->d_tverts, hv.size() * sizeof(float4));
+  hipError_t e = hipSetDevice(s->device);
+  if (e == hipSuccess) e = hipMalloc(&s->d_tverts, hv.size() * sizeof(float4));
   if (e == hipSuccess) e = hipMalloc(&s->d_tcells, hc.size() * sizeof(uint2));
   if (e == hipSuccess) e = hipMemcpy(s->d_tverts, hv.data(), hv.size() * sizeof(float4), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(s->d_tcells, hc.data(), hc.size() * sizeof(uint2), hipMemcpyHostToDevice);
@@ -284,7 +288,7 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   h.nsens = 0;
   for (int b = 0; b < GS_MAXB; ++b) h.sens_of_body[b] = -1;
   s->h_model = h;
-  hipSetDevice(s->device);
+  if (hipError_t e = hipSetDevice(s->device); e != hipSuccess) return hip_fail(e, "gs_sim_set_model hipSetDevice");
   if (!s->d_model) {
     hipError_t e = hipMalloc(&s->d_model, sizeof(DevModel));
     if (e != hipSuccess) return hip_fail(e, "gs_sim_set_model hipMalloc");
@@ -366,13 +370,18 @@ static int ready(gs_sim* s, const char* where) {
 
 static void timing_begin(gs_sim* s, hipStream_t st) {
   if (!s->timing) return;
-  if (!s->ev0) { hipEventCreate(&s->ev0); hipEventCreate(&s->ev1); }
-  hipEventRecord(s->ev0, st);
+  if (!s->ev0) {
+    // Timing is diagnostic: if the events cannot be made, switch it off rather than fail the step.
+    if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess) {
+      s->timing = false;
+      return;
+    }
+  }
+  (void)hipEventRecord(s->ev0, st);
 }
 static void timing_end(gs_sim* s, hipStream_t st) {
   if (!s->timing) return;
-  hipEventRecord(s->ev1, st);
-  s->timed = true;
+  s->timed = hipEventRecord(s->ev1, st) == hipSuccess;
 }
 
 int gs_sim_simulate(gs_sim* s, const float* dof_force, void* stream) {
@@ -472,8 +481,8 @@ int gs_sim_set_force_sensors(gs_sim* s, int n, const int32_t* bodies) {
     h.sens_of_body[b] = i;
   }
   h.nsens = n;
-  hipSetDevice(s->device);
-  hipError_t e = hipMemcpy(s->d_model, &h, sizeof(DevModel), hipMemcpyHostToDevice);
+  hipError_t e = hipSetDevice(s->device);
+  if (e == hipSuccess) e = hipMemcpy(s->d_model, &h, sizeof(DevModel), hipMemcpyHostToDevice);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_set_force_sensors hipMemcpy");
 }
 
