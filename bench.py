@@ -13,10 +13,12 @@ no data-path collective (weak scaling); the only collectives are the barrier and
 the max-over-ranks of the timed region.
 
 The rank-0 JSON line carries:
-  roofline     -- the fused physics kernel (gs_sim_pd_step): algorithmic HBM bytes
-                  per launch / its average HIP-event duration on the launch stream;
-  cpu_baseline -- the fp32 build of the CPU oracle (oracle/, kind "port") stepping
-                  a bounded sample of the same workload on the host cores;
+  roofline     -- the fused physics kernel (gs_sim_pd_step): SURVEY.md 8(d)'s algorithmic HBM
+                  bytes of the env step per launch / its average HIP-event duration on the launch
+                  stream (the kernel-scoped bytes beside it);
+  cpu_baseline -- the product's CPU pipeline (sim_device=cpu pipeline=cpu: libgymsim's host
+                  backend + the task's torch tail) stepping a bounded sample of the same workload
+                  on every usable host CPU and on 4 threads;
   other_configs-- env-steps/s of the other BASELINE.json configs on one GPU (Ant 4096, AnymalTerrain
                   trimesh 4096, UsefulHound 4096), same timed-region rules, --other-steps steps each;
   ppo          -- PPO samples/s (the metric's second half): the rl_games-compatible learner
@@ -42,8 +44,18 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measur
 FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector)
 
 
+# algorithmic HBM bytes of one AnymalTerrain env step (plane), every mutable
+# per-env buffer of the step read once and written once: reads 1,136 B (actions 48, root 52,
+# dof_state 96, last_actions 48, last_dof_vel 48, commands 16, feet_air_time 16, progress 8,
+# episode_sums 52, pre-drawn obs noise 752) + writes 1,298 B (obs 752, rew 4, reset 1, timeout 1,
+# progress 8, root 52, dof_state 96, contact forces 156, torques 48, last_actions 48,
+# last_dof_vel 48, feet_air_time 16, episode_sums 52, commands 16).
+STEP_BYTES_PER_ENV = 2434
+
+
 def physics_kernel_bytes_per_env(nd=12, nb=13, ns=9):
-    """Algorithmic HBM bytes one env moves through gs_sim_pd_step.
+    """Kernel-scoped algorithmic HBM bytes one env moves through gs_sim_pd_step alone (DESIGN.md
+    section 5), reported beside the step-scoped figure.
 
     reads : SoA state (13 + 2 nd) f32, actions nd, dof tensor (q, qd) 2 nd, shape friction ns
     writes: SoA state (13 + 2 nd), torques nd, dof tensor 2 nd, root tensor 13,
@@ -62,7 +74,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--num-envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="wall budget of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--kernel-launches", type=int, default=50, help="launches timed for the roofline figure")
     ap.add_argument("--other-steps", type=int, default=100,
                     help="timed steps of each other BASELINE config (Ant, trimesh AnymalTerrain, UsefulHound); 0 = skip")
@@ -71,46 +83,87 @@ def parse():
     return ap.parse_args()
 
 
+def host_cpu_info():
+    """The host the CPU baseline ran on: logical CPUs (nproc), the CPUs this process may run on
+    (affinity), the cgroup CPU quota, and the CPU model (lscpu's "Model name")."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity"] = os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(float(q) / float(per)))
+    except (OSError, ValueError):
+        pass
+    info["cgroup_cpus"] = quota
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    info["model"] = model
+    info["usable"] = min(x for x in (info["affinity"], quota) if x)
+    return info
+
+
 def cpu_baseline(num_envs: int, seconds: float):
-    """fp32 CPU oracle on the same per-env work, on the host cores the box grants (OMP_NUM_THREADS) and,
-    beside it, on 4 threads (the reference CPU pipeline's num_threads: 4, config.yaml:30-32)."""
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    """The product's CPU pipeline (sim_device=cpu pipeline=cpu: libgymsim's host backend + the task's
+    torch tail on the CPU) stepping the same AnymalTerrain workload, on every host CPU this process may
+    use and, beside it, on 4 threads (the reference CPU pipeline's physx.num_threads: 4,
+    cfg/config.yaml:30-32).  Bounded sample: ~`seconds` of stepping per thread count."""
+    info = host_cpu_info()
+    threads = info["usable"]
     main = _cpu_sample(num_envs, seconds, threads)
     four = _cpu_sample(num_envs, seconds / 2, 4) if threads != 4 else main
-    main["sample"] += (f"; on 4 threads (reference PhysX CPU num_threads 4): {four['value']:.0f} env-steps/s; "
-                       f"host: {os.cpu_count()} logical CPUs visible")
+    main["sample"] += (f"; on 4 threads (reference PhysX CPU num_threads 4): {four['value']:.0f} env-steps/s; host: "
+                       f"{info['model']}, nproc {info['nproc']}, affinity {info['affinity']} CPUs, cgroup quota "
+                       f"{info['cgroup_cpus']} CPUs")
     main["threads4_value"] = four["value"]
+    main["host"] = info
     return main
 
 
 def _cpu_sample(num_envs: int, seconds: float, threads: int):
-    """PD (decimation 4) + 5 substeps per env step, AnymalTerrain standing start, uniform random actions."""
-    import numpy as np
-    from oracle.oracle import OracleSim
-    from tests import helpers as H
-    art, flat = H.anymal()
-    sim = OracleSim(flat, H.ANYMAL_PARAMS, real_bits=32)
-    n = min(num_envs, 4096)
-    q0 = np.array([H.ANYMAL_DEFAULT[d] for d in art.dof_names()], dtype=np.float32)
-    root = np.zeros((n, 13), dtype=np.float32); root[:, 2] = 0.62; root[:, 6] = 1.0
-    dof = np.zeros((n, 12, 2), dtype=np.float32); dof[:, :, 0] = q0
-    mu = np.ones((n, flat["ns"]), dtype=np.float32)
-    rng = np.random.RandomState(0)
-    steps, t0 = 0, time.perf_counter()
-    while True:
-        a = (2 * rng.rand(n, 12) - 1).astype(np.float32)
-        for sub in range(5):
-            if sub < 4:
-                tau = np.clip(80.0 * (0.5 * a + q0 - dof[:, :, 0]) - 2.0 * dof[:, :, 1], -80, 80).astype(np.float32)
-            sim.simulate(root, dof, np.ascontiguousarray(tau), mu, num_threads=threads)
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds and steps >= 2:
-            break
-    return {"value": n * steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"fp32 oracle (oracle/physics_oracle.c) physics only: {n} envs x {steps} env steps "
-                      f"(PD decimation 4 + 5 substeps each) in {el:.1f} s on {threads} threads; the reference's "
-                      f"Python tail (8.9-12.5 ms/step at 4096 envs, SURVEY.md section 6) is not included"}
+    """VecTask.step of AnymalTerrain (plane) on the CPU pipeline: physics in libgymsim's host backend on
+    `threads` threads (physx.num_threads), the post-physics tail in torch on `threads` threads."""
+    import torch
+    import isaacgymenvs
+    from isaacgymenv_amd.isaacgymenvs.tasks.base import vec_task
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    vec_task.EXISTING_SIM = None
+    try:
+        env = isaacgymenvs.make(seed=42, task="AnymalTerrain", num_envs=num_envs, sim_device="cpu", rl_device="cpu",
+                                graphics_device_id=-1, headless=True, force_render=False,
+                                overrides=["pipeline=cpu", f"num_threads={threads}"])
+        assert env.sim.host and env.sim.cparams.num_threads == threads
+        gen = torch.Generator().manual_seed(1234)
+        pool = torch.empty((16, env.num_envs, env.num_actions)).uniform_(-1.0, 1.0, generator=gen)
+        env.reset()
+        for i in range(2):
+            env.step(pool[i])
+        steps, t0 = 0, time.perf_counter()
+        while True:
+            env.step(pool[steps % 16])
+            steps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds and steps >= 3:
+                break
+    finally:
+        torch.set_num_threads(prev)
+        vec_task.EXISTING_SIM = None
+    return {"value": num_envs * steps / el, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"product CPU pipeline (sim_device=cpu pipeline=cpu: libgymsim host backend, same solver "
+                      f"source as the HIP kernels, + the AnymalTerrain torch tail): {num_envs} envs x {steps} "
+                      f"VecTask.step calls (5 simulates each, tail included) in {el:.1f} s on {threads} threads"}
 
 
 def timed_region(step, steps: int, warmup: int, world: int, sync=lambda: None) -> float:
@@ -281,8 +334,12 @@ def _main():
     kernel_ms = ev0.elapsed_time(ev1) / args.kernel_launches
     variant = env.gym.amd_kernel_variant(env.sim)
     kernel_name = {1: "k_pd_step<Topo_anymal_c>", 2: "k_pd_step_team<Topo_anymal_c>"}.get(variant, str(variant))
-    bytes_per_launch = physics_kernel_bytes_per_env() * N
+    # roofline basis: SURVEY.md 8(d)'s step-scoped algorithmic bytes (2,434 B per env step) per launch of
+    # the dominant kernel; the kernel-scoped bytes (what gs_sim_pd_step alone moves) beside it
+    bytes_per_launch = STEP_BYTES_PER_ENV * N
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    kbytes_per_launch = physics_kernel_bytes_per_env() * N
+    kachieved = kbytes_per_launch / (kernel_ms * 1e-3) / 1e9
 
     ppo = None
     if args.ppo_epochs > 0:
@@ -294,13 +351,14 @@ def _main():
             others.append(other_config_leg(task, desc, ov, args.num_envs, args.other_steps, 20, device, rank, world))
 
     if rank == 0:
-        traffic = None
+        traffic, traffic_note = None, None
         pmc = os.path.join(ROOT, "profiles", "pmc_pd_step.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
                 d = json.load(f)
             if d.get("num_envs") == N:
                 traffic = d.get("hbm_bytes_per_launch")
+                traffic_note = d.get("note")
         # secondary roofline (SURVEY.md 8d "report both"): counted FP32 VALU FLOPs of the same kernel
         valu = None
         vj = os.path.join(ROOT, "profiles", "valu_pd_step.json")
@@ -336,7 +394,12 @@ def _main():
                        "num_envs_per_gpu": N, "global_num_envs": N * world, "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "kernel": f"gs_sim_pd_step ({kernel_name})",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "kernel_ms": kernel_ms, "bytes_per_launch": bytes_per_launch,
+                         "traffic": traffic, "traffic_note": traffic_note, "kernel_ms": kernel_ms,
+                         "bytes_per_launch": bytes_per_launch,
+                         "basis": f"SURVEY.md 8(d): {STEP_BYTES_PER_ENV} B per env step x {N} envs per launch",
+                         "kernel_scoped": {"bytes_per_launch": kbytes_per_launch, "achieved": kachieved,
+                                           "frac": kachieved / HBM_PEAK_GBS,
+                                           "basis": "gs_sim_pd_step's own reads + writes, DESIGN.md section 5"},
                          "valu": valu},
             "cpu_baseline": cpu,
             "ppo": ppo,

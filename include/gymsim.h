@@ -17,6 +17,12 @@
  *     `create_sim` returns None (vec_task.py:338-340).
  *   - a gs_sim is not thread safe; all work is stream ordered (no host sync)
  *     except gs_sim_create / gs_sim_set_model / gs_sim_prepare.
+ *   - host backend (ABI 3): gs_sim_create(device < 0, ...) makes a sim that runs the
+ *     same solver on the CPU -- the reference's sim_device=cpu pipeline (vec_task.py:82-88,
+ *     PhysX CPU with physx.num_threads workers, cfg/config.yaml:30-32).  Every buffer
+ *     argument of such a sim is a HOST pointer in the same layout, `stream` is ignored and
+ *     each call returns when its work is done (gym.fetch_results(sim, True) is a no-op).
+ *     It makes no HIP call, so it runs on a machine without a GPU.
  *   - tensor layouts are the reference's (AoS, float32):
  *       root state  [num_envs][13]  pos(3) quat xyzw(4) lin vel of COM(3) ang vel(3)
  *       dof state   [num_envs*num_dofs][2] (pos, vel)
@@ -39,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 2
+#define GS_ABI_VERSION 3
 
 typedef struct gs_sim gs_sim;
 
@@ -89,6 +95,8 @@ typedef struct gs_sim_params {
     int32_t contact_collection;         /* 0 never, 1 last substep (2 treated as 1)        */
     int32_t kernel_variant;             /* 0 auto, 1 one env per lane, 2 lane team (4 lanes/env) */
     double joint_limit_margin;          /* a limit row is active within this distance of the limit */
+    int32_t num_threads;                /* ABI 3, host backend: physx.num_threads (cfg/config.yaml:30)
+                                           solver threads including the caller; <= 1 = caller only */
 } gs_sim_params;
 
 /* Fused PD decimation step (AnymalTerrain.pre_physics_step + VecTask.step's
@@ -120,7 +128,8 @@ const char *gs_last_error(void);
 /* 1 if libgymsim was compiled with a specialised kernel for this topology. */
 int gs_topology_supported(const gs_model_desc *model);
 
-/* gym.create_sim(compute_device, graphics_device, SIM_PHYSX, sim_params)   vec_task.py:337 */
+/* gym.create_sim(compute_device, graphics_device, SIM_PHYSX, sim_params)   vec_task.py:337
+ * device >= 0: HIP device ordinal; device < 0: host backend (physx.use_gpu = False). */
 gs_sim *gs_sim_create(int device, const gs_sim_params *params);
 void gs_sim_destroy(gs_sim *sim);
 
@@ -188,11 +197,13 @@ int gs_sim_bind_force_sensors(gs_sim *sim, float *sensor_soa);
 /* refresh_force_sensor_tensor: SoA -> [N*n][6] (ant.py:233-235) */
 int gs_sim_refresh_force_sensor(gs_sim *sim, float *out, void *stream);
 
-/* Physics kernel selected by gs_sim_set_model: 1 one env per lane, 2 lane team; -1 on error. */
+/* Physics kernel selected by gs_sim_set_model: 1 one env per lane, 2 lane team, 3 host backend;
+ * -1 on error. */
 int gs_sim_kernel_variant(gs_sim *sim);
 
 /* Kernel time of the last gs_sim_pd_step / gs_sim_simulate launch measured with
- * HIP events on `stream` (ms); -1 if not recorded.  Used by bench.py. */
+ * HIP events on `stream` (ms; host backend: wall time of the call); -1 if not recorded.
+ * Used by bench.py. */
 int gs_sim_enable_timing(gs_sim *sim, int enable);
 float gs_sim_last_kernel_ms(gs_sim *sim);
 

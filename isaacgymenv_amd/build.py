@@ -18,19 +18,22 @@ LIBDIR = os.path.join(HERE, "_lib")
 ARCH = os.environ.get("GS_OFFLOAD_ARCH", "gfx950")
 
 LIBS = {
-    "libgymsim.so": ["gs_physics.hip", "gs_team.hip", "gs_kinematics.hip", "gs_capi.hip"],
+    "libgymsim.so": ["gs_physics.hip", "gs_team.hip", "gs_kinematics.hip", "gs_host.hip", "gs_capi.hip"],
     "libgymtask.so": ["gt_anymal.hip", "gt_hound.hip", "gt_ant.hip"],
     "libgymrl.so": ["rl_gae.hip"],
-    # phase-profiling build of the simulator (tools/phase_profile.py); never loaded by default
-    "libgymsim_prof.so": ["gs_physics.hip", "gs_team.hip", "gs_kinematics.hip", "gs_capi.hip"],
 }
+# phase-profiling build of the simulator (tools/phase_profile.py); never loaded by default, built only
+# on request (`python -m isaacgymenv_amd.build --prof`)
+PROF_LIBS = {"libgymsim_prof.so": LIBS["libgymsim.so"]}
 # the task kernels mirror torch's unfused elementwise arithmetic
 # -fno-slp-vectorize: the SLP vectorizer packs the scalar spatial algebra into v_pk_* pairs and
 # then spends ~1700 v_mov_b32 (and AGPR copies) arranging register pairs in the physics kernels
 SIM_FLAGS = ["-fno-slp-vectorize"]
 EXTRA_FLAGS = {"libgymtask.so": ["-ffp-contract=off"], "libgymrl.so": ["-ffp-contract=off"], "libgymsim.so": SIM_FLAGS,
                "libgymsim_prof.so": SIM_FLAGS + ["-DGS_PHASE_PROFILE"]}
-HEADERS = ["gs_internal.h", "gs_topologies.h", "gs_math.h", "gs_terrain.h", "torch_philox.h"]
+HEADERS = ["gs_internal.h", "gs_topologies.h", "gs_math.h", "gs_terrain.h", "gs_solver.h", "gs_kinematics.h",
+           "torch_philox.h"]
+OBJDIR = os.path.join(LIBDIR, "obj")
 
 
 def hipcc() -> str:
@@ -52,38 +55,65 @@ def _stale(out: str, srcs) -> bool:
     return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True) -> None:
-    """Compile every stale library; the libraries are independent, so hipcc runs in parallel."""
+def _deps_newer(out: str, deps) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = True, prof: bool = False) -> None:
+    """Compile every stale library.  Each source is its own hipcc job (objects under _lib/obj/<lib>/,
+    all jobs of all libraries in parallel: the physics sources dominate and compile independently),
+    then each library is linked from its objects."""
     from concurrent.futures import ThreadPoolExecutor
     os.makedirs(LIBDIR, exist_ok=True)
     cc = hipcc()
-    jobs = []
-    for lib, srcs in LIBS.items():
+    inc = ["-I", os.path.join(os.path.dirname(HERE), "include"), "-I", CSRC]
+    compile_jobs, link_jobs = [], []
+    for lib, srcs in (dict(LIBS, **PROF_LIBS) if prof else LIBS).items():
         if not all(os.path.exists(os.path.join(CSRC, s)) for s in srcs):
             raise RuntimeError(f"missing sources for {lib}: {srcs}")
         out = os.path.join(LIBDIR, lib)
         if not force and not _stale(out, srcs):
             continue
-        cmd = [cc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-I", os.path.join(os.path.dirname(HERE), "include"), "-I", CSRC, "-o", out]
-        cmd += EXTRA_FLAGS.get(lib, [])
-        cmd += [os.path.join(CSRC, s) for s in srcs]
-        jobs.append((lib, cmd))
+        odir = os.path.join(OBJDIR, lib.replace(".so", ""))
+        os.makedirs(odir, exist_ok=True)
+        header = {"gs_": "gymsim.h", "gt_": "gymtask.h", "rl_": "gymrl.h"}[srcs[0][:3]]
+        common = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.abspath(__file__),
+                                                              os.path.join(os.path.dirname(HERE), "include", header)]
+        objs = []
+        for src in srcs:
+            obj = os.path.join(odir, src.replace(".hip", ".o"))
+            objs.append(obj)
+            if force or _deps_newer(obj, [os.path.join(CSRC, src)] + common):
+                cmd = [cc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c"] + inc
+                cmd += EXTRA_FLAGS.get(lib, []) + ["-o", obj, os.path.join(CSRC, src)]
+                compile_jobs.append((f"{lib}:{src}", cmd))
+        link_jobs.append((lib, [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + ["-lpthread"]))
 
     def run(job):
-        lib, cmd = job
+        name, cmd = job
         if verbose:
             print("[build]", " ".join(cmd), flush=True)
-        return lib, subprocess.run(cmd, capture_output=True, text=True)
+        return name, subprocess.run(cmd, capture_output=True, text=True)
 
-    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "4") or 4)))
-    with ThreadPoolExecutor(max_workers=workers) as ex:
-        for lib, r in ex.map(run, jobs):
-            if r.returncode != 0:
-                raise RuntimeError(f"hipcc failed for {lib}:\n{r.stdout}\n{r.stderr}")
-            if verbose and r.stderr.strip():
-                print(r.stderr[-4000:], file=sys.stderr)
+    def run_all(jobs):
+        if not jobs:
+            return
+        workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "8") or 8)))
+        with ThreadPoolExecutor(max_workers=workers) as ex:
+            for name, r in ex.map(run, jobs):
+                if r.returncode != 0:
+                    raise RuntimeError(f"hipcc failed for {name}:\n{r.stdout}\n{r.stderr}")
+                if verbose and r.stderr.strip():
+                    print(r.stderr[-4000:], file=sys.stderr)
+
+    # the slowest sources first so they overlap everything else
+    compile_jobs.sort(key=lambda j: 0 if ("gs_team" in j[0] or "gs_physics" in j[0] or "gs_host" in j[0]) else 1)
+    run_all(compile_jobs)
+    run_all(link_jobs)
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, prof="--prof" in sys.argv)

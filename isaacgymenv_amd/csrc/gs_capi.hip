@@ -5,10 +5,15 @@
 // selected kernel specialisation, and binds the caller-owned (torch) device
 // buffers that hold the sim state.  All launches are stream ordered; nothing
 // here synchronises the host except create/set_model/prepare.
+//
+// A sim created with device < 0 is the host backend (gs_host.hip, the reference's
+// sim_device=cpu pipeline): same entry points, caller-owned HOST buffers, the solver
+// runs on a thread pool inside the call, `stream` is ignored, no HIP call is made.
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -80,6 +85,16 @@ struct gs_sim {
   bool timed = false;
   float4* d_tverts = nullptr;     // terrain mesh (gs_terrain.h)
   uint2* d_tcells = nullptr;
+  // host backend (device < 0)
+  bool host = false;
+  HostPool* pool = nullptr;
+  const HostTopoEntry* htopo = nullptr;
+  DevLinks h_links{};
+  std::vector<float4> h_tverts;
+  std::vector<uint2> h_tcells;
+  double host_ms = -1.0;          // wall time of the last simulate / pd_step (timing enabled)
+  const DevModel* model() const { return host ? &h_model : d_model; }
+  const DevLinks* links() const { return host ? &h_links : d_links; }
 };
 
 extern "C" {
@@ -92,17 +107,26 @@ int gs_topology_supported(const gs_model_desc* model) { return find_topology(mod
 gs_sim* gs_sim_create(int device, const gs_sim_params* p) {
   if (!p) { fail("gs_sim_create: null params"); return nullptr; }
   if (!(p->dt > 0)) { fail("gs_sim_create: dt must be > 0"); return nullptr; }
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
-    fail("gs_sim_create: no HIP device %s", std::to_string(device).c_str());
-    return nullptr;
+  gs_sim* s = nullptr;
+  if (device < 0) {
+    s = new gs_sim();
+    s->host = true;
+    s->device = -1;
+    // physx.num_threads (cfg/config.yaml:30): worker threads; 0 runs the solver on the caller only
+    s->pool = host_pool_create(p->num_threads > 0 ? p->num_threads : 1);
+  } else {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
+      fail("gs_sim_create: no HIP device %s", std::to_string(device).c_str());
+      return nullptr;
+    }
+    if (hipError_t e = hipSetDevice(device); e != hipSuccess) {
+      hip_fail(e, "gs_sim_create hipSetDevice");
+      return nullptr;
+    }
+    s = new gs_sim();
+    s->device = device;
   }
-  if (hipError_t e = hipSetDevice(device); e != hipSuccess) {
-    hip_fail(e, "gs_sim_create hipSetDevice");
-    return nullptr;
-  }
-  gs_sim* s = new gs_sim();
-  s->device = device;
   s->params = *p;
   const int sub = p->substeps > 0 ? p->substeps : 1;
   s->dp.h = (float)(p->dt / sub);
@@ -123,6 +147,11 @@ gs_sim* gs_sim_create(int device, const gs_sim_params* p) {
 
 void gs_sim_destroy(gs_sim* s) {
   if (!s) return;
+  if (s->host) {
+    host_pool_destroy(s->pool);
+    delete s;
+    return;
+  }
   // Teardown is best-effort: a failed free cannot be reported through a void API.
   (void)hipSetDevice(s->device);
   if (s->d_model) (void)hipFree(s->d_model);
@@ -218,15 +247,30 @@ int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_verti
       hc[(size_t)(i * (cols - 1) + j)] = make_uint2(zb, f);
     }
   }
-  hipError_t e = hipSetDevice(s->device);
-  if (e == hipSuccess) e = hipMalloc(&s->d_tverts, hv.size() * sizeof(float4));
-  if (e == hipSuccess) e = hipMalloc(&s->d_tcells, hc.size() * sizeof(uint2));
-  if (e == hipSuccess) e = hipMemcpy(s->d_tverts, hv.data(), hv.size() * sizeof(float4), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(s->d_tcells, hc.data(), hc.size() * sizeof(uint2), hipMemcpyHostToDevice);
-  if (e != hipSuccess) return hip_fail(e, "gs_sim_add_triangle_mesh");
   TerrainDev& T = s->dp.terr;
-  T.v = s->d_tverts;
-  T.cell = s->d_tcells;
+  if (s->host) {
+    s->h_tverts = std::move(hv);
+    s->h_tcells = std::move(hc);
+    T.v = s->h_tverts.data();
+    T.cell = s->h_tcells.data();
+  } else {
+    float4* dv = nullptr;
+    uint2* dc = nullptr;
+    hipError_t e = hipSetDevice(s->device);
+    if (e == hipSuccess) e = hipMalloc(&dv, hv.size() * sizeof(float4));
+    if (e == hipSuccess) e = hipMalloc(&dc, hc.size() * sizeof(uint2));
+    if (e == hipSuccess) e = hipMemcpy(dv, hv.data(), hv.size() * sizeof(float4), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dc, hc.data(), hc.size() * sizeof(uint2), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      if (dv) (void)hipFree(dv);
+      if (dc) (void)hipFree(dc);
+      return hip_fail(e, "gs_sim_add_triangle_mesh");
+    }
+    s->d_tverts = dv;
+    s->d_tcells = dc;
+    T.v = s->d_tverts;
+    T.cell = s->d_tcells;
+  }
   T.rows = (int)rows;
   T.cols = (int)cols;
   T.x0 = (float)(x0 + tx);
@@ -253,6 +297,8 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   if (!t)
     return fail("gs_sim_set_model: no compiled kernel for topology %s (add it to tools/gen_topologies.py)",
                 signature(m).c_str());
+  // Everything is built into locals first and committed at the end, so a failure leaves the sim as
+  // it was (no half-set topology with a null kernel or link table).
   DevModel h;
   std::memset(&h, 0, sizeof(h));
   for (int i = 0; i < m->num_bodies; ++i) {
@@ -287,34 +333,7 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   }
   h.nsens = 0;
   for (int b = 0; b < GS_MAXB; ++b) h.sens_of_body[b] = -1;
-  s->h_model = h;
-  if (hipError_t e = hipSetDevice(s->device); e != hipSuccess) return hip_fail(e, "gs_sim_set_model hipSetDevice");
-  if (!s->d_model) {
-    hipError_t e = hipMalloc(&s->d_model, sizeof(DevModel));
-    if (e != hipSuccess) return hip_fail(e, "gs_sim_set_model hipMalloc");
-  }
-  hipError_t e = hipMemcpy(s->d_model, &h, sizeof(DevModel), hipMemcpyHostToDevice);
-  if (e != hipSuccess) return hip_fail(e, "gs_sim_set_model hipMemcpy");
-  s->topo = t;
-  const TeamEntry* te = nullptr;
-  for (int i = 0; i < g_num_team_kernels; ++i)
-    if (std::strcmp(g_team_kernels[i].sig, t->sig) == 0 && g_team_kernels[i].sim) te = &g_team_kernels[i];
-  const int want = s->params.kernel_variant;
-  // the lane team has no joint-limit rows and no mesh contacts: the one-env-per-lane kernel runs
-  if (te && (any_lim || s->dp.has_terrain)) te = nullptr;
-  if (want == 2 && !te)
-    return fail("gs_sim_set_model: no lane-team kernel for this topology / joint limits / terrain mesh");
-  s->dp.any_limits = any_lim;
-  s->parent.assign(m->parent, m->parent + m->num_bodies);
-  if (te && want != 1) {
-    s->sim_fn = te->sim;
-    s->pd_fn = te->pd;
-    s->variant = 2;
-  } else {
-    s->sim_fn = t->sim;
-    s->pd_fn = t->pd;
-    s->variant = 1;
-  }
+
   DevLinks hl;
   std::memset(&hl, 0, sizeof(hl));
   hl.nb = m->num_bodies;
@@ -336,18 +355,64 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
     for (int k = 0; k < 3; ++k) hl.lt[l][k] = (float)m->link_pose[12 * l + 9 + k];
     for (int k = 0; k < 3; ++k) hl.lcom[l][k] = (float)m->link_com[3 * l + k];
   }
-  if (!s->d_links) {
-    hipError_t e2 = hipMalloc(&s->d_links, sizeof(DevLinks));
-    if (e2 != hipSuccess) return hip_fail(e2, "gs_sim_set_model hipMalloc links");
+
+  const int want = s->params.kernel_variant;
+  launch_sim_fn sim_fn = nullptr;
+  launch_pd_fn pd_fn = nullptr;
+  const HostTopoEntry* htopo = nullptr;
+  int variant = 0;
+  if (s->host) {
+    for (int i = 0; i < g_num_host_topologies; ++i)
+      if (std::strcmp(g_host_topologies[i].sig, t->sig) == 0) htopo = &g_host_topologies[i];
+    if (!htopo) return fail("gs_sim_set_model: no host solver for topology %s", t->sig);
+    if (want == 2) return fail("gs_sim_set_model: the lane-team kernel is a GPU kernel (host sim)");
+    variant = 3;
+  } else {
+    const TeamEntry* te = nullptr;
+    for (int i = 0; i < g_num_team_kernels; ++i)
+      if (std::strcmp(g_team_kernels[i].sig, t->sig) == 0 && g_team_kernels[i].sim) te = &g_team_kernels[i];
+    // the lane team has no joint-limit rows and no mesh contacts: the one-env-per-lane kernel runs
+    if (te && (any_lim || s->dp.has_terrain)) te = nullptr;
+    if (want == 2 && !te)
+      return fail("gs_sim_set_model: no lane-team kernel for this topology / joint limits / terrain mesh");
+    if (te && want != 1) {
+      sim_fn = te->sim;
+      pd_fn = te->pd;
+      variant = 2;
+    } else {
+      sim_fn = t->sim;
+      pd_fn = t->pd;
+      variant = 1;
+    }
+    if (hipError_t e = hipSetDevice(s->device); e != hipSuccess) return hip_fail(e, "gs_sim_set_model hipSetDevice");
+    DevModel* dm = s->d_model;
+    DevLinks* dl = s->d_links;
+    hipError_t e = hipSuccess;
+    if (!dm) e = hipMalloc(&dm, sizeof(DevModel));
+    if (e == hipSuccess && !dl) e = hipMalloc(&dl, sizeof(DevLinks));
+    // keep whatever was allocated (freed by gs_sim_destroy) even when a later step fails
+    s->d_model = dm;
+    s->d_links = dl;
+    if (e == hipSuccess) e = hipMemcpy(dm, &h, sizeof(DevModel), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dl, &hl, sizeof(DevLinks), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e, "gs_sim_set_model upload");
   }
-  e = hipMemcpy(s->d_links, &hl, sizeof(DevLinks), hipMemcpyHostToDevice);
-  if (e != hipSuccess) return hip_fail(e, "gs_sim_set_model hipMemcpy links");
+  // commit
+  s->h_model = h;
+  s->h_links = hl;
+  s->dp.any_limits = any_lim;
+  s->parent.assign(m->parent, m->parent + m->num_bodies);
+  s->sim_fn = sim_fn;
+  s->pd_fn = pd_fn;
+  s->htopo = htopo;
+  s->variant = variant;
   s->nr = m->num_links;
   s->nv = (m->fixed_base ? 0 : 6) + m->num_dofs;
   s->nb = m->num_bodies;
   s->nd = m->num_dofs;
   s->nc = m->num_candidates;
   s->ns = m->num_shapes;
+  s->topo = t;
   return 0;
 }
 
@@ -365,11 +430,13 @@ static SimBuffers buffers(gs_sim* s) { return SimBuffers{s->state, s->mu, s->cf,
 
 static int ready(gs_sim* s, const char* where) {
   if (!s || !s->topo || !s->state) return fail("%s: sim not prepared", where);
+  if (s->host ? !s->htopo : (!s->sim_fn || !s->pd_fn || !s->d_model || !s->d_links))
+    return fail("%s: sim model incomplete", where);
   return 0;
 }
 
 static void timing_begin(gs_sim* s, hipStream_t st) {
-  if (!s->timing) return;
+  if (!s->timing || s->host) return;
   if (!s->ev0) {
     // Timing is diagnostic: if the events cannot be made, switch it off rather than fail the step.
     if (hipEventCreate(&s->ev0) != hipSuccess || hipEventCreate(&s->ev1) != hipSuccess) {
@@ -380,12 +447,25 @@ static void timing_begin(gs_sim* s, hipStream_t st) {
   (void)hipEventRecord(s->ev0, st);
 }
 static void timing_end(gs_sim* s, hipStream_t st) {
-  if (!s->timing) return;
+  if (!s->timing || s->host) return;
   s->timed = hipEventRecord(s->ev1, st) == hipSuccess;
 }
 
+namespace {
+using host_clock = std::chrono::steady_clock;
+double ms_since(host_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(host_clock::now() - t0).count();
+}
+}  // namespace
+
 int gs_sim_simulate(gs_sim* s, const float* dof_force, void* stream) {
   if (ready(s, "gs_sim_simulate")) return -1;
+  if (s->host) {
+    const auto t0 = host_clock::now();
+    s->htopo->sim(&s->h_model, s->dp, buffers(s), dof_force, s->pool);
+    s->host_ms = ms_since(t0);
+    return 0;
+  }
   hipStream_t st = (hipStream_t)stream;
   timing_begin(s, st);
   hipError_t e = s->sim_fn(s->d_model, s->dp, buffers(s), dof_force, st);
@@ -409,6 +489,12 @@ int gs_sim_pd_step(gs_sim* s, const gs_pd_args* a, void* stream) {
   d.root_out = a->root_state_out;
   d.cf_out = a->contact_out;
   d.actions_copy = a->actions_copy_out;
+  if (s->host) {
+    const auto t0 = host_clock::now();
+    s->htopo->pd(&s->h_model, s->dp, buffers(s), d, s->pool);
+    s->host_ms = ms_since(t0);
+    return 0;
+  }
   hipStream_t st = (hipStream_t)stream;
   timing_begin(s, st);
   hipError_t e = s->pd_fn(s->d_model, s->dp, buffers(s), d, st);
@@ -418,48 +504,67 @@ int gs_sim_pd_step(gs_sim* s, const gs_pd_args* a, void* stream) {
 
 int gs_sim_refresh_root(gs_sim* s, float* out, void* stream) {
   if (ready(s, "gs_sim_refresh_root")) return -1;
+  if (s->host) {
+    host_refresh_root(s->state, s->N, &s->h_model.root_com[0], out, s->pool);
+    return 0;
+  }
   hipError_t e = launch_refresh_root(s->state, s->N, s->nd, &s->d_model->root_com[0], out, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_root");
 }
 int gs_sim_refresh_dof(gs_sim* s, float* out, void* stream) {
   if (ready(s, "gs_sim_refresh_dof")) return -1;
+  if (s->host) {
+    host_refresh_dof(s->state, s->N, s->nd, out, s->pool);
+    return 0;
+  }
   hipError_t e = launch_refresh_dof(s->state, s->N, s->nd, out, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_dof");
 }
 int gs_sim_refresh_contact(gs_sim* s, float* out, void* stream) {
   if (ready(s, "gs_sim_refresh_contact")) return -1;
+  if (s->host) {
+    host_soa_to_aos(s->cf, s->N, s->nr, 3, out, s->pool);
+    return 0;
+  }
   hipError_t e = launch_refresh_contact(s->cf, s->N, s->nr, out, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_contact");
 }
-int gs_sim_refresh_rigid_body(gs_sim* s, float* out, void* stream) {
-  if (ready(s, "gs_sim_refresh_rigid_body")) return -1;
-  if (!out) return fail("gs_sim_refresh_rigid_body: null output");
-  hipError_t e = launch_kinematics(s->d_model, s->d_links, s->state, s->N, s->nv, 1, out, nullptr, nullptr,
+static int kinematics(gs_sim* s, int mode, float* rb, float* jac, float* mm, void* stream, const char* where) {
+  if (ready(s, where)) return -1;
+  if (!rb && !jac && !mm) return fail("%s: null output", where);
+  if (s->host) {
+    host_kinematics(&s->h_model, &s->h_links, s->state, s->N, s->nv, mode, rb, jac, mm, s->pool);
+    return 0;
+  }
+  hipError_t e = launch_kinematics(s->d_model, s->d_links, s->state, s->N, s->nv, mode, rb, jac, mm,
                                    (hipStream_t)stream);
-  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_rigid_body");
+  return e == hipSuccess ? 0 : hip_fail(e, where);
+}
+int gs_sim_refresh_rigid_body(gs_sim* s, float* out, void* stream) {
+  return kinematics(s, 1, out, nullptr, nullptr, stream, "gs_sim_refresh_rigid_body");
 }
 int gs_sim_refresh_jacobian(gs_sim* s, float* out, void* stream) {
-  if (ready(s, "gs_sim_refresh_jacobian")) return -1;
-  if (!out) return fail("gs_sim_refresh_jacobian: null output");
-  hipError_t e = launch_kinematics(s->d_model, s->d_links, s->state, s->N, s->nv, 2, nullptr, out, nullptr,
-                                   (hipStream_t)stream);
-  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_jacobian");
+  return kinematics(s, 2, nullptr, out, nullptr, stream, "gs_sim_refresh_jacobian");
 }
 int gs_sim_refresh_mass_matrix(gs_sim* s, float* out, void* stream) {
-  if (ready(s, "gs_sim_refresh_mass_matrix")) return -1;
-  if (!out) return fail("gs_sim_refresh_mass_matrix: null output");
-  hipError_t e = launch_kinematics(s->d_model, s->d_links, s->state, s->N, s->nv, 4, nullptr, nullptr, out,
-                                   (hipStream_t)stream);
-  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_mass_matrix");
+  return kinematics(s, 4, nullptr, nullptr, out, stream, "gs_sim_refresh_mass_matrix");
 }
 int gs_sim_set_root(gs_sim* s, const float* src, const int32_t* idx, int n_idx, void* stream) {
   if (ready(s, "gs_sim_set_root")) return -1;
+  if (s->host) {
+    host_set_root(s->state, s->N, &s->h_model.root_com[0], src, idx, idx ? n_idx : s->N);
+    return 0;
+  }
   hipError_t e = launch_set_root(s->state, s->N, s->nd, &s->d_model->root_com[0], src, idx, n_idx,
                                  (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_set_root");
 }
 int gs_sim_set_dof(gs_sim* s, const float* src, const int32_t* idx, int n_idx, void* stream) {
   if (ready(s, "gs_sim_set_dof")) return -1;
+  if (s->host) {
+    host_set_dof(s->state, s->N, s->nd, src, idx, idx ? n_idx : s->N);
+    return 0;
+  }
   hipError_t e = launch_set_dof(s->state, s->N, s->nd, src, idx, n_idx, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_set_dof");
 }
@@ -481,6 +586,7 @@ int gs_sim_set_force_sensors(gs_sim* s, int n, const int32_t* bodies) {
     h.sens_of_body[b] = i;
   }
   h.nsens = n;
+  if (s->host) return 0;
   hipError_t e = hipSetDevice(s->device);
   if (e == hipSuccess) e = hipMemcpy(s->d_model, &h, sizeof(DevModel), hipMemcpyHostToDevice);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_set_force_sensors hipMemcpy");
@@ -497,6 +603,10 @@ int gs_sim_refresh_force_sensor(gs_sim* s, float* out, void* stream) {
   if (ready(s, "gs_sim_refresh_force_sensor")) return -1;
   if (s->h_model.nsens == 0) return 0;
   if (!s->sens) return fail("gs_sim_refresh_force_sensor: sensors not bound");
+  if (s->host) {
+    host_soa_to_aos(s->sens, s->N, s->h_model.nsens, 6, out, s->pool);
+    return 0;
+  }
   hipError_t e = launch_refresh_sensor(s->sens, s->N, s->h_model.nsens, out, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_refresh_force_sensor");
 }
@@ -504,6 +614,10 @@ int gs_sim_refresh_force_sensor(gs_sim* s, float* out, void* stream) {
 int gs_debug_terrain_query(gs_sim* s, const float* centres, const float* radii, int n, float* out, void* stream) {
   if (!s || !s->dp.has_terrain) return fail("gs_debug_terrain_query: no terrain mesh");
   if (n < 0 || (n > 0 && (!centres || !radii || !out))) return fail("gs_debug_terrain_query: bad buffers");
+  if (s->host) {
+    host_terrain_query(s->dp, centres, radii, n, out);
+    return 0;
+  }
   hipError_t e = launch_terrain_query(s->dp, centres, radii, n, out, (hipStream_t)stream);
   return e == hipSuccess ? 0 : hip_fail(e, "gs_debug_terrain_query");
 }
@@ -516,6 +630,7 @@ int gs_sim_enable_timing(gs_sim* s, int enable) {
   return 0;
 }
 float gs_sim_last_kernel_ms(gs_sim* s) {
+  if (s && s->host) return s->timing ? (float)s->host_ms : -1.f;
   if (!s || !s->timed) return -1.f;
   float ms = -1.f;
   if (hipEventSynchronize(s->ev1) != hipSuccess) return -1.f;

@@ -126,3 +126,27 @@ hipError_t launch_set_root(float* state, int N, int nd, const float* com0, const
                            int n_idx, hipStream_t s);
 hipError_t launch_set_dof(float* state, int N, int nd, const float* src, const int* idx, int n_idx,
                           hipStream_t s);
+
+// ---------------------------------------------------------------- host backend (gs_host.hip)
+// The sim_device=cpu pipeline: the same solver on host buffers, envs spread over a thread pool.
+struct HostPool;
+HostPool* host_pool_create(int threads);  // threads >= 1 (the calling thread included)
+void host_pool_destroy(HostPool* p);
+int host_pool_threads(const HostPool* p);
+typedef void (*host_sim_fn)(const DevModel*, const DevParams&, const SimBuffers&, const float* tau, HostPool*);
+typedef void (*host_pd_fn)(const DevModel*, const DevParams&, const SimBuffers&, const PdDev&, HostPool*);
+struct HostTopoEntry {
+  const char* sig;
+  host_sim_fn sim;
+  host_pd_fn pd;
+};
+extern HostTopoEntry g_host_topologies[];
+extern const int g_num_host_topologies;
+void host_refresh_root(const float* st, int N, const float* com0, float* out, HostPool* pool);
+void host_refresh_dof(const float* st, int N, int nd, float* out, HostPool* pool);
+void host_soa_to_aos(const float* soa, int N, int n, int comp, float* out, HostPool* pool);
+void host_set_root(float* st, int N, const float* com0, const float* src, const int* idx, int n);
+void host_set_dof(float* st, int N, int nd, const float* src, const int* idx, int n);
+void host_kinematics(const DevModel* M, const DevLinks* L, const float* st, int N, int nv, int mode, float* rb,
+                     float* jac, float* mm, HostPool* pool);
+void host_terrain_query(const DevParams& P, const float* c, const float* r, int n, float* out);

@@ -24,766 +24,10 @@
 //   (pos iterations with depenetration bias, then velocity iterations without)
 //   -> velocity limits -> semi-implicit integration with the position-phase
 //   velocity; the velocity-phase velocity is kept as state.
-#include "gs_internal.h"
-#include "gs_topologies.h"
-#include "gs_math.h"
+
+#include "gs_solver.h"
 
 namespace {
-
-// k-th node of the support path of a contact on the body moved by generalized dof
-// `leaf`: the leaf itself, then its ancestors towards the root.
-template <class T>
-__device__ __forceinline__ constexpr int supp_node(int leaf, int si) {
-  return si == 0 ? leaf : T::anc[leaf][si > 0 ? si - 1 : 0];
-}
-
-// body kk is b or one of its ancestors
-template <class T>
-__device__ __forceinline__ constexpr bool body_on_path(int kk, int b) {
-  for (int x = b; x > 0; x = T::parent[x])
-    if (x == kk) return true;
-  return kk == 0;
-}
-
-// Lanes (= envs) per workgroup: a full wave unless the topology's LDS rows would exceed the
-// 160 KB of LDS per CU (nv_ant: 25 candidates -> 748 slots -> 32 lanes).
-// TERR kernels (trimesh terrain) keep each active candidate's contact normal in 3 more slots.
-template <class T, bool TERR = false>
-struct LaneCfg {
-  static constexpr int SLOTS = T::NSLOT + (TERR ? 3 * T::NC : 0);
-  static constexpr int FIT = (SLOTS * 64 * 4 <= 160 * 1024) ? 64 : (SLOTS * 32 * 4 <= 160 * 1024) ? 32
-                           : (SLOTS * 16 * 4 <= 160 * 1024) ? 16 : 8;
-  // Below 16 lanes the rows of two workgroups no longer share a CU, and halving again measured
-  // ~10 % faster for Hound (2745 slots; r01n, profiles/r01n_experiments_other_configs.txt) while
-  // Ant (32 lanes) got slower at 4: only the LDS-starved widths go narrower.  The mesh-contact
-  // (TERR) variant is bound by its terrain queries, which gain from spreading the envs over more
-  // CUs: 16 lanes measured ~8 % faster than 64 for ANYmal on the trimesh map.
-#ifndef GS_NARROW_LANES
-#define GS_NARROW_LANES 4
-#endif
-#ifndef GS_TERR_LANES
-#define GS_TERR_LANES 16
-#endif
-  static constexpr int LB = FIT == 8 ? GS_NARROW_LANES : (TERR && FIT > GS_TERR_LANES) ? GS_TERR_LANES : FIT;
-  static_assert(SLOTS * LB * 4 <= 160 * 1024, "contact rows exceed the LDS of a CU even at 8 lanes");
-};
-
-// World-frame force of candidate c's impulses (normal from LDS, tangents rebuilt), / h.
-template <class T, int LB>
-__device__ __forceinline__ void contact_force_world(const float* lds, int c, const float* lam, float inv_h,
-                                                    float* f) {
-  const float* nsl = lds + (T::NSLOT + 3 * c) * LB;
-  const float n[3] = {nsl[0], nsl[LB], nsl[2 * LB]};
-  float t1[3], t2[3];
-  gs_terrain::tangents(n, t1, t2);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) f[k] = (lam[0] * n[k] + lam[1] * t1[k] + lam[2] * t2[k]) * inv_h;
-}
-
-// Register-resident env state.
-template <class T>
-struct EnvState {
-  float p[3], quat[4], vo[3], w[3];
-  float q[T::ND > 0 ? T::ND : 1], qd[T::ND > 0 ? T::ND : 1];
-};
-
-template <class T>
-__device__ __forceinline__ void load_state(const float* __restrict__ st, int N, int e, EnvState<T>& s) {
-#pragma unroll
-  for (int k = 0; k < 3; ++k) s.p[k] = st[k * N + e];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) s.quat[k] = st[(3 + k) * N + e];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) s.vo[k] = st[(7 + k) * N + e];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) s.w[k] = st[(10 + k) * N + e];
-#pragma unroll
-  for (int j = 0; j < T::ND; ++j) s.q[j] = st[(13 + j) * N + e];
-#pragma unroll
-  for (int j = 0; j < T::ND; ++j) s.qd[j] = st[(13 + T::ND + j) * N + e];
-}
-template <class T>
-__device__ __forceinline__ void store_state(float* __restrict__ st, int N, int e, const EnvState<T>& s) {
-#pragma unroll
-  for (int k = 0; k < 3; ++k) st[k * N + e] = s.p[k];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) st[(3 + k) * N + e] = s.quat[k];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) st[(7 + k) * N + e] = s.vo[k];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) st[(10 + k) * N + e] = s.w[k];
-#pragma unroll
-  for (int j = 0; j < T::ND; ++j) st[(13 + j) * N + e] = s.q[j];
-#pragma unroll
-  for (int j = 0; j < T::ND; ++j) st[(13 + T::ND + j) * N + e] = s.qd[j];
-}
-
-// One substep for one env.  `lds` points at this lane's column of the
-// workgroup's [NSLOT][64] contact-row staging area.
-//
-// Register budget: the tree is walked ONCE in DFS order.  Kinematics,
-// velocities, RNEA forces and composite inertias are accumulated post-order,
-// so only the bodies on the current root->leaf path are live at any time; a
-// body's bias force and its mass-matrix row are emitted the moment its subtree
-// is complete (T::subend).  Contact Jacobian rows are written to LDS during the
-// same walk (they need the path's motion subspaces) and turned into scaled
-// Z rows after the factorisation.
-template <class T, bool TERR>
-__device__ __forceinline__ void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvState<T>& s,
-                                        const float* tau, const float* __restrict__ mu_g, int N, int e, float* lds,
-                                        float* __restrict__ cf_soa, bool collect, float* __restrict__ sens_soa) {
-  constexpr int NB = T::NB, NV = T::NV, NB6 = T::NBASE, NC = T::NC, ND = T::ND;
-  constexpr int LB = LaneCfg<T, TERR>::LB;
-  constexpr int MS = T::MAXDEP + 1;
-  // Keep the model pointer opaque per substep: the constants are re-read with
-  // scalar loads (K$ hits) instead of being hoisted out of the substep loop
-  // into hundreds of SGPRs.
-  uintptr_t mp = reinterpret_cast<uintptr_t>(Min);
-  asm volatile("" : "+s"(mp));
-  const DevModel* __restrict__ M = reinterpret_cast<const DevModel*>(mp);
-  const float h = P.h;
-
-  float nu[NV];
-  if (NB6) {
-    nu[0] = s.w[0]; nu[1] = s.w[1]; nu[2] = s.w[2];
-    nu[3] = s.vo[0]; nu[4] = s.vo[1]; nu[5] = s.vo[2];
-  }
-#pragma unroll
-  for (int j = 0; j < T::ND; ++j) nu[NB6 + j] = s.qd[j];
-
-  float R[NB][9], X[NB][3], S[NB][6], V[NB][6], A[NB][6], Fc[NB][6];
-  SpI Ic[NB];
-  float Mm[NV][NV], bias[NV];
-  bool act[NC];
-  float sep[NC], cmu[NC];
-
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    // ---- kinematics of body i (positions relative to the root origin)
-    if (i == 0) {
-      float qn[4];
-      const float inv = rsqrtf(s.quat[0] * s.quat[0] + s.quat[1] * s.quat[1] + s.quat[2] * s.quat[2] +
-                               s.quat[3] * s.quat[3]);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) qn[k] = s.quat[k] * inv;
-      quat_to_mat(qn, R[0]);
-      X[0][0] = X[0][1] = X[0][2] = 0.f;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) V[0][k] = NB6 ? nu[k] : 0.f;
-      A[0][0] = A[0][1] = A[0][2] = 0.f;
-      A[0][3] = -P.g[0]; A[0][4] = -P.g[1]; A[0][5] = -P.g[2];
-    } else {
-      const int pa = T::parent[i];
-      float RJ[9], t[3], aw[3];
-      mat3mul(R[pa], M->jR[i], RJ);
-      mat3vec(R[pa], M->jt[i], t);
-      X[i][0] = X[pa][0] + t[0]; X[i][1] = X[pa][1] + t[1]; X[i][2] = X[pa][2] + t[2];
-      mat3vec(RJ, M->jaxis[i], aw);
-      const float qj = s.q[T::bdof[i]];
-      if (T::jkind[i] == 1) {
-        float sn, cs;
-        sincosf(qj, &sn, &cs);
-        const float* a = M->jaxis[i];
-        const float C = 1.f - cs;
-        float Rq[9];
-        Rq[0] = cs + a[0] * a[0] * C;        Rq[1] = a[0] * a[1] * C - a[2] * sn; Rq[2] = a[0] * a[2] * C + a[1] * sn;
-        Rq[3] = a[1] * a[0] * C + a[2] * sn; Rq[4] = cs + a[1] * a[1] * C;        Rq[5] = a[1] * a[2] * C - a[0] * sn;
-        Rq[6] = a[2] * a[0] * C - a[1] * sn; Rq[7] = a[2] * a[1] * C + a[0] * sn; Rq[8] = cs + a[2] * a[2] * C;
-        mat3mul(RJ, Rq, R[i]);
-        S[i][0] = aw[0]; S[i][1] = aw[1]; S[i][2] = aw[2];
-        cross3(X[i], aw, &S[i][3]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) R[i][k] = RJ[k];
-        X[i][0] += aw[0] * qj; X[i][1] += aw[1] * qj; X[i][2] += aw[2] * qj;
-        S[i][0] = S[i][1] = S[i][2] = 0.f;
-        S[i][3] = aw[0]; S[i][4] = aw[1]; S[i][5] = aw[2];
-      }
-      const float qd = nu[NB6 + T::bdof[i]];
-      float c6[6];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) V[i][k] = V[pa][k] + S[i][k] * qd;
-      crm(V[i], S[i], c6);
-#pragma unroll
-      for (int k = 0; k < 6; ++k) A[i][k] = A[pa][k] + c6[k] * qd;
-    }
-
-    // ---- spatial inertia of body i at O; RNEA force
-    {
-      float c[3];
-      mat3vec(R[i], M->com[i], c);
-      c[0] += X[i][0]; c[1] += X[i][1]; c[2] += X[i][2];
-      const float* Il = M->inertia[i];  // xx yy zz xy xz yz
-      const float* Rm = R[i];
-      float Am[9];
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        Am[3 * r + 0] = Rm[3 * r] * Il[0] + Rm[3 * r + 1] * Il[3] + Rm[3 * r + 2] * Il[4];
-        Am[3 * r + 1] = Rm[3 * r] * Il[3] + Rm[3 * r + 1] * Il[1] + Rm[3 * r + 2] * Il[5];
-        Am[3 * r + 2] = Rm[3 * r] * Il[4] + Rm[3 * r + 1] * Il[5] + Rm[3 * r + 2] * Il[2];
-      }
-      const float m = M->mass[i];
-      const float cc = c[0] * c[0] + c[1] * c[1] + c[2] * c[2];
-      SpI& I = Ic[i];
-      I.m = m;
-      I.h[0] = m * c[0]; I.h[1] = m * c[1]; I.h[2] = m * c[2];
-      I.I[0] = Am[0] * Rm[0] + Am[1] * Rm[1] + Am[2] * Rm[2] + m * (cc - c[0] * c[0]);
-      I.I[1] = Am[3] * Rm[3] + Am[4] * Rm[4] + Am[5] * Rm[5] + m * (cc - c[1] * c[1]);
-      I.I[2] = Am[6] * Rm[6] + Am[7] * Rm[7] + Am[8] * Rm[8] + m * (cc - c[2] * c[2]);
-      I.I[3] = Am[0] * Rm[3] + Am[1] * Rm[4] + Am[2] * Rm[5] - m * c[0] * c[1];
-      I.I[4] = Am[0] * Rm[6] + Am[1] * Rm[7] + Am[2] * Rm[8] - m * c[0] * c[2];
-      I.I[5] = Am[3] * Rm[6] + Am[4] * Rm[7] + Am[5] * Rm[8] - m * c[1] * c[2];
-      float ia[6], iv[6], x6[6];
-      spi_mul(I, A[i], ia);
-      spi_mul(I, V[i], iv);
-      crf(V[i], iv, x6);
-#pragma unroll
-      for (int k = 0; k < 6; ++k) Fc[i][k] = ia[k] + x6[k];
-    }
-
-    // ---- contact candidates on body i: activity test + Jacobian rows -> LDS
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      if (T::cbody[c] == i) {
-        float x[3];
-        mat3vec(R[i], M->cpoint[c], x);
-        x[0] += X[i][0]; x[1] += X[i][1]; x[2] += X[i][2];
-        const float r = M->cradius[c];
-        if constexpr (TERR) {
-          // deepest of the ground plane and the terrain mesh (gs_terrain.h); the contact frame is
-          // (n, t1, t2) with n stored in LDS for the force outputs
-          const float cw[3] = {s.p[0] + x[0], s.p[1] + x[1], s.p[2] + x[2]};
-          float dist = P.has_ground ? cw[2] - r : 3.0e38f;
-          float nrm[3] = {0.f, 0.f, 1.f};
-          float smu = P.ground_mu;
-          float st, nt[3];
-          if (gs_terrain::sphere_contact(P.terr, cw, r, r + P.contact_offset, st, nt) && st < dist) {
-            dist = st;
-            nrm[0] = nt[0]; nrm[1] = nt[1]; nrm[2] = nt[2];
-            smu = P.terr.mu;
-          }
-          act[c] = dist < P.contact_offset;
-          sep[c] = dist - P.rest_offset;
-          cmu[c] = 0.5f * (mu_g[T::cshape[c] * N + e] + smu);
-          if (act[c]) {
-            float* nsl = lds + (T::NSLOT + 3 * c) * LB;
-            nsl[0] = nrm[0]; nsl[LB] = nrm[1]; nsl[2 * LB] = nrm[2];
-            float dir[3][3];
-            dir[0][0] = nrm[0]; dir[0][1] = nrm[1]; dir[0][2] = nrm[2];
-            gs_terrain::tangents(nrm, dir[1], dir[2]);
-            const float xc[3] = {x[0] - r * nrm[0], x[1] - r * nrm[1], x[2] - r * nrm[2]};
-            const int SUP = T::csupp[c];
-            const int leaf = T::cleaf[c];
-            float* slot = lds + T::cslot[c] * LB;
-#pragma unroll
-            for (int rr = 0; rr < 3; ++rr) {
-              const float* d = dir[rr];
-              float xd[3];  // the row's angular part: d.(w x xc) = w.(xc x d)
-              cross3(xc, d, xd);
-#pragma unroll
-              for (int si = 0; si < MS; ++si) {
-                if (si < SUP) {
-                  const int k = supp_node<T>(leaf, si);
-                  float v;
-                  if (k < NB6) {
-                    v = k < 3 ? xd[k] : d[k - 3];
-                  } else {
-                    const float* Sk = S[T::gbody[k]];
-                    v = Sk[3] * d[0] + Sk[4] * d[1] + Sk[5] * d[2] + Sk[0] * xd[0] + Sk[1] * xd[1] + Sk[2] * xd[2];
-                  }
-                  slot[(rr * SUP + si) * LB] = v;
-                }
-              }
-            }
-          }
-        } else {
-        const float dist = s.p[2] + x[2] - r;
-        act[c] = P.has_ground && (dist < P.contact_offset);
-        sep[c] = dist - P.rest_offset;
-        cmu[c] = 0.5f * (mu_g[T::cshape[c] * N + e] + P.ground_mu);
-        if (act[c]) {
-          const float xc[3] = {x[0], x[1], x[2] - r};
-          const int SUP = T::csupp[c];
-          const int leaf = T::cleaf[c];
-          float* slot = lds + T::cslot[c] * LB;
-#pragma unroll
-          for (int rr = 0; rr < 3; ++rr) {
-            const int ax = (rr == 0) ? 2 : (rr == 1 ? 0 : 1);  // normal z, tangent x, tangent y
-#pragma unroll
-            for (int si = 0; si < MS; ++si) {
-              if (si < SUP) {
-                const int k = supp_node<T>(leaf, si);
-                float v;
-                if (k < NB6) {
-                  if (k < 3) {
-                    const float m3[3][3] = {{0.f, xc[2], -xc[1]}, {-xc[2], 0.f, xc[0]}, {xc[1], -xc[0], 0.f}};
-                    v = m3[ax][k];  // d(w x xc)/dw = -[xc]x
-                  } else {
-                    v = (ax == k - 3) ? 1.f : 0.f;
-                  }
-                } else {
-                  const float* Sk = S[T::gbody[k]];
-                  float t[3];
-                  cross3(Sk, xc, t);
-                  v = Sk[3 + ax] + t[ax];
-                }
-                slot[(rr * SUP + si) * LB] = v;
-              }
-            }
-          }
-        }
-        }  // !TERR
-      }
-    }
-
-    // ---- subtrees completed at body i: bias + mass-matrix rows, then fold into the parent
-#pragma unroll
-    for (int a = NB - 1; a >= 0; --a) {
-      if (a <= i && T::subend[a] == i && (a == i || true)) {
-        bool on_path = false;
-        // a must be i or an ancestor of i (subend == i implies that)
-        on_path = true;
-        if (on_path) {
-          if (a > 0) {
-            const int ga = NB6 + T::bdof[a];
-            bias[ga] = dot6(S[a], Fc[a]);
-            float F[6];
-            spi_mul(Ic[a], S[a], F);
-            Mm[ga][ga] = dot6(S[a], F) + M->armature[T::bdof[a]];
-#pragma unroll
-            for (int k = 0; k < T::MAXDEP; ++k) {
-              if (k < T::depth[ga]) {
-                const int an = T::anc[ga][k];
-                if (an >= NB6) Mm[ga][an] = dot6(S[T::gbody[an]], F);
-                else Mm[ga][an] = F[an];
-              }
-            }
-            const int pa = T::parent[a];
-            Ic[pa].m += Ic[a].m;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) Ic[pa].h[k] += Ic[a].h[k];
-#pragma unroll
-            for (int k = 0; k < 6; ++k) Ic[pa].I[k] += Ic[a].I[k];
-#pragma unroll
-            for (int k = 0; k < 6; ++k) Fc[pa][k] += Fc[a][k];
-          } else if (NB6) {
-#pragma unroll
-            for (int k = 0; k < 6; ++k) bias[k] = Fc[0][k];
-            const SpI& I0 = Ic[0];
-            Mm[0][0] = I0.I[0]; Mm[1][1] = I0.I[1]; Mm[2][2] = I0.I[2];
-            Mm[1][0] = I0.I[3]; Mm[2][0] = I0.I[4]; Mm[2][1] = I0.I[5];
-            Mm[3][0] = 0.f;       Mm[3][1] = I0.h[2];  Mm[3][2] = -I0.h[1];
-            Mm[4][0] = -I0.h[2];  Mm[4][1] = 0.f;      Mm[4][2] = I0.h[0];
-            Mm[5][0] = I0.h[1];   Mm[5][1] = -I0.h[0]; Mm[5][2] = 0.f;
-            Mm[3][3] = I0.m; Mm[4][4] = I0.m; Mm[5][5] = I0.m;
-            Mm[4][3] = 0.f; Mm[5][3] = 0.f; Mm[5][4] = 0.f;
-          }
-        }
-      }
-    }
-  }
-
-  // ---------------- joint-limit activity (substep start): one unilateral row per dof within
-  // limit_margin of a limit; sign +1 pushes q up (lower limit), -1 down (upper limit)
-  float lsgn[ND > 0 ? ND : 1], lsep[ND > 0 ? ND : 1];
-#pragma unroll
-  for (int j = 0; j < ND; ++j) {
-    lsgn[j] = 0.f;
-    lsep[j] = 0.f;
-    if (P.any_limits && M->has_lim[j]) {
-      const float lo = s.q[j] - M->lower[j], hi = M->upper[j] - s.q[j];
-      if (lo < P.limit_margin || hi < P.limit_margin) {
-        lsgn[j] = lo <= hi ? 1.f : -1.f;
-        lsep[j] = lo <= hi ? lo : hi;
-      }
-    }
-  }
-
-  // ---------------- L^T D L (Featherstone, tree-sparse, in place)
-#pragma unroll
-  for (int kk = 0; kk < NV; ++kk) {
-    const int k = NV - 1 - kk;
-    const float dinv = 1.f / Mm[k][k];
-#pragma unroll
-    for (int ai = 0; ai < T::MAXDEP; ++ai) {
-      if (ai < T::depth[k]) {
-        const int i = T::anc[k][ai];
-        const float a = Mm[k][i] * dinv;
-#pragma unroll
-        for (int aj = ai; aj < T::MAXDEP; ++aj) {
-          if (aj < T::depth[k]) {
-            const int j = T::anc[k][aj];
-            Mm[i][j] -= a * Mm[k][j];
-          }
-        }
-        Mm[k][i] = a;
-      }
-    }
-  }
-  float sD[NV];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) sD[k] = rsqrtf(Mm[k][k]);
-
-  // ---------------- free velocity: nu_f = nu + h M^-1 (tau - c) (+ mixed-frame term)
-  float nuf[NV];
-  {
-    float r[NV];
-    if (NB6) {
-#pragma unroll
-      for (int k = 0; k < 6; ++k) r[k] = -bias[k];
-    }
-#pragma unroll
-    for (int j = 0; j < T::ND; ++j) {
-      float t = tau[j];
-      const float e = M->effort[j];
-      if (e > 0.f) t = clampf(t, -e, e);
-      r[NB6 + j] = t - bias[NB6 + j];
-    }
-#pragma unroll
-    for (int kk = 0; kk < NV; ++kk) {
-      const int k = NV - 1 - kk;
-#pragma unroll
-      for (int ai = 0; ai < T::MAXDEP; ++ai)
-        if (ai < T::depth[k]) r[T::anc[k][ai]] -= Mm[k][T::anc[k][ai]] * r[k];
-    }
-#pragma unroll
-    for (int k = 0; k < NV; ++k) r[k] *= sD[k] * sD[k];
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-#pragma unroll
-      for (int ai = 0; ai < T::MAXDEP; ++ai)
-        if (ai < T::depth[k]) r[k] -= Mm[k][T::anc[k][ai]] * r[T::anc[k][ai]];
-    }
-#pragma unroll
-    for (int k = 0; k < NV; ++k) nuf[k] = nu[k] + h * r[k];
-    if (NB6) {
-      float wxp[3];
-      cross3(&nu[0], &nu[3], wxp);
-      nuf[3] += h * wxp[0]; nuf[4] += h * wxp[1]; nuf[5] += h * wxp[2];
-    }
-  }
-
-  // ---------------- contact rows: J (LDS) -> c = J nu_f, scaled Z = (L^-T J^T) D^-1/2, 1/diag
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    if (act[c]) {
-      const int SUP = T::csupp[c];
-      const int leaf = T::cleaf[c];
-      float* slot = lds + T::cslot[c] * LB;
-#pragma unroll
-      for (int rr = 0; rr < 3; ++rr) {
-        float jv[MS];
-        float cj = 0.f;
-#pragma unroll
-        for (int si = 0; si < MS; ++si) {
-          if (si < SUP) {
-            jv[si] = slot[(rr * SUP + si) * LB];
-            cj += jv[si] * nuf[supp_node<T>(leaf, si)];
-          }
-        }
-#pragma unroll
-        for (int si = 0; si < MS; ++si) {
-          if (si < SUP) {
-            const int k = supp_node<T>(leaf, si);
-#pragma unroll
-            for (int sj = si + 1; sj < MS; ++sj)
-              if (sj < SUP) jv[sj] -= Mm[k][supp_node<T>(leaf, sj)] * jv[si];
-          }
-        }
-        float d = 0.f;
-#pragma unroll
-        for (int si = 0; si < MS; ++si) {
-          if (si < SUP) {
-            const float zh = jv[si] * sD[supp_node<T>(leaf, si)];
-            d += zh * zh;
-            slot[(rr * SUP + si) * LB] = zh;
-          }
-        }
-        slot[(3 * SUP + rr) * LB] = cj;
-        slot[(3 * SUP + 3 + rr) * LB] = 1.f / d;
-      }
-    }
-  }
-
-  // ---------------- joint-limit rows: J = sign * e_dof -> c, scaled Z, 1/diag (same elimination)
-#pragma unroll
-  for (int j = 0; j < ND; ++j) {
-    if (lsgn[j] != 0.f) {
-      const int SUP = T::lsupp[j];
-      const int leaf = T::lleaf[j];
-      float* slot = lds + T::lslot[j] * LB;
-      float jv[MS];
-#pragma unroll
-      for (int si = 0; si < MS; ++si) jv[si] = si == 0 ? lsgn[j] : 0.f;
-#pragma unroll
-      for (int si = 0; si < MS; ++si) {
-        if (si < SUP) {
-          const int k = supp_node<T>(leaf, si);
-#pragma unroll
-          for (int sj = si + 1; sj < MS; ++sj)
-            if (sj < SUP) jv[sj] -= Mm[k][supp_node<T>(leaf, sj)] * jv[si];
-        }
-      }
-      float d = 0.f;
-#pragma unroll
-      for (int si = 0; si < MS; ++si) {
-        if (si < SUP) {
-          const float zh = jv[si] * sD[supp_node<T>(leaf, si)];
-          d += zh * zh;
-          slot[si * LB] = zh;
-        }
-      }
-      slot[SUP * LB] = lsgn[j] * nuf[leaf];
-      slot[(SUP + 1) * LB] = 1.f / d;
-    }
-  }
-
-  // ---------------- projected Gauss-Seidel in w-space (joint limits, then contacts)
-  float wt[NV], lam[NC][3], wpos[NV], laml[ND > 0 ? ND : 1];
-#pragma unroll
-  for (int j = 0; j < ND; ++j) laml[j] = 0.f;
-#pragma unroll
-  for (int k = 0; k < NV; ++k) wt[k] = 0.f;
-#pragma unroll
-  for (int c = 0; c < NC; ++c) lam[c][0] = lam[c][1] = lam[c][2] = 0.f;
-  const float inv_h = 1.f / h;
-  const int iters = P.pos_iters + P.vel_iters;
-  for (int it = 0; it < iters; ++it) {
-    const bool pos_phase = it < P.pos_iters;
-#pragma unroll
-    for (int j = 0; j < ND; ++j) {
-      if (lsgn[j] != 0.f) {
-        const int SUP = T::lsupp[j];
-        const int leaf = T::lleaf[j];
-        const float* slot = lds + T::lslot[j] * LB;
-        const float sc = lsep[j];
-        float target = -sc * inv_h;
-        if (sc < 0.f) target = pos_phase ? fminf(target, P.max_depen_vel) : 0.f;
-        float z[MS];
-        float u = slot[SUP * LB];
-#pragma unroll
-        for (int si = 0; si < MS; ++si) {
-          if (si < SUP) {
-            z[si] = slot[si * LB];
-            u += z[si] * wt[supp_node<T>(leaf, si)];
-          }
-        }
-        const float nl = fmaxf(laml[j] + (target - u) * slot[(SUP + 1) * LB], 0.f);
-        const float dl = nl - laml[j];
-        laml[j] = nl;
-#pragma unroll
-        for (int si = 0; si < MS; ++si)
-          if (si < SUP) wt[supp_node<T>(leaf, si)] += z[si] * dl;
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      if (act[c]) {
-        const int SUP = T::csupp[c];
-        const int leaf = T::cleaf[c];
-        const float* slot = lds + T::cslot[c] * LB;
-        const float sc = sep[c];
-        float target = -sc * inv_h;
-        if (sc < 0.f) target = pos_phase ? fminf(target, P.max_depen_vel) : 0.f;
-#pragma unroll
-        for (int rr = 0; rr < 3; ++rr) {
-          float z[MS];
-          float u = slot[(3 * SUP + rr) * LB];
-#pragma unroll
-          for (int si = 0; si < MS; ++si) {
-            if (si < SUP) {
-              z[si] = slot[(rr * SUP + si) * LB];
-              u += z[si] * wt[supp_node<T>(leaf, si)];
-            }
-          }
-          const float dinv = slot[(3 * SUP + 3 + rr) * LB];
-          float nl;
-          if (rr == 0) {
-            nl = fmaxf(lam[c][0] + (target - u) * dinv, 0.f);
-          } else {
-            const float lim = cmu[c] * lam[c][0];
-            nl = clampf(lam[c][rr] - u * dinv, -lim, lim);
-          }
-          const float dl = nl - lam[c][rr];
-          lam[c][rr] = nl;
-#pragma unroll
-          for (int si = 0; si < MS; ++si)
-            if (si < SUP) wt[supp_node<T>(leaf, si)] += z[si] * dl;
-        }
-      }
-    }
-    if (it == P.pos_iters - 1) {
-#pragma unroll
-      for (int k = 0; k < NV; ++k) wpos[k] = wt[k];
-    }
-  }
-  if (P.pos_iters <= 0) {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) wpos[k] = wt[k];
-  }
-  // dnu = L^-1 D^-1/2 w  for the velocity-phase (state) and position-phase (integration) solutions
-  float nun[NV], nupos[NV];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    float v = wt[k] * sD[k], vp = wpos[k] * sD[k];
-#pragma unroll
-    for (int ai = 0; ai < T::MAXDEP; ++ai) {
-      if (ai < T::depth[k]) {
-        const float l = Mm[k][T::anc[k][ai]];
-        v -= l * nun[T::anc[k][ai]];
-        vp -= l * nupos[T::anc[k][ai]];
-      }
-    }
-    nun[k] = v;
-    nupos[k] = vp;
-  }
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    nun[k] += nuf[k];
-    nupos[k] += nuf[k];
-  }
-
-  // ---------------- joint velocity limits
-#pragma unroll
-  for (int j = 0; j < T::ND; ++j) {
-    const float vm = M->vmax[j];
-    if (vm > 0.f) {
-      nun[NB6 + j] = clampf(nun[NB6 + j], -vm, vm);
-      nupos[NB6 + j] = clampf(nupos[NB6 + j], -vm, vm);
-    }
-  }
-
-  // ---------------- integrate positions with nu_pos; keep nu_new
-  if (NB6) {
-    s.p[0] += h * nupos[3]; s.p[1] += h * nupos[4]; s.p[2] += h * nupos[5];
-    const float wx = nupos[0], wy = nupos[1], wz = nupos[2];
-    float x = s.quat[0], y = s.quat[1], z = s.quat[2], w = s.quat[3];
-    const float hh = 0.5f * h;
-    const float dx = hh * (w * wx + wy * z - wz * y);
-    const float dy = hh * (w * wy + wz * x - wx * z);
-    const float dz = hh * (w * wz + wx * y - wy * x);
-    const float dw = -hh * (wx * x + wy * y + wz * z);
-    x += dx; y += dy; z += dz; w += dw;
-    const float n = rsqrtf(x * x + y * y + z * z + w * w);
-    s.quat[0] = x * n; s.quat[1] = y * n; s.quat[2] = z * n; s.quat[3] = w * n;
-    s.w[0] = nun[0]; s.w[1] = nun[1]; s.w[2] = nun[2];
-    s.vo[0] = nun[3]; s.vo[1] = nun[4]; s.vo[2] = nun[5];
-  }
-#pragma unroll
-  for (int j = 0; j < T::ND; ++j) {
-    s.q[j] += h * nupos[NB6 + j];
-    s.qd[j] = nun[NB6 + j];
-  }
-  if (collect) {
-    // net contact force per reported link of this (collecting) substep, SoA [3*nr][N]
-    // (links = bodies unless fixed-joint links are kept: then a candidate adds to its own link)
-#pragma unroll
-    for (int b = 0; b < T::NR; ++b) {
-      float f0 = 0.f, f1 = 0.f, f2 = 0.f;
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        if (T::clink[c] == b) {
-          if constexpr (TERR) {
-            if (act[c]) {
-              float fw[3];
-              contact_force_world<T, LB>(lds, c, lam[c], inv_h, fw);
-              f0 += fw[0]; f1 += fw[1]; f2 += fw[2];
-            }
-          } else {
-            f0 += lam[c][1] * inv_h;
-            f1 += lam[c][2] * inv_h;
-            f2 += lam[c][0] * inv_h;
-          }
-        }
-      }
-      cf_soa[(3 * b + 0) * N + e] = f0;
-      cf_soa[(3 * b + 1) * N + e] = f1;
-      cf_soa[(3 * b + 2) * N + e] = f2;
-    }
-  }
-  if (sens_soa && M->nsens > 0) {
-    // force sensors on leaf bodies: the wrench through the parent joint,
-    //   f_joint = I_b a_b + v_b x* I_b v_b - f_contact   (a_b with the gravity offset, RNEA form)
-    // with a_b = A_b (velocity products + gravity) + base acceleration + sum_path S_k qdd_k, where
-    // qdd = (nu_new - nu)/h and the base's spatial acceleration is (dw/h, dpdot/h - w x pdot).
-    // Fc[b] / Ic[b] of a leaf still hold the body's own RNEA force / inertia.
-    float ab[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) ab[k] = 0.f;
-    if (NB6) {
-      float wxp[3];
-      cross3(&nu[0], &nu[3], wxp);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        ab[k] = (nun[k] - nu[k]) * inv_h;
-        ab[3 + k] = (nun[3 + k] - nu[3 + k]) * inv_h - wxp[k];
-      }
-    }
-#pragma unroll
-    for (int b = 1; b < NB; ++b) {
-      const int si = M->sens_of_body[b];
-      if (si >= 0) {
-        float a[6];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) a[k] = ab[k];
-#pragma unroll
-        for (int kk = 0; kk < NB; ++kk) {  // path root -> b (compile-time ancestor test)
-            if (kk > 0 && body_on_path<T>(kk, b)) {
-            const int g = NB6 + T::bdof[kk];
-            const float qdd = (nun[g] - nu[g]) * inv_h;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) a[k] += S[kk][k] * qdd;
-          }
-        }
-        float ia[6], f[6];
-        spi_mul(Ic[b], a, ia);
-#pragma unroll
-        for (int k = 0; k < 6; ++k) f[k] = Fc[b][k] + ia[k];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          if (T::cbody[c] == b && act[c]) {
-            float x[3];
-            mat3vec(R[b], M->cpoint[c], x);
-            float fc[3];
-            if constexpr (TERR) {
-              const float* nsl = lds + (T::NSLOT + 3 * c) * LB;
-              const float r = M->cradius[c];
-              x[0] += X[b][0] - r * nsl[0]; x[1] += X[b][1] - r * nsl[LB]; x[2] += X[b][2] - r * nsl[2 * LB];
-              contact_force_world<T, LB>(lds, c, lam[c], inv_h, fc);
-            } else {
-              x[0] += X[b][0]; x[1] += X[b][1]; x[2] += X[b][2] - M->cradius[c];
-              fc[0] = lam[c][1] * inv_h; fc[1] = lam[c][2] * inv_h; fc[2] = lam[c][0] * inv_h;
-            }
-            float n[3];
-            cross3(x, fc, n);
-#pragma unroll
-            for (int k = 0; k < 3; ++k) { f[k] -= n[k]; f[3 + k] -= fc[k]; }
-          }
-        }
-        // torque about the body origin, then body axes
-        float xf[3], tq[3];
-        cross3(X[b], &f[3], xf);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) tq[k] = f[k] - xf[k];
-        const float* Rb = R[b];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          sens_soa[(6 * si + k) * N + e] = Rb[k] * f[3] + Rb[3 + k] * f[4] + Rb[6 + k] * f[5];
-          sens_soa[(6 * si + 3 + k) * N + e] = Rb[k] * tq[0] + Rb[3 + k] * tq[1] + Rb[6 + k] * tq[2];
-        }
-      }
-    }
-  }
-}
-
-template <class T>
-__device__ __forceinline__ void com_velocity(const DevModel* __restrict__ M, const EnvState<T>& s, float* v) {
-  float R[9], c[3], wc[3];
-  quat_to_mat(s.quat, R);
-  mat3vec(R, M->root_com, c);
-  cross3(s.w, c, wc);
-  v[0] = s.vo[0] + wc[0]; v[1] = s.vo[1] + wc[1]; v[2] = s.vo[2] + wc[2];
-}
 
 // ---------------------------------------------------------------- kernels
 template <class T, bool TERR>
@@ -793,18 +37,7 @@ __global__ __launch_bounds__((LaneCfg<T, TERR>::LB), 1) void k_simulate(const De
   __shared__ float lds[LaneCfg<T, TERR>::SLOTS * LB];
   const int e = blockIdx.x * LB + threadIdx.x;
   if (e >= B.N) return;
-  const int N = B.N;
-  EnvState<T> s;
-  load_state<T>(B.state, N, e, s);
-  float tau[T::ND > 0 ? T::ND : 1];
-#pragma unroll
-  for (int j = 0; j < T::ND; ++j) tau[j] = tau_aos ? tau_aos[(size_t)e * T::ND + j] : 0.f;
-  for (int sstep = 0; sstep < P.substeps; ++sstep) {
-    const bool last = (sstep == P.substeps - 1) && P.collect;
-    substep<T, TERR>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last,
-                     sstep == P.substeps - 1 ? B.sens : nullptr);
-  }
-  store_state<T>(B.state, N, e, s);
+  simulate_env<T, TERR, LB>(M, P, B, tau_aos, e, lds + threadIdx.x);
 }
 
 template <class T, bool TERR>
@@ -814,60 +47,7 @@ __global__ __launch_bounds__((LaneCfg<T, TERR>::LB), 1) void k_pd_step(const Dev
   __shared__ float lds[LaneCfg<T, TERR>::SLOTS * LB];
   const int e = blockIdx.x * LB + threadIdx.x;
   if (e >= B.N) return;
-  const int N = B.N;
-  constexpr int ND = T::ND;
-  EnvState<T> s;
-  load_state<T>(B.state, N, e, s);
-  float tau[ND];
-  // one call site for the substep so it is inlined once
-  const int sub = P.substeps;
-  const int n_pd = A.decimation * sub;
-  const int total = (A.decimation + A.extra) * sub;
-  for (int it = 0; it < total; ++it) {
-    if (it < n_pd && (it % sub) == 0) {
-      // the first PD evaluation reads the dof tensor the task holds (refreshed after the previous
-      // step's decimation loop, or written by reset_idx): anymal_terrain.py:444
-      const bool first = it == 0;
-#pragma unroll
-      for (int j = 0; j < ND; ++j) {
-        const float qj = first ? A.dof_state_in[((size_t)e * ND + j) * 2 + 0] : s.q[j];
-        const float qdj = first ? A.dof_state_in[((size_t)e * ND + j) * 2 + 1] : s.qd[j];
-        const float aj = A.actions[(size_t)e * ND + j];
-        tau[j] = clampf(A.kp * (A.scale * aj + A.default_pos[j] - qj) - A.kd * qdj, -A.tlim, A.tlim);
-      }
-    }
-    const bool last = ((it % sub) == sub - 1) && P.collect;
-    substep<T, TERR>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last, it == total - 1 ? B.sens : nullptr);
-    if (it == n_pd - 1 && A.dof_out) {
-#pragma unroll
-      for (int j = 0; j < ND; ++j) {
-        A.dof_out[((size_t)e * ND + j) * 2 + 0] = s.q[j];
-        A.dof_out[((size_t)e * ND + j) * 2 + 1] = s.qd[j];
-      }
-    }
-  }
-  store_state<T>(B.state, N, e, s);
-#pragma unroll
-  for (int j = 0; j < ND; ++j) A.torques_out[(size_t)e * ND + j] = tau[j];
-  if (A.actions_copy) {
-#pragma unroll
-    for (int j = 0; j < ND; ++j) A.actions_copy[(size_t)e * ND + j] = A.actions[(size_t)e * ND + j];
-  }
-  if (A.root_out) {
-    float* o = A.root_out + (size_t)e * 13;
-    o[0] = s.p[0]; o[1] = s.p[1]; o[2] = s.p[2];
-    o[3] = s.quat[0]; o[4] = s.quat[1]; o[5] = s.quat[2]; o[6] = s.quat[3];
-    float v[3];
-    com_velocity<T>(M, s, v);
-    o[7] = v[0]; o[8] = v[1]; o[9] = v[2];
-    o[10] = s.w[0]; o[11] = s.w[1]; o[12] = s.w[2];
-  }
-  if (P.collect && A.cf_out) {
-#pragma unroll
-    for (int b = 0; b < T::NR; ++b)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) A.cf_out[((size_t)e * T::NR + b) * 3 + k] = B.cf[(3 * b + k) * N + e];
-  }
+  pd_step_env<T, TERR, LB>(M, P, B, A, e, lds + threadIdx.x);
 }
 
 // ---------------------------------------------------------------- tensor API kernels
@@ -875,23 +55,7 @@ __global__ void k_refresh_root(const float* __restrict__ st, int N, const float*
                                float* __restrict__ out) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= N) return;
-  float q[4], R[9], c[3], w[3], wc[3];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) q[k] = st[(3 + k) * N + e];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) w[k] = st[(10 + k) * N + e];
-  quat_to_mat(q, R);
-  mat3vec(R, com0, c);
-  cross3(w, c, wc);
-  float* o = out + (size_t)e * 13;
-#pragma unroll
-  for (int k = 0; k < 3; ++k) o[k] = st[k * N + e];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) o[3 + k] = q[k];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) o[7 + k] = st[(7 + k) * N + e] + wc[k];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) o[10 + k] = w[k];
+  refresh_root_env(st, N, com0, out, e);
 }
 __global__ void k_refresh_dof(const float* __restrict__ st, int N, int nd, float* __restrict__ out) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;  // t = e*nd + j
@@ -921,22 +85,7 @@ __global__ void k_set_root(float* __restrict__ st, int N, const float* __restric
   if (t >= n) return;
   const int e = idx ? idx[t] : t;
   if (e < 0 || e >= N) return;
-  const float* r = src + (size_t)e * 13;
-  float q[4], R[9], c[3], wc[3];
-  const float inv = rsqrtf(r[3] * r[3] + r[4] * r[4] + r[5] * r[5] + r[6] * r[6]);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) q[k] = r[3 + k] * inv;
-  quat_to_mat(q, R);
-  mat3vec(R, com0, c);
-  cross3(r + 10, c, wc);
-#pragma unroll
-  for (int k = 0; k < 3; ++k) st[k * N + e] = r[k];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) st[(3 + k) * N + e] = q[k];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) st[(7 + k) * N + e] = r[7 + k] - wc[k];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) st[(10 + k) * N + e] = r[10 + k];
+  set_root_env(st, N, com0, src, e);
 }
 __global__ void k_set_dof(float* __restrict__ st, int N, int nd, const float* __restrict__ src,
                           const int* __restrict__ idx, int n) {

@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "gs_math.h"
+
 #define TERRAIN_BACK 0.1f
 
 struct TerrainDev {
@@ -43,11 +45,11 @@ struct TerrainDev {
 
 namespace gs_terrain {
 
-__device__ __forceinline__ float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+GS_HD float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
 // closest point on triangle (a, b, c) to p (Voronoi-region walk); returns true when the point is
 // interior to the face
-__device__ __forceinline__ bool closest_on_triangle(const float* p, const float* a, const float* b, const float* c,
+GS_HD bool closest_on_triangle(const float* p, const float* a, const float* b, const float* c,
                                                     float* q) {
   float ab[3], ac[3], ap[3];
 #pragma unroll
@@ -93,7 +95,7 @@ __device__ __forceinline__ bool closest_on_triangle(const float* p, const float*
 }
 
 // one triangle: update (bkey, best, n) when it is an admissible surface closer to the centre
-__device__ __forceinline__ void triangle(const float* p, float r, float thr, const float4& A, const float4& B,
+GS_HD void triangle(const float* p, float r, float thr, const float4& A, const float4& B,
                                          const float4& C, float& bkey, float& best, float* n) {
   const float a[3] = {A.x, A.y, A.z}, b[3] = {B.x, B.y, B.z}, c[3] = {C.x, C.y, C.z};
   const float e1[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
@@ -101,7 +103,7 @@ __device__ __forceinline__ void triangle(const float* p, float r, float thr, con
   float nf[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
   const float l2 = dot3(nf, nf);
   if (!(l2 > 1e-14f)) return;  // degenerate (collapsed by two vertex moves)
-  const float il = rsqrtf(l2);
+  const float il = gs_rsqrt(l2);
   nf[0] *= il; nf[1] *= il; nf[2] *= il;
   const float ap[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
   const float sd = dot3(nf, ap);
@@ -131,20 +133,20 @@ __device__ __forceinline__ void triangle(const float* p, float r, float thr, con
 }
 
 // Closest admissible mesh surface for sphere (p, r); false when none lies within thr.
-__device__ __forceinline__ bool sphere_contact(const TerrainDev& T, const float* p, float r, float thr, float& sep,
+GS_HD bool sphere_contact(const TerrainDev& T, const float* p, float r, float thr, float& sep,
                                                float* n) {
   // horizontal reach: a face can be admitted from behind up to r + TERRAIN_BACK away (walls)
   const float reach = fmaxf(thr, r + TERRAIN_BACK);
   const float gx = (p[0] - T.x0) * T.inv_hs, gy = (p[1] - T.y0) * T.inv_hs, gt = reach * T.inv_hs;
-  const int i0 = max((int)floorf(gx - gt) - 1, 0), i1 = min((int)floorf(gx + gt) + 1, T.rows - 2);
-  const int j0 = max((int)floorf(gy - gt) - 1, 0), j1 = min((int)floorf(gy + gt) + 1, T.cols - 2);
+  const int i0 = gs_imax((int)floorf(gx - gt) - 1, 0), i1 = gs_imin((int)floorf(gx + gt) + 1, T.rows - 2);
+  const int j0 = gs_imax((int)floorf(gy - gt) - 1, 0), j1 = gs_imin((int)floorf(gy + gt) + 1, T.cols - 2);
   float best = 3.0e38f, bkey = 3.0e38f;
   const float zlo = p[2] - thr;
   for (int i = i0; i <= i1; ++i) {
     const float cx0 = T.x0 + (float)i * T.hs;
     for (int j = j0; j <= j1; ++j) {
       const uint2 cinfo = T.cell[(size_t)i * (T.cols - 1) + j];
-      if (zlo > __uint_as_float(cinfo.x)) continue;
+      if (zlo > gs_bits_float(cinfo.x)) continue;
       const uint32_t f = cinfo.y;
       const float cy0 = T.y0 + (float)j * T.hs;
       const float bx0 = cx0 - ((f & TCELL_XLO) ? T.hs : 0.f), bx1 = cx0 + ((f & TCELL_XHI) ? 2.f : 1.f) * T.hs;
@@ -163,14 +165,14 @@ __device__ __forceinline__ bool sphere_contact(const TerrainDev& T, const float*
 
 // tangent basis of the contact frame: t1 = world x projected onto the contact plane (world y
 // when n is along x), t2 = n x t1; for n = +z this is (x, y), the plane contact's axes
-__device__ __forceinline__ void tangents(const float* n, float* t1, float* t2) {
+GS_HD void tangents(const float* n, float* t1, float* t2) {
   float a[3] = {1.f - n[0] * n[0], -n[0] * n[1], -n[0] * n[2]};
   float l2 = a[0] * a[0] + a[1] * a[1] + a[2] * a[2];
   if (l2 < 1e-6f) {
     a[0] = -n[1] * n[0]; a[1] = 1.f - n[1] * n[1]; a[2] = -n[1] * n[2];
     l2 = a[0] * a[0] + a[1] * a[1] + a[2] * a[2];
   }
-  const float il = rsqrtf(l2);
+  const float il = gs_rsqrt(l2);
   t1[0] = a[0] * il; t1[1] = a[1] * il; t1[2] = a[2] * il;
   t2[0] = n[1] * t1[2] - n[2] * t1[1];
   t2[1] = n[2] * t1[0] - n[0] * t1[2];

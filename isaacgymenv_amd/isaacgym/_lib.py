@@ -1,8 +1,10 @@
 """ctypes binding of libgymsim.so (include/gymsim.h).
 
-There is no fallback: if the HIP library or a GPU is missing, every call that
-needs it raises.  (The CPU oracle under oracle/ is test infrastructure and is
-never loaded from here.)
+There is no fallback: if the library is missing every call raises, and a GPU
+sim without a GPU fails at gs_sim_create.  The library's host backend
+(gs_sim_create with device < 0, gs_host.hip) is the product's sim_device=cpu
+pipeline -- the same solver source on host buffers, not a fallback.  (The CPU
+oracle under oracle/ is test infrastructure and is never loaded from here.)
 """
 from __future__ import annotations
 
@@ -30,7 +32,7 @@ class GsSimParams(C.Structure):
                 ("contact_offset", C.c_double), ("rest_offset", C.c_double),
                 ("bounce_threshold_velocity", C.c_double), ("max_depenetration_velocity", C.c_double),
                 ("contact_collection", C.c_int32), ("kernel_variant", C.c_int32),
-                ("joint_limit_margin", C.c_double)]
+                ("joint_limit_margin", C.c_double), ("num_threads", C.c_int32)]
 
 
 class GsPdArgs(C.Structure):

@@ -12,8 +12,11 @@ stream of the sim device.
 Scope notes:
   * one articulation actor per env, every env the same asset;
   * z-up ground plane contacts (trimesh/heightfield terrain is the next row);
-  * ``pipeline=cpu`` keeps host-side tensors, the physics still runs on the GPU
-    (there is no CPU physics in the product).
+  * ``sim_device=cpu`` (``physx.use_gpu`` False, vec_task.py:82-88 / the task YAMLs'
+    ``use_gpu: ${contains:"cuda",${....sim_device}}``) runs the host backend of libgymsim --
+    the same solver source on a thread pool of ``physx.num_threads`` threads, host tensors,
+    no GPU needed; ``sim_device=cuda:k pipeline=cpu`` runs the GPU solver behind host-side
+    tensors (staged copies), as Isaac Gym's PhysX GPU + CPU pipeline does.
 """
 from __future__ import annotations
 
@@ -295,7 +298,14 @@ class Sim:
         self.params = params
         self.compute_device = compute_device
         self.gpu_pipeline = bool(params.use_gpu_pipeline)
-        self.sim_device = torch.device("cuda", compute_device)
+        # host backend: sim_device=cpu (physx.use_gpu False), or no HIP device to run on
+        self.host = not bool(params.physx.use_gpu)
+        if not self.host and not self.gpu_pipeline and not torch.cuda.is_available():
+            print("*** no HIP device: running the physics on the CPU (host backend, physx.num_threads threads)")
+            self.host = True
+        if self.host and self.gpu_pipeline:
+            raise RuntimeError("the GPU pipeline needs GPU physics (physx.use_gpu, sim_device=cuda:k)")
+        self.sim_device = torch.device("cpu") if self.host else torch.device("cuda", compute_device)
         self.tensor_device = self.sim_device if self.gpu_pipeline else torch.device("cpu")
         self.envs: List[Env] = []
         self.asset: Optional[Asset] = None
@@ -320,9 +330,11 @@ class Sim:
         p.kernel_variant = {"auto": 0, "lane": 1, "team": 2}[os.environ.get("GS_PHYSICS_KERNEL", "auto")]
         # a joint-limit row is generated within this distance of a limit (rad / m)
         p.joint_limit_margin = JOINT_LIMIT_MARGIN
+        # PhysX CPU worker threads (cfg/config.yaml:30 num_threads: 4); 0 = the calling thread only
+        p.num_threads = max(1, int(getattr(px, "num_threads", 0) or 0))
         self.cparams = p
         L = _lib.lib()
-        h = L.gs_sim_create(int(compute_device), p)
+        h = L.gs_sim_create(-1 if self.host else int(compute_device), p)
         if not h:
             raise RuntimeError(L.gs_last_error().decode())
         self.handle = h
@@ -336,6 +348,8 @@ class Sim:
 
     # -------- stream of the sim device
     def stream(self):
+        if self.host:
+            return None  # host backend: every call completes before it returns
         import torch
         return torch.cuda.current_stream(self.sim_device).cuda_stream
 
@@ -395,8 +409,8 @@ class Sim:
             _lib.check(L.gs_sim_bind_force_sensors(self.handle, self.sens_soa.data_ptr()), "gs_sim_bind_force_sensors")
         self.sensor_tensor = torch.zeros(N * len(sens), 6, dtype=f32, device=tdev)
         self.dof_force = torch.zeros(N * nd, dtype=f32, device=dev)
-        # device mirrors used when the pipeline is on the CPU
-        if not self.gpu_pipeline:
+        # device mirrors used when the pipeline is on the CPU and the physics on the GPU
+        if not self.gpu_pipeline and not self.host:
             self._root_dev = torch.zeros(N, 13, dtype=f32, device=dev)
             self._dof_dev = torch.zeros(N * nd, 2, dtype=f32, device=dev)
             self._cf_dev = torch.zeros(N * nb, 3, dtype=f32, device=dev)
@@ -472,21 +486,21 @@ class Sim:
             dst = {"rigid_body": self.rb_tensor, "jacobian": self.jac_tensor, "mass_matrix": self.mm_tensor}[kind]
             if dst is None:
                 return  # never acquired: nothing to fill
-            out = dst if self.gpu_pipeline else torch_empty_like_on(dst, self.sim_device)
+            out = dst if self.gpu_pipeline or self.host else torch_empty_like_on(dst, self.sim_device)
             fn = {"rigid_body": L.gs_sim_refresh_rigid_body, "jacobian": L.gs_sim_refresh_jacobian,
                   "mass_matrix": L.gs_sim_refresh_mass_matrix}[kind]
             _lib.check(fn(self.handle, out.data_ptr(), s), f"refresh {kind}")
-            if not self.gpu_pipeline:
+            if out is not dst:
                 dst.copy_(out.cpu())
             return
         dst = {"root": self.root_tensor, "dof": self.dof_tensor, "contact": self.contact_tensor,
                "sensor": self.sensor_tensor}[kind]
-        out = dst if self.gpu_pipeline else {"root": self._root_dev, "dof": self._dof_dev,
-                                             "contact": self._cf_dev, "sensor": self._sens_dev}[kind]
+        out = dst if self.gpu_pipeline or self.host else {"root": self._root_dev, "dof": self._dof_dev,
+                                                          "contact": self._cf_dev, "sensor": self._sens_dev}[kind]
         fn = {"root": L.gs_sim_refresh_root, "dof": L.gs_sim_refresh_dof, "contact": L.gs_sim_refresh_contact,
               "sensor": L.gs_sim_refresh_force_sensor}[kind]
         _lib.check(fn(self.handle, out.data_ptr(), s), f"refresh {kind}")
-        if not self.gpu_pipeline:
+        if out is not dst:
             dst.copy_(out.cpu())
 
     def set_state(self, kind: str, src, idx=None, n: int = 0):
@@ -542,7 +556,7 @@ class Gym:
         sim.simulate()
 
     def fetch_results(self, sim: Sim, wait: bool = True):
-        if wait and not sim.gpu_pipeline:
+        if wait and not sim.gpu_pipeline and not sim.host:
             import torch
             torch.cuda.synchronize(sim.sim_device)
 
@@ -882,7 +896,7 @@ class Gym:
         simulates, + the root/contact refreshes of post_physics_step, in ONE kernel launch."""
         L = _lib.lib()
         a = _lib.GsPdArgs()
-        assert sim.gpu_pipeline, "the fused step needs the GPU pipeline"
+        assert sim.gpu_pipeline or sim.host, "the fused step needs the GPU pipeline or the host backend"
         a.actions = actions.data_ptr()
         a.default_pos = default_pos.data_ptr()
         a.kp, a.kd, a.action_scale, a.torque_limit = kp, kd, action_scale, torque_limit

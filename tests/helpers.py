@@ -132,9 +132,10 @@ def anymal_states(n, seed=0, spread=1.0):
     return root, dof, tau, mu
 
 
-def make_gpu_sim(kind: str, n: int, params: dict, terrain=None):
+def make_gpu_sim(kind: str, n: int, params: dict, terrain=None, host: bool = False, threads: int = 4):
     """A libgymsim sim built through the drop-in gymapi (GPU pipeline); `terrain` (terrain_from_heights)
-    adds the heightfield mesh with gym.add_triangle_mesh."""
+    adds the heightfield mesh with gym.add_triangle_mesh.  host=True builds the sim_device=cpu pipeline
+    instead (physx.use_gpu False: libgymsim's host backend on `threads` threads, host tensors)."""
     from isaacgymenv_amd.isaacgym import gymapi
     gym = gymapi.acquire_gym()
     sp = gymapi.SimParams()
@@ -142,7 +143,9 @@ def make_gpu_sim(kind: str, n: int, params: dict, terrain=None):
     sp.substeps = params["substeps"]
     sp.up_axis = gymapi.UP_AXIS_Z
     sp.gravity = gymapi.Vec3(*params["gravity"])
-    sp.use_gpu_pipeline = True
+    sp.use_gpu_pipeline = not host
+    sp.physx.use_gpu = not host
+    sp.physx.num_threads = threads
     sp.physx.num_position_iterations = params["pos_iters"]
     sp.physx.num_velocity_iterations = params["vel_iters"]
     sp.physx.contact_offset = params["contact_offset"]
@@ -190,6 +193,10 @@ def make_gpu_sim(kind: str, n: int, params: dict, terrain=None):
         gym.create_actor(env, asset, pose, kind, i, 0, 0)
     gym.prepare_sim(sim)
     return gym, sim
+
+
+def make_host_sim(kind: str, n: int, params: dict, terrain=None, threads: int = 4):
+    return make_gpu_sim(kind, n, params, terrain=terrain, host=True, threads=threads)
 
 
 def load_state_into(sim, root, dof, mu):

@@ -1,0 +1,290 @@
+"""The product's CPU pipeline (sim_device=cpu pipeline=cpu; BASELINE config 1) without a GPU.
+
+libgymsim's host backend (gs_host.hip) runs the same solver source as the HIP kernels
+(gs_solver.h / gs_kinematics.h are __host__ __device__) on a thread pool, on host tensors.
+Reference: vec_task.py:82-88 (device selection), cfg/config.yaml:30-32 (physx.num_threads 4),
+cfg/task/Cartpole.yaml:27-32 (use_gpu_pipeline / physx.use_gpu from pipeline / sim_device).
+
+Checked here, on CPU only (these are `-m "not gpu"` tests):
+  * one simulate from identical states vs the fp64 oracle with the GPU tests' tolerances
+    (DESIGN.md section 4): Cartpole, ANYmal (plane), Ant (limits + force sensors), Hound
+    (per-link contact forces), ANYmal on a rough trimesh; link kinematics vs the kinematics oracle;
+  * the thread count does not change a single bit (one env per task, no cross-env reduction);
+  * the fused decimation step equals the unfused gym call sequence on the host backend too;
+  * Cartpole 64 through isaacgymenvs.make(sim_device="cpu", pipeline=cpu): every env step of the
+    real sim tracks an oracle step from the same state, resets / timeouts behave as the reference's,
+    and the reward / done function reproduces tests/golden/cartpole.npz (reference outputs) on the
+    fixture's own observations (dynamics free).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import kinematics_oracle as KO
+from oracle.oracle import OracleSim
+from tests import helpers as H
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _oracle(flat, params, root, dof, tau, mu, steps=1, **kw):
+    sim = OracleSim(flat, params, **{k: v for k, v in kw.items() if k in ("sensor_bodies", "terrain")})
+    r, d = root.copy(), dof.copy()
+    cf = np.zeros((root.shape[0], flat["nb"], 3))
+    sens = kw.get("sens")
+    for _ in range(steps):
+        if sens is not None:
+            sim.simulate(r, d, np.ascontiguousarray(tau), mu, cf, sens=sens)
+        else:
+            sim.simulate(r, d, np.ascontiguousarray(tau), mu, cf)
+    return r, d, cf
+
+
+def _host(kind, n, params, root, dof, tau, mu, nd, steps=1, terrain=None, threads=4):
+    gym, sim = H.make_host_sim(kind, n, params, terrain=terrain, threads=threads)
+    assert sim.host and sim.kernel_variant == 3 and sim.state.device.type == "cpu"
+    H.load_state_into(sim, root, dof, mu)
+    sim.dof_force.copy_(torch.from_numpy(tau.astype(np.float32).reshape(-1)))
+    for _ in range(steps):
+        gym.simulate(sim)
+    g_root, g_dof = H.read_state(sim, nd)
+    return gym, sim, g_root, g_dof
+
+
+def _check_state(g_root, g_dof, o_root, o_dof, max_frac=5e-3):
+    assert np.all(np.isfinite(g_root)) and np.all(np.isfinite(g_dof))
+    H.assert_mostly_close(g_root[:, 0:7], o_root[:, 0:7], atol=2e-5, max_frac=max_frac, what="root pose")
+    H.assert_mostly_close(g_dof[:, :, 0], o_dof[:, :, 0], atol=2e-5, max_frac=max_frac, what="dof pos")
+    H.assert_mostly_close(g_root[:, 7:13], o_root[:, 7:13], atol=5e-3, rtol=5e-3, max_frac=max_frac, what="root vel")
+    H.assert_mostly_close(g_dof[:, :, 1], o_dof[:, :, 1], atol=5e-3, rtol=5e-3, max_frac=max_frac, what="dof vel")
+
+
+def test_no_gpu_is_used():
+    """These tests run on the host backend whether or not a GPU exists (the driver runs them here)."""
+    gym, sim = H.make_host_sim("cartpole", 4, H.CARTPOLE_PARAMS)
+    assert sim.host and sim.stream() is None
+    for t in (sim.state, sim.root_tensor, sim.dof_tensor, sim.contact_tensor):
+        assert t.device.type == "cpu"
+
+
+def test_cartpole_one_simulate_matches_oracle():
+    n = 64
+    art, flat = H.cartpole()
+    rng = np.random.RandomState(3)
+    root = np.zeros((n, 13)); root[:, 2] = 2.0; root[:, 6] = 1.0
+    dof = np.zeros((n, 2, 2))
+    dof[:, :, 0] = 0.2 * (rng.rand(n, 2) - 0.5)
+    dof[:, :, 1] = 0.5 * (rng.rand(n, 2) - 0.5)
+    tau = np.zeros((n, 2)); tau[:, 0] = rng.uniform(-400, 400, n)
+    mu = np.ones((n, flat["ns"]))
+    _, _, g_root, g_dof = _host("cartpole", n, H.CARTPOLE_PARAMS, root, dof, tau, mu, 2)
+    o_root, o_dof, _ = _oracle(flat, H.CARTPOLE_PARAMS, root, dof, tau, mu)
+    np.testing.assert_allclose(g_dof, o_dof, atol=1e-4, rtol=1e-4)
+
+
+def test_anymal_one_simulate_matches_oracle():
+    n = 128
+    art, flat = H.anymal()
+    root, dof, tau, mu = H.anymal_states(n, seed=1)
+    gym, sim, g_root, g_dof = _host("anymal", n, H.ANYMAL_PARAMS, root, dof, tau, mu, 12)
+    o_root, o_dof, o_cf = _oracle(flat, H.ANYMAL_PARAMS, root, dof, tau, mu)
+    _check_state(g_root, g_dof, o_root, o_dof, max_frac=0.0)
+    g_cf = sim.cf_soa.numpy().T.reshape(n, 13, 3)
+    np.testing.assert_allclose(g_cf, o_cf, atol=1.0, rtol=2e-2)
+    gym.refresh_net_contact_force_tensor(sim)
+    np.testing.assert_array_equal(sim.contact_tensor.numpy().reshape(n, 13, 3), g_cf)
+
+
+def test_ant_limits_and_sensors_match_oracle():
+    n = 128
+    art, flat = H.ant()
+    root, dof, tau, mu = H.ant_states(n, seed=3)
+    gym, sim, g_root, g_dof = _host("ant", n, H.ANT_PARAMS, root, dof, tau, mu, 8)
+    assert sim.num_sensors == 4
+    g_sens = sim.sens_soa.numpy().astype(np.float64).T.reshape(n, 4, 6)
+    gym.refresh_force_sensor_tensor(sim)
+    np.testing.assert_array_equal(sim.sensor_tensor.numpy().reshape(n, 4, 6), g_sens.astype(np.float32))
+    sens = np.zeros((n, 4, 6))
+    o_root, o_dof, _ = _oracle(flat, H.ANT_PARAMS, root, dof, tau, mu, sensor_bodies=H.ANT_FEET, sens=sens)
+    _check_state(g_root, g_dof, o_root, o_dof)
+    H.assert_mostly_close(g_sens, sens, atol=0.09, rtol=2e-2, max_frac=5e-3, what="foot sensors")
+
+
+def test_hound_per_link_contacts_match_oracle():
+    n = 96
+    art, flat = H.hound()
+    root, dof, tau, mu = H.hound_states(n, seed=5)
+    gym, sim, g_root, g_dof = _host("hound", n, H.HOUND_PARAMS, root, dof, tau, mu, 18)
+    gym.refresh_net_contact_force_tensor(sim)
+    g_cf = sim.contact_tensor.numpy().astype(np.float64).reshape(n, 24, 3)
+    osim = OracleSim(flat, H.HOUND_PARAMS)
+    o_root, o_dof, o_cf = root.copy(), dof.copy(), np.zeros((n, 24, 3))
+    osim.simulate(o_root, o_dof, np.ascontiguousarray(tau), mu, o_cf)
+    assert np.abs(o_cf).sum() > 0
+    _check_state(g_root, g_dof, o_root, o_dof)
+    H.assert_mostly_close(g_cf, o_cf, atol=1.0, rtol=2e-2, max_frac=5e-3, what="contact forces per link")
+
+
+def test_rough_trimesh_matches_oracle():
+    ter = H.rough_terrain(seed=5, rows=80, cols=80)
+    n = 96
+    art, flat = H.anymal()
+    params = dict(H.ANYMAL_PARAMS, has_ground=0)
+    root, dof, tau, mu = H.anymal_states(n, seed=2)
+    rng = np.random.RandomState(102)
+    root[:, 0] = rng.uniform(-3.0, 3.0, n)
+    root[:, 1] = rng.uniform(-3.0, 3.0, n)
+    v = ter["oracle"]["vertices"].reshape(-1, 3)
+    for i in range(n):
+        near = (np.abs(v[:, 0] - root[i, 0]) < 0.15) & (np.abs(v[:, 1] - root[i, 1]) < 0.15)
+        root[i, 2] += v[near, 2].mean() + 0.05
+    gym, sim, g_root, g_dof = _host("anymal", n, params, root, dof, tau, mu, 12, terrain=ter)
+    o_root, o_dof, o_cf = _oracle(flat, params, root, dof, tau, mu, terrain=ter["oracle"])
+    assert np.abs(o_cf).sum(axis=(1, 2)).astype(bool).mean() > 0.5, "most envs must touch the mesh"
+    _check_state(g_root, g_dof, o_root, o_dof)
+    g_cf = sim.cf_soa.numpy().T.reshape(n, 13, 3)
+    H.assert_mostly_close(g_cf, o_cf, atol=1.0, rtol=2e-2, max_frac=5e-3, what="contact forces")
+
+
+@pytest.mark.parametrize("kind", ["hound", "anymal", "cartpole"])
+def test_link_kinematics_match_oracle(kind):
+    n = 40
+    if kind == "hound":
+        art, flat = H.hound()
+        root, dof, _, mu = H.hound_states(n, seed=21)
+        params = H.HOUND_PARAMS
+    elif kind == "anymal":
+        art, flat = H.anymal()
+        root, dof, _, mu = H.anymal_states(n, seed=21)
+        params = H.ANYMAL_PARAMS
+    else:
+        art, flat = H.cartpole()
+        rng = np.random.RandomState(21)
+        root = np.zeros((n, 13)); root[:, 2] = 2.0; root[:, 6] = 1.0
+        dof = rng.uniform(-1.5, 1.5, (n, 2, 2))
+        mu = np.ones((n, flat["ns"]))
+        params = H.CARTPOLE_PARAMS
+    gym, sim = H.make_host_sim(kind, n, params)
+    H.load_state_into(sim, root, dof, mu)
+    from isaacgymenv_amd.isaacgym import gymtorch
+    rb = gymtorch.wrap_tensor(gym.acquire_rigid_body_state_tensor(sim))
+    jac_t = gymtorch.wrap_tensor(gym.acquire_jacobian_tensor(sim, kind))
+    mm_t = gymtorch.wrap_tensor(gym.acquire_mass_matrix_tensor(sim, kind))
+    gym.refresh_rigid_body_state_tensor(sim)
+    gym.refresh_jacobian_tensors(sim)
+    gym.refresh_mass_matrix_tensors(sim)
+    o_rb, o_jac, o_mm = KO.batch(flat, root, dof)
+    g_rb = rb.numpy().astype(np.float64)
+    nv = flat["nd"] + (0 if flat["fixed_base"] else 6)
+    if flat["fixed_base"]:
+        g_jac = np.concatenate([np.zeros((n, 1, 6, nv)), jac_t.numpy()], axis=1)
+    else:
+        g_jac = jac_t.numpy().astype(np.float64)
+    np.testing.assert_allclose(g_rb[:, 0:3], o_rb[:, 0:3], atol=2e-5, rtol=1e-5)
+    dots = np.abs(np.sum(g_rb[:, 3:7] * o_rb[:, 3:7], axis=1))
+    assert dots.min() >= 1 - 1e-6, dots.min()
+    np.testing.assert_allclose(g_rb[:, 7:13], o_rb[:, 7:13], atol=1e-4, rtol=1e-4)
+    np.testing.assert_allclose(g_jac, o_jac, atol=2e-5, rtol=1e-5)
+    np.testing.assert_allclose(mm_t.numpy(), o_mm, atol=1e-4, rtol=1e-4)
+
+
+def test_thread_count_is_bit_invariant():
+    n = 200
+    art, flat = H.anymal()
+    root, dof, tau, mu = H.anymal_states(n, seed=8, spread=2.0)
+    outs = []
+    for threads in (1, 3, 8):
+        _, sim, g_root, g_dof = _host("anymal", n, H.ANYMAL_PARAMS, root, dof, tau, mu, 12, steps=5, threads=threads)
+        outs.append((g_root, g_dof, sim.cf_soa.numpy().copy()))
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            np.testing.assert_array_equal(a, b)
+
+
+def test_fused_step_equals_unfused_calls_on_host():
+    """gs_sim_pd_step on the host backend == PD torque + simulate x4 + refresh dof, + 1 simulate."""
+    n = 64
+    art, flat = H.anymal()
+    root, dof, _, mu = H.anymal_states(n, seed=4)
+    q0 = np.array([H.ANYMAL_DEFAULT[d] for d in art.dof_names()], dtype=np.float32)
+    actions = torch.from_numpy(np.random.RandomState(0).uniform(-1, 1, (n, 12)).astype(np.float32))
+    res = {}
+    for mode in ("fused", "unfused"):
+        gym, sim = H.make_host_sim("anymal", n, H.ANYMAL_PARAMS)
+        H.load_state_into(sim, root, dof, mu)
+        gym.refresh_dof_state_tensor(sim)
+        dpos = torch.from_numpy(q0)
+        torques = torch.zeros(n, 12)
+        if mode == "fused":
+            gym.amd_pd_decimation_step(sim, actions, dpos, 80.0, 2.0, 0.5, 80.0, 4, 1, torques)
+        else:
+            dof_t = sim.dof_tensor.view(n, 12, 2)
+            for _ in range(4):
+                torques = torch.clip(80.0 * (0.5 * actions + dpos - dof_t[..., 0]) - 2.0 * dof_t[..., 1], -80., 80.)
+                sim.dof_force.copy_(torques.reshape(-1))
+                gym.simulate(sim)
+                gym.refresh_dof_state_tensor(sim)
+            gym.simulate(sim)
+            gym.refresh_actor_root_state_tensor(sim)
+            gym.refresh_net_contact_force_tensor(sim)
+        res[mode] = (sim.state.numpy().copy(), sim.dof_tensor.numpy().copy(), sim.root_tensor.numpy().copy(),
+                     sim.contact_tensor.numpy().copy(), torques.numpy().copy())
+    for a, b in zip(res["fused"], res["unfused"]):
+        np.testing.assert_allclose(a, b, atol=1e-5, rtol=1e-5)
+
+
+def test_cartpole64_cpu_pipeline_tracks_oracle(monkeypatch):
+    """BASELINE config 1 end to end: isaacgymenvs.make(task=Cartpole, num_envs=64, sim_device=cpu,
+    pipeline=cpu), 600 env steps (past the 500-step timeout); each step's physics vs an oracle
+    simulate from the state the sim held before the step."""
+    from isaacgymenv_amd.isaacgymenvs.tasks.base import vec_task
+    monkeypatch.setattr(vec_task, "EXISTING_SIM", None)
+    import isaacgymenvs
+    n = 64
+    env = isaacgymenvs.make(seed=42, task="Cartpole", num_envs=n, sim_device="cpu", rl_device="cpu", headless=True,
+                            overrides=["pipeline=cpu"])
+    assert env.device == "cpu" and env.sim.host and env.sim.kernel_variant == 3
+    assert env.sim.cparams.num_threads == 4  # physx.num_threads, cfg/config.yaml:30
+    art, flat = H.cartpole()
+    osim = OracleSim(flat, H.CARTPOLE_PARAMS)
+    gen = torch.Generator().manual_seed(5)
+    for t in range(600):
+        before_root, before_dof = H.read_state(env.sim, 2)
+        actions = 2 * torch.rand((n, 1), generator=gen) - 1
+        obs, rew, reset, extras = env.step(actions)
+        assert obs["obs"].shape == (n, 4) and obs["obs"].device.type == "cpu"
+        assert reset.dtype == torch.int64 and extras["time_outs"].dtype == torch.bool
+        assert int(env.progress_buf.max()) <= 499  # reset at progress >= max_episode_length - 1
+        # the physics of this step, for the envs that were not reset inside post_physics_step
+        tau = np.zeros((n, 2)); tau[:, 0] = actions.numpy()[:, 0] * 400.0
+        r, d = before_root.copy(), before_dof.copy()
+        osim.simulate(r, d, np.ascontiguousarray(tau), np.ones((n, flat["ns"])))
+        _, g_dof = H.read_state(env.sim, 2)
+        kept = (env.progress_buf.numpy() != 0)
+        np.testing.assert_allclose(g_dof[kept], d[kept], atol=1e-4, rtol=1e-4, err_msg=f"step {t}")
+        # observation = the refreshed dof tensor, clamped at clipObservations 5 (Cartpole.yaml:14)
+        exp = np.stack([g_dof[:, 0, 0], g_dof[:, 0, 1], g_dof[:, 1, 0], g_dof[:, 1, 1]], axis=1)
+        np.testing.assert_allclose(obs["obs"].numpy(), np.clip(exp, -5, 5), atol=1e-6)
+
+
+def test_cartpole_reward_and_done_reproduce_golden_outputs():
+    """Dynamics-free pin of the CPU pipeline's tail: compute_cartpole_reward on the fixture's own
+    observations gives the reference's rewards and fall resets (tests/golden/cartpole.npz)."""
+    from isaacgymenv_amd.isaacgymenvs.tasks.cartpole import compute_cartpole_reward
+    d = np.load(os.path.join(GOLDEN, "cartpole.npz"))
+    obs = torch.from_numpy(d["obs"]).double()
+    checked = 0
+    for t in range(obs.shape[0]):
+        o = obs[t]
+        inside = (o.abs() < 5.0).all(dim=1)  # the returned obs are clamped at 5; the reward used raw values
+        rew, reset = compute_cartpole_reward(o[:, 2], o[:, 3], o[:, 1], o[:, 0], 3.0,
+                                             torch.zeros(o.shape[0], dtype=torch.long),
+                                             torch.zeros(o.shape[0], dtype=torch.long), 500.0)
+        m = inside.numpy()
+        np.testing.assert_allclose(rew.numpy()[m], d["rew"][t][m], rtol=1e-5, atol=1e-6, err_msg=f"step {t}")
+        fell = d["reset"][t].astype(bool) & ~d["time_outs"][t].astype(bool)
+        np.testing.assert_array_equal(reset.numpy()[m].astype(bool), fell[m], err_msg=f"step {t}")
+        checked += int(m.sum())
+    assert checked > 80  # envs whose returned observation is unclamped
