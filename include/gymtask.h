@@ -119,8 +119,10 @@ typedef struct gt_anymal_reset_draws {
  * which: envs are ranked by index from reset_masks (torch.nonzero's order), row t of the draws
  * goes to the t-th flagged env.  env_ids_out int32[k] receives the flagged ids ascending (for
  * set_*_tensor_indexed); episode_out[13] = mean over the flagged envs of each episode sum /
- * episode_length_s (extras["episode"], :416-420), sums then zeroed.  scratch: 16 words of
- * zero-initialised device memory the kernel re-arms. */
+ * episode_length_s (extras["episode"], :416-420), sums then zeroed; the means are summed in a
+ * fixed order (bit-identical run to run).  scratch: GT_ANYMAL_RESET_SCRATCH_WORDS(num_envs) words
+ * of device memory, the first 16 zero-initialised (a counter the kernel re-arms). */
+#define GT_ANYMAL_RESET_SCRATCH_WORDS(num_envs) (16 + GT_ANYMAL_NUM_TERMS * (((num_envs) + 63) / 64))
 int gt_anymal_reset_flagged(const gt_anymal_params *p, const gt_anymal_buffers *b, int k,
                             const gt_anymal_reset_draws *draws, int32_t *env_ids_out, float *episode_out,
                             float episode_length_s, void *scratch, void *stream);

@@ -247,7 +247,7 @@ __global__ void __launch_bounds__(64) k_post_a(gt_anymal_params p, gt_anymal_buf
 
 __global__ void k_reset(gt_anymal_params p, gt_anymal_buffers b, const int32_t* __restrict__ ids, int k,
                         const float* __restrict__ off, const float* __restrict__ vel, const float* __restrict__ cx,
-                        const float* __restrict__ cy, const float* __restrict__ ch, float* __restrict__ ep) {
+                        const float* __restrict__ cy, const float* __restrict__ ch) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= k) return;
   const int e = ids[t];
@@ -274,10 +274,8 @@ __global__ void k_reset(gt_anymal_params p, gt_anymal_buffers b, const int32_t* 
   b.progress_buf[e] = 0;
   b.reset_buf[e] = 1;
   const size_t N = p.num_envs;
-  for (int term = 0; term < GT_ANYMAL_NUM_TERMS; ++term) {
-    atomicAdd(&ep[term], b.episode_sums[term * N + e]);
-    b.episode_sums[term * N + e] = 0.0f;
-  }
+  // the episode sums were summed by k_episode_sums (launched before this kernel)
+  for (int term = 0; term < GT_ANYMAL_NUM_TERMS; ++term) b.episode_sums[term * N + e] = 0.0f;
 }
 
 __device__ __forceinline__ int wave_sum(int v) {
@@ -291,13 +289,31 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// ep[term] = sum over t of episode_sums[term][ids[t]] in a FIXED order (extras["episode"] must not
+// depend on how waves were scheduled): one wave per term, lane l sums t = l, l + 64, ... in order,
+// then the butterfly reduction (itself a fixed order).
+__global__ void __launch_bounds__(64 * GT_ANYMAL_NUM_TERMS) k_episode_sums(gt_anymal_params p,
+                                                                          const float* __restrict__ sums,
+                                                                          const int32_t* __restrict__ ids, int k,
+                                                                          float* __restrict__ ep) {
+  const int term = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t N = p.num_envs;
+  float v = 0.0f;
+  for (int t = lane; t < k; t += 64) {
+    const int e = ids[t];
+    if (e >= 0 && e < p.num_envs) v += sums[term * N + e];
+  }
+  v = wave_sum(v);
+  if (lane == 0) ep[term] = v;
+}
+
 // reset_idx for the envs post_a flagged (anymal_terrain.py:384-425, plane terrain).  One lane
 // per env, one wave per workgroup; the rank of a flagged env among all flagged envs comes from
 // post_a's per-wave ballots (exclusive prefix of popcounts), so no compaction pass is needed.
 __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_anymal_buffers b, int k,
                                                       gt_anymal_reset_draws d, int32_t* __restrict__ ids_out,
                                                       float* __restrict__ ep_out, float len_s,
-                                                      float* __restrict__ acc, unsigned* __restrict__ done) {
+                                                      float* __restrict__ partial, unsigned* __restrict__ done) {
   const int lane = threadIdx.x;
   const int w = blockIdx.x;
   const int e = w * 64 + lane;
@@ -368,23 +384,26 @@ __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_any
     }
     ids_out[t] = e;
   }
-  if (mine) {
+  // Episode means, deterministic: every wave publishes its 13 wave sums (zeros when nothing was
+  // flagged) to its own slot of `partial`; the last wave to finish adds the slots in wave order.
+  // Agent-scope atomic stores / loads: the waves run on different XCDs, whose L2s are not coherent.
 #pragma unroll
-    for (int i = 0; i < GT_ANYMAL_NUM_TERMS; ++i) {
-      const float s = wave_sum(term[i]);
-      if (lane == 0) atomicAdd(&acc[i], s);
-    }
+  for (int i = 0; i < GT_ANYMAL_NUM_TERMS; ++i) {
+    const float s = mine ? wave_sum(term[i]) : 0.0f;
+    if (lane == i) __hip_atomic_store(&partial[(size_t)w * GT_ANYMAL_NUM_TERMS + i], s, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
   }
   unsigned old = 0;
-  if (lane == 0) {
-    __threadfence();
-    old = atomicAdd(done, 1u);
-  }
+  __threadfence();
+  if (lane == 0) old = atomicAdd(done, 1u);
   old = __shfl(old, 0, 64);
   if (old == gridDim.x - 1) {  // last wave: finalise the 13 terms in parallel lanes
     __threadfence();
     if (lane < GT_ANYMAL_NUM_TERMS) {
-      const float v = atomicExch(&acc[lane], 0.0f);
+      float v = 0.0f;
+      for (int q = 0; q < (int)gridDim.x; ++q)
+        v += __hip_atomic_load(&partial[(size_t)q * GT_ANYMAL_NUM_TERMS + lane], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
       ep_out[lane] = (v / (float)k) / len_s;  // torch.mean(sums[env_ids]) / max_episode_length_s
     }
     if (lane == 0) *done = 0u;
@@ -546,13 +565,16 @@ int gt_anymal_reset(const gt_anymal_params* p, const gt_anymal_buffers* b, const
                     const float* cmd_heading, float* episode_out, void* stream) {
   if (check_params(p)) return -1;
   hipStream_t st = (hipStream_t)stream;
-  hipError_t e = hipMemsetAsync(episode_out, 0, sizeof(float) * GT_ANYMAL_NUM_TERMS, st);
-  if (e != hipSuccess) return fail("gt_anymal_reset memset", e);
-  if (k <= 0) return 0;
+  if (k <= 0) {
+    hipError_t e = hipMemsetAsync(episode_out, 0, sizeof(float) * GT_ANYMAL_NUM_TERMS, st);
+    return e == hipSuccess ? 0 : fail("gt_anymal_reset memset", e);
+  }
+  hipLaunchKernelGGL(k_episode_sums, dim3(1), dim3(64 * GT_ANYMAL_NUM_TERMS), 0, st, *p, b->episode_sums, env_ids, k,
+                     episode_out);
   const int blk = 256;
   hipLaunchKernelGGL(k_reset, dim3((k + blk - 1) / blk), dim3(blk), 0, st, *p, *b, env_ids, k, pos_offset, dof_vel,
-                     cmd_x, cmd_y, cmd_heading, episode_out);
-  e = hipGetLastError();
+                     cmd_x, cmd_y, cmd_heading);
+  hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("gt_anymal_reset", e);
 }
 
@@ -590,10 +612,10 @@ int gt_anymal_reset_flagged(const gt_anymal_params* p, const gt_anymal_buffers* 
     return -1;
   }
   if (k == 0) return 0;
-  float* acc = static_cast<float*>(scratch);
-  unsigned* done = reinterpret_cast<unsigned*>(acc + GT_ANYMAL_NUM_TERMS);
+  unsigned* done = static_cast<unsigned*>(scratch);
+  float* partial = static_cast<float*>(scratch) + 16;
   hipLaunchKernelGGL(k_reset_flagged, dim3((p->num_envs + 63) / 64), dim3(64), 0, (hipStream_t)stream, *p, *b, k,
-                     *d, env_ids_out, episode_out, episode_length_s, acc, done);
+                     *d, env_ids_out, episode_out, episode_length_s, partial, done);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("gt_anymal_reset_flagged", e);
 }

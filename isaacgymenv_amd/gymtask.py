@@ -299,7 +299,8 @@ class AnymalTailKernels:
         self.noise_scale = t.noise_scale_vec.contiguous()
         self.reset_count = torch.zeros(3, dtype=torch.int32, device=dev)  # accumulator, wg counter, last count
         self.reset_masks = torch.zeros((N + 63) // 64, dtype=torch.int64, device=dev)
-        self.reset_scratch = torch.zeros(16, dtype=torch.float32, device=dev)
+        # GT_ANYMAL_RESET_SCRATCH_WORDS: re-armed counter (16 words) + per-wave episode partial sums
+        self.reset_scratch = torch.zeros(16 + len(self.TERMS) * ((N + 63) // 64), dtype=torch.float32, device=dev)
         # {count, seq} published by post_a straight into pinned host memory (gt_wait_host_seq)
         h, d = C.c_void_p(), C.c_void_p()
         _check(L.gt_host_alloc(8, C.byref(h), C.byref(d)), "gt_host_alloc")

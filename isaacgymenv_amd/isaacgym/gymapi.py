@@ -300,11 +300,13 @@ class Sim:
         self.gpu_pipeline = bool(params.use_gpu_pipeline)
         # host backend: sim_device=cpu (physx.use_gpu False), or no HIP device to run on
         self.host = not bool(params.physx.use_gpu)
+        if self.host and self.gpu_pipeline:
+            # as Isaac Gym, which cannot keep GPU-pipeline tensors with CPU PhysX: GPU physics
+            print("*** the GPU pipeline needs GPU physics: ignoring physx.use_gpu=False")
+            self.host = False
         if not self.host and not self.gpu_pipeline and not torch.cuda.is_available():
             print("*** no HIP device: running the physics on the CPU (host backend, physx.num_threads threads)")
             self.host = True
-        if self.host and self.gpu_pipeline:
-            raise RuntimeError("the GPU pipeline needs GPU physics (physx.use_gpu, sim_device=cuda:k)")
         self.sim_device = torch.device("cpu") if self.host else torch.device("cuda", compute_device)
         self.tensor_device = self.sim_device if self.gpu_pipeline else torch.device("cpu")
         self.envs: List[Env] = []

@@ -198,3 +198,27 @@ def test_ant_gpu_episode(monkeypatch):
     d = torch.stack(dones)
     assert int(d.sum()) >= n // 4
     assert torch.isfinite(extras["true_objective"]).all()
+
+
+def test_episode_extras_are_bit_identical_across_same_seed_runs(monkeypatch):
+    """extras["episode"] (the fused reset's per-term means) is reduced in a fixed order, so two runs
+    from the same seed give the same bits on every reset step (cross-wave float atomics)."""
+    n = 2048
+
+    def run():
+        env = _make("AnymalTerrain", n, monkeypatch, **{"task.env.learn.episodeLength_s": 0.6})
+        gen = torch.Generator(device="cuda:0").manual_seed(9)
+        eps = []
+        for _ in range(70):
+            _, _, reset, extras = env.step(2 * torch.rand((n, 12), device="cuda:0", generator=gen) - 1)
+            ep = extras.get("episode")
+            if ep is not None and bool(reset.any()):
+                eps.append(torch.stack([ep[k].float().reshape(()) for k in sorted(ep)]).cpu())
+            env.extras.pop("episode", None)
+        torch.cuda.synchronize()
+        return eps
+
+    a, b = run(), run()
+    assert len(a) >= 2 and len(a) == len(b)
+    for x, y in zip(a, b):
+        assert torch.equal(x.view(torch.int32), y.view(torch.int32))

@@ -197,9 +197,6 @@ def test_terrain_query_matches_oracle():
     both = found_g & found_o
     dsep = np.abs(g[both, 1] - ref[both, 1])
     dn = np.abs(g[both, 2:5] - ref[both, 2:5]).max(axis=1)
-    import os
-    os.makedirs("gpurun_out", exist_ok=True)
-    np.savez_compressed("gpurun_out/terrain_query_diff.npz", c=c, r=r, g=g, ref=ref)
     assert flips < 2e-4, flips
     assert (dsep > 1e-4).mean() < 5e-4, ((dsep > 1e-4).mean(), dsep.max())
     assert (dn > 1e-3).mean() < 5e-4, ((dn > 1e-3).mean(), dn.max())
