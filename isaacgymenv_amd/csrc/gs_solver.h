@@ -38,13 +38,13 @@ struct LaneCfg {
   // Below 16 lanes the rows of two workgroups no longer share a CU, and halving again measured
   // ~10 % faster for Hound (2745 slots; r01n, profiles/r01n_experiments_other_configs.txt) while
   // Ant (32 lanes) got slower at 4: only the LDS-starved widths go narrower.  The mesh-contact
-  // (TERR) variant is bound by its terrain queries, which gain from spreading the envs over more
-  // CUs: 16 lanes measured ~8 % faster than 64 for ANYmal on the trimesh map.
+  // (TERR) kernels run LB env lanes in a 64-lane workgroup whose other lanes help with the terrain
+  // queries (gs_physics.hip, k_*_terr): few env lanes = many query lanes per env.
 #ifndef GS_NARROW_LANES
 #define GS_NARROW_LANES 4
 #endif
 #ifndef GS_TERR_LANES
-#define GS_TERR_LANES 16
+#define GS_TERR_LANES 4
 #endif
   static constexpr int LB = FIT == 8 ? GS_NARROW_LANES : (TERR && FIT > GS_TERR_LANES) ? GS_TERR_LANES : FIT;
   static_assert(SLOTS * LB * 4 <= 160 * 1024, "contact rows exceed the LDS of a CU even at 8 lanes");
@@ -111,10 +111,14 @@ GS_HD void store_state(float* __restrict__ st, int N, int e, const EnvState<T>& 
 // is complete (T::subend).  Contact Jacobian rows are written to LDS during the
 // same walk (they need the path's motion subspaces) and turned into scaled
 // Z rows after the factorisation.
-template <class T, bool TERR, int LB = LaneCfg<T, TERR>::LB>
+// QS > 0 (TERR kernels): the terrain queries of this substep were already run by the whole workgroup
+// (terrain_queries, gs_physics.hip) and `qres` holds this env's results, [5 * c + k][QS] for
+// candidate c: (found, separation, normal xyz); QS == 0 runs each candidate's query inline.
+template <class T, bool TERR, int LB = LaneCfg<T, TERR>::LB, int QS = 0>
 GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvState<T>& s,
                                         const float* tau, const float* __restrict__ mu_g, int N, int e, float* lds,
-                                        float* __restrict__ cf_soa, bool collect, float* __restrict__ sens_soa) {
+                                        float* __restrict__ cf_soa, bool collect, float* __restrict__ sens_soa,
+                   const float* __restrict__ qres = nullptr) {
   constexpr int NB = T::NB, NV = T::NV, NB6 = T::NBASE, NC = T::NC, ND = T::ND;
   constexpr int MS = T::MAXDEP + 1;
   // Keep the model pointer opaque per substep: the constants are re-read with
@@ -237,7 +241,15 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
           float nrm[3] = {0.f, 0.f, 1.f};
           float smu = P.ground_mu;
           float st, nt[3];
-          if (gs_terrain::sphere_contact(P.terr, cw, r, r + P.contact_offset, st, nt) && st < dist) {
+          bool found;
+          if constexpr (QS > 0) {
+            found = qres[(5 * c) * QS] != 0.f;
+            st = qres[(5 * c + 1) * QS];
+            nt[0] = qres[(5 * c + 2) * QS]; nt[1] = qres[(5 * c + 3) * QS]; nt[2] = qres[(5 * c + 4) * QS];
+          } else {
+            found = gs_terrain::sphere_contact(P.terr, cw, r, r + P.contact_offset, st, nt);
+          }
+          if (found && st < dist) {
             dist = st;
             nrm[0] = nt[0]; nrm[1] = nt[1]; nrm[2] = nt[2];
             smu = P.terr.mu;
@@ -765,6 +777,61 @@ GS_HD void com_velocity(const DevModel* __restrict__ M, const EnvState<T>& s, fl
   v[0] = s.vo[0] + wc[0]; v[1] = s.vo[1] + wc[1]; v[2] = s.vo[2] + wc[2];
 }
 
+// World centres of env state s's contact candidates, exactly as substep's tree walk forms them
+// (cw = p + R_b cpoint + X_b), written to out[(4 * c + k) * stride] with the radius as k = 3.
+template <class T>
+GS_HD void candidate_centres(const DevModel* __restrict__ Min, const EnvState<T>& s, float* out, int stride) {
+  constexpr int NB = T::NB, NC = T::NC;
+  const DevModel* __restrict__ M = gs_opaque(Min);
+  float R[NB][9], X[NB][3];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    if (i == 0) {
+      float qn[4];
+      const float inv = gs_rsqrt(s.quat[0] * s.quat[0] + s.quat[1] * s.quat[1] + s.quat[2] * s.quat[2] +
+                                 s.quat[3] * s.quat[3]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) qn[k] = s.quat[k] * inv;
+      quat_to_mat(qn, R[0]);
+      X[0][0] = X[0][1] = X[0][2] = 0.f;
+    } else {
+      const int pa = T::parent[i];
+      float RJ[9], t[3], aw[3];
+      mat3mul(R[pa], M->jR[i], RJ);
+      mat3vec(R[pa], M->jt[i], t);
+      X[i][0] = X[pa][0] + t[0]; X[i][1] = X[pa][1] + t[1]; X[i][2] = X[pa][2] + t[2];
+      mat3vec(RJ, M->jaxis[i], aw);
+      const float qj = s.q[T::bdof[i]];
+      if (T::jkind[i] == 1) {
+        float sn, cs;
+        gs_sincos(qj, &sn, &cs);
+        const float* a = M->jaxis[i];
+        const float C = 1.f - cs;
+        float Rq[9];
+        Rq[0] = cs + a[0] * a[0] * C;        Rq[1] = a[0] * a[1] * C - a[2] * sn; Rq[2] = a[0] * a[2] * C + a[1] * sn;
+        Rq[3] = a[1] * a[0] * C + a[2] * sn; Rq[4] = cs + a[1] * a[1] * C;        Rq[5] = a[1] * a[2] * C - a[0] * sn;
+        Rq[6] = a[2] * a[0] * C - a[1] * sn; Rq[7] = a[2] * a[1] * C + a[0] * sn; Rq[8] = cs + a[2] * a[2] * C;
+        mat3mul(RJ, Rq, R[i]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R[i][k] = RJ[k];
+        X[i][0] += aw[0] * qj; X[i][1] += aw[1] * qj; X[i][2] += aw[2] * qj;
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int b = T::cbody[c];
+    float x[3];
+    mat3vec(R[b], M->cpoint[c], x);
+    x[0] += X[b][0]; x[1] += X[b][1]; x[2] += X[b][2];
+    out[(4 * c + 0) * stride] = s.p[0] + x[0];
+    out[(4 * c + 1) * stride] = s.p[1] + x[1];
+    out[(4 * c + 2) * stride] = s.p[2] + x[2];
+    out[(4 * c + 3) * stride] = M->cradius[c];
+  }
+}
+
 // ---------------------------------------------------------------- per-env entry points
 // gym.simulate for env e: `substeps` substeps with constant dof forces [N][nd] (or zero)
 template <class T, bool TERR, int LB>
@@ -783,42 +850,36 @@ GS_HD void simulate_env(const DevModel* __restrict__ M, const DevParams& P, cons
   store_state<T>(B.state, N, e, s);
 }
 
-// the fused decimation step (gs_pd_args, include/gymsim.h) for env e
-template <class T, bool TERR, int LB>
-GS_HD void pd_step_env(const DevModel* __restrict__ M, const DevParams& P, const SimBuffers& B, const PdDev& A, int e,
-                       float* lds) {
+// PD torques of the fused decimation step for env e (anymal_terrain.py:444-446); the first evaluation
+// of a launch reads the dof tensor the task holds (refreshed after the previous step's decimation
+// loop, or written by reset_idx)
+template <class T>
+GS_HD void pd_torques(const PdDev& A, int e, const EnvState<T>& s, bool first, float* tau) {
+  constexpr int ND = T::ND;
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    const float qj = first ? A.dof_state_in[((size_t)e * ND + j) * 2 + 0] : s.q[j];
+    const float qdj = first ? A.dof_state_in[((size_t)e * ND + j) * 2 + 1] : s.qd[j];
+    const float aj = A.actions[(size_t)e * ND + j];
+    tau[j] = clampf(A.kp * (A.scale * aj + A.default_pos[j] - qj) - A.kd * qdj, -A.tlim, A.tlim);
+  }
+}
+template <class T>
+GS_HD void pd_dof_out(const PdDev& A, int e, const EnvState<T>& s) {
+  constexpr int ND = T::ND;
+  if (!A.dof_out) return;
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    A.dof_out[((size_t)e * ND + j) * 2 + 0] = s.q[j];
+    A.dof_out[((size_t)e * ND + j) * 2 + 1] = s.qd[j];
+  }
+}
+// end of the fused step: state, last torques, the actions copy, root and contact tensors
+template <class T>
+GS_HD void pd_outputs(const DevModel* __restrict__ M, const DevParams& P, const SimBuffers& B, const PdDev& A, int e,
+                      const EnvState<T>& s, const float* tau) {
   const int N = B.N;
   constexpr int ND = T::ND;
-  EnvState<T> s;
-  load_state<T>(B.state, N, e, s);
-  float tau[ND];
-  // one call site for the substep so it is inlined once
-  const int sub = P.substeps;
-  const int n_pd = A.decimation * sub;
-  const int total = (A.decimation + A.extra) * sub;
-  for (int it = 0; it < total; ++it) {
-    if (it < n_pd && (it % sub) == 0) {
-      // the first PD evaluation reads the dof tensor the task holds (refreshed after the previous
-      // step's decimation loop, or written by reset_idx): anymal_terrain.py:444
-      const bool first = it == 0;
-#pragma unroll
-      for (int j = 0; j < ND; ++j) {
-        const float qj = first ? A.dof_state_in[((size_t)e * ND + j) * 2 + 0] : s.q[j];
-        const float qdj = first ? A.dof_state_in[((size_t)e * ND + j) * 2 + 1] : s.qd[j];
-        const float aj = A.actions[(size_t)e * ND + j];
-        tau[j] = clampf(A.kp * (A.scale * aj + A.default_pos[j] - qj) - A.kd * qdj, -A.tlim, A.tlim);
-      }
-    }
-    const bool last = ((it % sub) == sub - 1) && P.collect;
-    substep<T, TERR, LB>(M, P, s, tau, B.mu, N, e, lds, B.cf, last, it == total - 1 ? B.sens : nullptr);
-    if (it == n_pd - 1 && A.dof_out) {
-#pragma unroll
-      for (int j = 0; j < ND; ++j) {
-        A.dof_out[((size_t)e * ND + j) * 2 + 0] = s.q[j];
-        A.dof_out[((size_t)e * ND + j) * 2 + 1] = s.qd[j];
-      }
-    }
-  }
   store_state<T>(B.state, N, e, s);
 #pragma unroll
   for (int j = 0; j < ND; ++j) A.torques_out[(size_t)e * ND + j] = tau[j];
@@ -841,6 +902,27 @@ GS_HD void pd_step_env(const DevModel* __restrict__ M, const DevParams& P, const
 #pragma unroll
       for (int k = 0; k < 3; ++k) A.cf_out[((size_t)e * T::NR + b) * 3 + k] = B.cf[(3 * b + k) * N + e];
   }
+}
+
+// the fused decimation step (gs_pd_args, include/gymsim.h) for env e
+template <class T, bool TERR, int LB>
+GS_HD void pd_step_env(const DevModel* __restrict__ M, const DevParams& P, const SimBuffers& B, const PdDev& A, int e,
+                       float* lds) {
+  const int N = B.N;
+  EnvState<T> s;
+  load_state<T>(B.state, N, e, s);
+  float tau[T::ND];
+  // one call site for the substep so it is inlined once
+  const int sub = P.substeps;
+  const int n_pd = A.decimation * sub;
+  const int total = (A.decimation + A.extra) * sub;
+  for (int it = 0; it < total; ++it) {
+    if (it < n_pd && (it % sub) == 0) pd_torques<T>(A, e, s, it == 0, tau);
+    const bool last = ((it % sub) == sub - 1) && P.collect;
+    substep<T, TERR, LB>(M, P, s, tau, B.mu, N, e, lds, B.cf, last, it == total - 1 ? B.sens : nullptr);
+    if (it == n_pd - 1) pd_dof_out<T>(A, e, s);
+  }
+  pd_outputs<T>(M, P, B, A, e, s, tau);
 }
 
 // refresh_actor_root_state_tensor row e: SoA state -> [13] with the root link COM velocity
