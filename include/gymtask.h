@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GT_ABI_VERSION 1
+#define GT_ABI_VERSION 2
 #define GT_ANYMAL_NUM_TERMS 13  /* lin_vel_xy lin_vel_z ang_vel_z ang_vel_xy orient torques joint_acc
                                    base_height air_time collision stumble action_rate hip */
 
@@ -115,17 +115,38 @@ typedef struct gt_anymal_reset_draws {
     float cmd_x_range, cmd_x_lower, cmd_y_range, cmd_y_lower, cmd_h_range, cmd_h_lower;
 } gt_anymal_reset_draws;
 
-/* reset_idx (plane terrain) for the k envs the last post_a flagged, without the host knowing
+/* The trimesh terrain's part of reset_idx (ABI 2; custom origins, anymal_terrain.py:385-398 with
+ * update_terrain_level :427-435): before the reset, an env that walked less than a quarter of its
+ * commanded distance over the episode moves a level down, one that left its tile a level up
+ * (clip >= 0, modulo env_rows; only when update_levels = init_done && curriculum), and takes the
+ * origin terrain_origins[level][type]; the root then starts at base_init_state + origin with x, y
+ * offset by U(-0.5, 0.5) draws (drawn after the dof draws, before the command draws).
+ * episode_out[13] additionally receives mean(terrain_levels) over all envs (extras["episode"]
+ * ["terrain_level"]). */
+typedef struct gt_anymal_terrain_reset {
+    int64_t *terrain_levels;          /* [N]                   */
+    const int64_t *terrain_types;     /* [N]                   */
+    float *env_origins;               /* [N][3]                */
+    const float *terrain_origins;     /* [env_rows][env_cols][3] */
+    int32_t env_rows, env_cols, update_levels;
+    float env_length, max_episode_length_s;
+    const float *u_root_xy;           /* [k][2] drawn buffer, or NULL: use the plan */
+    gt_torch_rand_plan plan_root_xy;
+    float xy_range, xy_lower;
+} gt_anymal_terrain_reset;
+
+/* reset_idx for the k envs the last post_a flagged, without the host knowing
  * which: envs are ranked by index from reset_masks (torch.nonzero's order), row t of the draws
  * goes to the t-th flagged env.  env_ids_out int32[k] receives the flagged ids ascending (for
  * set_*_tensor_indexed); episode_out[13] = mean over the flagged envs of each episode sum /
  * episode_length_s (extras["episode"], :416-420), sums then zeroed; the means are summed in a
- * fixed order (bit-identical run to run).  scratch: GT_ANYMAL_RESET_SCRATCH_WORDS(num_envs) words
+ * fixed order (bit-identical run to run).  terrain: NULL for the plane, else the trimesh part above.  scratch: GT_ANYMAL_RESET_SCRATCH_WORDS(num_envs) words
  * of device memory, the first 16 zero-initialised (a counter the kernel re-arms). */
-#define GT_ANYMAL_RESET_SCRATCH_WORDS(num_envs) (16 + GT_ANYMAL_NUM_TERMS * (((num_envs) + 63) / 64))
+#define GT_ANYMAL_RESET_SCRATCH_WORDS(num_envs) (16 + (GT_ANYMAL_NUM_TERMS + 1) * (((num_envs) + 63) / 64))
 int gt_anymal_reset_flagged(const gt_anymal_params *p, const gt_anymal_buffers *b, int k,
-                            const gt_anymal_reset_draws *draws, int32_t *env_ids_out, float *episode_out,
-                            float episode_length_s, void *scratch, void *stream);
+                            const gt_anymal_reset_draws *draws, const struct gt_anymal_terrain_reset *terrain,
+                            int32_t *env_ids_out, float *episode_out, float episode_length_s, void *scratch,
+                            void *stream);
 
 /* Pinned, device-mapped, coherent host memory for host_count (hipHostMalloc). */
 int gt_host_alloc(uint64_t bytes, void **host_ptr, void **device_ptr);

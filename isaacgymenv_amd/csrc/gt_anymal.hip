@@ -311,7 +311,8 @@ __global__ void __launch_bounds__(64 * GT_ANYMAL_NUM_TERMS) k_episode_sums(gt_an
 // per env, one wave per workgroup; the rank of a flagged env among all flagged envs comes from
 // post_a's per-wave ballots (exclusive prefix of popcounts), so no compaction pass is needed.
 __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_anymal_buffers b, int k,
-                                                      gt_anymal_reset_draws d, int32_t* __restrict__ ids_out,
+                                                      gt_anymal_reset_draws d, gt_anymal_terrain_reset tr,
+                                                      bool has_terrain, int32_t* __restrict__ ids_out,
                                                       float* __restrict__ ep_out, float len_s,
                                                       float* __restrict__ partial, unsigned* __restrict__ done) {
   const int lane = threadIdx.x;
@@ -328,10 +329,10 @@ __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_any
   const size_t N = p.num_envs;
   // The wave's draws (2*nd + 3 per flagged env) are evaluated by all 64 lanes and exchanged
   // through LDS: one Philox chain per lane instead of 2*nd + 3 serial ones per flagged lane.
-  constexpr int kMaxDraws = 2 * 16 + 3;
+  constexpr int kMaxDraws = 2 * 16 + 3 + 2;
   __shared__ float u_lds[64 * kMaxDraws];
   const int m = (int)__popcll(mine);
-  const int D = 2 * nd + 3;
+  const int D = 2 * nd + 3 + (has_terrain ? 2 : 0);  // pos | vel | cmd x, y, heading | root x, y
   for (int s = lane; s < m * D; s += 64) {
     const int r = s / D, c = s - (s / D) * D;
     const int t = base + r;
@@ -342,7 +343,11 @@ __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_any
       u = d.u_vel ? d.u_vel[q] : torch_philox::rand_at(d.plan_vel, q);
     } else if (c == 2 * nd) u = d.u_cmd_x ? d.u_cmd_x[t] : torch_philox::rand_at(d.plan_cmd_x, t);
     else if (c == 2 * nd + 1) u = d.u_cmd_y ? d.u_cmd_y[t] : torch_philox::rand_at(d.plan_cmd_y, t);
-    else u = d.u_cmd_h ? d.u_cmd_h[t] : torch_philox::rand_at(d.plan_cmd_h, t);
+    else if (c == 2 * nd + 2) u = d.u_cmd_h ? d.u_cmd_h[t] : torch_philox::rand_at(d.plan_cmd_h, t);
+    else {
+      const size_t q = (size_t)t * 2 + (c - 2 * nd - 3);
+      u = tr.u_root_xy ? tr.u_root_xy[q] : torch_philox::rand_at(tr.plan_root_xy, q);
+    }
     u_lds[s] = u;
   }
   __syncthreads();
@@ -361,7 +366,32 @@ __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_any
       ds[2 * j + 1] = vel;
     }
     float* root = b.root_states + (size_t)e * 13;
-    for (int j = 0; j < 13; ++j) root[j] = p.base_init_state[j];
+    if (has_terrain) {
+      // update_terrain_level (:427-435) on the state BEFORE the reset, then the origin of the new level
+      long long lvl = tr.terrain_levels[e];
+      if (tr.update_levels) {
+        const float dx = root[0] - tr.env_origins[(size_t)e * 3 + 0];
+        const float dy = root[1] - tr.env_origins[(size_t)e * 3 + 1];
+        const float dist = sqrtf(dx * dx + dy * dy);
+        const float c0 = b.commands[(size_t)e * 4 + 0], c1 = b.commands[(size_t)e * 4 + 1];
+        const float cn = sqrtf(c0 * c0 + c1 * c1);
+        lvl -= (dist < cn * tr.max_episode_length_s * 0.25f) ? 1 : 0;
+        lvl += (dist > tr.env_length / 2.0f) ? 1 : 0;
+        lvl = (lvl < 0 ? 0 : lvl) % tr.env_rows;
+        tr.terrain_levels[e] = lvl;
+        const long long ty = tr.terrain_types[e];
+        for (int j = 0; j < 3; ++j)
+          tr.env_origins[(size_t)e * 3 + j] = tr.terrain_origins[((size_t)lvl * tr.env_cols + ty) * 3 + j];
+      }
+      float o[3];
+      for (int j = 0; j < 3; ++j) o[j] = tr.env_origins[(size_t)e * 3 + j];
+      for (int j = 0; j < 13; ++j) root[j] = p.base_init_state[j];
+      for (int j = 0; j < 3; ++j) root[j] = root[j] + o[j];
+      root[0] = root[0] + (tr.xy_range * u[2 * nd + 3] + tr.xy_lower);
+      root[1] = root[1] + (tr.xy_range * u[2 * nd + 4] + tr.xy_lower);
+    } else {
+      for (int j = 0; j < 13; ++j) root[j] = p.base_init_state[j];
+    }
     float cmd[4];
     const float ux = u[2 * nd], uy = u[2 * nd + 1], uh = u[2 * nd + 2];
     cmd[0] = d.cmd_x_range * ux + d.cmd_x_lower;
@@ -387,11 +417,19 @@ __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_any
   // Episode means, deterministic: every wave publishes its 13 wave sums (zeros when nothing was
   // flagged) to its own slot of `partial`; the last wave to finish adds the slots in wave order.
   // Agent-scope atomic stores / loads: the waves run on different XCDs, whose L2s are not coherent.
+  // slot NT (terrain): the wave's sum of terrain levels after the update, for mean(terrain_levels)
+  constexpr int NT = GT_ANYMAL_NUM_TERMS + 1;
 #pragma unroll
   for (int i = 0; i < GT_ANYMAL_NUM_TERMS; ++i) {
     const float s = mine ? wave_sum(term[i]) : 0.0f;
-    if (lane == i) __hip_atomic_store(&partial[(size_t)w * GT_ANYMAL_NUM_TERMS + i], s, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == i) __hip_atomic_store(&partial[(size_t)w * NT + i], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (has_terrain) {
+    // integer levels: the float sums are exact in any order (< 2^24)
+    const float lv = wave_sum(e < p.num_envs ? (float)tr.terrain_levels[e] : 0.0f);
+    if (lane == 0)
+      __hip_atomic_store(&partial[(size_t)w * NT + GT_ANYMAL_NUM_TERMS], lv, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
   unsigned old = 0;
   __threadfence();
@@ -399,12 +437,15 @@ __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_any
   old = __shfl(old, 0, 64);
   if (old == gridDim.x - 1) {  // last wave: finalise the 13 terms in parallel lanes
     __threadfence();
-    if (lane < GT_ANYMAL_NUM_TERMS) {
+    if (lane < GT_ANYMAL_NUM_TERMS + (has_terrain ? 1 : 0)) {
       float v = 0.0f;
       for (int q = 0; q < (int)gridDim.x; ++q)
-        v += __hip_atomic_load(&partial[(size_t)q * GT_ANYMAL_NUM_TERMS + lane], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-      ep_out[lane] = (v / (float)k) / len_s;  // torch.mean(sums[env_ids]) / max_episode_length_s
+        v += __hip_atomic_load(&partial[(size_t)q * NT + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane < GT_ANYMAL_NUM_TERMS)
+        // torch.mean(sums[env_ids]) / max_episode_length_s: mean = sum * (1/k), / scalar = * (1/scalar)
+        ep_out[lane] = (v * (1.0f / (float)k)) * (1.0f / len_s);
+      else
+        ep_out[lane] = v * (1.0f / (float)p.num_envs);  // torch.mean(terrain_levels.float())
     }
     if (lane == 0) *done = 0u;
   }
@@ -506,7 +547,10 @@ __global__ void __launch_bounds__(256) k_measure_heights(const int16_t* __restri
   (void)tz;
   px += border;
   py += border;
-  long ix = (long)(px / hs), iy = (long)(py / hs);
+  // torch on the GPU divides by a host scalar as a multiplication by its float reciprocal
+  // (ATen div_true with a CPU scalar): (pts / hs).long() is trunc(p * (1 / hs))
+  const float inv_hs = 1.0f / hs;
+  long ix = (long)(px * inv_hs), iy = (long)(py * inv_hs);
   ix = ix < 0 ? 0 : (ix > rows - 2 ? rows - 2 : ix);
   iy = iy < 0 ? 0 : (iy > cols - 2 ? cols - 2 : iy);
   const int h1 = hf[(size_t)ix * cols + iy];
@@ -604,18 +648,25 @@ int gt_anymal_post_physics_b(const gt_anymal_params* p, const gt_anymal_buffers*
 }
 
 int gt_anymal_reset_flagged(const gt_anymal_params* p, const gt_anymal_buffers* b, int k,
-                            const gt_anymal_reset_draws* d, int32_t* env_ids_out, float* episode_out,
-                            float episode_length_s, void* scratch, void* stream) {
+                            const gt_anymal_reset_draws* d, const gt_anymal_terrain_reset* terrain,
+                            int32_t* env_ids_out, float* episode_out, float episode_length_s, void* scratch,
+                            void* stream) {
   if (check_params(p)) return -1;
   if (!b->reset_masks || !d || !env_ids_out || !episode_out || !scratch || k < 0 || k > p->num_envs) {
     g_err = "gt_anymal_reset_flagged: invalid arguments";
     return -1;
   }
+  if (terrain && (!terrain->terrain_levels || !terrain->terrain_types || !terrain->env_origins ||
+                  !terrain->terrain_origins || terrain->env_rows <= 0 || terrain->env_cols <= 0)) {
+    g_err = "gt_anymal_reset_flagged: incomplete terrain reset";
+    return -1;
+  }
+  const gt_anymal_terrain_reset tr = terrain ? *terrain : gt_anymal_terrain_reset{};
   if (k == 0) return 0;
   unsigned* done = static_cast<unsigned*>(scratch);
   float* partial = static_cast<float*>(scratch) + 16;
   hipLaunchKernelGGL(k_reset_flagged, dim3((p->num_envs + 63) / 64), dim3(64), 0, (hipStream_t)stream, *p, *b, k,
-                     *d, env_ids_out, episode_out, episode_length_s, partial, done);
+                     *d, tr, terrain != nullptr, env_ids_out, episode_out, episode_length_s, partial, done);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("gt_anymal_reset_flagged", e);
 }

@@ -77,6 +77,13 @@ class GtAnymalResetDraws(C.Structure):
                                  "cmd_y_range", "cmd_y_lower", "cmd_h_range", "cmd_h_lower")]
 
 
+class GtAnymalTerrainReset(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("terrain_levels", "terrain_types", "env_origins", "terrain_origins")] + [
+        (n, C.c_int32) for n in ("env_rows", "env_cols", "update_levels")] + [
+        ("env_length", C.c_float), ("max_episode_length_s", C.c_float), ("u_root_xy", C.c_void_p),
+        ("plan_root_xy", GtTorchRandPlan), ("xy_range", C.c_float), ("xy_lower", C.c_float)]
+
+
 class GtHoundControlParams(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("num_envs", "nv", "num_links", "jac_row", "eef_link", "arm_control_stride")] + [
         (n, C.c_float) for n in ("kp", "kd", "action_scale", "torque_limit", "arm_action_scale")] + [
@@ -114,8 +121,8 @@ def lib():
                            "gt_anymal_reset": [P, B, vp, i, vp, vp, vp, vp, vp, vp, vp],
                            "gt_anymal_post_physics_b": [P, B, vp, C.POINTER(GtTorchRandPlan), vp],
                            "gt_torch_rand": [C.POINTER(GtTorchRandPlan), vp, vp],
-                           "gt_anymal_reset_flagged": [P, B, i, C.POINTER(GtAnymalResetDraws), vp, vp, C.c_float,
-                                                       vp, vp],
+                           "gt_anymal_reset_flagged": [P, B, i, C.POINTER(GtAnymalResetDraws),
+                                                       C.POINTER(GtAnymalTerrainReset), vp, vp, C.c_float, vp, vp],
                            "gt_host_alloc": [C.c_uint64, C.POINTER(vp), C.POINTER(vp)],
                            "gt_host_free": [vp],
                            "gt_wait_host_seq": [vp, C.c_int32, C.c_int32, C.POINTER(C.c_int32)],
@@ -300,7 +307,8 @@ class AnymalTailKernels:
         self.reset_count = torch.zeros(3, dtype=torch.int32, device=dev)  # accumulator, wg counter, last count
         self.reset_masks = torch.zeros((N + 63) // 64, dtype=torch.int64, device=dev)
         # GT_ANYMAL_RESET_SCRATCH_WORDS: re-armed counter (16 words) + per-wave episode partial sums
-        self.reset_scratch = torch.zeros(16 + len(self.TERMS) * ((N + 63) // 64), dtype=torch.float32, device=dev)
+        self.reset_scratch = torch.zeros(16 + (len(self.TERMS) + 1) * ((N + 63) // 64), dtype=torch.float32,
+                                         device=dev)
         # {count, seq} published by post_a straight into pinned host memory (gt_wait_host_seq)
         h, d = C.c_void_p(), C.c_void_p()
         _check(L.gt_host_alloc(8, C.byref(h), C.byref(d)), "gt_host_alloc")
@@ -445,14 +453,16 @@ class AnymalTailKernels:
         self._keep = (ids, pos_offset, vel, cx, cy, ch)
 
     def reset_flagged(self, k: int, rand_unit=None):
-        """reset_idx for the k envs the last post_a flagged (plane terrain), in one kernel.
+        """reset_idx for the k envs the last post_a flagged, in one kernel (plane and trimesh terrain).
 
         Draws u ~ U[0,1) with ``rand_unit(shape, device)`` in the reference's order and shapes
-        (anymal_terrain.py:385-398: dof offsets, dof velocities, cmd x, cmd y, cmd heading), so the
-        RNG stream advances exactly as torch_rand_float's would; the kernel applies the affine
-        maps, ranks the flagged envs (nonzero order) and fills extras["episode"]."""
+        (anymal_terrain.py:385-398: dof offsets, dof velocities, [trimesh: root x, y], cmd x, cmd y,
+        cmd heading), so the RNG stream advances exactly as torch_rand_float's would; the kernel
+        applies the affine maps, the trimesh curriculum (update_terrain_level, :427-435), ranks the
+        flagged envs (nonzero order) and fills extras["episode"]."""
         t = self.task
         dev, nd = t.device, t.num_dof
+        tr = self._terrain_reset() if t.custom_origins else None
         d = self._draws
         if d is None:  # the affine maps are fixed per task
             d = self._draws = GtAnymalResetDraws()
@@ -463,23 +473,54 @@ class AnymalTailKernels:
         if self.inkernel_rng:
             u = None
             d.u_pos = d.u_vel = d.u_cmd_x = d.u_cmd_y = d.u_cmd_h = None
-            d.plan_pos, d.plan_vel, d.plan_cmd_x, d.plan_cmd_y, d.plan_cmd_h = self.planner.plan_many(
-                (k * nd, k * nd, k, k, k))
+            if tr is None:
+                d.plan_pos, d.plan_vel, d.plan_cmd_x, d.plan_cmd_y, d.plan_cmd_h = self.planner.plan_many(
+                    (k * nd, k * nd, k, k, k))
+            else:
+                tr.u_root_xy = None
+                (d.plan_pos, d.plan_vel, tr.plan_root_xy, d.plan_cmd_x, d.plan_cmd_y,
+                 d.plan_cmd_h) = self.planner.plan_many((k * nd, k * nd, 2 * k, k, k, k))
         else:
             u = [rand_unit((k, nd), dev), rand_unit((k, nd), dev)]
+            if tr is not None:
+                u.append(rand_unit((k, 2), dev))
             u += [rand_unit((k, 1), dev) for _ in range(3)]
-            d.u_pos, d.u_vel, d.u_cmd_x, d.u_cmd_y, d.u_cmd_h = (x.data_ptr() for x in u)
+            d.u_pos, d.u_vel = u[0].data_ptr(), u[1].data_ptr()
+            d.u_cmd_x, d.u_cmd_y, d.u_cmd_h = (x.data_ptr() for x in u[-3:])
+            if tr is not None:
+                tr.u_root_xy = u[2].data_ptr()
         ids = torch.empty(k, dtype=torch.int32, device=dev)
-        ep = torch.empty(len(self.TERMS), dtype=torch.float32, device=dev)
-        _check(lib().gt_anymal_reset_flagged(self.p, self._buffers(), k, d, ids.data_ptr(), ep.data_ptr(),
+        ep = torch.empty(len(self.TERMS) + 1, dtype=torch.float32, device=dev)
+        _check(lib().gt_anymal_reset_flagged(self.p, self._buffers(), k, d, tr, ids.data_ptr(), ep.data_ptr(),
                                              float(t.max_episode_length_s), self.reset_scratch.data_ptr(),
                                              self._stream()), "gt_anymal_reset_flagged")
         t._set_reset_state(ids)
-        t.extras["episode"] = dict(zip(self._ep_keys, ep.unbind()))
-        if self._terrain_level is None:
-            self._terrain_level = torch.mean(t.terrain_levels.float())
-        t.extras["episode"]["terrain_level"] = self._terrain_level
+        t.extras["episode"] = dict(zip(self._ep_keys, ep[:len(self.TERMS)].unbind()))
+        if tr is not None:
+            t.extras["episode"]["terrain_level"] = ep[len(self.TERMS)]
+        else:
+            if self._terrain_level is None:
+                self._terrain_level = torch.mean(t.terrain_levels.float())
+            t.extras["episode"]["terrain_level"] = self._terrain_level
         self._keep = (u, ids)
+
+    def _terrain_reset(self):
+        """gt_anymal_terrain_reset over the task's curriculum tensors (rebuilt when the task rebinds one)."""
+        t = self.task
+        cur = (t.terrain_levels, t.terrain_types, t.env_origins, t.terrain_origins)
+        tr = getattr(self, "_tr", None)
+        if tr is None or any(x is not y for x, y in zip(cur, self._tr_bound)):
+            for x, dt in zip(cur, (torch.int64, torch.int64, torch.float32, torch.float32)):
+                assert x.is_contiguous() and x.dtype == dt and x.device.type == "cuda"
+            tr = GtAnymalTerrainReset()
+            tr.terrain_levels, tr.terrain_types, tr.env_origins, tr.terrain_origins = (x.data_ptr() for x in cur)
+            tr.env_rows, tr.env_cols = int(t.terrain.env_rows), int(t.terrain.env_cols)
+            tr.env_length = float(t.terrain.env_length)
+            tr.max_episode_length_s = float(t.max_episode_length_s)
+            tr.xy_range, tr.xy_lower = 1.0, -0.5  # torch_rand_float(-0.5, 0.5, (k, 2)), :396
+            self._tr, self._tr_bound = tr, cur
+        tr.update_levels = int(bool(t.init_done and t.curriculum))
+        return tr
 
     def post_b(self, noise, noise_plan=None):
         """Observations (+noise), history buffers, and VecTask's time_outs / clamped obs (vec_task.py:393-402)."""

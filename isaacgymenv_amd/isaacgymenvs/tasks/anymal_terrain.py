@@ -467,10 +467,7 @@ class AnymalTerrain(VecTask):
                 k = kern.last_reset_count
                 if snap is not None:
                     kern.rng_restore(snap)
-                if self.custom_origins:
-                    self.reset_idx(self.reset_buf.nonzero(as_tuple=False).flatten())
-                else:
-                    kern.reset_flagged(k, torch_rand_unit)  # reset_idx without nonzero / host sync
+                kern.reset_flagged(k, torch_rand_unit)  # reset_idx without nonzero / host sync
                 kern.observe()
             return
         self.progress_buf += 1

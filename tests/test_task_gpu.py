@@ -37,6 +37,8 @@ def _snapshot(env):
     s["sim_cf"] = env.sim.cf_soa.clone()
     s["rng"] = torch.cuda.get_rng_state()
     s["counter"] = env.common_step_counter
+    if env.custom_origins:
+        s["terrain"] = (env.terrain_levels.clone(), env.env_origins.clone())
     return s
 
 
@@ -52,6 +54,9 @@ def _restore(env, s):
     env.sim.cf_soa.copy_(s["sim_cf"])
     torch.cuda.set_rng_state(s["rng"])
     env.common_step_counter = s["counter"]
+    if "terrain" in s:
+        env.terrain_levels.copy_(s["terrain"][0])
+        env.env_origins.copy_(s["terrain"][1])
 
 
 def test_fused_step_equals_unfused_sequence(monkeypatch):
@@ -86,12 +91,23 @@ def test_fused_step_equals_unfused_sequence(monkeypatch):
         H.assert_mostly_close(c(r2), c(r1), atol=1e-4, rtol=1e-2, max_frac=2e-3, what="reward")
 
 
-def test_kernel_tail_equals_torch_tail_across_resets(monkeypatch):
+TRIMESH = {"task.env.terrain.terrainType": "trimesh", "task.env.terrain.numLevels": 4,
+           "task.env.terrain.numTerrains": 8}
+
+
+@pytest.mark.parametrize("terrain", ["plane", "trimesh"])
+def test_kernel_tail_equals_torch_tail_across_resets(terrain, monkeypatch):
     """The fused tail (post_a -> optimistic noise/post_b -> RNG rollback + reset_idx + post_b on
     reset steps) against the reference's torch statements, same physics kernel and same CUDA
-    RNG stream, over 5-step episodes so that most steps reset someone."""
+    RNG stream, over 5-step episodes so that most steps reset someone.  Trimesh: the fused reset
+    also runs the terrain curriculum (update_terrain_level, new origins, root x/y draws) and the
+    terrain-level mean."""
     n = 256
-    env = _make("AnymalTerrain", n, monkeypatch, **{"task.env.learn.episodeLength_s": 0.1})
+    over = {"task.env.learn.episodeLength_s": 0.1}
+    if terrain == "trimesh":
+        over.update(TRIMESH)
+    env = _make("AnymalTerrain", n, monkeypatch, **over)
+    assert env.custom_origins == (terrain == "trimesh")
     assert env.max_episode_length in (5, 6)
     gen = torch.Generator(device="cuda:0").manual_seed(9)
     acts = [2 * torch.rand((n, 12), device="cuda:0", generator=gen) - 1 for _ in range(12)]
@@ -110,7 +126,8 @@ def test_kernel_tail_equals_torch_tail_across_resets(monkeypatch):
             res.append((obs["obs"].clone(), rew.clone(), reset.clone(), extras["time_outs"].clone(),
                         None if ep is None else torch.stack([torch.as_tensor(v, device="cuda:0").float()
                                                              for v in ep.values()]),
-                        env.root_states.clone()))
+                        env.root_states.clone(),
+                        env.terrain_levels.clone() if env.custom_origins else None))
             env.extras.pop("episode", None)
         out[mode] = res
     env._kernels = kernels
@@ -125,6 +142,8 @@ def test_kernel_tail_equals_torch_tail_across_resets(monkeypatch):
         if a[4] is not None:
             torch.testing.assert_close(a[4], b[4], rtol=1e-4, atol=1e-7, msg=f"episode extras step {t}")
         torch.testing.assert_close(a[5], b[5], rtol=1e-5, atol=1e-5, msg=f"root states step {t}")
+        if a[6] is not None:
+            assert torch.equal(a[6], b[6]), f"terrain levels step {t}"
     assert n_reset_steps >= 2
 
 
