@@ -29,8 +29,10 @@ class FakeSim:
 class FakeGym(_g.Gym):
     """Pure-python Gym whose simulate() is a seeded deterministic rule."""
 
-    def __init__(self, seed: int = 12345, dof_drift: float = 0.0, z_drift: float = 0.0, xy_drift: float = 0.0):
+    def __init__(self, seed: int = 12345, dof_drift: float = 0.0, z_drift: float = 0.0, xy_drift: float = 0.0,
+                 base_contact_p: float = 0.01):
         self.seed = seed
+        self.base_contact_p = base_contact_p  # chance per simulate of a base contact (a fall -> reset)
         self.xy_drift = xy_drift    # walks even envs along +x (exercises terrain-level curriculum)
         self.dof_drift = dof_drift  # pushes joints out of range over time (exercises limit resets)
         self.z_drift = z_drift      # sinks random roots (exercises height terminations)
@@ -99,7 +101,7 @@ class FakeGym(_g.Gym):
         quat = sim.root[:, 3:7] + t32(rng.normal(0, 0.01, (N, 4)))
         sim.root[:, 3:7] = quat / quat.norm(dim=1, keepdim=True)
         cf = np.zeros((N, nb, 3), dtype=np.float32)
-        cf[:, 0, 2] = np.where(rng.rand(N) < 0.01, 5.0, 0.0)
+        cf[:, 0, 2] = np.where(rng.rand(N) < self.base_contact_p, 5.0, 0.0)
         for k in self.knees:
             cf[:, k, :] = np.where(rng.rand(N, 1) < 0.05, np.array([[2.0, 1.0, 3.0]]), 0.0)
         for k in self.feet:

@@ -24,8 +24,12 @@ def _close(a, b, what, rtol=1e-5, atol=2e-6):
                                err_msg=what)
 
 
-def test_fused_tail_kernels_match_reference_golden(monkeypatch):
-    d = np.load(os.path.join(GOLDEN, "anymal_terrain.npz"))
+@pytest.mark.parametrize("fixture", ["anymal_terrain.npz", "anymal_terrain_long.npz"])
+def test_fused_tail_kernels_match_reference_golden(fixture, monkeypatch):
+    """anymal_terrain.npz: 32 envs x 30 consecutive steps (short episodes, frequent pushes);
+    anymal_terrain_long.npz: 64 envs with the DEFAULT pushInterval_s / episodeLength_s, stored at
+    every 50th step of a 1010-step run plus the steps around the push (749) and the episode end (998)."""
+    d = np.load(os.path.join(GOLDEN, fixture))
     cfg = yaml.safe_load(str(d["cfg_yaml"]))
     cfg["sim"]["use_gpu_pipeline"] = True
     from isaacgymenv_amd.isaacgymenvs.tasks import anymal_terrain as at

@@ -69,6 +69,45 @@ def test_anymal_terrain_matches_reference(fake_gym):
             _close(got, d["ep_extras"][t], f"extras episode step {t}", rtol=1e-5, atol=1e-7)
 
 
+def test_anymal_terrain_long_matches_reference(fake_gym):
+    """Default pushInterval_s (push at step 749) and episodeLength_s (done at progress 999 -> step 998),
+    64 envs x 1010 steps on the fake, compared at the fixture's stored steps (make_golden.KEEP_LONG)."""
+    d = np.load(os.path.join(GOLDEN, "anymal_terrain_long.npz"))
+    fake_gym(FakeGym(base_contact_p=2e-5))  # make_golden.LONG_FAKE
+    from isaacgymenv_amd.isaacgymenvs.tasks.anymal_terrain import AnymalTerrain
+    cfg = yaml.safe_load(str(d["cfg_yaml"]))
+    assert cfg["env"]["learn"]["pushInterval_s"] == 15 and cfg["env"]["learn"]["episodeLength_s"] == 20
+    torch.manual_seed(42)
+    env = AnymalTerrain(copy.deepcopy(cfg), "cpu", "cpu", -1, True, False, False)
+    steps = [int(x) for x in d["steps"]]
+    assert 749 in steps and 998 in steps and steps[-1] >= 1000
+    rng = np.random.RandomState(7)
+    actions = (2 * rng.rand(steps[-1] + 1, env.num_envs, 12) - 1).astype(np.float32)
+    np.testing.assert_array_equal(actions[steps], d["actions"])
+    terms = [str(t) for t in d["terms"]]
+    pos = {s_: i for i, s_ in enumerate(steps)}
+    for t in range(steps[-1] + 1):
+        env.extras.pop("episode", None)
+        obs, rew, reset, extras = env.step(torch.from_numpy(actions[t]))
+        if t not in pos:
+            continue
+        i = pos[t]
+        np.testing.assert_array_equal(reset.numpy().astype(np.int64), d["reset"][i], err_msg=f"reset step {t}")
+        np.testing.assert_array_equal(extras["time_outs"].numpy().astype(np.int64), d["time_outs"][i])
+        np.testing.assert_array_equal(env.progress_buf.numpy(), d["progress"][i], err_msg=f"progress step {t}")
+        _close(rew.numpy(), d["rew"][i], f"reward step {t}")
+        _close(obs["obs"].numpy(), d["obs"][i], f"obs step {t}")
+        _close(env.commands.numpy(), d["commands"][i], f"commands step {t}")
+        _close(np.stack([env.episode_sums[k].numpy() for k in terms]), d["episode_sums"][i], f"episode sums {t}")
+        if d["ep_mask"][i]:
+            got = np.array([float(extras["episode"]["rew_" + k]) for k in terms] +
+                           [float(extras["episode"]["terrain_level"])])
+            _close(got, d["ep_extras"][i], f"extras episode step {t}", rtol=1e-5, atol=1e-7)
+    # the envs still in their first episode reset at progress 999 = step 998 (anymal_terrain.py:299)
+    first = d["progress"][pos[997]] == 998
+    assert first.sum() > 32 and d["reset"][pos[998]][first].all() and not d["time_outs"][pos[998]].any()
+
+
 def test_cartpole_matches_reference(fake_gym):
     d = np.load(os.path.join(GOLDEN, "cartpole.npz"))
     fake_gym(FakeGym(seed=777, dof_drift=1.0))
