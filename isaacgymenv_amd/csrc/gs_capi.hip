@@ -575,6 +575,9 @@ int gs_sim_set_force_sensors(gs_sim* s, int n, const int32_t* bodies) {
   if (n < 0 || n > GS_MAXS || (n > 0 && !bodies)) return fail("gs_sim_set_force_sensors: at most 8 sensors");
   if (n > 0 && s->variant == 2)
     return fail("gs_sim_set_force_sensors: the lane-team kernel has no force sensors (use kernel_variant 1)");
+  if (n > 0 && !s->topo->sens)
+    return fail("gs_sim_set_force_sensors: topology %s is compiled without force sensors (sensors flag in "
+                "tools/gen_topologies.py MODELS)", s->topo->name);
   DevModel& h = s->h_model;
   for (int b = 0; b < GS_MAXB; ++b) h.sens_of_body[b] = -1;
   for (int i = 0; i < n; ++i) {

@@ -84,6 +84,7 @@ struct TopoEntry {
   launch_sim_fn sim;
   launch_pd_fn pd;
   int nb, nd, nc, ns;
+  int sens;  // force sensors compiled in (T::SENS)
 };
 
 // Kinematics of the reported links (gs_kinematics.hip): runtime-sized tree tables, one copy in

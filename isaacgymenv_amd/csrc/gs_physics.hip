@@ -266,6 +266,6 @@ hipError_t launch_pd(const DevModel* M, const DevParams& P, const SimBuffers& B,
   return hipGetLastError();
 }
 
-#define GS_TOPO_ENTRY(T, SIG) {SIG, T::kName, &launch_sim<T>, &launch_pd<T>, T::NB, T::ND, T::NC, T::NS},
+#define GS_TOPO_ENTRY(T, SIG) {SIG, T::kName, &launch_sim<T>, &launch_pd<T>, T::NB, T::ND, T::NC, T::NS, T::SENS ? 1 : 0},
 TopoEntry g_topologies[] = {GS_FOR_EACH_TOPOLOGY(GS_TOPO_ENTRY)};
 const int g_num_topologies = sizeof(g_topologies) / sizeof(g_topologies[0]);

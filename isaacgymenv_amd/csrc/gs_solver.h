@@ -693,8 +693,8 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
       cf_soa[(3 * b + 2) * N + e] = f2;
     }
   }
-  if (sens_soa && M->nsens > 0) {
-    // force sensors on leaf bodies: the wrench through the parent joint,
+  if constexpr (T::SENS) if (sens_soa && M->nsens > 0) {
+    // force sensors on leaf bodies (topologies compiled with T::SENS): the wrench through the parent joint,
     //   f_joint = I_b a_b + v_b x* I_b v_b - f_contact   (a_b with the gravity offset, RNEA form)
     // with a_b = A_b (velocity products + gravity) + base acceleration + sum_path S_k qdd_k, where
     // qdd = (nu_new - nu)/h and the base's spatial acceleration is (dw/h, dpdot/h - w x pdot).

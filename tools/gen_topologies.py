@@ -22,12 +22,14 @@ sys.path.insert(0, ROOT)
 from isaacgymenv_amd.isaacgym._assets import RawModel, build_articulation, PACKED_DIR  # noqa: E402
 from isaacgymenv_amd.isaacgym._model import flatten, topology_signature  # noqa: E402
 
-# (struct name, packed model, asset options as the reference task sets them)
+# (struct name, packed model, asset options as the reference task sets them, force sensors compiled in)
+# Force sensors (gym.create_asset_force_sensor) keep every body's pose and motion subspace live until
+# the end of the substep; only the topologies whose tasks create sensors (Ant, ant.py:174-178) pay for it.
 MODELS = [
-    ("anymal_c", "anymal_c.model.json", dict(collapse_fixed_joints=True, replace_cylinder_with_capsule=True)),
-    ("cartpole", "cartpole.model.json", dict(fix_base_link=True)),
-    ("nv_ant", "nv_ant.model.json", dict()),
-    ("hound", "hound.model.json", dict(collapse_fixed_joints=False)),
+    ("anymal_c", "anymal_c.model.json", dict(collapse_fixed_joints=True, replace_cylinder_with_capsule=True), False),
+    ("cartpole", "cartpole.model.json", dict(fix_base_link=True), False),
+    ("nv_ant", "nv_ant.model.json", dict(), True),
+    ("hound", "hound.model.json", dict(collapse_fixed_joints=False), False),
 ]
 
 OUT = os.path.join(ROOT, "isaacgymenv_amd", "csrc", "gs_topologies.h")
@@ -159,7 +161,7 @@ def emit() -> str:
         "",
     ]
     reg = []
-    for name, packed, opts in MODELS:
+    for name, packed, opts, sens in MODELS:
         with open(os.path.join(PACKED_DIR, packed)) as f:
             art = build_articulation(RawModel.from_json(json.load(f)), opts)
         flat = flatten(art)
@@ -176,6 +178,7 @@ def emit() -> str:
             dim = n if len(t[k]) else "1"
             lines.append(f"  static constexpr int {k}[{dim}] = {carr(vals)};")
         lines.append(f"  static constexpr int anc[NV][MAXDEP] = {carr(t['anc'])};")
+        lines.append(f"  static constexpr bool SENS = {'true' if sens else 'false'};  // force sensors compiled in")
         tm = t["TEAM"]
         if tm:
             lines.append("  // lane-team layout (gs_team.hip): LANES lanes per env, lane c owns chain c")
