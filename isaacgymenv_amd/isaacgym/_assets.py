@@ -118,6 +118,9 @@ class RawLink:
     name: str
     inertial: Optional[RawInertial]
     shapes: List[RawShape]
+    # collision <mesh> files the contact generator does not simulate (gym.load_asset
+    # warns with the link names)
+    dropped_meshes: List[str] = field(default_factory=list)
 
 
 @dataclass
@@ -159,7 +162,8 @@ class RawModel:
             if l.inertial is not None:
                 inert = {"mass": l.inertial.mass, "com": l.inertial.com.tolist(),
                          "inertia": l.inertial.inertia.tolist()}
-            links.append({"name": n, "inertial": inert, "shapes": [shp(s) for s in l.shapes]})
+            links.append({"name": n, "inertial": inert, "shapes": [shp(s) for s in l.shapes],
+                          "dropped_meshes": list(l.dropped_meshes)})
         joints = [{"name": j.name, "kind": j.kind, "parent": j.parent, "child": j.child,
                    "origin": j.origin.to_json(), "axis": j.axis.tolist(), "lower": j.lower,
                    "upper": j.upper, "has_limits": j.has_limits, "effort": j.effort,
@@ -178,7 +182,7 @@ class RawModel:
                 inert = RawInertial(l["inertial"]["mass"], np.array(l["inertial"]["com"]),
                                     np.array(l["inertial"]["inertia"]))
             shapes = [RawShape(s["kind"], Pose.from_json(s["pose"]), list(s["size"])) for s in l["shapes"]]
-            links[l["name"]] = RawLink(l["name"], inert, shapes)
+            links[l["name"]] = RawLink(l["name"], inert, shapes, list(l.get("dropped_meshes", [])))
             order.append(l["name"])
         joints = [RawJoint(j["name"], j["kind"], j["parent"], j["child"], Pose.from_json(j["origin"]),
                            np.array(j["axis"], dtype=np.float64), j["lower"], j["upper"], j["has_limits"],
@@ -230,7 +234,7 @@ def parse_urdf(path: str) -> RawModel:
                               [g("ixz"), g("iyz"), g("izz")]])
             # inertia expressed in the inertial frame -> rotate into link axes
             inert = RawInertial(mass, op.t.copy(), op.R @ I @ op.R.T)
-        shapes = []
+        shapes, dropped = [], []
         for ce in le.findall("collision"):
             op = _origin(ce)
             ge = ce.find("geometry")
@@ -246,8 +250,11 @@ def parse_urdf(path: str) -> RawModel:
                 shapes.append(RawShape(SHAPE_CAPSULE, op, [float(c.get("radius")), float(c.get("length"))]))
             elif ge.find("box") is not None:
                 shapes.append(RawShape(SHAPE_BOX, op, _floats(ge.find("box").get("size"), 3)))
-            # meshes: not supported by the plane contact generator (documented in DESIGN.md)
-        links[name] = RawLink(name, inert, shapes)
+            elif ge.find("mesh") is not None:
+                # triangle-mesh collision geometry is not simulated: recorded so
+                # that gym.load_asset can name the links it affects
+                dropped.append(ge.find("mesh").get("filename", ""))
+        links[name] = RawLink(name, inert, shapes, dropped)
         order.append(name)
     joints = []
     kinds = {"fixed": JOINT_FIXED, "revolute": JOINT_REVOLUTE, "continuous": JOINT_REVOLUTE,

@@ -24,6 +24,7 @@ import ctypes as C
 import enum
 import math
 import os
+import warnings
 from typing import List, Optional
 
 import numpy as np
@@ -32,6 +33,10 @@ from . import _assets
 from ._assets import build_articulation, load_raw, mat_to_quat_xyzw, quat_xyzw_to_mat
 from ._model import flatten
 from . import _lib
+
+class PhysicsDeviationWarning(UserWarning):
+    """A requested PhysX feature the MI355X solver does not reproduce (DESIGN.md sections 3 and 6)."""
+
 
 # ------------------------------------------------------------------ constants
 SIM_PHYSX = 0
@@ -335,6 +340,10 @@ class Sim:
         # PhysX CPU worker threads (cfg/config.yaml:30 num_threads: 4); 0 = the calling thread only
         p.num_threads = max(1, int(getattr(px, "num_threads", 0) or 0))
         self.cparams = p
+        if int(getattr(px, "solver_type", 0)) == 1:
+            warnings.warn("physx.solver_type=1 (TGS) requested: the MI355X solver runs projected Gauss-Seidel "
+                          "with split impulse (DESIGN.md section 3); num_position/velocity_iterations keep "
+                          "their PGS meaning", PhysicsDeviationWarning, stacklevel=3)
         L = _lib.lib()
         h = L.gs_sim_create(-1 if self.host else int(compute_device), p)
         if not h:
@@ -595,6 +604,10 @@ class Gym:
     def load_asset(self, sim: Sim, root: str, filename: str, options: Optional[AssetOptions] = None) -> Asset:
         options = options or AssetOptions()
         raw = load_raw(root, filename)
+        meshes = [n for n in raw.link_order if raw.links[n].dropped_meshes]
+        if meshes:
+            warnings.warn(f"{filename}: triangle-mesh collision geometry is not simulated (DESIGN.md section 6); "
+                          f"links without contacts: {', '.join(meshes)}", PhysicsDeviationWarning, stacklevel=2)
         art = build_articulation(raw, options.as_dict())
         return Asset(art, options)
 
@@ -679,6 +692,11 @@ class Gym:
         a = Actor(env, asset, pose, name, group, filter)
         env.actors.append(a)
         owner = env.sim
+        if filter == 0 and asset.art.num_bodies > 1 and not getattr(owner, "_warned_self", False):
+            owner._warned_self = True
+            warnings.warn("collision filter 0 enables self-collisions in Isaac Gym; the MI355X solver generates "
+                          "contacts against the ground and the terrain mesh only (DESIGN.md section 6)",
+                          PhysicsDeviationWarning, stacklevel=2)
         if owner.asset is None:
             owner.asset = asset
         elif owner.asset is not asset:

@@ -32,6 +32,6 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU" \
   i=$((i+1))
   timeout -s KILL 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $OUT/sq_$i -o run -- \
     $BENCH > $OUT/sq_$i.log 2>&1 || { echo "sq group $i failed: $grp"; exit 1; }
-  rm -f $OUT/sq_$i/*kernel_trace.csv
 done
-echo "sq ok"; du -sh $OUT
+echo "sq ok"
+cd $ROOT && python3 tools/counter_summary.py $OUT && du -sh $OUT
