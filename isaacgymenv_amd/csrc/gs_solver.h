@@ -32,7 +32,8 @@ GS_HD constexpr bool body_on_path(int kk, int b) {
 // TERR kernels (trimesh terrain) keep each active candidate's contact normal in 3 more slots.
 template <class T, bool TERR = false>
 struct LaneCfg {
-  static constexpr int SLOTS = T::NSLOT + (TERR ? 3 * T::NC : 0);
+  // contact rows (NSLOT), [TERR: normals 3 NC], separation NC, friction NC, impulses 3 NC
+  static constexpr int SLOTS = T::NSLOT + (TERR ? 3 * T::NC : 0) + 5 * T::NC;
   static constexpr int FIT = (SLOTS * 64 * 4 <= 160 * 1024) ? 64 : (SLOTS * 32 * 4 <= 160 * 1024) ? 32
                            : (SLOTS * 16 * 4 <= 160 * 1024) ? 16 : 8;
   // Below 16 lanes the rows of two workgroups no longer share a CU, and halving again measured
@@ -138,8 +139,14 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
   float R[NB][9], X[NB][3], S[NB][6], V[NB][6], A[NB][6], Fc[NB][6];
   SpI Ic[NB];
   float Mm[NV][NV], bias[NV];
-  bool act[NC];
-  float sep[NC], cmu[NC];
+  // per-candidate activity as per-lane bits; separation, friction and impulses live in the lane's LDS
+  // column (slots XS...: compile-time offsets), so an 84-candidate robot does not spill them to scratch
+  constexpr int XS = T::NSLOT + (TERR ? 3 * NC : 0);
+  constexpr int X_SEP = XS, X_MU = XS + NC, X_LAM = XS + 2 * NC;
+  unsigned actb[(NC + 31) / 32];
+#pragma unroll
+  for (int w = 0; w < (NC + 31) / 32; ++w) actb[w] = 0u;
+#define GS_ACT(c) ((actb[(c) >> 5] >> ((c) & 31)) & 1u)
 
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
@@ -254,10 +261,11 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
             nrm[0] = nt[0]; nrm[1] = nt[1]; nrm[2] = nt[2];
             smu = P.terr.mu;
           }
-          act[c] = dist < P.contact_offset;
-          sep[c] = dist - P.rest_offset;
-          cmu[c] = 0.5f * (mu_g[T::cshape[c] * N + e] + smu);
-          if (act[c]) {
+          const bool actc = dist < P.contact_offset;
+          if (actc) {
+            actb[c >> 5] |= 1u << (c & 31);
+            lds[(X_SEP + c) * LB] = dist - P.rest_offset;
+            lds[(X_MU + c) * LB] = 0.5f * (mu_g[T::cshape[c] * N + e] + smu);
             float* nsl = lds + (T::NSLOT + 3 * c) * LB;
             nsl[0] = nrm[0]; nsl[LB] = nrm[1]; nsl[2 * LB] = nrm[2];
             float dir[3][3];
@@ -290,10 +298,11 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
           }
         } else {
         const float dist = s.p[2] + x[2] - r;
-        act[c] = P.has_ground && (dist < P.contact_offset);
-        sep[c] = dist - P.rest_offset;
-        cmu[c] = 0.5f * (mu_g[T::cshape[c] * N + e] + P.ground_mu);
-        if (act[c]) {
+        const bool actc = P.has_ground && (dist < P.contact_offset);
+        if (actc) {
+          actb[c >> 5] |= 1u << (c & 31);
+          lds[(X_SEP + c) * LB] = dist - P.rest_offset;
+          lds[(X_MU + c) * LB] = 0.5f * (mu_g[T::cshape[c] * N + e] + P.ground_mu);
           const float xc[3] = {x[0], x[1], x[2] - r};
           const int SUP = T::csupp[c];
           const int leaf = T::cleaf[c];
@@ -458,7 +467,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
   // ---------------- contact rows: J (LDS) -> c = J nu_f, scaled Z = (L^-T J^T) D^-1/2, 1/diag
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    if (act[c]) {
+    if (GS_ACT(c)) {
       const int SUP = T::csupp[c];
       const int leaf = T::cleaf[c];
       float* slot = lds + T::cslot[c] * LB;
@@ -531,13 +540,15 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
   }
 
   // ---------------- projected Gauss-Seidel in w-space (joint limits, then contacts)
-  float wt[NV], lam[NC][3], wpos[NV], laml[ND > 0 ? ND : 1];
+  float wt[NV], wpos[NV], laml[ND > 0 ? ND : 1];
+  float* lamc = lds + X_LAM * LB;  // impulses of candidate c: lamc[(3 * c + rr) * LB]
 #pragma unroll
   for (int j = 0; j < ND; ++j) laml[j] = 0.f;
 #pragma unroll
   for (int k = 0; k < NV; ++k) wt[k] = 0.f;
 #pragma unroll
-  for (int c = 0; c < NC; ++c) lam[c][0] = lam[c][1] = lam[c][2] = 0.f;
+  for (int c = 0; c < NC; ++c)
+    if (GS_ACT(c)) lamc[(3 * c) * LB] = lamc[(3 * c + 1) * LB] = lamc[(3 * c + 2) * LB] = 0.f;
   const float inv_h = 1.f / h;
   const int iters = P.pos_iters + P.vel_iters;
   for (int it = 0; it < iters; ++it) {
@@ -570,11 +581,13 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
     }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      if (act[c]) {
+      if (GS_ACT(c)) {
         const int SUP = T::csupp[c];
         const int leaf = T::cleaf[c];
         const float* slot = lds + T::cslot[c] * LB;
-        const float sc = sep[c];
+        const float sc = lds[(X_SEP + c) * LB];
+        const float cmu = lds[(X_MU + c) * LB];
+        float lam[3] = {lamc[(3 * c) * LB], lamc[(3 * c + 1) * LB], lamc[(3 * c + 2) * LB]};
         float target = -sc * inv_h;
         if (sc < 0.f) target = pos_phase ? fminf(target, P.max_depen_vel) : 0.f;
 #pragma unroll
@@ -591,17 +604,20 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
           const float dinv = slot[(3 * SUP + 3 + rr) * LB];
           float nl;
           if (rr == 0) {
-            nl = fmaxf(lam[c][0] + (target - u) * dinv, 0.f);
+            nl = fmaxf(lam[0] + (target - u) * dinv, 0.f);
           } else {
-            const float lim = cmu[c] * lam[c][0];
-            nl = clampf(lam[c][rr] - u * dinv, -lim, lim);
+            const float lim = cmu * lam[0];
+            nl = clampf(lam[rr] - u * dinv, -lim, lim);
           }
-          const float dl = nl - lam[c][rr];
-          lam[c][rr] = nl;
+          const float dl = nl - lam[rr];
+          lam[rr] = nl;
 #pragma unroll
           for (int si = 0; si < MS; ++si)
             if (si < SUP) wt[supp_node<T>(leaf, si)] += z[si] * dl;
         }
+        lamc[(3 * c) * LB] = lam[0];
+        lamc[(3 * c + 1) * LB] = lam[1];
+        lamc[(3 * c + 2) * LB] = lam[2];
       }
     }
     if (it == P.pos_iters - 1) {
@@ -675,16 +691,17 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         if (T::clink[c] == b) {
-          if constexpr (TERR) {
-            if (act[c]) {
+          if (GS_ACT(c)) {
+            const float lam[3] = {lamc[(3 * c) * LB], lamc[(3 * c + 1) * LB], lamc[(3 * c + 2) * LB]};
+            if constexpr (TERR) {
               float fw[3];
-              contact_force_world<T, LB>(lds, c, lam[c], inv_h, fw);
+              contact_force_world<T, LB>(lds, c, lam, inv_h, fw);
               f0 += fw[0]; f1 += fw[1]; f2 += fw[2];
+            } else {
+              f0 += lam[1] * inv_h;
+              f1 += lam[2] * inv_h;
+              f2 += lam[0] * inv_h;
             }
-          } else {
-            f0 += lam[c][1] * inv_h;
-            f1 += lam[c][2] * inv_h;
-            f2 += lam[c][0] * inv_h;
           }
         }
       }
@@ -733,7 +750,8 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
         for (int k = 0; k < 6; ++k) f[k] = Fc[b][k] + ia[k];
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-          if (T::cbody[c] == b && act[c]) {
+          if (T::cbody[c] == b && GS_ACT(c)) {
+            const float lamv[3] = {lamc[(3 * c) * LB], lamc[(3 * c + 1) * LB], lamc[(3 * c + 2) * LB]};
             float x[3];
             mat3vec(R[b], M->cpoint[c], x);
             float fc[3];
@@ -741,10 +759,10 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
               const float* nsl = lds + (T::NSLOT + 3 * c) * LB;
               const float r = M->cradius[c];
               x[0] += X[b][0] - r * nsl[0]; x[1] += X[b][1] - r * nsl[LB]; x[2] += X[b][2] - r * nsl[2 * LB];
-              contact_force_world<T, LB>(lds, c, lam[c], inv_h, fc);
+              contact_force_world<T, LB>(lds, c, lamv, inv_h, fc);
             } else {
               x[0] += X[b][0]; x[1] += X[b][1]; x[2] += X[b][2] - M->cradius[c];
-              fc[0] = lam[c][1] * inv_h; fc[1] = lam[c][2] * inv_h; fc[2] = lam[c][0] * inv_h;
+              fc[0] = lamv[1] * inv_h; fc[1] = lamv[2] * inv_h; fc[2] = lamv[0] * inv_h;
             }
             float n[3];
             cross3(x, fc, n);
@@ -767,6 +785,8 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
     }
   }
 }
+
+#undef GS_ACT
 
 template <class T>
 GS_HD void com_velocity(const DevModel* __restrict__ M, const EnvState<T>& s, float* v) {
