@@ -17,11 +17,52 @@ from .running_mean_std import RunningMeanStd
 
 _ACT = {"elu": nn.ELU, "relu": nn.ReLU, "tanh": nn.Tanh, "selu": nn.SELU, "None": nn.Identity, None: nn.Identity}
 
+# Weight gradients of a minibatch (dW = g^T x, a reduction over the 16384 rows of AnymalTerrainPPO's
+# minibatch) are split over SPLIT_K row blocks as one batched GEMM + a float32 sum: as a single GEMM the
+# library tiles only the small N x K output (24-48 workgroups for 512 x 188) and takes ~100 us on
+# MI355X; split, ~25 us (tools/probes/gemm_splitk.py).
+SPLIT_K = 16
+SPLIT_K_MIN_ROWS = 4096
+
+
+class _SplitKLinearFn(torch.autograd.Function):
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda")
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        return torch.nn.functional.linear(x, w, b)
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        gx = g @ w.to(g.dtype) if ctx.needs_input_grad[0] else None
+        gw = None
+        if ctx.needs_input_grad[1]:
+            rows = g.shape[0]
+            xs = x.to(g.dtype)
+            gw = torch.bmm(g.reshape(SPLIT_K, rows // SPLIT_K, -1).transpose(1, 2),
+                           xs.reshape(SPLIT_K, rows // SPLIT_K, -1)).sum(0, dtype=torch.float32)
+        gb = g.sum(0, dtype=torch.float32) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return gx, gw, gb
+
+
+class Linear(nn.Linear):
+    """nn.Linear (same parameters and state_dict) whose backward splits the weight-gradient reduction
+    over the batch (SPLIT_K) for the learner's large minibatches."""
+
+    def forward(self, x):
+        if (torch.is_grad_enabled() and x.dim() == 2 and x.shape[0] >= SPLIT_K_MIN_ROWS
+                and x.shape[0] % SPLIT_K == 0 and x.is_cuda):
+            return _SplitKLinearFn.apply(x, self.weight, self.bias)
+        return super().forward(x)
+
 
 def _mlp(in_size: int, units: List[int], activation: str) -> nn.Sequential:
     layers = []
     for u in units:
-        layers += [nn.Linear(in_size, u), _ACT[activation]()]
+        layers += [Linear(in_size, u), _ACT[activation]()]
         in_size = u
     return nn.Sequential(*layers)
 
@@ -35,12 +76,12 @@ class ActorCriticNetwork(nn.Module):
         self.actor_mlp = _mlp(obs_dim, units, activation)
         self.critic_mlp = _mlp(obs_dim, units, activation) if separate else None
         out = units[-1] if units else obs_dim
-        self.value = nn.Linear(out, value_size)
-        self.mu = nn.Linear(out, actions_num)
+        self.value = Linear(out, value_size)
+        self.mu = Linear(out, actions_num)
         if fixed_sigma:
             self.sigma = nn.Parameter(torch.zeros(actions_num, dtype=torch.float32), requires_grad=True)
         else:
-            self.sigma = nn.Linear(out, actions_num)
+            self.sigma = Linear(out, actions_num)
         for m in self.modules():
             if isinstance(m, nn.Linear) and m.bias is not None:
                 nn.init.zeros_(m.bias)

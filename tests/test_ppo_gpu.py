@@ -114,3 +114,27 @@ def test_graph_replayed_backward_is_replay_invariant():
         g.replay()
         torch.cuda.synchronize()
         torch.testing.assert_close(agent.flat_grad, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_split_k_linear_matches_torch_linear():
+    """rl.network.Linear's split-K weight gradient equals nn.Linear's (fp32: 1e-5; fp16 autocast: the
+    half-precision rounding of the partial sums, 2e-3 of the gradient's scale)."""
+    from isaacgymenv_amd.rl.network import Linear
+    torch.manual_seed(0)
+    for autocast in (False, True):
+        lin = Linear(188, 512).cuda()
+        ref = torch.nn.Linear(188, 512).cuda()
+        ref.load_state_dict(lin.state_dict())
+        x = torch.randn(16384, 188, device="cuda")
+        g = torch.randn(16384, 512, device="cuda")
+        outs = []
+        for m in (lin, ref):
+            m.zero_grad()
+            xi = x.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.float16, enabled=autocast):
+                y = m(xi)
+            (y.float() * g).sum().backward()
+            outs.append((y.float(), m.weight.grad.clone(), m.bias.grad.clone(), xi.grad.clone()))
+        for a, b in zip(outs[0], outs[1]):
+            tol = 2e-3 if autocast else 1e-5
+            assert float((a - b).abs().max()) <= tol * float(b.abs().max()) + 1e-6
