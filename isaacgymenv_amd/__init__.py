@@ -4,7 +4,7 @@ HIP runtime setting applied before the runtime initialises: ``DEBUG_CLR_GRAPH_PA
 With graph packet capture on (the ROCm 7 default), a replayed HIP graph of the PPO minibatch
 backward returned a wrong first-layer bias gradient on some replays (deterministically so under
 AMD_SERIALIZE_KERNEL=3); with it off, every replay equals the eager gradient
-(tools/graph_bisect_probe.py, gpurun_out logs summarised in DESIGN.md).  ``GRAPHS_SAFE`` records
+(tools/probes/graph_bisect_probe.py, gpurun_out logs summarised in DESIGN.md).  ``GRAPHS_SAFE`` records
 whether the setting is in force; the PPO learner only captures graphs when it is.
 """
 import os as _os

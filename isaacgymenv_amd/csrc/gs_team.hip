@@ -57,6 +57,15 @@ __device__ __forceinline__ float quad_sum(float x) {
   x = x + qperm<0xB1>(x);  // quad_perm(1,0,3,2)
   return x + qperm<0x4E>(x);  // quad_perm(2,3,0,1)
 }
+// three independent quad sums, interleaved so no DPP read waits on the VALU write before it
+__device__ __forceinline__ void quad_sum3(float* u) {
+  const float a0 = qperm<0xB1>(u[0]), a1 = qperm<0xB1>(u[1]), a2 = qperm<0xB1>(u[2]);
+  const float t0 = u[0] + a0, t1 = u[1] + a1, t2 = u[2] + a2;
+  const float b0 = qperm<0x4E>(t0), b1 = qperm<0x4E>(t1), b2 = qperm<0x4E>(t2);
+  u[0] = t0 + b0;
+  u[1] = t1 + b1;
+  u[2] = t2 + b2;
+}
 // broadcast lane L of the quad to all four lanes; L is a constant after unrolling, the switch folds
 __device__ __forceinline__ float bcast(float x, int L) {
   switch (L) {
@@ -86,30 +95,39 @@ struct CM {
   static constexpr int LANES = T::T_LANES;
 };
 
-// LDS row stride: one float per lane plus a pad, so the 4 lanes of a team reading 4 different slots
-// of one column land in 4 different banks
-constexpr int RW = GS_WAVE + 1;
+#ifndef GS_TEAM_BLOCK
+#define GS_TEAM_BLOCK 64
+#endif
+constexpr int kTeamBlock = GS_TEAM_BLOCK;  // lanes per workgroup (one wave at most): 64 -> 16 envs
+static_assert(kTeamBlock % 4 == 0 && kTeamBlock <= GS_WAVE, "a workgroup holds whole teams within one wave");
+
+// LDS row stride: one float per lane of the workgroup plus a pad, so the 4 lanes of a team reading 4
+// different slots of one column land in 4 different banks (and a narrow workgroup's rows stay small
+// enough for several workgroups per CU)
+constexpr int RW = kTeamBlock + 1;
 
 // LDS contact records, layout [slot][lane]: chain candidates in the owner lane's column, then root
 // candidates (replicated, every lane its own column).  A record holds everything a lane needs
 // to run the contact's three Gauss-Seidel rows without cross-lane traffic:
-//   Z rows (3 x [Zb 6 | Zc CL]) | c (3) | 1/G_rr (3) | G10/G11 G20/G22 G21/G22 | target/G00 (pos, vel
-//   phase) | mu | active
+//   Z rows (3 x 16 slots: [Zb 6 | Zc CL | c] spread over the team's lanes) | 1/G_rr (3) |
+//   G10/G11 G20/G22 G21/G22 | target/G00 (pos, vel phase) | mu | active
 // where G = Z Z^T is the contact's 3x3 Delassus block (couples its rows within one GS pass); the
 // couplings and the target are stored pre-scaled by the row's 1/G_rr so that the serial part of a
 // contact's Gauss-Seidel update is as short as possible (contact_block).
 template <class T>
 struct RowSlots {
   static constexpr int CL = T::T_CL;
-  // A Z row's 9 components (base 6 | chain 3) in PGS-owner order: lane l's three components
-  // (l, l+4, 8 or a zero pad) are consecutive slots, so a lane reads them with paired LDS loads
-  // and the four lanes of a team hit four different banks (stride RW).
-  static constexpr int ZROW = 12;
-  static constexpr int RZROW = 12;
-  __device__ static constexpr int zslot(int comp) { return comp < 4 ? 3 * comp : comp < 8 ? 3 * (comp - 4) + 1 : 2; }
-  static constexpr int C_C = 3 * ZROW, C_DI = C_C + 3, C_G = C_DI + 3, C_TP = C_G + 3, C_TV = C_TP + 1,
+  // A Z row's 9 components (base 6 | chain 3) plus c = J nu_f in PGS-owner order, four consecutive
+  // slots per lane (two paired LDS loads; the four lanes of a team hit four different banks):
+  // lane l < 3 owns base 2l, base 2l+1 and chain component l (slot 4l+3 a zero pad), lane 3 holds
+  // only c (slot 15), so every lane's partial of u = c + Z w is the same three FMAs.
+  static constexpr int ZROW = 16;
+  static constexpr int RZROW = 16;
+  static constexpr int CSLOT = 15;
+  __device__ static constexpr int zslot(int comp) { return comp < 6 ? 4 * (comp >> 1) + (comp & 1) : 4 * (comp - 6) + 2; }
+  static constexpr int C_DI = 3 * ZROW, C_G = C_DI + 3, C_TP = C_G + 3, C_TV = C_TP + 1,
                        C_MU = C_TV + 1, C_ACT = C_MU + 1, PER_CONTACT = C_ACT + 1;
-  static constexpr int R_C = 3 * RZROW, R_DI = R_C + 3, R_G = R_DI + 3, R_TP = R_G + 3, R_TV = R_TP + 1,
+  static constexpr int R_DI = 3 * RZROW, R_G = R_DI + 3, R_TP = R_G + 3, R_TV = R_TP + 1,
                        R_MU = R_TV + 1, PER_ROOT = R_MU + 1;
   static constexpr int CHAIN = PER_CONTACT * T::T_CC;
   static constexpr int ROOT = PER_ROOT * (T::T_RC > 0 ? T::T_RC : 1);
@@ -128,17 +146,17 @@ __device__ __forceinline__ float sel_chain(const float (&x)[NCH][K], int lc, int
   return v;
 }
 
-// Distributed PGS velocity -> replicated base w (6) and this lane's chain w (3).  Owners: base b<4
-// lane b (wA), base 4,5 lanes 0,1 (wBb), chain c comps 0,1 lanes 2,3 (wB[c]), comp 2 lane 0 (wC[c]).
+// Distributed PGS velocity -> replicated base w (6) and this lane's chain w (3).  Owners: base 2l
+// and 2l+1 lane l < 3 (wA, wA2), chain c component l lane l < 3 (wC[c]).
 template <class T>
-__device__ __forceinline__ void gather_w(int lc, float wA, float wBb, const float (&wB)[T::T_NCH],
-                                         const float (&wC)[T::T_NCH], float* wb, float* wc) {
-  wb[0] = bcast(wA, 0); wb[1] = bcast(wA, 1); wb[2] = bcast(wA, 2); wb[3] = bcast(wA, 3);
-  wb[4] = bcast(wBb, 0); wb[5] = bcast(wBb, 1);
+__device__ __forceinline__ void gather_w(int lc, float wA, float wA2, const float (&wC)[T::T_NCH], float* wb,
+                                         float* wc) {
+  wb[0] = bcast(wA, 0); wb[1] = bcast(wA2, 0); wb[2] = bcast(wA, 1); wb[3] = bcast(wA2, 1);
+  wb[4] = bcast(wA, 2); wb[5] = bcast(wA2, 2);
   wc[0] = wc[1] = wc[2] = 0.f;
 #pragma unroll
   for (int c = 0; c < T::T_NCH; ++c) {
-    const float c0 = bcast(wB[c], 2), c1 = bcast(wB[c], 3), c2 = bcast(wC[c], 0);
+    const float c0 = bcast(wC[c], 0), c1 = bcast(wC[c], 1), c2 = bcast(wC[c], 2);
     wc[0] = lc == c ? c0 : wc[0];
     wc[1] = lc == c ? c1 : wc[1];
     wc[2] = lc == c ? c2 : wc[2];
@@ -621,10 +639,13 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
           row[RS::zslot(6 + k) * RW] = z;
           zr[rr][6 + k] = z;
         }
-        row[5 * RW] = 0.f;  // zero pads read as lanes 1-3's third component
-        row[8 * RW] = 0.f;
+        row[3 * RW] = 0.f;  // pads: lanes 0-2 add no constant, lane 3 owns no component
+        row[7 * RW] = 0.f;
         row[11 * RW] = 0.f;
-        rec[(RS::C_C + rr) * RW] = cj;
+        row[12 * RW] = 0.f;
+        row[13 * RW] = 0.f;
+        row[14 * RW] = 0.f;
+        row[RS::CSLOT * RW] = cj;
         dir[rr] = __builtin_amdgcn_rcpf(d);
         rec[(RS::C_DI + rr) * RW] = dir[rr];
       }
@@ -678,9 +699,16 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
           rec[(rr * RS::RZROW + RS::zslot(b)) * RW] = zb[b];
           zr[rr][b] = zb[b];
         }
-        rec[(rr * RS::RZROW + RS::zslot(6)) * RW] = 0.f;  // lanes 2, 3: second component is chain-only
-        rec[(rr * RS::RZROW + RS::zslot(7)) * RW] = 0.f;
-        rec[(RS::R_C + rr) * RW] = cj;
+        float* rz = rec + rr * RS::RZROW * RW;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {  // no chain components; pads as in the chain records
+          rz[(4 * k + 2) * RW] = 0.f;
+          rz[(4 * k + 3) * RW] = 0.f;
+        }
+        rz[12 * RW] = 0.f;
+        rz[13 * RW] = 0.f;
+        rz[14 * RW] = 0.f;
+        rz[RS::CSLOT * RW] = cj;
         dir[rr] = __builtin_amdgcn_rcpf(d);
         rec[(RS::R_DI + rr) * RW] = dir[rr];
       }
@@ -707,16 +735,14 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
   GS_PROF(3)  // contact records
   // ================= projected Gauss-Seidel, global contact order: root candidates, chain 0, 1, ...
   // The 9 velocity components a chain contact row touches (base 6 | its chain's 3) are spread over
-  // the team: lane l owns components l, l+4 and (lane 0 only) 8, i.e. base l, base 4+l / chain
-  // comp l-2, chain comp 2.  Each lane forms its partial of the 3 rows' u = c + Z w, a DPP quad
-  // sum completes them (bit-identical in the 4 lanes), the 3-row projection through the
-  // contact's Delassus couplings runs replicated, and each lane updates only what it owns.
+  // the team: lane l < 3 owns base 2l, base 2l+1 and chain component l (RowSlots).  Each lane forms
+  // its partial of the 3 rows' u = c + Z w (lane 3: c), a DPP quad sum completes them
+  // (bit-identical in the 4 lanes), the 3-row projection through the contact's Delassus couplings
+  // runs replicated, and each lane updates only what it owns.
   static_assert(CL == 3, "component distribution assumes 3-dof chains");
-  const bool low = lc < 2;            // component l+4 is a base component (else chain comp l-2)
-  const float lane0 = lc == 0 ? 1.f : 0.f;
-  float wA = 0.f, wBb = 0.f, wB[NCH], wC[NCH];
+  float wA = 0.f, wA2 = 0.f, wC[NCH];
 #pragma unroll
-  for (int c = 0; c < NCH; ++c) wB[c] = wC[c] = 0.f;
+  for (int c = 0; c < NCH; ++c) wC[c] = 0.f;
   float lamc[NCH][CC][3], lamr[RC > 0 ? RC : 1][3];
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
@@ -733,81 +759,77 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     for (int j = 0; j < RC; ++j) {
       if (ract[j]) {
         const float* rec = rows_own + RS::root(j) * RW;
-        const float* recl = rec + 3 * lc * RW;
-        float za[3], zb2[3], u[3];
+        const float* recl = rec + 4 * lc * RW;
+        float z[12], u[3];
 #pragma unroll
-        for (int rr = 0; rr < 3; ++rr) {
-          za[rr] = recl[(rr * RS::RZROW) * RW];
-          zb2[rr] = recl[(rr * RS::RZROW + 1) * RW];
-          const float c0 = rec[(RS::R_C + rr) * RW] * lane0;  // c joins lane 0's partial
-          u[rr] = quad_sum(fmaf(za[rr], wA, fmaf(zb2[rr], wBb, c0)));
-        }
+        for (int i = 0; i < 12; ++i) z[i] = recl[((i >> 2) * RS::RZROW + (i & 3)) * RW];
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) u[rr] = fmaf(z[4 * rr], wA, fmaf(z[4 * rr + 1], wA2, z[4 * rr + 3]));
+        quad_sum3(u);
         float dl0, dl1, dl2;
         contact_block(u[0], u[1], u[2], rec[RS::R_DI * RW], rec[(RS::R_DI + 1) * RW], rec[(RS::R_DI + 2) * RW],
                       rec[RS::R_G * RW], rec[(RS::R_G + 1) * RW], rec[(RS::R_G + 2) * RW], rec[rsel * RW],
                       rec[RS::R_MU * RW], lamr[j], dl0, dl1, dl2);
-        wA += za[0] * dl0 + za[1] * dl1 + za[2] * dl2;
-        wBb += zb2[0] * dl0 + zb2[1] * dl1 + zb2[2] * dl2;  // lanes 2, 3 read the zero pads
+        wA = fmaf(z[8], dl2, fmaf(z[4], dl1, fmaf(z[0], dl0, wA)));
+        wA2 = fmaf(z[9], dl2, fmaf(z[5], dl1, fmaf(z[1], dl0, wA2)));
       }
     }
-    // software-pipelined over the NCH*CC chain contacts: the next contact's activity, Z components
-    // and c are loaded before this contact's (divergent) block, so their LDS latency overlaps it
-    float nact, nz[9], nc[3];
-    auto fetch = [&](int n, float& act_o, float* z_o, float* c_o) {
+    // software-pipelined over the NCH*CC chain contacts: the next contact's whole record (activity,
+    // this lane's Z components and c, the Delassus block, target, mu) is loaded before this
+    // contact's (divergent) block, so its LDS latency overlaps the block
+    float nact, nz[12], nk[8];  // nk: 1/G_rr (3) | scaled couplings (3) | target | mu
+    auto fetch = [&](int n) {
       const int cc = n / CC, j = n - (n / CC) * CC;
       const float* rec = rows_team + cc + RS::chain(j) * RW;
-      const float* recl = rec + 3 * lc * RW;
-      act_o = rec[RS::C_ACT * RW];
+      const float* recl = rec + 4 * lc * RW;
+      nact = rec[RS::C_ACT * RW];
 #pragma unroll
-      for (int rr = 0; rr < 3; ++rr) {
-        const float* row = recl + rr * RS::ZROW * RW;
-        z_o[3 * rr + 0] = row[0];
-        z_o[3 * rr + 1] = row[RW];
-        z_o[3 * rr + 2] = row[2 * RW];
-        c_o[rr] = rec[(RS::C_C + rr) * RW] * lane0;  // multiply, not select: no divergent load
-      }
+      for (int i = 0; i < 12; ++i) nz[i] = recl[((i >> 2) * RS::ZROW + (i & 3)) * RW];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) nk[i] = rec[(RS::C_DI + i) * RW];
+      nk[6] = rec[tsel * RW];
+      nk[7] = rec[RS::C_MU * RW];
     };
-    fetch(0, nact, nz, nc);
+    fetch(0);
 #pragma unroll
     for (int n = 0; n < NCH * CC; ++n) {
       const int cc = n / CC, j = n - (n / CC) * CC;
-      const float* rec = rows_team + cc + RS::chain(j) * RW;
-      float z[9], c3[3];
+      float z[12], k8[8];
       const float act_n = nact;
 #pragma unroll
-      for (int i = 0; i < 9; ++i) z[i] = nz[i];
+      for (int i = 0; i < 12; ++i) z[i] = nz[i];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) c3[i] = nc[i];
-      if (n + 1 < NCH * CC) fetch(n + 1, nact, nz, nc);
+      for (int i = 0; i < 8; ++i) k8[i] = nk[i];
+      // (the scheduler hoists all 12 records' loads to the top of the sweep and parks them in AGPRs;
+      // measured faster than keeping the prefetch one contact deep with a scheduling fence:
+      // 0.0886 vs 0.0915 ms per launch, profiles/r02o_experiments_team_pgs.txt)
+      if (n + 1 < NCH * CC) fetch(n + 1);
       const bool a_o = act_n != 0.f;
 #ifdef GS_PHASE_PROFILE
       if (__ballot(a_o) != 0ull) GS_PROF_COUNT(8, 1)  // chain contacts the wave executes
 #endif
       if (a_o) {
-        const float wBv = low ? wBb : wB[cc];
         float u[3];
 #pragma unroll
-        for (int rr = 0; rr < 3; ++rr)  // c joins lane 0's partial; the w terms last (they carry the chain)
-          u[rr] = quad_sum(fmaf(z[3 * rr], wA, fmaf(z[3 * rr + 1], wBv, fmaf(z[3 * rr + 2], wC[cc], c3[rr]))));
+        for (int rr = 0; rr < 3; ++rr)  // the w terms last (they carry the Gauss-Seidel chain)
+          u[rr] = fmaf(z[4 * rr], wA, fmaf(z[4 * rr + 1], wA2, fmaf(z[4 * rr + 2], wC[cc], z[4 * rr + 3])));
+        quad_sum3(u);
         float dl0, dl1, dl2;
-        contact_block(u[0], u[1], u[2], rec[RS::C_DI * RW], rec[(RS::C_DI + 1) * RW], rec[(RS::C_DI + 2) * RW],
-                      rec[RS::C_G * RW], rec[(RS::C_G + 1) * RW], rec[(RS::C_G + 2) * RW], rec[tsel * RW],
-                      rec[RS::C_MU * RW], lamc[cc][j], dl0, dl1, dl2);
-        wA += z[0] * dl0 + z[3] * dl1 + z[6] * dl2;
-        const float nB = wBv + (z[1] * dl0 + z[4] * dl1 + z[7] * dl2);
-        wBb = low ? nB : wBb;
-        wB[cc] = low ? wB[cc] : nB;
-        wC[cc] += z[2] * dl0 + z[5] * dl1 + z[8] * dl2;
+        contact_block(u[0], u[1], u[2], k8[0], k8[1], k8[2], k8[3], k8[4], k8[5], k8[6], k8[7], lamc[cc][j], dl0,
+                      dl1, dl2);
+        wA = fmaf(z[8], dl2, fmaf(z[4], dl1, fmaf(z[0], dl0, wA)));
+        wA2 = fmaf(z[9], dl2, fmaf(z[5], dl1, fmaf(z[1], dl0, wA2)));
+        wC[cc] = fmaf(z[10], dl2, fmaf(z[6], dl1, fmaf(z[2], dl0, wC[cc])));
       }
     }
 #ifdef GS_PHASE_PROFILE
     for (int j = 0; j < RC; ++j)
       if (__ballot(ract[j]) != 0ull) GS_PROF_COUNT(9, 1)  // root contacts the wave executes
 #endif
-    if (it == P.pos_iters - 1) gather_w<T>(lc, wA, wBb, wB, wC, wbp, wcp);
+    if (it == P.pos_iters - 1) gather_w<T>(lc, wA, wA2, wC, wbp, wcp);
   }
   float wb[6], wc[CL];
-  gather_w<T>(lc, wA, wBb, wB, wC, wb, wc);
+  gather_w<T>(lc, wA, wA2, wC, wb, wc);
   if (P.pos_iters <= 0) {
 #pragma unroll
     for (int b = 0; b < 6; ++b) wbp[b] = wb[b];
@@ -925,12 +947,6 @@ __device__ __forceinline__ void team_com_velocity(const DevModel* __restrict__ M
   cross3(s.w, c, wc);
   v[0] = s.vo[0] + wc[0]; v[1] = s.vo[1] + wc[1]; v[2] = s.vo[2] + wc[2];
 }
-
-#ifndef GS_TEAM_BLOCK
-#define GS_TEAM_BLOCK 64
-#endif
-constexpr int kTeamBlock = GS_TEAM_BLOCK;  // lanes per workgroup (one wave at most): 64 -> 16 envs
-static_assert(kTeamBlock % 4 == 0 && kTeamBlock <= GS_WAVE, "a workgroup holds whole teams within one wave");
 
 template <class T>
 __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel* __restrict__ M, DevParams P,

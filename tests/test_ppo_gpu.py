@@ -55,7 +55,7 @@ def _agent(task, num_envs, **over):
 
 def test_cartpole_ppo_learns():
     # rl_games solves Cartpole (episode 500 steps) in ~100 epochs; this learner reaches ~490 mean
-    # episode length by epoch 60 (tools/ppo_probe.py); random play lasts ~3 steps
+    # episode length by epoch 60 (tools/probes/ppo_probe.py); random play lasts ~3 steps
     agent = _agent("Cartpole", 512)
     for ep in range(60):
         agent.train_epoch()
