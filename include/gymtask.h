@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GT_ABI_VERSION 2
+#define GT_ABI_VERSION 3
 #define GT_ANYMAL_NUM_TERMS 13  /* lin_vel_xy lin_vel_z ang_vel_z ang_vel_xy orient torques joint_acc
                                    base_height air_time collision stumble action_rate hip */
 
@@ -54,6 +54,8 @@ typedef struct gt_anymal_params {
     float default_dof_pos[16];
     float base_init_state[13];
 } gt_anymal_params;
+
+struct gt_anymal_hound;
 
 typedef struct gt_anymal_buffers {
     float *root_states;          /* [N][13]                                   */
@@ -88,9 +90,37 @@ typedef struct gt_anymal_buffers {
     float *obs_out;              /* [N][num_obs] or NULL: VecTask's clamped obs copy (vec_task.py:402) */
     uint8_t *time_outs;          /* [N] bool or NULL: (progress >= T-1) & reset (vec_task.py:394)     */
     float clip_obs;              /* clipObservations (inf -> plain copy)                    */
-    const float *measured_heights; /* [N][num_obs - 36 - nd] terrain heights under the probes
+    const float *measured_heights; /* [N][140] terrain heights under the probes
                                     (gt_measure_heights), or NULL: plane terrain, heights 0 */
+    const struct gt_anymal_hound *hound; /* NULL for AnymalTerrain; UsefulHound's differences (ABI 3) */
 } gt_anymal_buffers;
+
+/* UsefulHound (reference tasks/useful_hound.py) runs the same tail with these differences
+ * (ABI 3; the gt_anymal_* entry points take them through gt_anymal_buffers.hound):
+ *   - num_dofs in gt_anymal_params is the 12 LEG dofs (default_dof_pos, hip terms, last_dof_vel
+ *     [N][12], joint_acc, dof observations); dof_state rows hold num_actions (18) dofs, legs first;
+ *     torques / actions / last_actions are [N][num_actions];
+ *   - check_termination (:467-480): thigh ("knee") contacts terminate regardless of
+ *     allow_knee_contacts, and so do the shoulder links (base_indices);
+ *   - compute_reward (:499-567): collision = knees * s + shoulders * s;
+ *   - reset_idx (:569-642): after the leg draws (and the trimesh root x, y) one torch.rand(k, 6) for
+ *     the arm: q_arm = clamp(arm_default + arm_noise2 * (u - 0.5), arm_lower, arm_upper), qd_arm = 0,
+ *     pos_control = q_arm, effort_control = 0;
+ *   - compute_observations (:482-497): 204 = 12 base | 12 dof pos | 12 dof vel | 140 heights |
+ *     18 actions | end-effector position (3) and quaternion (4) from the rigid-body row eef_state
+ *     + e * eef_stride | arm_commands [N][3]. */
+typedef struct gt_anymal_hound {
+    int32_t num_actions;                 /* 18 */
+    int32_t num_shoulders, shoulder_idx[4];
+    const float *eef_state;              /* env 0's end-effector rigid-body row (pos | quat | ...) */
+    int32_t eef_stride;                  /* floats between consecutive envs' rows */
+    const float *arm_commands;           /* [N][3] */
+    float *pos_control, *effort_control; /* [N][6] */
+    float arm_default[6], arm_lower[6], arm_upper[6];
+    float arm_noise2;                    /* float(houndarmDofNoise * 2.0) */
+    const float *u_arm;                  /* [k][6] drawn buffer, or NULL: use plan_arm */
+    gt_torch_rand_plan plan_arm;
+} gt_anymal_hound;
 
 int gt_abi_version(void);
 const char *gt_last_error(void);

@@ -74,12 +74,17 @@ __device__ __forceinline__ void load_dof_row(const float* __restrict__ src, int 
   }
 }
 
+constexpr int kMaxActions = 20;  // UsefulHound: 18
+
 // One env: every input is loaded first (one memory round trip), then computed, then stored:
 // the buffers may alias as far as the compiler knows, so interleaved loads and stores would
-// serialise into one round trip per statement group.
-template <bool VEC>
-__device__ __forceinline__ bool post_a_env(const gt_anymal_params& p, const gt_anymal_buffers& b, const int e) {
+// serialise into one round trip per statement group.  HOUND: UsefulHound's tail (gymtask.h,
+// gt_anymal_hound; useful_hound.py:467-567).
+template <bool VEC, bool HOUND>
+__device__ __forceinline__ bool post_a_env(const gt_anymal_params& p, const gt_anymal_buffers& b,
+                                           const gt_anymal_hound& h, const int e) {
   const int nd = p.num_dofs, nb = p.num_bodies;
+  const int na = HOUND ? h.num_actions : nd;  // torques / actions width and dof_state row width
   const size_t N = p.num_envs;
   // ---- loads
   const int64_t prog = b.progress_buf[e] + 1;
@@ -104,12 +109,36 @@ __device__ __forceinline__ bool post_a_env(const gt_anymal_params& p, const gt_a
       fknee[k][c] = k < p.num_knees ? cf[3 * p.knee_idx[k] + c] : 0.0f;
       ffoot[k][c] = k < p.num_feet ? cf[3 * p.feet_idx[k] + c] : 0.0f;
     }
-  float tq[16], act[16], lact[16], lqd[16], dq[16], dqd[16];
-  load_row16<VEC>(b.torques + (size_t)e * nd, nd, tq);
-  load_row16<VEC>(b.actions + (size_t)e * nd, nd, act);
-  load_row16<VEC>(b.last_actions + (size_t)e * nd, nd, lact);
-  load_row16<VEC>(b.last_dof_vel + (size_t)e * nd, nd, lqd);
-  load_dof_row<VEC>(b.dof_state + (size_t)e * nd * 2, nd, dq, dqd);
+  float fsh[4][3];
+  if constexpr (HOUND) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) fsh[k][c] = k < h.num_shoulders ? cf[3 * h.shoulder_idx[k] + c] : 0.0f;
+  }
+  float tq[kMaxActions], act[kMaxActions], lact[kMaxActions], lqd[16], dq[16], dqd[16];
+  if constexpr (HOUND) {
+#pragma unroll
+    for (int j = 0; j < kMaxActions; ++j)
+      if (j < na) {
+        tq[j] = b.torques[(size_t)e * na + j];
+        act[j] = b.actions[(size_t)e * na + j];
+        lact[j] = b.last_actions[(size_t)e * na + j];
+      }
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j < nd) {
+        lqd[j] = b.last_dof_vel[(size_t)e * nd + j];
+        dq[j] = b.dof_state[((size_t)e * na + j) * 2];
+        dqd[j] = b.dof_state[((size_t)e * na + j) * 2 + 1];
+      }
+  } else {
+    load_row16<VEC>(b.torques + (size_t)e * nd, nd, tq);
+    load_row16<VEC>(b.actions + (size_t)e * nd, nd, act);
+    load_row16<VEC>(b.last_actions + (size_t)e * nd, nd, lact);
+    load_row16<VEC>(b.last_dof_vel + (size_t)e * nd, nd, lqd);
+    load_dof_row<VEC>(b.dof_state + (size_t)e * nd * 2, nd, dq, dqd);
+  }
   float not_timeout;
   if (b.timeout_is_int64) not_timeout = (float)(~((const int64_t*)b.timeout_buf)[e]);
   else not_timeout = ((const uint8_t*)b.timeout_buf)[e] ? 0.0f : 1.0f;
@@ -142,7 +171,15 @@ __device__ __forceinline__ bool post_a_env(const gt_anymal_params& p, const gt_a
   int knee_count = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) knee_count += (k < p.num_knees && norm3(fknee[k]) > 1.0f) ? 1 : 0;
-  if (!p.allow_knee_contacts && knee_count > 0) reset = true;
+  int sh_count = 0;
+  if constexpr (HOUND) {
+    // useful_hound.py:467-480: thigh and shoulder contacts terminate, allowKneeContacts is not read
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sh_count += (k < h.num_shoulders && norm3(fsh[k]) > 1.0f) ? 1 : 0;
+    if (knee_count > 0 || sh_count > 0) reset = true;
+  } else {
+    if (!p.allow_knee_contacts && knee_count > 0) reset = true;
+  }
   if (prog >= p.max_episode_length - 1) reset = true;
 
   // ---- compute_reward (:315-382, reference order)
@@ -156,16 +193,17 @@ __device__ __forceinline__ bool post_a_env(const gt_anymal_params& p, const gt_a
   const float r_height = sq(root[2] - 0.52f) * p.s_base_height;
   float s_tq = 0.f, s_acc = 0.f, s_rate = 0.f;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    if (j < nd) {
+  for (int j = 0; j < kMaxActions; ++j) {
+    if (j < na) {
       s_tq += sq(tq[j]);
-      s_acc += sq(lqd[j] - dqd[j]);
       s_rate += sq(lact[j] - act[j]);
     }
+    if (j < 16 && j < nd) s_acc += sq(lqd[j] - dqd[j]);
   }
   const float r_torque = s_tq * p.s_torque;
   const float r_jacc = s_acc * p.s_joint_acc;
-  const float r_coll = (float)knee_count * p.s_collision;
+  const float r_coll = HOUND ? (float)knee_count * p.s_collision + (float)sh_count * p.s_collision
+                             : (float)knee_count * p.s_collision;
   int stumble = 0;
   float air_sum = 0.f;
 #pragma unroll
@@ -218,11 +256,11 @@ __device__ __forceinline__ bool post_a_env(const gt_anymal_params& p, const gt_a
 
 // One lane per env, one wave per workgroup (4096 envs -> 64 workgroups on 64 CUs: the tail is
 // latency bound, so spreading it over CUs beats packing 4 waves per CU).
-template <bool VEC>
-__global__ void __launch_bounds__(64) k_post_a(gt_anymal_params p, gt_anymal_buffers b) {
+template <bool VEC, bool HOUND>
+__global__ void __launch_bounds__(64) k_post_a(gt_anymal_params p, gt_anymal_buffers b, gt_anymal_hound h) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   bool reset = false;
-  if (e < p.num_envs) reset = post_a_env<VEC>(p, b, e);
+  if (e < p.num_envs) reset = post_a_env<VEC, HOUND>(p, b, h, e);
   // reset count: one 64-bit atomic per wave carries {waves done << 32 | count}; the wave that
   // completes the grid publishes the total (device word reset_count[2], and {count, seq} into
   // host memory for the host's spin wait) and re-arms the accumulator for the next launch
@@ -310,8 +348,9 @@ __global__ void __launch_bounds__(64 * GT_ANYMAL_NUM_TERMS) k_episode_sums(gt_an
 // reset_idx for the envs post_a flagged (anymal_terrain.py:384-425, plane terrain).  One lane
 // per env, one wave per workgroup; the rank of a flagged env among all flagged envs comes from
 // post_a's per-wave ballots (exclusive prefix of popcounts), so no compaction pass is needed.
-__global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_anymal_buffers b, int k,
-                                                      gt_anymal_reset_draws d, gt_anymal_terrain_reset tr,
+template <bool HOUND>
+__global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_anymal_buffers b, gt_anymal_hound h,
+                                                      int k, gt_anymal_reset_draws d, gt_anymal_terrain_reset tr,
                                                       bool has_terrain, int32_t* __restrict__ ids_out,
                                                       float* __restrict__ ep_out, float len_s,
                                                       float* __restrict__ partial, unsigned* __restrict__ done) {
@@ -326,13 +365,15 @@ __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_any
   const unsigned long long mine = b.reset_masks[w];
   const bool flagged = (mine >> lane) & 1ull;
   const int nd = p.num_dofs;
+  const int na = HOUND ? h.num_actions : nd;
   const size_t N = p.num_envs;
   // The wave's draws (2*nd + 3 per flagged env) are evaluated by all 64 lanes and exchanged
   // through LDS: one Philox chain per lane instead of 2*nd + 3 serial ones per flagged lane.
-  constexpr int kMaxDraws = 2 * 16 + 3 + 2;
+  constexpr int kMaxDraws = 2 * 16 + 3 + 2 + (HOUND ? 6 : 0);
   __shared__ float u_lds[64 * kMaxDraws];
   const int m = (int)__popcll(mine);
-  const int D = 2 * nd + 3 + (has_terrain ? 2 : 0);  // pos | vel | cmd x, y, heading | root x, y
+  const int DT = 2 * nd + 3 + (has_terrain ? 2 : 0);  // pos | vel | cmd x, y, heading | root x, y
+  const int D = DT + (HOUND ? 6 : 0);                  // | arm (UsefulHound)
   for (int s = lane; s < m * D; s += 64) {
     const int r = s / D, c = s - (s / D) * D;
     const int t = base + r;
@@ -344,9 +385,12 @@ __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_any
     } else if (c == 2 * nd) u = d.u_cmd_x ? d.u_cmd_x[t] : torch_philox::rand_at(d.plan_cmd_x, t);
     else if (c == 2 * nd + 1) u = d.u_cmd_y ? d.u_cmd_y[t] : torch_philox::rand_at(d.plan_cmd_y, t);
     else if (c == 2 * nd + 2) u = d.u_cmd_h ? d.u_cmd_h[t] : torch_philox::rand_at(d.plan_cmd_h, t);
-    else {
+    else if (c < DT) {
       const size_t q = (size_t)t * 2 + (c - 2 * nd - 3);
       u = tr.u_root_xy ? tr.u_root_xy[q] : torch_philox::rand_at(tr.plan_root_xy, q);
+    } else {
+      const size_t q = (size_t)t * 6 + (c - DT);
+      u = h.u_arm ? h.u_arm[q] : torch_philox::rand_at(h.plan_arm, q);
     }
     u_lds[s] = u;
   }
@@ -358,12 +402,23 @@ __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_any
     const int r = (int)__popcll(mine & ((1ull << lane) - 1ull));
     const int t = base + r;
     const float* u = u_lds + r * D;
-    float* ds = b.dof_state + (size_t)e * nd * 2;
+    float* ds = b.dof_state + (size_t)e * na * 2;
     for (int j = 0; j < nd; ++j) {
       const float off = d.pos_range * u[j] + d.pos_lower;
       const float vel = d.vel_range * u[nd + j] + d.vel_lower;
       ds[2 * j] = p.default_dof_pos[j] * off;
       ds[2 * j + 1] = vel;
+    }
+    if constexpr (HOUND) {
+      // useful_hound.py:592-601: tensor_clamp(default + noise * 2.0 * (u - 0.5), lower, upper)
+      for (int j = 0; j < 6; ++j) {
+        const float x = h.arm_default[j] + (u[DT + j] - 0.5f) * h.arm_noise2;
+        const float q = fmaxf(fminf(x, h.arm_upper[j]), h.arm_lower[j]);
+        ds[2 * (nd + j)] = q;
+        ds[2 * (nd + j) + 1] = 0.0f;
+        h.pos_control[(size_t)e * 6 + j] = q;
+        h.effort_control[(size_t)e * 6 + j] = 0.0f;
+      }
     }
     float* root = b.root_states + (size_t)e * 13;
     if (has_terrain) {
@@ -400,10 +455,8 @@ __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_any
     cmd[3] = d.cmd_h_range * uh + d.cmd_h_lower;
     const float m = sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]) > 0.25f ? 1.0f : 0.0f;
     for (int j = 0; j < 4; ++j) b.commands[(size_t)e * 4 + j] = cmd[j] * m;
-    for (int j = 0; j < nd; ++j) {
-      b.last_actions[(size_t)e * nd + j] = 0.0f;
-      b.last_dof_vel[(size_t)e * nd + j] = 0.0f;
-    }
+    for (int j = 0; j < na; ++j) b.last_actions[(size_t)e * na + j] = 0.0f;
+    for (int j = 0; j < nd; ++j) b.last_dof_vel[(size_t)e * nd + j] = 0.0f;
     for (int j = 0; j < 4; ++j) b.feet_air_time[(size_t)e * 4 + j] = 0.0f;
     b.progress_buf[e] = 0;
     b.reset_buf[e] = 1;
@@ -454,21 +507,22 @@ __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_any
 // One workgroup per env, one lane per observation element (compute_observations, :302-313).
 // Each lane selects its source address and scale first and then issues ONE load, so the
 // ragged segments of the obs row do not serialise into one memory round trip per segment.
-template <int NOISE>  // 0 none, 1 drawn buffer, 2 in-kernel torch.rand stream
-__global__ void __launch_bounds__(256) k_post_b(gt_anymal_params p, gt_anymal_buffers b,
+template <int NOISE, bool HOUND>  // NOISE: 0 none, 1 drawn buffer, 2 in-kernel torch.rand stream
+__global__ void __launch_bounds__(256) k_post_b(gt_anymal_params p, gt_anymal_buffers b, gt_anymal_hound h,
                                                 const float* __restrict__ noise, gt_torch_rand_plan plan) {
   const int e = blockIdx.x;
   const int k = threadIdx.x;
   const int no = p.num_obs;
   if (k >= no) return;
   const int nd = p.num_dofs;
+  const int na = HOUND ? h.num_actions : nd;    // actions width, dof_state row width
+  const int ne = HOUND ? 10 : 0;                // end-effector position, quaternion, arm command
+  const int nh = no - 12 - 2 * nd - na - ne;    // height probes (140)
   const size_t t = (size_t)e * no + k;
   // side outputs: last_actions / last_dof_vel (:484-485) and VecTask's time_outs (vec_task.py:394)
   float la = 0.0f, lq = 0.0f;
-  if (k < nd) {
-    la = b.actions[(size_t)e * nd + k];
-    lq = b.dof_state[((size_t)e * nd + k) * 2 + 1];
-  }
+  if (k < na) la = b.actions[(size_t)e * na + k];
+  if (k < nd) lq = b.dof_state[((size_t)e * na + k) * 2 + 1];
   int64_t prog = 0;
   uint8_t rst = 0;
   if (k == 0 && b.time_outs) {
@@ -487,14 +541,18 @@ __global__ void __launch_bounds__(256) k_post_b(gt_anymal_params p, gt_anymal_bu
   } else if (k < 12) {
     src = b.commands + (size_t)e * 4 + k - 9; sc = k < 11 ? p.lin_vel_scale : p.ang_vel_scale;
   } else if (k < 12 + nd) {
-    src = b.dof_state + ((size_t)e * nd + (k - 12)) * 2; sc = p.dof_pos_scale;
+    src = b.dof_state + ((size_t)e * na + (k - 12)) * 2; sc = p.dof_pos_scale;
   } else if (k < 12 + 2 * nd) {
-    src = b.dof_state + ((size_t)e * nd + (k - 12 - nd)) * 2 + 1; sc = p.dof_vel_scale;
-  } else if (k < no - nd) {
+    src = b.dof_state + ((size_t)e * na + (k - 12 - nd)) * 2 + 1; sc = p.dof_vel_scale;
+  } else if (k < 12 + 2 * nd + nh) {
     // the base height; the probe's terrain height is subtracted below
     src = b.root_states + (size_t)e * 13 + 2; height = true;
+  } else if (k < 12 + 2 * nd + nh + na) {
+    src = b.actions + (size_t)e * na + (k - (12 + 2 * nd + nh));
+  } else if (k < no - 3) {  // UsefulHound: end-effector position | quaternion (useful_hound.py:492-493)
+    src = h.eef_state + (size_t)e * h.eef_stride + (k - (no - ne));
   } else {
-    src = b.actions + (size_t)e * nd + (k - (no - nd));
+    src = h.arm_commands + (size_t)e * 3 + (k - (no - 3));
   }
   const float x = *src;
   const float nz = NOISE == 1 ? noise[t] : NOISE == 2 ? torch_philox::rand_at(plan, t) : 0.0f;
@@ -502,7 +560,7 @@ __global__ void __launch_bounds__(256) k_post_b(gt_anymal_params p, gt_anymal_bu
   float v;
   if (height) {
     // clip(z - 0.5 - measured_height, -1, 1) * scale (:303-304); plane terrain: heights are 0
-    const float mh = b.measured_heights ? b.measured_heights[(size_t)e * (no - 36 - nd) + (k - 12 - 2 * nd)] : 0.0f;
+    const float mh = b.measured_heights ? b.measured_heights[(size_t)e * nh + (k - 12 - 2 * nd)] : 0.0f;
     v = fminf(fmaxf(x - 0.5f - mh, -1.0f), 1.0f) * p.height_meas_scale;
   }
   else if (k < 12 + 2 * nd && !(k >= 6 && k < 9)) v = x * sc;
@@ -511,10 +569,8 @@ __global__ void __launch_bounds__(256) k_post_b(gt_anymal_params p, gt_anymal_bu
   b.obs_buf[t] = v;
   if (b.obs_out) b.obs_out[t] = fminf(fmaxf(v, -b.clip_obs), b.clip_obs);
   if (k == 0 && b.time_outs) b.time_outs[e] = (prog >= p.max_episode_length - 1) && (rst != 0);
-  if (k < nd) {
-    b.last_actions[(size_t)e * nd + k] = la;
-    b.last_dof_vel[(size_t)e * nd + k] = lq;
-  }
+  if (k < na) b.last_actions[(size_t)e * na + k] = la;
+  if (k < nd) b.last_dof_vel[(size_t)e * nd + k] = lq;
 }
 
 // get_heights, one lane per (env, probe).  The statement order follows the reference's torch
@@ -569,14 +625,22 @@ int fail(const char* what, hipError_t e) {
   g_err = buf;
   return -1;
 }
-int check_params(const gt_anymal_params* p) {
-  if (!p || p->num_envs <= 0 || p->num_dofs <= 0 || p->num_dofs > 16 || p->num_feet > 4 || p->num_knees > 4 ||
-      p->num_obs != 36 + 140 + p->num_dofs) {
+int check_params(const gt_anymal_params* p, const gt_anymal_buffers* b) {
+  const gt_anymal_hound* h = b ? b->hound : nullptr;
+  const int na = h ? h->num_actions : (p ? p->num_dofs : 0);
+  if (!p || !b || p->num_envs <= 0 || p->num_dofs <= 0 || p->num_dofs > 16 || p->num_feet > 4 || p->num_knees > 4 ||
+      na < p->num_dofs || na > kMaxActions || p->num_obs != 12 + 2 * p->num_dofs + 140 + na + (h ? 10 : 0)) {
     g_err = "gt_anymal: invalid parameters";
+    return -1;
+  }
+  if (h && (h->num_shoulders < 0 || h->num_shoulders > 4 || !h->eef_state || !h->arm_commands || !h->pos_control ||
+            !h->effort_control || h->num_actions != p->num_dofs + 6)) {
+    g_err = "gt_anymal: invalid UsefulHound extension";
     return -1;
   }
   return 0;
 }
+gt_anymal_hound hound_of(const gt_anymal_buffers* b) { return b->hound ? *b->hound : gt_anymal_hound{}; }
 }  // namespace
 
 // shared with the other task kernels of libgymtask (gt_hound.hip)
@@ -588,7 +652,7 @@ int gt_abi_version(void) { return GT_ABI_VERSION; }
 const char* gt_last_error(void) { return g_err.c_str(); }
 
 int gt_anymal_post_physics_a(const gt_anymal_params* p, const gt_anymal_buffers* b, void* stream) {
-  if (check_params(p)) return -1;
+  if (check_params(p, b)) return -1;
   if (!b->reset_count) {
     g_err = "gt_anymal_post_physics_a: reset_count (int32[3], zero-initialised) is required";
     return -1;
@@ -598,8 +662,10 @@ int gt_anymal_post_physics_a(const gt_anymal_params* p, const gt_anymal_buffers*
   auto aligned = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
   const bool vec = p->num_dofs % 4 == 0 && aligned(b->torques) && aligned(b->actions) && aligned(b->last_actions) &&
                    aligned(b->last_dof_vel) && aligned(b->dof_state);
-  if (vec) hipLaunchKernelGGL(k_post_a<true>, grid, dim3(blk), 0, (hipStream_t)stream, *p, *b);
-  else hipLaunchKernelGGL(k_post_a<false>, grid, dim3(blk), 0, (hipStream_t)stream, *p, *b);
+  const gt_anymal_hound h = hound_of(b);
+  if (b->hound) hipLaunchKernelGGL((k_post_a<false, true>), grid, dim3(blk), 0, (hipStream_t)stream, *p, *b, h);
+  else if (vec) hipLaunchKernelGGL((k_post_a<true, false>), grid, dim3(blk), 0, (hipStream_t)stream, *p, *b, h);
+  else hipLaunchKernelGGL((k_post_a<false, false>), grid, dim3(blk), 0, (hipStream_t)stream, *p, *b, h);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("gt_anymal_post_physics_a", e);
 }
@@ -607,7 +673,11 @@ int gt_anymal_post_physics_a(const gt_anymal_params* p, const gt_anymal_buffers*
 int gt_anymal_reset(const gt_anymal_params* p, const gt_anymal_buffers* b, const int32_t* env_ids, int k,
                     const float* pos_offset, const float* dof_vel, const float* cmd_x, const float* cmd_y,
                     const float* cmd_heading, float* episode_out, void* stream) {
-  if (check_params(p)) return -1;
+  if (check_params(p, b)) return -1;
+  if (b->hound) {
+    g_err = "gt_anymal_reset: UsefulHound resets go through gt_anymal_reset_flagged";
+    return -1;
+  }
   hipStream_t st = (hipStream_t)stream;
   if (k <= 0) {
     hipError_t e = hipMemsetAsync(episode_out, 0, sizeof(float) * GT_ANYMAL_NUM_TERMS, st);
@@ -624,7 +694,7 @@ int gt_anymal_reset(const gt_anymal_params* p, const gt_anymal_buffers* b, const
 
 int gt_anymal_post_physics_b(const gt_anymal_params* p, const gt_anymal_buffers* b, const float* noise,
                              const gt_torch_rand_plan* noise_plan, void* stream) {
-  if (check_params(p)) return -1;
+  if (check_params(p, b)) return -1;
   if (p->num_obs > 256) {
     g_err = "gt_anymal_post_physics_b: num_obs > 256";
     return -1;
@@ -632,17 +702,22 @@ int gt_anymal_post_physics_b(const gt_anymal_params* p, const gt_anymal_buffers*
   const int blk = (p->num_obs + 63) / 64 * 64;
   gt_torch_rand_plan plan{};
   hipStream_t st = (hipStream_t)stream;
-  if (noise) {
-    hipLaunchKernelGGL(k_post_b<1>, dim3(p->num_envs), dim3(blk), 0, st, *p, *b, noise, plan);
-  } else if (noise_plan) {
-    if ((uint64_t)noise_plan->numel != (uint64_t)p->num_envs * p->num_obs || noise_plan->threads == 0) {
-      g_err = "gt_anymal_post_physics_b: noise plan does not cover obs_buf";
-      return -1;
-    }
-    hipLaunchKernelGGL(k_post_b<2>, dim3(p->num_envs), dim3(blk), 0, st, *p, *b, nullptr, *noise_plan);
-  } else {
-    hipLaunchKernelGGL(k_post_b<0>, dim3(p->num_envs), dim3(blk), 0, st, *p, *b, nullptr, plan);
+  const gt_anymal_hound h = hound_of(b);
+  if (noise_plan && !noise &&
+      ((uint64_t)noise_plan->numel != (uint64_t)p->num_envs * p->num_obs || noise_plan->threads == 0)) {
+    g_err = "gt_anymal_post_physics_b: noise plan does not cover obs_buf";
+    return -1;
   }
+  const int mode = noise ? 1 : noise_plan ? 2 : 0;
+  const gt_torch_rand_plan pl = (mode == 2) ? *noise_plan : plan;
+  const dim3 g(p->num_envs), bl(blk);
+#define GT_POST_B(M, H) hipLaunchKernelGGL((k_post_b<M, H>), g, bl, 0, st, *p, *b, h, noise, pl)
+  if (b->hound) {
+    if (mode == 1) GT_POST_B(1, true); else if (mode == 2) GT_POST_B(2, true); else GT_POST_B(0, true);
+  } else {
+    if (mode == 1) GT_POST_B(1, false); else if (mode == 2) GT_POST_B(2, false); else GT_POST_B(0, false);
+  }
+#undef GT_POST_B
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("gt_anymal_post_physics_b", e);
 }
@@ -651,7 +726,7 @@ int gt_anymal_reset_flagged(const gt_anymal_params* p, const gt_anymal_buffers* 
                             const gt_anymal_reset_draws* d, const gt_anymal_terrain_reset* terrain,
                             int32_t* env_ids_out, float* episode_out, float episode_length_s, void* scratch,
                             void* stream) {
-  if (check_params(p)) return -1;
+  if (check_params(p, b)) return -1;
   if (!b->reset_masks || !d || !env_ids_out || !episode_out || !scratch || k < 0 || k > p->num_envs) {
     g_err = "gt_anymal_reset_flagged: invalid arguments";
     return -1;
@@ -665,8 +740,14 @@ int gt_anymal_reset_flagged(const gt_anymal_params* p, const gt_anymal_buffers* 
   if (k == 0) return 0;
   unsigned* done = static_cast<unsigned*>(scratch);
   float* partial = static_cast<float*>(scratch) + 16;
-  hipLaunchKernelGGL(k_reset_flagged, dim3((p->num_envs + 63) / 64), dim3(64), 0, (hipStream_t)stream, *p, *b, k,
-                     *d, tr, terrain != nullptr, env_ids_out, episode_out, episode_length_s, partial, done);
+  const gt_anymal_hound h = hound_of(b);
+  const dim3 g((p->num_envs + 63) / 64), bl(64);
+  if (b->hound)
+    hipLaunchKernelGGL(k_reset_flagged<true>, g, bl, 0, (hipStream_t)stream, *p, *b, h, k, *d, tr, terrain != nullptr,
+                       env_ids_out, episode_out, episode_length_s, partial, done);
+  else
+    hipLaunchKernelGGL(k_reset_flagged<false>, g, bl, 0, (hipStream_t)stream, *p, *b, h, k, *d, tr,
+                       terrain != nullptr, env_ids_out, episode_out, episode_length_s, partial, done);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("gt_anymal_reset_flagged", e);
 }

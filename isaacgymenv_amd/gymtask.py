@@ -67,7 +67,16 @@ class GtAnymalBuffers(C.Structure):
         (n, C.c_void_p) for n in ("rew_buf", "episode_sums", "base_lin_vel", "base_ang_vel", "projected_gravity",
                                   "obs_buf", "noise_scale", "reset_count", "host_count")] + [
         ("seq", C.c_int32), ("reset_masks", C.c_void_p), ("obs_out", C.c_void_p), ("time_outs", C.c_void_p),
-        ("clip_obs", C.c_float), ("measured_heights", C.c_void_p)]
+        ("clip_obs", C.c_float), ("measured_heights", C.c_void_p), ("hound", C.c_void_p)]
+
+
+class GtAnymalHound(C.Structure):
+    """gt_anymal_hound (include/gymtask.h, ABI 3): UsefulHound's differences to the AnymalTerrain tail."""
+    _fields_ = [("num_actions", C.c_int32), ("num_shoulders", C.c_int32), ("shoulder_idx", C.c_int32 * 4),
+                ("eef_state", C.c_void_p), ("eef_stride", C.c_int32), ("arm_commands", C.c_void_p),
+                ("pos_control", C.c_void_p), ("effort_control", C.c_void_p), ("arm_default", C.c_float * 6),
+                ("arm_lower", C.c_float * 6), ("arm_upper", C.c_float * 6), ("arm_noise2", C.c_float),
+                ("u_arm", C.c_void_p), ("plan_arm", GtTorchRandPlan)]
 
 
 class GtAnymalResetDraws(C.Structure):
@@ -254,7 +263,9 @@ def _ptr(t):
 
 
 class AnymalTailKernels:
-    """Drives gt_anymal_* for an AnymalTerrain task on the GPU pipeline."""
+    """Drives gt_anymal_* for an AnymalTerrain task on the GPU pipeline, and for UsefulHound (the same
+    tail with the gt_anymal_hound differences: 12 leg dofs of 18, shoulder terminations, the arm's
+    reset draw, end-effector observations)."""
 
     TERMS = ["lin_vel_xy", "lin_vel_z", "ang_vel_z", "ang_vel_xy", "orient", "torques", "joint_acc",
              "base_height", "air_time", "collision", "stumble", "action_rate", "hip"]
@@ -264,8 +275,11 @@ class AnymalTailKernels:
         self.task = t = task
         dev = t.device
         N = t.num_envs
+        self.hound = hasattr(t, "hound_num_dof")
+        nd = int(t.hound_num_dof) if self.hound else int(t.num_dof)
+        self.nd = nd
         p = GtAnymalParams()
-        p.num_envs, p.num_dofs, p.num_bodies, p.num_obs = N, t.num_dof, t.num_bodies, t.num_obs
+        p.num_envs, p.num_dofs, p.num_bodies, p.num_obs = N, nd, int(t.contact_forces.shape[1]), t.num_obs
         p.base_index = int(t.base_index)
         p.num_feet = len(t.feet_indices)
         p.num_knees = len(t.knee_indices)
@@ -289,7 +303,8 @@ class AnymalTailKernels:
         p.lin_vel_scale, p.ang_vel_scale = float(t.lin_vel_scale), float(t.ang_vel_scale)
         p.dof_pos_scale, p.dof_vel_scale = float(t.dof_pos_scale), float(t.dof_vel_scale)
         p.height_meas_scale = float(t.height_meas_scale)
-        for k, v in enumerate(t.default_dof_pos[0].tolist()):
+        default = t.hound_default_dof_pos if self.hound else t.default_dof_pos
+        for k, v in enumerate(default[0].tolist()):
             p.default_dof_pos[k] = v
         for k, v in enumerate(t.base_init_state.tolist()):
             p.base_init_state[k] = v
@@ -324,6 +339,30 @@ class AnymalTailKernels:
         self._terrain_level = None
         self._b = None
         self._bound = None
+        # (struct field, task attribute) of the buffers whose storage the kernels use
+        self._stable = [(n, "last_hound_dof_vel" if (self.hound and n == "last_dof_vel") else n) for n in self._STABLE]
+        self._h = self._hound_struct() if self.hound else None
+
+    def _hound_struct(self):
+        t = self.task
+        h = GtAnymalHound()
+        h.num_actions = int(t.num_actions)
+        h.num_shoulders = len(t.base_indices)
+        for k, v in enumerate(t.base_indices.tolist()):
+            h.shoulder_idx[k] = v
+        rb = t._rigid_body_state
+        for x in (rb, t.arm_commands, t._pos_control, t._effort_control):
+            assert x.is_contiguous() and x.dtype == torch.float32 and x.device.type == "cuda"
+        h.eef_state = rb[0, t.eef_index].data_ptr()
+        h.eef_stride = int(rb.stride(0))
+        h.arm_commands, h.pos_control, h.effort_control = (x.data_ptr() for x in (t.arm_commands, t._pos_control,
+                                                                                   t._effort_control))
+        h.arm_default[:] = [float(v) for v in t.houndarm_default_dof_pos[:6].tolist()]
+        h.arm_lower[:] = [float(v) for v in t.houndarm_dof_lower_limits[:6].tolist()]
+        h.arm_upper[:] = [float(v) for v in t.houndarm_dof_upper_limits[:6].tolist()]
+        h.arm_noise2 = float(t.houndarm_dof_noise * 2.0)  # useful_hound.py:598, a Python double cast once
+        self._h_keep = (rb, t.arm_commands, t._pos_control, t._effort_control)
+        return h
 
     def __del__(self):
         if getattr(self, "_host_words", None) and _lib is not None:
@@ -338,13 +377,14 @@ class AnymalTailKernels:
     def _buffers(self):
         """The gt_anymal_buffers struct; rebuilt only if the task rebound a buffer (cheap on the hot path)."""
         t = self.task
-        cur = tuple(getattr(t, n) for n in self._STABLE)
+        cur = tuple(getattr(t, attr) for _, attr in self._stable)
         b = self._b
         if b is None or any(x is not y for x, y in zip(cur, self._bound)):
             b = GtAnymalBuffers()
-            for name, v in zip(self._STABLE, cur):
-                assert v.is_contiguous() and v.device.type == "cuda", name
+            for (name, attr), v in zip(self._stable, cur):
+                assert v.is_contiguous() and v.device.type == "cuda", attr
                 setattr(b, name, v.data_ptr())
+            b.hound = C.cast(C.pointer(self._h), C.c_void_p) if self._h is not None else None
             b.reset_buf = self.reset_bool.data_ptr()
             b.episode_sums = self.sums.data_ptr()
             b.noise_scale = self.noise_scale.data_ptr()
@@ -461,8 +501,9 @@ class AnymalTailKernels:
         applies the affine maps, the trimesh curriculum (update_terrain_level, :427-435), ranks the
         flagged envs (nonzero order) and fills extras["episode"]."""
         t = self.task
-        dev, nd = t.device, t.num_dof
+        dev, nd = t.device, self.nd
         tr = self._terrain_reset() if t.custom_origins else None
+        h = self._h
         d = self._draws
         if d is None:  # the affine maps are fixed per task
             d = self._draws = GtAnymalResetDraws()
@@ -470,25 +511,36 @@ class AnymalTailKernels:
                                    ("cmd_y", t.command_y_range), ("cmd_h", t.command_yaw_range)):
                 setattr(d, name + "_range", float(hi - lo))
                 setattr(d, name + "_lower", float(lo))
+        # draw order (anymal_terrain.py:385-398, useful_hound.py:571-605): dof offsets, dof velocities,
+        # [trimesh: root x, y], [UsefulHound: arm reset noise (k, 6)], command x, y, heading
         if self.inkernel_rng:
             u = None
             d.u_pos = d.u_vel = d.u_cmd_x = d.u_cmd_y = d.u_cmd_h = None
-            if tr is None:
-                d.plan_pos, d.plan_vel, d.plan_cmd_x, d.plan_cmd_y, d.plan_cmd_h = self.planner.plan_many(
-                    (k * nd, k * nd, k, k, k))
-            else:
+            sizes = [k * nd, k * nd] + ([2 * k] if tr is not None else []) + ([6 * k] if h is not None else [])
+            plans = self.planner.plan_many(sizes + [k, k, k])
+            d.plan_pos, d.plan_vel = plans[0], plans[1]
+            d.plan_cmd_x, d.plan_cmd_y, d.plan_cmd_h = plans[-3:]
+            rest = plans[2:-3]
+            if tr is not None:
                 tr.u_root_xy = None
-                (d.plan_pos, d.plan_vel, tr.plan_root_xy, d.plan_cmd_x, d.plan_cmd_y,
-                 d.plan_cmd_h) = self.planner.plan_many((k * nd, k * nd, 2 * k, k, k, k))
+                tr.plan_root_xy = rest.pop(0)
+            if h is not None:
+                h.u_arm = None
+                h.plan_arm = rest.pop(0)
         else:
             u = [rand_unit((k, nd), dev), rand_unit((k, nd), dev)]
             if tr is not None:
                 u.append(rand_unit((k, 2), dev))
+            if h is not None:
+                u.append(rand_unit((k, 6), dev))  # torch.rand((k, 6)), useful_hound.py:596
             u += [rand_unit((k, 1), dev) for _ in range(3)]
             d.u_pos, d.u_vel = u[0].data_ptr(), u[1].data_ptr()
             d.u_cmd_x, d.u_cmd_y, d.u_cmd_h = (x.data_ptr() for x in u[-3:])
+            extra = u[2:-3]
             if tr is not None:
-                tr.u_root_xy = u[2].data_ptr()
+                tr.u_root_xy = extra.pop(0).data_ptr()
+            if h is not None:
+                h.u_arm = extra.pop(0).data_ptr()
         ids = torch.empty(k, dtype=torch.int32, device=dev)
         ep = torch.empty(len(self.TERMS) + 1, dtype=torch.float32, device=dev)
         _check(lib().gt_anymal_reset_flagged(self.p, self._buffers(), k, d, tr, ids.data_ptr(), ep.data_ptr(),

@@ -20,7 +20,10 @@ tensor API's link kinematics (rigid-body state, Jacobian, mass matrix) in gs_kin
   draw and observation noise.
 On the GPU pipeline the leg PD + arm OSC of each decimation step is one HIP kernel (gt_hound_control,
 float64 6x6 algebra, one lane per env) instead of ~40 torch launches with two host-synchronising
-batched inverses; the torch statements remain the CPU-pipeline path (and the golden-tested spec).
+batched inverses, and the post-physics tail is AnymalTerrain's fused kernels with the UsefulHound
+extension (gt_anymal_hound: termination, reward, reset with the arm draw, 204-wide observations)
+without a nonzero() / host sync; the torch statements remain the CPU-pipeline path (and the
+golden-tested spec).
 The end-effector state comes from the rigid-body state tensor, which the reference acquires but
 never refreshes outside its debug-viz branch: it holds the prepared (initial) state, and so does
 ours.
@@ -34,7 +37,7 @@ from isaacgym import gymapi, gymtorch
 
 from ..utils.torch_jit_utils import (get_axis_params, quat_apply, quat_rotate_inverse, tensor_clamp, to_torch,
                                      torch_rand_float)
-from .anymal_terrain import REWARD_TERMS, AnymalTerrain, wrap_to_pi
+from .anymal_terrain import REWARD_TERMS, AnymalTerrain, torch_rand_unit, wrap_to_pi
 from .base.vec_task import VecTask
 
 HOUND_LEG_DOFS, HOUND_ARM_DOFS = 12, 6
@@ -152,11 +155,19 @@ class UsefulHound(AnymalTerrain):
         self.arm_commands = zeros(self.num_envs, 3)
         self._fused_refreshed = False
         self._control = None
+        self._kernels = None
+        self._heights_dev = None
         if self.device != "cpu":
-            # GPU pipeline: the leg PD + arm OSC of every decimation step is one kernel (gt_hound_control)
-            from ...gymtask import HoundControlKernel  # fails loudly when libgymtask.so is missing
+            # GPU pipeline: the leg PD + arm OSC of every decimation step is one kernel (gt_hound_control),
+            # the post-physics tail the fused AnymalTerrain kernels with the UsefulHound extension
+            from ...gymtask import AnymalTailKernels, HoundControlKernel  # fail loudly without libgymtask.so
             self._control = HoundControlKernel(self)
             self._torque_buf = zeros(self.num_envs, self.num_actions)
+            self.torques = self._torque_buf
+            if self.custom_origins:
+                self._heights_dev = zeros(self.num_envs, self.num_height_points)
+                self.height_points = self.height_points.contiguous()
+            self._kernels = AnymalTailKernels(self)
         self.gym.refresh_actor_root_state_tensor(self.sim)
         self.gym.refresh_net_contact_force_tensor(self.sim)
         self.gym.refresh_jacobian_tensors(self.sim)
@@ -384,16 +395,7 @@ class UsefulHound(AnymalTerrain):
         self.commands[env_ids, 3] = torch_rand_float(self.command_yaw_range[0], self.command_yaw_range[1], (k, 1),
                                                      device=dev).squeeze()
         self.commands[env_ids] *= (torch.norm(self.commands[env_ids, :2], dim=1) > 0.25).unsqueeze(1)
-        self.gym.set_actor_root_state_tensor_indexed(self.sim, gymtorch.unwrap_tensor(self.root_states),
-                                                     gymtorch.unwrap_tensor(env_ids_int32), len(env_ids_int32))
-        self.gym.set_dof_state_tensor_indexed(self.sim, gymtorch.unwrap_tensor(self.dof_state),
-                                              gymtorch.unwrap_tensor(env_ids_int32), len(env_ids_int32))
-        total_pos = torch.cat([self.hound_dof_pos, self._pos_control], axis=1)
-        total_effort = torch.zeros_like(total_pos)
-        self.gym.set_dof_position_target_tensor_indexed(self.sim, gymtorch.unwrap_tensor(total_pos),
-                                                        gymtorch.unwrap_tensor(env_ids_int32), len(env_ids_int32))
-        self.gym.set_dof_actuation_force_tensor_indexed(self.sim, gymtorch.unwrap_tensor(total_effort),
-                                                        gymtorch.unwrap_tensor(env_ids_int32), len(env_ids_int32))
+        self._set_reset_state(env_ids_int32)
         self.last_actions[env_ids] = 0.0
         self.last_hound_dof_vel[env_ids] = 0.0
         self.feet_air_time[env_ids] = 0.0
@@ -405,6 +407,20 @@ class UsefulHound(AnymalTerrain):
                 self.max_episode_length_s
             self.episode_sums[key][env_ids] = 0.0
         self.extras["episode"]["terrain_level"] = torch.mean(self.terrain_levels.float())
+
+    def _set_reset_state(self, env_ids_int32):
+        """useful_hound.py:608-627: root and dof state, arm position targets and zero efforts of the reset envs."""
+        n = len(env_ids_int32)
+        self.gym.set_actor_root_state_tensor_indexed(self.sim, gymtorch.unwrap_tensor(self.root_states),
+                                                     gymtorch.unwrap_tensor(env_ids_int32), n)
+        self.gym.set_dof_state_tensor_indexed(self.sim, gymtorch.unwrap_tensor(self.dof_state),
+                                              gymtorch.unwrap_tensor(env_ids_int32), n)
+        total_pos = torch.cat([self.hound_dof_pos, self._pos_control], axis=1)
+        total_effort = torch.zeros_like(total_pos)
+        self.gym.set_dof_position_target_tensor_indexed(self.sim, gymtorch.unwrap_tensor(total_pos),
+                                                        gymtorch.unwrap_tensor(env_ids_int32), n)
+        self.gym.set_dof_actuation_force_tensor_indexed(self.sim, gymtorch.unwrap_tensor(total_effort),
+                                                        gymtorch.unwrap_tensor(env_ids_int32), n)
 
     # ------------------------------------------------------------------ arm control
     def _compute_osc_torques(self, dpose):
@@ -455,10 +471,25 @@ class UsefulHound(AnymalTerrain):
         self.gym.refresh_net_contact_force_tensor(self.sim)
         self.gym.refresh_jacobian_tensors(self.sim)
         self.gym.refresh_mass_matrix_tensors(self.sim)
+        self.common_step_counter += 1
+        push = self.common_step_counter % self.push_interval == 0
+        if self._kernels is not None:
+            # the fused tail (AnymalTerrain.post_physics_step's kernel path, UsefulHound extension)
+            if push:
+                self.push_robots()
+            kern = self._kernels
+            kern.post_a()
+            snap = kern.rng_snapshot() if self.add_noise else None
+            kern.observe()
+            if kern.wait_reset_count() > 0:
+                if snap is not None:
+                    kern.rng_restore(snap)
+                kern.reset_flagged(kern.last_reset_count, torch_rand_unit)
+                kern.observe()
+            return
         self.progress_buf += 1
         self.randomize_buf += 1
-        self.common_step_counter += 1
-        if self.common_step_counter % self.push_interval == 0:
+        if push:
             self.push_robots()
         self.base_quat = self.root_states[:, 3:7]
         self.base_lin_vel = quat_rotate_inverse(self.base_quat, self.root_states[:, 7:10])

@@ -372,8 +372,41 @@ def record_hound(num_envs=N_HOUND, steps=STEPS_HOUND):
     rng = np.random.RandomState(17)
     actions = (2 * rng.rand(steps, num_envs, 18) - 1).astype(np.float32)
     recs = {k: [] for k in ("obs", "rew", "reset", "time_outs", "progress", "torques", "dof_state", "commands",
-                            "feet_air_time", "ep_mask", "ep_extras")}
+                            "feet_air_time", "ep_mask", "ep_extras",
+                            # tail inputs (state at post_physics_step entry, after its refreshes), for the
+                            # fused GPU tail (tests/test_hound_tail_gpu.py)
+                            "in_root", "in_contact", "in_dof", "in_torques", "in_actions", "in_last_actions",
+                            "in_last_dof_vel", "in_commands", "in_feet_air_time", "in_progress", "in_episode_sums",
+                            "in_timeout", "in_timeout_is_long", "in_rng_state", "in_push", "in_eef",
+                            "out_root", "out_dof", "out_last_actions", "out_last_dof_vel", "episode_sums")}
     terms = list(env.episode_sums.keys())
+    orig_post = env.post_physics_step
+
+    def traced_post():
+        sim = env.sim
+        recs["in_root"].append(_np(sim.root))
+        recs["in_contact"].append(_np(sim.cf).reshape(num_envs, -1, 3))
+        recs["in_dof"].append(_np(env.dof_state))
+        recs["in_torques"].append(_np(env.torques))
+        recs["in_actions"].append(_np(env.actions))
+        recs["in_last_actions"].append(_np(env.last_actions))
+        recs["in_last_dof_vel"].append(_np(env.last_hound_dof_vel))
+        recs["in_commands"].append(_np(env.commands))
+        recs["in_feet_air_time"].append(_np(env.feet_air_time))
+        recs["in_progress"].append(_np(env.progress_buf))
+        recs["in_episode_sums"].append(np.stack([_np(env.episode_sums[k]) for k in terms]))
+        recs["in_timeout"].append(_np(env.timeout_buf).astype(np.int64))
+        recs["in_timeout_is_long"].append(int(env.timeout_buf.dtype == torch.int64))
+        recs["in_rng_state"].append(torch.get_rng_state().numpy().copy())
+        recs["in_push"].append(int((env.common_step_counter + 1) % env.push_interval == 0))
+        recs["in_eef"].append(_np(env._eef_state))
+        orig_post()
+        recs["out_root"].append(_np(env.root_states))
+        recs["out_dof"].append(_np(env.dof_state))
+        recs["out_last_actions"].append(_np(env.last_actions))
+        recs["out_last_dof_vel"].append(_np(env.last_hound_dof_vel))
+
+    env.post_physics_step = traced_post
     for t in range(steps):
         obs, rew, reset, extras = env.step(torch.from_numpy(actions[t]))
         recs["obs"].append(_np(obs["obs"]))
@@ -385,6 +418,7 @@ def record_hound(num_envs=N_HOUND, steps=STEPS_HOUND):
         recs["dof_state"].append(_np(env.dof_state))
         recs["commands"].append(_np(env.commands))
         recs["feet_air_time"].append(_np(env.feet_air_time))
+        recs["episode_sums"].append(np.stack([_np(env.episode_sums[k]) for k in terms]))
         ep = extras.get("episode")
         recs["ep_mask"].append(int(ep is not None))
         recs["ep_extras"].append(np.array([float(ep["rew_" + k]) for k in terms] + [float(ep["terrain_level"])])

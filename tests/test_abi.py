@@ -83,7 +83,8 @@ def test_ctypes_struct_layouts_match_the_headers(tmp_path):
                "gt_torch_rand_plan": gymtask.GtTorchRandPlan, "gt_anymal_params": gymtask.GtAnymalParams,
                "gt_anymal_buffers": gymtask.GtAnymalBuffers, "gt_anymal_reset_draws": gymtask.GtAnymalResetDraws,
                "gt_hound_control_params": gymtask.GtHoundControlParams, "gt_ant_params": gymtask.GtAntParams,
-               "gt_ant_buffers": gymtask.GtAntBuffers, "gt_anymal_terrain_reset": gymtask.GtAnymalTerrainReset}
+               "gt_ant_buffers": gymtask.GtAntBuffers, "gt_anymal_terrain_reset": gymtask.GtAnymalTerrainReset,
+               "gt_anymal_hound": gymtask.GtAnymalHound}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gymsim.h"', '#include "gymtask.h"',
              "int main(void) {"]
     expect = []
