@@ -193,7 +193,11 @@ def timed_region(step, steps: int, warmup: int, world: int, sync=lambda: None) -
     return elapsed
 
 
-def ppo_leg(env, device, rank, world, epochs):
+FP32_MATRIX_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, 64 cyc/SIMD
+FP16_MATRIX_PEAK_TFLOPS = 2500.0  # dense bf16/f16 MFMA
+
+
+def ppo_leg(env, device, rank, world, epochs, task="AnymalTerrain"):
     import torch
     from isaacgymenv_amd.isaacgymenvs.config import compose
     from isaacgymenv_amd.rl import A2CAgent, PpoConfig
@@ -219,25 +223,40 @@ def ppo_leg(env, device, rank, world, epochs):
     elapsed = timed_region(agent.train_epoch, epochs, 0, world, sync=torch.cuda.synchronize)
     samples = agent.batch_size * world * epochs
     st = agent.epoch_stats()
-    return {"metric": "PPO samples/sec AnymalTerrain (rl_games a2c_continuous, AnymalTerrainPPO.yaml)",
+    # GEMM roofline of the two phases: 2*in*out flops per sample per Linear layer forward; the update
+    # runs forward + backward (input and weight gradients: ~3x the forward) over every sample mini_epochs times
+    fwd = sum(2 * m.in_features * m.out_features for m in agent.model.modules() if isinstance(m, torch.nn.Linear))
+    roll_flops = fwd * agent.batch_size
+    upd_flops = 3 * fwd * agent.batch_size * pcfg.mini_epochs
+    roll_tf = roll_flops / (t1 - t0) / 1e12
+    upd_tf = upd_flops / (t2 - t1) / 1e12
+    gemm = {"flops_per_sample_forward": fwd,
+            "rollout": {"flops": roll_flops, "achieved_tflops": roll_tf, "peak_tflops": FP32_MATRIX_PEAK_TFLOPS,
+                        "frac": roll_tf / FP32_MATRIX_PEAK_TFLOPS, "dtype": "f32",
+                        "note": "rollout time includes the env steps (VecTask.step x horizon)"},
+            "update": {"flops": upd_flops, "achieved_tflops": upd_tf, "peak_tflops": FP16_MATRIX_PEAK_TFLOPS,
+                       "frac": upd_tf / FP16_MATRIX_PEAK_TFLOPS, "dtype": "fp16 autocast"}}
+    return {"metric": f"PPO samples/sec {task} (rl_games a2c_continuous, AnymalTerrainPPO.yaml)",
             "value": samples / elapsed, "unit": "samples/s", "epochs": epochs,
             "ms_per_epoch": 1e3 * elapsed / epochs, "samples_per_epoch": agent.batch_size * world,
             "rollout_ms": 1e3 * (t1 - t0), "update_ms": 1e3 * (t2 - t1),
             "minibatches_per_epoch": pcfg.mini_epochs * agent.num_minibatches,
             "allreduce_bytes_per_minibatch": agent.num_params * 4 if world > 1 else 0,
             "dtype": "f32 rollout, fp16 autocast update (mixed_precision: True)",
-            "last_kl": st["kl"], "last_lr": st["lr"]}
+            "last_kl": st["kl"], "last_lr": st["lr"], "gemm_roofline": gemm}
 
 
-OTHER_CONFIGS = [  # BASELINE.json configs beside the headline one (one GPU, 4096 envs each)
-    ("Ant", "Ant num_envs=4096 (MJCF articulation, flat-ground contacts, 1 simulate/step)", []),
+OTHER_CONFIGS = [  # BASELINE.json configs beside the headline one (one GPU, 4096 envs each); the last field:
+    # also time PPO on it (BASELINE config 3 is "AnymalTerrain + PPO, heightfield contacts")
+    ("Ant", "Ant num_envs=4096 (MJCF articulation, flat-ground contacts, 1 simulate/step)", [], False),
     ("AnymalTerrain", "AnymalTerrain num_envs=4096 trimesh heightfield (5 simulates/step)",
-     ["task.env.terrain.terrainType=trimesh"]),
-    ("UsefulHound", "UsefulHound num_envs=4096 (quadruped + 6-DoF arm OSC, 18 DoF, 24 links, 5 simulates/step)", []),
+     ["task.env.terrain.terrainType=trimesh"], True),
+    ("UsefulHound", "UsefulHound num_envs=4096 (quadruped + 6-DoF arm OSC, 18 DoF, 24 links, 5 simulates/step)", [],
+     False),
 ]
 
 
-def other_config_leg(task, desc, overrides, num_envs, steps, warmup, device, rank, world):
+def other_config_leg(task, desc, overrides, num_envs, steps, warmup, device, rank, world, ppo_epochs=0):
     """env-steps/s of another BASELINE config (same timed-region rules) and the average duration of its
     physics launch (HIP events around gym.simulate on the launch stream)."""
     import torch
@@ -269,6 +288,8 @@ def other_config_leg(task, desc, overrides, num_envs, steps, warmup, device, ran
     out = {"task": task, "workload": desc, "value": env.num_envs * world * steps / elapsed, "unit": "env-steps/s",
            "steps": steps, "ms_per_step": 1e3 * elapsed / steps, "simulate_kernel_ms": ev0.elapsed_time(ev1) / 20,
            "kernel_variant": env.gym.amd_kernel_variant(env.sim)}
+    if ppo_epochs > 0:
+        out["ppo"] = ppo_leg(env, device, rank, world, ppo_epochs, task=f"{task} trimesh")
     del env, pool
     vec_task.EXISTING_SIM = None
     torch.cuda.empty_cache()
@@ -347,8 +368,9 @@ def _main():
     others = []
     if args.other_steps > 0:
         del env
-        for task, desc, ov in OTHER_CONFIGS:
-            others.append(other_config_leg(task, desc, ov, args.num_envs, args.other_steps, 20, device, rank, world))
+        for task, desc, ov, with_ppo in OTHER_CONFIGS:
+            others.append(other_config_leg(task, desc, ov, args.num_envs, args.other_steps, 20, device, rank, world,
+                                           ppo_epochs=min(args.ppo_epochs, 2) if with_ppo else 0))
 
     if rank == 0:
         traffic, traffic_note = None, None

@@ -8,7 +8,8 @@
 //
 // Contact rule (the oracle restates it in oracle/physics_oracle.c):
 //   for a candidate sphere (centre c, radius r) and threshold thr = r + contact_offset, every
-//   triangle whose closest point q to c lies within thr is a candidate surface:
+//   triangle whose closest point q to c lies within thr, and whose face normal is not pointing down
+//   (n_z >= TERRAIN_DOWN_NZ), is a candidate surface:
 //     * q interior to the face: normal = the face normal nf, separation = nf.(c - a) - r, also
 //       when the centre is below the face by at most r + TERRAIN_BACK (penetration);
 //     * q on an edge or vertex: only from the front side (nf.(c - a) >= 0), normal = (c - q)/|c - q|,
@@ -28,6 +29,11 @@
 #include "gs_math.h"
 
 #define TERRAIN_BACK 0.1f
+// faces whose unit normal points down (z below this) generate no contact: a heightfield's surface
+// faces up or sideways, and the slope-threshold vertex moves can invert a triangle, whose back face
+// would otherwise admit a sphere centre lying inside the terrain and push it down along the
+// inverted normal (trimesh AnymalTerrain blow-up, tools/probes/trimesh_nan_replay.py)
+#define TERRAIN_DOWN_NZ (-0.5f)
 
 struct TerrainDev {
   const float4* v;     // [rows*cols] world xyz (transform applied), w unused
@@ -105,6 +111,7 @@ GS_HD void triangle(const float* p, float r, float thr, const float4& A, const f
   if (!(l2 > 1e-14f)) return;  // degenerate (collapsed by two vertex moves)
   const float il = gs_rsqrt(l2);
   nf[0] *= il; nf[1] *= il; nf[2] *= il;
+  if (nf[2] < TERRAIN_DOWN_NZ) return;  // inverted (downward-facing) triangle
   const float ap[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
   const float sd = dot3(nf, ap);
   if (sd > thr || sd < -(r + TERRAIN_BACK)) return;

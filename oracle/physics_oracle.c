@@ -132,10 +132,12 @@ static void quat_to_mat(const real *q, real *R) { /* xyzw */
  * Sphere vs triangle, stated with a plane projection and edge clamping (the kernel walks the
  * Voronoi regions instead): the projection of c inside the triangle -> face contact along the face
  * normal (also from behind, up to r + TERRAIN_BACK); otherwise the nearest point of the three
- * edges, from the front side only.  The triangle CLOSEST to the centre gives the contact (first
+ * edges, from the front side only; triangles facing down (n_z < TERRAIN_DOWN_NZ, inverted by the
+ * slope-threshold vertex moves) are skipped.  The triangle CLOSEST to the centre gives the contact (first
  * found on ties).  Full scan of a window 3 cells wider than any triangle of a grid cell can reach
  * (vertices move at most one cell). */
 #define TERRAIN_BACK 0.1
+#define TERRAIN_DOWN_NZ (-0.5) /* downward-facing (inverted) triangles generate no contact */
 static void seg_closest(const real *p, const real *a, const real *b, real *q) {
     real ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, ap[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
     const real l2 = dot3(ab, ab);
@@ -153,6 +155,7 @@ static void tri_test(const real *p, real r, real thr, const real *a, const real 
     const real l = sqrt(dot3(nf, nf));
     if (!(l * l > 1e-14)) return;
     for (int k = 0; k < 3; ++k) nf[k] /= l;
+    if (nf[2] < TERRAIN_DOWN_NZ) return;
     const real ap[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
     const real sd = dot3(nf, ap);
     if (sd > thr || sd < -(r + TERRAIN_BACK)) return;
