@@ -284,7 +284,8 @@ int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_verti
 
 int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   if (!s || !m) return fail("gs_sim_set_model: null argument");
-  if (m->num_bodies > GS_MAXB || m->num_dofs > GS_MAXD || m->num_candidates > GS_MAXC || m->num_links > GS_MAXL)
+  if (m->num_bodies > GS_MAXB || m->num_dofs > GS_MAXD || m->num_candidates > GS_MAXC || m->num_links > GS_MAXL ||
+      m->num_shapes > GS_MAXSH)
     return fail("gs_sim_set_model: articulation exceeds compiled maxima (bodies/dofs/candidates/links)");
   if (m->num_links < m->num_bodies || !m->link_body || !m->link_pose || !m->link_com ||
       (m->num_candidates > 0 && !m->cand_link))
@@ -320,6 +321,26 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   for (int c = 0; c < m->num_candidates; ++c) {
     for (int k = 0; k < 3; ++k) h.cpoint[c][k] = (float)m->cand_point[3 * c + k];
     h.cradius[c] = (float)m->cand_radius[c];
+  }
+  // bounding sphere of each shape's candidates (centre = mean point, radius = farthest point + its
+  // radius, widened by 1e-4 relative so that float rounding never culls an active candidate)
+  for (int sh = 0; sh < m->num_shapes; ++sh) {
+    double cen[3] = {0, 0, 0}, rad = 0.0;
+    int cnt = 0;
+    for (int c = 0; c < m->num_candidates; ++c)
+      if (m->cand_shape[c] == sh) {
+        for (int k = 0; k < 3; ++k) cen[k] += m->cand_point[3 * c + k];
+        ++cnt;
+      }
+    for (int k = 0; k < 3; ++k) cen[k] /= cnt > 0 ? cnt : 1;
+    for (int c = 0; c < m->num_candidates; ++c)
+      if (m->cand_shape[c] == sh) {
+        double d2 = 0.0;
+        for (int k = 0; k < 3; ++k) d2 += (m->cand_point[3 * c + k] - cen[k]) * (m->cand_point[3 * c + k] - cen[k]);
+        rad = std::max(rad, std::sqrt(d2) + m->cand_radius[c]);
+      }
+    for (int k = 0; k < 3; ++k) h.shc[sh][k] = (float)cen[k];
+    h.shc[sh][3] = (float)(rad * (1.0 + 1e-4) + 1e-5);
   }
   int any_lim = 0;
   for (int j = 0; j < m->num_dofs; ++j) {

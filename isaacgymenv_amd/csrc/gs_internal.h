@@ -6,9 +6,10 @@
 
 #define GS_MAXB 32   // bodies per articulation
 #define GS_MAXD 32   // dofs per articulation
-#define GS_MAXC 96   // plane-contact candidates per articulation
+#define GS_MAXC 192  // contact candidates per articulation (UsefulHound with its arm hulls: 175)
 #define GS_MAXL 40   // reported links per articulation (fixed-joint links included)
 #define GS_MAXS 8    // force sensors per articulation
+#define GS_MAXSH 32  // collision shapes per articulation
 #define GS_WAVE 64
 
 // Model constants shared by every env, float32, one copy in device memory.
@@ -25,6 +26,9 @@ struct DevModel {
   float inertia[GS_MAXB][6]; // about COM, body axes: xx yy zz xy xz yz
   float cpoint[GS_MAXC][3];  // contact candidate, body frame
   float cradius[GS_MAXC];
+  // per collision shape: bounding sphere of its candidates (body frame centre xyz, radius incl. the
+  // candidates' own radii); a shape whose sphere clears the ground plane has no active candidate
+  float shc[GS_MAXSH][4];
   float effort[GS_MAXD];     // <= 0 : unlimited
   float vmax[GS_MAXD];       // <= 0 : unlimited
   float armature[GS_MAXD];

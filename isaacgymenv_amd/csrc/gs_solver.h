@@ -47,7 +47,12 @@ struct LaneCfg {
 #ifndef GS_TERR_LANES
 #define GS_TERR_LANES 4
 #endif
-  static constexpr int LB = FIT == 8 ? GS_NARROW_LANES : (TERR && FIT > GS_TERR_LANES) ? GS_TERR_LANES : FIT;
+  // LDS-starved topologies (FIT == 8): the widest of 4 / 2 / 1 env lanes that still lets 3 workgroups
+  // share a CU (their kernels hold 512 VGPR+AGPR per lane, so at most 4 waves per CU anyway): UsefulHound
+  // with its arm hulls (6,599 slots) runs 2 lanes, 3 workgroups per CU, instead of 4 lanes, 1 per CU
+  static constexpr int NARROW = (SLOTS * 4 * 4 * 3 <= 160 * 1024) ? 4 : (SLOTS * 2 * 4 * 3 <= 160 * 1024) ? 2 : 1;
+  static constexpr int LB = FIT == 8 ? (GS_NARROW_LANES < NARROW ? GS_NARROW_LANES : NARROW)
+                                     : (TERR && FIT > GS_TERR_LANES) ? GS_TERR_LANES : FIT;
   static_assert(SLOTS * LB * 4 <= 160 * 1024, "contact rows exceed the LDS of a CU even at 8 lanes");
 };
 
@@ -101,6 +106,19 @@ GS_HD void store_state(float* __restrict__ st, int N, int e, const EnvState<T>& 
   for (int j = 0; j < T::ND; ++j) st[(13 + T::ND + j) * N + e] = s.qd[j];
 }
 
+// f(c) for every candidate c of every shape whose bit is set in shb, in candidate order; shapes are
+// visited by compile-time recursion so each shape's candidate loop has constant bounds (and unrolls)
+template <class T, int SH = 0, class F>
+GS_HD __attribute__((always_inline)) void for_active_shapes(unsigned shb, F&& f) {
+  if constexpr (SH < T::NS) {
+    if ((shb >> SH) & 1u) {
+#pragma unroll
+      for (int c = T::sh_c0[SH]; c < T::sh_c1[SH]; ++c) f(c);
+    }
+    for_active_shapes<T, SH + 1>(shb, f);
+  }
+}
+
 // One substep for one env.  `lds` points at this lane's column of the
 // workgroup's [SLOTS][LB] contact-row staging area (LB = 1 in the host backend: a per-thread
 // scratch row).
@@ -147,6 +165,10 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
 #pragma unroll
   for (int w = 0; w < (NC + 31) / 32; ++w) actb[w] = 0u;
 #define GS_ACT(c) ((actb[(c) >> 5] >> ((c) & 31)) & 1u)
+  // shapes with an active candidate: the row, impulse and sweep loops visit only their candidates
+  // (same global candidate order: shapes in order, a shape's candidates contiguous)
+  static_assert(T::NS <= 32, "shape activity is one 32-bit word");
+  unsigned shb = 0u;
 
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
@@ -233,9 +255,24 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
     }
 
     // ---- contact candidates on body i: activity test + Jacobian rows -> LDS
+    // Plane: a shape whose bounding sphere clears the ground by contact_offset has no active candidate
+    // (exact: every candidate lies inside the sphere), so its candidates are not even transformed --
+    // boxes and mesh hulls away from the ground cost one test per shape instead of one per point.
+    bool shape_near[T::NS];
+#pragma unroll
+    for (int sh = 0; sh < T::NS; ++sh) {
+      shape_near[sh] = true;
+      if constexpr (!TERR) {
+        if (T::sh_body[sh] == i && T::sh_c1[sh] - T::sh_c0[sh] > 1) {
+          const float* sc = M->shc[sh];
+          const float cz = s.p[2] + X[i][2] + R[i][6] * sc[0] + R[i][7] * sc[1] + R[i][8] * sc[2];
+          shape_near[sh] = P.has_ground && (cz - sc[3] < P.contact_offset);
+        }
+      }
+    }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      if (T::cbody[c] == i) {
+      if (T::cbody[c] == i && shape_near[T::cshape[c]]) {
         float x[3];
         mat3vec(R[i], M->cpoint[c], x);
         x[0] += X[i][0]; x[1] += X[i][1]; x[2] += X[i][2];
@@ -263,7 +300,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
           }
           const bool actc = dist < P.contact_offset;
           if (actc) {
-            actb[c >> 5] |= 1u << (c & 31);
+            actb[c >> 5] |= 1u << (c & 31);  shb |= 1u << T::cshape[c];
             lds[(X_SEP + c) * LB] = dist - P.rest_offset;
             lds[(X_MU + c) * LB] = 0.5f * (mu_g[T::cshape[c] * N + e] + smu);
             float* nsl = lds + (T::NSLOT + 3 * c) * LB;
@@ -300,7 +337,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
         const float dist = s.p[2] + x[2] - r;
         const bool actc = P.has_ground && (dist < P.contact_offset);
         if (actc) {
-          actb[c >> 5] |= 1u << (c & 31);
+          actb[c >> 5] |= 1u << (c & 31);  shb |= 1u << T::cshape[c];
           lds[(X_SEP + c) * LB] = dist - P.rest_offset;
           lds[(X_MU + c) * LB] = 0.5f * (mu_g[T::cshape[c] * N + e] + P.ground_mu);
           const float xc[3] = {x[0], x[1], x[2] - r};
@@ -465,8 +502,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
   }
 
   // ---------------- contact rows: J (LDS) -> c = J nu_f, scaled Z = (L^-T J^T) D^-1/2, 1/diag
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
+  for_active_shapes<T>(shb, [&](const int c) {
     if (GS_ACT(c)) {
       const int SUP = T::csupp[c];
       const int leaf = T::cleaf[c];
@@ -504,7 +540,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
         slot[(3 * SUP + 3 + rr) * LB] = 1.f / d;
       }
     }
-  }
+  });
 
   // ---------------- joint-limit rows: J = sign * e_dof -> c, scaled Z, 1/diag (same elimination)
 #pragma unroll
@@ -546,9 +582,9 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
   for (int j = 0; j < ND; ++j) laml[j] = 0.f;
 #pragma unroll
   for (int k = 0; k < NV; ++k) wt[k] = 0.f;
-#pragma unroll
-  for (int c = 0; c < NC; ++c)
+  for_active_shapes<T>(shb, [&](const int c) {
     if (GS_ACT(c)) lamc[(3 * c) * LB] = lamc[(3 * c + 1) * LB] = lamc[(3 * c + 2) * LB] = 0.f;
+  });
   const float inv_h = 1.f / h;
   const int iters = P.pos_iters + P.vel_iters;
   for (int it = 0; it < iters; ++it) {
@@ -579,8 +615,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
           if (si < SUP) wt[supp_node<T>(leaf, si)] += z[si] * dl;
       }
     }
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
+    for_active_shapes<T>(shb, [&](const int c) {
       if (GS_ACT(c)) {
         const int SUP = T::csupp[c];
         const int leaf = T::cleaf[c];
@@ -619,7 +654,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
         lamc[(3 * c + 1) * LB] = lam[1];
         lamc[(3 * c + 2) * LB] = lam[2];
       }
-    }
+    });
     if (it == P.pos_iters - 1) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) wpos[k] = wt[k];
@@ -690,7 +725,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
       float f0 = 0.f, f1 = 0.f, f2 = 0.f;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        if (T::clink[c] == b) {
+        if (T::clink[c] == b && ((shb >> T::cshape[c]) & 1u)) {
           if (GS_ACT(c)) {
             const float lam[3] = {lamc[(3 * c) * LB], lamc[(3 * c + 1) * LB], lamc[(3 * c + 2) * LB]};
             if constexpr (TERR) {

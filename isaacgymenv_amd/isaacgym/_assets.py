@@ -20,7 +20,11 @@ callers rely on:
 
 Collision geometry is reduced to *contact candidates* for the plane contact
 generator in the kernels: a sphere is one point with radius r, a capsule is its
-two segment end points with radius r, a box is its 8 corners with radius 0.
+two segment end points with radius r, a box is its 8 corners with radius 0, and a
+triangle-mesh (STL) collision shape is its convex hull -- Isaac Gym's default
+treatment of a mesh collider (vhacd off) -- reduced to the hull's support points
+in 14 directions (the 6 axes and the 8 cube diagonals; a box gives back its 8
+corners) with radius 0.
 """
 from __future__ import annotations
 
@@ -35,7 +39,48 @@ from typing import Dict, List, Optional
 import numpy as np
 
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_PRISMATIC, JOINT_FREE = 0, 1, 2, 3
-SHAPE_SPHERE, SHAPE_CAPSULE, SHAPE_BOX, SHAPE_CYLINDER = 0, 1, 2, 3
+SHAPE_SPHERE, SHAPE_CAPSULE, SHAPE_BOX, SHAPE_CYLINDER, SHAPE_CONVEX = 0, 1, 2, 3, 4
+
+# support directions of a convex mesh collider's contact points: the 6 axes and the 8 cube diagonals
+_HULL_DIRS = np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1]] +
+                      [[sx, sy, sz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)], dtype=np.float64)
+
+
+def read_stl(path: str) -> np.ndarray:
+    """Vertices [3 * triangles, 3] of a binary or ASCII STL file."""
+    with open(path, "rb") as f:
+        data = f.read()
+    if len(data) >= 84:
+        n = int.from_bytes(data[80:84], "little")
+        if 84 + 50 * n == len(data):
+            rec = np.frombuffer(data[84:], dtype=np.dtype([("n", "<f4", 3), ("v", "<f4", (3, 3)), ("a", "<u2")]))
+            return rec["v"].reshape(-1, 3).astype(np.float64)
+    pts = [[float(x) for x in line.split()[1:4]] for line in data.decode("ascii", "replace").splitlines()
+           if line.strip().startswith("vertex")]
+    if not pts:
+        raise ValueError(f"{path}: not an STL file")
+    return np.array(pts, dtype=np.float64)
+
+
+def hull_support_points(vertices: np.ndarray) -> np.ndarray:
+    """The convex hull's support points along _HULL_DIRS (a linear function's maximum over a mesh is
+    attained at a hull vertex, so no hull construction is needed), duplicates removed, in direction order."""
+    idx = []
+    for d in _HULL_DIRS:
+        i = int(np.argmax(vertices @ d))
+        if not any(np.allclose(vertices[i], vertices[j], atol=1e-9) for j in idx):
+            idx.append(i)
+    return vertices[idx]
+
+
+def _mesh_file(urdf_dir: str, filename: str) -> Optional[str]:
+    name = filename[len("package://"):] if filename.startswith("package://") else filename
+    for base in (urdf_dir, os.path.dirname(urdf_dir)):
+        p = os.path.join(base, name)
+        if os.path.isfile(p):
+            return p
+    p = os.path.join(urdf_dir, os.path.basename(name))
+    return p if os.path.isfile(p) else None
 
 
 # --------------------------------------------------------------------------
@@ -110,7 +155,7 @@ class RawInertial:
 class RawShape:
     kind: int
     pose: Pose
-    size: List[float]  # sphere [r]; capsule/cylinder [r, length]; box [sx, sy, sz]
+    size: List[float]  # sphere [r]; capsule/cylinder [r, length]; box [sx, sy, sz]; convex [x, y, z, ...] points
 
 
 @dataclass
@@ -118,8 +163,8 @@ class RawLink:
     name: str
     inertial: Optional[RawInertial]
     shapes: List[RawShape]
-    # collision <mesh> files the contact generator does not simulate (gym.load_asset
-    # warns with the link names)
+    # collision <mesh> files the importer could not read as STL (gym.load_asset warns
+    # with the link names)
     dropped_meshes: List[str] = field(default_factory=list)
 
 
@@ -251,9 +296,20 @@ def parse_urdf(path: str) -> RawModel:
             elif ge.find("box") is not None:
                 shapes.append(RawShape(SHAPE_BOX, op, _floats(ge.find("box").get("size"), 3)))
             elif ge.find("mesh") is not None:
-                # triangle-mesh collision geometry is not simulated: recorded so
-                # that gym.load_asset can name the links it affects
-                dropped.append(ge.find("mesh").get("filename", ""))
+                # triangle-mesh collision geometry: its convex hull's support points (STL); a file that is
+                # missing or not STL is recorded so that gym.load_asset can name the links it affects
+                me = ge.find("mesh")
+                fn = me.get("filename", "")
+                mp = _mesh_file(os.path.dirname(os.path.abspath(path)), fn)
+                scale = np.array(_floats(me.get("scale"), 3, 1.0))
+                try:
+                    pts = hull_support_points(read_stl(mp) * scale) if mp and mp.lower().endswith(".stl") else None
+                except ValueError:
+                    pts = None
+                if pts is None:
+                    dropped.append(fn)
+                else:
+                    shapes.append(RawShape(SHAPE_CONVEX, op, pts.reshape(-1).tolist()))
         links[name] = RawLink(name, inert, shapes, dropped)
         order.append(name)
     joints = []
@@ -378,7 +434,8 @@ class Articulation:
         for bi, b in enumerate(self.bodies):
             for s in b.shapes:
                 link = self.shape_links[s_index] if self.shape_links is not None else bi
-                n = {SHAPE_SPHERE: 1, SHAPE_CAPSULE: 2, SHAPE_CYLINDER: 2, SHAPE_BOX: 8}[s.kind]
+                n = (len(s.size) // 3 if s.kind == SHAPE_CONVEX else
+                     {SHAPE_SPHERE: 1, SHAPE_CAPSULE: 2, SHAPE_CYLINDER: 2, SHAPE_BOX: 8}[s.kind])
                 out += [link] * n
                 s_index += 1
         return out
@@ -426,6 +483,9 @@ class Articulation:
                         for sy in (-1, 1):
                             for sz in (-1, 1):
                                 out.append((bi, s.pose.apply([sx * hx, sy * hy, sz * hz]), 0.0, s_index))
+                elif s.kind == SHAPE_CONVEX:
+                    for p in np.asarray(s.size, dtype=np.float64).reshape(-1, 3):
+                        out.append((bi, s.pose.apply(p), 0.0, s_index))
                 s_index += 1
         return out
 

@@ -606,8 +606,9 @@ class Gym:
         raw = load_raw(root, filename)
         meshes = [n for n in raw.link_order if raw.links[n].dropped_meshes]
         if meshes:
-            warnings.warn(f"{filename}: triangle-mesh collision geometry is not simulated (DESIGN.md section 6); "
-                          f"links without contacts: {', '.join(meshes)}", PhysicsDeviationWarning, stacklevel=2)
+            warnings.warn(f"{filename}: collision meshes that are not readable STL files are not simulated "
+                          f"(STL meshes collide as their convex hull, DESIGN.md section 6); links without "
+                          f"contacts: {', '.join(meshes)}", PhysicsDeviationWarning, stacklevel=2)
         art = build_articulation(raw, options.as_dict())
         return Asset(art, options)
 

@@ -47,7 +47,7 @@ typedef REAL real;
 
 #define MAXB 32
 #define MAXV 40
-#define MAXC 96
+#define MAXC 192
 
 typedef struct {
     int32_t nb, nd, nc, ns, fixed_base;

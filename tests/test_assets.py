@@ -60,3 +60,33 @@ def test_cartpole_model():
     assert art.dof_names() == ["slider_to_cart", "cart_to_pole"]
     assert art.fixed_base and art.dofs[0].has_limits and not art.dofs[1].has_limits
     assert all(b != 0 for b in flat["cbody"])  # no candidates on the welded root
+
+
+def test_stl_collision_meshes_collide_as_convex_hull_support_points(tmp_path):
+    """Hound.urdf:508-661: the arm's STL collision meshes become convex-hull contact points,
+    the support points of the hull in 14 directions (a box mesh gives back its 8 corners)."""
+    import numpy as np
+    from isaacgymenv_amd.isaacgym import _assets as A
+    from isaacgymenv_amd.isaacgym._model import flatten
+    # a binary STL cube [0, 2] x [0, 4] x [0, 6] mm -> scaled 0.001: corners only
+    corners = np.array([[x, y, z] for x in (0, 2) for y in (0, 4) for z in (0, 6)], dtype=np.float32)
+    faces = [(0, 1, 3), (0, 3, 2), (4, 6, 7), (4, 7, 5), (0, 4, 5), (0, 5, 1), (2, 3, 7), (2, 7, 6),
+             (0, 2, 6), (0, 6, 4), (1, 5, 7), (1, 7, 3)]
+    rec = np.zeros(len(faces), dtype=np.dtype([("n", "<f4", 3), ("v", "<f4", (3, 3)), ("a", "<u2")]))
+    rec["v"] = corners[np.array(faces)]
+    (tmp_path / "cube.stl").write_bytes(b"\0" * 80 + len(faces).to_bytes(4, "little") + rec.tobytes())
+    pts = A.hull_support_points(A.read_stl(str(tmp_path / "cube.stl")) * 0.001)
+    assert pts.shape == (8, 3)
+    assert {tuple(np.round(p * 1000).astype(int)) for p in pts} == {tuple(c) for c in corners.astype(int)}
+    # the packed Hound model: every arm link collides through its hull, none is dropped
+    raw = A.load_raw("/nonexistent", "urdf/UsefulHound/urdf/Hound.urdf")
+    arm = ["link1", "link2", "link3", "link4", "link5", "link6", "end_link"]
+    for n in arm:
+        assert not raw.links[n].dropped_meshes
+        assert [s.kind for s in raw.links[n].shapes] == [A.SHAPE_CONVEX]
+    art = A.build_articulation(raw, dict(collapse_fixed_joints=False, replace_cylinder_with_capsule=False))
+    flat = flatten(art)
+    assert flat["nc"] == 84 + 91 and flat["ns"] == 24
+    names = art.link_names()
+    cand_links = [names[i] for i in art.candidate_links()]
+    assert sum(n in arm for n in cand_links) == 91

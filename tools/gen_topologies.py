@@ -84,13 +84,18 @@ def topo_tables(flat: dict) -> dict:
     for b in range(nb - 1, 0, -1):
         subend[parent[b]] = max(subend[parent[b]], subend[b])
     cshape = [int(s) for s in flat["cshape"]]
+    ns = int(flat["ns"])
+    # candidates of shape s are contiguous (body, shape, point order): [sh_c0[s], sh_c1[s]) on body sh_body[s]
+    sh_c0 = [min([c for c in range(nc) if cshape[c] == s] or [nc]) for s in range(ns)]
+    sh_c1 = [max([c + 1 for c in range(nc) if cshape[c] == s] or [nc]) for s in range(ns)]
+    sh_body = [cbody[sh_c0[s]] if sh_c0[s] < nc else 0 for s in range(ns)]
     jkind = [int(k) for k in flat["jkind"]]
     team = team_tables(flat, parent, bdof, nbase)
     return dict(NR=int(flat["nr"]), clink=[int(l) for l in flat["clink"]], TEAM=team, NB=nb, ND=nd, NC=nc, NS=int(flat["ns"]), FIXED=fixed, NBASE=nbase, NV=nv, MAXDEP=maxdep,
                 parent=parent, bdof=bdof, jkind=jkind, dpar=dpar, depth=[len(a) for a in anc],
                 anc=[a + [-1] * (maxdep - len(a)) for a in anc], bgdof=bgdof, cbody=cbody, cleaf=cleaf,
                 csupp=csupp, cslot=cslot, NSLOT=max(off, 1), gbody=gbody, cshape=cshape, subend=subend,
-                lleaf=lleaf, lsupp=lsupp, lslot=lslot)
+                lleaf=lleaf, lsupp=lsupp, lslot=lslot, sh_c0=sh_c0, sh_c1=sh_c1, sh_body=sh_body)
 
 
 def team_tables(flat, parent, bdof, nbase):
@@ -173,7 +178,8 @@ def emit() -> str:
             lines.append(f"  static constexpr int {k} = {t[k]};")
         for k, n in (("parent", "NB"), ("bdof", "NB"), ("jkind", "NB"), ("bgdof", "NB"), ("subend", "NB"), ("dpar", "NV"),
                      ("depth", "NV"), ("gbody", "NV"), ("cbody", "NC"), ("clink", "NC"), ("cshape", "NC"), ("cleaf", "NC"), ("csupp", "NC"), ("cslot", "NC"),
-                     ("lleaf", "ND"), ("lsupp", "ND"), ("lslot", "ND")):
+                     ("lleaf", "ND"), ("lsupp", "ND"), ("lslot", "ND"), ("sh_c0", "NS"), ("sh_c1", "NS"),
+                     ("sh_body", "NS")):
             vals = t[k] if len(t[k]) else [0]
             dim = n if len(t[k]) else "1"
             lines.append(f"  static constexpr int {k}[{dim}] = {carr(vals)};")
