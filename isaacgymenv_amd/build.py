@@ -18,7 +18,8 @@ LIBDIR = os.path.join(HERE, "_lib")
 ARCH = os.environ.get("GS_OFFLOAD_ARCH", "gfx950")
 
 LIBS = {
-    "libgymsim.so": ["gs_physics.hip", "gs_team.hip", "gs_kinematics.hip", "gs_host.hip", "gs_capi.hip"],
+    "libgymsim.so": ["gs_physics.hip", "gs_phys_inst.hip", "gs_team.hip", "gs_kinematics.hip", "gs_host.hip",
+                     "gs_capi.hip"],
     "libgymtask.so": ["gt_anymal.hip", "gt_hound.hip", "gt_ant.hip"],
     "libgymrl.so": ["rl_gae.hip"],
 }
@@ -32,7 +33,26 @@ SIM_FLAGS = ["-fno-slp-vectorize"]
 EXTRA_FLAGS = {"libgymtask.so": ["-ffp-contract=off"], "libgymrl.so": ["-ffp-contract=off"], "libgymsim.so": SIM_FLAGS,
                "libgymsim_prof.so": SIM_FLAGS + ["-DGS_PHASE_PROFILE"]}
 HEADERS = ["gs_internal.h", "gs_topologies.h", "gs_math.h", "gs_terrain.h", "gs_solver.h", "gs_kinematics.h",
-           "torch_philox.h"]
+           "gs_physics_impl.h", "torch_philox.h"]
+# gs_phys_inst.hip is compiled once per (topology, kernel form): 0 simulate plane, 1 simulate terrain-mesh,
+# 2 fused PD step plane, 3 fused PD step terrain-mesh (gs_physics_impl.h)
+INST_SRC = "gs_phys_inst.hip"
+INST_FORMS = (0, 1, 2, 3)
+
+
+def topologies() -> list:
+    """Topology struct names in GS_FOR_EACH_TOPOLOGY order (gs_topologies.h, tools/gen_topologies.py)."""
+    import re
+    text = open(os.path.join(CSRC, "gs_topologies.h")).read()
+    body = text[text.index("#define GS_FOR_EACH_TOPOLOGY"):]
+    return re.findall(r"X\((Topo_\w+),", body)
+
+
+def _units(src: str) -> list:
+    """(object suffix, extra flags) of each compile of one source."""
+    if src != INST_SRC:
+        return [("", [])]
+    return [(f"_{t[5:]}_{f}", [f"-DGS_INST_TOPO={t}", f"-DGS_INST_FORM={f}"]) for t in topologies() for f in INST_FORMS]
 OBJDIR = os.path.join(LIBDIR, "obj")
 
 
@@ -84,12 +104,13 @@ def build(force: bool = False, verbose: bool = True, prof: bool = False) -> None
                                                               os.path.join(os.path.dirname(HERE), "include", header)]
         objs = []
         for src in srcs:
-            obj = os.path.join(odir, src.replace(".hip", ".o"))
-            objs.append(obj)
-            if force or _deps_newer(obj, [os.path.join(CSRC, src)] + common):
-                cmd = [cc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c"] + inc
-                cmd += EXTRA_FLAGS.get(lib, []) + ["-o", obj, os.path.join(CSRC, src)]
-                compile_jobs.append((f"{lib}:{src}", cmd))
+            for suffix, defs in _units(src):
+                obj = os.path.join(odir, src.replace(".hip", suffix + ".o"))
+                objs.append(obj)
+                if force or _deps_newer(obj, [os.path.join(CSRC, src)] + common):
+                    cmd = [cc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c"] + inc + defs
+                    cmd += EXTRA_FLAGS.get(lib, []) + ["-o", obj, os.path.join(CSRC, src)]
+                    compile_jobs.append((f"{lib}:{src}{suffix}", cmd))
         link_jobs.append((lib, [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + ["-lpthread"]))
 
     def run(job):
@@ -110,7 +131,8 @@ def build(force: bool = False, verbose: bool = True, prof: bool = False) -> None
                     print(r.stderr[-4000:], file=sys.stderr)
 
     # the slowest sources first so they overlap everything else
-    compile_jobs.sort(key=lambda j: 0 if ("gs_team" in j[0] or "gs_physics" in j[0] or "gs_host" in j[0]) else 1)
+    compile_jobs.sort(key=lambda j: 0 if "hound" in j[0] else (1 if ("gs_team" in j[0] or "gs_phys" in j[0]
+                                                                     or "gs_host" in j[0]) else 2))
     run_all(compile_jobs)
     run_all(link_jobs)
 

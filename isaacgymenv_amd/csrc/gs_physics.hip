@@ -25,120 +25,9 @@
 //   -> velocity limits -> semi-implicit integration with the position-phase
 //   velocity; the velocity-phase velocity is kept as state.
 
-#include "gs_solver.h"
+#include "gs_solver.h"  // (kernels: gs_physics_impl.h)
 
 namespace {
-
-// ---------------------------------------------------------------- kernels
-template <class T, bool TERR>
-__global__ __launch_bounds__((LaneCfg<T, TERR>::LB), 1) void k_simulate(const DevModel* __restrict__ M, DevParams P,
-                                                                SimBuffers B, const float* __restrict__ tau_aos) {
-  constexpr int LB = LaneCfg<T, TERR>::LB;
-  __shared__ float lds[LaneCfg<T, TERR>::SLOTS * LB];
-  const int e = blockIdx.x * LB + threadIdx.x;
-  if (e >= B.N) return;
-  simulate_env<T, TERR, LB>(M, P, B, tau_aos, e, lds + threadIdx.x);
-}
-
-template <class T, bool TERR>
-__global__ __launch_bounds__((LaneCfg<T, TERR>::LB), 1) void k_pd_step(const DevModel* __restrict__ M, DevParams P,
-                                                               SimBuffers B, PdDev A) {
-  constexpr int LB = LaneCfg<T, TERR>::LB;
-  __shared__ float lds[LaneCfg<T, TERR>::SLOTS * LB];
-  const int e = blockIdx.x * LB + threadIdx.x;
-  if (e >= B.N) return;
-  pd_step_env<T, TERR, LB>(M, P, B, A, e, lds + threadIdx.x);
-}
-
-// ---------------------------------------------------------------- terrain-mesh (TERR) kernels
-// The mesh narrowphase (gs_terrain::sphere_contact, a scan of the grid cells around a candidate) is
-// most of a TERR substep, and the candidates' queries are independent.  A 64-lane workgroup holds
-// LB env lanes (the per-env solver, as in k_simulate) and, before every substep, the WHOLE wave runs
-// the LB x NC queries of its envs: env lanes publish their candidate centres (candidate_centres, the
-// positions the solver's tree walk forms), every lane takes queries l, l + 64, ..., and the env lanes'
-// substep reads the results instead of querying inline (substep<..., QS = LB>).  Same results as the
-// inline query; the serial query chain per env shrinks from NC to ~NC * LB / 64.
-constexpr int kTerrWave = 64;
-
-template <class T, int LB>
-__device__ __forceinline__ void terrain_queries(const DevParams& P, int N, int e0, const float* __restrict__ qin,
-                                                float* __restrict__ qout) {
-  constexpr int NQ = T::NC * LB;
-  for (int q = threadIdx.x; q < NQ; q += kTerrWave) {
-    const int c = q / LB, l = q - c * LB;
-    if (e0 + l >= N) continue;
-    const float p[3] = {qin[(4 * c + 0) * LB + l], qin[(4 * c + 1) * LB + l], qin[(4 * c + 2) * LB + l]};
-    const float r = qin[(4 * c + 3) * LB + l];
-    float sep = 0.f, n[3] = {0.f, 0.f, 0.f};
-    const bool f = gs_terrain::sphere_contact(P.terr, p, r, r + P.contact_offset, sep, n);
-    qout[(5 * c + 0) * LB + l] = f ? 1.f : 0.f;
-    qout[(5 * c + 1) * LB + l] = sep;
-    qout[(5 * c + 2) * LB + l] = n[0];
-    qout[(5 * c + 3) * LB + l] = n[1];
-    qout[(5 * c + 4) * LB + l] = n[2];
-  }
-}
-
-template <class T>
-__global__ __launch_bounds__(kTerrWave, 1) void k_simulate_terr(const DevModel* __restrict__ M, DevParams P,
-                                                                SimBuffers B, const float* __restrict__ tau_aos) {
-  constexpr int LB = LaneCfg<T, true>::LB, NC = T::NC;
-  __shared__ float lds[LaneCfg<T, true>::SLOTS * LB];
-  __shared__ float qin[4 * NC * LB], qout[5 * NC * LB];
-  const int N = B.N, e0 = blockIdx.x * LB, e = e0 + threadIdx.x;
-  const bool env_lane = threadIdx.x < LB && e < N;
-  EnvState<T> s;
-  float tau[T::ND > 0 ? T::ND : 1];
-  if (env_lane) {
-    load_state<T>(B.state, N, e, s);
-#pragma unroll
-    for (int j = 0; j < T::ND; ++j) tau[j] = tau_aos ? tau_aos[(size_t)e * T::ND + j] : 0.f;
-  }
-  for (int sstep = 0; sstep < P.substeps; ++sstep) {  // uniform trip count: every lane meets every barrier
-    if (env_lane) candidate_centres<T>(M, s, qin + threadIdx.x, LB);
-    __syncthreads();
-    terrain_queries<T, LB>(P, N, e0, qin, qout);
-    __syncthreads();
-    if (env_lane) {
-      const bool last = (sstep == P.substeps - 1) && P.collect;
-      substep<T, true, LB, LB>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last,
-                               sstep == P.substeps - 1 ? B.sens : nullptr, qout + threadIdx.x);
-    }
-  }
-  if (env_lane) store_state<T>(B.state, N, e, s);
-}
-
-template <class T>
-__global__ __launch_bounds__(kTerrWave, 1) void k_pd_step_terr(const DevModel* __restrict__ M, DevParams P,
-                                                               SimBuffers B, PdDev A) {
-  constexpr int LB = LaneCfg<T, true>::LB, NC = T::NC;
-  __shared__ float lds[LaneCfg<T, true>::SLOTS * LB];
-  __shared__ float qin[4 * NC * LB], qout[5 * NC * LB];
-  const int N = B.N, e0 = blockIdx.x * LB, e = e0 + threadIdx.x;
-  const bool env_lane = threadIdx.x < LB && e < N;
-  EnvState<T> s;
-  float tau[T::ND];
-  if (env_lane) load_state<T>(B.state, N, e, s);
-  const int sub = P.substeps;
-  const int n_pd = A.decimation * sub;
-  const int total = (A.decimation + A.extra) * sub;
-  for (int it = 0; it < total; ++it) {  // uniform trip count: every lane meets every barrier
-    if (env_lane) {
-      if (it < n_pd && (it % sub) == 0) pd_torques<T>(A, e, s, it == 0, tau);
-      candidate_centres<T>(M, s, qin + threadIdx.x, LB);
-    }
-    __syncthreads();
-    terrain_queries<T, LB>(P, N, e0, qin, qout);
-    __syncthreads();
-    if (env_lane) {
-      const bool last = ((it % sub) == sub - 1) && P.collect;
-      substep<T, true, LB, LB>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last,
-                               it == total - 1 ? B.sens : nullptr, qout + threadIdx.x);
-      if (it == n_pd - 1) pd_dof_out<T>(A, e, s);
-    }
-  }
-  if (env_lane) pd_outputs<T>(M, P, B, A, e, s, tau);
-}
 
 // ---------------------------------------------------------------- tensor API kernels
 __global__ void k_refresh_root(const float* __restrict__ st, int N, const float* __restrict__ com0,
@@ -243,27 +132,23 @@ hipError_t launch_set_dof(float* state, int N, int nd, const float* src, const i
   return hipGetLastError();
 }
 
+// per-form launchers: defined in gs_physics_impl.h, instantiated in gs_phys_inst.hip
+template <class T>
+hipError_t launch_sim_plane(const DevModel*, const DevParams&, const SimBuffers&, const float*, hipStream_t);
+template <class T>
+hipError_t launch_sim_terr(const DevModel*, const DevParams&, const SimBuffers&, const float*, hipStream_t);
+template <class T>
+hipError_t launch_pd_plane(const DevModel*, const DevParams&, const SimBuffers&, const PdDev&, hipStream_t);
+template <class T>
+hipError_t launch_pd_terr(const DevModel*, const DevParams&, const SimBuffers&, const PdDev&, hipStream_t);
+
 template <class T>
 hipError_t launch_sim(const DevModel* M, const DevParams& P, const SimBuffers& B, const float* tau, hipStream_t st) {
-  if (P.has_terrain) {
-    constexpr int LB = LaneCfg<T, true>::LB;
-    hipLaunchKernelGGL((k_simulate_terr<T>), dim3((B.N + LB - 1) / LB), dim3(kTerrWave), 0, st, M, P, B, tau);
-  } else {
-    constexpr int LB = LaneCfg<T, false>::LB;
-    hipLaunchKernelGGL((k_simulate<T, false>), dim3((B.N + LB - 1) / LB), dim3(LB), 0, st, M, P, B, tau);
-  }
-  return hipGetLastError();
+  return P.has_terrain ? launch_sim_terr<T>(M, P, B, tau, st) : launch_sim_plane<T>(M, P, B, tau, st);
 }
 template <class T>
 hipError_t launch_pd(const DevModel* M, const DevParams& P, const SimBuffers& B, const PdDev& A, hipStream_t st) {
-  if (P.has_terrain) {
-    constexpr int LB = LaneCfg<T, true>::LB;
-    hipLaunchKernelGGL((k_pd_step_terr<T>), dim3((B.N + LB - 1) / LB), dim3(kTerrWave), 0, st, M, P, B, A);
-  } else {
-    constexpr int LB = LaneCfg<T, false>::LB;
-    hipLaunchKernelGGL((k_pd_step<T, false>), dim3((B.N + LB - 1) / LB), dim3(LB), 0, st, M, P, B, A);
-  }
-  return hipGetLastError();
+  return P.has_terrain ? launch_pd_terr<T>(M, P, B, A, st) : launch_pd_plane<T>(M, P, B, A, st);
 }
 
 #define GS_TOPO_ENTRY(T, SIG) {SIG, T::kName, &launch_sim<T>, &launch_pd<T>, T::NB, T::ND, T::NC, T::NS, T::SENS ? 1 : 0},
