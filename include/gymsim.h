@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 3
+#define GS_ABI_VERSION 4
 
 typedef struct gs_sim gs_sim;
 
@@ -196,6 +196,19 @@ int gs_sim_set_force_sensors(gs_sim *sim, int n, const int32_t *bodies);
 int gs_sim_bind_force_sensors(gs_sim *sim, float *sensor_soa);
 /* refresh_force_sensor_tensor: SoA -> [N*n][6] (ant.py:233-235) */
 int gs_sim_refresh_force_sensor(gs_sim *sim, float *out, void *stream);
+
+/* Joint drives (ABI 4): gym.set_actor_dof_properties with driveMode / stiffness / damping
+ * (useful_hound.py:391-404 sets them; PhysX articulation joint drives).  Per dof of the asset:
+ * mode 1 DOF_MODE_POS drives with stiffness kp and damping kd toward the position / velocity targets,
+ * mode 2 DOF_MODE_VEL with damping kd toward the velocity target, other modes no drive.  Implicit
+ * spring-damper per substep: kp (q* - q - h qd) + kd (qd* - qd) with (h kd + h^2 kp) added to the dof's
+ * mass-matrix diagonal.  Call after gs_sim_set_model; a sim with drives runs the
+ * one-env-per-lane kernel. */
+int gs_sim_set_dof_drives(gs_sim *sim, const int32_t *mode, const double *stiffness, const double *damping);
+/* Caller-owned drive targets [N*nd] float32 (set_dof_position_target_tensor(_indexed) /
+ * set_dof_velocity_target_tensor, useful_hound.py:622-627), read by every later simulate / pd_step;
+ * NULL = zero targets. */
+int gs_sim_bind_dof_targets(gs_sim *sim, const float *pos_targets, const float *vel_targets);
 
 /* Physics kernel selected by gs_sim_set_model: 1 one env per lane, 2 lane team, 3 host backend;
  * -1 on error. */

@@ -616,6 +616,51 @@ int gs_sim_set_force_sensors(gs_sim* s, int n, const int32_t* bodies) {
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_set_force_sensors hipMemcpy");
 }
 
+int gs_sim_set_dof_drives(gs_sim* s, const int32_t* mode, const double* stiffness, const double* damping) {
+  if (!s || !s->topo) return fail("gs_sim_set_dof_drives: model not set");
+  if (s->nd > 0 && (!mode || !stiffness || !damping)) return fail("gs_sim_set_dof_drives: null argument");
+  DevModel h = s->h_model;
+  int any = 0;
+  for (int j = 0; j < s->nd; ++j) {
+    // gymapi.DofDriveMode: 1 POS (stiffness, damping), 2 VEL (damping); NONE / EFFORT: no drive
+    const double kp = mode[j] == 1 ? stiffness[j] : 0.0;
+    const double kd = (mode[j] == 1 || mode[j] == 2) ? damping[j] : 0.0;
+    if (!(kp >= 0.0) || !(kd >= 0.0)) return fail("gs_sim_set_dof_drives: negative or NaN drive gain");
+    h.dkp[j] = (float)kp;
+    h.dkd[j] = (float)kd;
+    any |= (kp > 0.0 || kd > 0.0);
+  }
+  // the lane-team kernel has no drive terms: drives run the one-env-per-lane kernel
+  launch_sim_fn sim_fn = s->sim_fn;
+  launch_pd_fn pd_fn = s->pd_fn;
+  int variant = s->variant;
+  if (any && variant == 2) {
+    if (s->params.kernel_variant == 2)
+      return fail("gs_sim_set_dof_drives: the lane-team kernel (kernel_variant 2) has no joint drives");
+    sim_fn = s->topo->sim;
+    pd_fn = s->topo->pd;
+    variant = 1;
+  }
+  if (!s->host) {
+    hipError_t e = hipSetDevice(s->device);
+    if (e == hipSuccess) e = hipMemcpy(s->d_model, &h, sizeof(DevModel), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e, "gs_sim_set_dof_drives hipMemcpy");
+  }
+  s->h_model = h;
+  s->dp.any_drive = any;
+  s->sim_fn = sim_fn;
+  s->pd_fn = pd_fn;
+  s->variant = variant;
+  return 0;
+}
+
+int gs_sim_bind_dof_targets(gs_sim* s, const float* pos_targets, const float* vel_targets) {
+  if (!s || !s->topo) return fail("gs_sim_bind_dof_targets: model not set");
+  s->dp.ptgt = pos_targets;
+  s->dp.vtgt = vel_targets;
+  return 0;
+}
+
 int gs_sim_bind_force_sensors(gs_sim* s, float* soa) {
   if (ready(s, "gs_sim_bind_force_sensors")) return -1;
   if (s->h_model.nsens > 0 && !soa) return fail("gs_sim_bind_force_sensors: buffer required");

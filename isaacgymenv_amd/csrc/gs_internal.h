@@ -32,6 +32,9 @@ struct DevModel {
   float effort[GS_MAXD];     // <= 0 : unlimited
   float vmax[GS_MAXD];       // <= 0 : unlimited
   float armature[GS_MAXD];
+  // joint drives (DOF_MODE_POS: stiffness + damping, DOF_MODE_VEL: damping; 0 otherwise), implicit
+  // spring-damper folded into the substep's mass matrix and free velocity
+  float dkp[GS_MAXD], dkd[GS_MAXD];
   float lower[GS_MAXD], upper[GS_MAXD];  // joint limits where has_lim
   int has_lim[GS_MAXD];
   int nsens;                    // force sensors (leaf bodies)
@@ -51,6 +54,9 @@ struct DevParams {
   int any_limits;        // some dof has limits (uniform: skips the limit rows entirely)
   int has_terrain;       // a heightfield triangle mesh is present (TERR kernels, gs_terrain.h)
   TerrainDev terr;
+  int any_drive;         // some dof has drive gains (uniform: skips the drive terms entirely)
+  const float* ptgt;     // [N][nd] dof position targets or null (= 0)
+  const float* vtgt;     // [N][nd] dof velocity targets or null (= 0)
 };
 
 // SoA state: field f of env e at state[f*N + e]

@@ -388,6 +388,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
             float F[6];
             spi_mul(Ic[a], S[a], F);
             Mm[ga][ga] = dot6(S[a], F) + M->armature[T::bdof[a]];
+            if (P.any_drive) Mm[ga][ga] += h * (M->dkd[T::bdof[a]] + h * M->dkp[T::bdof[a]]);
 #pragma unroll
             for (int k = 0; k < T::MAXDEP; ++k) {
               if (k < T::depth[ga]) {
@@ -473,9 +474,14 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
 #pragma unroll
     for (int j = 0; j < T::ND; ++j) {
       float t = tau[j];
-      const float e = M->effort[j];
-      if (e > 0.f) t = clampf(t, -e, e);
+      const float ef = M->effort[j];
+      if (ef > 0.f) t = clampf(t, -ef, ef);
       r[NB6 + j] = t - bias[NB6 + j];
+      if (P.any_drive) {  // implicit drive: kp (q* - q - h qd) + kd (qd* - qd), (h kd + h^2 kp) on M's diagonal
+        const float pt = P.ptgt ? P.ptgt[(size_t)e * ND + j] : 0.f;
+        const float vt = P.vtgt ? P.vtgt[(size_t)e * ND + j] : 0.f;
+        r[NB6 + j] += M->dkp[j] * (pt - s.q[j] - h * s.qd[j]) + M->dkd[j] * (vt - s.qd[j]);
+      }
     }
 #pragma unroll
     for (int kk = 0; kk < NV; ++kk) {

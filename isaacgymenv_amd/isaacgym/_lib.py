@@ -78,6 +78,8 @@ def lib():
             "gs_debug_phase_cycles": (i, [vp, i, i]),
             "gs_sim_set_force_sensors": (i, [vp, i, vp]),
             "gs_sim_bind_force_sensors": (i, [vp, vp]),
+            "gs_sim_set_dof_drives": (i, [vp, vp, vp, vp]),
+            "gs_sim_bind_dof_targets": (i, [vp, vp, vp]),
             "gs_sim_refresh_force_sensor": (i, [vp, vp, vp]),
             "gs_sim_add_triangle_mesh": (i, [vp, vp, C.c_int64, vp, C.c_int64, vp, d, d, d]),
             "gs_debug_terrain_query": (i, [vp, vp, vp, i, vp, vp]),
@@ -102,7 +104,7 @@ EXPORTED_SYMBOLS = [
     "gs_sim_kernel_variant", "gs_sim_enable_timing", "gs_sim_last_kernel_ms", "gs_debug_phase_cycles",
     "gs_sim_set_force_sensors", "gs_sim_bind_force_sensors", "gs_sim_refresh_force_sensor",
     "gs_sim_add_triangle_mesh", "gs_debug_terrain_query", "gs_sim_refresh_rigid_body", "gs_sim_refresh_jacobian",
-    "gs_sim_refresh_mass_matrix",
+    "gs_sim_refresh_mass_matrix", "gs_sim_set_dof_drives", "gs_sim_bind_dof_targets",
 ]
 
 

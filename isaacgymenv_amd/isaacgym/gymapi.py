@@ -319,6 +319,7 @@ class Sim:
         self.ground: Optional[PlaneParams] = None
         self.mesh = None
         self.prepared = False
+        self.drives_dirty = False
         self.handle = None
         px = params.physx
         p = _lib.GsSimParams()
@@ -420,6 +421,13 @@ class Sim:
             _lib.check(L.gs_sim_bind_force_sensors(self.handle, self.sens_soa.data_ptr()), "gs_sim_bind_force_sensors")
         self.sensor_tensor = torch.zeros(N * len(sens), 6, dtype=f32, device=tdev)
         self.dof_force = torch.zeros(N * nd, dtype=f32, device=dev)
+        # joint-drive targets (set_dof_position/velocity_target_tensor), bound once; the gains come
+        # from the actors' dof properties (DOF_MODE_POS / DOF_MODE_VEL with stiffness / damping)
+        self.pos_target = torch.zeros(N * nd, dtype=f32, device=dev)
+        self.vel_target = torch.zeros(N * nd, dtype=f32, device=dev)
+        _lib.check(L.gs_sim_bind_dof_targets(self.handle, self.pos_target.data_ptr(), self.vel_target.data_ptr()),
+                   "gs_sim_bind_dof_targets")
+        self.apply_drives()
         # device mirrors used when the pipeline is on the CPU and the physics on the GPU
         if not self.gpu_pipeline and not self.host:
             self._root_dev = torch.zeros(N, 13, dtype=f32, device=dev)
@@ -433,23 +441,43 @@ class Sim:
         for kind in ("rigid_body", "jacobian", "mass_matrix"):  # acquired before prepare_sim
             self.refresh(kind)
 
-    def position_drives(self) -> bool:
-        """Some actor has a DOF_MODE_POS dof with drive gains (checked once: dof properties are fixed
-        once the sim is prepared; the reset path of UsefulHound asks on every reset)."""
-        if getattr(self, "_pos_drives", None) is None or not self.prepared:
-            found = False
-            for e in self.envs:
-                for a in e.actors:
-                    p = a.dof_props
-                    if np.any((p["driveMode"] == DOF_MODE_POS) & ((p["stiffness"] != 0) | (p["damping"] != 0))):
-                        found = True
-                        break
-                if found:
-                    break
-            if not self.prepared:
-                return found
-            self._pos_drives = found
-        return self._pos_drives
+    def drive_tables(self):
+        """(mode int32 [nd], stiffness [nd], damping [nd]) of the actors' dof properties.  Isaac Gym keeps
+        drive gains per actor; this simulator holds one set per sim (the in-scope tasks give every actor
+        the same properties), so actors whose drive settings differ are refused."""
+        first = None
+        for e in self.envs:
+            for a in e.actors:
+                p = a.dof_props
+                t = (p["driveMode"].astype(np.int32), p["stiffness"].astype(np.float64),
+                     p["damping"].astype(np.float64))
+                if first is None:
+                    first = t
+                elif not all(np.array_equal(x, y) for x, y in zip(first, t)):
+                    raise NotImplementedError("joint drives: actors with different driveMode / stiffness / damping "
+                                              "(one drive setting per sim, DESIGN.md section 6)")
+        return first
+
+    def apply_drives(self):
+        """Upload the drive gains (gs_sim_set_dof_drives); called at prepare_sim and whenever dof
+        properties change afterwards (set_actor_dof_properties)."""
+        self.drives_dirty = False
+        mode, kp, kd = self.drive_tables()
+        mode, kp, kd = (np.ascontiguousarray(x) for x in (mode, kp, kd))
+        _lib.check(_lib.lib().gs_sim_set_dof_drives(self.handle, mode.ctypes.data, kp.ctypes.data, kd.ctypes.data),
+                   "gs_sim_set_dof_drives")
+        self.kernel_variant = _lib.lib().gs_sim_kernel_variant(self.handle)
+
+    def set_targets(self, kind: str, src, idx=None, n: int = 0):
+        """Copy (or scatter, for the listed actor indices) a [N*nd] target tensor into the bound buffer."""
+        import torch
+        dst = self.pos_target if kind == "pos" else self.vel_target
+        src = src.reshape(self.num_envs, self.num_dofs).to(self.sim_device, dtype=torch.float32)
+        if idx is None:
+            dst.view(self.num_envs, self.num_dofs).copy_(src)
+            return
+        ids = idx[:n].to(self.sim_device, dtype=torch.long) if n else idx.to(self.sim_device, dtype=torch.long)
+        dst.view(self.num_envs, self.num_dofs)[ids] = src[ids]
 
     def _tensors(self):
         """Reference-layout tensors (sim owned; wrap_tensor shares them), sized from the created envs.
@@ -531,6 +559,8 @@ class Sim:
 
     def simulate(self):
         L = _lib.lib()
+        if self.drives_dirty:
+            self.apply_drives()
         _lib.check(L.gs_sim_simulate(self.handle, self.dof_force.data_ptr(), self.stream()), "gs_sim_simulate")
 
 
@@ -715,6 +745,8 @@ class Gym:
 
     def set_actor_dof_properties(self, env: Env, actor: int, props) -> bool:
         env.actors[actor].dof_props = np.array(props, dtype=DofPropertiesDtype).copy()
+        if getattr(env.sim, "prepared", False):
+            env.sim.drives_dirty = True  # uploaded before the next simulate (tasks update actor by actor)
         return True
 
     def get_actor_rigid_shape_properties(self, env: Env, actor: int):
@@ -858,21 +890,22 @@ class Gym:
         return True
 
     def set_dof_position_target_tensor(self, sim: Sim, t: GymTensor) -> bool:
-        return self._check_effort_mode(sim, "set_dof_position_target_tensor")
+        """Targets of DOF_MODE_POS dofs (joint drives); other dofs ignore them."""
+        sim.set_targets("pos", t.tensor)
+        return True
 
     def set_dof_position_target_tensor_indexed(self, sim: Sim, t: GymTensor, idx: GymTensor, n: int) -> bool:
-        """Position targets drive DOF_MODE_POS dofs only.  The in-scope tasks drive every dof in
-        DOF_MODE_EFFORT (UsefulHound sets targets on reset, useful_hound.py:624-627, with zero PhysX
-        stiffness / damping), where a target has no effect: accepted and ignored."""
-        return self._check_effort_mode(sim, "set_dof_position_target_tensor_indexed")
+        """UsefulHound sets targets on reset (useful_hound.py:622-627); its dofs are DOF_MODE_EFFORT,
+        where a target has no effect."""
+        sim.set_targets("pos", t.tensor, idx.tensor, n)
+        return True
 
     def set_dof_velocity_target_tensor(self, sim: Sim, t: GymTensor) -> bool:
-        return self._check_effort_mode(sim, "set_dof_velocity_target_tensor")
+        sim.set_targets("vel", t.tensor)
+        return True
 
-    @staticmethod
-    def _check_effort_mode(sim: Sim, what: str) -> bool:
-        if sim.position_drives():
-            raise NotImplementedError(f"{what}: position-drive dofs are not simulated (DESIGN.md 6)")
+    def set_dof_velocity_target_tensor_indexed(self, sim: Sim, t: GymTensor, idx: GymTensor, n: int) -> bool:
+        sim.set_targets("vel", t.tensor, idx.tensor, n)
         return True
 
     # ---- viewer / rendering (headless build: no-ops)
@@ -927,6 +960,8 @@ class Gym:
         a.root_state_out = sim.root_tensor.data_ptr() if write_root else None
         a.contact_out = sim.contact_tensor.data_ptr() if write_contacts else None
         a.actions_copy_out = actions_copy_out.data_ptr() if actions_copy_out is not None else None
+        if sim.drives_dirty:
+            sim.apply_drives()
         _lib.check(L.gs_sim_pd_step(sim.handle, a, sim.stream()), "gs_sim_pd_step")
 
     def amd_enable_kernel_timing(self, sim: Sim, enable: bool = True):

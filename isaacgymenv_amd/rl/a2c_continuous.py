@@ -130,8 +130,9 @@ class _AverageMeter:
         old_size = torch.minimum(self.max_size - size, self.current_size)
         size_sum = old_size + size
         upd = cnt > 0
-        self.mean = torch.where(upd, (self.mean * old_size + new_mean * size) / size_sum.clamp(min=1.0), self.mean)
-        self.current_size = torch.where(upd, size_sum, self.current_size)
+        # in place: the rollout's captured step graphs hold these tensors
+        self.mean.copy_(torch.where(upd, (self.mean * old_size + new_mean * size) / size_sum.clamp(min=1.0), self.mean))
+        self.current_size.copy_(torch.where(upd, size_sum, self.current_size))
 
 
 class A2CAgent:
@@ -218,6 +219,13 @@ class A2CAgent:
         self.use_graphs = on_gpu and use_graphs and isaacgymenv_amd.GRAPHS_SAFE
         self._act_graph = None
         self._mb_graphs = None
+        # rollout bookkeeping around env.step, one (pre, post) graph pair per horizon slot once captured;
+        # env outputs are copied into these static buffers first (both paths, same arithmetic)
+        self._step_graphs = None
+        self._s_rew = torch.zeros(N, dtype=torch.float32, device=dev)
+        self._s_dones = torch.zeros(N, dtype=torch.uint8, device=dev)
+        self._s_timeouts = torch.zeros(N, dtype=torch.float32, device=dev)
+        self._has_timeouts = False
 
     # ------------------------------------------------------------------ multi-GPU
     def _broadcast_params(self):
@@ -255,36 +263,59 @@ class A2CAgent:
         self.obs = self.env.reset()
         return self.obs
 
+    def _store_pre(self, n, obs, res):
+        """Experience of slot n before env.step (rl_games play_steps' update_data calls)."""
+        self.b_obs[:, n] = obs
+        self.t_dones[n] = self.dones
+        self.t_values[n] = res["values"][:, 0]
+        self.b_actions[:, n] = res["actions"]
+        self.b_neglogp[:, n] = res["neglogpacs"]
+        self.b_mu[:, n] = res["mus"]
+        self.b_sigma[:, n] = res["sigmas"]
+
+    def _store_post(self, n, res):
+        """After env.step, from the static copies of its outputs: dones, shaped reward (value
+        bootstrap on time_outs), episode meters."""
+        cfg = self.cfg
+        rewards = self._s_rew
+        self.dones.copy_(self._s_dones)
+        shaped = (rewards + cfg.reward_shift) * cfg.reward_scale
+        if cfg.value_bootstrap and self._has_timeouts:
+            shaped = shaped + cfg.gamma * res["values"][:, 0] * self._s_timeouts
+        self.t_rewards[n] = shaped
+        self.current_rewards += rewards
+        self.current_lengths += 1
+        done = self.dones.bool()
+        self.game_rewards.update_masked(self.current_rewards, done)
+        self.game_lengths.update_masked(self.current_lengths, done)
+        not_done = 1.0 - self.dones.float()
+        self.current_rewards *= not_done
+        self.current_lengths *= not_done
+
     def play_steps(self):
         cfg = self.cfg
         if self.obs is None:
             self.env_reset()
+        graphs = self._step_graphs is not None
         for n in range(self.horizon):
             res = self.get_action_values(self.obs)
-            self.b_obs[:, n] = self._obs(self.obs)
-            self.t_dones[n] = self.dones
-            self.t_values[n] = res["values"][:, 0]
-            self.b_actions[:, n] = res["actions"]
-            self.b_neglogp[:, n] = res["neglogpacs"]
-            self.b_mu[:, n] = res["mus"]
-            self.b_sigma[:, n] = res["sigmas"]
+            if graphs:
+                self._step_graphs[n][0].replay()
+            else:
+                self._store_pre(n, self._obs(self.obs), res)
             actions = res["actions"]
             if cfg.clip_actions:
                 actions = torch.clamp(actions, -1.0, 1.0)  # action space is [-1, 1]: rescale is identity
             self.obs, rewards, dones, infos = self.env.step(actions)
-            self.dones = dones.to(torch.uint8)
-            shaped = (rewards + cfg.reward_shift) * cfg.reward_scale
-            if cfg.value_bootstrap and "time_outs" in infos:
-                shaped = shaped + cfg.gamma * res["values"][:, 0] * infos["time_outs"].float()
-            self.t_rewards[n] = shaped
-            self.current_rewards += rewards
-            self.current_lengths += 1
-            done = self.dones.bool()
-            self.game_rewards.update_masked(self.current_rewards, done)
-            self.game_lengths.update_masked(self.current_lengths, done)
-            not_done = 1.0 - self.dones.float()
-            self.current_rewards *= not_done
-            self.current_lengths *= not_done
+            self._s_rew.copy_(rewards)
+            self._s_dones.copy_(dones)
+            self._has_timeouts = "time_outs" in infos
+            if self._has_timeouts:
+                self._s_timeouts.copy_(infos["time_outs"])
+            if graphs:
+                self._step_graphs[n][1].replay()
+            else:
+                self._store_post(n, res)
         last_values = self.get_values(self.obs)[:, 0].contiguous()
         returns, advs, values = discount_values(self.t_rewards, self.t_values, self.t_dones, last_values,
                                                 self.dones.contiguous(), cfg.gamma, cfg.tau)
@@ -416,6 +447,16 @@ class A2CAgent:
             with torch.no_grad():
                 self._g_res = self.model({"is_train": False, "obs": self._g_obs})
         self._act_graph = g
+        # rollout bookkeeping per horizon slot (reads the act graph's static obs / outputs)
+        spool = torch.cuda.graph_pool_handle()
+        self._step_graphs = []
+        for n in range(self.horizon):
+            g_pre, g_post = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_pre, pool=spool):
+                self._store_pre(n, self._g_obs, self._g_res)
+            with torch.cuda.graph(g_post, pool=spool):
+                self._store_post(n, self._g_res)
+            self._step_graphs.append((g_pre, g_post))
         self.model.train()
         pool = torch.cuda.graph_pool_handle()
         self._mb_graphs = []

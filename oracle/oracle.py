@@ -23,7 +23,8 @@ class OModel(C.Structure):
         (n, C.c_void_p) for n in ("parent", "jkind", "bdof", "jorigin", "jaxis", "mass", "com", "inertia",
                                   "cbody", "cpoint", "cradius", "cshape", "effort", "vmax", "armature",
                                   "lower", "upper", "has_limits")] + [
-        ("nsens", C.c_int32), ("sens_body", C.c_void_p), ("nr", C.c_int32), ("clink", C.c_void_p)]
+        ("nsens", C.c_int32), ("sens_body", C.c_void_p), ("nr", C.c_int32), ("clink", C.c_void_p),
+        ("dkp", C.c_void_p), ("dkd", C.c_void_p)]
 
 
 class OParams(C.Structure):
@@ -52,6 +53,9 @@ def _lib(real_bits: int):
         lib = C.CDLL(path)
         lib.oracle_simulate.restype = C.c_int
         lib.oracle_simulate.argtypes = [C.POINTER(OModel), C.POINTER(OParams), C.c_int] + [C.c_void_p] * 6 + [C.c_int]
+        lib.oracle_simulate_targets.restype = C.c_int
+        lib.oracle_simulate_targets.argtypes = [C.POINTER(OModel), C.POINTER(OParams), C.c_int] + \
+            [C.c_void_p] * 6 + [C.c_int, C.c_void_p, C.c_void_p]
         lib.oracle_terrain_query.restype = C.c_int
         lib.oracle_terrain_query.argtypes = [C.POINTER(OParams), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         _LIBS[real_bits] = lib
@@ -61,9 +65,10 @@ def _lib(real_bits: int):
 class OracleSim:
     """Holds the model arrays alive and steps numpy state in place."""
 
-    def __init__(self, flat: dict, params: dict, real_bits: int = 64, sensor_bodies=(), terrain=None):
+    def __init__(self, flat: dict, params: dict, real_bits: int = 64, sensor_bodies=(), terrain=None, drives=None):
         """terrain: optional dict(vertices float32 [rows*cols, 3] world coordinates, rows, cols, x0, y0,
-        hs, friction) -- the heightfield-grid mesh of gym.add_triangle_mesh."""
+        hs, friction) -- the heightfield-grid mesh of gym.add_triangle_mesh.
+        drives: optional (kp [nd], kd [nd]) joint-drive gains."""
         self.flat = flat
         self.real = np.float64 if real_bits == 64 else np.float32
         self.lib = _lib(real_bits)
@@ -81,6 +86,12 @@ class OracleSim:
             a = np.ascontiguousarray(flat[k], dtype=np.float64)
             keep[k] = a
             setattr(m, k, a.ctypes.data)
+        if drives is not None:
+            for k, a in zip(("dkp", "dkd"), drives):
+                a = np.ascontiguousarray(a, dtype=np.float64)
+                assert a.shape == (int(flat["nd"]),)
+                keep[k] = a
+                setattr(m, k, a.ctypes.data)
         sb = np.ascontiguousarray(list(sensor_bodies) or [0], dtype=np.int32)
         keep["sens_body"] = sb
         m.nsens = len(sensor_bodies)
@@ -122,13 +133,17 @@ class OracleSim:
             raise RuntimeError("oracle_terrain_query: no terrain")
         return out
 
-    def simulate(self, root, dof, tau, mu, cf=None, num_threads: int = 1, sens=None) -> None:
-        for a in (root, dof, tau, mu) + ((cf,) if cf is not None else ()) + ((sens,) if sens is not None else ()):
+    def simulate(self, root, dof, tau, mu, cf=None, num_threads: int = 1, sens=None, pos_targets=None,
+                 vel_targets=None) -> None:
+        opt = tuple(a for a in (cf, sens, pos_targets, vel_targets) if a is not None)
+        for a in (root, dof, tau, mu) + opt:
             assert a.dtype == self.real and a.flags.c_contiguous
         n = root.shape[0]
-        rc = self.lib.oracle_simulate(C.byref(self.model), C.byref(self.params), n, root.ctypes.data,
-                                      dof.ctypes.data, tau.ctypes.data, mu.ctypes.data,
-                                      cf.ctypes.data if cf is not None else None,
-                                      sens.ctypes.data if sens is not None else None, num_threads)
+        rc = self.lib.oracle_simulate_targets(C.byref(self.model), C.byref(self.params), n, root.ctypes.data,
+                                              dof.ctypes.data, tau.ctypes.data, mu.ctypes.data,
+                                              cf.ctypes.data if cf is not None else None,
+                                              sens.ctypes.data if sens is not None else None, num_threads,
+                                              pos_targets.ctypes.data if pos_targets is not None else None,
+                                              vel_targets.ctypes.data if vel_targets is not None else None)
         if rc != 0:
             raise RuntimeError(f"oracle_simulate failed rc={rc}")

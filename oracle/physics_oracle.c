@@ -73,6 +73,10 @@ typedef struct {
     const int32_t *sens_body;   /* [nsens] leaf bodies */
     int32_t nr;                 /* reported links (>= nb: fixed-joint links kept, _model.flatten) */
     const int32_t *clink;       /* [nc] link whose net contact force a candidate adds to */
+    /* joint drives (PhysX articulation drives as an implicit spring-damper per
+     * substep), NULL = none: kp (q* - q - h qd) + kd (qd* - qd) with h kd + h^2 kp on M's diagonal */
+    const double *dkp;          /* [nd] or NULL */
+    const double *dkd;          /* [nd] or NULL */
 } OModel;
 
 typedef struct {
@@ -278,7 +282,8 @@ static void chol_solve(const real *L, int n, const real *b, real *x) {
 /* ------------------------------------------------------------- one env */
 static void env_substep(const OModel *m, const OParams *p, real h,
                         real *root, real *dq, const real *tau_in, const real *mu_shape,
-                        real *cforce /* nb*3 or NULL */, real *sens /* nsens*6 or NULL */)
+                        real *cforce /* nb*3 or NULL */, real *sens /* nsens*6 or NULL */,
+                        const real *ptgt /* nd or NULL */, const real *vtgt /* nd or NULL */)
 {
     const int nb = m->nb, nd = m->nd, fb = m->fixed_base;
     const int nbase = fb ? 0 : 6, nv = nbase + nd;
@@ -399,6 +404,8 @@ static void env_substep(const OModel *m, const OParams *p, real h,
         real Fi[6];
         spi_mul(&Ic[i], S[i], Fi);
         M[di * MAXV + di] = dot6(S[i], Fi) + (real)m->armature[m->bdof[i]];
+        if (m->dkp && m->dkd)
+            M[di * MAXV + di] += h * ((real)m->dkd[m->bdof[i]] + h * (real)m->dkp[m->bdof[i]]);
         for (int j = m->parent[i]; j > 0; j = m->parent[j]) {
             const int dj = nbase + m->bdof[j];
             const real v = dot6(S[j], Fi);
@@ -416,6 +423,11 @@ static void env_substep(const OModel *m, const OParams *p, real h,
         const real e = (real)m->effort[j];
         if (e > 0) t = t > e ? e : (t < -e ? -e : t);
         rhs[nbase + j] = t - bias[nbase + j];
+        if (m->dkp && m->dkd) {
+            const real pt = ptgt ? ptgt[j] : 0, vt = vtgt ? vtgt[j] : 0;
+            const real q = dq[2 * j], qd = dq[2 * j + 1];
+            rhs[nbase + j] += (real)m->dkp[j] * (pt - q - h * qd) + (real)m->dkd[j] * (vt - qd);
+        }
     }
     chol_solve(M, nv, rhs, acc);
     for (int k = 0; k < nv; ++k) nuf[k] = nu[k] + h * acc[k];
@@ -661,8 +673,20 @@ static void env_substep(const OModel *m, const OParams *p, real h,
  * cf    : [N][nr][3]  net contact force per reported link (written when collect_contacts), may be NULL
  * sens  : [N][nsens][6] force-sensor readings of the last substep, may be NULL
  */
+int oracle_simulate_targets(const OModel *m, const OParams *p, int n_envs, real *root, real *dof,
+                            const real *tau, const real *mu, real *cf, real *sens, int num_threads,
+                            const real *ptgt, const real *vtgt);
+
 int oracle_simulate(const OModel *m, const OParams *p, int n_envs, real *root, real *dof,
                     const real *tau, const real *mu, real *cf, real *sens, int num_threads)
+{
+    return oracle_simulate_targets(m, p, n_envs, root, dof, tau, mu, cf, sens, num_threads, NULL, NULL);
+}
+
+/* oracle_simulate with joint-drive targets ptgt / vtgt [N][nd] (NULL = 0) */
+int oracle_simulate_targets(const OModel *m, const OParams *p, int n_envs, real *root, real *dof,
+                            const real *tau, const real *mu, real *cf, real *sens, int num_threads,
+                            const real *ptgt, const real *vtgt)
 {
     if (m->nb > MAXB || m->nd + 6 > MAXV || m->nc > MAXC || m->nr < m->nb) return -1;
     const real h = (real)(p->dt / (p->substeps > 0 ? p->substeps : 1));
@@ -675,7 +699,8 @@ int oracle_simulate(const OModel *m, const OParams *p, int n_envs, real *root, r
             const int last = (s == p->substeps - 1);
             env_substep(m, p, h, root + 13 * e, dof + 2 * m->nd * e, tau + m->nd * e, mu + m->ns * e,
                         (cf && p->collect_contacts && last) ? cf + 3 * m->nr * e : NULL,
-                        (sens && last) ? sens + 6 * m->nsens * e : NULL);
+                        (sens && last) ? sens + 6 * m->nsens * e : NULL,
+                        ptgt ? ptgt + m->nd * e : NULL, vtgt ? vtgt + m->nd * e : NULL);
         }
     }
     (void)num_threads;

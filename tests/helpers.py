@@ -132,10 +132,11 @@ def anymal_states(n, seed=0, spread=1.0):
     return root, dof, tau, mu
 
 
-def make_gpu_sim(kind: str, n: int, params: dict, terrain=None, host: bool = False, threads: int = 4):
+def make_gpu_sim(kind: str, n: int, params: dict, terrain=None, host: bool = False, threads: int = 4, drives=None):
     """A libgymsim sim built through the drop-in gymapi (GPU pipeline); `terrain` (terrain_from_heights)
     adds the heightfield mesh with gym.add_triangle_mesh.  host=True builds the sim_device=cpu pipeline
-    instead (physx.use_gpu False: libgymsim's host backend on `threads` threads, host tensors)."""
+    instead (physx.use_gpu False: libgymsim's host backend on `threads` threads, host tensors).
+    drives = (mode [nd], stiffness [nd], damping [nd]) sets every actor's dof drive properties."""
     from isaacgymenv_amd.isaacgym import gymapi
     gym = gymapi.acquire_gym()
     sp = gymapi.SimParams()
@@ -190,13 +191,17 @@ def make_gpu_sim(kind: str, n: int, params: dict, terrain=None, host: bool = Fal
         env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 1), 8)
         pose = gymapi.Transform()
         pose.p = gymapi.Vec3(0, 0, {"anymal": 0.62, "ant": 0.44, "hound": 0.55}.get(kind, 2.0))
-        gym.create_actor(env, asset, pose, kind, i, 0, 0)
+        a = gym.create_actor(env, asset, pose, kind, i, 0, 0)
+        if drives is not None:
+            props = gym.get_actor_dof_properties(env, a)
+            props["driveMode"], props["stiffness"], props["damping"] = drives
+            gym.set_actor_dof_properties(env, a, props)
     gym.prepare_sim(sim)
     return gym, sim
 
 
-def make_host_sim(kind: str, n: int, params: dict, terrain=None, threads: int = 4):
-    return make_gpu_sim(kind, n, params, terrain=terrain, host=True, threads=threads)
+def make_host_sim(kind: str, n: int, params: dict, terrain=None, threads: int = 4, drives=None):
+    return make_gpu_sim(kind, n, params, terrain=terrain, host=True, threads=threads, drives=drives)
 
 
 def load_state_into(sim, root, dof, mu):

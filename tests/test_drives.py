@@ -1,0 +1,193 @@
+"""Joint drives (gymapi DOF_MODE_POS / DOF_MODE_VEL with stiffness / damping).
+
+Isaac Gym exposes PhysX articulation joint drives through the dof properties (driveMode, stiffness,
+damping) and the target tensors (set_dof_position_target_tensor(_indexed),
+set_dof_velocity_target_tensor; the reference's UsefulHound calls the indexed position setter at
+useful_hound.py:622-627).  The solver applies them as an implicit spring-damper per substep,
+kp (q* - q - h qd) + kd (qd* - qd) with (h kd + h^2 kp) on the mass-matrix diagonal; the fp64 oracle
+restates the same rule (oracle/physics_oracle.c).  Parity vs PhysX's drive is unpinned (PhysX is
+closed and absent).
+
+CPU tests (host backend, no GPU): host vs oracle with random targets (Cartpole, fixed base; Hound,
+floating base with ground contacts), a drive holds a pendulum at its target, indexed targets
+scatter by actor, drive settings that differ between actors are refused.
+GPU tests: the one-env-per-lane kernel vs the oracle, and a drive on ANYmal moves the sim off the
+lane-team kernel.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle.oracle import OracleSim
+from tests import helpers as H
+
+DOF_MODE_POS, DOF_MODE_VEL, DOF_MODE_EFFORT = 1, 2, 3
+
+
+def _cartpole_case(n, seed):
+    rng = np.random.RandomState(seed)
+    root = np.zeros((n, 13)); root[:, 2] = 2.0; root[:, 6] = 1.0
+    dof = np.zeros((n, 2, 2))
+    dof[:, :, 0] = 0.4 * (rng.rand(n, 2) - 0.5)
+    dof[:, :, 1] = 1.0 * (rng.rand(n, 2) - 0.5)
+    tau = np.zeros((n, 2)); tau[:, 0] = rng.uniform(-50, 50, n)
+    mu = np.ones((n, 1))
+    ptgt = rng.uniform(-0.5, 0.5, (n, 2))
+    vtgt = rng.uniform(-0.3, 0.3, (n, 2))
+    return root, dof, tau, mu, ptgt, vtgt
+
+
+CARTPOLE_DRIVES = (np.array([DOF_MODE_POS, DOF_MODE_VEL], dtype=np.int32), np.array([400.0, 0.0]),
+                   np.array([30.0, 2.0]))
+
+
+def _run_sim(kind, n, params, root, dof, tau, mu, ptgt, vtgt, drives, steps, host):
+    gym, sim = H.make_gpu_sim(kind, n, params, host=host, drives=drives)
+    H.load_state_into(sim, root, dof, mu)
+    dev = sim.state.device
+    sim.dof_force.copy_(torch.from_numpy(tau.astype(np.float32).reshape(-1)).to(dev))
+    from isaacgymenv_amd.isaacgym import gymtorch
+    gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(torch.from_numpy(ptgt.astype(np.float32)).to(dev)))
+    gym.set_dof_velocity_target_tensor(sim, gymtorch.unwrap_tensor(torch.from_numpy(vtgt.astype(np.float32)).to(dev)))
+    for _ in range(steps):
+        gym.simulate(sim)
+    if not host:
+        torch.cuda.synchronize()
+    return gym, sim, H.read_state(sim, dof.shape[1])
+
+
+def _run_oracle(flat, params, root, dof, tau, mu, ptgt, vtgt, drives, steps):
+    _, kp, kd = drives
+    kp = np.where(drives[0] == DOF_MODE_POS, kp, 0.0)
+    kd = np.where((drives[0] == DOF_MODE_POS) | (drives[0] == DOF_MODE_VEL), kd, 0.0)
+    o = OracleSim(flat, params, drives=(kp, kd))
+    r, d = root.copy(), dof.copy()
+    for _ in range(steps):
+        o.simulate(r, d, np.ascontiguousarray(tau), np.ascontiguousarray(mu),
+                   pos_targets=np.ascontiguousarray(ptgt), vel_targets=np.ascontiguousarray(vtgt))
+    return r, d
+
+
+def _cartpole_vs_oracle(host):
+    n, steps = 64, 20
+    art, flat = H.cartpole()
+    root, dof, tau, mu, ptgt, vtgt = _cartpole_case(n, seed=7)
+    gym, sim, (g_root, g_dof) = _run_sim("cartpole", n, H.CARTPOLE_PARAMS, root, dof, tau, mu, ptgt, vtgt,
+                                         CARTPOLE_DRIVES, steps, host)
+    o_root, o_dof = _run_oracle(flat, H.CARTPOLE_PARAMS, root, dof, tau, mu, ptgt, vtgt, CARTPOLE_DRIVES, steps)
+    np.testing.assert_allclose(g_dof, o_dof, atol=2e-4, rtol=1e-3)
+    # the drives are in effect: without them the same 20 steps end elsewhere
+    f_root, f_dof = _run_oracle(flat, H.CARTPOLE_PARAMS, root, dof, tau, mu, ptgt, vtgt,
+                                (CARTPOLE_DRIVES[0], np.zeros(2), np.zeros(2)), steps)
+    assert np.abs(f_dof - o_dof).max() > 1e-2
+    return sim
+
+
+def _hound_vs_oracle(host):
+    n = 96
+    art, flat = H.hound()
+    root, dof, tau, mu = H.hound_states(n, seed=9)
+    rng = np.random.RandomState(4)
+    mode = np.full(18, DOF_MODE_EFFORT, dtype=np.int32)
+    mode[12:] = DOF_MODE_POS  # arm joints position-driven, legs by effort
+    kp = np.where(mode == DOF_MODE_POS, 300.0, 7000.0)  # effort dofs keep gains that must be ignored
+    kd = np.where(mode == DOF_MODE_POS, 10.0, 50.0)
+    drives = (mode, kp, kd)
+    ptgt = rng.uniform(-1.0, 1.0, (n, 18))
+    vtgt = np.zeros((n, 18))
+    gym, sim, (g_root, g_dof) = _run_sim("hound", n, H.HOUND_PARAMS, root, dof, tau, mu, ptgt, vtgt, drives, 1, host)
+    o_root, o_dof = _run_oracle(flat, H.HOUND_PARAMS, root, dof, tau, mu, ptgt, vtgt, drives, 1)
+    assert np.all(np.isfinite(g_root)) and np.all(np.isfinite(g_dof))
+    H.assert_mostly_close(g_root[:, 0:7], o_root[:, 0:7], atol=2e-5, max_frac=5e-3, what="root pose")
+    H.assert_mostly_close(g_dof[:, :, 0], o_dof[:, :, 0], atol=2e-5, max_frac=5e-3, what="dof pos")
+    H.assert_mostly_close(g_root[:, 7:13], o_root[:, 7:13], atol=5e-3, rtol=5e-3, max_frac=5e-3, what="root vel")
+    H.assert_mostly_close(g_dof[:, :, 1], o_dof[:, :, 1], atol=5e-3, rtol=5e-3, max_frac=5e-3, what="dof vel")
+    return sim
+
+
+def test_cartpole_drives_host_match_oracle():
+    _cartpole_vs_oracle(host=True)
+
+
+def test_hound_arm_drives_host_match_oracle():
+    _hound_vs_oracle(host=True)
+
+
+def test_position_drive_holds_pendulum_at_target():
+    """Pole under gravity with a stiff position drive and no actuation settles at its target
+    (steady-state error = gravity torque / kp)."""
+    n = 8
+    drives = (np.array([DOF_MODE_POS, DOF_MODE_POS], dtype=np.int32), np.array([2000.0, 2000.0]),
+              np.array([200.0, 200.0]))
+    root = np.zeros((n, 13)); root[:, 2] = 2.0; root[:, 6] = 1.0
+    dof = np.zeros((n, 2, 2))
+    tgt = np.stack([np.linspace(-0.5, 0.5, n), np.linspace(0.4, -0.4, n)], axis=1)
+    gym, sim, (g_root, g_dof) = _run_sim("cartpole", n, H.CARTPOLE_PARAMS, root, dof, np.zeros((n, 2)),
+                                         np.ones((n, 1)), tgt, np.zeros((n, 2)), drives, 300, True)
+    np.testing.assert_allclose(g_dof[:, :, 0], tgt, atol=5e-3)
+    assert np.abs(g_dof[:, :, 1]).max() < 1e-2
+
+
+def test_indexed_targets_scatter_by_actor():
+    n = 6
+    gym, sim = H.make_host_sim("cartpole", n, H.CARTPOLE_PARAMS, drives=CARTPOLE_DRIVES)
+    from isaacgymenv_amd.isaacgym import gymtorch
+    src = torch.arange(2 * n, dtype=torch.float32).reshape(n, 2)
+    ids = torch.tensor([1, 4], dtype=torch.int32)
+    gym.set_dof_position_target_tensor_indexed(sim, gymtorch.unwrap_tensor(src), gymtorch.unwrap_tensor(ids), 2)
+    got = sim.pos_target.reshape(n, 2)
+    want = torch.zeros(n, 2)
+    want[[1, 4]] = src[[1, 4]]
+    assert torch.equal(got, want)
+
+
+def test_different_drive_gains_per_actor_are_refused():
+    gym, sim = H.make_host_sim("cartpole", 2, H.CARTPOLE_PARAMS, drives=CARTPOLE_DRIVES)
+    props = gym.get_actor_dof_properties(sim.envs[1], 0)
+    props["stiffness"][0] = 123.0
+    gym.set_actor_dof_properties(sim.envs[1], 0, props)
+    with pytest.raises(NotImplementedError):
+        gym.simulate(sim)
+
+
+def test_drives_updated_after_prepare_take_effect():
+    """Dof properties set actor by actor after prepare_sim are uploaded before the next simulate."""
+    n = 4
+    gym, sim = H.make_host_sim("cartpole", n, H.CARTPOLE_PARAMS)
+    for e in sim.envs:
+        props = gym.get_actor_dof_properties(e, 0)
+        props["driveMode"], props["stiffness"], props["damping"] = CARTPOLE_DRIVES
+        gym.set_actor_dof_properties(e, 0, props)
+    gym.simulate(sim)
+    assert not sim.drives_dirty
+
+
+@pytest.mark.gpu
+def test_cartpole_drives_gpu_match_oracle():
+    sim = _cartpole_vs_oracle(host=False)
+    assert sim.kernel_variant == 1
+
+
+@pytest.mark.gpu
+def test_hound_arm_drives_gpu_match_oracle():
+    _hound_vs_oracle(host=False)
+
+
+@pytest.mark.gpu
+def test_anymal_drives_leave_the_lane_team_kernel():
+    """ANYmal runs the lane-team kernel, which has no drive terms; position drives select the
+    one-env-per-lane kernel, and its step matches the oracle."""
+    n = 128
+    art, flat = H.anymal()
+    gym, sim = H.make_gpu_sim("anymal", n, H.ANYMAL_PARAMS)
+    assert sim.kernel_variant == 2
+    root, dof, tau, mu = H.anymal_states(n, seed=2)
+    mode = np.full(12, DOF_MODE_POS, dtype=np.int32)
+    drives = (mode, np.full(12, 80.0), np.full(12, 2.0))
+    ptgt = np.tile(dof[:, :, 0].mean(0), (n, 1)) + 0.1
+    gym, sim, (g_root, g_dof) = _run_sim("anymal", n, H.ANYMAL_PARAMS, root, dof, tau, mu, ptgt,
+                                         np.zeros((n, 12)), drives, 1, False)
+    assert sim.kernel_variant == 1
+    o_root, o_dof = _run_oracle(flat, H.ANYMAL_PARAMS, root, dof, tau, mu, ptgt, np.zeros((n, 12)), drives, 1)
+    H.assert_mostly_close(g_dof[:, :, 0], o_dof[:, :, 0], atol=2e-5, max_frac=5e-3, what="dof pos")
+    H.assert_mostly_close(g_dof[:, :, 1], o_dof[:, :, 1], atol=5e-3, rtol=5e-3, max_frac=5e-3, what="dof vel")
