@@ -9,6 +9,11 @@
  *            swap_and_flatten01 re-layout of the experience buffer: reads the
  *            time-major horizon buffers the rollout wrote, writes env-major
  *            [N][H] rows the PPO minibatches slice.
+ *   rl_splitk_accum : finish of the learner's split-K weight gradients (the
+ *            backward of rl_games' actor/critic nn.Linear layers, network_builder.py
+ *            A2CBuilder, as a batched GEMM over row blocks): sums the partials in
+ *            a fixed order and adds them into the parameter's fp32 gradient.
+ *   rl_rollout_post : the rollout bookkeeping after each env step (play_steps).
  *
  * All pointers are device pointers; calls are ordered on `stream` (a hipStream_t,
  * NULL = legacy default stream) and return 0 on success, otherwise a nonzero
@@ -23,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 1
+#define RL_ABI_VERSION 2
 
 int rl_abi_version(void);
 const char *rl_last_error(void);
@@ -44,6 +49,33 @@ const char *rl_last_error(void);
 int rl_gae(const float *rewards, const float *values, const uint8_t *dones, const float *last_values,
            const uint8_t *last_dones, int32_t horizon, int32_t num_envs, double gamma, double tau,
            float *returns_out, float *advs_out, float *values_out, void *stream);
+
+/*
+ * grad[i] += sum_{p = 0..num_parts-1} parts[p * n + i]   (i < n; fp32 sum in ascending p order)
+ *   parts  [num_parts][n]  fp16 (parts_are_f16 != 0) or f32, device
+ *   grad   [n] f32, device; any float offset (a view into a flat gradient buffer)
+ * Replaces `grad += parts.sum(0, dtype=float32)` (rl/network.py split-K weight gradient).
+ */
+int rl_splitk_accum(const void *parts, int32_t num_parts, int64_t n, int32_t parts_are_f16, float *grad,
+                    void *stream);
+
+/*
+ * Rollout bookkeeping after one VecTask.step (rl_games a2c_common.py play_steps, the statements after
+ * env_step: rewards_shaper + value bootstrap on time-outs, experience rewards / dones, current episode
+ * reward / length, game_rewards / game_lengths AverageMeter updates of the done envs, reset of the
+ * done envs' counters).  One workgroup; N <= any.
+ *   rewards [N] f32; dones [N] (dones_bytes 1: bool / uint8, 8: int64)
+ *   time_outs [N] (time_outs_bytes as dones) and values [N] f32: both null = no value bootstrap
+ *   shaped = (r + reward_shift) * reward_scale [+ gamma * value * (time_out != 0)]   (fp32, torch's order)
+ * Writes dones_out [N] u8, rewards_out [N] f32 (= shaped), current_rewards / current_lengths [N] f32
+ * (+= r, += 1, then * (1 - done)), meter_rewards / meter_lengths [2] f32 = (mean, current_size) of
+ * the AverageMeter(games_to_track) updated with the done envs' episode rewards / lengths.
+ */
+int rl_rollout_post(const float *rewards, const void *dones, int32_t dones_bytes, const void *time_outs,
+                    int32_t time_outs_bytes, const float *values, double reward_shift, double reward_scale,
+                    double gamma, int32_t num_envs, uint8_t *dones_out, float *rewards_out, float *current_rewards,
+                    float *current_lengths, float *meter_rewards, float *meter_lengths, int32_t games_to_track,
+                    void *stream);
 
 #ifdef __cplusplus
 }

@@ -85,6 +85,8 @@ struct gs_sim {
   bool timed = false;
   float4* d_tverts = nullptr;     // terrain mesh (gs_terrain.h)
   uint2* d_tcells = nullptr;
+  float* d_rows = nullptr;        // contact-row tiles of the GLOBAL-row kernels (TopoEntry::row_floats)
+  size_t rows_cap = 0;            // floats allocated
   // host backend (device < 0)
   bool host = false;
   HostPool* pool = nullptr;
@@ -158,6 +160,7 @@ void gs_sim_destroy(gs_sim* s) {
   if (s->d_links) (void)hipFree(s->d_links);
   if (s->d_tverts) (void)hipFree(s->d_tverts);
   if (s->d_tcells) (void)hipFree(s->d_tcells);
+  if (s->d_rows) (void)hipFree(s->d_rows);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   delete s;
@@ -447,12 +450,31 @@ int gs_sim_prepare(gs_sim* s, int num_envs, float* state, const float* shape_fri
   return 0;
 }
 
-static SimBuffers buffers(gs_sim* s) { return SimBuffers{s->state, s->mu, s->cf, s->N, s->sens}; }
+static SimBuffers buffers(gs_sim* s) { return SimBuffers{s->state, s->mu, s->cf, s->N, s->sens, s->d_rows}; }
+
+// floats of contact-row tiles the selected GPU kernel needs for N envs (0: its rows live in LDS)
+static size_t rows_needed(const gs_sim* s) {
+  if (s->host || !s->topo || s->variant != 1 || s->dp.has_terrain || s->topo->row_floats <= 0 || s->N <= 0) return 0;
+  const size_t lanes = (size_t)s->topo->row_lanes;
+  return ((size_t)s->N + lanes - 1) / lanes * lanes * (size_t)s->topo->row_floats;
+}
 
 static int ready(gs_sim* s, const char* where) {
   if (!s || !s->topo || !s->state) return fail("%s: sim not prepared", where);
   if (s->host ? !s->htopo : (!s->sim_fn || !s->pd_fn || !s->d_model || !s->d_links))
     return fail("%s: sim model incomplete", where);
+  if (const size_t need = rows_needed(s); need > s->rows_cap) {
+    // first step of an LDS-starved topology (or more envs than before): the row tiles, once
+    if (hipError_t e = hipSetDevice(s->device); e != hipSuccess) return hip_fail(e, where);
+    if (s->d_rows) (void)hipFree(s->d_rows);
+    s->d_rows = nullptr;
+    s->rows_cap = 0;
+    if (hipError_t e = hipMalloc(&s->d_rows, need * sizeof(float)); e != hipSuccess) {
+      s->d_rows = nullptr;
+      return hip_fail(e, where);
+    }
+    s->rows_cap = need;
+  }
   return 0;
 }
 

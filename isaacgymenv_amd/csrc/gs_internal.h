@@ -68,6 +68,7 @@ struct SimBuffers {
   float* cf;             // [3*nr][N]  (nr reported links)
   int N;
   float* sens;           // [6*nsens][N] force-sensor readings or null
+  float* rows;           // contact-row tiles of the GLOBAL-row kernels (LaneCfg::GLOBAL), else null
 };
 
 struct PdDev {
@@ -95,6 +96,8 @@ struct TopoEntry {
   launch_pd_fn pd;
   int nb, nd, nc, ns;
   int sens;  // force sensors compiled in (T::SENS)
+  int row_floats, row_lanes;  // SimBuffers::rows of the plane one-env-per-lane kernels: floats per env
+                              // (0 = rows in LDS) and env lanes per workgroup (LaneCfg<T, false>)
 };
 
 // Kinematics of the reported links (gs_kinematics.hip): runtime-sized tree tables, one copy in

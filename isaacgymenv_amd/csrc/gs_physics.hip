@@ -151,6 +151,8 @@ hipError_t launch_pd(const DevModel* M, const DevParams& P, const SimBuffers& B,
   return P.has_terrain ? launch_pd_terr<T>(M, P, B, A, st) : launch_pd_plane<T>(M, P, B, A, st);
 }
 
-#define GS_TOPO_ENTRY(T, SIG) {SIG, T::kName, &launch_sim<T>, &launch_pd<T>, T::NB, T::ND, T::NC, T::NS, T::SENS ? 1 : 0},
+#define GS_TOPO_ENTRY(T, SIG)                                                                          \
+  {SIG, T::kName, &launch_sim<T>, &launch_pd<T>, T::NB, T::ND, T::NC, T::NS, T::SENS ? 1 : 0,            \
+   LaneCfg<T, false>::ROW_FLOATS, LaneCfg<T, false>::LB},
 TopoEntry g_topologies[] = {GS_FOR_EACH_TOPOLOGY(GS_TOPO_ENTRY)};
 const int g_num_topologies = sizeof(g_topologies) / sizeof(g_topologies[0]);

@@ -11,21 +11,25 @@ namespace gs_phys {
 template <class T, bool TERR>
 __global__ __launch_bounds__((LaneCfg<T, TERR>::LB), 1) void k_simulate(const DevModel* __restrict__ M, DevParams P,
                                                                 SimBuffers B, const float* __restrict__ tau_aos) {
-  constexpr int LB = LaneCfg<T, TERR>::LB;
-  __shared__ float lds[LaneCfg<T, TERR>::SLOTS * LB];
+  using C = LaneCfg<T, TERR>;
+  constexpr int LB = C::LB;
+  __shared__ float lds[C::GLOBAL ? 1 : C::SLOTS * LB];
   const int e = blockIdx.x * LB + threadIdx.x;
   if (e >= B.N) return;
-  simulate_env<T, TERR, LB>(M, P, B, tau_aos, e, lds + threadIdx.x);
+  float* rows = C::GLOBAL ? B.rows + (size_t)blockIdx.x * C::SLOTS * LB + threadIdx.x : lds + threadIdx.x;
+  simulate_env<T, TERR, LB>(M, P, B, tau_aos, e, rows);
 }
 
 template <class T, bool TERR>
 __global__ __launch_bounds__((LaneCfg<T, TERR>::LB), 1) void k_pd_step(const DevModel* __restrict__ M, DevParams P,
                                                                SimBuffers B, PdDev A) {
-  constexpr int LB = LaneCfg<T, TERR>::LB;
-  __shared__ float lds[LaneCfg<T, TERR>::SLOTS * LB];
+  using C = LaneCfg<T, TERR>;
+  constexpr int LB = C::LB;
+  __shared__ float lds[C::GLOBAL ? 1 : C::SLOTS * LB];
   const int e = blockIdx.x * LB + threadIdx.x;
   if (e >= B.N) return;
-  pd_step_env<T, TERR, LB>(M, P, B, A, e, lds + threadIdx.x);
+  float* rows = C::GLOBAL ? B.rows + (size_t)blockIdx.x * C::SLOTS * LB + threadIdx.x : lds + threadIdx.x;
+  pd_step_env<T, TERR, LB>(M, P, B, A, e, rows);
 }
 
 // ---------------------------------------------------------------- terrain-mesh (TERR) kernels

@@ -51,9 +51,22 @@ struct LaneCfg {
   // share a CU (their kernels hold 512 VGPR+AGPR per lane, so at most 4 waves per CU anyway): UsefulHound
   // with its arm hulls (6,599 slots) runs 2 lanes, 3 workgroups per CU, instead of 4 lanes, 1 per CU
   static constexpr int NARROW = (SLOTS * 4 * 4 * 3 <= 160 * 1024) ? 4 : (SLOTS * 2 * 4 * 3 <= 160 * 1024) ? 2 : 1;
-  static constexpr int LB = FIT == 8 ? (GS_NARROW_LANES < NARROW ? GS_NARROW_LANES : NARROW)
+  // GLOBAL (compile knob GS_GLOBAL_LANES > 0, off by default): the LDS-starved plane kernels keep the
+  // contact rows in a per-workgroup tile of device memory (SimBuffers::rows, [SLOTS][LB] per workgroup)
+  // instead of LDS, so the lane count is no longer set by the 160 KB (GS_GLOBAL_LANES env lanes per wave;
+  // 4 = 1024 waves, one per SIMD, at 4096 envs).  Same arithmetic, same order.  Measured r02x: UsefulHound
+  // simulate 1.17 -> 2.34 ms per launch (the Gauss-Seidel chain waits on L2 latency instead of LDS), so
+  // the default keeps the rows in LDS (profiles/r02x_experiment_global_rows.txt).
+#ifndef GS_GLOBAL_LANES
+#define GS_GLOBAL_LANES 0
+#endif
+  static constexpr bool GLOBAL = (FIT == 8) && !TERR && (GS_GLOBAL_LANES > 0);
+  static constexpr int LB = GLOBAL ? GS_GLOBAL_LANES
+                          : FIT == 8 ? (GS_NARROW_LANES < NARROW ? GS_NARROW_LANES : NARROW)
                                      : (TERR && FIT > GS_TERR_LANES) ? GS_TERR_LANES : FIT;
-  static_assert(SLOTS * LB * 4 <= 160 * 1024, "contact rows exceed the LDS of a CU even at 8 lanes");
+  static_assert(GLOBAL || SLOTS * LB * 4 <= 160 * 1024, "contact rows exceed the LDS of a CU even at 8 lanes");
+  // floats of SimBuffers::rows per env (0: the rows live in LDS)
+  static constexpr int ROW_FLOATS = GLOBAL ? SLOTS : 0;
 };
 
 // World-frame force of candidate c's impulses (normal from LDS, tangents rebuilt), / h.

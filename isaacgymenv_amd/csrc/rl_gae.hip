@@ -70,6 +70,8 @@ __global__ __launch_bounds__(kWave) void k_gae(const float *__restrict__ rewards
 
 }  // namespace
 
+int rl_set_error(const char *msg) { return fail(msg); }
+
 extern "C" {
 
 int rl_abi_version(void) { return RL_ABI_VERSION; }

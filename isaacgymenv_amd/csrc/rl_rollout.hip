@@ -1,0 +1,111 @@
+// libgymrl.so -- rollout bookkeeping after each VecTask.step of the PPO learner (include/gymrl.h).
+//
+// rl_games a2c_common.py play_steps (v1.6.x), the statements after `self.env_step(actions)`:
+//   shaped_rewards = rewards_shaper(rewards) [+ gamma * values * time_outs  (value_bootstrap)]
+//   experience rewards[n] = shaped; current_rewards += rewards; current_lengths += 1
+//   game_rewards / game_lengths .update(current_* of the envs done this step)  (torch_ext.AverageMeter)
+//   current_* *= 1 - dones
+// as ONE workgroup (1024 lanes, 4096 envs = 4 per lane): the elementwise part is the same fp32
+// arithmetic torch's kernels do (built with -ffp-contract=off); the meters' masked sums are reduced
+// per lane in env order, then across the workgroup in a fixed LDS tree (deterministic, but not torch's
+// reduction order: the meters agree with the torch path to fp32 rounding).  Replaces ~20 torch launches
+// (~0.14 ms replayed as a HIP graph at 4096 envs) and the three static-buffer copies in front of them.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "gymrl.h"
+
+int rl_set_error(const char* msg);  // rl_gae.hip
+
+namespace {
+
+constexpr int kLanes = 1024;
+
+__device__ __forceinline__ bool flag(const void* p, int bytes, int i) {
+    return bytes == 8 ? static_cast<const int64_t*>(p)[i] != 0 : static_cast<const uint8_t*>(p)[i] != 0;
+}
+
+// AverageMeter.update with the masked sums (rl/a2c_continuous.py _AverageMeter.update_masked)
+__device__ void meter_update(float* m, float cnt, float vsum, float max_size) {
+    if (!(cnt > 0.f)) return;
+    const float new_mean = vsum / fmaxf(cnt, 1.f);
+    const float size = fminf(cnt, max_size);
+    const float old_size = fminf(max_size - size, m[1]);
+    const float size_sum = old_size + size;
+    m[0] = (m[0] * old_size + new_mean * size) / fmaxf(size_sum, 1.f);
+    m[1] = size_sum;
+}
+
+__global__ __launch_bounds__(kLanes) void k_rollout_post(
+    const float* __restrict__ rew, const void* __restrict__ dones_in, int dones_bytes,
+    const void* __restrict__ timeouts, int timeouts_bytes, const float* __restrict__ values, float shift, float scale,
+    float gamma, int N, uint8_t* __restrict__ dones_out, float* __restrict__ t_rewards, float* __restrict__ cur_rew,
+    float* __restrict__ cur_len, float* __restrict__ meter_rew, float* __restrict__ meter_len, float max_size) {
+    __shared__ float red[3][kLanes];
+    const int t = threadIdx.x;
+    float cnt = 0.f, srew = 0.f, slen = 0.f;
+    for (int i = t; i < N; i += kLanes) {
+        const float r = rew[i];
+        const bool d = flag(dones_in, dones_bytes, i);
+        dones_out[i] = d ? 1 : 0;
+        float shaped = (r + shift) * scale;
+        if (values && timeouts) {
+            const float to = flag(timeouts, timeouts_bytes, i) ? 1.f : 0.f;
+            shaped = shaped + gamma * values[i] * to;
+        }
+        t_rewards[i] = shaped;
+        const float cr = cur_rew[i] + r;
+        const float cl = cur_len[i] + 1.f;
+        if (d) {
+            cnt += 1.f;
+            srew += cr;
+            slen += cl;
+        }
+        const float nd = 1.f - (d ? 1.f : 0.f);
+        cur_rew[i] = cr * nd;
+        cur_len[i] = cl * nd;
+    }
+    red[0][t] = cnt;
+    red[1][t] = srew;
+    red[2][t] = slen;
+    __syncthreads();
+    for (int s = kLanes / 2; s > 0; s >>= 1) {
+        if (t < s) {
+            red[0][t] += red[0][t + s];
+            red[1][t] += red[1][t + s];
+            red[2][t] += red[2][t + s];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        meter_update(meter_rew, red[0][0], red[1][0], max_size);
+        meter_update(meter_len, red[0][0], red[2][0], max_size);
+    }
+}
+
+}  // namespace
+
+extern "C" int rl_rollout_post(const float* rewards, const void* dones, int32_t dones_bytes, const void* time_outs,
+                               int32_t time_outs_bytes, const float* values, double reward_shift, double reward_scale,
+                               double gamma, int32_t num_envs, uint8_t* dones_out, float* rewards_out,
+                               float* current_rewards, float* current_lengths, float* meter_rewards,
+                               float* meter_lengths, int32_t games_to_track, void* stream) {
+    if (num_envs <= 0) return rl_set_error("rl_rollout_post: num_envs must be positive");
+    if (!rewards || !dones || !dones_out || !rewards_out || !current_rewards || !current_lengths || !meter_rewards ||
+        !meter_lengths)
+        return rl_set_error("rl_rollout_post: null required pointer");
+    if ((dones_bytes != 1 && dones_bytes != 8) || (time_outs && time_outs_bytes != 1 && time_outs_bytes != 8))
+        return rl_set_error("rl_rollout_post: flags must be 1-byte (bool / uint8) or 8-byte (int64) elements");
+    hipLaunchKernelGGL(k_rollout_post, dim3(1), dim3(kLanes), 0, (hipStream_t)stream, rewards, dones, (int)dones_bytes,
+                       time_outs, (int)time_outs_bytes, values, (float)reward_shift, (float)reward_scale,
+                       (float)gamma, (int)num_envs, dones_out, rewards_out, current_rewards, current_lengths,
+                       meter_rewards, meter_lengths, (float)games_to_track);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        char msg[256];
+        snprintf(msg, sizeof(msg), "rl_rollout_post: launch failed: %s", hipGetErrorString(e));
+        return rl_set_error(msg) + 1;
+    }
+    return 0;
+}

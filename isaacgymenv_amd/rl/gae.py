@@ -14,7 +14,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libgymrl.so")
-EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae"]
+EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accum", "rl_rollout_post"]
 _lib = None
 
 
@@ -28,6 +28,11 @@ def lib():
         vp = C.c_void_p
         L.rl_gae.restype = C.c_int
         L.rl_gae.argtypes = [vp, vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_double, C.c_double, vp, vp, vp, vp]
+        L.rl_splitk_accum.restype = C.c_int
+        L.rl_splitk_accum.argtypes = [vp, C.c_int32, C.c_int64, C.c_int32, vp, vp]
+        L.rl_rollout_post.restype = C.c_int
+        L.rl_rollout_post.argtypes = [vp, vp, C.c_int32, vp, C.c_int32, vp, C.c_double, C.c_double, C.c_double,
+                                      C.c_int32, vp, vp, vp, vp, vp, vp, C.c_int32, vp]
         L.rl_last_error.restype = C.c_char_p
         L.rl_abi_version.restype = C.c_int
         _lib = L
@@ -76,3 +81,55 @@ def discount_values(rewards, values, dones, last_values, last_dones, gamma: floa
     if rc != 0:
         raise RuntimeError(f"rl_gae failed: {lib().rl_last_error().decode()}")
     return returns, advs, vals
+
+
+def splitk_accum(parts: torch.Tensor, grad: torch.Tensor) -> None:
+    """grad += parts.sum(0) in fp32, partials added in ascending order (include/gymrl.h rl_splitk_accum).
+    parts [P, ...] fp16 / f32 contiguous, grad f32 contiguous with parts[0]'s element count, both on one
+    device; ordered on torch's current stream (graph-capturable)."""
+    assert parts.is_cuda and grad.is_cuda and parts.device == grad.device
+    assert parts.is_contiguous() and grad.is_contiguous() and grad.dtype == torch.float32
+    assert parts.dtype in (torch.float16, torch.float32) and parts[0].numel() == grad.numel()
+    stream = torch.cuda.current_stream(grad.device).cuda_stream
+    rc = lib().rl_splitk_accum(parts.data_ptr(), parts.shape[0], grad.numel(), int(parts.dtype == torch.float16),
+                               grad.data_ptr(), stream)
+    if rc != 0:
+        raise RuntimeError(f"rl_splitk_accum failed: {lib().rl_last_error().decode()}")
+
+
+_FLAG_BYTES = {torch.bool: 1, torch.uint8: 1, torch.int64: 8}
+
+
+def rollout_post(rewards, dones, time_outs, values, reward_shift: float, reward_scale: float, gamma: float,
+                 dones_out, rewards_out, current_rewards, current_lengths, meter_rewards, meter_lengths,
+                 games_to_track: int) -> None:
+    """rl_games play_steps after env.step as one kernel (include/gymrl.h rl_rollout_post).
+    rewards f32 [N]; dones / time_outs bool, uint8 or int64 [N] (time_outs None: no value bootstrap);
+    values f32 [N] or [N, 1] or None; dones_out u8 [N]; rewards_out, current_* f32 [N];
+    meter_* f32 [2] = (mean, current_size)."""
+    N = rewards.shape[0]
+    dev = rewards.device
+    if dones.dtype not in _FLAG_BYTES:
+        dones = dones.to(torch.uint8)
+    if time_outs is not None and time_outs.dtype not in _FLAG_BYTES:
+        time_outs = time_outs.to(torch.uint8)
+    for t in (rewards, dones, dones_out, rewards_out, current_rewards, current_lengths, meter_rewards, meter_lengths,
+              time_outs, values):
+        if t is not None:
+            assert t.is_cuda and t.device == dev and t.is_contiguous()
+    assert rewards.dtype == rewards_out.dtype == current_rewards.dtype == current_lengths.dtype == torch.float32
+    assert dones_out.dtype == torch.uint8 and dones.numel() == N and dones_out.numel() == N
+    assert rewards_out.numel() == N and current_rewards.numel() == N and current_lengths.numel() == N
+    assert meter_rewards.numel() == 2 and meter_lengths.numel() == 2
+    assert (time_outs is None) == (values is None), "value bootstrap needs both time_outs and values"
+    if values is not None:
+        assert values.dtype == torch.float32 and values.numel() == N and time_outs.numel() == N
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    rc = lib().rl_rollout_post(rewards.data_ptr(), dones.data_ptr(), _FLAG_BYTES[dones.dtype], ptr(time_outs),
+                               _FLAG_BYTES[time_outs.dtype] if time_outs is not None else 0, ptr(values),
+                               float(reward_shift), float(reward_scale), float(gamma), N, dones_out.data_ptr(),
+                               rewards_out.data_ptr(), current_rewards.data_ptr(), current_lengths.data_ptr(),
+                               meter_rewards.data_ptr(), meter_lengths.data_ptr(), int(games_to_track), stream)
+    if rc != 0:
+        raise RuntimeError(f"rl_rollout_post failed: {lib().rl_last_error().decode()}")

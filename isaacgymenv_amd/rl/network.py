@@ -13,6 +13,7 @@ from typing import Dict, List
 import torch
 import torch.nn as nn
 
+from . import gae
 from .running_mean_std import RunningMeanStd
 
 _ACT = {"elu": nn.ELU, "relu": nn.ReLU, "tanh": nn.Tanh, "selu": nn.SELU, "None": nn.Identity, None: nn.Identity}
@@ -20,32 +21,45 @@ _ACT = {"elu": nn.ELU, "relu": nn.ReLU, "tanh": nn.Tanh, "selu": nn.SELU, "None"
 # Weight gradients of a minibatch (dW = g^T x, a reduction over the 16384 rows of AnymalTerrainPPO's
 # minibatch) are split over SPLIT_K row blocks as one batched GEMM + a float32 sum: as a single GEMM the
 # library tiles only the small N x K output (24-48 workgroups for 512 x 188) and takes ~100 us on
-# MI355X; split, ~25 us (tools/probes/gemm_splitk.py).
+# MI355X; split, ~25 us (tools/probes/gemm_splitk.py).  The sum is one HIP kernel that accumulates
+# into weight.grad (rl_splitk_accum, csrc/rl_grad.hip).
 SPLIT_K = 16
 SPLIT_K_MIN_ROWS = 4096
 
 
 class _SplitKLinearFn(torch.autograd.Function):
+    """Linear whose weight gradient is SPLIT_K row-block partial GEMMs finished by ONE HIP kernel that
+    adds them (fixed order, fp32) straight into ``weight.grad`` (libgymrl rl_splitk_accum; under the
+    learner ``weight.grad`` is a view into its flat gradient buffer).  The forward casts once to the
+    autocast dtype and keeps the cast operands for the backward, so the backward re-casts nothing."""
+
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda")
     def forward(ctx, x, w, b):
-        ctx.save_for_backward(x, w)
+        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+        xc, wc = x.to(dt), w.to(dt)
+        ctx.save_for_backward(xc, wc)
+        ctx.w = w
         ctx.has_bias = b is not None
-        return torch.nn.functional.linear(x, w, b)
+        return torch.nn.functional.linear(xc, wc, b.to(dt) if b is not None else None)
 
     @staticmethod
     @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, g):
-        x, w = ctx.saved_tensors
-        gx = g @ w.to(g.dtype) if ctx.needs_input_grad[0] else None
-        gw = None
+        xc, wc = ctx.saved_tensors
+        g = g.contiguous()
+        gx = g @ wc.to(g.dtype) if ctx.needs_input_grad[0] else None
         if ctx.needs_input_grad[1]:
+            w = ctx.w
             rows = g.shape[0]
-            xs = x.to(g.dtype)
-            gw = torch.bmm(g.reshape(SPLIT_K, rows // SPLIT_K, -1).transpose(1, 2),
-                           xs.reshape(SPLIT_K, rows // SPLIT_K, -1)).sum(0, dtype=torch.float32)
+            parts = torch.bmm(g.reshape(SPLIT_K, rows // SPLIT_K, -1).transpose(1, 2),
+                              xc.to(g.dtype).reshape(SPLIT_K, rows // SPLIT_K, -1))
+            if w.grad is None:
+                w.grad = torch.zeros_like(w, dtype=torch.float32)
+            gae.splitk_accum(parts, w.grad)
         gb = g.sum(0, dtype=torch.float32) if ctx.has_bias and ctx.needs_input_grad[2] else None
-        return gx, gw, gb
+        # the weight gradient is already in weight.grad (accumulated like autograd would)
+        return gx, None, gb
 
 
 class Linear(nn.Linear):
@@ -54,7 +68,7 @@ class Linear(nn.Linear):
 
     def forward(self, x):
         if (torch.is_grad_enabled() and x.dim() == 2 and x.shape[0] >= SPLIT_K_MIN_ROWS
-                and x.shape[0] % SPLIT_K == 0 and x.is_cuda):
+                and x.shape[0] % SPLIT_K == 0 and x.is_cuda and self.weight.dtype == torch.float32):
             return _SplitKLinearFn.apply(x, self.weight, self.bias)
         return super().forward(x)
 
