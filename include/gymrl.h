@@ -13,6 +13,7 @@
  *            backward of rl_games' actor/critic nn.Linear layers, network_builder.py
  *            A2CBuilder, as a batched GEMM over row blocks): sums the partials in
  *            a fixed order and adds them into the parameter's fp32 gradient.
+ *   rl_colsum_accum : the same layers' bias gradients (column sums), deterministic.
  *   rl_rollout_post : the rollout bookkeeping after each env step (play_steps).
  *
  * All pointers are device pointers; calls are ordered on `stream` (a hipStream_t,
@@ -57,6 +58,16 @@ int rl_gae(const float *rewards, const float *values, const uint8_t *dones, cons
  * Replaces `grad += parts.sum(0, dtype=float32)` (rl/network.py split-K weight gradient).
  */
 int rl_splitk_accum(const void *parts, int32_t num_parts, int64_t n, int32_t parts_are_f16, float *grad,
+                    void *stream);
+
+/*
+ * grad[c] += sum_r g[r * cols + c]   (the bias gradient of a Linear layer: column sums of its output
+ * gradient; fp32 sums, deterministic: fixed-order row-block partials, then the partials added in a
+ * fixed order; two launches on `stream`)
+ *   g [rows][cols] fp16 (g_is_f16 != 0) or f32, 16-byte aligned; cols % 8 == 0 and cols <= 2048
+ *   grad [cols] f32 (any float offset); work >= 256 * cols f32 scratch (calls sharing it: one stream)
+ */
+int rl_colsum_accum(const void *g, int32_t rows, int32_t cols, int32_t g_is_f16, float *grad, float *work,
                     void *stream);
 
 /*

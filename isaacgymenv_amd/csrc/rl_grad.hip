@@ -83,3 +83,106 @@ extern "C" int rl_splitk_accum(const void* parts, int32_t num_parts, int64_t n, 
     }
     return 0;
 }
+
+// ---------------------------------------------------------------- bias gradients
+// grad[c] += sum_r g[r][c] over a [rows][cols] fp16 / f32 matrix (the bias gradient of a Linear layer
+// is the column sum of its output gradient).  Deterministic, two launches:
+//   k_colsum_part: workgroup b sums rows [b*R, (b+1)*R) (lane = 8 consecutive columns of one row,
+//                  256 / (cols/8) rows side by side, folded in a fixed order) -> work[b][cols];
+//   k_colsum_fin : workgroup = 8 columns; 32 lane groups each add every 32nd partial in order, then
+//                  the 32 group sums are added in order into grad.
+namespace {
+
+constexpr int kColVec = 8;
+constexpr int kMaxParts = 256;
+constexpr int kFinGroups = kBlock / kColVec;  // 32
+
+template <bool HALF>
+__global__ __launch_bounds__(kBlock) void k_colsum_part(const void* __restrict__ g, int rows, int cols,
+                                                        float* __restrict__ work) {
+    __shared__ float red[kBlock * kColVec];
+    const int cv = cols / kColVec;
+    const int row_lanes = kBlock / cv;
+    const int t = threadIdx.x;
+    const int lane_row = t / cv, lane_col = t - lane_row * cv;
+    const int per = (rows + gridDim.x - 1) / gridDim.x;
+    const int r0 = blockIdx.x * per, r1 = min(rows, r0 + per);
+    float acc[kColVec];
+#pragma unroll
+    for (int k = 0; k < kColVec; ++k) acc[k] = 0.f;
+    if (lane_row < row_lanes) {
+        for (int r = r0 + lane_row; r < r1; r += row_lanes) {
+            if constexpr (HALF) {
+                const uint4 raw = *reinterpret_cast<const uint4*>(static_cast<const __half*>(g) + (size_t)r * cols +
+                                                                  lane_col * kColVec);
+                const __half2* h = reinterpret_cast<const __half2*>(&raw);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float2 f = __half22float2(h[k]);
+                    acc[2 * k] += f.x;
+                    acc[2 * k + 1] += f.y;
+                }
+            } else {
+                const float4* p = reinterpret_cast<const float4*>(static_cast<const float*>(g) + (size_t)r * cols +
+                                                                  lane_col * kColVec);
+                const float4 a = p[0], b = p[1];
+                acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+                acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kColVec; ++k) red[t * kColVec + k] = acc[k];
+    __syncthreads();
+    for (int c = t; c < cols; c += kBlock) {
+        const int v = c / kColVec, k = c - v * kColVec;
+        float s = 0.f;
+        for (int lr = 0; lr < row_lanes; ++lr) s += red[(lr * cv + v) * kColVec + k];
+        work[(size_t)blockIdx.x * cols + c] = s;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_colsum_fin(const float* __restrict__ work, int parts, int cols,
+                                                       float* __restrict__ grad) {
+    __shared__ float red[kFinGroups][kColVec];
+    const int t = threadIdx.x;
+    const int k = t % kColVec, j = t / kColVec;
+    const int c = blockIdx.x * kColVec + k;
+    float s = 0.f;
+    if (c < cols)
+        for (int b = j; b < parts; b += kFinGroups) s += work[(size_t)b * cols + c];
+    red[j][k] = s;
+    __syncthreads();
+    if (t < kColVec && c < cols) {
+        float a = 0.f;
+        for (int q = 0; q < kFinGroups; ++q) a += red[q][t];
+        grad[c] += a;
+    }
+}
+
+}  // namespace
+
+extern "C" int rl_colsum_accum(const void* g, int32_t rows, int32_t cols, int32_t g_is_f16, float* grad, float* work,
+                               void* stream) {
+    if (rows <= 0 || cols <= 0) return rl_set_error("rl_colsum_accum: rows and cols must be positive");
+    if (!g || !grad || !work) return rl_set_error("rl_colsum_accum: null pointer");
+    if (cols % kColVec != 0 || cols / kColVec > kBlock || ((uintptr_t)g % 16) != 0)
+        return rl_set_error("rl_colsum_accum: cols must be a multiple of 8 and <= 2048, g 16-byte aligned");
+    // ~64 rows per partial: enough workgroups to cover the CUs, few enough partials for the finish
+    int parts = (rows + 63) / 64;
+    parts = parts < 1 ? 1 : (parts > kMaxParts ? kMaxParts : parts);
+    hipStream_t st = (hipStream_t)stream;
+    if (g_is_f16)
+        hipLaunchKernelGGL(k_colsum_part<true>, dim3(parts), dim3(kBlock), 0, st, g, (int)rows, (int)cols, work);
+    else
+        hipLaunchKernelGGL(k_colsum_part<false>, dim3(parts), dim3(kBlock), 0, st, g, (int)rows, (int)cols, work);
+    hipLaunchKernelGGL(k_colsum_fin, dim3((cols + kColVec - 1) / kColVec), dim3(kBlock), 0, st, work, parts, (int)cols,
+                       grad);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        char msg[256];
+        snprintf(msg, sizeof(msg), "rl_colsum_accum: launch failed: %s", hipGetErrorString(e));
+        return rl_set_error(msg) + 1;
+    }
+    return 0;
+}

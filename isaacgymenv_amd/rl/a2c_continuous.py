@@ -41,7 +41,7 @@ import isaacgymenv_amd
 
 from . import gae
 from .gae import discount_values
-from .network import ActorCriticNetwork, ModelA2CContinuousLogStd
+from .network import ActorCriticNetwork, Linear, ModelA2CContinuousLogStd
 
 
 @dataclass
@@ -167,6 +167,27 @@ class A2CAgent:
         self.model.to(self.device)
         self.params = [p for p in self.model.parameters()]
         self.num_params = sum(p.numel() for p in self.params)
+        # one flat parameter buffer (every parameter a view into it) and, for the fp16 update, its fp16
+        # shadow: one cast per minibatch refreshes the fp16 weights every Linear layer reads
+        self.flat_param = torch.cat([p.detach().reshape(-1) for p in self.params]).to(self.device)
+        off = 0
+        for p in self.params:
+            p.data = self.flat_param[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        self.flat_param_half = None
+        if cfg.mixed_precision and self.device.type == "cuda":
+            self.flat_param_half = torch.empty(self.num_params, dtype=torch.float16, device=self.device)
+            offs, off = {}, 0
+            for p in self.params:
+                offs[id(p)] = off
+                off += p.numel()
+            for m in self.model.modules():
+                if isinstance(m, Linear):
+                    o = offs[id(m.weight)]
+                    m.half_weight = self.flat_param_half[o:o + m.weight.numel()].view_as(m.weight)
+                    if m.bias is not None:
+                        o = offs[id(m.bias)]
+                        m.half_bias = self.flat_param_half[o:o + m.bias.numel()].view_as(m.bias)
         # one flat gradient buffer; .grad of every parameter is a view into it
         self.flat_grad = torch.zeros(self.num_params, dtype=torch.float32, device=self.device)
         off = 0
@@ -370,6 +391,8 @@ class A2CAgent:
         cfg = self.cfg
         e = cfg.e_clip
         mb = self._minibatch(i)
+        if self.mixed_precision and self.flat_param_half is not None:
+            self.flat_param_half.copy_(self.flat_param)  # the fp16 weights of this minibatch, one cast
         with torch.autocast("cuda", dtype=torch.float16, enabled=self.mixed_precision, cache_enabled=False):
             res = self.model({"is_train": True, "prev_actions": mb["actions"], "obs": mb["obs"]})
             action_log_probs, values, entropy = res["prev_neglogp"], res["values"], res["entropy"]

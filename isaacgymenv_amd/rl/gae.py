@@ -14,7 +14,7 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libgymrl.so")
-EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accum", "rl_rollout_post"]
+EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accum", "rl_colsum_accum", "rl_rollout_post"]
 _lib = None
 
 
@@ -30,6 +30,8 @@ def lib():
         L.rl_gae.argtypes = [vp, vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_double, C.c_double, vp, vp, vp, vp]
         L.rl_splitk_accum.restype = C.c_int
         L.rl_splitk_accum.argtypes = [vp, C.c_int32, C.c_int64, C.c_int32, vp, vp]
+        L.rl_colsum_accum.restype = C.c_int
+        L.rl_colsum_accum.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, vp, vp]
         L.rl_rollout_post.restype = C.c_int
         L.rl_rollout_post.argtypes = [vp, vp, C.c_int32, vp, C.c_int32, vp, C.c_double, C.c_double, C.c_double,
                                       C.c_int32, vp, vp, vp, vp, vp, vp, C.c_int32, vp]
@@ -95,6 +97,29 @@ def splitk_accum(parts: torch.Tensor, grad: torch.Tensor) -> None:
                                grad.data_ptr(), stream)
     if rc != 0:
         raise RuntimeError(f"rl_splitk_accum failed: {lib().rl_last_error().decode()}")
+
+
+_COLSUM_WORK = {}  # device -> f32 scratch [256 * 2048], allocated before any graph capture
+
+
+def colsum_supported(g: torch.Tensor) -> bool:
+    return (g.is_cuda and g.dim() == 2 and g.is_contiguous() and g.dtype in (torch.float16, torch.float32)
+            and g.shape[1] % 8 == 0 and g.shape[1] <= 2048 and g.data_ptr() % 16 == 0 and g.shape[0] > 0)
+
+
+def colsum_accum(g: torch.Tensor, grad: torch.Tensor) -> None:
+    """grad += g.sum(0) in fp32, deterministic (include/gymrl.h rl_colsum_accum); g [rows, cols] with
+    colsum_supported(g), grad f32 [cols] contiguous on the same device."""
+    assert colsum_supported(g) and grad.is_cuda and grad.device == g.device and grad.is_contiguous()
+    assert grad.dtype == torch.float32 and grad.numel() == g.shape[1]
+    ws = _COLSUM_WORK.get(g.device)
+    if ws is None:
+        ws = _COLSUM_WORK[g.device] = torch.empty(256 * 2048, dtype=torch.float32, device=g.device)
+    stream = torch.cuda.current_stream(g.device).cuda_stream
+    rc = lib().rl_colsum_accum(g.data_ptr(), g.shape[0], g.shape[1], int(g.dtype == torch.float16), grad.data_ptr(),
+                               ws.data_ptr(), stream)
+    if rc != 0:
+        raise RuntimeError(f"rl_colsum_accum failed: {lib().rl_last_error().decode()}")
 
 
 _FLAG_BYTES = {torch.bool: 1, torch.uint8: 1, torch.int64: 8}

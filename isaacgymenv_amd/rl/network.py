@@ -35,13 +35,18 @@ class _SplitKLinearFn(torch.autograd.Function):
 
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda")
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, w_half=None, b_half=None):
         dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
-        xc, wc = x.to(dt), w.to(dt)
+        # w_half / b_half: the learner's fp16 copies of the parameters, refreshed once per minibatch by
+        # one cast of its flat parameter buffer (A2CAgent._refresh_half_params) instead of a cast per tensor
+        use_half = w_half is not None and dt == torch.float16
+        xc = x.to(dt)
+        wc = w_half if use_half else w.to(dt)
+        bc = None if b is None else (b_half if use_half and b_half is not None else b.to(dt))
         ctx.save_for_backward(xc, wc)
-        ctx.w = w
+        ctx.w, ctx.b = w, b
         ctx.has_bias = b is not None
-        return torch.nn.functional.linear(xc, wc, b.to(dt) if b is not None else None)
+        return torch.nn.functional.linear(xc, wc, bc)
 
     @staticmethod
     @torch.amp.custom_bwd(device_type="cuda")
@@ -57,19 +62,30 @@ class _SplitKLinearFn(torch.autograd.Function):
             if w.grad is None:
                 w.grad = torch.zeros_like(w, dtype=torch.float32)
             gae.splitk_accum(parts, w.grad)
-        gb = g.sum(0, dtype=torch.float32) if ctx.has_bias and ctx.needs_input_grad[2] else None
-        # the weight gradient is already in weight.grad (accumulated like autograd would)
-        return gx, None, gb
+        gb = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            b = ctx.b
+            if gae.colsum_supported(g):
+                if b.grad is None:
+                    b.grad = torch.zeros_like(b, dtype=torch.float32)
+                gae.colsum_accum(g, b.grad)
+            else:  # the narrow heads (value: 1 column, mu: 12)
+                gb = g.sum(0, dtype=torch.float32)
+        # the weight (and wide bias) gradients are already in .grad (accumulated like autograd would)
+        return gx, None, gb, None, None
 
 
 class Linear(nn.Linear):
     """nn.Linear (same parameters and state_dict) whose backward splits the weight-gradient reduction
     over the batch (SPLIT_K) for the learner's large minibatches."""
 
+    half_weight = None  # fp16 views set by the learner (A2CAgent), else None
+    half_bias = None
+
     def forward(self, x):
         if (torch.is_grad_enabled() and x.dim() == 2 and x.shape[0] >= SPLIT_K_MIN_ROWS
                 and x.shape[0] % SPLIT_K == 0 and x.is_cuda and self.weight.dtype == torch.float32):
-            return _SplitKLinearFn.apply(x, self.weight, self.bias)
+            return _SplitKLinearFn.apply(x, self.weight, self.bias, self.half_weight, self.half_bias)
         return super().forward(x)
 
 
