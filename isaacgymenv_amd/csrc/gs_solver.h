@@ -61,9 +61,16 @@ struct LaneCfg {
 #define GS_GLOBAL_LANES 0
 #endif
   static constexpr bool GLOBAL = (FIT == 8) && !TERR && (GS_GLOBAL_LANES > 0);
+  // GS_LANE_CAP: at most this many env lanes per workgroup for the others, so 4096 envs make >= 256
+  // workgroups (one per CU) instead of 64-128: Ant simulate 0.136 -> 0.119 ms at 16 (32 = LDS fit),
+  // 0.134 at 8, 0.163 at 4 (r02z A/B, profiles/r02z_experiment_lane_cap.txt)
+#ifndef GS_LANE_CAP
+#define GS_LANE_CAP 16
+#endif
   static constexpr int LB = GLOBAL ? GS_GLOBAL_LANES
                           : FIT == 8 ? (GS_NARROW_LANES < NARROW ? GS_NARROW_LANES : NARROW)
-                                     : (TERR && FIT > GS_TERR_LANES) ? GS_TERR_LANES : FIT;
+                                     : (TERR && FIT > GS_TERR_LANES) ? GS_TERR_LANES
+                                                                     : (FIT < GS_LANE_CAP ? FIT : GS_LANE_CAP);
   static_assert(GLOBAL || SLOTS * LB * 4 <= 160 * 1024, "contact rows exceed the LDS of a CU even at 8 lanes");
   // floats of SimBuffers::rows per env (0: the rows live in LDS)
   static constexpr int ROW_FLOATS = GLOBAL ? SLOTS : 0;
