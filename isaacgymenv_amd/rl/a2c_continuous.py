@@ -199,17 +199,10 @@ class A2CAgent:
         on_gpu = self.device.type == "cuda"
         self.lr = torch.tensor(cfg.learning_rate, dtype=torch.float64, device=self.device)
         if on_gpu:
-            # Adam, the grad-norm clip and the scaler's unscale run on the flat parameter / gradient
-            # buffers as ONE tensor (Adam is elementwise: the same update as per tensor; one fused launch
-            # instead of a multi-tensor launch over every parameter).  Checkpoints keep the per-parameter
-            # optimizer state layout (get_full_state_weights / restore).
-            self.opt_param = nn.Parameter(self.flat_param, requires_grad=False)
-            self.opt_param.grad = self.flat_grad
             self._opt_lr = torch.tensor(cfg.learning_rate, dtype=torch.float32, device=self.device)
-            self.optimizer = torch.optim.Adam([self.opt_param], lr=self._opt_lr, eps=1e-08,
+            self.optimizer = torch.optim.Adam(self.params, lr=self._opt_lr, eps=1e-08,
                                               weight_decay=cfg.weight_decay, fused=True, capturable=True)
         else:
-            self.opt_param = None
             self._opt_lr = None
             self.optimizer = torch.optim.Adam(self.params, lr=cfg.learning_rate, eps=1e-08,
                                               weight_decay=cfg.weight_decay)
@@ -427,8 +420,7 @@ class A2CAgent:
         new policy against the dataset's old mu/sigma."""
         if self.cfg.truncate_grads:
             self.scaler.unscale_(self.optimizer)
-            nn.utils.clip_grad_norm_([self.opt_param] if self.opt_param is not None else self.params,
-                                     self.cfg.grad_norm)
+            nn.utils.clip_grad_norm_(self.params, self.cfg.grad_norm)
         self.scaler.step(self.optimizer)
         self.scaler.update()
         mb = self._minibatch(i)
@@ -587,45 +579,9 @@ class A2CAgent:
         return stats
 
     # ------------------------------------------------------------------ checkpoints
-    def _optimizer_state_per_param(self):
-        """The optimizer state_dict in the per-parameter layout (torch.optim.Adam over model.parameters(),
-        as rl_games saves it), also when the learner steps Adam on the flat buffer."""
-        sd = self.optimizer.state_dict()
-        if self.opt_param is None:
-            return sd
-        st = sd["state"].get(0)
-        state, off = {}, 0
-        for i, p in enumerate(self.params):
-            n = p.numel()
-            if st is not None:
-                state[i] = {k: (v[off:off + n].view_as(p).clone() if torch.is_tensor(v) and v.numel() == self.num_params
-                                else (v.clone() if torch.is_tensor(v) else v)) for k, v in st.items()}
-            off += n
-        groups = [dict(sd["param_groups"][0], params=list(range(len(self.params))))]
-        return {"state": state, "param_groups": groups}
-
-    def _load_optimizer_state(self, sd):
-        if self.opt_param is None:
-            self.optimizer.load_state_dict(sd)
-            return
-        st = sd["state"]
-        if len(sd["param_groups"][0]["params"]) == 1:  # already flat
-            self.optimizer.load_state_dict(sd)
-            return
-        flat = {}
-        if st:
-            first = st[sd["param_groups"][0]["params"][0]]
-            for k, v in first.items():
-                if torch.is_tensor(v) and k != "step":  # per-element moments; "step" is one counter
-                    flat[k] = torch.cat([st[i][k].reshape(-1).to(self.device) for i in sd["param_groups"][0]["params"]])
-                else:
-                    flat[k] = v
-        self.optimizer.load_state_dict({"state": {0: flat} if flat else {},
-                                        "param_groups": [dict(sd["param_groups"][0], params=[0])]})
-
     def get_full_state_weights(self):
         return {"model": self.model.state_dict(), "epoch": self.epoch_num, "frame": self.frame,
-                "optimizer": self._optimizer_state_per_param(), "last_lr": float(self.lr)}
+                "optimizer": self.optimizer.state_dict(), "last_lr": float(self.lr)}
 
     def save(self, path: str):
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
@@ -637,7 +593,7 @@ class A2CAgent:
         self.epoch_num = int(ckpt.get("epoch", 0))
         self.frame = int(ckpt.get("frame", 0))
         if "optimizer" in ckpt:
-            self._load_optimizer_state(ckpt["optimizer"])
+            self.optimizer.load_state_dict(ckpt["optimizer"])
         lr = float(ckpt.get("last_lr", self.cfg.learning_rate))
         self.lr.fill_(lr)
         if self._opt_lr is not None:
