@@ -14,6 +14,7 @@
  *            A2CBuilder, as a batched GEMM over row blocks): sums the partials in
  *            a fixed order and adds them into the parameter's fp32 gradient.
  *   rl_colsum_accum : the same layers' bias gradients (column sums), deterministic.
+ *   rl_ppo_loss / rl_ppo_loss_backward : the minibatch PPO loss and its gradient.
  *   rl_rollout_post : the rollout bookkeeping after each env step (play_steps).
  *
  * All pointers are device pointers; calls are ordered on `stream` (a hipStream_t,
@@ -69,6 +70,30 @@ int rl_splitk_accum(const void *parts, int32_t num_parts, int64_t n, int32_t par
  */
 int rl_colsum_accum(const void *g, int32_t rows, int32_t cols, int32_t g_is_f16, float *grad, float *work,
                     void *stream);
+
+/*
+ * The PPO minibatch loss and its gradient (rl_games a2c_continuous calc_gradients for the
+ * continuous_a2c_logstd model with fixed sigma): actor (clipped surrogate), critic (clipped value
+ * loss if clip_value), entropy and bound losses of `rows` samples with `num_actions` <= 32 actions.
+ *   mu [rows][A], values [rows] (fp16 if *_is_f16 else f32), logstd [A] f32 (the sigma parameter),
+ *   actions [rows][A], old_neglogp, advantages, old_values, returns [rows] f32
+ * Writes loss (0-d: a + 0.5 c critic_coef - entropy entropy_coef + b bounds_loss_coef of the means),
+ * stats[4] = the means (a, c, entropy, b), and the UNSCALED gradients of loss: dmu [rows][A],
+ * dvalues [rows], dlogstd [A] (f32); partials >= ceil(rows / 256) * 36 f32 scratch.  Two launches.
+ */
+int rl_ppo_loss(const void *mu, int32_t mu_is_f16, const void *values, int32_t values_is_f16, const float *logstd,
+                const float *actions, const float *old_neglogp, const float *advantages, const float *old_values,
+                const float *returns, int32_t rows, int32_t num_actions, double e_clip, int32_t clip_value,
+                double critic_coef, double entropy_coef, double bounds_loss_coef, float *dmu, float *dvalues,
+                float *partials, float *loss, float *stats, float *dlogstd, void *stream);
+
+/*
+ * Backward of rl_ppo_loss: d(upstream) = grad_loss[0] (device f32, e.g. the GradScaler scale) times the
+ * stored gradients, cast to the dtypes of mu / values: dmu_out [rows][A], dvalues_out [rows], dlogstd_out [A].
+ */
+int rl_ppo_loss_backward(const float *grad_loss, const float *dmu, const float *dvalues, const float *dlogstd,
+                         int32_t rows, int32_t num_actions, void *dmu_out, int32_t dmu_is_f16, void *dvalues_out,
+                         int32_t dvalues_is_f16, float *dlogstd_out, void *stream);
 
 /*
  * Rollout bookkeeping after one VecTask.step (rl_games a2c_common.py play_steps, the statements after

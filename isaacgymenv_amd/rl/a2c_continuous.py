@@ -252,6 +252,10 @@ class A2CAgent:
         self._has_timeouts = False
         # after env.step on the GPU: one fused kernel instead of the static copies + post graph
         self._fused_post = on_gpu
+        # minibatch loss + gradient as one HIP pass for the fixed-sigma, separate actor / critic model
+        # (AnymalTerrainPPO.yaml); other network shapes keep the torch statement of the loss
+        net = self.model.a2c_network
+        self._fused_loss = on_gpu and net.fixed_sigma and net.separate and self.actions_num <= 32
 
     # ------------------------------------------------------------------ multi-GPU
     def _broadcast_params(self):
@@ -393,6 +397,8 @@ class A2CAgent:
         mb = self._minibatch(i)
         if self.mixed_precision and self.flat_param_half is not None:
             self.flat_param_half.copy_(self.flat_param)  # the fp16 weights of this minibatch, one cast
+        if self._fused_loss:
+            return self._mb_forward_backward_fused(mb)
         with torch.autocast("cuda", dtype=torch.float16, enabled=self.mixed_precision, cache_enabled=False):
             res = self.model({"is_train": True, "prev_actions": mb["actions"], "obs": mb["obs"]})
             action_log_probs, values, entropy = res["prev_neglogp"], res["values"], res["entropy"]
@@ -414,6 +420,26 @@ class A2CAgent:
         self.flat_grad.zero_()
         self.scaler.scale(loss).backward()
         return (a_loss.detach(), c_loss.detach(), entropy.detach(), b_loss.detach(), mu.detach(), sigma.detach())
+
+    def _mb_forward_backward_fused(self, mb):
+        """_mb_forward_backward with the loss and its gradient as one HIP pass (gae.PpoLossFn,
+        rl_ppo_loss): the network forward / backward stay torch + hipBLASLt; the ~80 launches of the
+        loss statements and their autograd become three.  Same terms, same autograd rules."""
+        cfg = self.cfg
+        net = self.model.a2c_network
+        obs = self.model.norm_obs(mb["obs"])
+        with torch.autocast("cuda", dtype=torch.float16, enabled=self.mixed_precision, cache_enabled=False):
+            a_out = net.actor_mlp(obs)
+            c_out = net.critic_mlp(obs)
+            values = net.value(c_out)
+            mu = net.mu(a_out)
+        loss, stats = gae.PpoLossFn.apply(mu, values, net.sigma, mb["actions"], mb["old_logp_actions"],
+                                          mb["advantages"], mb["old_values"], mb["returns"], cfg.e_clip,
+                                          cfg.clip_value, cfg.critic_coef, self.entropy_coef, cfg.bounds_loss_coef)
+        self.flat_grad.zero_()
+        self.scaler.scale(loss).backward()
+        sigma = torch.exp(net.sigma.detach()).expand(mu.shape[0], -1)
+        return (stats[0], stats[1], stats[2], stats[3], mu.detach(), sigma)
 
     def _mb_step(self, i, out):
         """Phase 2 (after the gradient all-reduce): unscale, clip, Adam, scaler update; KL of the

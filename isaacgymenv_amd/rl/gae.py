@@ -14,7 +14,8 @@ import os
 import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libgymrl.so")
-EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accum", "rl_colsum_accum", "rl_rollout_post"]
+EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accum", "rl_colsum_accum", "rl_rollout_post",
+                    "rl_ppo_loss", "rl_ppo_loss_backward"]
 _lib = None
 
 
@@ -32,6 +33,13 @@ def lib():
         L.rl_splitk_accum.argtypes = [vp, C.c_int32, C.c_int64, C.c_int32, vp, vp]
         L.rl_colsum_accum.restype = C.c_int
         L.rl_colsum_accum.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, vp, vp]
+        L.rl_ppo_loss.restype = C.c_int
+        L.rl_ppo_loss.argtypes = [vp, C.c_int32, vp, C.c_int32, vp, vp, vp, vp, vp, vp, C.c_int32, C.c_int32,
+                                  C.c_double, C.c_int32, C.c_double, C.c_double, C.c_double, vp, vp, vp, vp, vp, vp,
+                                  vp]
+        L.rl_ppo_loss_backward.restype = C.c_int
+        L.rl_ppo_loss_backward.argtypes = [vp, vp, vp, vp, C.c_int32, C.c_int32, vp, C.c_int32, vp, C.c_int32, vp,
+                                           vp]
         L.rl_rollout_post.restype = C.c_int
         L.rl_rollout_post.argtypes = [vp, vp, C.c_int32, vp, C.c_int32, vp, C.c_double, C.c_double, C.c_double,
                                       C.c_int32, vp, vp, vp, vp, vp, vp, C.c_int32, vp]
@@ -158,3 +166,60 @@ def rollout_post(rewards, dones, time_outs, values, reward_shift: float, reward_
                                meter_rewards.data_ptr(), meter_lengths.data_ptr(), int(games_to_track), stream)
     if rc != 0:
         raise RuntimeError(f"rl_rollout_post failed: {lib().rl_last_error().decode()}")
+
+
+class PpoLossFn(torch.autograd.Function):
+    """The PPO minibatch loss (rl_ppo_loss): forward computes the loss, its four terms' means and the
+    unscaled gradients in one pass; backward scales them by the upstream gradient (rl_ppo_loss_backward).
+    Inputs: mu [B, A] and values [B, 1] (fp16 under autocast, or f32), logstd [A] (the sigma parameter),
+    actions [B, A], old_neglogp [B], advantages [B], old_values [B, 1], returns [B, 1] (f32).
+    Returns (loss 0-d, stats [4] = means of actor, critic, entropy, bound loss; not differentiable)."""
+
+    @staticmethod
+    def forward(ctx, mu, values, logstd, actions, old_neglogp, advantages, old_values, returns, e_clip: float,
+                clip_value: bool, critic_coef: float, entropy_coef: float, bounds_loss_coef: float):
+        B, A = mu.shape
+        dev = mu.device
+        for t in (mu, values, logstd, actions, old_neglogp, advantages, old_values, returns):
+            assert t.is_cuda and t.device == dev and t.is_contiguous()
+        assert mu.dtype in (torch.float16, torch.float32) and values.dtype in (torch.float16, torch.float32)
+        assert values.numel() == B and old_values.numel() == B and returns.numel() == B and logstd.numel() == A
+        assert old_neglogp.numel() == B and advantages.numel() == B and actions.shape == (B, A)
+        f32 = torch.float32
+        dmu = torch.empty(B, A, dtype=f32, device=dev)
+        dv = torch.empty(B, dtype=f32, device=dev)
+        part = torch.empty(((B + 255) // 256) * 36, dtype=f32, device=dev)
+        loss = torch.empty((), dtype=f32, device=dev)
+        stats = torch.empty(4, dtype=f32, device=dev)
+        dls = torch.empty(A, dtype=f32, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        rc = lib().rl_ppo_loss(mu.data_ptr(), int(mu.dtype == torch.float16), values.data_ptr(),
+                               int(values.dtype == torch.float16), logstd.data_ptr(), actions.data_ptr(),
+                               old_neglogp.data_ptr(), advantages.data_ptr(), old_values.data_ptr(), returns.data_ptr(),
+                               B, A, float(e_clip), int(bool(clip_value)), float(critic_coef), float(entropy_coef),
+                               float(bounds_loss_coef), dmu.data_ptr(), dv.data_ptr(), part.data_ptr(), loss.data_ptr(),
+                               stats.data_ptr(), dls.data_ptr(), stream)
+        if rc != 0:
+            raise RuntimeError(f"rl_ppo_loss failed: {lib().rl_last_error().decode()}")
+        ctx.save_for_backward(dmu, dv, dls)
+        ctx.meta = (mu.dtype, values.dtype, tuple(values.shape))
+        ctx.mark_non_differentiable(stats)
+        return loss, stats
+
+    @staticmethod
+    def backward(ctx, g_loss, g_stats):
+        dmu, dv, dls = ctx.saved_tensors
+        mu_dt, v_dt, v_shape = ctx.meta
+        B, A = dmu.shape
+        dev = dmu.device
+        g = (g_loss if g_loss is not None else torch.ones((), device=dev)).float().contiguous()
+        dmu_out = torch.empty(B, A, dtype=mu_dt, device=dev)
+        dv_out = torch.empty(v_shape, dtype=v_dt, device=dev)
+        dls_out = torch.empty(A, dtype=torch.float32, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        rc = lib().rl_ppo_loss_backward(g.data_ptr(), dmu.data_ptr(), dv.data_ptr(), dls.data_ptr(), B, A,
+                                        dmu_out.data_ptr(), int(mu_dt == torch.float16), dv_out.data_ptr(),
+                                        int(v_dt == torch.float16), dls_out.data_ptr(), stream)
+        if rc != 0:
+            raise RuntimeError(f"rl_ppo_loss_backward failed: {lib().rl_last_error().decode()}")
+        return (dmu_out, dv_out, dls_out) + (None,) * 10

@@ -240,3 +240,27 @@ def test_checkpoint_round_trip(tmp_path):
         for k in ("exp_avg", "exp_avg_sq", "step"):
             assert torch.equal(sa[i][k], sb[i][k]), (i, k)
     assert torch.equal(a.flat_param, b.flat_param)
+
+
+def test_fused_ppo_loss_matches_torch_loss():
+    """The minibatch loss + gradient as one HIP pass (rl_ppo_loss) against the torch statement of the
+    same loss on the same minibatch, fp16 autocast as AnymalTerrainPPO.yaml: loss terms to 1e-4, the flat
+    gradient (all parameters) within 1e-2 of its scale (fp16 rounding of the two backward orders)."""
+    agent = _agent("AnymalTerrain", 1024, minibatch_size=8192, bounds_loss_coef=0.01)
+    assert agent._fused_loss and agent.mixed_precision
+    agent.use_graphs = False
+    agent.train_epoch()
+    agent.model.train()
+    agent.model.running_mean_std.eval()
+    agent.scaler = torch.amp.GradScaler("cuda", init_scale=1024.0)
+    res = {}
+    for fused in (False, True):
+        agent._fused_loss = fused
+        out = agent._mb_forward_backward(1)
+        torch.cuda.synchronize()
+        res[fused] = ([float(x) for x in out[:4]], agent.flat_grad.clone(), out[4].float(), out[5].float())
+    (l0, g0, m0, s0), (l1, g1, m1, s1) = res[False], res[True]
+    np.testing.assert_allclose(l1, l0, rtol=1e-4, atol=1e-6)
+    assert torch.equal(m0, m1) and torch.allclose(s0, s1)
+    scale = float(g0.abs().max())
+    assert scale > 0 and float((g1 - g0).abs().max()) <= 1e-2 * scale, (float((g1 - g0).abs().max()), scale)
