@@ -252,10 +252,10 @@ class A2CAgent:
         self._has_timeouts = False
         # after env.step on the GPU: one fused kernel instead of the static copies + post graph
         self._fused_post = on_gpu
-        # minibatch loss + gradient as one HIP pass for the fixed-sigma, separate actor / critic model
-        # (AnymalTerrainPPO.yaml); other network shapes keep the torch statement of the loss
+        # minibatch loss + gradient as one HIP pass for the fixed-sigma models (every in-scope train
+        # config); a learned-sigma head keeps the torch statement of the loss
         net = self.model.a2c_network
-        self._fused_loss = on_gpu and net.fixed_sigma and net.separate and self.actions_num <= 32
+        self._fused_loss = on_gpu and net.fixed_sigma and self.actions_num <= 32
 
     # ------------------------------------------------------------------ multi-GPU
     def _broadcast_params(self):
@@ -430,7 +430,7 @@ class A2CAgent:
         obs = self.model.norm_obs(mb["obs"])
         with torch.autocast("cuda", dtype=torch.float16, enabled=self.mixed_precision, cache_enabled=False):
             a_out = net.actor_mlp(obs)
-            c_out = net.critic_mlp(obs)
+            c_out = net.critic_mlp(obs) if net.separate else a_out
             values = net.value(c_out)
             mu = net.mu(a_out)
         loss, stats = gae.PpoLossFn.apply(mu, values, net.sigma, mb["actions"], mb["old_logp_actions"],

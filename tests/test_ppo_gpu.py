@@ -54,6 +54,7 @@ def _agent(task, num_envs, **over):
 
 
 def test_cartpole_ppo_learns():
+    # (through the fused loss kernel, f32: CartpolePPO.yaml has no mixed precision, shared trunk)
     # rl_games solves Cartpole (episode 500 steps) in ~100 epochs; this learner reaches ~490 mean
     # episode length by epoch 60 (tools/probes/ppo_probe.py); random play lasts ~3 steps
     agent = _agent("Cartpole", 512)
