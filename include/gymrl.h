@@ -15,6 +15,7 @@
  *            a fixed order and adds them into the parameter's fp32 gradient.
  *   rl_colsum_accum : the same layers' bias gradients (column sums), deterministic.
  *   rl_ppo_loss / rl_ppo_loss_backward : the minibatch PPO loss and its gradient.
+ *   rl_rms_normalize : the model's running mean / std input normalisation.
  *   rl_rollout_post : the rollout bookkeeping after each env step (play_steps).
  *
  * All pointers are device pointers; calls are ordered on `stream` (a hipStream_t,
@@ -79,7 +80,7 @@ int rl_colsum_accum(const void *g, int32_t rows, int32_t cols, int32_t g_is_f16,
  *   actions [rows][A], old_neglogp, advantages, old_values, returns [rows] f32
  * Writes loss (0-d: a + 0.5 c critic_coef - entropy entropy_coef + b bounds_loss_coef of the means),
  * stats[4] = the means (a, c, entropy, b), and the UNSCALED gradients of loss: dmu [rows][A],
- * dvalues [rows], dlogstd [A] (f32); partials >= ceil(rows / 256) * 36 f32 scratch.  Two launches.
+ * dvalues [rows], dlogstd [A] (f32); partials >= ceil(rows / 128) * 36 f32 scratch.  Two launches.
  */
 int rl_ppo_loss(const void *mu, int32_t mu_is_f16, const void *values, int32_t values_is_f16, const float *logstd,
                 const float *actions, const float *old_neglogp, const float *advantages, const float *old_values,
@@ -94,6 +95,16 @@ int rl_ppo_loss(const void *mu, int32_t mu_is_f16, const void *values, int32_t v
 int rl_ppo_loss_backward(const float *grad_loss, const float *dmu, const float *dvalues, const float *dlogstd,
                          int32_t rows, int32_t num_actions, void *dmu_out, int32_t dmu_is_f16, void *dvalues_out,
                          int32_t dvalues_is_f16, float *dlogstd_out, void *stream);
+
+/*
+ * RunningMeanStd of the model input (rl_games algos_torch/running_mean_std.py): with update != 0 the
+ * batch mean / unbiased var of x [rows][cols] (cols <= 256) are merged into the float64 running moments
+ * running_mean / running_var [cols] and count (0-d) as the reference does in train mode; then
+ * y = clamp((x - float(mean)) / sqrt(float(var) + epsilon), -5, 5).  partials >= ceil(rows / 128) * cols * 2
+ * f32 scratch (update only).  Three launches (update) or one.
+ */
+int rl_rms_normalize(const float *x, int32_t rows, int32_t cols, double *running_mean, double *running_var,
+                     double *count, double epsilon, int32_t update, float *partials, float *y, void *stream);
 
 /*
  * Rollout bookkeeping after one VecTask.step (rl_games a2c_common.py play_steps, the statements after

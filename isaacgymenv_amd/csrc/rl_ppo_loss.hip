@@ -28,7 +28,7 @@ int rl_set_error(const char* msg);  // rl_gae.hip
 
 namespace {
 
-constexpr int kRows = 256;
+constexpr int kRows = 128;  // 128 workgroups for a 16384-row minibatch
 constexpr int kMaxA = 32;
 constexpr int kNT = 4 + kMaxA;  // partial slots per block: a, c, entropy, b, dlogstd[A]
 
@@ -134,8 +134,16 @@ __global__ __launch_bounds__(64) void k_ppo_finish(const float* __restrict__ par
     __shared__ float m[4];
     const int t = threadIdx.x;
     if (t < 4 + A) {
-        float s = 0.f;
-        for (int b = 0; b < blocks; ++b) s += part[(size_t)b * kNT + t];
+        // 8 independent partial chains (b mod 8, combined pairwise): the loads issue together instead of
+        // one L2 round trip per block; a fixed order, so the sums stay run-to-run identical
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        int b = 0;
+        for (; b + 8 <= blocks; b += 8) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += part[(size_t)(b + k) * kNT + t];
+        }
+        for (; b < blocks; ++b) acc[0] += part[(size_t)b * kNT + t];
+        const float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
         if (t < 4) {
             m[t] = s * invB;
             stats[t] = m[t];

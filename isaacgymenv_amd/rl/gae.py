@@ -15,7 +15,7 @@ import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libgymrl.so")
 EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accum", "rl_colsum_accum", "rl_rollout_post",
-                    "rl_ppo_loss", "rl_ppo_loss_backward"]
+                    "rl_ppo_loss", "rl_ppo_loss_backward", "rl_rms_normalize"]
 _lib = None
 
 
@@ -40,6 +40,8 @@ def lib():
         L.rl_ppo_loss_backward.restype = C.c_int
         L.rl_ppo_loss_backward.argtypes = [vp, vp, vp, vp, C.c_int32, C.c_int32, vp, C.c_int32, vp, C.c_int32, vp,
                                            vp]
+        L.rl_rms_normalize.restype = C.c_int
+        L.rl_rms_normalize.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp, C.c_double, C.c_int32, vp, vp, vp]
         L.rl_rollout_post.restype = C.c_int
         L.rl_rollout_post.argtypes = [vp, vp, C.c_int32, vp, C.c_int32, vp, C.c_double, C.c_double, C.c_double,
                                       C.c_int32, vp, vp, vp, vp, vp, vp, C.c_int32, vp]
@@ -188,7 +190,7 @@ class PpoLossFn(torch.autograd.Function):
         f32 = torch.float32
         dmu = torch.empty(B, A, dtype=f32, device=dev)
         dv = torch.empty(B, dtype=f32, device=dev)
-        part = torch.empty(((B + 255) // 256) * 36, dtype=f32, device=dev)
+        part = torch.empty(((B + 127) // 128) * 36, dtype=f32, device=dev)
         loss = torch.empty((), dtype=f32, device=dev)
         stats = torch.empty(4, dtype=f32, device=dev)
         dls = torch.empty(A, dtype=f32, device=dev)
@@ -223,3 +225,26 @@ class PpoLossFn(torch.autograd.Function):
         if rc != 0:
             raise RuntimeError(f"rl_ppo_loss_backward failed: {lib().rl_last_error().decode()}")
         return (dmu_out, dv_out, dls_out) + (None,) * 10
+
+
+def rms_supported(x: torch.Tensor) -> bool:
+    return x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and x.is_contiguous() and 0 < x.shape[1] <= 256 \
+        and x.shape[0] > 0
+
+
+def rms_normalize(x, running_mean, running_var, count, epsilon: float, update: bool) -> torch.Tensor:
+    """RunningMeanStd forward (include/gymrl.h rl_rms_normalize): x f32 [N, C] (rms_supported), float64
+    running_mean / running_var [C] and count 0-d updated in place when ``update``; returns y f32 [N, C]."""
+    assert rms_supported(x)
+    for t in (running_mean, running_var, count):
+        assert t.dtype == torch.float64 and t.is_contiguous() and t.device == x.device
+    N, Cc = x.shape
+    y = torch.empty_like(x)
+    part = torch.empty(((N + 127) // 128) * Cc * 2, dtype=torch.float32, device=x.device) if update else None
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    rc = lib().rl_rms_normalize(x.data_ptr(), N, Cc, running_mean.data_ptr(), running_var.data_ptr(),
+                                count.data_ptr(), float(epsilon), int(bool(update)),
+                                part.data_ptr() if part is not None else None, y.data_ptr(), stream)
+    if rc != 0:
+        raise RuntimeError(f"rl_rms_normalize failed: {lib().rl_last_error().decode()}")
+    return y

@@ -9,6 +9,8 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from . import gae
+
 
 class RunningMeanStd(nn.Module):
     def __init__(self, insize, epsilon: float = 1e-05, norm_only: bool = False):
@@ -33,6 +35,10 @@ class RunningMeanStd(nn.Module):
         return new_mean, new_var, tot_count
 
     def forward(self, input, unnorm: bool = False):
+        if not unnorm and not self.norm_only and gae.rms_supported(input):
+            # device path: the moment update and the normalisation as one HIP pass (rl_rms_normalize)
+            return gae.rms_normalize(input, self.running_mean, self.running_var, self.count, self.epsilon,
+                                     update=self.training)
         if self.training:
             mean = input.mean(self.axis)
             var = input.var(self.axis)

@@ -265,3 +265,29 @@ def test_fused_ppo_loss_matches_torch_loss():
     assert torch.equal(m0, m1) and torch.allclose(s0, s1)
     scale = float(g0.abs().max())
     assert scale > 0 and float((g1 - g0).abs().max()) <= 1e-2 * scale, (float((g1 - g0).abs().max()), scale)
+
+
+@pytest.mark.parametrize("rows,cols", [(16384, 188), (4096, 188), (1000, 13), (3, 256)])
+def test_rms_normalize_kernel_matches_torch(rows, cols):
+    """rl_rms_normalize (train-mode moment update + normalisation, then the eval-mode path) against the
+    torch statement of RunningMeanStd on the same inputs: float64 running moments to 1e-6 relative (the
+    batch moments' reduction order differs), normalised output to 2e-5."""
+    from isaacgymenv_amd.rl import gae
+    from isaacgymenv_amd.rl.running_mean_std import RunningMeanStd
+    gen = torch.Generator().manual_seed(rows + cols)
+    ref = RunningMeanStd((cols,)).cuda()
+    mine = RunningMeanStd((cols,)).cuda()
+    for step in range(3):
+        x = (torch.randn(rows, cols, generator=gen) * (1 + 3 * torch.rand(cols, generator=gen))
+             + 5 * torch.randn(cols, generator=gen)).cuda()
+        ref.train()
+        # the torch statement: a non-contiguous view of x takes RunningMeanStd's torch path
+        y_ref = RunningMeanStd.forward(ref, x.t().contiguous().t())
+        y = gae.rms_normalize(x, mine.running_mean, mine.running_var, mine.count, mine.epsilon, update=True)
+        torch.testing.assert_close(mine.running_mean, ref.running_mean, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(mine.running_var, ref.running_var, rtol=1e-5, atol=1e-6)
+        assert float(mine.count) == float(ref.count)
+        torch.testing.assert_close(y, y_ref, rtol=2e-5, atol=2e-5)
+    y_eval = gae.rms_normalize(x, mine.running_mean, mine.running_var, mine.count, mine.epsilon, update=False)
+    ref.eval()
+    torch.testing.assert_close(y_eval, RunningMeanStd.forward(ref, x.t().contiguous().t()), rtol=2e-5, atol=2e-5)
