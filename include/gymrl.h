@@ -100,7 +100,7 @@ int rl_ppo_loss_backward(const float *grad_loss, const float *dmu, const float *
  * RunningMeanStd of the model input (rl_games algos_torch/running_mean_std.py): with update != 0 the
  * batch mean / unbiased var of x [rows][cols] (cols <= 256) are merged into the float64 running moments
  * running_mean / running_var [cols] and count (0-d) as the reference does in train mode; then
- * y = clamp((x - float(mean)) / sqrt(float(var) + epsilon), -5, 5).  partials >= ceil(rows / 128) * cols * 2
+ * y = clamp((x - float(mean)) / sqrt(float(var) + epsilon), -5, 5).  partials >= ceil(rows / 64) * cols * 2
  * f32 scratch (update only).  Three launches (update) or one.
  */
 int rl_rms_normalize(const float *x, int32_t rows, int32_t cols, double *running_mean, double *running_var,

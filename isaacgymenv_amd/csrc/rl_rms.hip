@@ -5,11 +5,12 @@
 // float64 running moments, then y = clamp((x - mean) / sqrt(var + eps), -5, 5) with the float32
 // casts of the running moments.  torch spends ~25 launches on it (a Welford reduction of ~40 us at
 // 16384 x 188, ~15 float64 elementwise ops on [C], the normalisation chain); here:
-//   k_rms_part: workgroup b, lane c = column c: Welford over the workgroup's rows (fp32)
-//   k_rms_fin : lane c merges the workgroups' (mean, M2) in fp64 in block order (Chan et al.), rounds the
+//   k_rms_part: workgroup b, lane c = column c: Welford over the workgroup's 64 rows (fp32, loads issued 8 ahead)
+//   k_rms_fin : 4 lanes per column merge the workgroups' (mean, M2) in fp64 (Chan et al.; lane j takes blocks
+//               j, j + 4, ... in order, then the 4 in lane order: fixed, deterministic), rounds the
 //               batch mean / var to fp32 as torch's fp32 reductions return them, then updates the running
 //               moments with the reference formula in fp64, same operation order
-//   k_rms_norm: the normalisation (also the eval-mode path, update = 0)
+//   k_rms_norm: the normalisation (also the eval-mode path, update = 0); bumps the running count
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -20,8 +21,11 @@ int rl_set_error(const char* msg);  // rl_gae.hip
 
 namespace {
 
-constexpr int kCols = 256;     // columns <= 256: one lane each
-constexpr int kRowBlock = 128; // rows per partial
+constexpr int kCols = 256;     // columns <= 256
+constexpr int kRowBlock = 64;  // rows per partial
+constexpr int kPre = 8;        // loads issued ahead of the dependent Welford / merge chain
+constexpr int kFinCols = 64;   // finish: columns per workgroup, kFinSub lanes per column
+constexpr int kFinSub = 4;
 
 __global__ __launch_bounds__(kCols) void k_rms_part(const float* __restrict__ x, int N, int C,
                                                     float* __restrict__ part) {
@@ -30,55 +34,88 @@ __global__ __launch_bounds__(kCols) void k_rms_part(const float* __restrict__ x,
     const int r0 = blockIdx.x * kRowBlock, r1 = min(N, r0 + kRowBlock);
     float mean = 0.f, m2 = 0.f;
     int n = 0;
-    for (int r = r0; r < r1; ++r) {
-        const float v = x[(size_t)r * C + c];
-        ++n;
-        const float d = v - mean;
-        mean += d / (float)n;
-        m2 += d * (v - mean);
+    for (int r = r0; r < r1; r += kPre) {
+        float v[kPre];
+#pragma unroll
+        for (int k = 0; k < kPre; ++k) v[k] = r + k < r1 ? x[(size_t)(r + k) * C + c] : 0.f;
+#pragma unroll
+        for (int k = 0; k < kPre; ++k) {
+            if (r + k < r1) {
+                ++n;
+                const float d = v[k] - mean;
+                mean += d / (float)n;
+                m2 += d * (v[k] - mean);
+            }
+        }
     }
     part[((size_t)blockIdx.x * C + c) * 2 + 0] = mean;
     part[((size_t)blockIdx.x * C + c) * 2 + 1] = m2;
 }
 
-__global__ __launch_bounds__(kCols) void k_rms_fin(const float* __restrict__ part, int blocks, int N, int C,
-                                                   double* __restrict__ rmean, double* __restrict__ rvar,
-                                                   double* __restrict__ count) {
-    const int c = threadIdx.x;
-    const double cnt = *count;  // every lane reads it before lane 0 updates it
-    __syncthreads();
+// Chan et al. merge of (na, mean, M2) with (nb, pm, pm2), float64
+__device__ __forceinline__ void merge(double& na, double& mean, double& M2, double nb, double pm, double pm2) {
+    const double tot = na + nb;
+    const double delta = pm - mean;
+    mean += delta * nb / tot;
+    M2 += pm2 + delta * delta * na * nb / tot;
+    na = tot;
+}
+
+// workgroup = kFinCols columns x kFinSub lanes; lane j merges the partials b = j, j + kFinSub, ... in order,
+// then lane 0 merges the kFinSub results in lane order (fixed: deterministic)
+__global__ __launch_bounds__(kFinCols * kFinSub) void k_rms_fin(const float* __restrict__ part, int blocks, int N,
+                                                                int C, double* __restrict__ rmean,
+                                                                double* __restrict__ rvar,
+                                                                const double* __restrict__ count) {
+    __shared__ double sh[kFinSub][kFinCols][3];
+    const int cl = threadIdx.x % kFinCols, j = threadIdx.x / kFinCols;
+    const int c = blockIdx.x * kFinCols + cl;
+    double na = 0.0, mean = 0.0, M2 = 0.0;
     if (c < C) {
-        double na = 0.0, mean = 0.0, M2 = 0.0;
-        for (int b = 0; b < blocks; ++b) {
-            const double nb = (double)(min(N, (b + 1) * kRowBlock) - b * kRowBlock);
-            const double pm = part[((size_t)b * C + c) * 2 + 0], pm2 = part[((size_t)b * C + c) * 2 + 1];
-            const double tot = na + nb;
-            const double delta = pm - mean;
-            mean += delta * nb / tot;
-            M2 += pm2 + delta * delta * na * nb / tot;
-            na = tot;
+        for (int b0 = j; b0 < blocks; b0 += kFinSub * kPre) {
+            float pm[kPre], pm2[kPre];
+#pragma unroll
+            for (int k = 0; k < kPre; ++k) {
+                const int b = b0 + k * kFinSub;
+                pm[k] = b < blocks ? part[((size_t)b * C + c) * 2 + 0] : 0.f;
+                pm2[k] = b < blocks ? part[((size_t)b * C + c) * 2 + 1] : 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < kPre; ++k) {
+                const int b = b0 + k * kFinSub;
+                if (b < blocks) merge(na, mean, M2, (double)(min(N, (b + 1) * kRowBlock) - b * kRowBlock), pm[k], pm2[k]);
+            }
         }
-        // torch: input.mean / input.var on float32 return float32
-        const double bmean = (double)(float)mean;
-        const double bvar = (double)(float)(N > 1 ? M2 / (double)(N - 1) : 0.0);
-        const double bc = (double)N;
-        // RunningMeanStd._update_mean_var_count_from_moments, same order of operations
-        const double delta = bmean - rmean[c];
-        const double tot = cnt + bc;
-        const double new_mean = rmean[c] + delta * bc / tot;
-        const double m_a = rvar[c] * cnt;
-        const double m_b = bvar * bc;
-        const double m2 = m_a + m_b + delta * delta * cnt * bc / tot;
-        rmean[c] = new_mean;
-        rvar[c] = m2 / tot;
     }
-    if (c == 0) *count = cnt + (double)N;
+    sh[j][cl][0] = na;
+    sh[j][cl][1] = mean;
+    sh[j][cl][2] = M2;
+    __syncthreads();
+    if (j != 0 || c >= C) return;
+    for (int q = 1; q < kFinSub; ++q)
+        if (sh[q][cl][0] > 0.0) merge(na, mean, M2, sh[q][cl][0], sh[q][cl][1], sh[q][cl][2]);
+    const double cnt = *count;  // updated by k_rms_norm, after every column's update
+    // torch: input.mean / input.var on float32 return float32
+    const double bmean = (double)(float)mean;
+    const double bvar = (double)(float)(N > 1 ? M2 / (double)(N - 1) : 0.0);
+    const double bc = (double)N;
+    // RunningMeanStd._update_mean_var_count_from_moments, same order of operations
+    const double delta = bmean - rmean[c];
+    const double tot = cnt + bc;
+    const double new_mean = rmean[c] + delta * bc / tot;
+    const double m_a = rvar[c] * cnt;
+    const double m_b = bvar * bc;
+    const double m2 = m_a + m_b + delta * delta * cnt * bc / tot;
+    rmean[c] = new_mean;
+    rvar[c] = m2 / tot;
 }
 
 __global__ __launch_bounds__(256) void k_rms_norm(const float* __restrict__ x, int64_t n, int C,
                                                   const double* __restrict__ rmean, const double* __restrict__ rvar,
-                                                  float eps, float* __restrict__ y) {
+                                                  float eps, float* __restrict__ y, double* __restrict__ count,
+                                                  double add) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (count && i == 0) *count += add;  // the running count, after k_rms_fin read it
     if (i >= n) return;
     const int c = (int)(i % C);
     const float m = (float)rmean[c];
@@ -98,12 +135,12 @@ extern "C" int rl_rms_normalize(const float* x, int32_t rows, int32_t cols, doub
     if (update) {
         const int blocks = (rows + kRowBlock - 1) / kRowBlock;
         hipLaunchKernelGGL(k_rms_part, dim3(blocks), dim3(kCols), 0, st, x, (int)rows, (int)cols, partials);
-        hipLaunchKernelGGL(k_rms_fin, dim3(1), dim3(kCols), 0, st, partials, blocks, (int)rows, (int)cols,
-                           running_mean, running_var, count);
+        hipLaunchKernelGGL(k_rms_fin, dim3((cols + kFinCols - 1) / kFinCols), dim3(kFinCols * kFinSub), 0, st, partials,
+                           blocks, (int)rows, (int)cols, running_mean, running_var, count);
     }
     const int64_t n = (int64_t)rows * cols;
     hipLaunchKernelGGL(k_rms_norm, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, (int)cols,
-                       running_mean, running_var, (float)epsilon, y);
+                       running_mean, running_var, (float)epsilon, y, update ? count : nullptr, (double)rows);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         char msg[256];

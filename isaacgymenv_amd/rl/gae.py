@@ -240,7 +240,7 @@ def rms_normalize(x, running_mean, running_var, count, epsilon: float, update: b
         assert t.dtype == torch.float64 and t.is_contiguous() and t.device == x.device
     N, Cc = x.shape
     y = torch.empty_like(x)
-    part = torch.empty(((N + 127) // 128) * Cc * 2, dtype=torch.float32, device=x.device) if update else None
+    part = torch.empty(((N + 63) // 64) * Cc * 2, dtype=torch.float32, device=x.device) if update else None
     stream = torch.cuda.current_stream(x.device).cuda_stream
     rc = lib().rl_rms_normalize(x.data_ptr(), N, Cc, running_mean.data_ptr(), running_var.data_ptr(),
                                 count.data_ptr(), float(epsilon), int(bool(update)),
