@@ -16,6 +16,7 @@
  *   rl_colsum_accum : the same layers' bias gradients (column sums), deterministic.
  *   rl_ppo_loss / rl_ppo_loss_backward : the minibatch PPO loss and its gradient.
  *   rl_rms_normalize : the model's running mean / std input normalisation.
+ *   rl_policy_head : the act forward's sampling / neglogp / value unnormalisation.
  *   rl_rollout_post : the rollout bookkeeping after each env step (play_steps).
  *
  * All pointers are device pointers; calls are ordered on `stream` (a hipStream_t,
@@ -105,6 +106,17 @@ int rl_ppo_loss_backward(const float *grad_loss, const float *dmu, const float *
  */
 int rl_rms_normalize(const float *x, int32_t rows, int32_t cols, double *running_mean, double *running_var,
                      double *count, double epsilon, int32_t update, float *partials, float *y, void *stream);
+
+/*
+ * Act-forward head of the fixed-sigma continuous model (rl_games ModelA2CContinuousLogStd eval forward):
+ *   sigmas = exp(logstd) [N][A], actions = noise * sigma + mu (noise: torch's normal_(0, 1) draws),
+ *   neglogp [N] of the actions, value_out [N] = value unnormalised by the value RunningMeanStd
+ *   (value_mean / value_var: its float64 moments, [1]; both null = no value normalisation).
+ *   mu, noise [N][A], logstd [A], value [N]: f32.
+ */
+int rl_policy_head(const float *mu, const float *noise, const float *logstd, const float *value,
+                   const double *value_mean, const double *value_var, double value_eps, int32_t num_envs,
+                   int32_t num_actions, float *actions, float *sigmas, float *neglogp, float *value_out, void *stream);
 
 /*
  * Rollout bookkeeping after one VecTask.step (rl_games a2c_common.py play_steps, the statements after

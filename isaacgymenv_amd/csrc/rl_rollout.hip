@@ -109,3 +109,64 @@ extern "C" int rl_rollout_post(const float* rewards, const void* dones, int32_t 
     }
     return 0;
 }
+
+// ---------------------------------------------------------------- act forward head
+// models.ModelA2CContinuousLogStd eval forward after the network (fixed sigma), rl/network.py:
+//   sigma = exp(logstd); action = normal(0, 1) * sigma + mu  (the standard normals drawn by torch's
+//   normal_, so the RNG stream is torch's); neglogp(action); value = RunningMeanStd unnorm (clamp to
+//   [-5, 5], * sqrt(float(var) + eps) + float(mean)).  One lane per env; replaces ~14 launches.
+namespace {
+
+__global__ __launch_bounds__(256) void k_policy_head(const float* __restrict__ mu, const float* __restrict__ noise,
+                                                     const float* __restrict__ logstd, const float* __restrict__ value,
+                                                     const double* __restrict__ vmean, const double* __restrict__ vvar,
+                                                     float veps, int N, int A, float nlp_const,
+                                                     float* __restrict__ actions, float* __restrict__ sigmas,
+                                                     float* __restrict__ neglogp, float* __restrict__ value_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    float sq = 0.f, sls = 0.f;
+    for (int a = 0; a < A; ++a) {
+        const size_t k = (size_t)i * A + a;
+        const float ls = logstd[a];
+        const float s = expf(ls);
+        const float m = mu[k];
+        const float t = noise[k] * s;
+        const float x = t + m;
+        actions[k] = x;
+        sigmas[k] = s;
+        const float z = (x - m) / s;
+        sq += z * z;
+        sls += ls;
+    }
+    neglogp[i] = 0.5f * sq + nlp_const + sls;
+    float v = value[i];
+    if (vmean) {
+        v = fminf(fmaxf(v, -5.f), 5.f);
+        v = sqrtf((float)vvar[0] + veps) * v + (float)vmean[0];
+    }
+    value_out[i] = v;
+}
+
+}  // namespace
+
+extern "C" int rl_policy_head(const float* mu, const float* noise, const float* logstd, const float* value,
+                              const double* value_mean, const double* value_var, double value_eps, int32_t num_envs,
+                              int32_t num_actions, float* actions, float* sigmas, float* neglogp, float* value_out,
+                              void* stream) {
+    if (num_envs <= 0 || num_actions <= 0) return rl_set_error("rl_policy_head: num_envs, num_actions must be positive");
+    if (!mu || !noise || !logstd || !value || !actions || !sigmas || !neglogp || !value_out ||
+        (!value_mean) != (!value_var))
+        return rl_set_error("rl_policy_head: null pointer");
+    const double c = 0.5 * 1.8378770664093453 * num_actions;  // 0.5 * math.log(2 pi) * A, as Python computes it
+    hipLaunchKernelGGL(k_policy_head, dim3((num_envs + 255) / 256), dim3(256), 0, (hipStream_t)stream, mu, noise, logstd,
+                       value, value_mean, value_var, (float)value_eps, (int)num_envs, (int)num_actions, (float)c,
+                       actions, sigmas, neglogp, value_out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        char msg[256];
+        snprintf(msg, sizeof(msg), "rl_policy_head: launch failed: %s", hipGetErrorString(e));
+        return rl_set_error(msg) + 1;
+    }
+    return 0;
+}

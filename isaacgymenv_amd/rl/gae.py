@@ -15,7 +15,8 @@ import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libgymrl.so")
 EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accum", "rl_colsum_accum", "rl_rollout_post",
-                    "rl_ppo_loss", "rl_ppo_loss_backward", "rl_rms_normalize"]
+                    "rl_ppo_loss", "rl_ppo_loss_backward", "rl_rms_normalize",
+                    "rl_policy_head"]
 _lib = None
 
 
@@ -42,6 +43,8 @@ def lib():
                                            vp]
         L.rl_rms_normalize.restype = C.c_int
         L.rl_rms_normalize.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp, C.c_double, C.c_int32, vp, vp, vp]
+        L.rl_policy_head.restype = C.c_int
+        L.rl_policy_head.argtypes = [vp, vp, vp, vp, vp, vp, C.c_double, C.c_int32, C.c_int32, vp, vp, vp, vp, vp]
         L.rl_rollout_post.restype = C.c_int
         L.rl_rollout_post.argtypes = [vp, vp, C.c_int32, vp, C.c_int32, vp, C.c_double, C.c_double, C.c_double,
                                       C.c_int32, vp, vp, vp, vp, vp, vp, C.c_int32, vp]
@@ -248,3 +251,26 @@ def rms_normalize(x, running_mean, running_var, count, epsilon: float, update: b
     if rc != 0:
         raise RuntimeError(f"rl_rms_normalize failed: {lib().rl_last_error().decode()}")
     return y
+
+
+def policy_head(mu, noise, logstd, value, value_rms=None):
+    """Act-forward head (include/gymrl.h rl_policy_head): returns (actions [N, A], sigmas [N, A],
+    neglogp [N], values [N, 1]); value_rms: the value RunningMeanStd (value_size 1) or None."""
+    N, A = mu.shape
+    for t in (mu, noise, logstd, value):
+        assert t.is_cuda and t.device == mu.device and t.dtype == torch.float32 and t.is_contiguous()
+    assert noise.shape == mu.shape and logstd.numel() == A and value.numel() == N
+    actions, sigmas = torch.empty_like(mu), torch.empty_like(mu)
+    neglogp = torch.empty(N, dtype=torch.float32, device=mu.device)
+    vout = torch.empty(N, 1, dtype=torch.float32, device=mu.device)
+    vm = vv = None
+    eps = 0.0
+    if value_rms is not None:
+        assert value_rms.running_mean.numel() == 1
+        vm, vv, eps = value_rms.running_mean.data_ptr(), value_rms.running_var.data_ptr(), value_rms.epsilon
+    stream = torch.cuda.current_stream(mu.device).cuda_stream
+    rc = lib().rl_policy_head(mu.data_ptr(), noise.data_ptr(), logstd.data_ptr(), value.data_ptr(), vm, vv, float(eps),
+                              N, A, actions.data_ptr(), sigmas.data_ptr(), neglogp.data_ptr(), vout.data_ptr(), stream)
+    if rc != 0:
+        raise RuntimeError(f"rl_policy_head failed: {lib().rl_last_error().decode()}")
+    return actions, sigmas, neglogp, vout

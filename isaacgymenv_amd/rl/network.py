@@ -161,6 +161,18 @@ class ModelA2CContinuousLogStd(nn.Module):
         is_train = input_dict.get("is_train", True)
         prev_actions = input_dict.get("prev_actions", None)
         obs = self.norm_obs(input_dict["obs"])
+        net = self.a2c_network
+        if (not is_train and obs.is_cuda and obs.dtype == torch.float32 and net.fixed_sigma
+                and (not self.normalize_value or self.value_mean_std.running_mean.numel() == 1)):
+            # act forward on the device: the network, torch's normal_ draws, then one kernel for the head
+            a_out = net.actor_mlp(obs)
+            c_out = net.critic_mlp(obs) if net.separate else a_out
+            value = net.value(c_out).contiguous()
+            mu = net.mu(a_out).contiguous()
+            noise = torch.empty_like(mu).normal_(0.0, 1.0)
+            actions, sigmas, neglogp, values = gae.policy_head(
+                mu, noise, net.sigma.detach(), value, self.value_mean_std if self.normalize_value else None)
+            return {"neglogpacs": neglogp, "values": values, "actions": actions, "mus": mu, "sigmas": sigmas}
         mu, logstd, value = self.a2c_network(obs)
         sigma = torch.exp(logstd)
         distr = torch.distributions.Normal(mu, sigma, validate_args=False)

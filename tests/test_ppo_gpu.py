@@ -291,3 +291,30 @@ def test_rms_normalize_kernel_matches_torch(rows, cols):
     y_eval = gae.rms_normalize(x, mine.running_mean, mine.running_var, mine.count, mine.epsilon, update=False)
     ref.eval()
     torch.testing.assert_close(y_eval, RunningMeanStd.forward(ref, x.t().contiguous().t()), rtol=2e-5, atol=2e-5)
+
+
+def test_policy_head_kernel_matches_torch_act_forward():
+    """The act forward through rl_policy_head against the torch statement of the same forward (same
+    torch normal_ draws): actions, sigmas and values bit-identical, neglogp to 1e-5."""
+    agent = _agent("AnymalTerrain", 1024, minibatch_size=8192)
+    agent.use_graphs = False
+    agent.train_epoch()
+    model = agent.model
+    model.eval()
+    obs = agent.obs["obs"]
+    with torch.no_grad():
+        torch.manual_seed(3)
+        fused = model({"is_train": False, "obs": obs})
+        torch.manual_seed(3)
+        # the torch statement: a non-contiguous copy of obs takes RunningMeanStd's torch path and a float64
+        # obs is not taken by the fused head; instead call the pieces as the torch path does
+        net = model.a2c_network
+        o = model.norm_obs(obs)
+        mu, logstd, value = net(o)
+        sigma = torch.exp(logstd)
+        act = torch.empty_like(mu).normal_(0.0, 1.0).mul_(sigma).add_(mu)
+        nlp = model.neglogp(act, mu, sigma, logstd)
+        val = model.denorm_value(value)
+    assert torch.equal(fused["actions"], act) and torch.equal(fused["sigmas"], sigma)
+    assert torch.equal(fused["values"], val) and torch.equal(fused["mus"], mu)
+    torch.testing.assert_close(fused["neglogpacs"], nlp, rtol=1e-5, atol=1e-5)
