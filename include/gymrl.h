@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 2
+#define RL_ABI_VERSION 3
 
 int rl_abi_version(void);
 const char *rl_last_error(void);

@@ -69,6 +69,10 @@ struct gs_sim {
   launch_sim_fn sim_fn = nullptr;
   launch_pd_fn pd_fn = nullptr;
   int variant = 0;  // kernel actually selected: 1 lane, 2 team
+  // the kernel gs_sim_set_model selected (drives may move the sim to the lane kernel and back)
+  launch_sim_fn model_sim_fn = nullptr;
+  launch_pd_fn model_pd_fn = nullptr;
+  int model_variant = 0;
   DevModel* d_model = nullptr;
   DevModel h_model{};             // host copy (sensors are added after set_model)
   DevLinks* d_links = nullptr;    // link kinematics tables (gs_kinematics.hip)
@@ -430,6 +434,9 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   s->pd_fn = pd_fn;
   s->htopo = htopo;
   s->variant = variant;
+  s->model_sim_fn = sim_fn;
+  s->model_pd_fn = pd_fn;
+  s->model_variant = variant;
   s->nr = m->num_links;
   s->nv = (m->fixed_base ? 0 : 6) + m->num_dofs;
   s->nb = m->num_bodies;
@@ -652,10 +659,11 @@ int gs_sim_set_dof_drives(gs_sim* s, const int32_t* mode, const double* stiffnes
     h.dkd[j] = (float)kd;
     any |= (kp > 0.0 || kd > 0.0);
   }
-  // the lane-team kernel has no drive terms: drives run the one-env-per-lane kernel
-  launch_sim_fn sim_fn = s->sim_fn;
-  launch_pd_fn pd_fn = s->pd_fn;
-  int variant = s->variant;
+  // the lane-team kernel has no drive terms: drives run the one-env-per-lane kernel; the kernel
+  // gs_sim_set_model selected comes back once every gain is zero again
+  launch_sim_fn sim_fn = s->model_sim_fn;
+  launch_pd_fn pd_fn = s->model_pd_fn;
+  int variant = s->model_variant;
   if (any && variant == 2) {
     if (s->params.kernel_variant == 2)
       return fail("gs_sim_set_dof_drives: the lane-team kernel (kernel_variant 2) has no joint drives");
@@ -664,7 +672,10 @@ int gs_sim_set_dof_drives(gs_sim* s, const int32_t* mode, const double* stiffnes
     variant = 1;
   }
   if (!s->host) {
+    // the physics kernels read d_model: the blocking upload must not overtake a launch still queued on
+    // a caller's (non-blocking) stream, so the device drains first (cold path: dof property changes)
     hipError_t e = hipSetDevice(s->device);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipMemcpy(s->d_model, &h, sizeof(DevModel), hipMemcpyHostToDevice);
     if (e != hipSuccess) return hip_fail(e, "gs_sim_set_dof_drives hipMemcpy");
   }

@@ -174,6 +174,23 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
 #pragma unroll
   for (int j = 0; j < T::ND; ++j) nu[NB6 + j] = s.qd[j];
 
+  // joint drives: the drive force estimate kp (q* - q - h qd) + kd (qd* - qd) of each dof;
+  // within the dof's effort limit the drive is implicit ((h kd + h^2 kp) on M's diagonal), a saturated drive
+  // applies the clamped force explicitly (PhysX: the drive's max force is the dof's effort property)
+  float dforce[ND > 0 ? ND : 1];
+  bool dimpl[ND > 0 ? ND : 1];
+  if (P.any_drive) {
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const float pt = P.ptgt ? P.ptgt[(size_t)e * ND + j] : 0.f;
+      const float vt = P.vtgt ? P.vtgt[(size_t)e * ND + j] : 0.f;
+      const float f = M->dkp[j] * (pt - s.q[j] - h * s.qd[j]) + M->dkd[j] * (vt - s.qd[j]);
+      const float ef = M->effort[j];
+      dimpl[j] = !(ef > 0.f) || fabsf(f) <= ef;
+      dforce[j] = dimpl[j] ? f : clampf(f, -ef, ef);
+    }
+  }
+
   float R[NB][9], X[NB][3], S[NB][6], V[NB][6], A[NB][6], Fc[NB][6];
   SpI Ic[NB];
   float Mm[NV][NV], bias[NV];
@@ -408,7 +425,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
             float F[6];
             spi_mul(Ic[a], S[a], F);
             Mm[ga][ga] = dot6(S[a], F) + M->armature[T::bdof[a]];
-            if (P.any_drive) Mm[ga][ga] += h * (M->dkd[T::bdof[a]] + h * M->dkp[T::bdof[a]]);
+            if (P.any_drive && dimpl[T::bdof[a]]) Mm[ga][ga] += h * (M->dkd[T::bdof[a]] + h * M->dkp[T::bdof[a]]);
 #pragma unroll
             for (int k = 0; k < T::MAXDEP; ++k) {
               if (k < T::depth[ga]) {
@@ -497,11 +514,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
       const float ef = M->effort[j];
       if (ef > 0.f) t = clampf(t, -ef, ef);
       r[NB6 + j] = t - bias[NB6 + j];
-      if (P.any_drive) {  // implicit drive: kp (q* - q - h qd) + kd (qd* - qd), (h kd + h^2 kp) on M's diagonal
-        const float pt = P.ptgt ? P.ptgt[(size_t)e * ND + j] : 0.f;
-        const float vt = P.vtgt ? P.vtgt[(size_t)e * ND + j] : 0.f;
-        r[NB6 + j] += M->dkp[j] * (pt - s.q[j] - h * s.qd[j]) + M->dkd[j] * (vt - s.qd[j]);
-      }
+      if (P.any_drive) r[NB6 + j] += dforce[j];
     }
 #pragma unroll
     for (int kk = 0; kk < NV; ++kk) {

@@ -444,16 +444,20 @@ class Sim:
     def drive_tables(self):
         """(mode int32 [nd], stiffness [nd], damping [nd]) of the actors' dof properties.  Isaac Gym keeps
         drive gains per actor; this simulator holds one set per sim (the in-scope tasks give every actor
-        the same properties), so actors whose drive settings differ are refused."""
+        the same properties), so actors whose EFFECTIVE drive gains differ are refused: stiffness counts
+        only where driveMode is POS, damping where it is POS or VEL (EFFORT / NONE dofs ignore both, as
+        gs_sim_set_dof_drives does)."""
         first = None
         for e in self.envs:
             for a in e.actors:
                 p = a.dof_props
-                t = (p["driveMode"].astype(np.int32), p["stiffness"].astype(np.float64),
-                     p["damping"].astype(np.float64))
+                mode = p["driveMode"].astype(np.int32)
+                pos, vel = mode == int(DOF_MODE_POS), mode == int(DOF_MODE_VEL)
+                t = (mode, p["stiffness"].astype(np.float64), p["damping"].astype(np.float64))
+                eff = (np.where(pos, t[1], 0.0), np.where(pos | vel, t[2], 0.0))
                 if first is None:
-                    first = t
-                elif not all(np.array_equal(x, y) for x, y in zip(first, t)):
+                    first, first_eff = t, eff
+                elif not all(np.array_equal(x, y) for x, y in zip(first_eff, eff)):
                     raise NotImplementedError("joint drives: actors with different driveMode / stiffness / damping "
                                               "(one drive setting per sim, DESIGN.md section 6)")
         return first

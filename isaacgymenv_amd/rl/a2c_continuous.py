@@ -194,6 +194,10 @@ class A2CAgent:
         for p in self.params:
             p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
             off += p.numel()
+        # the learner's .backward() lets the split-K Linear layers accumulate straight into these views
+        for m in self.model.modules():
+            if isinstance(m, Linear):
+                m.direct_grad = True
         if self.multi_gpu:
             self._broadcast_params()
         on_gpu = self.device.type == "cuda"

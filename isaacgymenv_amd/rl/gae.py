@@ -20,6 +20,9 @@ EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accu
 _lib = None
 
 
+RL_ABI_VERSION = 3  # include/gymrl.h
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -27,6 +30,11 @@ def lib():
             raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m isaacgymenv_amd.build`. "
                                "Device tensors have no torch fallback for GAE.")
         L = C.CDLL(LIB_PATH)
+        L.rl_abi_version.restype = C.c_int
+        got = L.rl_abi_version()
+        if got != RL_ABI_VERSION:
+            raise RuntimeError(f"{LIB_PATH} has RL ABI {got}, this package needs {RL_ABI_VERSION}: rebuild it "
+                               "with `python -m isaacgymenv_amd.build`")
         vp = C.c_void_p
         L.rl_gae.restype = C.c_int
         L.rl_gae.argtypes = [vp, vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_double, C.c_double, vp, vp, vp, vp]

@@ -31,11 +31,16 @@ class _SplitKLinearFn(torch.autograd.Function):
     """Linear whose weight gradient is SPLIT_K row-block partial GEMMs finished by ONE HIP kernel that
     adds them (fixed order, fp32) straight into ``weight.grad`` (libgymrl rl_splitk_accum; under the
     learner ``weight.grad`` is a view into its flat gradient buffer).  The forward casts once to the
-    autocast dtype and keeps the cast operands for the backward, so the backward re-casts nothing."""
+    autocast dtype and keeps the cast operands for the backward, so the backward re-casts nothing.
+
+    ``direct`` (set by the learner, A2CAgent, whose ``.backward()`` is the only caller) accumulates the weight
+    and wide bias gradients straight into ``.grad`` and returns no tensor for them; otherwise (torch.autograd.grad,
+    hooks, any other caller) the same kernels finish the sum into a fresh tensor that autograd returns, as
+    nn.Linear does."""
 
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda")
-    def forward(ctx, x, w, b, w_half=None, b_half=None):
+    def forward(ctx, x, w, b, w_half=None, b_half=None, direct=False):
         dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
         # w_half / b_half: the learner's fp16 copies of the parameters, refreshed once per minibatch by
         # one cast of its flat parameter buffer (A2CAgent._refresh_half_params) instead of a cast per tensor
@@ -46,6 +51,7 @@ class _SplitKLinearFn(torch.autograd.Function):
         ctx.save_for_backward(xc, wc)
         ctx.w, ctx.b = w, b
         ctx.has_bias = b is not None
+        ctx.direct = bool(direct)
         return torch.nn.functional.linear(xc, wc, bc)
 
     @staticmethod
@@ -54,25 +60,34 @@ class _SplitKLinearFn(torch.autograd.Function):
         xc, wc = ctx.saved_tensors
         g = g.contiguous()
         gx = g @ wc.to(g.dtype) if ctx.needs_input_grad[0] else None
+        gw = None
         if ctx.needs_input_grad[1]:
             w = ctx.w
             rows = g.shape[0]
             parts = torch.bmm(g.reshape(SPLIT_K, rows // SPLIT_K, -1).transpose(1, 2),
                               xc.to(g.dtype).reshape(SPLIT_K, rows // SPLIT_K, -1))
-            if w.grad is None:
-                w.grad = torch.zeros_like(w, dtype=torch.float32)
-            gae.splitk_accum(parts, w.grad)
+            if ctx.direct:
+                if w.grad is None:
+                    w.grad = torch.zeros_like(w, dtype=torch.float32)
+                gae.splitk_accum(parts, w.grad)
+            else:
+                gw = torch.zeros_like(w, dtype=torch.float32)
+                gae.splitk_accum(parts, gw)
         gb = None
         if ctx.has_bias and ctx.needs_input_grad[2]:
             b = ctx.b
             if gae.colsum_supported(g):
-                if b.grad is None:
-                    b.grad = torch.zeros_like(b, dtype=torch.float32)
-                gae.colsum_accum(g, b.grad)
+                if ctx.direct:
+                    if b.grad is None:
+                        b.grad = torch.zeros_like(b, dtype=torch.float32)
+                    gae.colsum_accum(g, b.grad)
+                else:
+                    gb = torch.zeros_like(b, dtype=torch.float32)
+                    gae.colsum_accum(g, gb)
             else:  # the narrow heads (value: 1 column, mu: 12)
                 gb = g.sum(0, dtype=torch.float32)
-        # the weight (and wide bias) gradients are already in .grad (accumulated like autograd would)
-        return gx, None, gb, None, None
+        # direct: the weight (and wide bias) gradients are already in .grad (accumulated like autograd would)
+        return gx, gw, gb, None, None, None
 
 
 class Linear(nn.Linear):
@@ -81,11 +96,12 @@ class Linear(nn.Linear):
 
     half_weight = None  # fp16 views set by the learner (A2CAgent), else None
     half_bias = None
+    direct_grad = False  # set by the learner: its .backward() accumulates straight into .grad
 
     def forward(self, x):
         if (torch.is_grad_enabled() and x.dim() == 2 and x.shape[0] >= SPLIT_K_MIN_ROWS
                 and x.shape[0] % SPLIT_K == 0 and x.is_cuda and self.weight.dtype == torch.float32):
-            return _SplitKLinearFn.apply(x, self.weight, self.bias, self.half_weight, self.half_bias)
+            return _SplitKLinearFn.apply(x, self.weight, self.bias, self.half_weight, self.half_bias, self.direct_grad)
         return super().forward(x)
 
 

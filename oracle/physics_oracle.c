@@ -380,6 +380,21 @@ static void env_substep(const OModel *m, const OParams *p, real h,
     if (!fb) for (int k = 0; k < 6; ++k) bias[k] = F[0][k];
     for (int i = 1; i < nb; ++i) bias[nbase + m->bdof[i]] = dot6(S[i], F[i]);
 
+    /* ---- joint drives: force estimate kp (q* - q - h qd) + kd (qd* - qd); implicit
+     * within the dof's effort limit, the clamped force applied explicitly when saturated */
+    real dforce[MAXV];
+    int dimpl[MAXV];
+    if (m->dkp && m->dkd) {
+        for (int j = 0; j < nd; ++j) {
+            const real pt = ptgt ? ptgt[j] : 0, vt = vtgt ? vtgt[j] : 0;
+            const real q = dq[2 * j], qd = dq[2 * j + 1];
+            const real f = (real)m->dkp[j] * (pt - q - h * qd) + (real)m->dkd[j] * (vt - qd);
+            const real ef = (real)m->effort[j];
+            dimpl[j] = !(ef > 0) || fabs(f) <= ef;
+            dforce[j] = dimpl[j] ? f : (f > ef ? ef : -ef);
+        }
+    }
+
     /* ---- CRBA dense mass matrix */
     real M[MAXV * MAXV];
     memset(M, 0, sizeof(M));
@@ -404,7 +419,7 @@ static void env_substep(const OModel *m, const OParams *p, real h,
         real Fi[6];
         spi_mul(&Ic[i], S[i], Fi);
         M[di * MAXV + di] = dot6(S[i], Fi) + (real)m->armature[m->bdof[i]];
-        if (m->dkp && m->dkd)
+        if (m->dkp && m->dkd && dimpl[m->bdof[i]])
             M[di * MAXV + di] += h * ((real)m->dkd[m->bdof[i]] + h * (real)m->dkp[m->bdof[i]]);
         for (int j = m->parent[i]; j > 0; j = m->parent[j]) {
             const int dj = nbase + m->bdof[j];
@@ -423,11 +438,7 @@ static void env_substep(const OModel *m, const OParams *p, real h,
         const real e = (real)m->effort[j];
         if (e > 0) t = t > e ? e : (t < -e ? -e : t);
         rhs[nbase + j] = t - bias[nbase + j];
-        if (m->dkp && m->dkd) {
-            const real pt = ptgt ? ptgt[j] : 0, vt = vtgt ? vtgt[j] : 0;
-            const real q = dq[2 * j], qd = dq[2 * j + 1];
-            rhs[nbase + j] += (real)m->dkp[j] * (pt - q - h * qd) + (real)m->dkd[j] * (vt - qd);
-        }
+        if (m->dkp && m->dkd) rhs[nbase + j] += dforce[j];
     }
     chol_solve(M, nv, rhs, acc);
     for (int k = 0; k < nv; ++k) nuf[k] = nu[k] + h * acc[k];

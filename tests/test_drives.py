@@ -4,8 +4,9 @@ Isaac Gym exposes PhysX articulation joint drives through the dof properties (dr
 damping) and the target tensors (set_dof_position_target_tensor(_indexed),
 set_dof_velocity_target_tensor; the reference's UsefulHound calls the indexed position setter at
 useful_hound.py:622-627).  The solver applies them as an implicit spring-damper per substep,
-kp (q* - q - h qd) + kd (qd* - qd) with (h kd + h^2 kp) on the mass-matrix diagonal; the fp64 oracle
-restates the same rule (oracle/physics_oracle.c).  Parity vs PhysX's drive is unpinned (PhysX is
+kp (q* - q - h qd) + kd (qd* - qd) with (h kd + h^2 kp) on the mass-matrix diagonal, and a drive whose
+force exceeds the dof's effort limit applies the clamped force explicitly; the fp64 oracle restates the
+same rule (oracle/physics_oracle.c).  Parity vs PhysX's drive is unpinned (PhysX is
 closed and absent).
 
 CPU tests (host backend, no GPU): host vs oracle with random targets (Cartpole, fixed base; Hound,
@@ -128,6 +129,29 @@ def test_position_drive_holds_pendulum_at_target():
     assert np.abs(g_dof[:, :, 1]).max() < 1e-2
 
 
+def test_saturated_drive_is_limited_by_effort():
+    """A drive whose force exceeds the dof's effort limit applies the limit (PhysX: the drive's max
+    force is the dof's effort property): a stiff position drive on the cart slider toward a far target
+    moves the cart exactly as an actuation force equal to the effort does; host backend = oracle."""
+    n, steps = 16, 1
+    art, flat = H.cartpole()
+    root, dof, _, mu, _, _ = _cartpole_case(n, seed=3)
+    eff = float(flat["effort"][0])
+    drives = (np.array([DOF_MODE_POS, DOF_MODE_EFFORT], dtype=np.int32), np.array([1.0e5, 0.0]),
+              np.array([50.0, 0.0]))
+    ptgt = np.zeros((n, 2)); ptgt[:, 0] = 5.0          # 1e5 * ~5 m >> effort: saturated every substep
+    vtgt = np.zeros((n, 2))
+    zero_tau = np.zeros((n, 2))
+    gym, sim, (g_root, g_dof) = _run_sim("cartpole", n, H.CARTPOLE_PARAMS, root, dof, zero_tau, mu, ptgt, vtgt,
+                                         drives, steps, True)
+    o_root, o_dof = _run_oracle(flat, H.CARTPOLE_PARAMS, root, dof, zero_tau, mu, ptgt, vtgt, drives, steps)
+    np.testing.assert_allclose(g_dof, o_dof, atol=2e-5, rtol=1e-4)
+    tau_eff = np.zeros((n, 2)); tau_eff[:, 0] = eff
+    e_root, e_dof = _run_oracle(flat, H.CARTPOLE_PARAMS, root, dof, tau_eff, mu, ptgt, vtgt,
+                                (drives[0], np.zeros(2), np.zeros(2)), steps)
+    np.testing.assert_allclose(o_dof, e_dof, atol=1e-12, rtol=1e-12)
+
+
 def test_indexed_targets_scatter_by_actor():
     n = 6
     gym, sim = H.make_host_sim("cartpole", n, H.CARTPOLE_PARAMS, drives=CARTPOLE_DRIVES)
@@ -148,6 +172,20 @@ def test_different_drive_gains_per_actor_are_refused():
     gym.set_actor_dof_properties(sim.envs[1], 0, props)
     with pytest.raises(NotImplementedError):
         gym.simulate(sim)
+
+
+def test_gains_of_undriven_dofs_may_differ_between_actors():
+    """Only effective gains count (stiffness where driveMode is POS, damping where POS or VEL): actors whose
+    EFFORT dofs carry different stiffness / damping values are accepted."""
+    gym, sim = H.make_host_sim("cartpole", 2, H.CARTPOLE_PARAMS)
+    for i, e in enumerate(sim.envs):
+        props = gym.get_actor_dof_properties(e, 0)
+        props["driveMode"][:] = DOF_MODE_EFFORT
+        props["stiffness"][:] = 10.0 * (i + 1)
+        props["damping"][:] = 3.0 * (i + 1)
+        gym.set_actor_dof_properties(e, 0, props)
+    gym.simulate(sim)
+    assert not sim.drives_dirty
 
 
 def test_drives_updated_after_prepare_take_effect():

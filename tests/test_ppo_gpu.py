@@ -122,8 +122,9 @@ def test_split_k_linear_matches_torch_linear():
     half-precision rounding of the partial sums, 2e-3 of the gradient's scale)."""
     from isaacgymenv_amd.rl.network import Linear
     torch.manual_seed(0)
-    for autocast in (False, True):
+    for autocast, direct in ((False, False), (True, False), (False, True), (True, True)):
         lin = Linear(188, 512).cuda()
+        lin.direct_grad = direct
         ref = torch.nn.Linear(188, 512).cuda()
         ref.load_state_dict(lin.state_dict())
         x = torch.randn(16384, 188, device="cuda")
@@ -139,6 +140,22 @@ def test_split_k_linear_matches_torch_linear():
         for a, b in zip(outs[0], outs[1]):
             tol = 2e-3 if autocast else 1e-5
             assert float((a - b).abs().max()) <= tol * float(b.abs().max()) + 1e-6
+
+
+def test_split_k_linear_autograd_grad_returns_gradients():
+    """Outside the learner (direct_grad False), torch.autograd.grad receives the split-K weight and bias
+    gradients as results and nothing leaks into .grad."""
+    from isaacgymenv_amd.rl.network import Linear
+    torch.manual_seed(1)
+    lin = Linear(188, 512).cuda()
+    ref = torch.nn.Linear(188, 512).cuda()
+    ref.load_state_dict(lin.state_dict())
+    x = torch.randn(16384, 188, device="cuda")
+    gw, gb = torch.autograd.grad(lin(x).sum(), (lin.weight, lin.bias))
+    rw, rb = torch.autograd.grad(ref(x).sum(), (ref.weight, ref.bias))
+    assert lin.weight.grad is None and lin.bias.grad is None
+    assert float((gw - rw).abs().max()) <= 1e-5 * float(rw.abs().max()) + 1e-6
+    assert float((gb - rb).abs().max()) <= 1e-5 * float(rb.abs().max()) + 1e-6
 
 
 @pytest.mark.parametrize("n,offset,dtype", [(96256, 0, torch.float16), (1539, 1, torch.float16),
