@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 4
+#define GS_ABI_VERSION 5
 
 typedef struct gs_sim gs_sim;
 
@@ -79,6 +79,29 @@ typedef struct gs_model_desc {
     const int32_t *link_body;     /* [nl] dynamic body the link is welded into          */
     const double *link_pose;      /* [nl][12] link frame in the body frame: R (9) t (3) */
     const double *link_com;       /* [nl][3] link COM, link frame                       */
+    /* convex hulls and self-collision (ABI 5).  A convex hull (STL mesh
+     * collider, useful_hound.py:329) keeps every hull vertex; against the ground it has 4 dynamic
+     * candidates (cand_dyn 0..3) filled every substep from its vertices.  Filter-0 actors
+     * (gym.create_actor(..., filter=0), anymal_terrain.py:282, useful_hound.py:421) collide their
+     * own shapes pairwise (gs_sim_set_self_collision). */
+    const int32_t *cand_dyn;      /* [nc] hull slot of a dynamic candidate, -1 fixed point */
+    const int32_t *shape_kind;    /* [ns] 0 sphere 1 capsule 2 box 3 cylinder 4 hull      */
+    const int32_t *shape_body;    /* [ns]                                               */
+    const int32_t *shape_link;    /* [ns]                                               */
+    const double *shape_pose;     /* [ns][12] shape frame in the body frame: R (9) t (3) */
+    const double *shape_size;     /* [ns][3] sphere r | capsule / cylinder r, half length | box half extents */
+    const double *shape_margin;   /* [ns] core radius of the pair narrowphase           */
+    const double *shape_sphere;   /* [ns][4] bounding sphere, body frame centre + radius */
+    int32_t num_hull_verts;
+    const double *hull_verts;     /* [nhv][4] body frame xyz + core factor f (core vertex = c + f (v - c),
+                                     c = shape_sphere centre) */
+    const int32_t *shape_hv0;     /* [ns] hull vertex range [hv0, hv1)                   */
+    const int32_t *shape_hv1;     /* [ns]                                               */
+    int32_t num_pairs;
+    const int32_t *pair_a;        /* [np] shape a < shape b of a link pair that may collide */
+    const int32_t *pair_b;        /* [np]                                               */
+    const int32_t *pair_kind;     /* [np] 0 sphere-sphere 1 sphere-capsule 2 capsule-capsule 3 GJK */
+    int32_t pair_pool;            /* self-contact slots per env (the compiled topology's) */
 } gs_model_desc;
 
 /* gymapi.SimParams subset the reference sets (vec_task.py:514-562). */
@@ -209,6 +232,11 @@ int gs_sim_set_dof_drives(gs_sim *sim, const int32_t *mode, const double *stiffn
  * set_dof_velocity_target_tensor, useful_hound.py:622-627), read by every later simulate / pd_step;
  * NULL = zero targets. */
 int gs_sim_bind_dof_targets(gs_sim *sim, const float *pos_targets, const float *vel_targets);
+
+/* Self-collision (ABI 5): gym.create_actor with collision filter 0 (anymal_terrain.py:282,
+ * useful_hound.py:421) makes Isaac Gym collide an actor's shapes with each other except on links joined
+ * by a joint.  enable = 1 turns the model's pairs on (every actor of the sim must agree). */
+int gs_sim_set_self_collision(gs_sim *sim, int enable);
 
 /* Physics kernel selected by gs_sim_set_model: 1 one env per lane, 2 lane team, 3 host backend;
  * -1 on error. */

@@ -73,6 +73,7 @@ struct gs_sim {
   launch_sim_fn model_sim_fn = nullptr;
   launch_pd_fn model_pd_fn = nullptr;
   int model_variant = 0;
+  bool team_pairs = false;  // the lane-team kernel solves self-contacts (gs_team.hip)
   DevModel* d_model = nullptr;
   DevModel h_model{};             // host copy (sensors are added after set_model)
   DevLinks* d_links = nullptr;    // link kinematics tables (gs_kinematics.hip)
@@ -305,6 +306,12 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   if (!t)
     return fail("gs_sim_set_model: no compiled kernel for topology %s (add it to tools/gen_topologies.py)",
                 signature(m).c_str());
+  if (m->num_pairs > 0 && m->pair_pool != t->npk)
+    return fail("gs_sim_set_model: self-contact pool differs from the compiled topology's %s",
+                std::to_string(t->npk).c_str());
+  for (int c = 0; c < m->num_candidates; ++c)
+    if (m->cand_dyn && m->cand_dyn[c] != t->cdyn[c])
+      return fail("gs_sim_set_model: hull slots differ from the compiled topology (tools/gen_topologies.py)");
   // Everything is built into locals first and committed at the end, so a failure leaves the sim as
   // it was (no half-set topology with a null kernel or link table).
   DevModel h;
@@ -329,25 +336,48 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
     for (int k = 0; k < 3; ++k) h.cpoint[c][k] = (float)m->cand_point[3 * c + k];
     h.cradius[c] = (float)m->cand_radius[c];
   }
-  // bounding sphere of each shape's candidates (centre = mean point, radius = farthest point + its
-  // radius, widened by 1e-4 relative so that float rounding never culls an active candidate)
+  // shapes (ABI 5): bounding spheres widened by 1e-4 relative so that float rounding never culls an active
+  // candidate or pair; hull vertices; self-collision pairs
+  if (!m->shape_kind || !m->shape_body || !m->shape_link || !m->shape_pose || !m->shape_size || !m->shape_margin ||
+      !m->shape_sphere || !m->shape_hv0 || !m->shape_hv1 || (m->num_candidates > 0 && !m->cand_dyn))
+    return fail("gs_sim_set_model: shape tables missing (gs_model_desc ABI 5)");
+  if (m->num_hull_verts < 0 || m->num_hull_verts > GS_MAXHV || m->num_pairs < 0 || m->num_pairs > GS_MAXP ||
+      (m->num_hull_verts > 0 && !m->hull_verts) || (m->num_pairs > 0 && (!m->pair_a || !m->pair_b || !m->pair_kind)))
+    return fail("gs_sim_set_model: hull vertices / self-collision pairs exceed compiled maxima");
   for (int sh = 0; sh < m->num_shapes; ++sh) {
-    double cen[3] = {0, 0, 0}, rad = 0.0;
-    int cnt = 0;
-    for (int c = 0; c < m->num_candidates; ++c)
-      if (m->cand_shape[c] == sh) {
-        for (int k = 0; k < 3; ++k) cen[k] += m->cand_point[3 * c + k];
-        ++cnt;
-      }
-    for (int k = 0; k < 3; ++k) cen[k] /= cnt > 0 ? cnt : 1;
-    for (int c = 0; c < m->num_candidates; ++c)
-      if (m->cand_shape[c] == sh) {
-        double d2 = 0.0;
-        for (int k = 0; k < 3; ++k) d2 += (m->cand_point[3 * c + k] - cen[k]) * (m->cand_point[3 * c + k] - cen[k]);
-        rad = std::max(rad, std::sqrt(d2) + m->cand_radius[c]);
-      }
-    for (int k = 0; k < 3; ++k) h.shc[sh][k] = (float)cen[k];
-    h.shc[sh][3] = (float)(rad * (1.0 + 1e-4) + 1e-5);
+    for (int k = 0; k < 3; ++k) h.shc[sh][k] = (float)m->shape_sphere[4 * sh + k];
+    h.shc[sh][3] = (float)(m->shape_sphere[4 * sh + 3] * (1.0 + 1e-4) + 1e-5);
+    h.shkind[sh] = m->shape_kind[sh];
+    h.shbody[sh] = m->shape_body[sh];
+    h.shlink[sh] = m->shape_link[sh];
+    for (int k = 0; k < 9; ++k) h.shR[sh][k] = (float)m->shape_pose[12 * sh + k];
+    for (int k = 0; k < 3; ++k) h.sht[sh][k] = (float)m->shape_pose[12 * sh + 9 + k];
+    for (int k = 0; k < 3; ++k) h.shsize[sh][k] = (float)m->shape_size[3 * sh + k];
+    h.shm[sh] = (float)m->shape_margin[sh];
+    h.hv0[sh] = m->shape_hv0[sh];
+    h.hv1[sh] = m->shape_hv1[sh];
+    if (h.shbody[sh] < 0 || h.shbody[sh] >= m->num_bodies || h.shlink[sh] < 0 || h.shlink[sh] >= m->num_links ||
+        h.hv0[sh] < 0 || h.hv1[sh] < h.hv0[sh] || h.hv1[sh] > m->num_hull_verts ||
+        (h.shkind[sh] == 4 && h.hv1[sh] == h.hv0[sh]))
+      return fail("gs_sim_set_model: shape %s tables out of range", std::to_string(sh).c_str());
+  }
+  for (int v = 0; v < m->num_hull_verts; ++v)
+    for (int k = 0; k < 4; ++k) h.hv[v][k] = (float)m->hull_verts[4 * v + k];
+  for (int c = 0; c < m->num_candidates; ++c)
+    if (m->cand_dyn[c] >= 0 && m->shape_kind[m->cand_shape[c]] != 4)
+      return fail("gs_sim_set_model: dynamic candidate %s on a shape that is not a hull", std::to_string(c).c_str());
+  h.np = m->num_pairs;
+  for (int q = 0; q < m->num_pairs; ++q) {
+    h.pa[q] = m->pair_a[q];
+    h.pb[q] = m->pair_b[q];
+    h.pk[q] = m->pair_kind[q];
+    if (h.pa[q] < 0 || h.pb[q] <= h.pa[q] || h.pb[q] >= m->num_shapes || h.pk[q] < 0 || h.pk[q] > 3)
+      return fail("gs_sim_set_model: self-collision pair %s out of range", std::to_string(q).c_str());
+  }
+  for (int b = 0; b < m->num_bodies; ++b) {
+    unsigned mask = 0;
+    for (int a = b; a >= 0; a = m->parent[a]) mask |= 1u << a;
+    h.banc[b] = mask;
   }
   int any_lim = 0;
   for (int j = 0; j < m->num_dofs; ++j) {
@@ -684,6 +714,21 @@ int gs_sim_set_dof_drives(gs_sim* s, const int32_t* mode, const double* stiffnes
   s->sim_fn = sim_fn;
   s->pd_fn = pd_fn;
   s->variant = variant;
+  return 0;
+}
+
+int gs_sim_set_self_collision(gs_sim* s, int enable) {
+  if (!s || !s->topo) return fail("gs_sim_set_self_collision: model not set");
+  if (enable && s->h_model.np > 0 && s->topo->npk <= 0)
+    return fail("gs_sim_set_self_collision: the compiled topology has no self-contact pool");
+  s->dp.self_collide = enable && s->h_model.np > 0;
+  if (s->dp.self_collide && s->variant == 2 && !s->team_pairs) {  // this lane-team build has no pair rows
+    if (s->params.kernel_variant == 2)
+      return fail("gs_sim_set_self_collision: the lane-team kernel (kernel_variant 2) has no self-collision");
+    s->sim_fn = s->topo->sim;
+    s->pd_fn = s->topo->pd;
+    s->variant = 1;
+  }
   return 0;
 }
 

@@ -10,7 +10,12 @@
 #define GS_MAXL 40   // reported links per articulation (fixed-joint links included)
 #define GS_MAXS 8    // force sensors per articulation
 #define GS_MAXSH 32  // collision shapes per articulation
+#define GS_MAXHV 2048  // convex-hull vertices per articulation (UsefulHound's arm: 1503)
+#define GS_MAXP 512   // self-collision shape pairs per articulation (UsefulHound: 253)
+#define GS_MAXPOOL 8  // self-contact slots per env
 #define GS_WAVE 64
+// a contact row whose J M^-1 J^T falls below this takes no impulse (an overlap no dof can separate)
+#define GS_MIN_RESPONSE 1e-7f
 
 // Model constants shared by every env, float32, one copy in device memory.
 // Kernels index it with compile-time body / candidate indices from a uniform
@@ -39,6 +44,17 @@ struct DevModel {
   int has_lim[GS_MAXD];
   int nsens;                    // force sensors (leaf bodies)
   int sens_of_body[GS_MAXB];    // sensor index of body b, -1 if none
+  // ---- convex hulls and self-collision
+  unsigned banc[GS_MAXB];       // bit a set: body a is b or an ancestor of b
+  int shkind[GS_MAXSH];         // 0 sphere 1 capsule 2 box 3 cylinder 4 hull
+  int shbody[GS_MAXSH], shlink[GS_MAXSH];
+  float shR[GS_MAXSH][9], sht[GS_MAXSH][3];  // shape frame in the body frame
+  float shsize[GS_MAXSH][3];    // sphere r | capsule r, half length | box half extents
+  float shm[GS_MAXSH];          // core radius (pair narrowphase margin)
+  int hv0[GS_MAXSH], hv1[GS_MAXSH];  // hull vertex range
+  int np;                       // self-collision pairs
+  int pa[GS_MAXP], pb[GS_MAXP], pk[GS_MAXP];  // shape a < shape b, kind 0 SS 1 SC 2 CC 3 GJK
+  float hv[GS_MAXHV][4];        // hull vertices, body frame xyz + core factor (core = c + f (v - c))
 };
 
 struct DevParams {
@@ -55,6 +71,7 @@ struct DevParams {
   int has_terrain;       // a heightfield triangle mesh is present (TERR kernels, gs_terrain.h)
   TerrainDev terr;
   int any_drive;         // some dof has drive gains (uniform: skips the drive terms entirely)
+  int self_collide;      // filter-0 actors: self-collision pairs
   const float* ptgt;     // [N][nd] dof position targets or null (= 0)
   const float* vtgt;     // [N][nd] dof velocity targets or null (= 0)
 };
@@ -98,6 +115,8 @@ struct TopoEntry {
   int sens;  // force sensors compiled in (T::SENS)
   int row_floats, row_lanes;  // SimBuffers::rows of the plane one-env-per-lane kernels: floats per env
                               // (0 = rows in LDS) and env lanes per workgroup (LaneCfg<T, false>)
+  int npk;                    // self-contact pool slots (T::NPK)
+  const int* cdyn;            // [nc] hull slot of each candidate (T::cdyn)
 };
 
 // Kinematics of the reported links (gs_kinematics.hip): runtime-sized tree tables, one copy in

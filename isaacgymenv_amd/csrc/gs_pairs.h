@@ -1,0 +1,611 @@
+// gs_pairs.h -- convex-hull ground contacts and self-collision narrowphase of the solver.
+//
+// __host__ __device__ like gs_solver.h (the host backend compiles the same source).  The fp64 restatement
+// the kernels are checked against is oracle/physics_oracle.c (hull_ground_select, self_contacts); both follow
+// the same rules, in the same order, so the selected vertices / pairs agree away from exact ties.
+//
+// Reference behaviour restated: Isaac Gym collides a filter-0 actor's shapes with each other
+// (anymal_terrain.py:282, useful_hound.py:421) except on links joined by a joint, and a mesh collider is
+// its convex hull (useful_hound.py:329, Hound.urdf:508-733).
+#pragma once
+#include "gs_internal.h"
+#include "gs_math.h"
+#include "gs_terrain.h"
+
+namespace {
+
+GS_HD float dot3f(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+// ---------------------------------------------------------------- hull vs ground
+// Vertices of hull shape sh (body pose R, X relative to the root origin; root height rootz) below
+// contact_offset, reduced to at most 4: the deepest; the farthest from it horizontally; the one spanning the
+// largest horizontal triangle with those two; the one farthest outside that triangle.  First index wins
+// ties; a step whose best value is <= 1e-10 ends the selection.  Returns the count, vertex indices in sel.
+GS_HD int hull_ground_select(const DevModel* __restrict__ M, int sh, const float* R, const float* X, float rootz,
+                             float off, int* sel) {
+  const int v0 = M->hv0[sh], v1 = M->hv1[sh];
+  auto world = [&](int k, float* w) {
+    const float* v = M->hv[k];
+    w[0] = X[0] + R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
+    w[1] = X[1] + R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
+    w[2] = rootz + X[2] + R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
+  };
+  int i0 = -1;
+  float zmin = 3.0e38f;
+  for (int k = v0; k < v1; ++k) {
+    float w[3];
+    world(k, w);
+    if (w[2] < zmin) { zmin = w[2]; i0 = k; }
+  }
+  if (i0 < 0 || !(zmin < off)) return 0;
+  int n = 0;
+  float p0[3];
+  world(i0, p0);
+  sel[n++] = i0;
+  int i1 = -1;
+  float best = 1e-10f;
+  for (int k = v0; k < v1; ++k) {
+    float w[3];
+    world(k, w);
+    if (!(w[2] < off)) continue;
+    const float d2 = (w[0] - p0[0]) * (w[0] - p0[0]) + (w[1] - p0[1]) * (w[1] - p0[1]);
+    if (d2 > best) { best = d2; i1 = k; }
+  }
+  if (i1 < 0) return n;
+  float p1[3];
+  world(i1, p1);
+  sel[n++] = i1;
+  const float ex = p1[0] - p0[0], ey = p1[1] - p0[1];
+  int i2 = -1;
+  best = 1e-10f;
+  for (int k = v0; k < v1; ++k) {
+    float w[3];
+    world(k, w);
+    if (!(w[2] < off)) continue;
+    const float a = fabsf(ex * (w[1] - p0[1]) - ey * (w[0] - p0[0]));
+    if (a > best) { best = a; i2 = k; }
+  }
+  if (i2 < 0) return n;
+  float p2[3];
+  world(i2, p2);
+  sel[n++] = i2;
+  const float sg = (ex * (p2[1] - p0[1]) - ey * (p2[0] - p0[0])) > 0.f ? 1.f : -1.f;
+  int i3 = -1;
+  best = 1e-10f;
+  for (int k = v0; k < v1; ++k) {
+    float w[3];
+    world(k, w);
+    if (!(w[2] < off)) continue;
+    const float e0 = sg * ((p1[0] - p0[0]) * (w[1] - p0[1]) - (p1[1] - p0[1]) * (w[0] - p0[0]));
+    const float e1 = sg * ((p2[0] - p1[0]) * (w[1] - p1[1]) - (p2[1] - p1[1]) * (w[0] - p1[0]));
+    const float e2 = sg * ((p0[0] - p2[0]) * (w[1] - p2[1]) - (p0[1] - p2[1]) * (w[0] - p2[0]));
+    const float mn = fminf(fminf(e0, e1), e2);
+    if (-mn > best) { best = -mn; i3 = k; }
+  }
+  if (i3 >= 0) sel[n++] = i3;
+  return n;
+}
+
+// ---------------------------------------------------------------- self-collision
+// Shape world data in the lane's LDS column: [SHW * sh + f], f: R (9), centre c (3), bounding-sphere centre (3)
+constexpr int kShW = 15;
+// Self-contact pool entry p at [PE * p + f]: x (3) n (3) t1 (3) t2 (3) sep mu bodyA bodyB linkA linkB | lam (3)
+// | c = J nu_f (3) | 1 / diag (3) | J then scaled Z rows (3 x NV)
+constexpr int kPoolX = 0, kPoolN = 3, kPoolT1 = 6, kPoolT2 = 9, kPoolSep = 12, kPoolMu = 13, kPoolBA = 14,
+              kPoolBB = 15, kPoolLA = 16, kPoolLB = 17, kPoolLam = 18, kPoolC = 21, kPoolDi = 24, kPoolJ = 27;
+template <class T>
+struct PoolCfg {
+  static constexpr int PE = kPoolJ + 3 * T::NV;
+  static constexpr int FLOATS = T::NPK > 0 ? T::NPK * PE : 0;
+};
+
+struct ShapeW {
+  float R[9], c[3], sc[3];
+};
+
+template <int LB>
+GS_HD void load_shape_w(const float* shw, int sh, ShapeW& w) {
+  const float* p = shw + kShW * sh * LB;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) w.R[k] = p[k * LB];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { w.c[k] = p[(9 + k) * LB]; w.sc[k] = p[(12 + k) * LB]; }
+}
+
+// core support point of shape sh (world data W) in direction d; a hull's body pose is its shape pose
+GS_HD void core_support(const DevModel* __restrict__ M, int sh, const ShapeW& W, const float* d, float* out) {
+  const int kind = M->shkind[sh];
+  const float* sz = M->shsize[sh];
+  if (kind == 0) {
+    out[0] = W.c[0]; out[1] = W.c[1]; out[2] = W.c[2];
+  } else if (kind == 1) {
+    const float ax[3] = {W.R[2], W.R[5], W.R[8]};
+    const float s = dot3f(ax, d) >= 0.f ? sz[1] : -sz[1];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) out[k] = W.c[k] + s * ax[k];
+  } else if (kind == 3) {  // flat-ended cylinder: rim point of the end disc (core radius r - m, half length h - m)
+    const float mg = M->shm[sh];
+    const float ax[3] = {W.R[2], W.R[5], W.R[8]};
+    const float da = dot3f(ax, d);
+    const float pp[3] = {d[0] - da * ax[0], d[1] - da * ax[1], d[2] - da * ax[2]};
+    const float lp = sqrtf(dot3f(pp, pp));
+    const float s = da >= 0.f ? sz[1] - mg : -(sz[1] - mg);
+    const float rs = lp > 1e-12f ? (sz[0] - mg) / lp : 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) out[k] = W.c[k] + s * ax[k] + rs * pp[k];
+  } else if (kind == 2) {
+    const float mg = M->shm[sh];
+    out[0] = W.c[0]; out[1] = W.c[1]; out[2] = W.c[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float e[3] = {W.R[i], W.R[3 + i], W.R[6 + i]};
+      const float s = dot3f(e, d) >= 0.f ? sz[i] - mg : -(sz[i] - mg);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) out[k] += s * e[k];
+    }
+  } else {
+    const float dl[3] = {W.R[0] * d[0] + W.R[3] * d[1] + W.R[6] * d[2], W.R[1] * d[0] + W.R[4] * d[1] + W.R[7] * d[2],
+                         W.R[2] * d[0] + W.R[5] * d[1] + W.R[8] * d[2]};
+    const float* cc = M->shc[sh];
+    float best = -3.0e38f, bv[3] = {0.f, 0.f, 0.f};
+    for (int k = M->hv0[sh]; k < M->hv1[sh]; ++k) {
+      const float* v = M->hv[k];
+      const float f = v[3];
+      const float p[3] = {cc[0] + f * (v[0] - cc[0]), cc[1] + f * (v[1] - cc[1]), cc[2] + f * (v[2] - cc[2])};
+      const float t = dot3f(p, dl);
+      if (t > best) { best = t; bv[0] = p[0]; bv[1] = p[1]; bv[2] = p[2]; }
+    }
+    mat3vec(W.R, bv, out);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) out[k] += W.c[k];
+  }
+}
+
+// Centroid of shape sh's core support feature in direction d: the core points within kFeatureEps of the
+// support plane (box corners, hull vertices; a cylinder's end disc, side line or rim point; a capsule's segment
+// or end; a sphere's centre).  Returns the feature's extent, 0 for a single point (the oracle's core_feature).
+constexpr float kFeatureEps = 2e-3f;
+GS_HD float core_feature(const DevModel* __restrict__ M, int sh, const ShapeW& W, const float* d, float* cen) {
+  const int kind = M->shkind[sh];
+  const float* sz = M->shsize[sh];
+  const float mg = M->shm[sh];
+  if (kind == 0) {
+    cen[0] = W.c[0]; cen[1] = W.c[1]; cen[2] = W.c[2];
+    return 0.f;
+  }
+  if (kind == 1 || kind == 3) {
+    const float ax[3] = {W.R[2], W.R[5], W.R[8]};
+    const float hl = kind == 1 ? sz[1] : sz[1] - mg, rr = kind == 1 ? 0.f : sz[0] - mg;
+    const float da = dot3f(ax, d);
+    const float pp[3] = {d[0] - da * ax[0], d[1] - da * ax[1], d[2] - da * ax[2]};
+    const float lp = sqrtf(dot3f(pp, pp));
+    const bool side = 2.f * hl * fabsf(da) <= kFeatureEps;
+    const bool disc = kind == 3 && 2.f * rr * lp <= kFeatureEps;
+    const float s = side ? 0.f : (da >= 0.f ? hl : -hl);
+    const float rs = (disc || !(lp > 1e-12f)) ? 0.f : rr / lp;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) cen[k] = W.c[k] + s * ax[k] + rs * pp[k];
+    return side ? hl : (disc ? rr : 0.f);
+  }
+  if (kind == 2) {
+    float pts[8][3], hmax = -3.0e38f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) pts[c][k] = W.c[k];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const float sg = ((c >> i) & 1) ? 1.f : -1.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) pts[c][k] += sg * (sz[i] - mg) * W.R[3 * k + i];
+      }
+      hmax = fmaxf(hmax, dot3f(pts[c], d));
+    }
+    float acc[3] = {0.f, 0.f, 0.f};
+    int n = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (dot3f(pts[c], d) >= hmax - kFeatureEps) {
+        acc[0] += pts[c][0]; acc[1] += pts[c][1]; acc[2] += pts[c][2];
+        ++n;
+      }
+    const float inv = 1.f / (float)n;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) cen[k] = acc[k] * inv;
+    float ext = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      if (dot3f(pts[c], d) >= hmax - kFeatureEps) {
+        const float dd[3] = {pts[c][0] - cen[0], pts[c][1] - cen[1], pts[c][2] - cen[2]};
+        ext = fmaxf(ext, sqrtf(dot3f(dd, dd)));
+      }
+    return ext;
+  }
+  const float dl[3] = {W.R[0] * d[0] + W.R[3] * d[1] + W.R[6] * d[2], W.R[1] * d[0] + W.R[4] * d[1] + W.R[7] * d[2],
+                       W.R[2] * d[0] + W.R[5] * d[1] + W.R[8] * d[2]};
+  const float* cc = M->shc[sh];
+  auto corev = [&](int k, float* p) {
+    const float* v = M->hv[k];
+    const float f = v[3];
+    p[0] = cc[0] + f * (v[0] - cc[0]); p[1] = cc[1] + f * (v[1] - cc[1]); p[2] = cc[2] + f * (v[2] - cc[2]);
+  };
+  float hmax = -3.0e38f;
+  for (int k = M->hv0[sh]; k < M->hv1[sh]; ++k) {
+    float p[3];
+    corev(k, p);
+    hmax = fmaxf(hmax, dot3f(p, dl));
+  }
+  float acc[3] = {0.f, 0.f, 0.f};
+  int n = 0;
+  for (int k = M->hv0[sh]; k < M->hv1[sh]; ++k) {
+    float p[3];
+    corev(k, p);
+    if (dot3f(p, dl) >= hmax - kFeatureEps) {
+      acc[0] += p[0]; acc[1] += p[1]; acc[2] += p[2];
+      ++n;
+    }
+  }
+  const float inv = 1.f / (float)n;
+  acc[0] *= inv; acc[1] *= inv; acc[2] *= inv;
+  float ext = 0.f;
+  for (int k = M->hv0[sh]; k < M->hv1[sh]; ++k) {
+    float p[3];
+    corev(k, p);
+    if (dot3f(p, dl) >= hmax - kFeatureEps) {
+      const float dd[3] = {p[0] - acc[0], p[1] - acc[1], p[2] - acc[2]};
+      ext = fmaxf(ext, sqrtf(dot3f(dd, dd)));
+    }
+  }
+  mat3vec(W.R, acc, cen);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) cen[k] += W.c[k];
+  return ext;
+}
+
+// Closest point of conv(W[0..k)) to the origin: every vertex subset whose affine closest point has positive
+// barycentrics is a candidate, the nearest wins (first subset on ties).  Subsets are compile-time masks, so
+// the simplex stays in registers.  Returns the chosen mask (0: none valid).
+template <int MASK>
+GS_HD void simplex_subset(const float (&W)[4][3], int k, float& best, int& bm, float* v, float* lam) {
+  constexpr int n = ((MASK >> 0) & 1) + ((MASK >> 1) & 1) + ((MASK >> 2) & 1) + ((MASK >> 3) & 1);
+  constexpr int top = (MASK & 8) ? 4 : (MASK & 4) ? 3 : (MASK & 2) ? 2 : 1;
+  if (top > k) return;
+  int id[4] = {0, 0, 0, 0};
+  {
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if ((MASK >> i) & 1) id[c++] = i;
+  }
+  float l[4] = {1.f, 0.f, 0.f, 0.f}, p[3];
+  if constexpr (n == 1) {
+    p[0] = W[id[0]][0]; p[1] = W[id[0]][1]; p[2] = W[id[0]][2];
+  } else {
+    constexpr int q = n - 1;
+    float E[3][3], G[3][3], r[3], mu[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 1; j < n; ++j)
+#pragma unroll
+      for (int a = 0; a < 3; ++a) E[j - 1][a] = W[id[j]][a] - W[id[0]][a];
+#pragma unroll
+    for (int i = 0; i < q; ++i) {
+      r[i] = -dot3f(W[id[0]], E[i]);
+#pragma unroll
+      for (int j = 0; j < q; ++j) G[i][j] = dot3f(E[i], E[j]);
+    }
+    if constexpr (q == 1) {
+      if (!(G[0][0] > 1e-18f)) return;
+      mu[0] = r[0] / G[0][0];
+    } else if constexpr (q == 2) {
+      const float det = G[0][0] * G[1][1] - G[0][1] * G[1][0];
+      if (!(fabsf(det) > 1e-12f * G[0][0] * G[1][1]) || !(det != 0.f)) return;
+      mu[0] = (r[0] * G[1][1] - G[0][1] * r[1]) / det;
+      mu[1] = (G[0][0] * r[1] - r[0] * G[1][0]) / det;
+    } else {
+      auto det3 = [](const float (&A)[3][3]) {
+        return A[0][0] * (A[1][1] * A[2][2] - A[1][2] * A[2][1]) - A[0][1] * (A[1][0] * A[2][2] - A[1][2] * A[2][0]) +
+               A[0][2] * (A[1][0] * A[2][1] - A[1][1] * A[2][0]);
+      };
+      const float det = det3(G);
+      if (!(fabsf(det) > 1e-12f * G[0][0] * G[1][1] * G[2][2]) || !(det != 0.f)) return;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        float Gc[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) Gc[i][j] = j == c ? r[i] : G[i][j];
+        mu[c] = det3(Gc) / det;
+      }
+    }
+    float l0 = 1.f;
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < q; ++j) {
+      l0 -= mu[j];
+      l[j + 1] = mu[j];
+      ok = ok && (mu[j] > 1e-12f);
+    }
+    l[0] = l0;
+    if (!ok || !(l0 > 1e-12f)) return;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      p[a] = W[id[0]][a];
+#pragma unroll
+      for (int j = 0; j < q; ++j) p[a] += mu[j] * E[j][a];
+    }
+  }
+  const float d2 = dot3f(p, p);
+  if (d2 < best) {
+    best = d2;
+    bm = MASK;
+    v[0] = p[0]; v[1] = p[1]; v[2] = p[2];
+    int j = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lam[i] = ((MASK >> i) & 1) ? l[j++] : 0.f;
+  }
+}
+template <int MASK = 1>
+GS_HD void simplex_all(const float (&W)[4][3], int k, float& best, int& bm, float* v, float* lam) {
+  if constexpr (MASK < 16) {
+    simplex_subset<MASK>(W, k, best, bm, v, lam);
+    simplex_all<MASK + 1>(W, k, best, bm, v, lam);
+  }
+}
+
+// GJK distance between the cores of shapes a and b: closest points pa, pb; returns the distance, 0 when the
+// cores overlap (same iteration and termination rules as the oracle's gjk_cores)
+GS_HD float gjk_cores(const DevModel* __restrict__ M, int sa, int sb, const ShapeW& Wa, const ShapeW& Wb, float* pa,
+                      float* pb) {
+  float v[3] = {Wa.sc[0] - Wb.sc[0], Wa.sc[1] - Wb.sc[1], Wa.sc[2] - Wb.sc[2]};
+  if (dot3f(v, v) < 1e-18f) { v[0] = 1.f; v[1] = 0.f; v[2] = 0.f; }
+  float W[4][3], A[4][3], B[4][3], lam[4] = {1.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 3; ++t) W[i][t] = A[i][t] = B[i][t] = 0.f;
+  int k = 0;
+  for (int it = 0; it < 32; ++it) {
+    const float nv[3] = {-v[0], -v[1], -v[2]};
+    float a[3], b[3], w[3];
+    core_support(M, sa, Wa, nv, a);
+    core_support(M, sb, Wb, v, b);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) w[t] = a[t] - b[t];
+    const float vv = dot3f(v, v);
+    if (k > 0 && vv - dot3f(v, w) <= 1e-10f * vv + 1e-14f) break;
+    bool dup = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float d[3] = {W[i][0] - w[0], W[i][1] - w[1], W[i][2] - w[2]};
+      dup = dup || (i < k && dot3f(d, d) < 1e-16f);
+    }
+    if (dup) break;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i == k) {
+#pragma unroll
+        for (int t = 0; t < 3; ++t) { W[i][t] = w[t]; A[i][t] = a[t]; B[i][t] = b[t]; }
+      }
+    ++k;
+    float best = 3.0e38f, l4[4] = {0.f, 0.f, 0.f, 0.f};
+    int mask = 0;
+    simplex_all(W, k, best, mask, v, l4);
+    if (!mask) return 0.f;
+    // keep the chosen subset, in order (compile-time moves under runtime conditions)
+    float W2[4][3], A2[4][3], B2[4][3];
+    int n = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) W2[i][t] = A2[i][t] = B2[i][t] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if ((mask >> i) & 1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (j == n) {
+#pragma unroll
+            for (int t = 0; t < 3; ++t) { W2[j][t] = W[i][t]; A2[j][t] = A[i][t]; B2[j][t] = B[i][t]; }
+            lam[j] = l4[i];
+          }
+        ++n;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) { W[i][t] = W2[i][t]; A[i][t] = A2[i][t]; B[i][t] = B2[i][t]; }
+    k = n;
+    if (k == 4 || dot3f(v, v) < 1e-18f) return 0.f;
+  }
+  pa[0] = pa[1] = pa[2] = pb[0] = pb[1] = pb[2] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (i < k)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) { pa[t] += lam[i] * A[i][t]; pb[t] += lam[i] * B[i][t]; }
+  return sqrtf(dot3f(v, v));
+}
+
+GS_HD void seg_closest_pt(const float* p, const float* a, const float* b, float* q) {
+  const float ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, ap[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
+  const float l2 = dot3f(ab, ab);
+  float t = l2 > 0.f ? dot3f(ap, ab) / l2 : 0.f;
+  t = t < 0.f ? 0.f : (t > 1.f ? 1.f : t);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) q[k] = a[k] + t * ab[k];
+}
+
+// closest points of segments p1q1, p2q2 (Ericson), parameters s, t; den = a e - b^2
+GS_HD void seg_seg(const float* p1, const float* q1, const float* p2, const float* q2, float& s, float& t, float& den,
+                   float& a, float& e) {
+  float d1[3], d2[3], r[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { d1[k] = q1[k] - p1[k]; d2[k] = q2[k] - p2[k]; r[k] = p1[k] - p2[k]; }
+  a = dot3f(d1, d1);
+  e = dot3f(d2, d2);
+  const float f = dot3f(d2, r);
+  s = 0.f; t = 0.f; den = 0.f;
+  auto cl = [](float x) { return x < 0.f ? 0.f : (x > 1.f ? 1.f : x); };
+  if (a <= 1e-12f && e <= 1e-12f) {
+  } else if (a <= 1e-12f) {
+    t = cl(f / e);
+  } else {
+    const float c = dot3f(d1, r);
+    if (e <= 1e-12f) {
+      s = cl(-c / a);
+    } else {
+      const float b = dot3f(d1, d2);
+      den = a * e - b * b;
+      s = den > 0.f ? cl((b * f - c * e) / den) : 0.f;
+      t = (b * s + f) / e;
+      if (t < 0.f) { t = 0.f; s = cl(-c / a); }
+      else if (t > 1.f) { t = 1.f; s = cl((b - c) / a); }
+    }
+  }
+}
+
+// Self-contacts of one env in pair order, at most T::NPK (later ones dropped): broadphase on the shapes'
+// bounding spheres (within contact_offset), closed-form sphere / capsule pairs, GJK on margin-rounded cores
+// otherwise.  Writes the pool entries' geometry (x relative to the root origin, n from B to A, tangents,
+// separation, friction, bodies, links); returns the count.
+template <class T, int LB>
+GS_HD int self_contacts(const DevModel* __restrict__ M, const DevParams& P, const float* __restrict__ mu_g, int N,
+                        int e, const float* shw, float* pool) {
+  constexpr int PE = PoolCfg<T>::PE;
+  const float off = P.contact_offset;
+  int n = 0;
+  const int np = M->np;
+  for (int q = 0; q < np; ++q) {
+    if (n >= T::NPK) break;
+    const int a = M->pa[q], b = M->pb[q], kind = M->pk[q];
+    const float* sa = shw + (kShW * a + 12) * LB;
+    const float* sb = shw + (kShW * b + 12) * LB;
+    const float d[3] = {sa[0] - sb[0], sa[LB] - sb[LB], sa[2 * LB] - sb[2 * LB]};
+    const float rr = M->shc[a][3] + M->shc[b][3] + off;
+    if (!(dot3f(d, d) < rr * rr)) continue;
+    ShapeW Wa, Wb;
+    load_shape_w<LB>(shw, a, Wa);
+    load_shape_w<LB>(shw, b, Wb);
+    const float ra = M->shm[a], rb = M->shm[b];
+    float pa[2][3], pb[2][3];
+    int nct = 1;
+    bool gdeep = false;
+    if (kind == 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { pa[0][k] = Wa.c[k]; pb[0][k] = Wb.c[k]; }
+    } else if (kind == 1) {
+      const bool a_sph = M->shkind[a] == 0;
+      const ShapeW& Wc = a_sph ? Wb : Wa;
+      const ShapeW& Ws = a_sph ? Wa : Wb;
+      const float hl = M->shsize[a_sph ? b : a][1];
+      const float ax[3] = {Wc.R[2], Wc.R[5], Wc.R[8]};
+      float e0[3], e1[3], q3[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { e0[k] = Wc.c[k] - hl * ax[k]; e1[k] = Wc.c[k] + hl * ax[k]; }
+      seg_closest_pt(Ws.c, e0, e1, q3);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        pa[0][k] = a_sph ? Ws.c[k] : q3[k];
+        pb[0][k] = a_sph ? q3[k] : Ws.c[k];
+      }
+    } else if (kind == 2) {
+      const float ha = M->shsize[a][1], hb = M->shsize[b][1];
+      float p1[3], q1[3], p2[3], q2[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float axa = Wa.R[3 * k + 2], axb = Wb.R[3 * k + 2];
+        p1[k] = Wa.c[k] - ha * axa; q1[k] = Wa.c[k] + ha * axa;
+        p2[k] = Wb.c[k] - hb * axb; q2[k] = Wb.c[k] + hb * axb;
+      }
+      float s, t, den, aa, ee;
+      seg_seg(p1, q1, p2, q2, s, t, den, aa, ee);
+      bool two = false;
+      float lo = 0.f, hi = 0.f;
+      if (aa > 1e-12f && ee > 1e-12f && den <= 1e-4f * aa * ee) {
+        float d1[3], w0[3], w1[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { d1[k] = q1[k] - p1[k]; w0[k] = p2[k] - p1[k]; w1[k] = q2[k] - p1[k]; }
+        const float s0 = dot3f(w0, d1) / aa, s1 = dot3f(w1, d1) / aa;
+        lo = fminf(s0, s1);
+        hi = fmaxf(s0, s1);
+        lo = lo < 0.f ? 0.f : lo;
+        hi = hi > 1.f ? 1.f : hi;
+        two = hi - lo > 1e-3f;
+      }
+      if (two) {
+        nct = 2;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const float sc2 = c == 0 ? lo : hi;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) pa[c][k] = p1[k] + sc2 * (q1[k] - p1[k]);
+          seg_closest_pt(pa[c], p2, q2, pb[c]);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { pa[0][k] = p1[k] + s * (q1[k] - p1[k]); pb[0][k] = p2[k] + t * (q2[k] - p2[k]); }
+      }
+    } else {
+      const float dist = gjk_cores(M, a, b, Wa, Wb, pa[0], pb[0]);
+      if (!(dist > 1e-9f)) {
+        gdeep = true;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { pa[0][k] = Wa.sc[k]; pb[0][k] = Wb.sc[k]; }
+      } else {
+        // the contact point: the centroid of the smaller of the two support features facing each other (a
+        // face's, not GJK's arbitrary point of it), kept at the cores' distance
+        const float inv = 1.f / dist;
+        const float nn[3] = {(pa[0][0] - pb[0][0]) * inv, (pa[0][1] - pb[0][1]) * inv, (pa[0][2] - pb[0][2]) * inv};
+        const float mn[3] = {-nn[0], -nn[1], -nn[2]};
+        float ca[3], cb[3];
+        const float ea = core_feature(M, a, Wa, mn, ca);
+        const float eb = core_feature(M, b, Wb, nn, cb);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          if (ea <= eb) { pa[0][k] = ca[k]; pb[0][k] = ca[k] - dist * nn[k]; }
+          else { pb[0][k] = cb[k]; pa[0][k] = cb[k] + dist * nn[k]; }
+        }
+      }
+    }
+    for (int c = 0; c < nct; ++c) {
+      if (n >= T::NPK) break;
+      float nn[3] = {pa[c][0] - pb[c][0], pa[c][1] - pb[c][1], pa[c][2] - pb[c][2]};
+      float dist = sqrtf(dot3f(nn, nn));
+      if (!(dist > 1e-9f)) {
+        float f[3] = {Wa.sc[0] - Wb.sc[0], Wa.sc[1] - Wb.sc[1], Wa.sc[2] - Wb.sc[2]};
+        float l = sqrtf(dot3f(f, f));
+        if (!(l > 1e-9f)) { f[0] = 0.f; f[1] = 0.f; f[2] = 1.f; l = 1.f; }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) nn[k] = f[k] / l;
+        dist = 0.f;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) nn[k] /= dist;
+      }
+      const float sep = gdeep ? -(ra + rb) : dist - ra - rb;
+      if (!(sep < off)) continue;
+      float* o = pool + PE * n * LB;
+      float t1[3], t2[3];
+      gs_terrain::tangents(nn, t1, t2);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        o[(kPoolX + k) * LB] = 0.5f * ((pa[c][k] - ra * nn[k]) + (pb[c][k] + rb * nn[k]));
+        o[(kPoolN + k) * LB] = nn[k];
+        o[(kPoolT1 + k) * LB] = t1[k];
+        o[(kPoolT2 + k) * LB] = t2[k];
+      }
+      o[kPoolSep * LB] = sep;
+      o[kPoolMu * LB] = 0.5f * (mu_g[a * N + e] + mu_g[b * N + e]);
+      o[kPoolBA * LB] = (float)M->shbody[a];
+      o[kPoolBB * LB] = (float)M->shbody[b];
+      o[kPoolLA * LB] = (float)M->shlink[a];
+      o[kPoolLB * LB] = (float)M->shlink[b];
+      ++n;
+    }
+  }
+  return n;
+}
+
+}  // namespace

@@ -9,6 +9,7 @@
 #include "gs_internal.h"
 #include "gs_topologies.h"
 #include "gs_math.h"
+#include "gs_pairs.h"
 
 namespace {
 
@@ -32,8 +33,12 @@ GS_HD constexpr bool body_on_path(int kk, int b) {
 // TERR kernels (trimesh terrain) keep each active candidate's contact normal in 3 more slots.
 template <class T, bool TERR = false>
 struct LaneCfg {
-  // contact rows (NSLOT), [TERR: normals 3 NC], separation NC, friction NC, impulses 3 NC
-  static constexpr int SLOTS = T::NSLOT + (TERR ? 3 * T::NC : 0) + 5 * T::NC;
+  // contact rows (NSLOT), [TERR: normals 3 NC], separation NC, friction NC, impulses 3 NC, self-contact pool
+  static constexpr int X_POOL = T::NSLOT + (TERR ? 3 * T::NC : 0) + 5 * T::NC;
+  static constexpr int SLOTS = X_POOL + PoolCfg<T>::FLOATS;
+  // the self-collision prepass keeps the shapes' world data in the contact-row area (rows are written later)
+  static_assert(T::NPK == 0 || kShW * T::NS <= T::NSLOT, "shape world data must fit the contact-row area");
+  static_assert(T::NPK <= GS_MAXPOOL, "self-contact pool exceeds GS_MAXPOOL");
   static constexpr int FIT = (SLOTS * 64 * 4 <= 160 * 1024) ? 64 : (SLOTS * 32 * 4 <= 160 * 1024) ? 32
                            : (SLOTS * 16 * 4 <= 160 * 1024) ? 16 : 8;
   // Below 16 lanes the rows of two workgroups no longer share a CU, and halving again measured
@@ -139,6 +144,47 @@ GS_HD __attribute__((always_inline)) void for_active_shapes(unsigned shb, F&& f)
   }
 }
 
+// Body rotations R_b and positions X_b relative to the root origin, exactly as substep's tree walk forms them.
+template <class T>
+GS_HD void body_poses(const DevModel* __restrict__ M, const EnvState<T>& s, float (&R)[T::NB][9], float (&X)[T::NB][3]) {
+  constexpr int NB = T::NB;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    if (i == 0) {
+      float qn[4];
+      const float inv = gs_rsqrt(s.quat[0] * s.quat[0] + s.quat[1] * s.quat[1] + s.quat[2] * s.quat[2] +
+                                 s.quat[3] * s.quat[3]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) qn[k] = s.quat[k] * inv;
+      quat_to_mat(qn, R[0]);
+      X[0][0] = X[0][1] = X[0][2] = 0.f;
+    } else {
+      const int pa = T::parent[i];
+      float RJ[9], t[3], aw[3];
+      mat3mul(R[pa], M->jR[i], RJ);
+      mat3vec(R[pa], M->jt[i], t);
+      X[i][0] = X[pa][0] + t[0]; X[i][1] = X[pa][1] + t[1]; X[i][2] = X[pa][2] + t[2];
+      mat3vec(RJ, M->jaxis[i], aw);
+      const float qj = s.q[T::bdof[i]];
+      if (T::jkind[i] == 1) {
+        float sn, cs;
+        gs_sincos(qj, &sn, &cs);
+        const float* a = M->jaxis[i];
+        const float C = 1.f - cs;
+        float Rq[9];
+        Rq[0] = cs + a[0] * a[0] * C;        Rq[1] = a[0] * a[1] * C - a[2] * sn; Rq[2] = a[0] * a[2] * C + a[1] * sn;
+        Rq[3] = a[1] * a[0] * C + a[2] * sn; Rq[4] = cs + a[1] * a[1] * C;        Rq[5] = a[1] * a[2] * C - a[0] * sn;
+        Rq[6] = a[2] * a[0] * C - a[1] * sn; Rq[7] = a[2] * a[1] * C + a[0] * sn; Rq[8] = cs + a[2] * a[2] * C;
+        mat3mul(RJ, Rq, R[i]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R[i][k] = RJ[k];
+        X[i][0] += aw[0] * qj; X[i][1] += aw[1] * qj; X[i][2] += aw[2] * qj;
+      }
+    }
+  }
+}
+
 // One substep for one env.  `lds` points at this lane's column of the
 // workgroup's [SLOTS][LB] contact-row staging area (LB = 1 in the host backend: a per-thread
 // scratch row).
@@ -165,6 +211,37 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
   // into hundreds of SGPRs.
   const DevModel* __restrict__ M = gs_opaque(Min);
   const float h = P.h;
+
+  // ---- self-collision prepass: shape world data into the (not yet written) contact-row
+  // area, narrowphase into the self-contact pool; the pool's J rows are filled during the tree walk
+  constexpr int XP = LaneCfg<T, TERR>::X_POOL;
+  constexpr int PE = PoolCfg<T>::PE;
+  float* pool = lds + XP * LB;
+  int npc = 0;
+  if constexpr (T::NPK > 0) {
+    if (P.self_collide) {
+      float Rb[NB][9], Xb[NB][3];
+      body_poses<T>(M, s, Rb, Xb);
+#pragma unroll
+      for (int sh = 0; sh < T::NS; ++sh) {
+        const int b = T::sh_body[sh];
+        float Rs[9], t[3];
+        mat3mul(Rb[b], M->shR[sh], Rs);
+        float* o = lds + kShW * sh * LB;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) o[k * LB] = Rs[k];
+        mat3vec(Rb[b], M->sht[sh], t);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) o[(9 + k) * LB] = Xb[b][k] + t[k];
+        mat3vec(Rb[b], M->shc[sh], t);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) o[(12 + k) * LB] = Xb[b][k] + t[k];
+      }
+      npc = self_contacts<T, LB>(M, P, mu_g, N, e, lds, pool);
+      for (int p = 0; p < npc; ++p)
+        for (int k = 0; k < 3 * NV; ++k) pool[(PE * p + kPoolJ + k) * LB] = 0.f;
+    }
+  }
 
   float nu[NV];
   if (NB6) {
@@ -258,6 +335,32 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
       for (int k = 0; k < 6; ++k) A[i][k] = A[pa][k] + c6[k] * qd;
     }
 
+    // ---- self-contact rows, column of body i's dof: n.(v_A(x) - v_B(x)) takes S_i's velocity at x when i is on
+    // A's path and minus it on B's (a common ancestor's column cancels; the base columns always do)
+    if constexpr (T::NPK > 0) {
+      if (i > 0) {
+        const int col = NB6 + T::bdof[i];
+        for (int p = 0; p < npc; ++p) {
+          float* o = pool + PE * p * LB;
+          const int ba = (int)o[kPoolBA * LB], bb = (int)o[kPoolBB * LB];
+          const float coef = (float)((M->banc[ba] >> i) & 1u) - (float)((M->banc[bb] >> i) & 1u);
+          if (coef != 0.f) {
+            const float x[3] = {o[kPoolX * LB], o[(kPoolX + 1) * LB], o[(kPoolX + 2) * LB]};
+            float vx[3];  // velocity of the point x under S_i: S_lin + S_ang x x
+            cross3(S[i], x, vx);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) vx[k] += S[i][3 + k];
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+              const int dofs = rr == 0 ? kPoolN : (rr == 1 ? kPoolT1 : kPoolT2);
+              const float d[3] = {o[dofs * LB], o[(dofs + 1) * LB], o[(dofs + 2) * LB]};
+              o[(kPoolJ + rr * NV + col) * LB] = coef * dot3f(d, vx);
+            }
+          }
+        }
+      }
+    }
+
     // ---- spatial inertia of body i at O; RNEA force
     {
       float c[3];
@@ -296,9 +399,11 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
     // (exact: every candidate lies inside the sphere), so its candidates are not even transformed --
     // boxes and mesh hulls away from the ground cost one test per shape instead of one per point.
     bool shape_near[T::NS];
+    int hsel[T::NS][4], hn[T::NS];
 #pragma unroll
     for (int sh = 0; sh < T::NS; ++sh) {
       shape_near[sh] = true;
+      hn[sh] = 0;
       if constexpr (!TERR) {
         if (T::sh_body[sh] == i && T::sh_c1[sh] - T::sh_c0[sh] > 1) {
           const float* sc = M->shc[sh];
@@ -306,12 +411,15 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
           shape_near[sh] = P.has_ground && (cz - sc[3] < P.contact_offset);
         }
       }
+      // a convex hull's ground contacts: the 4-point manifold of its vertices (plane only)
+      if (T::shkind[sh] == 4 && T::sh_body[sh] == i && shape_near[sh] && P.has_ground)
+        hn[sh] = hull_ground_select(M, sh, R[i], X[i], s.p[2], P.contact_offset, hsel[sh]);
     }
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      if (T::cbody[c] == i && shape_near[T::cshape[c]]) {
+      if (T::cbody[c] == i && shape_near[T::cshape[c]] && (T::cdyn[c] < 0 || T::cdyn[c] < hn[T::cshape[c]])) {
         float x[3];
-        mat3vec(R[i], M->cpoint[c], x);
+        mat3vec(R[i], T::cdyn[c] < 0 ? M->cpoint[c] : M->hv[hsel[T::cshape[c]][T::cdyn[c] & 3]], x);
         x[0] += X[i][0]; x[1] += X[i][1]; x[2] += X[i][2];
         const float r = M->cradius[c];
         if constexpr (TERR) {
@@ -323,7 +431,9 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
           float smu = P.ground_mu;
           float st, nt[3];
           bool found;
-          if constexpr (QS > 0) {
+          if (T::cdyn[c] >= 0) {  // hull slots: ground plane only
+            found = false;
+          } else if constexpr (QS > 0) {
             found = qres[(5 * c) * QS] != 0.f;
             st = qres[(5 * c + 1) * QS];
             nt[0] = qres[(5 * c + 2) * QS]; nt[1] = qres[(5 * c + 3) * QS]; nt[2] = qres[(5 * c + 4) * QS];
@@ -576,7 +686,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
           }
         }
         slot[(3 * SUP + rr) * LB] = cj;
-        slot[(3 * SUP + 3 + rr) * LB] = 1.f / d;
+        slot[(3 * SUP + 3 + rr) * LB] = d > GS_MIN_RESPONSE ? 1.f / d : 0.f;
       }
     }
   });
@@ -611,6 +721,40 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
       }
       slot[SUP * LB] = lsgn[j] * nuf[leaf];
       slot[(SUP + 1) * LB] = 1.f / d;
+    }
+  }
+
+  // ---------------- self-contact rows: dense J over the tree -> c = J nu_f, scaled Z = (L^-T J^T) D^-1/2, 1/diag
+  if constexpr (T::NPK > 0) {
+    for (int p = 0; p < npc; ++p) {
+      float* o = pool + PE * p * LB;
+#pragma unroll
+      for (int rr = 0; rr < 3; ++rr) {
+        float jv[NV];
+        float cj = 0.f;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          jv[k] = o[(kPoolJ + rr * NV + k) * LB];
+          cj += jv[k] * nuf[k];
+        }
+#pragma unroll
+        for (int kk = 0; kk < NV; ++kk) {
+          const int k = NV - 1 - kk;
+#pragma unroll
+          for (int ai = 0; ai < T::MAXDEP; ++ai)
+            if (ai < T::depth[k]) jv[T::anc[k][ai]] -= Mm[k][T::anc[k][ai]] * jv[k];
+        }
+        float d = 0.f;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          const float zh = jv[k] * sD[k];
+          d += zh * zh;
+          o[(kPoolJ + rr * NV + k) * LB] = zh;
+        }
+        o[(kPoolC + rr) * LB] = cj;
+        o[(kPoolDi + rr) * LB] = d > GS_MIN_RESPONSE ? 1.f / d : 0.f;
+        o[(kPoolLam + rr) * LB] = 0.f;
+      }
     }
   }
 
@@ -675,7 +819,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
               u += z[si] * wt[supp_node<T>(leaf, si)];
             }
           }
-          const float dinv = slot[(3 * SUP + 3 + rr) * LB];
+          const float dinv = slot[(3 * SUP + 3 + rr) * LB];  // 0 below GS_MIN_RESPONSE (no impulse)
           float nl;
           if (rr == 0) {
             nl = fmaxf(lam[0] + (target - u) * dinv, 0.f);
@@ -694,6 +838,36 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
         lamc[(3 * c + 2) * LB] = lam[2];
       }
     });
+    if constexpr (T::NPK > 0) {
+      for (int p = 0; p < npc; ++p) {
+        float* o = pool + PE * p * LB;
+        const float sc = o[kPoolSep * LB];
+        float target = -sc * inv_h;
+        if (sc < 0.f) target = pos_phase ? fminf(target, P.max_depen_vel) : 0.f;
+        float lam[3] = {o[kPoolLam * LB], o[(kPoolLam + 1) * LB], o[(kPoolLam + 2) * LB]};
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) {
+          float u = o[(kPoolC + rr) * LB];
+#pragma unroll
+          for (int k = 0; k < NV; ++k) u += o[(kPoolJ + rr * NV + k) * LB] * wt[k];
+          const float dinv = o[(kPoolDi + rr) * LB];
+          float nl;
+          if (rr == 0) {
+            nl = fmaxf(lam[0] + (target - u) * dinv, 0.f);
+          } else {
+            const float lim = o[kPoolMu * LB] * lam[0];
+            nl = clampf(lam[rr] - u * dinv, -lim, lim);
+          }
+          const float dl = nl - lam[rr];
+          lam[rr] = nl;
+#pragma unroll
+          for (int k = 0; k < NV; ++k) wt[k] += o[(kPoolJ + rr * NV + k) * LB] * dl;
+        }
+        o[kPoolLam * LB] = lam[0];
+        o[(kPoolLam + 1) * LB] = lam[1];
+        o[(kPoolLam + 2) * LB] = lam[2];
+      }
+    }
     if (it == P.pos_iters - 1) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) wpos[k] = wt[k];
@@ -783,6 +957,19 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
       cf_soa[(3 * b + 1) * N + e] = f1;
       cf_soa[(3 * b + 2) * N + e] = f2;
     }
+    if constexpr (T::NPK > 0) {  // self-contacts: +f on link A, -f on link B
+      for (int p = 0; p < npc; ++p) {
+        const float* o = pool + PE * p * LB;
+        const int la = (int)o[kPoolLA * LB], lb = (int)o[kPoolLB * LB];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const float f = (o[kPoolLam * LB] * o[(kPoolN + k) * LB] + o[(kPoolLam + 1) * LB] * o[(kPoolT1 + k) * LB] +
+                           o[(kPoolLam + 2) * LB] * o[(kPoolT2 + k) * LB]) * inv_h;
+          cf_soa[(3 * la + k) * N + e] += f;
+          cf_soa[(3 * lb + k) * N + e] -= f;
+        }
+      }
+    }
   }
   if constexpr (T::SENS) if (sens_soa && M->nsens > 0) {
     // force sensors on leaf bodies (topologies compiled with T::SENS): the wrench through the parent joint,
@@ -844,6 +1031,24 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
             for (int k = 0; k < 3; ++k) { f[k] -= n[k]; f[3 + k] -= fc[k]; }
           }
         }
+        if constexpr (T::NPK > 0) {
+          for (int p = 0; p < npc; ++p) {
+            const float* o = pool + PE * p * LB;
+            const int ba = (int)o[kPoolBA * LB], bbd = (int)o[kPoolBB * LB];
+            if (ba != b && bbd != b) continue;
+            const float sg = ba == b ? inv_h : -inv_h;
+            float fc[3], x[3], n3[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+              fc[k] = sg * (o[kPoolLam * LB] * o[(kPoolN + k) * LB] + o[(kPoolLam + 1) * LB] * o[(kPoolT1 + k) * LB] +
+                            o[(kPoolLam + 2) * LB] * o[(kPoolT2 + k) * LB]);
+              x[k] = o[(kPoolX + k) * LB];
+            }
+            cross3(x, fc, n3);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) { f[k] -= n3[k]; f[3 + k] -= fc[k]; }
+          }
+        }
         // torque about the body origin, then body axes
         float xf[3], tq[3];
         cross3(X[b], &f[3], xf);
@@ -872,47 +1077,14 @@ GS_HD void com_velocity(const DevModel* __restrict__ M, const EnvState<T>& s, fl
 }
 
 // World centres of env state s's contact candidates, exactly as substep's tree walk forms them
-// (cw = p + R_b cpoint + X_b), written to out[(4 * c + k) * stride] with the radius as k = 3.
+// (cw = p + R_b cpoint + X_b), written to out[(4 * c + k) * stride] with the radius as k = 3.  (A hull's
+// dynamic candidates take no terrain-mesh contact: their query result is not read.)
 template <class T>
 GS_HD void candidate_centres(const DevModel* __restrict__ Min, const EnvState<T>& s, float* out, int stride) {
   constexpr int NB = T::NB, NC = T::NC;
   const DevModel* __restrict__ M = gs_opaque(Min);
   float R[NB][9], X[NB][3];
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    if (i == 0) {
-      float qn[4];
-      const float inv = gs_rsqrt(s.quat[0] * s.quat[0] + s.quat[1] * s.quat[1] + s.quat[2] * s.quat[2] +
-                                 s.quat[3] * s.quat[3]);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) qn[k] = s.quat[k] * inv;
-      quat_to_mat(qn, R[0]);
-      X[0][0] = X[0][1] = X[0][2] = 0.f;
-    } else {
-      const int pa = T::parent[i];
-      float RJ[9], t[3], aw[3];
-      mat3mul(R[pa], M->jR[i], RJ);
-      mat3vec(R[pa], M->jt[i], t);
-      X[i][0] = X[pa][0] + t[0]; X[i][1] = X[pa][1] + t[1]; X[i][2] = X[pa][2] + t[2];
-      mat3vec(RJ, M->jaxis[i], aw);
-      const float qj = s.q[T::bdof[i]];
-      if (T::jkind[i] == 1) {
-        float sn, cs;
-        gs_sincos(qj, &sn, &cs);
-        const float* a = M->jaxis[i];
-        const float C = 1.f - cs;
-        float Rq[9];
-        Rq[0] = cs + a[0] * a[0] * C;        Rq[1] = a[0] * a[1] * C - a[2] * sn; Rq[2] = a[0] * a[2] * C + a[1] * sn;
-        Rq[3] = a[1] * a[0] * C + a[2] * sn; Rq[4] = cs + a[1] * a[1] * C;        Rq[5] = a[1] * a[2] * C - a[0] * sn;
-        Rq[6] = a[2] * a[0] * C - a[1] * sn; Rq[7] = a[2] * a[1] * C + a[0] * sn; Rq[8] = cs + a[2] * a[2] * C;
-        mat3mul(RJ, Rq, R[i]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) R[i][k] = RJ[k];
-        X[i][0] += aw[0] * qj; X[i][1] += aw[1] * qj; X[i][2] += aw[2] * qj;
-      }
-    }
-  }
+  body_poses<T>(M, s, R, X);
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int b = T::cbody[c];

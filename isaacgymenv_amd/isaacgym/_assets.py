@@ -22,9 +22,15 @@ Collision geometry is reduced to *contact candidates* for the plane contact
 generator in the kernels: a sphere is one point with radius r, a capsule is its
 two segment end points with radius r, a box is its 8 corners with radius 0, and a
 triangle-mesh (STL) collision shape is its convex hull -- Isaac Gym's default
-treatment of a mesh collider (vhacd off) -- reduced to the hull's support points
-in 14 directions (the 6 axes and the 8 cube diagonals; a box gives back its 8
-corners) with radius 0.
+treatment of a mesh collider (vhacd off) -- with ALL hull vertices kept: against
+the ground it has HULL_SLOTS dynamic contact slots filled every substep from the
+hull vertices within contact_offset (deepest first, then the 4-point manifold
+reduction of DESIGN.md 3.3), so its lowest point is exact at any orientation.
+
+Self-collision (filter 0 actors, anymal_terrain.py:282, useful_hound.py:421): every
+pair of shapes on two links that are neither the same dynamic body nor joined by a
+joint (PhysX filters parent-child link pairs of an articulation) is a potential
+contact pair (:meth:`Articulation.self_collision_pairs`).
 """
 from __future__ import annotations
 
@@ -41,9 +47,13 @@ import numpy as np
 JOINT_FIXED, JOINT_REVOLUTE, JOINT_PRISMATIC, JOINT_FREE = 0, 1, 2, 3
 SHAPE_SPHERE, SHAPE_CAPSULE, SHAPE_BOX, SHAPE_CYLINDER, SHAPE_CONVEX = 0, 1, 2, 3, 4
 
-# support directions of a convex mesh collider's contact points: the 6 axes and the 8 cube diagonals
-_HULL_DIRS = np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1]] +
-                      [[sx, sy, sz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)], dtype=np.float64)
+# ground contact slots of a convex hull (dynamic 4-point manifold over its vertices)
+HULL_SLOTS = 4
+# pair narrowphase kinds: closed forms for sphere/capsule pairs, GJK on margin-rounded cores
+PAIR_SS, PAIR_SC, PAIR_CC, PAIR_GJK = 0, 1, 2, 3
+# self-contact slots per env (the pool the solver fills in pair order), per articulation size
+def pair_pool_size(num_pairs: int) -> int:
+    return 0 if num_pairs == 0 else (4 if num_pairs <= 64 else 8)
 
 
 def read_stl(path: str) -> np.ndarray:
@@ -62,15 +72,13 @@ def read_stl(path: str) -> np.ndarray:
     return np.array(pts, dtype=np.float64)
 
 
-def hull_support_points(vertices: np.ndarray) -> np.ndarray:
-    """The convex hull's support points along _HULL_DIRS (a linear function's maximum over a mesh is
-    attained at a hull vertex, so no hull construction is needed), duplicates removed, in direction order."""
-    idx = []
-    for d in _HULL_DIRS:
-        i = int(np.argmax(vertices @ d))
-        if not any(np.allclose(vertices[i], vertices[j], atol=1e-9) for j in idx):
-            idx.append(i)
-    return vertices[idx]
+def convex_hull_vertices(vertices: np.ndarray) -> np.ndarray:
+    """Every vertex of the mesh's convex hull (qhull through scipy), duplicates merged, in the order of
+    their first occurrence in the mesh."""
+    from scipy.spatial import ConvexHull
+    _, first = np.unique(np.round(vertices, 12), axis=0, return_index=True)
+    uniq = vertices[np.sort(first)]
+    return uniq[np.sort(ConvexHull(uniq).vertices)]
 
 
 def _mesh_file(urdf_dir: str, filename: str) -> Optional[str]:
@@ -303,7 +311,7 @@ def parse_urdf(path: str) -> RawModel:
                 mp = _mesh_file(os.path.dirname(os.path.abspath(path)), fn)
                 scale = np.array(_floats(me.get("scale"), 3, 1.0))
                 try:
-                    pts = hull_support_points(read_stl(mp) * scale) if mp and mp.lower().endswith(".stl") else None
+                    pts = convex_hull_vertices(read_stl(mp) * scale) if mp and mp.lower().endswith(".stl") else None
                 except ValueError:
                     pts = None
                 if pts is None:
@@ -434,10 +442,85 @@ class Articulation:
         for bi, b in enumerate(self.bodies):
             for s in b.shapes:
                 link = self.shape_links[s_index] if self.shape_links is not None else bi
-                n = (len(s.size) // 3 if s.kind == SHAPE_CONVEX else
+                n = (HULL_SLOTS if s.kind == SHAPE_CONVEX else
                      {SHAPE_SPHERE: 1, SHAPE_CAPSULE: 2, SHAPE_CYLINDER: 2, SHAPE_BOX: 8}[s.kind])
                 out += [link] * n
                 s_index += 1
+        return out
+
+    def shape_links_all(self) -> List[int]:
+        """Reported link of every shape (shape order)."""
+        out, s_index = [], 0
+        for bi, b in enumerate(self.bodies):
+            for _ in b.shapes:
+                out.append(self.shape_links[s_index] if self.shape_links is not None else bi)
+                s_index += 1
+        return out
+
+    def shape_table(self) -> List[dict]:
+        """Every collision shape in the solver's terms (body frame), shape order:
+        kind (0 sphere, 1 capsule, 2 box, 3 cylinder, 4 convex hull), body, link,
+        pose (R, t), size (sphere [r]; capsule / cylinder [r, half length]; box half extents), margin (the
+        core radius of the pair narrowphase: sphere / capsule radius; boxes, cylinders and hulls are rounded
+        by m = min(0.01, a quarter of their smallest half extent)), bounding sphere (centre, radius) and,
+        for hulls, the vertices (body frame) with the factor f that moves each toward the vertex centroid
+        by the margin (core vertex = c + f (v - c))."""
+        out, links = [], self.shape_links_all()
+        s_index = 0
+        for bi, b in enumerate(self.bodies):
+            for s in b.shapes:
+                d = dict(body=bi, link=links[s_index], R=s.pose.R.copy(), t=s.pose.t.copy(), verts=None, f=None)
+                if s.kind == SHAPE_SPHERE:
+                    r = float(s.size[0])
+                    d.update(kind=0, size=[r, 0.0, 0.0], margin=r, centre=s.pose.t.copy(), radius=r)
+                elif s.kind == SHAPE_CAPSULE:
+                    r, length = (float(v) for v in s.size)
+                    d.update(kind=1, size=[r, 0.5 * length, 0.0], margin=r, centre=s.pose.t.copy(),
+                             radius=0.5 * length + r)
+                elif s.kind == SHAPE_CYLINDER:  # (replace_cylinder_with_capsule=False): flat-ended
+                    r, length = (float(v) for v in s.size)
+                    d.update(kind=3, size=[r, 0.5 * length, 0.0], margin=min(0.01, 0.25 * min(r, 0.5 * length)),
+                             centre=s.pose.t.copy(), radius=float(np.hypot(r, 0.5 * length)))
+                elif s.kind == SHAPE_BOX:
+                    h = [0.5 * float(v) for v in s.size]
+                    d.update(kind=2, size=h, margin=min(0.01, 0.25 * min(h)), centre=s.pose.t.copy(),
+                             radius=float(np.linalg.norm(h)))
+                else:
+                    v = np.array([s.pose.apply(p) for p in np.asarray(s.size, dtype=np.float64).reshape(-1, 3)])
+                    c = v.mean(0)
+                    dist = np.linalg.norm(v - c, axis=1)
+                    half = 0.5 * (v.max(0) - v.min(0))
+                    m = min(0.01, 0.25 * float(half.min()))
+                    d.update(kind=4, size=[0.0, 0.0, 0.0], margin=m, centre=c, radius=float(dist.max()),
+                             R=np.eye(3), t=np.zeros(3), verts=v, f=np.where(dist > m, 1.0 - m / np.maximum(dist, 1e-12), 0.0))
+                out.append(d)
+                s_index += 1
+        return out
+
+    def self_collision_pairs(self) -> List[tuple]:
+        """(shape a, shape b, kind, contact slots) for every shape pair a < b on links that may collide:
+        not welded into the same dynamic body and not joined by a joint (parent-child links).  kind:
+        PAIR_SS / PAIR_SC (sphere first or second) / PAIR_CC (2 slots: a parallel pair contacts at both
+        ends of its overlap) / PAIR_GJK (any pair with a box, a flat-ended cylinder or a hull).
+        (A cylinder's GROUND contacts stay its two end points with the radius, as before.)"""
+        tab = self.shape_table()
+        lt = self.link_table()
+        lpar = [l.parent for l in lt]
+        out = []
+        for a in range(len(tab)):
+            for b in range(a + 1, len(tab)):
+                la, lb = tab[a]["link"], tab[b]["link"]
+                if tab[a]["body"] == tab[b]["body"] or la == lb or lpar[la] == lb or lpar[lb] == la:
+                    continue
+                ka, kb = tab[a]["kind"], tab[b]["kind"]
+                if ka == 0 and kb == 0:
+                    out.append((a, b, PAIR_SS, 1))
+                elif {ka, kb} == {0, 1}:
+                    out.append((a, b, PAIR_SC, 1))
+                elif ka == 1 and kb == 1:
+                    out.append((a, b, PAIR_CC, 2))
+                else:
+                    out.append((a, b, PAIR_GJK, 1))
         return out
 
     def dof_names(self):
@@ -460,32 +543,36 @@ class Articulation:
         return out
 
     def contact_candidates(self):
-        """(body, local point, radius, shape index) for every plane-contact candidate.
+        """(body, local point, radius, shape index, hull slot) for every plane-contact candidate.
 
         Candidate order = body order, then shape order, then point order (this is
-        the Gauss-Seidel order of the contact solver)."""
+        the Gauss-Seidel order of the contact solver).  A convex hull has HULL_SLOTS
+        dynamic candidates (hull slot 0..3; their point is chosen every substep from
+        the hull's vertices, the stored point is the vertex centroid); every other
+        candidate has hull slot -1."""
         out = []
         s_index = 0
         for bi, b in enumerate(self.bodies):
             for s in b.shapes:
                 if s.kind == SHAPE_SPHERE:
-                    out.append((bi, s.pose.t.copy(), s.size[0], s_index))
+                    out.append((bi, s.pose.t.copy(), s.size[0], s_index, -1))
                 elif s.kind in (SHAPE_CAPSULE, SHAPE_CYLINDER):
                     r, length = s.size
                     half = 0.5 * length
                     # URDF cylinders/capsules run along the local z axis of their origin frame
                     ax = s.pose.R @ np.array([0.0, 0.0, 1.0])
-                    out.append((bi, s.pose.t - half * ax, r, s_index))
-                    out.append((bi, s.pose.t + half * ax, r, s_index))
+                    out.append((bi, s.pose.t - half * ax, r, s_index, -1))
+                    out.append((bi, s.pose.t + half * ax, r, s_index, -1))
                 elif s.kind == SHAPE_BOX:
                     hx, hy, hz = (0.5 * v for v in s.size)
                     for sx in (-1, 1):
                         for sy in (-1, 1):
                             for sz in (-1, 1):
-                                out.append((bi, s.pose.apply([sx * hx, sy * hy, sz * hz]), 0.0, s_index))
+                                out.append((bi, s.pose.apply([sx * hx, sy * hy, sz * hz]), 0.0, s_index, -1))
                 elif s.kind == SHAPE_CONVEX:
-                    for p in np.asarray(s.size, dtype=np.float64).reshape(-1, 3):
-                        out.append((bi, s.pose.apply(p), 0.0, s_index))
+                    v = np.array([s.pose.apply(p) for p in np.asarray(s.size, dtype=np.float64).reshape(-1, 3)])
+                    for k in range(HULL_SLOTS):
+                        out.append((bi, v.mean(0), 0.0, s_index, k))
                 s_index += 1
         return out
 

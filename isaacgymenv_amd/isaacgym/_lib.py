@@ -23,7 +23,12 @@ class GsModelDesc(C.Structure):
                                   "com", "inertia", "cand_body", "cand_point", "cand_radius", "cand_shape",
                                   "dof_effort", "dof_velocity", "dof_armature", "dof_lower", "dof_upper",
                                   "dof_has_limits")] + [
-        ("num_links", C.c_int32)] + [(n, C.c_void_p) for n in ("cand_link", "link_body", "link_pose", "link_com")]
+        ("num_links", C.c_int32)] + [(n, C.c_void_p) for n in ("cand_link", "link_body", "link_pose", "link_com")] + [
+        (n, C.c_void_p) for n in ("cand_dyn", "shape_kind", "shape_body", "shape_link", "shape_pose", "shape_size",
+                                  "shape_margin", "shape_sphere")] + [
+        ("num_hull_verts", C.c_int32), ("hull_verts", C.c_void_p), ("shape_hv0", C.c_void_p),
+        ("shape_hv1", C.c_void_p), ("num_pairs", C.c_int32), ("pair_a", C.c_void_p), ("pair_b", C.c_void_p),
+        ("pair_kind", C.c_void_p), ("pair_pool", C.c_int32)]
 
 
 class GsSimParams(C.Structure):
@@ -80,6 +85,7 @@ def lib():
             "gs_sim_bind_force_sensors": (i, [vp, vp]),
             "gs_sim_set_dof_drives": (i, [vp, vp, vp, vp]),
             "gs_sim_bind_dof_targets": (i, [vp, vp, vp]),
+            "gs_sim_set_self_collision": (i, [vp, i]),
             "gs_sim_refresh_force_sensor": (i, [vp, vp, vp]),
             "gs_sim_add_triangle_mesh": (i, [vp, vp, C.c_int64, vp, C.c_int64, vp, d, d, d]),
             "gs_debug_terrain_query": (i, [vp, vp, vp, i, vp, vp]),
@@ -104,7 +110,7 @@ EXPORTED_SYMBOLS = [
     "gs_sim_kernel_variant", "gs_sim_enable_timing", "gs_sim_last_kernel_ms", "gs_debug_phase_cycles",
     "gs_sim_set_force_sensors", "gs_sim_bind_force_sensors", "gs_sim_refresh_force_sensor",
     "gs_sim_add_triangle_mesh", "gs_debug_terrain_query", "gs_sim_refresh_rigid_body", "gs_sim_refresh_jacobian",
-    "gs_sim_refresh_mass_matrix", "gs_sim_set_dof_drives", "gs_sim_bind_dof_targets",
+    "gs_sim_refresh_mass_matrix", "gs_sim_set_dof_drives", "gs_sim_bind_dof_targets", "gs_sim_set_self_collision",
 ]
 
 
@@ -124,8 +130,17 @@ def model_desc(flat: dict):
              ("dof_armature", "armature", np.float64), ("dof_lower", "lower", np.float64),
              ("dof_upper", "upper", np.float64), ("dof_has_limits", "has_limits", np.int32),
              ("cand_link", "clink", np.int32), ("link_body", "lbody", np.int32),
-             ("link_pose", "lpose", np.float64), ("link_com", "lcom", np.float64)]
+             ("link_pose", "lpose", np.float64), ("link_com", "lcom", np.float64),
+             ("cand_dyn", "cdyn", np.int32), ("shape_kind", "shkind", np.int32), ("shape_body", "shbody", np.int32),
+             ("shape_link", "shlink", np.int32), ("shape_pose", "shpose", np.float64),
+             ("shape_size", "shsize", np.float64), ("shape_margin", "shmargin", np.float64),
+             ("shape_sphere", "shsphere", np.float64), ("hull_verts", "hverts", np.float64),
+             ("shape_hv0", "shv0", np.int32), ("shape_hv1", "shv1", np.int32), ("pair_a", "pair_a", np.int32),
+             ("pair_b", "pair_b", np.int32), ("pair_kind", "pair_kind", np.int32)]
     m.num_links = flat["nr"]
+    m.num_hull_verts = len(flat["hverts"])
+    m.num_pairs = int(flat["npair"])
+    m.pair_pool = int(flat["npool"])
     for field, key, dt in pairs:
         a = np.ascontiguousarray(flat[key], dtype=dt)
         if a.size == 0:

@@ -11,12 +11,18 @@ The same flat arrays feed the product library (``gs_sim_set_model`` in
 * reported links (the tensor API's rigid bodies): ``nr``, ``clink[nc]`` (link whose net contact
   force a candidate adds to), ``lbody[nr]`` (dynamic body), ``lpose[nr][12]`` (link frame in the
   body frame, R row-major then t), ``lcom[nr][3]`` (link COM, link frame), ``lmass[nr]``
+* ``cdyn[nc]``: hull slot of a convex hull's dynamic ground candidate (0..3), -1 for fixed points
+* shapes (``Articulation.shape_table``): ``shkind``, ``shbody``, ``shlink`` [ns]; ``shpose[ns][12]`` (body
+  frame); ``shsize[ns][3]``; ``shmargin[ns]``; ``shsphere[ns][4]`` (bounding sphere, body frame);
+  hull vertices ``hverts[nhv][4]`` (body frame xyz, core factor f) with ``shv0``/``shv1`` [ns] ranges
+* self-collision pairs (``Articulation.self_collision_pairs``): ``npair``, ``pair_a``, ``pair_b``,
+  ``pair_kind`` [npair]; ``npool`` self-contact slots per env
 """
 from __future__ import annotations
 
 import numpy as np
 
-from ._assets import Articulation, JOINT_FREE, JOINT_FIXED
+from ._assets import Articulation, JOINT_FREE, JOINT_FIXED, pair_pool_size
 
 
 def flatten(art: Articulation, armature: float | None = None) -> dict:
@@ -47,6 +53,7 @@ def flatten(art: Articulation, armature: float | None = None) -> dict:
     cpoint = np.array([c[1] for c in cands], dtype=np.float64).reshape(nc, 3)
     cradius = np.array([c[2] for c in cands], dtype=np.float64).reshape(nc)
     cshape = np.array([c[3] for c in cands], dtype=np.int32).reshape(nc)
+    cdyn = np.array([c[4] for c in cands], dtype=np.int32).reshape(nc)
     clinks = art.candidate_links()
     if art.fixed_base:
         clinks = [l for l, c in zip(clinks, art.contact_candidates()) if c[0] != 0]
@@ -58,6 +65,18 @@ def flatten(art: Articulation, armature: float | None = None) -> dict:
         lpose[i, :9] = l.pose.R.reshape(-1)
         lpose[i, 9:] = l.pose.t
     arm = art.options.get("armature", 0.0) if armature is None else armature
+    tab = art.shape_table()
+    ns = len(tab)
+    shpose = np.zeros((ns, 12))
+    hv, shv0, shv1 = [], [], []
+    for i, d in enumerate(tab):
+        shpose[i, :9] = d["R"].reshape(-1)
+        shpose[i, 9:] = d["t"]
+        shv0.append(len(hv))
+        if d["verts"] is not None:
+            hv += [list(v) + [float(f)] for v, f in zip(d["verts"], d["f"])]
+        shv1.append(len(hv))
+    pairs = art.self_collision_pairs() if not art.fixed_base else []
     return dict(
         nb=nb, nd=nd, nc=nc, ns=art.num_shapes, fixed_base=int(art.fixed_base),
         parent=parent, jkind=jkind, bdof=bdof, jorigin=jorigin, jaxis=jaxis, mass=mass, com=com,
@@ -72,6 +91,20 @@ def flatten(art: Articulation, armature: float | None = None) -> dict:
         nr=nr, clink=clink, lbody=np.array([l.body for l in links], dtype=np.int32), lpose=lpose,
         lcom=np.array([l.com for l in links], dtype=np.float64).reshape(nr, 3),
         lmass=np.array([l.mass for l in links], dtype=np.float64),
+        cdyn=cdyn,
+        shkind=np.array([d["kind"] for d in tab], dtype=np.int32).reshape(ns),
+        shbody=np.array([d["body"] for d in tab], dtype=np.int32).reshape(ns),
+        shlink=np.array([d["link"] for d in tab], dtype=np.int32).reshape(ns),
+        shpose=shpose, shsize=np.array([d["size"] for d in tab], dtype=np.float64).reshape(ns, 3),
+        shmargin=np.array([d["margin"] for d in tab], dtype=np.float64).reshape(ns),
+        shsphere=np.array([list(d["centre"]) + [d["radius"]] for d in tab], dtype=np.float64).reshape(ns, 4),
+        hverts=np.array(hv, dtype=np.float64).reshape(len(hv), 4),
+        shv0=np.array(shv0, dtype=np.int32).reshape(ns), shv1=np.array(shv1, dtype=np.int32).reshape(ns),
+        npair=len(pairs),
+        pair_a=np.array([p[0] for p in pairs], dtype=np.int32).reshape(len(pairs)),
+        pair_b=np.array([p[1] for p in pairs], dtype=np.int32).reshape(len(pairs)),
+        pair_kind=np.array([p[2] for p in pairs], dtype=np.int32).reshape(len(pairs)),
+        npool=pair_pool_size(len(pairs)),
     )
 
 

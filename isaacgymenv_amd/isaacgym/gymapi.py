@@ -383,6 +383,13 @@ class Sim:
             _lib.check(L.gs_sim_add_triangle_mesh(self.handle, v.ctypes.data, v.size // 3, t.ctypes.data, t.size // 3,
                                                   tpa, smu, dmu, rest), "gs_sim_add_triangle_mesh")
         _lib.check(L.gs_sim_set_model(self.handle, desc), "gs_sim_set_model")
+        # collision filter 0: Isaac Gym collides the actor's own shapes
+        filters = {a.filter == 0 for e in self.envs for a in e.actors}
+        if len(filters) > 1:
+            raise NotImplementedError("actors with and without self-collision (collision filter 0) in one sim "
+                                      "(DESIGN.md section 6)")
+        self.self_collide = bool(filters.pop()) and int(flat["npair"]) > 0
+        _lib.check(L.gs_sim_set_self_collision(self.handle, int(self.self_collide)), "gs_sim_set_self_collision")
         sens = [b for b, _ in self.asset.sensors]
         if sens:
             sb = np.ascontiguousarray(sens, dtype=np.int32)
@@ -727,11 +734,6 @@ class Gym:
         a = Actor(env, asset, pose, name, group, filter)
         env.actors.append(a)
         owner = env.sim
-        if filter == 0 and asset.art.num_bodies > 1 and not getattr(owner, "_warned_self", False):
-            owner._warned_self = True
-            warnings.warn("collision filter 0 enables self-collisions in Isaac Gym; the MI355X solver generates "
-                          "contacts against the ground and the terrain mesh only (DESIGN.md section 6)",
-                          PhysicsDeviationWarning, stacklevel=2)
         if owner.asset is None:
             owner.asset = asset
         elif owner.asset is not asset:

@@ -24,7 +24,11 @@ class OModel(C.Structure):
                                   "cbody", "cpoint", "cradius", "cshape", "effort", "vmax", "armature",
                                   "lower", "upper", "has_limits")] + [
         ("nsens", C.c_int32), ("sens_body", C.c_void_p), ("nr", C.c_int32), ("clink", C.c_void_p),
-        ("dkp", C.c_void_p), ("dkd", C.c_void_p)]
+        ("dkp", C.c_void_p), ("dkd", C.c_void_p)] + [
+        (n, C.c_void_p) for n in ("cdyn", "shkind", "shbody", "shlink", "shpose", "shsize", "shmargin", "shsphere",
+                                  "hverts", "shv0", "shv1")] + [
+        ("npair", C.c_int32), ("pair_a", C.c_void_p), ("pair_b", C.c_void_p), ("pair_kind", C.c_void_p),
+        ("npool", C.c_int32), ("self_collide", C.c_int32)]
 
 
 class OParams(C.Structure):
@@ -56,6 +60,11 @@ def _lib(real_bits: int):
         lib.oracle_simulate_targets.restype = C.c_int
         lib.oracle_simulate_targets.argtypes = [C.POINTER(OModel), C.POINTER(OParams), C.c_int] + \
             [C.c_void_p] * 6 + [C.c_int, C.c_void_p, C.c_void_p]
+        lib.oracle_self_contacts.restype = C.c_int
+        lib.oracle_self_contacts.argtypes = [C.POINTER(OModel), C.POINTER(OParams), C.c_int] + [C.c_void_p] * 5
+        lib.oracle_hull_select.restype = C.c_int
+        lib.oracle_hull_select.argtypes = [C.POINTER(OModel), C.POINTER(OParams), C.c_int] + [C.c_void_p] * 2 + \
+            [C.c_double if real_bits == 64 else C.c_float, C.c_void_p]
         lib.oracle_terrain_query.restype = C.c_int
         lib.oracle_terrain_query.argtypes = [C.POINTER(OParams), C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         _LIBS[real_bits] = lib
@@ -65,10 +74,13 @@ def _lib(real_bits: int):
 class OracleSim:
     """Holds the model arrays alive and steps numpy state in place."""
 
-    def __init__(self, flat: dict, params: dict, real_bits: int = 64, sensor_bodies=(), terrain=None, drives=None):
+    def __init__(self, flat: dict, params: dict, real_bits: int = 64, sensor_bodies=(), terrain=None, drives=None,
+                 self_collide=None):
         """terrain: optional dict(vertices float32 [rows*cols, 3] world coordinates, rows, cols, x0, y0,
         hs, friction) -- the heightfield-grid mesh of gym.add_triangle_mesh.
-        drives: optional (kp [nd], kd [nd]) joint-drive gains."""
+        drives: optional (kp [nd], kd [nd]) joint-drive gains.
+        self_collide: the actor's collision filter is 0 (self-collision pairs); None follows
+        flat["self_collide"] (absent: off)."""
         self.flat = flat
         self.real = np.float64 if real_bits == 64 else np.float32
         self.lib = _lib(real_bits)
@@ -77,12 +89,13 @@ class OracleSim:
         for k in ("nb", "nd", "nc", "ns", "fixed_base"):
             setattr(m, k, int(flat[k]))
         m.nr = int(flat.get("nr", flat["nb"]))
-        for k in ("parent", "jkind", "bdof", "cbody", "cshape", "has_limits", "clink"):
+        for k in ("parent", "jkind", "bdof", "cbody", "cshape", "has_limits", "clink", "cdyn", "shkind", "shbody",
+                  "shlink", "shv0", "shv1", "pair_a", "pair_b", "pair_kind"):
             a = np.ascontiguousarray(flat[k], dtype=np.int32)
             keep[k] = a
             setattr(m, k, a.ctypes.data)
         for k in ("jorigin", "jaxis", "mass", "com", "inertia", "cpoint", "cradius", "effort", "vmax", "armature",
-                  "lower", "upper"):
+                  "lower", "upper", "shpose", "shsize", "shmargin", "shsphere", "hverts"):
             a = np.ascontiguousarray(flat[k], dtype=np.float64)
             keep[k] = a
             setattr(m, k, a.ctypes.data)
@@ -92,6 +105,9 @@ class OracleSim:
                 assert a.shape == (int(flat["nd"]),)
                 keep[k] = a
                 setattr(m, k, a.ctypes.data)
+        m.npair = int(flat["npair"])
+        m.npool = int(flat["npool"])
+        m.self_collide = int(bool(flat.get("self_collide", 0) if self_collide is None else self_collide))
         sb = np.ascontiguousarray(list(sensor_bodies) or [0], dtype=np.int32)
         keep["sens_body"] = sb
         m.nsens = len(sensor_bodies)
@@ -132,6 +148,31 @@ class OracleSim:
                                          out.ctypes.data) != 0:
             raise RuntimeError("oracle_terrain_query: no terrain")
         return out
+
+    def hull_select(self, shape: int, R, P, rootz: float):
+        """Indices (into flat["hverts"]) of hull shape `shape`'s ground contact vertices for body pose R, P
+        (relative to the root origin) and root height rootz (test hook)."""
+        Ra = np.ascontiguousarray(R, dtype=self.real).reshape(9)
+        Pa = np.ascontiguousarray(P, dtype=self.real).reshape(3)
+        sel = np.zeros(4, dtype=np.int32)
+        n = self.lib.oracle_hull_select(C.byref(self.model), C.byref(self.params), shape, Ra.ctypes.data,
+                                        Pa.ctypes.data, rootz, sel.ctypes.data)
+        if n < 0:
+            raise RuntimeError("oracle_hull_select: not a hull shape")
+        return sel[:n].copy()
+
+    def self_contacts(self, root, dof, mu):
+        """The self-contact pool of each env's state (test hook): (contacts [n, npool, 10] = x xyz, n xyz,
+        separation, friction, body a, body b; counts [n])."""
+        n = root.shape[0]
+        npool = max(1, int(self.model.npool))
+        out = np.zeros((n, npool, 10), dtype=self.real)
+        cnt = np.zeros(n, dtype=np.int32)
+        args = [np.ascontiguousarray(a, dtype=self.real) for a in (root, dof, mu)]
+        if self.lib.oracle_self_contacts(C.byref(self.model), C.byref(self.params), n, *(a.ctypes.data for a in args),
+                                         out.ctypes.data, cnt.ctypes.data) != 0:
+            raise RuntimeError("oracle_self_contacts failed")
+        return out, cnt
 
     def simulate(self, root, dof, tau, mu, cf=None, num_threads: int = 1, sens=None, pos_targets=None,
                  vel_targets=None) -> None:

@@ -48,6 +48,8 @@ typedef REAL real;
 #define MAXB 32
 #define MAXV 40
 #define MAXC 192
+#define MAXPOOL 16
+#define MIN_RESPONSE 1e-7 /* a contact row whose J M^-1 J^T falls below this takes no impulse */
 
 typedef struct {
     int32_t nb, nd, nc, ns, fixed_base;
@@ -77,6 +79,21 @@ typedef struct {
      * substep), NULL = none: kp (q* - q - h qd) + kd (qd* - qd) with h kd + h^2 kp on M's diagonal */
     const double *dkp;          /* [nd] or NULL */
     const double *dkd;          /* [nd] or NULL */
+    /* ---- convex hulls and self-collision */
+    const int32_t *cdyn;        /* [nc] hull slot (0..3) of a hull's dynamic ground candidate, -1 fixed point */
+    const int32_t *shkind;      /* [ns] 0 sphere 1 capsule 2 box 3 cylinder 4 hull */
+    const int32_t *shbody;      /* [ns] */
+    const int32_t *shlink;      /* [ns] */
+    const double *shpose;       /* [ns][12] body frame R (9) t (3) */
+    const double *shsize;       /* [ns][3] sphere r | capsule r, half length | box half extents */
+    const double *shmargin;     /* [ns] core radius of the pair narrowphase */
+    const double *shsphere;     /* [ns][4] bounding sphere, body frame centre + radius */
+    const double *hverts;       /* [nhv][4] hull vertices, body frame xyz + core factor */
+    const int32_t *shv0, *shv1; /* [ns] hull vertex range */
+    int32_t npair;
+    const int32_t *pair_a, *pair_b, *pair_kind; /* [npair] shape a < shape b; 0 SS 1 SC 2 CC 3 GJK */
+    int32_t npool;              /* self-contact slots per env (pair order, later contacts dropped) */
+    int32_t self_collide;       /* filter-0 actor: self-collision pairs enabled */
 } OModel;
 
 typedef struct {
@@ -222,6 +239,451 @@ static void tangents(const real *n, real *t1, real *t2) {
     const real l = sqrt(l2);
     for (int k = 0; k < 3; ++k) t1[k] = a[k] / l;
     cross3(n, t1, t2);
+}
+
+/* ---------------------------------------------------------------- convex hull vs ground
+ * Vertices of hull shape sh whose height is below contact_offset, reduced to at most 4 contact points:
+ * the deepest; the one farthest from it horizontally; the one spanning the largest horizontal triangle with
+ * those two; the one farthest outside that triangle.  First vertex index wins ties; a step whose best
+ * value is <= 1e-10 ends the selection. */
+static int hull_ground_select(const OModel *m, int sh, const real *R, const real *P, real rootz, real off,
+                              int *sel) {
+    const int v0 = m->shv0[sh], v1 = m->shv1[sh];
+    int n = 0, i0 = -1;
+    real zmin = 1e300;
+#define HV(k, out)                                                           \
+    {                                                                        \
+        real vl[3] = {(real)m->hverts[4 * (k)], (real)m->hverts[4 * (k) + 1], (real)m->hverts[4 * (k) + 2]}; \
+        matvec3(R, vl, out);                                                 \
+        for (int a_ = 0; a_ < 3; ++a_) out[a_] += P[a_];                     \
+        out[2] += rootz;                                                     \
+    }
+    for (int k = v0; k < v1; ++k) { real w[3]; HV(k, w); if (w[2] < zmin) { zmin = w[2]; i0 = k; } }
+    if (i0 < 0 || !(zmin < off)) return 0;
+    real p0[3]; HV(i0, p0);
+    sel[n++] = i0;
+    int i1 = -1; real best = 1e-10;
+    for (int k = v0; k < v1; ++k) {
+        real w[3]; HV(k, w);
+        if (!(w[2] < off)) continue;
+        const real d2 = (w[0] - p0[0]) * (w[0] - p0[0]) + (w[1] - p0[1]) * (w[1] - p0[1]);
+        if (d2 > best) { best = d2; i1 = k; }
+    }
+    if (i1 < 0) return n;
+    real p1[3]; HV(i1, p1);
+    sel[n++] = i1;
+    const real ex = p1[0] - p0[0], ey = p1[1] - p0[1];
+    int i2 = -1; best = 1e-10;
+    for (int k = v0; k < v1; ++k) {
+        real w[3]; HV(k, w);
+        if (!(w[2] < off)) continue;
+        const real a = fabs(ex * (w[1] - p0[1]) - ey * (w[0] - p0[0]));
+        if (a > best) { best = a; i2 = k; }
+    }
+    if (i2 < 0) return n;
+    real p2[3]; HV(i2, p2);
+    sel[n++] = i2;
+    const real sg = (ex * (p2[1] - p0[1]) - ey * (p2[0] - p0[0])) > 0 ? 1 : -1;
+    int i3 = -1; best = 1e-10;
+    for (int k = v0; k < v1; ++k) {
+        real w[3]; HV(k, w);
+        if (!(w[2] < off)) continue;
+        const real e0 = sg * ((p1[0] - p0[0]) * (w[1] - p0[1]) - (p1[1] - p0[1]) * (w[0] - p0[0]));
+        const real e1 = sg * ((p2[0] - p1[0]) * (w[1] - p1[1]) - (p2[1] - p1[1]) * (w[0] - p1[0]));
+        const real e2 = sg * ((p0[0] - p2[0]) * (w[1] - p2[1]) - (p0[1] - p2[1]) * (w[0] - p2[0]));
+        real mn = e0 < e1 ? e0 : e1;
+        mn = mn < e2 ? mn : e2;
+        if (-mn > best) { best = -mn; i3 = k; }
+    }
+#undef HV
+    if (i3 >= 0) sel[n++] = i3;
+    return n;
+}
+
+/* ---------------------------------------------------------------- self-collision */
+typedef struct { real R[9], c[3], sc[3]; } ShapeW; /* world (root-origin-relative) pose + bounding-sphere centre */
+
+/* core support point of shape sh (pose W) in direction d */
+static void core_support(const OModel *m, int sh, const ShapeW *W, const real *Rb, const real *Pb, const real *d,
+                         real *out) {
+    const int kind = m->shkind[sh];
+    const double *sz = m->shsize + 3 * sh;
+    if (kind == 0) { for (int k = 0; k < 3; ++k) out[k] = W->c[k]; return; }
+    if (kind == 1) {
+        const real ax[3] = {W->R[2], W->R[5], W->R[8]};
+        const real s = dot3(ax, d) >= 0 ? sz[1] : -sz[1];
+        for (int k = 0; k < 3; ++k) out[k] = W->c[k] + s * ax[k];
+        return;
+    }
+    if (kind == 3) { /* flat-ended cylinder: rim point of the end disc (core radius r - m, half length h - m) */
+        const real mg = (real)m->shmargin[sh];
+        const real ax[3] = {W->R[2], W->R[5], W->R[8]};
+        const real da = dot3(ax, d);
+        real pp[3] = {d[0] - da * ax[0], d[1] - da * ax[1], d[2] - da * ax[2]};
+        const real lp = sqrt(dot3(pp, pp));
+        const real s = da >= 0 ? sz[1] - mg : -(sz[1] - mg);
+        for (int k = 0; k < 3; ++k) out[k] = W->c[k] + s * ax[k] + (lp > 1e-12 ? (sz[0] - mg) * pp[k] / lp : 0);
+        return;
+    }
+    if (kind == 2) {
+        const real mg = (real)m->shmargin[sh];
+        for (int k = 0; k < 3; ++k) out[k] = W->c[k];
+        for (int i = 0; i < 3; ++i) {
+            const real e[3] = {W->R[i], W->R[3 + i], W->R[6 + i]};
+            const real s = dot3(e, d) >= 0 ? sz[i] - mg : -(sz[i] - mg);
+            for (int k = 0; k < 3; ++k) out[k] += s * e[k];
+        }
+        return;
+    }
+    /* hull: body-frame vertices moved toward the centroid by the margin */
+    real dl[3] = {Rb[0] * d[0] + Rb[3] * d[1] + Rb[6] * d[2], Rb[1] * d[0] + Rb[4] * d[1] + Rb[7] * d[2],
+                  Rb[2] * d[0] + Rb[5] * d[1] + Rb[8] * d[2]};
+    const double *cc = m->shsphere + 4 * sh;
+    real best = -1e300, bv[3] = {0, 0, 0};
+    for (int k = m->shv0[sh]; k < m->shv1[sh]; ++k) {
+        const double *v = m->hverts + 4 * k;
+        const real f = (real)v[3];
+        const real p[3] = {cc[0] + f * (v[0] - cc[0]), cc[1] + f * (v[1] - cc[1]), cc[2] + f * (v[2] - cc[2])};
+        const real t = dot3(p, dl);
+        if (t > best) { best = t; bv[0] = p[0]; bv[1] = p[1]; bv[2] = p[2]; }
+    }
+    matvec3(Rb, bv, out);
+    for (int k = 0; k < 3; ++k) out[k] += Pb[k];
+}
+
+/* Centroid of shape sh's core support feature in direction d: the core points within FEATURE_EPS of the
+ * support plane (box corners, hull vertices; a cylinder's end disc, side line or rim point; a capsule's
+ * segment or end; a sphere's centre).  Returns the feature's extent (largest distance of its points from the
+ * centroid), 0 for a single point. */
+#define FEATURE_EPS 2e-3
+static real core_feature(const OModel *m, int sh, const ShapeW *W, const real *Rb, const real *Pb, const real *d,
+                         real *cen) {
+    const int kind = m->shkind[sh];
+    const double *sz = m->shsize + 3 * sh;
+    const real mg = (real)m->shmargin[sh];
+    if (kind == 0) { for (int k = 0; k < 3; ++k) cen[k] = W->c[k]; return 0; }
+    if (kind == 1 || kind == 3) {
+        const real ax[3] = {W->R[2], W->R[5], W->R[8]};
+        const real hl = kind == 1 ? (real)sz[1] : (real)sz[1] - mg, rr = kind == 1 ? 0 : (real)sz[0] - mg;
+        const real da = dot3(ax, d);
+        real pp[3] = {d[0] - da * ax[0], d[1] - da * ax[1], d[2] - da * ax[2]};
+        const real lp = sqrt(dot3(pp, pp));
+        /* the two ends' support heights differ by 2 hl |da|: both ends within the band -> the side segment */
+        const int side = 2 * hl * fabs(da) <= FEATURE_EPS;
+        /* a cylinder end disc faces d when the rim spread 2 rr lp stays within the band */
+        const int disc = kind == 3 && 2 * rr * lp <= FEATURE_EPS;
+        const real s = side ? 0 : (da >= 0 ? hl : -hl);
+        for (int k = 0; k < 3; ++k) cen[k] = W->c[k] + s * ax[k] + (disc || !(lp > 1e-12) ? 0 : rr * pp[k] / lp);
+        return side ? hl : (disc ? rr : 0);
+    }
+    if (kind == 2) {
+        real hmax = -1e300, pts[8][3];
+        for (int c = 0; c < 8; ++c) {
+            for (int k = 0; k < 3; ++k) pts[c][k] = W->c[k];
+            for (int i = 0; i < 3; ++i) {
+                const real sg = (c >> i & 1) ? 1 : -1;
+                for (int k = 0; k < 3; ++k) pts[c][k] += sg * ((real)sz[i] - mg) * W->R[3 * k + i];
+            }
+            const real h = dot3(pts[c], d);
+            if (h > hmax) hmax = h;
+        }
+        int n = 0;
+        for (int k = 0; k < 3; ++k) cen[k] = 0;
+        for (int c = 0; c < 8; ++c)
+            if (dot3(pts[c], d) >= hmax - FEATURE_EPS) { for (int k = 0; k < 3; ++k) cen[k] += pts[c][k]; ++n; }
+        for (int k = 0; k < 3; ++k) cen[k] /= n;
+        real ext = 0;
+        for (int c = 0; c < 8; ++c)
+            if (dot3(pts[c], d) >= hmax - FEATURE_EPS) {
+                const real dd[3] = {pts[c][0] - cen[0], pts[c][1] - cen[1], pts[c][2] - cen[2]};
+                const real l = sqrt(dot3(dd, dd));
+                if (l > ext) ext = l;
+            }
+        return ext;
+    }
+    /* hull (body-frame core vertices) */
+    const real dl[3] = {Rb[0] * d[0] + Rb[3] * d[1] + Rb[6] * d[2], Rb[1] * d[0] + Rb[4] * d[1] + Rb[7] * d[2],
+                        Rb[2] * d[0] + Rb[5] * d[1] + Rb[8] * d[2]};
+    const double *cc = m->shsphere + 4 * sh;
+    real hmax = -1e300;
+    for (int k = m->shv0[sh]; k < m->shv1[sh]; ++k) {
+        const double *v = m->hverts + 4 * k;
+        const real f = (real)v[3];
+        const real p[3] = {cc[0] + f * (v[0] - cc[0]), cc[1] + f * (v[1] - cc[1]), cc[2] + f * (v[2] - cc[2])};
+        const real h = dot3(p, dl);
+        if (h > hmax) hmax = h;
+    }
+    real acc[3] = {0, 0, 0};
+    int n = 0;
+    for (int k = m->shv0[sh]; k < m->shv1[sh]; ++k) {
+        const double *v = m->hverts + 4 * k;
+        const real f = (real)v[3];
+        const real p[3] = {cc[0] + f * (v[0] - cc[0]), cc[1] + f * (v[1] - cc[1]), cc[2] + f * (v[2] - cc[2])};
+        if (dot3(p, dl) >= hmax - FEATURE_EPS) { for (int t = 0; t < 3; ++t) acc[t] += p[t]; ++n; }
+    }
+    for (int t = 0; t < 3; ++t) acc[t] /= n;
+    real ext = 0;
+    for (int k = m->shv0[sh]; k < m->shv1[sh]; ++k) {
+        const double *v = m->hverts + 4 * k;
+        const real f = (real)v[3];
+        const real p[3] = {cc[0] + f * (v[0] - cc[0]), cc[1] + f * (v[1] - cc[1]), cc[2] + f * (v[2] - cc[2])};
+        if (dot3(p, dl) >= hmax - FEATURE_EPS) {
+            const real dd[3] = {p[0] - acc[0], p[1] - acc[1], p[2] - acc[2]};
+            const real l = sqrt(dot3(dd, dd));
+            if (l > ext) ext = l;
+        }
+    }
+    matvec3(Rb, acc, cen);
+    for (int t = 0; t < 3; ++t) cen[t] += Pb[t];
+    return ext;
+}
+
+/* closest point of conv(W[0..k)) to the origin: every vertex subset whose affine closest point has positive
+ * barycentrics is a candidate, the nearest wins (first subset on ties); returns the subset mask */
+static int simplex_closest(real W[4][3], int k, real *v, real *lam) {
+    real best = 1e300;
+    int bm = 0;
+    for (int mask = 1; mask < (1 << k); ++mask) {
+        int id[4], n = 0;
+        for (int i = 0; i < k; ++i) if (mask >> i & 1) id[n++] = i;
+        real l[4] = {1, 0, 0, 0}, p[3];
+        if (n == 1) {
+            for (int a = 0; a < 3; ++a) p[a] = W[id[0]][a];
+        } else {
+            real E[3][3], G[3][3], r[3], mu[3];
+            for (int j = 1; j < n; ++j) for (int a = 0; a < 3; ++a) E[j - 1][a] = W[id[j]][a] - W[id[0]][a];
+            const int q = n - 1;
+            for (int i = 0; i < q; ++i) {
+                r[i] = -dot3(W[id[0]], E[i]);
+                for (int j = 0; j < q; ++j) G[i][j] = dot3(E[i], E[j]);
+            }
+            if (q == 1) {
+                if (!(G[0][0] > 1e-18)) continue;
+                mu[0] = r[0] / G[0][0];
+            } else if (q == 2) {
+                const real det = G[0][0] * G[1][1] - G[0][1] * G[1][0];
+                if (!(fabs(det) > 1e-12 * G[0][0] * G[1][1]) || !(det != 0)) continue;
+                mu[0] = (r[0] * G[1][1] - G[0][1] * r[1]) / det;
+                mu[1] = (G[0][0] * r[1] - r[0] * G[1][0]) / det;
+            } else {
+                const real det = G[0][0] * (G[1][1] * G[2][2] - G[1][2] * G[2][1]) -
+                                 G[0][1] * (G[1][0] * G[2][2] - G[1][2] * G[2][0]) +
+                                 G[0][2] * (G[1][0] * G[2][1] - G[1][1] * G[2][0]);
+                if (!(fabs(det) > 1e-12 * G[0][0] * G[1][1] * G[2][2]) || !(det != 0)) continue;
+                for (int c = 0; c < 3; ++c) {
+                    real Gc[3][3];
+                    for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) Gc[i][j] = j == c ? r[i] : G[i][j];
+                    mu[c] = (Gc[0][0] * (Gc[1][1] * Gc[2][2] - Gc[1][2] * Gc[2][1]) -
+                             Gc[0][1] * (Gc[1][0] * Gc[2][2] - Gc[1][2] * Gc[2][0]) +
+                             Gc[0][2] * (Gc[1][0] * Gc[2][1] - Gc[1][1] * Gc[2][0])) / det;
+                }
+            }
+            real l0 = 1;
+            int ok = 1;
+            for (int j = 0; j < q; ++j) { l0 -= mu[j]; l[j + 1] = mu[j]; if (!(mu[j] > 1e-12)) ok = 0; }
+            l[0] = l0;
+            if (!ok || !(l0 > 1e-12)) continue;
+            for (int a = 0; a < 3; ++a) {
+                p[a] = W[id[0]][a];
+                for (int j = 0; j < q; ++j) p[a] += mu[j] * E[j][a];
+            }
+        }
+        const real d2 = dot3(p, p);
+        if (d2 < best) {
+            best = d2;
+            bm = mask;
+            for (int a = 0; a < 3; ++a) v[a] = p[a];
+            for (int i = 0, j = 0; i < k; ++i) lam[i] = (mask >> i & 1) ? l[j++] : 0;
+        }
+    }
+    return bm;
+}
+
+/* GJK distance between the cores of shapes a and b: closest points pa, pb; returns the distance, 0 when
+ * the cores overlap */
+static real gjk_cores(const OModel *m, int sa, int sb, const ShapeW *Wa, const ShapeW *Wb, const real *Ra,
+                      const real *Pa, const real *Rb, const real *Pb, real *pa, real *pb) {
+    real v[3] = {Wa->sc[0] - Wb->sc[0], Wa->sc[1] - Wb->sc[1], Wa->sc[2] - Wb->sc[2]};
+    if (dot3(v, v) < 1e-18) { v[0] = 1; v[1] = 0; v[2] = 0; }
+    real W[4][3], A[4][3], B[4][3], lam[4] = {1, 0, 0, 0};
+    int k = 0;
+    for (int it = 0; it < 32; ++it) {
+        const real nv[3] = {-v[0], -v[1], -v[2]};
+        real a[3], b[3], w[3];
+        core_support(m, sa, Wa, Ra, Pa, nv, a);
+        core_support(m, sb, Wb, Rb, Pb, v, b);
+        for (int t = 0; t < 3; ++t) w[t] = a[t] - b[t];
+        const real vv = dot3(v, v);
+        if (k > 0 && vv - dot3(v, w) <= 1e-10 * vv + 1e-14) break;
+        int dup = 0;
+        for (int i = 0; i < k; ++i) {
+            const real d[3] = {W[i][0] - w[0], W[i][1] - w[1], W[i][2] - w[2]};
+            if (dot3(d, d) < 1e-16) dup = 1;
+        }
+        if (dup) break;
+        for (int t = 0; t < 3; ++t) { W[k][t] = w[t]; A[k][t] = a[t]; B[k][t] = b[t]; }
+        ++k;
+        real l4[4];
+        const int mask = simplex_closest(W, k, v, l4);
+        if (!mask) return 0;
+        int n = 0;
+        for (int i = 0; i < k; ++i)
+            if (mask >> i & 1) {
+                for (int t = 0; t < 3; ++t) { W[n][t] = W[i][t]; A[n][t] = A[i][t]; B[n][t] = B[i][t]; }
+                lam[n++] = l4[i];
+            }
+        k = n;
+        if (k == 4 || dot3(v, v) < 1e-18) return 0;
+    }
+    for (int t = 0; t < 3; ++t) { pa[t] = 0; pb[t] = 0; }
+    for (int i = 0; i < k; ++i)
+        for (int t = 0; t < 3; ++t) { pa[t] += lam[i] * A[i][t]; pb[t] += lam[i] * B[i][t]; }
+    return sqrt(dot3(v, v));
+}
+
+/* closest points of segments p1q1, p2q2 (Ericson): parameters s, t; returns a e - b^2 and a, e */
+static void seg_seg(const real *p1, const real *q1, const real *p2, const real *q2, real *s_, real *t_, real *den_,
+                    real *a_, real *e_) {
+    real d1[3], d2[3], r[3];
+    for (int k = 0; k < 3; ++k) { d1[k] = q1[k] - p1[k]; d2[k] = q2[k] - p2[k]; r[k] = p1[k] - p2[k]; }
+    const real a = dot3(d1, d1), e = dot3(d2, d2), f = dot3(d2, r);
+    real s = 0, t = 0, den = 0;
+    if (a <= 1e-12 && e <= 1e-12) { s = t = 0; }
+    else if (a <= 1e-12) { s = 0; t = f / e; t = t < 0 ? 0 : (t > 1 ? 1 : t); }
+    else {
+        const real c = dot3(d1, r);
+        if (e <= 1e-12) { t = 0; s = -c / a; s = s < 0 ? 0 : (s > 1 ? 1 : s); }
+        else {
+            const real b = dot3(d1, d2);
+            den = a * e - b * b;
+            if (den > 0) { s = (b * f - c * e) / den; s = s < 0 ? 0 : (s > 1 ? 1 : s); }
+            else s = 0;
+            t = (b * s + f) / e;
+            if (t < 0) { t = 0; s = -c / a; s = s < 0 ? 0 : (s > 1 ? 1 : s); }
+            else if (t > 1) { t = 1; s = (b - c) / a; s = s < 0 ? 0 : (s > 1 ? 1 : s); }
+        }
+    }
+    *s_ = s; *t_ = t; *den_ = den; *a_ = a; *e_ = e;
+}
+
+typedef struct { real x[3], n[3], sep, mu; int ba, bb, la, lb; } PairContact;
+
+/* self-contacts of one env, pair order, at most npool: broadphase on the shapes' bounding spheres
+ * (within contact_offset), closed-form sphere / capsule pairs, GJK on margin-rounded cores otherwise */
+static int self_contacts(const OModel *m, const OParams *p, real R[][9], real P[][3], const real *mu_shape,
+                         PairContact *out) {
+    ShapeW W[64];
+    const real off = (real)p->contact_offset;
+    for (int sh = 0; sh < m->ns; ++sh) {
+        const int b = m->shbody[sh];
+        real Rl[9], tl[3], t[3], sc[3];
+        for (int k = 0; k < 9; ++k) Rl[k] = (real)m->shpose[12 * sh + k];
+        for (int k = 0; k < 3; ++k) { tl[k] = (real)m->shpose[12 * sh + 9 + k]; sc[k] = (real)m->shsphere[4 * sh + k]; }
+        matmul3(R[b], Rl, W[sh].R);
+        matvec3(R[b], tl, t);
+        for (int k = 0; k < 3; ++k) W[sh].c[k] = P[b][k] + t[k];
+        matvec3(R[b], sc, t);
+        for (int k = 0; k < 3; ++k) W[sh].sc[k] = P[b][k] + t[k];
+    }
+    int n = 0;
+    for (int q = 0; q < m->npair && n < m->npool; ++q) {
+        const int a = m->pair_a[q], b = m->pair_b[q], kind = m->pair_kind[q];
+        const real d[3] = {W[a].sc[0] - W[b].sc[0], W[a].sc[1] - W[b].sc[1], W[a].sc[2] - W[b].sc[2]};
+        const real rr = (real)m->shsphere[4 * a + 3] + (real)m->shsphere[4 * b + 3] + off;
+        if (!(dot3(d, d) < rr * rr)) continue;
+        const int ba = m->shbody[a], bb = m->shbody[b];
+        const real ra = (real)m->shmargin[a], rb = (real)m->shmargin[b];
+        real pa[2][3], pb[2][3];
+        int nct = 1, gdeep = 0;
+        if (kind == 0) {
+            for (int k = 0; k < 3; ++k) { pa[0][k] = W[a].c[k]; pb[0][k] = W[b].c[k]; }
+        } else if (kind == 1) {
+            const int sa_sph = m->shkind[a] == 0;
+            const int cap = sa_sph ? b : a, sph = sa_sph ? a : b;
+            const real ax[3] = {W[cap].R[2], W[cap].R[5], W[cap].R[8]}, hl = (real)m->shsize[3 * cap + 1];
+            real e0[3], e1[3], q3[3];
+            for (int k = 0; k < 3; ++k) { e0[k] = W[cap].c[k] - hl * ax[k]; e1[k] = W[cap].c[k] + hl * ax[k]; }
+            seg_closest(W[sph].c, e0, e1, q3);
+            for (int k = 0; k < 3; ++k) {
+                (sa_sph ? pa : pb)[0][k] = W[sph].c[k];
+                (sa_sph ? pb : pa)[0][k] = q3[k];
+            }
+        } else if (kind == 2) {
+            const real axa[3] = {W[a].R[2], W[a].R[5], W[a].R[8]}, axb[3] = {W[b].R[2], W[b].R[5], W[b].R[8]};
+            const real ha = (real)m->shsize[3 * a + 1], hb = (real)m->shsize[3 * b + 1];
+            real p1[3], q1[3], p2[3], q2[3];
+            for (int k = 0; k < 3; ++k) {
+                p1[k] = W[a].c[k] - ha * axa[k]; q1[k] = W[a].c[k] + ha * axa[k];
+                p2[k] = W[b].c[k] - hb * axb[k]; q2[k] = W[b].c[k] + hb * axb[k];
+            }
+            real s, t, den, aa, ee;
+            seg_seg(p1, q1, p2, q2, &s, &t, &den, &aa, &ee);
+            int two = 0;
+            real lo = 0, hi = 0;
+            if (aa > 1e-12 && ee > 1e-12 && den <= 1e-4 * aa * ee) {
+                /* parallel: both ends of the overlap of B's projection onto A */
+                real d1[3], w0[3], w1[3];
+                for (int k = 0; k < 3; ++k) { d1[k] = q1[k] - p1[k]; w0[k] = p2[k] - p1[k]; w1[k] = q2[k] - p1[k]; }
+                const real s0 = dot3(w0, d1) / aa, s1 = dot3(w1, d1) / aa;
+                lo = s0 < s1 ? s0 : s1; hi = s0 < s1 ? s1 : s0;
+                lo = lo < 0 ? 0 : lo; hi = hi > 1 ? 1 : hi;
+                two = hi - lo > 1e-3;
+            }
+            if (two) {
+                nct = 2;
+                for (int c = 0; c < 2; ++c) {
+                    const real sc2 = c == 0 ? lo : hi;
+                    for (int k = 0; k < 3; ++k) pa[c][k] = p1[k] + sc2 * (q1[k] - p1[k]);
+                    seg_closest(pa[c], p2, q2, pb[c]);
+                }
+            } else {
+                for (int k = 0; k < 3; ++k) { pa[0][k] = p1[k] + s * (q1[k] - p1[k]); pb[0][k] = p2[k] + t * (q2[k] - p2[k]); }
+            }
+        } else {
+            const real dist = gjk_cores(m, a, b, &W[a], &W[b], R[ba], P[ba], R[bb], P[bb], pa[0], pb[0]);
+            if (!(dist > 1e-9)) { /* overlapping cores: centres' direction, depth = both margins */
+                gdeep = 1;
+                for (int k = 0; k < 3; ++k) { pa[0][k] = W[a].sc[k]; pb[0][k] = W[b].sc[k]; }
+            } else {
+                /* the contact point: the centroid of the smaller of the two support features facing each
+                 * other (a face's, not GJK's arbitrary point of it), kept at the cores' distance */
+                const real nn[3] = {(pa[0][0] - pb[0][0]) / dist, (pa[0][1] - pb[0][1]) / dist, (pa[0][2] - pb[0][2]) / dist};
+                const real mn[3] = {-nn[0], -nn[1], -nn[2]};
+                real ca[3], cb[3];
+                const real ea = core_feature(m, a, &W[a], R[ba], P[ba], mn, ca);
+                const real eb = core_feature(m, b, &W[b], R[bb], P[bb], nn, cb);
+                for (int k = 0; k < 3; ++k) {
+                    if (ea <= eb) { pa[0][k] = ca[k]; pb[0][k] = ca[k] - dist * nn[k]; }
+                    else { pb[0][k] = cb[k]; pa[0][k] = cb[k] + dist * nn[k]; }
+                }
+            }
+        }
+        for (int c = 0; c < nct && n < m->npool; ++c) {
+            real nn[3] = {pa[c][0] - pb[c][0], pa[c][1] - pb[c][1], pa[c][2] - pb[c][2]};
+            real dist = sqrt(dot3(nn, nn));
+            const int deep = gdeep;
+            if (!(dist > 1e-9)) {
+                real f[3] = {W[a].sc[0] - W[b].sc[0], W[a].sc[1] - W[b].sc[1], W[a].sc[2] - W[b].sc[2]};
+                real l = sqrt(dot3(f, f));
+                if (!(l > 1e-9)) { f[0] = 0; f[1] = 0; f[2] = 1; l = 1; }
+                for (int k = 0; k < 3; ++k) nn[k] = f[k] / l;
+                dist = 0;
+            } else {
+                for (int k = 0; k < 3; ++k) nn[k] /= dist;
+            }
+            const real sep = deep ? -(ra + rb) : dist - ra - rb;
+            if (!(sep < off)) continue;
+            PairContact *o = &out[n++];
+            for (int k = 0; k < 3; ++k) {
+                o->n[k] = nn[k];
+                o->x[k] = 0.5 * ((pa[c][k] - ra * nn[k]) + (pb[c][k] + rb * nn[k]));
+            }
+            o->sep = sep;
+            o->mu = (real)0.5 * (mu_shape[a] + mu_shape[b]);
+            o->ba = ba; o->bb = bb; o->la = m->shlink[a]; o->lb = m->shlink[b];
+        }
+    }
+    return n;
 }
 
 /* spatial inertia at O (world axes): m, h = m c, I_O (3x3) */
@@ -476,17 +938,31 @@ static void env_substep(const OModel *m, const OParams *p, real h,
     const int ncap = m->nc > 0 ? m->nc : 1;
     real J[3 * ncap * MAXV], W[3 * ncap * MAXV];
     real Dr[3 * MAXC];
+    int hsel[64][4], hn[64];
+    if (m->shkind) {
+        for (int sh = 0; sh < m->ns; ++sh) {
+            hn[sh] = 0; /* a hull's ground slots: the plane only (no terrain-mesh contact) */
+            if (m->shkind[sh] == 4 && p->has_ground)
+                hn[sh] = hull_ground_select(m, sh, R[m->shbody[sh]], P[m->shbody[sh]], root[2], (real)p->contact_offset,
+                                            hsel[sh]);
+        }
+    }
     if (p->has_ground || p->has_terrain) {
         for (int c = 0; c < m->nc; ++c) {
             const int b = m->cbody[c];
             real xl[3], x[3];
             for (int k = 0; k < 3; ++k) xl[k] = (real)m->cpoint[3 * c + k];
+            if (m->cdyn && m->cdyn[c] >= 0) { /* a hull's ground slot: the selected vertex, if any */
+                const int sh = m->cshape[c], k = m->cdyn[c];
+                if (k >= hn[sh]) continue;
+                for (int a = 0; a < 3; ++a) xl[a] = (real)m->hverts[4 * hsel[sh][k] + a];
+            }
             matvec3(R[b], xl, x);
             for (int k = 0; k < 3; ++k) x[k] += P[b][k];
             const real r = (real)m->cradius[c];
             real dist = p->has_ground ? root[2] + x[2] - r : 1e300;
             real nrm[3] = {0, 0, 1}, smu = (real)p->ground_friction;
-            if (p->has_terrain) {
+            if (p->has_terrain && !(m->cdyn && m->cdyn[c] >= 0)) {
                 const real cw[3] = {root[0] + x[0], root[1] + x[1], root[2] + x[2]};
                 real st, nt[3];
                 if (terrain_query(p, cw, r, r + (real)p->contact_offset, &st, nt) && st < dist) {
@@ -532,11 +1008,45 @@ static void env_substep(const OModel *m, const OParams *p, real h,
         }
     }
 
+    /* ---- self-contacts: rows J = n.(v_A(x) - v_B(x)) over both bodies' paths (the common
+     * ancestors' columns cancel), solved after the ground contacts in pool order */
+    PairContact pc[MAXPOOL];
+    int npc = 0;
+    real PJ[3 * MAXPOOL * MAXV], PW[3 * MAXPOOL * MAXV], PD[3 * MAXPOOL];
+    if (m->self_collide && m->npair > 0 && m->npool > 0) {
+        npc = self_contacts(m, p, R, P, mu_shape, pc);
+        for (int a = 0; a < npc; ++a) {
+            real dir[3][3];
+            for (int k = 0; k < 3; ++k) dir[0][k] = pc[a].n[k];
+            tangents(pc[a].n, dir[1], dir[2]);
+            for (int rr = 0; rr < 3; ++rr) {
+                real *Jr = PJ + (3 * a + rr) * MAXV, *Wr = PW + (3 * a + rr) * MAXV;
+                for (int k = 0; k < nv; ++k) Jr[k] = 0;
+                for (int side = 0; side < 2; ++side) {
+                    const real sg = side == 0 ? 1 : -1;
+                    for (int i = side == 0 ? pc[a].ba : pc[a].bb; i > 0; i = m->parent[i]) {
+                        real t[3];
+                        cross3(S[i], pc[a].x, t);
+                        const int di = nbase + m->bdof[i];
+                        Jr[di] += sg * (dir[rr][0] * (S[i][3] + t[0]) + dir[rr][1] * (S[i][4] + t[1]) +
+                                        dir[rr][2] * (S[i][5] + t[2]));
+                    }
+                }
+                chol_solve(M, nv, Jr, Wr);
+                real d = 0;
+                for (int k = 0; k < nv; ++k) d += Jr[k] * Wr[k];
+                PD[3 * a + rr] = d;
+            }
+        }
+    }
+
     /* ---- sequential impulses (joint space) */
     real v[MAXV], lam[3 * MAXC], nupos[MAXV], laml[MAXV];
     memcpy(v, nuf, sizeof(real) * nv);
     for (int k = 0; k < 3 * nact; ++k) lam[k] = 0;
     for (int k = 0; k < nlim; ++k) laml[k] = 0;
+    real plam[3 * MAXPOOL];
+    for (int k = 0; k < 3 * npc; ++k) plam[k] = 0;
     const int iters = p->pos_iters + p->vel_iters;
     for (int it = 0; it < iters; ++it) {
         const int pos_phase = it < p->pos_iters;
@@ -566,7 +1076,7 @@ static void env_substep(const OModel *m, const OParams *p, real h,
                 if (s >= 0) target = -s / h;
                 else if (pos_phase) { target = -s / h; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
                 else target = 0;
-                real ln = lam[r] + (target - u) / Dr[r];
+                real ln = Dr[r] > MIN_RESPONSE ? lam[r] + (target - u) / Dr[r] : lam[r];
                 if (ln < 0) ln = 0;
                 const real dl = ln - lam[r];
                 lam[r] = ln;
@@ -578,11 +1088,37 @@ static void env_substep(const OModel *m, const OParams *p, real h,
                 real u = 0;
                 for (int k = 0; k < nv; ++k) u += Jr[k] * v[k];
                 const real lim = cmu[a] * lam[3 * a];
-                real lt = lam[r] - u / Dr[r];
+                real lt = Dr[r] > MIN_RESPONSE ? lam[r] - u / Dr[r] : lam[r];
                 if (lt > lim) lt = lim;
                 if (lt < -lim) lt = -lim;
                 const real dl = lt - lam[r];
                 lam[r] = lt;
+                for (int k = 0; k < nv; ++k) v[k] += Wr[k] * dl;
+            }
+        }
+        for (int a = 0; a < npc; ++a) {
+            const real s = pc[a].sep;
+            for (int t = 0; t < 3; ++t) {
+                const int r = 3 * a + t;
+                const real *Jr = PJ + r * MAXV, *Wr = PW + r * MAXV;
+                real u = 0;
+                for (int k = 0; k < nv; ++k) u += Jr[k] * v[k];
+                real ln;
+                if (t == 0) {
+                    real target;
+                    if (s >= 0) target = -s / h;
+                    else if (pos_phase) { target = -s / h; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
+                    else target = 0;
+                    ln = PD[r] > MIN_RESPONSE ? plam[r] + (target - u) / PD[r] : plam[r];
+                    if (ln < 0) ln = 0;
+                } else {
+                    const real lim = pc[a].mu * plam[3 * a];
+                    ln = PD[r] > MIN_RESPONSE ? plam[r] - u / PD[r] : plam[r];
+                    if (ln > lim) ln = lim;
+                    if (ln < -lim) ln = -lim;
+                }
+                const real dl = ln - plam[r];
+                plam[r] = ln;
                 for (int k = 0; k < nv; ++k) v[k] += Wr[k] * dl;
             }
         }
@@ -627,6 +1163,15 @@ static void env_substep(const OModel *m, const OParams *p, real h,
             for (int k = 0; k < 3; ++k)
                 cforce[3 * b + k] += (lam[3 * a] * cn[a][k] + lam[3 * a + 1] * t1[k] + lam[3 * a + 2] * t2[k]) / h;
         }
+        for (int a = 0; a < npc; ++a) {
+            real t1[3], t2[3];
+            tangents(pc[a].n, t1, t2);
+            for (int k = 0; k < 3; ++k) {
+                const real f = (plam[3 * a] * pc[a].n[k] + plam[3 * a + 1] * t1[k] + plam[3 * a + 2] * t2[k]) / h;
+                cforce[3 * pc[a].la + k] += f;
+                cforce[3 * pc[a].lb + k] -= f;
+            }
+        }
     }
     if (sens && m->nsens > 0) {
         /* joint-reaction wrench of each sensor (leaf) body: I a + v x* I v - f_contact, with the
@@ -664,6 +1209,16 @@ static void env_substep(const OModel *m, const OParams *p, real h,
                 cross3(x, fc, n);
                 for (int k = 0; k < 3; ++k) { f[k] -= n[k]; f[3 + k] -= fc[k]; }
             }
+            for (int a = 0; a < npc; ++a) {
+                if (pc[a].ba != b && pc[a].bb != b) continue;
+                const real sg = pc[a].ba == b ? 1 : -1;
+                real t1[3], t2[3], fc[3], n3[3];
+                tangents(pc[a].n, t1, t2);
+                for (int k = 0; k < 3; ++k)
+                    fc[k] = sg * (plam[3 * a] * pc[a].n[k] + plam[3 * a + 1] * t1[k] + plam[3 * a + 2] * t2[k]) / h;
+                cross3(pc[a].x, fc, n3);
+                for (int k = 0; k < 3; ++k) { f[k] -= n3[k]; f[3 + k] -= fc[k]; }
+            }
             real xf[3], tq[3];
             cross3(P[b], f + 3, xf);
             for (int k = 0; k < 3; ++k) tq[k] = f[k] - xf[k];
@@ -699,7 +1254,7 @@ int oracle_simulate_targets(const OModel *m, const OParams *p, int n_envs, real 
                             const real *tau, const real *mu, real *cf, real *sens, int num_threads,
                             const real *ptgt, const real *vtgt)
 {
-    if (m->nb > MAXB || m->nd + 6 > MAXV || m->nc > MAXC || m->nr < m->nb) return -1;
+    if (m->nb > MAXB || m->nd + 6 > MAXV || m->nc > MAXC || m->nr < m->nb || m->ns > 64 || m->npool > MAXPOOL) return -1;
     const real h = (real)(p->dt / (p->substeps > 0 ? p->substeps : 1));
 #ifdef _OPENMP
     if (num_threads > 0) omp_set_num_threads(num_threads);
@@ -729,4 +1284,50 @@ int oracle_terrain_query(const OParams *p, int n, const real *centres, const rea
         out[5 * t] = f; out[5 * t + 1] = sep; out[5 * t + 2] = nn[0]; out[5 * t + 3] = nn[1]; out[5 * t + 4] = nn[2];
     }
     return 0;
+}
+
+/* test hook: the self-contacts of each env's current state, out[n][npool][10] =
+ * (x xyz, n xyz, separation, friction, body a, body b); returns per-env counts in cnt[n] */
+int oracle_self_contacts(const OModel *m, const OParams *p, int n_envs, const real *root, const real *dof,
+                         const real *mu, real *out, int32_t *cnt) {
+    if (m->npool > MAXPOOL || m->ns > 64) return -1;
+    for (int e = 0; e < n_envs; ++e) {
+        const real *rt = root + 13 * e, *dq = dof + 2 * m->nd * e;
+        real R[MAXB][9], P[MAXB][3];
+        real q4[4] = {rt[3], rt[4], rt[5], rt[6]};
+        const real qn = 1 / sqrt(q4[0] * q4[0] + q4[1] * q4[1] + q4[2] * q4[2] + q4[3] * q4[3]);
+        for (int k = 0; k < 4; ++k) q4[k] *= qn;
+        quat_to_mat(q4, R[0]);
+        P[0][0] = P[0][1] = P[0][2] = 0;
+        for (int i = 1; i < m->nb; ++i) {
+            const int pa = m->parent[i];
+            real Ro[9], to[3], RJ[9], a[3], tt[3];
+            for (int k = 0; k < 9; ++k) Ro[k] = (real)m->jorigin[12 * i + k];
+            for (int k = 0; k < 3; ++k) { to[k] = (real)m->jorigin[12 * i + 9 + k]; a[k] = (real)m->jaxis[3 * i + k]; }
+            matmul3(R[pa], Ro, RJ);
+            matvec3(R[pa], to, tt);
+            for (int k = 0; k < 3; ++k) P[i][k] = P[pa][k] + tt[k];
+            const real qj = dq[2 * m->bdof[i]];
+            if (m->jkind[i] == 1) { real Rq[9]; axis_angle(a, qj, Rq); matmul3(RJ, Rq, R[i]); }
+            else { real aw[3]; matvec3(RJ, a, aw); memcpy(R[i], RJ, sizeof(RJ)); for (int k = 0; k < 3; ++k) P[i][k] += aw[k] * qj; }
+        }
+        PairContact pc[MAXPOOL];
+        const int k = self_contacts(m, p, R, P, mu + m->ns * e, pc);
+        cnt[e] = k;
+        for (int a = 0; a < k; ++a) {
+            real *o = out + ((size_t)e * m->npool + a) * 10;
+            for (int t = 0; t < 3; ++t) { o[t] = pc[a].x[t]; o[3 + t] = pc[a].n[t]; }
+            o[6] = pc[a].sep; o[7] = pc[a].mu; o[8] = pc[a].ba; o[9] = pc[a].bb;
+        }
+    }
+    return 0;
+}
+
+/* test hook: the ground contact vertices of hull shape sh for body pose (R row-major, P, root height) */
+int oracle_hull_select(const OModel *m, const OParams *p, int sh, const real *R, const real *P, real rootz, int32_t *sel) {
+    if (!m->shkind || sh < 0 || sh >= m->ns || m->shkind[sh] != 4) return -1;
+    int s4[4];
+    const int n = hull_ground_select(m, sh, R, P, rootz, (real)p->contact_offset, s4);
+    for (int k = 0; k < n; ++k) sel[k] = s4[k];
+    return n;
 }

@@ -62,9 +62,10 @@ def test_cartpole_model():
     assert all(b != 0 for b in flat["cbody"])  # no candidates on the welded root
 
 
-def test_stl_collision_meshes_collide_as_convex_hull_support_points(tmp_path):
-    """Hound.urdf:508-661: the arm's STL collision meshes become convex-hull contact points,
-    the support points of the hull in 14 directions (a box mesh gives back its 8 corners)."""
+def test_stl_collision_meshes_collide_as_convex_hulls(tmp_path):
+    """Hound.urdf:508-661: the arm's STL collision meshes become convex hulls with ALL hull
+    vertices kept (a box mesh gives back its 8 corners, interior and duplicate vertices are dropped); each
+    hull has HULL_SLOTS dynamic ground candidates."""
     import numpy as np
     from isaacgymenv_amd.isaacgym import _assets as A
     from isaacgymenv_amd.isaacgym._model import flatten
@@ -75,9 +76,12 @@ def test_stl_collision_meshes_collide_as_convex_hull_support_points(tmp_path):
     rec = np.zeros(len(faces), dtype=np.dtype([("n", "<f4", 3), ("v", "<f4", (3, 3)), ("a", "<u2")]))
     rec["v"] = corners[np.array(faces)]
     (tmp_path / "cube.stl").write_bytes(b"\0" * 80 + len(faces).to_bytes(4, "little") + rec.tobytes())
-    pts = A.hull_support_points(A.read_stl(str(tmp_path / "cube.stl")) * 0.001)
+    pts = A.convex_hull_vertices(A.read_stl(str(tmp_path / "cube.stl")) * 0.001)
     assert pts.shape == (8, 3)
     assert {tuple(np.round(p * 1000).astype(int)) for p in pts} == {tuple(c) for c in corners.astype(int)}
+    # an interior point is not a hull vertex
+    inner = np.concatenate([A.read_stl(str(tmp_path / "cube.stl")), [[1.0, 2.0, 3.0]]])
+    assert len(A.convex_hull_vertices(inner)) == 8
     # the packed Hound model: every arm link collides through its hull, none is dropped
     raw = A.load_raw("/nonexistent", "urdf/UsefulHound/urdf/Hound.urdf")
     arm = ["link1", "link2", "link3", "link4", "link5", "link6", "end_link"]
@@ -86,7 +90,8 @@ def test_stl_collision_meshes_collide_as_convex_hull_support_points(tmp_path):
         assert [s.kind for s in raw.links[n].shapes] == [A.SHAPE_CONVEX]
     art = A.build_articulation(raw, dict(collapse_fixed_joints=False, replace_cylinder_with_capsule=False))
     flat = flatten(art)
-    assert flat["nc"] == 84 + 91 and flat["ns"] == 24
+    assert flat["nc"] == 84 + 7 * A.HULL_SLOTS and flat["ns"] == 24
+    assert len(flat["hverts"]) > 1000 and (flat["cdyn"] >= 0).sum() == 7 * A.HULL_SLOTS
     names = art.link_names()
     cand_links = [names[i] for i in art.candidate_links()]
-    assert sum(n in arm for n in cand_links) == 91
+    assert sum(n in arm for n in cand_links) == 7 * A.HULL_SLOTS

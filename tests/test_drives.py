@@ -99,10 +99,10 @@ def _hound_vs_oracle(host):
     gym, sim, (g_root, g_dof) = _run_sim("hound", n, H.HOUND_PARAMS, root, dof, tau, mu, ptgt, vtgt, drives, 1, host)
     o_root, o_dof = _run_oracle(flat, H.HOUND_PARAMS, root, dof, tau, mu, ptgt, vtgt, drives, 1)
     assert np.all(np.isfinite(g_root)) and np.all(np.isfinite(g_dof))
-    H.assert_mostly_close(g_root[:, 0:7], o_root[:, 0:7], atol=2e-5, max_frac=5e-3, what="root pose")
-    H.assert_mostly_close(g_dof[:, :, 0], o_dof[:, :, 0], atol=2e-5, max_frac=5e-3, what="dof pos")
-    H.assert_mostly_close(g_root[:, 7:13], o_root[:, 7:13], atol=5e-3, rtol=5e-3, max_frac=5e-3, what="root vel")
-    H.assert_mostly_close(g_dof[:, :, 1], o_dof[:, :, 1], atol=5e-3, rtol=5e-3, max_frac=5e-3, what="dof vel")
+    H.assert_mostly_close(g_root[:, 0:7], o_root[:, 0:7], atol=2e-5, max_frac=H.HOUND_SELF_FRAC, what="root pose")
+    H.assert_mostly_close(g_dof[:, :, 0], o_dof[:, :, 0], atol=2e-5, max_frac=H.HOUND_SELF_FRAC, what="dof pos")
+    H.assert_mostly_close(g_root[:, 7:13], o_root[:, 7:13], atol=5e-3, rtol=5e-3, max_frac=H.HOUND_SELF_FRAC, what="root vel")
+    H.assert_mostly_close(g_dof[:, :, 1], o_dof[:, :, 1], atol=5e-3, rtol=5e-3, max_frac=H.HOUND_SELF_FRAC, what="dof vel")
     return sim
 
 

@@ -91,7 +91,9 @@ def topo_tables(flat: dict) -> dict:
     sh_body = [cbody[sh_c0[s]] if sh_c0[s] < nc else 0 for s in range(ns)]
     jkind = [int(k) for k in flat["jkind"]]
     team = team_tables(flat, parent, bdof, nbase)
-    return dict(NR=int(flat["nr"]), clink=[int(l) for l in flat["clink"]], TEAM=team, NB=nb, ND=nd, NC=nc, NS=int(flat["ns"]), FIXED=fixed, NBASE=nbase, NV=nv, MAXDEP=maxdep,
+    return dict(cdyn=[int(k) for k in flat["cdyn"]], shkind=[int(k) for k in flat["shkind"]],
+                NPK=int(flat["npool"]), NPAIR=int(flat["npair"]),
+                NR=int(flat["nr"]), clink=[int(l) for l in flat["clink"]], TEAM=team, NB=nb, ND=nd, NC=nc, NS=int(flat["ns"]), FIXED=fixed, NBASE=nbase, NV=nv, MAXDEP=maxdep,
                 parent=parent, bdof=bdof, jkind=jkind, dpar=dpar, depth=[len(a) for a in anc],
                 anc=[a + [-1] * (maxdep - len(a)) for a in anc], bgdof=bgdof, cbody=cbody, cleaf=cleaf,
                 csupp=csupp, cslot=cslot, NSLOT=max(off, 1), gbody=gbody, cshape=cshape, subend=subend,
@@ -174,12 +176,12 @@ def emit() -> str:
         sig = topology_signature(flat)
         lines.append(f"struct Topo_{name} {{")
         lines.append(f'  static constexpr const char* kName = "{name}";')
-        for k in ("NB", "NR", "ND", "NC", "NS", "FIXED", "NBASE", "NV", "MAXDEP", "NSLOT"):
+        for k in ("NB", "NR", "ND", "NC", "NS", "FIXED", "NBASE", "NV", "MAXDEP", "NSLOT", "NPAIR", "NPK"):
             lines.append(f"  static constexpr int {k} = {t[k]};")
         for k, n in (("parent", "NB"), ("bdof", "NB"), ("jkind", "NB"), ("bgdof", "NB"), ("subend", "NB"), ("dpar", "NV"),
                      ("depth", "NV"), ("gbody", "NV"), ("cbody", "NC"), ("clink", "NC"), ("cshape", "NC"), ("cleaf", "NC"), ("csupp", "NC"), ("cslot", "NC"),
                      ("lleaf", "ND"), ("lsupp", "ND"), ("lslot", "ND"), ("sh_c0", "NS"), ("sh_c1", "NS"),
-                     ("sh_body", "NS")):
+                     ("sh_body", "NS"), ("cdyn", "NC"), ("shkind", "NS")):
             vals = t[k] if len(t[k]) else [0]
             dim = n if len(t[k]) else "1"
             lines.append(f"  static constexpr int {k}[{dim}] = {carr(vals)};")
