@@ -467,6 +467,7 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   s->model_sim_fn = sim_fn;
   s->model_pd_fn = pd_fn;
   s->model_variant = variant;
+  s->team_pairs = variant == 2;  // the lane-team kernel solves self-contacts (gs_team.hip team_self_contacts)
   s->nr = m->num_links;
   s->nv = (m->fixed_base ? 0 : 6) + m->num_dofs;
   s->nb = m->num_bodies;

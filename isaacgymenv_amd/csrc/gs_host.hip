@@ -14,6 +14,9 @@
 #include <mutex>
 #include <thread>
 #include <vector>
+#include <limits>
+#include <algorithm>
+#include <cstdlib>
 
 #include "gs_solver.h"
 #include "gs_kinematics.h"
@@ -96,11 +99,19 @@ int host_pool_threads(const HostPool* p) { return p ? (int)p->workers.size() + 1
 
 namespace {
 
-// per-thread contact-row scratch (the LDS column of one lane in the kernels, LB = 1)
+// per-thread contact-row scratch (the LDS column of one lane in the kernels, LB = 1).  GS_HOST_POISON=1 fills it
+// with NaN before every env (debug: any read of a slot the env did not write shows up as a NaN state)
+bool host_poison() {
+  static const bool on = [] { const char* v = std::getenv("GS_HOST_POISON"); return v && v[0] == '1'; }();
+  return on;
+}
 float* scratch(int slots) {
   thread_local std::vector<float> buf;
   if ((int)buf.size() < slots) buf.resize(slots);
   return buf.data();
+}
+void poison(float* lds, int slots) {
+  if (host_poison()) std::fill(lds, lds + slots, std::numeric_limits<float>::quiet_NaN());
 }
 
 template <class T>
@@ -108,12 +119,12 @@ void host_sim(const DevModel* M, const DevParams& P, const SimBuffers& B, const 
   if (P.has_terrain) {
     pool->run(B.N, [&](int b, int e1) {
       float* lds = scratch(LaneCfg<T, true>::SLOTS);
-      for (int e = b; e < e1; ++e) simulate_env<T, true, 1>(M, P, B, tau, e, lds);
+      for (int e = b; e < e1; ++e) { poison(lds, LaneCfg<T, true>::SLOTS); simulate_env<T, true, 1>(M, P, B, tau, e, lds); }
     });
   } else {
     pool->run(B.N, [&](int b, int e1) {
       float* lds = scratch(LaneCfg<T, false>::SLOTS);
-      for (int e = b; e < e1; ++e) simulate_env<T, false, 1>(M, P, B, tau, e, lds);
+      for (int e = b; e < e1; ++e) { poison(lds, LaneCfg<T, false>::SLOTS); simulate_env<T, false, 1>(M, P, B, tau, e, lds); }
     });
   }
 }
@@ -123,12 +134,12 @@ void host_pd(const DevModel* M, const DevParams& P, const SimBuffers& B, const P
   if (P.has_terrain) {
     pool->run(B.N, [&](int b, int e1) {
       float* lds = scratch(LaneCfg<T, true>::SLOTS);
-      for (int e = b; e < e1; ++e) pd_step_env<T, true, 1>(M, P, B, A, e, lds);
+      for (int e = b; e < e1; ++e) { poison(lds, LaneCfg<T, true>::SLOTS); pd_step_env<T, true, 1>(M, P, B, A, e, lds); }
     });
   } else {
     pool->run(B.N, [&](int b, int e1) {
       float* lds = scratch(LaneCfg<T, false>::SLOTS);
-      for (int e = b; e < e1; ++e) pd_step_env<T, false, 1>(M, P, B, A, e, lds);
+      for (int e = b; e < e1; ++e) { poison(lds, LaneCfg<T, false>::SLOTS); pd_step_env<T, false, 1>(M, P, B, A, e, lds); }
     });
   }
 }

@@ -14,8 +14,11 @@
 #define GS_MAXP 512   // self-collision shape pairs per articulation (UsefulHound: 253)
 #define GS_MAXPOOL 8  // self-contact slots per env
 #define GS_WAVE 64
-// a contact row whose J M^-1 J^T falls below this takes no impulse (an overlap no dof can separate)
-#define GS_MIN_RESPONSE 1e-7f
+// a contact row whose J M^-1 J^T falls below this -- an effective mass above 1000 kg, an overlap no dof can
+// separate (UsefulHound's arm pinned on its trunk) -- takes no impulse; the oracle uses the same bound
+#ifndef GS_MIN_RESPONSE
+#define GS_MIN_RESPONSE 1e-3f
+#endif
 
 // Model constants shared by every env, float32, one copy in device memory.
 // Kernels index it with compile-time body / candidate indices from a uniform

@@ -165,6 +165,9 @@ GS_HD void core_support(const DevModel* __restrict__ M, int sh, const ShapeW& W,
 // support plane (box corners, hull vertices; a cylinder's end disc, side line or rim point; a capsule's segment
 // or end; a sphere's centre).  Returns the feature's extent, 0 for a single point (the oracle's core_feature).
 constexpr float kFeatureEps = 2e-3f;
+#ifndef GS_DEEP_SKIP
+#define GS_DEEP_SKIP 1
+#endif
 GS_HD float core_feature(const DevModel* __restrict__ M, int sh, const ShapeW& W, const float* d, float* cen) {
   const int kind = M->shkind[sh];
   const float* sz = M->shsize[sh];
@@ -470,10 +473,11 @@ GS_HD void seg_seg(const float* p1, const float* q1, const float* p2, const floa
 // bounding spheres (within contact_offset), closed-form sphere / capsule pairs, GJK on margin-rounded cores
 // otherwise.  Writes the pool entries' geometry (x relative to the root origin, n from B to A, tangents,
 // separation, friction, bodies, links); returns the count.
-template <class T, int LB>
+// (shape data at stride LB, pool entries at stride LBP with PE floats per entry: the one-env-per-lane solver
+// keeps both in its lane column; the lane team reads a per-team shape table and keeps a shorter entry)
+template <class T, int LB, int LBP = LB, int PE = PoolCfg<T>::PE>
 GS_HD int self_contacts(const DevModel* __restrict__ M, const DevParams& P, const float* __restrict__ mu_g, int N,
                         int e, const float* shw, float* pool) {
-  constexpr int PE = PoolCfg<T>::PE;
   const float off = P.contact_offset;
   int n = 0;
   const int np = M->np;
@@ -584,24 +588,25 @@ GS_HD int self_contacts(const DevModel* __restrict__ M, const DevParams& P, cons
 #pragma unroll
         for (int k = 0; k < 3; ++k) nn[k] /= dist;
       }
+      if (gdeep && GS_DEEP_SKIP) continue;
       const float sep = gdeep ? -(ra + rb) : dist - ra - rb;
       if (!(sep < off)) continue;
-      float* o = pool + PE * n * LB;
+      float* o = pool + PE * n * LBP;
       float t1[3], t2[3];
       gs_terrain::tangents(nn, t1, t2);
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        o[(kPoolX + k) * LB] = 0.5f * ((pa[c][k] - ra * nn[k]) + (pb[c][k] + rb * nn[k]));
-        o[(kPoolN + k) * LB] = nn[k];
-        o[(kPoolT1 + k) * LB] = t1[k];
-        o[(kPoolT2 + k) * LB] = t2[k];
+        o[(kPoolX + k) * LBP] = 0.5f * ((pa[c][k] - ra * nn[k]) + (pb[c][k] + rb * nn[k]));
+        o[(kPoolN + k) * LBP] = nn[k];
+        o[(kPoolT1 + k) * LBP] = t1[k];
+        o[(kPoolT2 + k) * LBP] = t2[k];
       }
-      o[kPoolSep * LB] = sep;
-      o[kPoolMu * LB] = 0.5f * (mu_g[a * N + e] + mu_g[b * N + e]);
-      o[kPoolBA * LB] = (float)M->shbody[a];
-      o[kPoolBB * LB] = (float)M->shbody[b];
-      o[kPoolLA * LB] = (float)M->shlink[a];
-      o[kPoolLB * LB] = (float)M->shlink[b];
+      o[kPoolSep * LBP] = sep;
+      o[kPoolMu * LBP] = 0.5f * (mu_g[a * N + e] + mu_g[b * N + e]);
+      o[kPoolBA * LBP] = (float)M->shbody[a];
+      o[kPoolBB * LBP] = (float)M->shbody[b];
+      o[kPoolLA * LBP] = (float)M->shlink[a];
+      o[kPoolLB * LBP] = (float)M->shlink[b];
       ++n;
     }
   }

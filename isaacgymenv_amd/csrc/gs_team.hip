@@ -18,6 +18,7 @@
 #include "gs_internal.h"
 #include "gs_topologies.h"
 #include "gs_math.h"
+#include "gs_pairs.h"
 
 // Phase profiler (profiling build only, -DGS_PHASE_PROFILE -> libgymsim_prof.so): per-wave
 // s_memtime deltas per solver phase, summed over waves into gs_phase_cycles (gs_capi.hip).
@@ -131,7 +132,14 @@ struct RowSlots {
                        R_MU = R_TV + 1, PER_ROOT = R_MU + 1;
   static constexpr int CHAIN = PER_CONTACT * T::T_CC;
   static constexpr int ROOT = PER_ROOT * (T::T_RC > 0 ? T::T_RC : 1);
-  static constexpr int TOTAL = CHAIN + ROOT;
+  // self-contact pool, replicated in every lane's column of a team: the entry's geometry
+  // (gs_pairs.h kPool* layout), impulses, then per row the lane's 5 components of the distributed Z row
+  // [base 2l, base 2l+1, chain A comp l, chain B comp l, c (lane 3)], 1/G_rr (3), scaled couplings (3),
+  // target/G00 (pos, vel), chains A and B
+  static constexpr int P_Z = kPoolLam + 3, P_DI = P_Z + 15, P_G = P_DI + 3, P_TP = P_G + 3, P_TV = P_TP + 1,
+                       P_CA = P_TV + 1, P_CB = P_CA + 1, PER_POOL = P_CB + 1;
+  static constexpr int POOL = CHAIN + ROOT;
+  static constexpr int TOTAL = POOL + PER_POOL * T::NPK;
   __device__ static constexpr int chain(int j) { return j * PER_CONTACT; }
   __device__ static constexpr int chain_row(int j, int rr) { return j * PER_CONTACT + rr * ZROW; }
   __device__ static constexpr int root(int j) { return CHAIN + j * PER_ROOT; }
@@ -290,13 +298,95 @@ __device__ __forceinline__ float base_jac(const float* xc, int ax, int k) {
   return (ax == k - 3) ? 1.f : 0.f;
 }
 
+// Per-team shape table for the self-collision prepass: [(kShW * sh + f) * TPW + team] (TPW teams per workgroup)
+constexpr int kTeamsPerBlock = kTeamBlock / 4;
+
+// Self-collision prepass of a team: every lane publishes its chain's shapes' bounding-sphere
+// centres (lane 0 also the root's), the lanes split the pair list for the broadphase; a wave with a near pair
+// in any team publishes the shapes' full poses and runs the narrowphase replicated in each lane of the team
+// (gs_pairs.h self_contacts: the same pair order and rules as the one-env-per-lane solver and the oracle).
+// Returns the team's self-contact count (the pool geometry is in the lane's own column).
+template <class T>
+__device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M, const DevParams& P,
+                                                  const float* __restrict__ mu_g, int N, int e, int lc,
+                                                  const float (&R0)[9], const float (&R)[T::T_CL][9],
+                                                  const float (&X)[T::T_CL][3], float* __restrict__ shw_tab,
+                                                  float* __restrict__ pool) {
+  constexpr int TPW = kTeamsPerBlock, CL = T::T_CL;
+  const int team = threadIdx.x >> 2;
+  float* tab = shw_tab + team;
+  // bounding-sphere centres (relative to the root origin)
+#pragma unroll
+  for (int j = 0; j < T::T_SPC; ++j) {
+    constexpr int dummy = 0;
+    (void)dummy;
+    const int sh = T::T_RS + lc * T::T_SPC + j;
+    const int k = T::sh_body[T::T_RS + j] - 1;  // chain-local body (chain 0's layout, the same for every chain)
+    float t[3];
+    mat3vec(R[k], M->shc[sh], t);
+#pragma unroll
+    for (int f = 0; f < 3; ++f) tab[(kShW * sh + 12 + f) * TPW] = X[k][f] + t[f];
+  }
+  if (lc == 0) {
+#pragma unroll
+    for (int sh = 0; sh < T::T_RS; ++sh) {
+      float t[3];
+      mat3vec(R0, M->shc[sh], t);
+#pragma unroll
+      for (int f = 0; f < 3; ++f) tab[(kShW * sh + 12 + f) * TPW] = t[f];
+    }
+  }
+  __syncthreads();
+  bool near = false;
+  for (int q = lc; q < M->np; q += 4) {
+    const int a = M->pa[q], b = M->pb[q];
+    const float d[3] = {tab[(kShW * a + 12) * TPW] - tab[(kShW * b + 12) * TPW],
+                        tab[(kShW * a + 13) * TPW] - tab[(kShW * b + 13) * TPW],
+                        tab[(kShW * a + 14) * TPW] - tab[(kShW * b + 14) * TPW]};
+    const float rr = M->shc[a][3] + M->shc[b][3] + P.contact_offset;
+    near = near || (d[0] * d[0] + d[1] * d[1] + d[2] * d[2] < rr * rr);
+  }
+  if (__ballot(near) == 0ull) return 0;  // wave-uniform: no team of the wave has a near pair
+  // full shape poses for the narrowphase
+#pragma unroll
+  for (int j = 0; j < T::T_SPC; ++j) {
+    const int sh = T::T_RS + lc * T::T_SPC + j;
+    const int k = T::sh_body[T::T_RS + j] - 1;
+    float Rs[9], t[3];
+    mat3mul(R[k], M->shR[sh], Rs);
+    mat3vec(R[k], M->sht[sh], t);
+#pragma unroll
+    for (int f = 0; f < 9; ++f) tab[(kShW * sh + f) * TPW] = Rs[f];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) tab[(kShW * sh + 9 + f) * TPW] = X[k][f] + t[f];
+  }
+  if (lc == 0) {
+#pragma unroll
+    for (int sh = 0; sh < T::T_RS; ++sh) {
+      float Rs[9], t[3];
+      mat3mul(R0, M->shR[sh], Rs);
+      mat3vec(R0, M->sht[sh], t);
+#pragma unroll
+      for (int f = 0; f < 9; ++f) tab[(kShW * sh + f) * TPW] = Rs[f];
+#pragma unroll
+      for (int f = 0; f < 3; ++f) tab[(kShW * sh + 9 + f) * TPW] = t[f];
+    }
+  }
+  __syncthreads();
+  // any lane of the team near -> the team's narrowphase (replicated, team-uniform result)
+  const bool tnear = quad_sum(near ? 1.f : 0.f) > 0.f;
+  if (!tnear) return 0;
+  return self_contacts<T, TPW, RW, RowSlots<T>::PER_POOL>(M, P, mu_g, N, e, tab, pool);
+  (void)CL;
+}
+
 template <class T>
 __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, const float* __restrict__ mdl,
                                              const DevParams& P, TeamState<T>& s, const float* tau,
                                              const float* __restrict__ mu_g, int N, int e, int lc,
                                              float* __restrict__ rows_own, const float* __restrict__ rows_team,
                                              float* __restrict__ cf_soa, bool collect,
-                                             float* __restrict__ cf_aos GS_PROF_PARAM) {
+                                             float* __restrict__ cf_aos, float* __restrict__ shw_tab GS_PROF_PARAM) {
   constexpr int CL = T::T_CL, CC = T::T_CC, RC = T::T_RC, NCH = T::T_NCH, LN = T::T_LANES;
   static_assert(NCH == LN && LN == 4, "lane teams are DPP quads with one chain per lane");
   using C = CM<T>;
@@ -429,6 +519,13 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         }
       }
     }
+  }
+
+  // ================= self-collision prepass (rare narrowphase; the pool rows are built with the contact records)
+  int npc = 0;
+  float* pool = rows_own + RS::POOL * RW;
+  if constexpr (T::NPK > 0) {
+    if (P.self_collide) npc = team_self_contacts<T>(M, P, mu_g, N, e, lc, R0, R, X, shw_tab, pool);
   }
 
   GS_PROF(0)  // root + chain forward pass + contact Jacobians
@@ -729,6 +826,116 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       rec[RS::R_MU * RW] = 0.5f * (mu_g[T::T_rcs[j] * N + e] + P.ground_mu);
     }
   }
+  // self-contact pool rows: J = n.(v_A(x) - v_B(x)) has columns only on the two chains below
+  // the root (the base columns cancel); each lane forms its own chain's part, eliminates it through its L factor,
+  // the base part is the team sum eliminated through the replicated base block; the lane then keeps the
+  // components it owns in the distributed PGS (base 2l, 2l+1; component l of chains A and B; lane 3: c)
+  if constexpr (T::NPK > 0) {
+    for (int p = 0; p < npc; ++p) {
+      float* o = pool + RS::PER_POOL * p * RW;
+      const int ba = (int)o[kPoolBA * RW], bb = (int)o[kPoolBB * RW];
+      const int ca = ba > 0 ? (ba - 1) / CL : -1, ka = ba > 0 ? (ba - 1) - ca * CL : -1;
+      const int cb = bb > 0 ? (bb - 1) / CL : -1, kb = bb > 0 ? (bb - 1) - cb * CL : -1;
+      const float x[3] = {o[kPoolX * RW], o[(kPoolX + 1) * RW], o[(kPoolX + 2) * RW]};
+      float zr[3][6], zc3[3][CL], dd[3];
+#pragma unroll
+      for (int rr = 0; rr < 3; ++rr) {
+        const int dofs = rr == 0 ? kPoolN : (rr == 1 ? kPoolT1 : kPoolT2);
+        const float d[3] = {o[dofs * RW], o[(dofs + 1) * RW], o[(dofs + 2) * RW]};
+        float zc[CL], zbc[6];
+        float cpart = 0.f;
+#pragma unroll
+        for (int k = 0; k < CL; ++k) {
+          const float coef = (lc == ca && k <= ka ? 1.f : 0.f) - (lc == cb && k <= kb ? 1.f : 0.f);
+          float vx[3];
+          cross3(S[k], x, vx);
+          zc[k] = coef * (d[0] * (S[k][3] + vx[0]) + d[1] * (S[k][4] + vx[1]) + d[2] * (S[k][5] + vx[2]));
+          cpart += zc[k] * nufc[k];
+        }
+#pragma unroll
+        for (int b = 0; b < 6; ++b) zbc[b] = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < CL; ++kk) {
+          const int k = CL - 1 - kk;
+#pragma unroll
+          for (int i = 0; i < k; ++i) zc[i] -= Mcc[k][i] * zc[k];
+#pragma unroll
+          for (int b = 0; b < 6; ++b) zbc[b] -= Mcb[k][b] * zc[k];
+        }
+        float zb[6];
+#pragma unroll
+        for (int b = 0; b < 6; ++b) zb[b] = quad_sum(zbc[b]);
+#pragma unroll
+        for (int kk = 0; kk < 6; ++kk) {
+          const int k = 5 - kk;
+#pragma unroll
+          for (int b = 0; b < k; ++b) zb[b] -= Mbb[k][b] * zb[k];
+        }
+        float own = 0.f, db = 0.f;
+#pragma unroll
+        for (int b = 0; b < 6; ++b) { zb[b] *= sDb[b]; db += zb[b] * zb[b]; zr[rr][b] = zb[b]; }
+#pragma unroll
+        for (int k = 0; k < CL; ++k) { zc[k] *= sDc[k]; own += zc[k] * zc[k]; zc3[rr][k] = zc[k]; }
+        dd[rr] = db + quad_sum(own);
+        const float cj = quad_sum(cpart);
+        // distributed components: chain A / B component lc (from lane ca / cb), base 2 lc, 2 lc + 1
+        float za = 0.f, zbb = 0.f;
+#pragma unroll
+        for (int l = 0; l < CL; ++l) {
+          float va = 0.f, vb = 0.f;
+#pragma unroll
+          for (int L = 0; L < 4; ++L) {
+            const float t = bcast(zc[l], L);
+            va = L == ca ? t : va;
+            vb = L == cb ? t : vb;
+          }
+          za = lc == l ? va : za;
+          zbb = lc == l ? vb : zbb;
+        }
+        if (cb == ca) zbb = 0.f;  // one chain: its components carry both sides already
+        const float b0 = lc == 0 ? zb[0] : (lc == 1 ? zb[2] : (lc == 2 ? zb[4] : 0.f));
+        const float b1 = lc == 0 ? zb[1] : (lc == 1 ? zb[3] : (lc == 2 ? zb[5] : 0.f));
+        float* zo = o + (RS::P_Z + 5 * rr) * RW;
+        zo[0] = b0;
+        zo[RW] = b1;
+        zo[2 * RW] = za;
+        zo[3 * RW] = zbb;
+        zo[4 * RW] = lc == 3 ? cj : 0.f;
+      }
+      float g10 = 0.f, g20 = 0.f, g21 = 0.f, c10 = 0.f, c20 = 0.f, c21 = 0.f;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+        g10 += zr[1][b] * zr[0][b];
+        g20 += zr[2][b] * zr[0][b];
+        g21 += zr[2][b] * zr[1][b];
+      }
+#pragma unroll
+      for (int k = 0; k < CL; ++k) {
+        c10 += zc3[1][k] * zc3[0][k];
+        c20 += zc3[2][k] * zc3[0][k];
+        c21 += zc3[2][k] * zc3[1][k];
+      }
+      g10 += quad_sum(c10);
+      g20 += quad_sum(c20);
+      g21 += quad_sum(c21);
+      float di[3];
+#pragma unroll
+      for (int rr = 0; rr < 3; ++rr) {
+        di[rr] = dd[rr] > GS_MIN_RESPONSE ? __builtin_amdgcn_rcpf(dd[rr]) : 0.f;
+        o[(RS::P_DI + rr) * RW] = di[rr];
+        o[(kPoolLam + rr) * RW] = 0.f;
+      }
+      o[(RS::P_G + 0) * RW] = g10 * di[1];
+      o[(RS::P_G + 1) * RW] = g20 * di[2];
+      o[(RS::P_G + 2) * RW] = g21 * di[2];
+      const float sc = o[kPoolSep * RW];
+      const float tgt = -sc * inv_h;
+      o[RS::P_TP * RW] = (sc < 0.f ? fminf(tgt, P.max_depen_vel) : tgt) * di[0];
+      o[RS::P_TV * RW] = (sc < 0.f ? 0.f : tgt) * di[0];
+      o[RS::P_CA * RW] = (float)ca;
+      o[RS::P_CB * RW] = (float)(cb == ca ? -1 : cb);
+    }
+  }
   // the sweeps read other lanes' records: make this wave's LDS writes visible (one-wave block)
   __syncthreads();
 
@@ -822,6 +1029,40 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         wC[cc] = fmaf(z[10], dl2, fmaf(z[6], dl1, fmaf(z[2], dl0, wC[cc])));
       }
     }
+    if constexpr (T::NPK > 0) {
+      const int psel = it < P.pos_iters ? RS::P_TP : RS::P_TV;
+      for (int p = 0; p < npc; ++p) {
+        float* o = pool + RS::PER_POOL * p * RW;
+        const int ca = (int)o[RS::P_CA * RW], cb = (int)o[RS::P_CB * RW];
+        float wa = 0.f, wb = 0.f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          wa = c == ca ? wC[c] : wa;
+          wb = c == cb ? wC[c] : wb;
+        }
+        float z[15], u[3];
+#pragma unroll
+        for (int i = 0; i < 15; ++i) z[i] = o[(RS::P_Z + i) * RW];
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr)
+          u[rr] = fmaf(z[5 * rr], wA, fmaf(z[5 * rr + 1], wA2, fmaf(z[5 * rr + 2], wa, fmaf(z[5 * rr + 3], wb, z[5 * rr + 4]))));
+        quad_sum3(u);
+        float lam[3] = {o[kPoolLam * RW], o[(kPoolLam + 1) * RW], o[(kPoolLam + 2) * RW]};
+        float dl0, dl1, dl2;
+        contact_block(u[0], u[1], u[2], o[RS::P_DI * RW], o[(RS::P_DI + 1) * RW], o[(RS::P_DI + 2) * RW],
+                      o[RS::P_G * RW], o[(RS::P_G + 1) * RW], o[(RS::P_G + 2) * RW], o[psel * RW], o[kPoolMu * RW], lam,
+                      dl0, dl1, dl2);
+        o[kPoolLam * RW] = lam[0];
+        o[(kPoolLam + 1) * RW] = lam[1];
+        o[(kPoolLam + 2) * RW] = lam[2];
+        wA = fmaf(z[10], dl2, fmaf(z[5], dl1, fmaf(z[0], dl0, wA)));
+        wA2 = fmaf(z[11], dl2, fmaf(z[6], dl1, fmaf(z[1], dl0, wA2)));
+        const float da = fmaf(z[12], dl2, fmaf(z[7], dl1, z[2] * dl0));
+        const float db = fmaf(z[13], dl2, fmaf(z[8], dl1, z[3] * dl0));
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) wC[c] += (c == ca ? da : 0.f) + (c == cb ? db : 0.f);
+      }
+    }
 #ifdef GS_PHASE_PROFILE
     for (int j = 0; j < RC; ++j)
       if (__ballot(ract[j]) != 0ull) GS_PROF_COUNT(9, 1)  // root contacts the wave executes
@@ -910,6 +1151,19 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
           f2 += l0 * inv_h;
         }
       }
+      if constexpr (T::NPK > 0) {  // self-contacts: +f on body A, -f on body B
+        for (int p = 0; p < npc; ++p) {
+          const float* o = pool + RS::PER_POOL * p * RW;
+          const int bk = 1 + lc * CL + k;
+          const float sg = ((int)o[kPoolBA * RW] == bk ? inv_h : 0.f) - ((int)o[kPoolBB * RW] == bk ? inv_h : 0.f);
+          if (sg != 0.f) {
+            const float l0 = o[kPoolLam * RW], l1 = o[(kPoolLam + 1) * RW], l2 = o[(kPoolLam + 2) * RW];
+            f0 += sg * (l0 * o[kPoolN * RW] + l1 * o[kPoolT1 * RW] + l2 * o[kPoolT2 * RW]);
+            f1 += sg * (l0 * o[(kPoolN + 1) * RW] + l1 * o[(kPoolT1 + 1) * RW] + l2 * o[(kPoolT2 + 1) * RW]);
+            f2 += sg * (l0 * o[(kPoolN + 2) * RW] + l1 * o[(kPoolT1 + 2) * RW] + l2 * o[(kPoolT2 + 2) * RW]);
+          }
+        }
+      }
       const int b = 1 + lc * CL + k;
       cf_soa[(3 * b + 0) * N + e] = f0;
       cf_soa[(3 * b + 1) * N + e] = f1;
@@ -926,6 +1180,18 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         f0 += lamr[j][1] * inv_h;
         f1 += lamr[j][2] * inv_h;
         f2 += lamr[j][0] * inv_h;
+      }
+      if constexpr (T::NPK > 0) {
+        for (int p = 0; p < npc; ++p) {
+          const float* o = pool + RS::PER_POOL * p * RW;
+          const float sg = ((int)o[kPoolBA * RW] == 0 ? inv_h : 0.f) - ((int)o[kPoolBB * RW] == 0 ? inv_h : 0.f);
+          if (sg != 0.f) {
+            const float l0 = o[kPoolLam * RW], l1 = o[(kPoolLam + 1) * RW], l2 = o[(kPoolLam + 2) * RW];
+            f0 += sg * (l0 * o[kPoolN * RW] + l1 * o[kPoolT1 * RW] + l2 * o[kPoolT2 * RW]);
+            f1 += sg * (l0 * o[(kPoolN + 1) * RW] + l1 * o[(kPoolT1 + 1) * RW] + l2 * o[(kPoolT2 + 1) * RW]);
+            f2 += sg * (l0 * o[(kPoolN + 2) * RW] + l1 * o[(kPoolT1 + 2) * RW] + l2 * o[(kPoolT2 + 2) * RW]);
+          }
+        }
       }
       cf_soa[0 * N + e] = f0;
       cf_soa[1 * N + e] = f1;
@@ -954,6 +1220,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel*
   constexpr int LN = T::T_LANES, CL = T::T_CL, ND = T::ND;
   __shared__ float mdl[CM<T>::NP * LN];
   __shared__ float rows[RowSlots<T>::TOTAL * RW];
+  __shared__ float shw_tab[T::NPK > 0 ? kShW * T::NS * kTeamsPerBlock : 1];
   stage_chain_model<T>(M, mdl);
   __syncthreads();
   const int lc = threadIdx.x & (LN - 1);
@@ -970,7 +1237,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel*
   GS_PROF_DECL
   for (int sstep = 0; sstep < P.substeps; ++sstep) {
     const bool last = (sstep == P.substeps - 1) && P.collect;
-    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, nullptr GS_PROF_ARGS);
+    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, nullptr, shw_tab GS_PROF_ARGS);
   }
   team_store<T>(B.state, N, e, lc, s);
   GS_PROF_FLUSH
@@ -982,6 +1249,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
   constexpr int LN = T::T_LANES, CL = T::T_CL, ND = T::ND, NB = T::NB;
   __shared__ float mdl[CM<T>::NP * LN];
   __shared__ float rows[RowSlots<T>::TOTAL * RW];
+  __shared__ float shw_tab[T::NPK > 0 ? kShW * T::NS * kTeamsPerBlock : 1];
   stage_chain_model<T>(M, mdl);
   __syncthreads();
   const int lc = threadIdx.x & (LN - 1);
@@ -1012,7 +1280,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
     const bool last = ((it % sub) == sub - 1) && P.collect;
     GS_PROF(6)  // PD torque
     float* cf_aos = (it == total - 1) ? A.cf_out : nullptr;
-    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, cf_aos GS_PROF_ARGS);
+    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, cf_aos, shw_tab GS_PROF_ARGS);
     if (it == n_pd - 1 && A.dof_out) {
 #pragma unroll
       for (int k = 0; k < CL; ++k) {

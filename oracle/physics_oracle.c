@@ -49,7 +49,8 @@ typedef REAL real;
 #define MAXV 40
 #define MAXC 192
 #define MAXPOOL 16
-#define MIN_RESPONSE 1e-7 /* a contact row whose J M^-1 J^T falls below this takes no impulse */
+#define MIN_RESPONSE 1e-3 /* a contact row whose J M^-1 J^T falls below this (an effective mass above 1000 kg:
+                             an overlap no dof can separate) takes no impulse (GS_MIN_RESPONSE) */
 
 typedef struct {
     int32_t nb, nd, nc, ns, fixed_base;
@@ -671,7 +672,8 @@ static int self_contacts(const OModel *m, const OParams *p, real R[][9], real P[
             } else {
                 for (int k = 0; k < 3; ++k) nn[k] /= dist;
             }
-            const real sep = deep ? -(ra + rb) : dist - ra - rb;
+            if (deep) continue; /* overlapping cores: no contact */
+            const real sep = dist - ra - rb;
             if (!(sep < off)) continue;
             PairContact *o = &out[n++];
             for (int k = 0; k < 3; ++k) {
