@@ -102,6 +102,10 @@ typedef struct gs_model_desc {
     const int32_t *pair_b;        /* [np]                                               */
     const int32_t *pair_kind;     /* [np] 0 sphere-sphere 1 sphere-capsule 2 capsule-capsule 3 GJK */
     int32_t pair_pool;            /* self-contact slots per env (the compiled topology's) */
+    int32_t num_pair_verts;
+    const double *pair_verts;     /* [npv][4] the hulls' self-collision core vertices (a subset of hull_verts) */
+    const int32_t *shape_pv0;     /* [ns] range [pv0, pv1)                              */
+    const int32_t *shape_pv1;     /* [ns]                                               */
 } gs_model_desc;
 
 /* gymapi.SimParams subset the reference sets (vec_task.py:514-562). */

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GT_ABI_VERSION 3
+#define GT_ABI_VERSION 4
 #define GT_ANYMAL_NUM_TERMS 13  /* lin_vel_xy lin_vel_z ang_vel_z ang_vel_xy orient torques joint_acc
                                    base_height air_time collision stumble action_rate hip */
 
@@ -243,9 +243,34 @@ typedef struct gt_ant_buffers {
     int32_t *reset_count;        /* [3] device, zero-initialised accumulator (re-armed by the kernel) */
     int32_t *host_count;         /* [2] host-mapped {count, seq} or NULL */
     int32_t seq;
+    uint64_t *reset_masks;       /* ABI 4: [ceil(N/64)] the done mask's per-wave ballots (gt_ant_reset_flagged) */
 } gt_ant_buffers;
 
 int gt_ant_post_physics(const gt_ant_params *p, const gt_ant_buffers *b, void *stream);
+
+/* Ant reset_idx (ant.py:252-279), fused (ABI 4), for the k envs the previous gt_ant_post_physics flagged
+ * (its reset_masks ballots; env ids ascending = torch's nonzero order):
+ *   offsets    = torch_rand_float(-0.2, 0.2, (k, 8)), velocities = torch_rand_float(-0.1, 0.1, (k, 8))
+ *                (pos_range * u + pos_lower etc.; u from the two consecutive torch.rand plans, evaluated in-kernel
+ *                bit-identically to torch's Philox, or from explicit uniforms u_pos / u_vel [k][8])
+ *   dof_state[e] = (tensor_clamp(initial_dof_pos[e] + offsets, lower, upper), velocities)
+ *   prev_potentials[e] = potentials[e] = -|planar(targets[e] - initial_root_states[e, 0:3])| / dt
+ *   progress_buf[e] = 0, reset_buf[e] = 0, env_ids_out[rank] = e
+ * The caller then applies set_actor_root_state_tensor_indexed(initial_root_states, env_ids_out, k) and
+ * set_dof_state_tensor_indexed(dof_state, env_ids_out, k) as the reference does. */
+typedef struct gt_ant_reset_args {
+    gt_torch_rand_plan plan_pos, plan_vel;
+    const float *u_pos, *u_vel;
+    float pos_range, pos_lower, vel_range, vel_lower;
+    const float *initial_dof_pos;      /* [N][8]  */
+    const float *initial_root_states;  /* [N][13] */
+    float *dof_state;                  /* [N*8][2] the task's dof tensor */
+    int64_t *progress_buf;             /* [N] */
+    int32_t *env_ids_out;              /* [>= k] */
+} gt_ant_reset_args;
+
+int gt_ant_reset_flagged(const gt_ant_params *p, const gt_ant_buffers *b, int k, const gt_ant_reset_args *r,
+                         void *stream);
 
 /* out[plan.numel] = torch.rand(plan.numel) for the given plan (checks torch_philox.h against torch) */
 int gt_torch_rand(const gt_torch_rand_plan *plan, float *out, void *stream);

@@ -312,6 +312,16 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   for (int c = 0; c < m->num_candidates; ++c)
     if (m->cand_dyn && m->cand_dyn[c] != t->cdyn[c])
       return fail("gs_sim_set_model: hull slots differ from the compiled topology (tools/gen_topologies.py)");
+  // the kernels unroll the self-collision pairs and shape kinds at compile time
+  if (m->num_pairs > 0 && m->num_pairs != t->npair)
+    return fail("gs_sim_set_model: self-collision pair count differs from the compiled topology's %s",
+                std::to_string(t->npair).c_str());
+  for (int q = 0; q < m->num_pairs; ++q)
+    if (m->pair_a[q] != t->pair_a[q] || m->pair_b[q] != t->pair_b[q] || m->pair_kind[q] != t->pair_k[q])
+      return fail("gs_sim_set_model: self-collision pairs differ from the compiled topology (tools/gen_topologies.py)");
+  for (int sh = 0; sh < m->num_shapes; ++sh)
+    if (m->shape_kind && m->shape_kind[sh] != t->shkind[sh])
+      return fail("gs_sim_set_model: shape kinds differ from the compiled topology (tools/gen_topologies.py)");
   // Everything is built into locals first and committed at the end, so a failure leaves the sim as
   // it was (no half-set topology with a null kernel or link table).
   DevModel h;
@@ -363,6 +373,18 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   }
   for (int v = 0; v < m->num_hull_verts; ++v)
     for (int k = 0; k < 4; ++k) h.hv[v][k] = (float)m->hull_verts[4 * v + k];
+  if (m->num_pair_verts < 0 || m->num_pair_verts > GS_MAXPV || !m->shape_pv0 || !m->shape_pv1 ||
+      (m->num_pair_verts > 0 && !m->pair_verts))
+    return fail("gs_sim_set_model: hull self-collision cores missing or beyond GS_MAXPV");
+  for (int v = 0; v < m->num_pair_verts; ++v)
+    for (int k = 0; k < 4; ++k) h.pv[v][k] = (float)m->pair_verts[4 * v + k];
+  for (int sh = 0; sh < m->num_shapes; ++sh) {
+    h.pv0[sh] = m->shape_pv0[sh];
+    h.pv1[sh] = m->shape_pv1[sh];
+    if (h.pv0[sh] < 0 || h.pv1[sh] < h.pv0[sh] || h.pv1[sh] > m->num_pair_verts ||
+        (h.shkind[sh] == 4 && h.pv1[sh] == h.pv0[sh]))
+      return fail("gs_sim_set_model: shape %s self-collision core out of range", std::to_string(sh).c_str());
+  }
   for (int c = 0; c < m->num_candidates; ++c)
     if (m->cand_dyn[c] >= 0 && m->shape_kind[m->cand_shape[c]] != 4)
       return fail("gs_sim_set_model: dynamic candidate %s on a shape that is not a hull", std::to_string(c).c_str());

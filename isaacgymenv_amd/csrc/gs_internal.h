@@ -12,6 +12,7 @@
 #define GS_MAXSH 32  // collision shapes per articulation
 #define GS_MAXHV 2048  // convex-hull vertices per articulation (UsefulHound's arm: 1503)
 #define GS_MAXP 512   // self-collision shape pairs per articulation (UsefulHound: 253)
+#define GS_MAXPV 512  // hull self-collision core vertices per articulation (UsefulHound: 7 x <= 48)
 #define GS_MAXPOOL 8  // self-contact slots per env
 #define GS_WAVE 64
 // a contact row whose J M^-1 J^T falls below this -- an effective mass above 1000 kg, an overlap no dof can
@@ -58,6 +59,8 @@ struct DevModel {
   int np;                       // self-collision pairs
   int pa[GS_MAXP], pb[GS_MAXP], pk[GS_MAXP];  // shape a < shape b, kind 0 SS 1 SC 2 CC 3 GJK
   float hv[GS_MAXHV][4];        // hull vertices, body frame xyz + core factor (core = c + f (v - c))
+  int pv0[GS_MAXSH], pv1[GS_MAXSH];  // a hull's self-collision core vertices (subset of hv)
+  float pv[GS_MAXPV][4];
 };
 
 struct DevParams {
@@ -120,6 +123,8 @@ struct TopoEntry {
                               // (0 = rows in LDS) and env lanes per workgroup (LaneCfg<T, false>)
   int npk;                    // self-contact pool slots (T::NPK)
   const int* cdyn;            // [nc] hull slot of each candidate (T::cdyn)
+  int npair;                  // self-collision pair table (T::NPAIR, T::pair_a / pair_b / pair_k) and shape
+  const int *pair_a, *pair_b, *pair_k, *shkind;  // kinds (T::shkind): the kernels unroll over them
 };
 
 // Kinematics of the reported links (gs_kinematics.hip): runtime-sized tree tables, one copy in

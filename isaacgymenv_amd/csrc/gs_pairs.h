@@ -148,8 +148,8 @@ GS_HD void core_support(const DevModel* __restrict__ M, int sh, const ShapeW& W,
                          W.R[2] * d[0] + W.R[5] * d[1] + W.R[8] * d[2]};
     const float* cc = M->shc[sh];
     float best = -3.0e38f, bv[3] = {0.f, 0.f, 0.f};
-    for (int k = M->hv0[sh]; k < M->hv1[sh]; ++k) {
-      const float* v = M->hv[k];
+    for (int k = M->pv0[sh]; k < M->pv1[sh]; ++k) {
+      const float* v = M->pv[k];
       const float f = v[3];
       const float p[3] = {cc[0] + f * (v[0] - cc[0]), cc[1] + f * (v[1] - cc[1]), cc[2] + f * (v[2] - cc[2])};
       const float t = dot3f(p, dl);
@@ -228,19 +228,19 @@ GS_HD float core_feature(const DevModel* __restrict__ M, int sh, const ShapeW& W
                        W.R[2] * d[0] + W.R[5] * d[1] + W.R[8] * d[2]};
   const float* cc = M->shc[sh];
   auto corev = [&](int k, float* p) {
-    const float* v = M->hv[k];
+    const float* v = M->pv[k];
     const float f = v[3];
     p[0] = cc[0] + f * (v[0] - cc[0]); p[1] = cc[1] + f * (v[1] - cc[1]); p[2] = cc[2] + f * (v[2] - cc[2]);
   };
   float hmax = -3.0e38f;
-  for (int k = M->hv0[sh]; k < M->hv1[sh]; ++k) {
+  for (int k = M->pv0[sh]; k < M->pv1[sh]; ++k) {
     float p[3];
     corev(k, p);
     hmax = fmaxf(hmax, dot3f(p, dl));
   }
   float acc[3] = {0.f, 0.f, 0.f};
   int n = 0;
-  for (int k = M->hv0[sh]; k < M->hv1[sh]; ++k) {
+  for (int k = M->pv0[sh]; k < M->pv1[sh]; ++k) {
     float p[3];
     corev(k, p);
     if (dot3f(p, dl) >= hmax - kFeatureEps) {
@@ -251,7 +251,7 @@ GS_HD float core_feature(const DevModel* __restrict__ M, int sh, const ShapeW& W
   const float inv = 1.f / (float)n;
   acc[0] *= inv; acc[1] *= inv; acc[2] *= inv;
   float ext = 0.f;
-  for (int k = M->hv0[sh]; k < M->hv1[sh]; ++k) {
+  for (int k = M->pv0[sh]; k < M->pv1[sh]; ++k) {
     float p[3];
     corev(k, p);
     if (dot3f(p, dl) >= hmax - kFeatureEps) {
@@ -358,8 +358,10 @@ GS_HD void simplex_all(const float (&W)[4][3], int k, float& best, int& bm, floa
 
 // GJK distance between the cores of shapes a and b: closest points pa, pb; returns the distance, 0 when the
 // cores overlap (same iteration and termination rules as the oracle's gjk_cores)
+// stop: a distance beyond which the caller has no use for the closest points -- once GJK's lower bound (the
+// support plane's offset v.w / |v|) exceeds it, the search ends and returns that bound (pa, pb unset)
 GS_HD float gjk_cores(const DevModel* __restrict__ M, int sa, int sb, const ShapeW& Wa, const ShapeW& Wb, float* pa,
-                      float* pb) {
+                      float* pb, float stop = 3.0e38f) {
   float v[3] = {Wa.sc[0] - Wb.sc[0], Wa.sc[1] - Wb.sc[1], Wa.sc[2] - Wb.sc[2]};
   if (dot3f(v, v) < 1e-18f) { v[0] = 1.f; v[1] = 0.f; v[2] = 0.f; }
   float W[4][3], A[4][3], B[4][3], lam[4] = {1.f, 0.f, 0.f, 0.f};
@@ -375,8 +377,9 @@ GS_HD float gjk_cores(const DevModel* __restrict__ M, int sa, int sb, const Shap
     core_support(M, sb, Wb, v, b);
 #pragma unroll
     for (int t = 0; t < 3; ++t) w[t] = a[t] - b[t];
-    const float vv = dot3f(v, v);
-    if (k > 0 && vv - dot3f(v, w) <= 1e-10f * vv + 1e-14f) break;
+    const float vv = dot3f(v, v), vw = dot3f(v, w);
+    if (vw > 0.f && vw * vw > stop * stop * vv) return vw / sqrtf(vv);  // separated by more than stop
+    if (k > 0 && vv - vw <= 1e-10f * vv + 1e-14f) break;
     bool dup = false;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -469,26 +472,29 @@ GS_HD void seg_seg(const float* p1, const float* q1, const float* p2, const floa
   }
 }
 
+constexpr int kUnrollPairs = 64;  // pair tables up to this size are unrolled at compile time
+
 // Self-contacts of one env in pair order, at most T::NPK (later ones dropped): broadphase on the shapes'
 // bounding spheres (within contact_offset), closed-form sphere / capsule pairs, GJK on margin-rounded cores
 // otherwise.  Writes the pool entries' geometry (x relative to the root origin, n from B to A, tangents,
 // separation, friction, bodies, links); returns the count.
 // (shape data at stride LB, pool entries at stride LBP with PE floats per entry: the one-env-per-lane solver
 // keeps both in its lane column; the lane team reads a per-team shape table and keeps a shorter entry)
-template <class T, int LB, int LBP = LB, int PE = PoolCfg<T>::PE>
-GS_HD int self_contacts(const DevModel* __restrict__ M, const DevParams& P, const float* __restrict__ mu_g, int N,
-                        int e, const float* shw, float* pool) {
+// One pair (shapes a < b, pair kind) of self_contacts: appends its contacts to the pool (n counts them).
+template <class T, int LB, int LBP, int PE>
+GS_HD __attribute__((always_inline)) inline void self_pair(const DevModel* __restrict__ M, const DevParams& P,
+                                                           const float* __restrict__ mu_g, int N, int e,
+                                                           const float* shw, float* pool, int a, int b, int kind,
+                                                           int& n) {
   const float off = P.contact_offset;
-  int n = 0;
-  const int np = M->np;
-  for (int q = 0; q < np; ++q) {
-    if (n >= T::NPK) break;
-    const int a = M->pa[q], b = M->pb[q], kind = M->pk[q];
+  {
     const float* sa = shw + (kShW * a + 12) * LB;
     const float* sb = shw + (kShW * b + 12) * LB;
     const float d[3] = {sa[0] - sb[0], sa[LB] - sb[LB], sa[2 * LB] - sb[2 * LB]};
     const float rr = M->shc[a][3] + M->shc[b][3] + off;
-    if (!(dot3f(d, d) < rr * rr)) continue;
+    if (!(dot3f(d, d) < rr * rr)) return;
+  }
+  {
     ShapeW Wa, Wb;
     load_shape_w<LB>(shw, a, Wa);
     load_shape_w<LB>(shw, b, Wb);
@@ -552,7 +558,11 @@ GS_HD int self_contacts(const DevModel* __restrict__ M, const DevParams& P, cons
         for (int k = 0; k < 3; ++k) { pa[0][k] = p1[k] + s * (q1[k] - p1[k]); pb[0][k] = p2[k] + t * (q2[k] - p2[k]); }
       }
     } else {
-      const float dist = gjk_cores(M, a, b, Wa, Wb, pa[0], pb[0]);
+      // (a pair whose cores are farther apart than contact_offset + radii makes no contact: stop there, with a
+      // hair of slack so the bound's rounding never drops a contact the full search would keep)
+      const float stop = (off + ra + rb) * 1.001f + 1e-5f;
+      const float dist = gjk_cores(M, a, b, Wa, Wb, pa[0], pb[0], stop);
+      if (dist > stop) return;
       if (!(dist > 1e-9f)) {
         gdeep = true;
 #pragma unroll
@@ -608,6 +618,25 @@ GS_HD int self_contacts(const DevModel* __restrict__ M, const DevParams& P, cons
       o[kPoolLA * LBP] = (float)M->shlink[a];
       o[kPoolLB * LBP] = (float)M->shlink[b];
       ++n;
+    }
+  }
+}
+
+template <class T, int LB, int LBP = LB, int PE = PoolCfg<T>::PE>
+GS_HD int self_contacts(const DevModel* __restrict__ M, const DevParams& P, const float* __restrict__ mu_g, int N,
+                        int e, const float* shw, float* pool) {
+  int n = 0;
+  if constexpr (T::NPAIR <= kUnrollPairs) {
+    // the compiled topology's pair table (gs_sim_set_model checks it against the model's): shapes and pair
+    // kinds fold into the code, the shapes' constants are independent loads
+#pragma unroll
+    for (int q = 0; q < T::NPAIR; ++q)
+      if (n < T::NPK) self_pair<T, LB, LBP, PE>(M, P, mu_g, N, e, shw, pool, T::pair_a[q], T::pair_b[q], T::pair_k[q], n);
+  } else {
+    const int np = M->np;
+    for (int q = 0; q < np; ++q) {
+      if (n >= T::NPK) break;
+      self_pair<T, LB, LBP, PE>(M, P, mu_g, N, e, shw, pool, M->pa[q], M->pb[q], M->pk[q], n);
     }
   }
   return n;

@@ -153,6 +153,7 @@ hipError_t launch_pd(const DevModel* M, const DevParams& P, const SimBuffers& B,
 
 #define GS_TOPO_ENTRY(T, SIG)                                                                          \
   {SIG, T::kName, &launch_sim<T>, &launch_pd<T>, T::NB, T::ND, T::NC, T::NS, T::SENS ? 1 : 0,            \
-   LaneCfg<T, false>::ROW_FLOATS, LaneCfg<T, false>::LB, T::NPK, T::cdyn},
+   LaneCfg<T, false>::ROW_FLOATS, LaneCfg<T, false>::LB, T::NPK, T::cdyn, T::NPAIR, T::pair_a, T::pair_b,      \
+   T::pair_k, T::shkind},
 TopoEntry g_topologies[] = {GS_FOR_EACH_TOPOLOGY(GS_TOPO_ENTRY)};
 const int g_num_topologies = sizeof(g_topologies) / sizeof(g_topologies[0]);

@@ -8,7 +8,7 @@
 namespace gs_phys {
 
 // ---------------------------------------------------------------- kernels
-template <class T, bool TERR>
+template <class T, bool TERR, bool SELF>
 __global__ __launch_bounds__((LaneCfg<T, TERR>::LB), 1) void k_simulate(const DevModel* __restrict__ M, DevParams P,
                                                                 SimBuffers B, const float* __restrict__ tau_aos) {
   using C = LaneCfg<T, TERR>;
@@ -17,10 +17,10 @@ __global__ __launch_bounds__((LaneCfg<T, TERR>::LB), 1) void k_simulate(const De
   const int e = blockIdx.x * LB + threadIdx.x;
   if (e >= B.N) return;
   float* rows = C::GLOBAL ? B.rows + (size_t)blockIdx.x * C::SLOTS * LB + threadIdx.x : lds + threadIdx.x;
-  simulate_env<T, TERR, LB>(M, P, B, tau_aos, e, rows);
+  simulate_env<T, TERR, LB, SELF>(M, P, B, tau_aos, e, rows);
 }
 
-template <class T, bool TERR>
+template <class T, bool TERR, bool SELF>
 __global__ __launch_bounds__((LaneCfg<T, TERR>::LB), 1) void k_pd_step(const DevModel* __restrict__ M, DevParams P,
                                                                SimBuffers B, PdDev A) {
   using C = LaneCfg<T, TERR>;
@@ -29,7 +29,7 @@ __global__ __launch_bounds__((LaneCfg<T, TERR>::LB), 1) void k_pd_step(const Dev
   const int e = blockIdx.x * LB + threadIdx.x;
   if (e >= B.N) return;
   float* rows = C::GLOBAL ? B.rows + (size_t)blockIdx.x * C::SLOTS * LB + threadIdx.x : lds + threadIdx.x;
-  pd_step_env<T, TERR, LB>(M, P, B, A, e, rows);
+  pd_step_env<T, TERR, LB, SELF>(M, P, B, A, e, rows);
 }
 
 // ---------------------------------------------------------------- terrain-mesh (TERR) kernels
@@ -61,7 +61,7 @@ __device__ __forceinline__ void terrain_queries(const DevParams& P, int N, int e
   }
 }
 
-template <class T>
+template <class T, bool SELF>
 __global__ __launch_bounds__(kTerrWave, 1) void k_simulate_terr(const DevModel* __restrict__ M, DevParams P,
                                                                 SimBuffers B, const float* __restrict__ tau_aos) {
   constexpr int LB = LaneCfg<T, true>::LB, NC = T::NC;
@@ -83,14 +83,14 @@ __global__ __launch_bounds__(kTerrWave, 1) void k_simulate_terr(const DevModel* 
     __syncthreads();
     if (env_lane) {
       const bool last = (sstep == P.substeps - 1) && P.collect;
-      substep<T, true, LB, LB>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last,
+      substep<T, true, LB, LB, SELF>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last,
                                sstep == P.substeps - 1 ? B.sens : nullptr, qout + threadIdx.x);
     }
   }
   if (env_lane) store_state<T>(B.state, N, e, s);
 }
 
-template <class T>
+template <class T, bool SELF>
 __global__ __launch_bounds__(kTerrWave, 1) void k_pd_step_terr(const DevModel* __restrict__ M, DevParams P,
                                                                SimBuffers B, PdDev A) {
   constexpr int LB = LaneCfg<T, true>::LB, NC = T::NC;
@@ -114,7 +114,7 @@ __global__ __launch_bounds__(kTerrWave, 1) void k_pd_step_terr(const DevModel* _
     __syncthreads();
     if (env_lane) {
       const bool last = ((it % sub) == sub - 1) && P.collect;
-      substep<T, true, LB, LB>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last,
+      substep<T, true, LB, LB, SELF>(M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last,
                                it == total - 1 ? B.sens : nullptr, qout + threadIdx.x);
       if (it == n_pd - 1) pd_dof_out<T>(A, e, s);
     }
@@ -128,25 +128,40 @@ __global__ __launch_bounds__(kTerrWave, 1) void k_pd_step_terr(const DevModel* _
 template <class T>
 hipError_t launch_sim_plane(const DevModel* M, const DevParams& P, const SimBuffers& B, const float* tau, hipStream_t st) {
   constexpr int LB = LaneCfg<T, false>::LB;
-  hipLaunchKernelGGL((gs_phys::k_simulate<T, false>), dim3((B.N + LB - 1) / LB), dim3(LB), 0, st, M, P, B, tau);
+  if (P.self_collide)
+    hipLaunchKernelGGL((gs_phys::k_simulate<T, false, true>), dim3((B.N + LB - 1) / LB), dim3(LB), 0, st, M, P, B, tau);
+  else
+    hipLaunchKernelGGL((gs_phys::k_simulate<T, false, false>), dim3((B.N + LB - 1) / LB), dim3(LB), 0, st, M, P, B, tau);
   return hipGetLastError();
 }
 template <class T>
 hipError_t launch_sim_terr(const DevModel* M, const DevParams& P, const SimBuffers& B, const float* tau, hipStream_t st) {
   constexpr int LB = LaneCfg<T, true>::LB;
-  hipLaunchKernelGGL((gs_phys::k_simulate_terr<T>), dim3((B.N + LB - 1) / LB), dim3(gs_phys::kTerrWave), 0, st, M, P, B,
-                     tau);
+  if (P.self_collide)
+    hipLaunchKernelGGL((gs_phys::k_simulate_terr<T, true>), dim3((B.N + LB - 1) / LB), dim3(gs_phys::kTerrWave), 0, st, M, P,
+                       B, tau);
+  else
+    hipLaunchKernelGGL((gs_phys::k_simulate_terr<T, false>), dim3((B.N + LB - 1) / LB), dim3(gs_phys::kTerrWave), 0, st, M,
+                       P, B, tau);
   return hipGetLastError();
 }
 template <class T>
 hipError_t launch_pd_plane(const DevModel* M, const DevParams& P, const SimBuffers& B, const PdDev& A, hipStream_t st) {
   constexpr int LB = LaneCfg<T, false>::LB;
-  hipLaunchKernelGGL((gs_phys::k_pd_step<T, false>), dim3((B.N + LB - 1) / LB), dim3(LB), 0, st, M, P, B, A);
+  if (P.self_collide)
+    hipLaunchKernelGGL((gs_phys::k_pd_step<T, false, true>), dim3((B.N + LB - 1) / LB), dim3(LB), 0, st, M, P, B, A);
+  else
+    hipLaunchKernelGGL((gs_phys::k_pd_step<T, false, false>), dim3((B.N + LB - 1) / LB), dim3(LB), 0, st, M, P, B, A);
   return hipGetLastError();
 }
 template <class T>
 hipError_t launch_pd_terr(const DevModel* M, const DevParams& P, const SimBuffers& B, const PdDev& A, hipStream_t st) {
   constexpr int LB = LaneCfg<T, true>::LB;
-  hipLaunchKernelGGL((gs_phys::k_pd_step_terr<T>), dim3((B.N + LB - 1) / LB), dim3(gs_phys::kTerrWave), 0, st, M, P, B, A);
+  if (P.self_collide)
+    hipLaunchKernelGGL((gs_phys::k_pd_step_terr<T, true>), dim3((B.N + LB - 1) / LB), dim3(gs_phys::kTerrWave), 0, st, M, P,
+                       B, A);
+  else
+    hipLaunchKernelGGL((gs_phys::k_pd_step_terr<T, false>), dim3((B.N + LB - 1) / LB), dim3(gs_phys::kTerrWave), 0, st, M, P,
+                       B, A);
   return hipGetLastError();
 }

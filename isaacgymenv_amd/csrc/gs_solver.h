@@ -199,7 +199,8 @@ GS_HD void body_poses(const DevModel* __restrict__ M, const EnvState<T>& s, floa
 // QS > 0 (TERR kernels): the terrain queries of this substep were already run by the whole workgroup
 // (terrain_queries, gs_physics.hip) and `qres` holds this env's results, [5 * c + k][QS] for
 // candidate c: (found, separation, normal xyz); QS == 0 runs each candidate's query inline.
-template <class T, bool TERR, int LB = LaneCfg<T, TERR>::LB, int QS = 0>
+// SELF = false compiles the self-collision path out (kernels launched for sims without it)
+template <class T, bool TERR, int LB = LaneCfg<T, TERR>::LB, int QS = 0, bool SELF = true>
 GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvState<T>& s,
                                         const float* tau, const float* __restrict__ mu_g, int N, int e, float* lds,
                                         float* __restrict__ cf_soa, bool collect, float* __restrict__ sens_soa,
@@ -218,7 +219,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
   constexpr int PE = PoolCfg<T>::PE;
   float* pool = lds + XP * LB;
   int npc = 0;
-  if constexpr (T::NPK > 0) {
+  if constexpr (T::NPK > 0 && SELF) {
     if (P.self_collide) {
       float Rb[NB][9], Xb[NB][3];
       body_poses<T>(M, s, Rb, Xb);
@@ -337,7 +338,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
 
     // ---- self-contact rows, column of body i's dof: n.(v_A(x) - v_B(x)) takes S_i's velocity at x when i is on
     // A's path and minus it on B's (a common ancestor's column cancels; the base columns always do)
-    if constexpr (T::NPK > 0) {
+    if constexpr (T::NPK > 0 && SELF) {
       if (i > 0) {
         const int col = NB6 + T::bdof[i];
         for (int p = 0; p < npc; ++p) {
@@ -725,7 +726,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
   }
 
   // ---------------- self-contact rows: dense J over the tree -> c = J nu_f, scaled Z = (L^-T J^T) D^-1/2, 1/diag
-  if constexpr (T::NPK > 0) {
+  if constexpr (T::NPK > 0 && SELF) {
     for (int p = 0; p < npc; ++p) {
       float* o = pool + PE * p * LB;
 #pragma unroll
@@ -838,7 +839,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
         lamc[(3 * c + 2) * LB] = lam[2];
       }
     });
-    if constexpr (T::NPK > 0) {
+    if constexpr (T::NPK > 0 && SELF) {
       for (int p = 0; p < npc; ++p) {
         float* o = pool + PE * p * LB;
         const float sc = o[kPoolSep * LB];
@@ -957,7 +958,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
       cf_soa[(3 * b + 1) * N + e] = f1;
       cf_soa[(3 * b + 2) * N + e] = f2;
     }
-    if constexpr (T::NPK > 0) {  // self-contacts: +f on link A, -f on link B
+    if constexpr (T::NPK > 0 && SELF) {  // self-contacts: +f on link A, -f on link B
       for (int p = 0; p < npc; ++p) {
         const float* o = pool + PE * p * LB;
         const int la = (int)o[kPoolLA * LB], lb = (int)o[kPoolLB * LB];
@@ -1031,7 +1032,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
             for (int k = 0; k < 3; ++k) { f[k] -= n[k]; f[3 + k] -= fc[k]; }
           }
         }
-        if constexpr (T::NPK > 0) {
+        if constexpr (T::NPK > 0 && SELF) {
           for (int p = 0; p < npc; ++p) {
             const float* o = pool + PE * p * LB;
             const int ba = (int)o[kPoolBA * LB], bbd = (int)o[kPoolBB * LB];
@@ -1100,7 +1101,7 @@ GS_HD void candidate_centres(const DevModel* __restrict__ Min, const EnvState<T>
 
 // ---------------------------------------------------------------- per-env entry points
 // gym.simulate for env e: `substeps` substeps with constant dof forces [N][nd] (or zero)
-template <class T, bool TERR, int LB>
+template <class T, bool TERR, int LB, bool SELF = true>
 GS_HD void simulate_env(const DevModel* __restrict__ M, const DevParams& P, const SimBuffers& B,
                         const float* __restrict__ tau_aos, int e, float* lds) {
   const int N = B.N;
@@ -1111,7 +1112,7 @@ GS_HD void simulate_env(const DevModel* __restrict__ M, const DevParams& P, cons
   for (int j = 0; j < T::ND; ++j) tau[j] = tau_aos ? tau_aos[(size_t)e * T::ND + j] : 0.f;
   for (int sstep = 0; sstep < P.substeps; ++sstep) {
     const bool last = (sstep == P.substeps - 1) && P.collect;
-    substep<T, TERR, LB>(M, P, s, tau, B.mu, N, e, lds, B.cf, last, sstep == P.substeps - 1 ? B.sens : nullptr);
+    substep<T, TERR, LB, 0, SELF>(M, P, s, tau, B.mu, N, e, lds, B.cf, last, sstep == P.substeps - 1 ? B.sens : nullptr);
   }
   store_state<T>(B.state, N, e, s);
 }
@@ -1171,7 +1172,7 @@ GS_HD void pd_outputs(const DevModel* __restrict__ M, const DevParams& P, const 
 }
 
 // the fused decimation step (gs_pd_args, include/gymsim.h) for env e
-template <class T, bool TERR, int LB>
+template <class T, bool TERR, int LB, bool SELF = true>
 GS_HD void pd_step_env(const DevModel* __restrict__ M, const DevParams& P, const SimBuffers& B, const PdDev& A, int e,
                        float* lds) {
   const int N = B.N;
@@ -1185,7 +1186,7 @@ GS_HD void pd_step_env(const DevModel* __restrict__ M, const DevParams& P, const
   for (int it = 0; it < total; ++it) {
     if (it < n_pd && (it % sub) == 0) pd_torques<T>(A, e, s, it == 0, tau);
     const bool last = ((it % sub) == sub - 1) && P.collect;
-    substep<T, TERR, LB>(M, P, s, tau, B.mu, N, e, lds, B.cf, last, it == total - 1 ? B.sens : nullptr);
+    substep<T, TERR, LB, 0, SELF>(M, P, s, tau, B.mu, N, e, lds, B.cf, last, it == total - 1 ? B.sens : nullptr);
     if (it == n_pd - 1) pd_dof_out<T>(A, e, s);
   }
   pd_outputs<T>(M, P, B, A, e, s, tau);

@@ -92,7 +92,10 @@ struct CM {
   static constexpr int BODY = 25;  // jR 9 | jt 3 | axis 3 | mass 1 | com 3 | inertia 6
   static constexpr int CAND = BODY * CL;  // point 3 | radius 1
   static constexpr int DOF = CAND + 4 * CC;  // effort | vmax | armature
-  static constexpr int NP = DOF + 3 * CL;
+  // self-collision broadphase: each chain shape's core segment end points in its body frame (a sphere's
+  // centre twice) and its core radius
+  static constexpr int SHP = DOF + 3 * CL;
+  static constexpr int NP = SHP + (T::NPK > 0 ? 8 * T::T_SPC : 0);
   static constexpr int LANES = T::T_LANES;
 };
 
@@ -219,10 +222,24 @@ __device__ __forceinline__ void stage_chain_model(const DevModel* __restrict__ M
       const int j = (p - C::CAND) / 4, f = (p - C::CAND) - 4 * j;
       const int cand = T::T_RC + c * C::CC + j;
       v = f < 3 ? M->cpoint[cand][f] : M->cradius[cand];
-    } else {
+    } else if (p < C::SHP) {
       const int k = (p - C::DOF) / 3, f = (p - C::DOF) - 3 * k;
       const int d = c * C::CL + k;
       v = f == 0 ? M->effort[d] : (f == 1 ? M->vmax[d] : M->armature[d]);
+    } else {
+      const int j = (p - C::SHP) / 8, f = (p - C::SHP) - 8 * j;
+      const int sh = T::T_RS + c * T::T_SPC + j;
+      const int kind = M->shkind[sh];
+      const float hl = kind == 1 ? M->shsize[sh][1] : 0.f;  // capsules: segment; spheres (and others): centre
+      if (f < 6) {
+        const float sg = f < 3 ? -hl : hl;
+        const int a = f % 3;
+        v = kind == 0 || kind == 1 ? M->sht[sh][a] + sg * M->shR[sh][3 * a + 2] : M->shc[sh][a];
+      } else if (f == 6) {
+        v = kind == 0 || kind == 1 ? M->shm[sh] : M->shc[sh][3];
+      } else {
+        v = hl;  // half length: bounding sphere radius = hl + radius around the segment's midpoint
+      }
     }
     mdl[p * C::LANES + c] = v;
   }
@@ -306,78 +323,175 @@ constexpr int kTeamsPerBlock = kTeamBlock / 4;
 // in any team publishes the shapes' full poses and runs the narrowphase replicated in each lane of the team
 // (gs_pairs.h self_contacts: the same pair order and rules as the one-env-per-lane solver and the oracle).
 // Returns the team's self-contact count (the pool geometry is in the lane's own column).
+// Squared distance between segments p1q1 and p2q2, branch-free (Ericson's closest points with v_rcp: s from the
+// lines' closest points, t from s, s again from t, each clamped; a point segment has a = 0 or e = 0).  The
+// reciprocals' ~1 ulp error is covered by the broadphase's slack; the narrowphase recomputes exactly.
+__device__ __forceinline__ float seg_seg_d2(const float* p1, const float* q1, const float* p2, const float* q2) {
+  float d1[3], d2[3], r[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { d1[k] = q1[k] - p1[k]; d2[k] = q2[k] - p2[k]; r[k] = p1[k] - p2[k]; }
+  const float a = dot3f(d1, d1), e = dot3f(d2, d2), b = dot3f(d1, d2), c = dot3f(d1, r), f = dot3f(d2, r);
+  const float ia = a > 1e-12f ? __builtin_amdgcn_rcpf(a) : 0.f;
+  const float ie = e > 1e-12f ? __builtin_amdgcn_rcpf(e) : 0.f;
+  const float den = a * e - b * b;
+  float s = den > 1e-12f * a * e ? __builtin_amdgcn_fmed3f((b * f - c * e) * __builtin_amdgcn_rcpf(den), 0.f, 1.f) : 0.f;
+  const float t = __builtin_amdgcn_fmed3f((b * s + f) * ie, 0.f, 1.f);
+  s = __builtin_amdgcn_fmed3f((b * t - c) * ia, 0.f, 1.f);
+  float dd = 0.f;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float x = r[k] + s * d1[k] - t * d2[k];
+    dd += x * x;
+  }
+  return dd;
+}
+
+// shapes a < b of a topology collide (its self-collision pair table, gs_topologies.h)
 template <class T>
-__device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M, const DevParams& P,
-                                                  const float* __restrict__ mu_g, int N, int e, int lc,
-                                                  const float (&R0)[9], const float (&R)[T::T_CL][9],
+__host__ __device__ constexpr bool team_pair(int a, int b) {
+  for (int q = 0; q < T::NPAIR; ++q)
+    if (T::pair_a[q] == a && T::pair_b[q] == b) return true;
+  return false;
+}
+
+// Self-collision prepass of a team.  Broadphase in registers, every substep: each lane holds its
+// chain's shapes as core segments + radius (a sphere is a point segment; boxes / hulls their bounding sphere) and
+// the root's; it tests the pairs root x own chain, own chain x itself, own chain x chain lc+1 and (lanes 0, 1)
+// x chain lc+2, the neighbours' shapes arriving by DPP quad rotations -- the exact core distance for sphere /
+// capsule pairs, within contact_offset.  Only a wave with such a pair writes the shapes' full poses to the team's
+// LDS table and runs the narrowphase, replicated in each lane of the teams concerned (gs_pairs.h self_contacts:
+// the pair order and rules of the one-env-per-lane solver and the oracle).  Returns the team's self-contact count
+// (the pool in the lane's own column).
+template <class T>
+__device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M, const float* __restrict__ cm,
+                                                  const DevParams& P, const float* __restrict__ mu_g, int N, int e,
+                                                  int lc, const float (&R0)[9], const float (&R)[T::T_CL][9],
                                                   const float (&X)[T::T_CL][3], float* __restrict__ shw_tab,
                                                   float* __restrict__ pool) {
-  constexpr int TPW = kTeamsPerBlock, CL = T::T_CL;
-  const int team = threadIdx.x >> 2;
-  float* tab = shw_tab + team;
-  // bounding-sphere centres (relative to the root origin)
+  constexpr int TPW = kTeamsPerBlock, LN = T::T_LANES, SPC = T::T_SPC, RSH = T::T_RS;
+  using C = CM<T>;
+  // (conservative by a hair: the narrowphase recomputes the distance in another association order)
+  const float off = P.contact_offset * 1.001f + 1e-5f;
+  float p0[SPC][3], p1[SPC][3], rad[SPC], hl[SPC];
 #pragma unroll
-  for (int j = 0; j < T::T_SPC; ++j) {
-    constexpr int dummy = 0;
-    (void)dummy;
-    const int sh = T::T_RS + lc * T::T_SPC + j;
-    const int k = T::sh_body[T::T_RS + j] - 1;  // chain-local body (chain 0's layout, the same for every chain)
-    float t[3];
-    mat3vec(R[k], M->shc[sh], t);
+  for (int j = 0; j < SPC; ++j) {
+    const int k = T::sh_body[RSH + j] - 1;  // chain-local body (chain 0's layout, the same for every chain)
+    const float* sp = cm + (C::SHP + 8 * j) * LN;
+    const float l0[3] = {sp[0], sp[LN], sp[2 * LN]}, l1[3] = {sp[3 * LN], sp[4 * LN], sp[5 * LN]};
+    mat3vec(R[k], l0, p0[j]);
+    mat3vec(R[k], l1, p1[j]);
 #pragma unroll
-    for (int f = 0; f < 3; ++f) tab[(kShW * sh + 12 + f) * TPW] = X[k][f] + t[f];
+    for (int f = 0; f < 3; ++f) { p0[j][f] += X[k][f]; p1[j][f] += X[k][f]; }
+    rad[j] = sp[6 * LN];
+    hl[j] = sp[7 * LN];
   }
-  if (lc == 0) {
+  bool near = false;
+  // bounding spheres first (midpoint, half length + radius); the exact segment distance only where they meet
+  auto test = [&](const float* a0, const float* a1, float ra, float ha, const float* b0, const float* b1, float rb,
+                  float hb) {
+    const float rr = ra + rb + off;
+    float dc = 0.f;
 #pragma unroll
-    for (int sh = 0; sh < T::T_RS; ++sh) {
-      float t[3];
-      mat3vec(R0, M->shc[sh], t);
+    for (int k = 0; k < 3; ++k) {
+      const float x = 0.5f * ((a0[k] + a1[k]) - (b0[k] + b1[k]));
+      dc += x * x;
+    }
+    const float rs = rr + ha + hb;
+    if (dc < rs * rs) near = near || (seg_seg_d2(a0, a1, b0, b1) < rr * rr);
+  };
 #pragma unroll
-      for (int f = 0; f < 3; ++f) tab[(kShW * sh + 12 + f) * TPW] = t[f];
+  for (int sr = 0; sr < RSH; ++sr) {
+    const int kind = T::shkind[sr];
+    const bool seg = kind == 0 || kind == 1;
+    const float rhl = kind == 1 ? M->shsize[sr][1] : 0.f;
+    float l0[3], l1[3], r0[3], r1[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      l0[a] = seg ? M->sht[sr][a] - rhl * M->shR[sr][3 * a + 2] : M->shc[sr][a];
+      l1[a] = seg ? M->sht[sr][a] + rhl * M->shR[sr][3 * a + 2] : M->shc[sr][a];
+    }
+    mat3vec(R0, l0, r0);
+    mat3vec(R0, l1, r1);
+    const float rr = seg ? M->shm[sr] : M->shc[sr][3];
+#pragma unroll
+    for (int j = 0; j < SPC; ++j)
+      if (team_pair<T>(sr, RSH + j)) test(r0, r1, rr, rhl, p0[j], p1[j], rad[j], hl[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < SPC; ++j)
+#pragma unroll
+    for (int j2 = j + 1; j2 < SPC; ++j2)
+      if (team_pair<T>(RSH + j, RSH + j2)) test(p0[j], p1[j], rad[j], hl[j], p0[j2], p1[j2], rad[j2], hl[j2]);
+  // chains lc + 1 (every lane) and lc + 2 (lanes 0 and 1): each inter-chain pair exactly once
+#pragma unroll
+  for (int dl = 1; dl <= 2; ++dl) {
+    float q0[SPC][3], q1[SPC][3];
+#pragma unroll
+    for (int j = 0; j < SPC; ++j) {
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+        q0[j][f] = dl == 1 ? qperm<0x39>(p0[j][f]) : qperm<0x4E>(p0[j][f]);
+        q1[j][f] = dl == 1 ? qperm<0x39>(p1[j][f]) : qperm<0x4E>(p1[j][f]);
+      }
+    }
+    if (dl == 1 || lc < 2) {
+#pragma unroll
+      for (int j = 0; j < SPC; ++j)
+#pragma unroll
+        for (int j2 = 0; j2 < SPC; ++j2)
+          if (team_pair<T>(RSH + j, RSH + SPC + j2)) test(p0[j], p1[j], rad[j], hl[j], q0[j2], q1[j2], rad[j2], hl[j2]);
     }
   }
-  __syncthreads();
-  bool near = false;
-  for (int q = lc; q < M->np; q += 4) {
-    const int a = M->pa[q], b = M->pb[q];
-    const float d[3] = {tab[(kShW * a + 12) * TPW] - tab[(kShW * b + 12) * TPW],
-                        tab[(kShW * a + 13) * TPW] - tab[(kShW * b + 13) * TPW],
-                        tab[(kShW * a + 14) * TPW] - tab[(kShW * b + 14) * TPW]};
-    const float rr = M->shc[a][3] + M->shc[b][3] + P.contact_offset;
-    near = near || (d[0] * d[0] + d[1] * d[1] + d[2] * d[2] < rr * rr);
-  }
-  if (__ballot(near) == 0ull) return 0;  // wave-uniform: no team of the wave has a near pair
-  // full shape poses for the narrowphase
+  if (__ballot(near) == 0ull) return 0;  // wave-uniform: no team of the wave has a pair within contact_offset
+#ifdef GS_PHASE_PROFILE
+  if ((threadIdx.x & 63) == 0) atomicAdd(&gs_phase_cycles[12], 1ull);  // substeps a wave runs the narrowphase
+  const long long np_t0 = clock64();
+#endif
+  const int team = threadIdx.x >> 2;
+  float* tab = shw_tab + team;
+  __syncthreads();  // an earlier substep's narrowphase may still be reading the table
+  // full shape poses for the narrowphase: R (9), centre (3), bounding-sphere centre (3)
 #pragma unroll
   for (int j = 0; j < T::T_SPC; ++j) {
     const int sh = T::T_RS + lc * T::T_SPC + j;
     const int k = T::sh_body[T::T_RS + j] - 1;
-    float Rs[9], t[3];
+    float Rs[9], t[3], c[3];
     mat3mul(R[k], M->shR[sh], Rs);
     mat3vec(R[k], M->sht[sh], t);
+    mat3vec(R[k], M->shc[sh], c);
 #pragma unroll
     for (int f = 0; f < 9; ++f) tab[(kShW * sh + f) * TPW] = Rs[f];
 #pragma unroll
-    for (int f = 0; f < 3; ++f) tab[(kShW * sh + 9 + f) * TPW] = X[k][f] + t[f];
+    for (int f = 0; f < 3; ++f) {
+      tab[(kShW * sh + 9 + f) * TPW] = X[k][f] + t[f];
+      tab[(kShW * sh + 12 + f) * TPW] = X[k][f] + c[f];
+    }
   }
   if (lc == 0) {
 #pragma unroll
     for (int sh = 0; sh < T::T_RS; ++sh) {
-      float Rs[9], t[3];
+      float Rs[9], t[3], c[3];
       mat3mul(R0, M->shR[sh], Rs);
       mat3vec(R0, M->sht[sh], t);
+      mat3vec(R0, M->shc[sh], c);
 #pragma unroll
       for (int f = 0; f < 9; ++f) tab[(kShW * sh + f) * TPW] = Rs[f];
 #pragma unroll
-      for (int f = 0; f < 3; ++f) tab[(kShW * sh + 9 + f) * TPW] = t[f];
+      for (int f = 0; f < 3; ++f) {
+        tab[(kShW * sh + 9 + f) * TPW] = t[f];
+        tab[(kShW * sh + 12 + f) * TPW] = c[f];
+      }
     }
   }
   __syncthreads();
   // any lane of the team near -> the team's narrowphase (replicated, team-uniform result)
   const bool tnear = quad_sum(near ? 1.f : 0.f) > 0.f;
-  if (!tnear) return 0;
-  return self_contacts<T, TPW, RW, RowSlots<T>::PER_POOL>(M, P, mu_g, N, e, tab, pool);
-  (void)CL;
+  int cnt = 0;
+  if (tnear) cnt = self_contacts<T, TPW, RW, RowSlots<T>::PER_POOL>(M, P, mu_g, N, e, tab, pool);
+#ifdef GS_PHASE_PROFILE
+  if ((threadIdx.x & 63) == 0) atomicAdd(&gs_phase_cycles[13], (unsigned long long)(clock64() - np_t0));
+#endif
+  return cnt;
 }
 
 template <class T>
@@ -521,14 +635,14 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     }
   }
 
+  GS_PROF(0)  // root + chain forward pass + contact Jacobians
   // ================= self-collision prepass (rare narrowphase; the pool rows are built with the contact records)
   int npc = 0;
   float* pool = rows_own + RS::POOL * RW;
   if constexpr (T::NPK > 0) {
-    if (P.self_collide) npc = team_self_contacts<T>(M, P, mu_g, N, e, lc, R0, R, X, shw_tab, pool);
+    if (P.self_collide) npc = team_self_contacts<T>(M, cm, P, mu_g, N, e, lc, R0, R, X, shw_tab, pool);
   }
-
-  GS_PROF(0)  // root + chain forward pass + contact Jacobians
+  GS_PROF(11)  // self-collision prepass
   // ================= chain backward pass: composite inertia / force, bias, chain rows of M
   float Mcc[CL][CL], Mcb[CL][6], biasc[CL];
 #pragma unroll

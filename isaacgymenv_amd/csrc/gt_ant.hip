@@ -15,6 +15,7 @@
 #include <cstdio>
 
 #include "../../include/gymtask.h"
+#include "torch_philox.h"
 
 void gt_set_last_error(const char* msg);
 
@@ -149,6 +150,7 @@ __global__ void __launch_bounds__(64) k_ant_tail(gt_ant_params p, gt_ant_buffers
   // done count: one 64-bit atomic per wave {waves done << 32 | count}; the grid's last wave publishes
   // {count, seq} to host memory and re-arms the accumulator (the protocol of gt_anymal_post_physics_a)
   const unsigned long long m = __ballot(done);
+  if (b.reset_masks && (threadIdx.x & 63) == 0) b.reset_masks[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = m;
   if ((threadIdx.x & 63) == 0) {
     const unsigned nwaves = (gridDim.x * blockDim.x + 63) / 64;
     unsigned long long* acc = reinterpret_cast<unsigned long long*>(b.reset_count);
@@ -166,7 +168,70 @@ __global__ void __launch_bounds__(64) k_ant_tail(gt_ant_params p, gt_ant_buffers
   }
 }
 
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// reset_idx of the flagged envs (gymtask.h gt_ant_reset_flagged): one lane per env, one wave per workgroup;
+// a flagged env's rank among all flagged envs is the exclusive prefix of the earlier waves' ballot popcounts
+__global__ void __launch_bounds__(64) k_ant_reset_flagged(gt_ant_params p, gt_ant_buffers b, gt_ant_reset_args r) {
+  constexpr int ND = 8;
+  const int lane = threadIdx.x, w = blockIdx.x, e = w * 64 + lane;
+  int base = 0;
+  for (int c = 0; c < w; c += 64) {
+    const int i = c + lane;
+    base += wave_sum_i(i < w ? (int)__popcll(b.reset_masks[i]) : 0);
+  }
+  const unsigned long long mine = b.reset_masks[w];
+  if (e >= p.num_envs || !((mine >> lane) & 1ull)) return;
+  const int t = base + (int)__popcll(mine & ((1ull << lane) - 1ull));
+  float* ds = r.dof_state + (size_t)e * ND * 2;
+#pragma unroll
+  for (int j = 0; j < ND; ++j) {
+    const size_t q = (size_t)t * ND + j;
+    const float up = r.u_pos ? r.u_pos[q] : torch_philox::rand_at(r.plan_pos, q);
+    const float uv = r.u_vel ? r.u_vel[q] : torch_philox::rand_at(r.plan_vel, q);
+    const float off = r.pos_range * up + r.pos_lower;  // torch_rand_float: (upper - lower) * rand + lower
+    const float x = r.initial_dof_pos[(size_t)e * ND + j] + off;
+    ds[2 * j] = fmaxf(fminf(x, p.dof_upper[j]), p.dof_lower[j]);  // tensor_clamp = max(min(t, upper), lower)
+    ds[2 * j + 1] = r.vel_range * uv + r.vel_lower;
+  }
+  const float* tg = b.targets + (size_t)e * 3;
+  const float* ir = r.initial_root_states + (size_t)e * 13;
+  const float px = tg[0] - ir[0], py = tg[1] - ir[1], pz = 0.0f;
+  // -torch.norm(planar) / dt: ATen divides by a host scalar as a product with its float reciprocal
+  const float prev = -sqrtf(px * px + py * py + pz * pz) * (1.0f / p.dt);
+  b.prev_potentials[e] = prev;
+  b.potentials[e] = prev;
+  r.progress_buf[e] = 0;
+  b.reset_buf[e] = 0;
+  r.env_ids_out[t] = e;
+}
+
 }  // namespace
+
+extern "C" int gt_ant_reset_flagged(const gt_ant_params* p, const gt_ant_buffers* b, int k, const gt_ant_reset_args* r,
+                                    void* stream) {
+  if (!p || !b || !r || p->num_envs <= 0 || p->num_dofs != 8 || !b->reset_masks || !b->targets || !b->potentials ||
+      !b->prev_potentials || !b->reset_buf || !r->initial_dof_pos || !r->initial_root_states || !r->dof_state ||
+      !r->progress_buf || !r->env_ids_out || k < 0 || k > p->num_envs ||
+      (!r->u_pos && r->plan_pos.numel != (uint32_t)k * 8u) || (!r->u_vel && r->plan_vel.numel != (uint32_t)k * 8u)) {
+    gt_set_last_error("gt_ant_reset_flagged: invalid parameters, null buffers or plans that do not cover k x 8");
+    return -1;
+  }
+  if (k == 0) return 0;
+  hipLaunchKernelGGL(k_ant_reset_flagged, dim3((p->num_envs + 63) / 64), dim3(64), 0, (hipStream_t)stream, *p, *b, *r);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    char buf[256];
+    std::snprintf(buf, sizeof(buf), "gt_ant_reset_flagged: %s", hipGetErrorString(e));
+    gt_set_last_error(buf);
+    return -1;
+  }
+  return 0;
+}
 
 extern "C" int gt_ant_post_physics(const gt_ant_params* p, const gt_ant_buffers* b, void* stream) {
   if (!p || !b || p->num_envs <= 0 || p->num_dofs != 8 || !b->root_states || !b->dof_state || !b->sensors ||

@@ -112,7 +112,16 @@ class GtAntBuffers(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("root_states", "dof_state", "sensors", "actions", "targets",
                                           "inv_start_rot", "potentials", "prev_potentials", "up_vec",
                                           "heading_vec", "obs_buf", "rew_buf", "true_objective", "reset_buf",
-                                          "progress_buf", "reset_count", "host_count")] + [("seq", C.c_int32)]
+                                          "progress_buf", "reset_count", "host_count")] + [("seq", C.c_int32),
+                                                                                           ("reset_masks", C.c_void_p)]
+
+
+class GtAntResetArgs(C.Structure):
+    _fields_ = [("plan_pos", GtTorchRandPlan), ("plan_vel", GtTorchRandPlan), ("u_pos", C.c_void_p),
+                ("u_vel", C.c_void_p)] + [(n, C.c_float) for n in ("pos_range", "pos_lower", "vel_range",
+                                                                     "vel_lower")] + [
+        (n, C.c_void_p) for n in ("initial_dof_pos", "initial_root_states", "dof_state", "progress_buf",
+                                  "env_ids_out")]
 
 
 _lib = None
@@ -139,7 +148,9 @@ def lib():
                                                   vp],
                            "gt_hound_control": [C.POINTER(GtHoundControlParams), vp, vp, vp, vp, vp, vp, vp, vp,
                                                 vp],
-                           "gt_ant_post_physics": [C.POINTER(GtAntParams), C.POINTER(GtAntBuffers), vp]}.items():
+                           "gt_ant_post_physics": [C.POINTER(GtAntParams), C.POINTER(GtAntBuffers), vp],
+                           "gt_ant_reset_flagged": [C.POINTER(GtAntParams), C.POINTER(GtAntBuffers), i,
+                                                    C.POINTER(GtAntResetArgs), vp]}.items():
             fn = getattr(L, name)
             fn.restype = C.c_int
             fn.argtypes = args
@@ -152,7 +163,7 @@ def lib():
 EXPORTED_SYMBOLS = ["gt_abi_version", "gt_last_error", "gt_anymal_post_physics_a", "gt_anymal_reset",
                     "gt_anymal_post_physics_b", "gt_anymal_reset_flagged", "gt_torch_rand", "gt_host_alloc",
                     "gt_host_free", "gt_wait_host_seq", "gt_measure_heights", "gt_hound_control",
-                    "gt_ant_post_physics"]
+                    "gt_ant_post_physics", "gt_ant_reset_flagged"]
 
 
 class AntTailKernel:
@@ -181,6 +192,9 @@ class AntTailKernel:
         self._seq = 0
         self._launched = False
         self._count = C.c_int32(0)
+        self.reset_masks = torch.zeros((t.num_envs + 63) // 64, dtype=torch.int64, device=t.device)
+        self.env_ids = torch.zeros(t.num_envs, dtype=torch.int32, device=t.device)
+        self.planner = TorchRandPlanner(t.device)
 
     def __del__(self):
         if getattr(self, "_host_words", None) and _lib is not None:
@@ -195,7 +209,34 @@ class AntTailKernel:
                "gt_wait_host_seq")
         return int(self._count.value)
 
-    def __call__(self):
+    def reset_flagged(self, k: int, u_pos=None, u_vel=None):
+        """ant.py:252-279 reset_idx for the k envs the previous launch flagged, in one kernel: the two
+        torch_rand_float draws evaluated in-kernel from the device generator (advanced exactly as torch.rand
+        would be) or taken from u_pos / u_vel [k, 8], the clamped dof state, potentials, counters; then the
+        reference's two indexed state sets.  Returns the flagged env ids (int32 [k])."""
+        from .isaacgym import gymtorch
+        t = self.env
+        r = GtAntResetArgs()
+        if u_pos is None:
+            r.plan_pos, r.plan_vel = self.planner.plan_many((k * t.num_dof, k * t.num_dof))
+        else:
+            r.u_pos, r.u_vel = u_pos.contiguous().data_ptr(), u_vel.contiguous().data_ptr()
+        # torch_rand_float(lower, upper): (upper - lower) * rand + lower, the range a Python double
+        r.pos_range, r.pos_lower = 0.2 - (-0.2), -0.2
+        r.vel_range, r.vel_lower = 0.1 - (-0.1), -0.1
+        r.initial_dof_pos, r.initial_root_states = t.initial_dof_pos.data_ptr(), t.initial_root_states.data_ptr()
+        r.dof_state, r.progress_buf, r.env_ids_out = t.dof_state.data_ptr(), t.progress_buf.data_ptr(), \
+            self.env_ids.data_ptr()
+        stream = torch.cuda.current_stream(t.root_states.device).cuda_stream
+        _check(lib().gt_ant_reset_flagged(C.byref(self.p), C.byref(self._buffers()), k, C.byref(r),
+                                          C.c_void_p(stream)), "gt_ant_reset_flagged")
+        ids = self.env_ids[:k]
+        t.gym.set_actor_root_state_tensor_indexed(t.sim, gymtorch.unwrap_tensor(t.initial_root_states),
+                                                  gymtorch.unwrap_tensor(ids), k)
+        t.gym.set_dof_state_tensor_indexed(t.sim, gymtorch.unwrap_tensor(t.dof_state), gymtorch.unwrap_tensor(ids), k)
+        return ids
+
+    def _buffers(self):
         t = self.env
         b = GtAntBuffers()
         for name, ten in (("root_states", t.root_states), ("dof_state", t.dof_state), ("sensors", t.vec_sensor_tensor),
@@ -207,10 +248,16 @@ class AntTailKernel:
             assert ten.is_contiguous() and ten.is_cuda, name
             setattr(b, name, ten.data_ptr())
         assert t.reset_buf.dtype == torch.int64 and t.progress_buf.dtype == torch.int64
-        self._seq += 1
         b.seq = self._seq
         b.reset_count = self.reset_count.data_ptr()
         b.host_count = self._host_words_dev
+        b.reset_masks = self.reset_masks.data_ptr()
+        return b
+
+    def __call__(self):
+        t = self.env
+        self._seq += 1
+        b = self._buffers()
         stream = torch.cuda.current_stream(t.root_states.device).cuda_stream
         _check(lib().gt_ant_post_physics(C.byref(self.p), C.byref(b), C.c_void_p(stream)), "gt_ant_post_physics")
         self._launched = True

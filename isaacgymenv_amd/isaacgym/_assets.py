@@ -49,6 +49,22 @@ SHAPE_SPHERE, SHAPE_CAPSULE, SHAPE_BOX, SHAPE_CYLINDER, SHAPE_CONVEX = 0, 1, 2, 
 
 # ground contact slots of a convex hull (dynamic 4-point manifold over its vertices)
 HULL_SLOTS = 4
+# vertices of a hull's self-collision core (farthest-point sample of its vertices; the ground keeps them all):
+# UsefulHound's arm hulls (16-473 vertices) lose at most 2.5 mm of their surface
+HULL_PAIR_VERTS = 48
+
+
+def farthest_point_sample(v: np.ndarray, n: int) -> np.ndarray:
+    """Indices (ascending) of n points of v: the one farthest from the centroid, then repeatedly the point
+    farthest from those chosen (first index on ties)."""
+    c = v.mean(0)
+    idx = [int(np.argmax(np.linalg.norm(v - c, axis=1)))]
+    d = np.linalg.norm(v - v[idx[0]], axis=1)
+    while len(idx) < min(n, len(v)):
+        i = int(np.argmax(d))
+        idx.append(i)
+        d = np.minimum(d, np.linalg.norm(v - v[i], axis=1))
+    return np.sort(np.array(idx, dtype=np.int64))
 # pair narrowphase kinds (DESIGN.md 3.12): closed forms for sphere/capsule pairs, GJK on margin-rounded cores
 PAIR_SS, PAIR_SC, PAIR_CC, PAIR_GJK = 0, 1, 2, 3
 # self-contact slots per env (the pool the solver fills in pair order), per articulation size
@@ -464,12 +480,14 @@ class Articulation:
         core radius of the pair narrowphase: sphere / capsule radius; boxes, cylinders and hulls are rounded
         by m = min(0.01, a quarter of their smallest half extent)), bounding sphere (centre, radius) and,
         for hulls, the vertices (body frame) with the factor f that moves each toward the vertex centroid
-        by the margin (core vertex = c + f (v - c))."""
+        by the margin (core vertex = c + f (v - c)), and the HULL_PAIR_VERTS of them (pverts, pf) the pair
+        narrowphase uses."""
         out, links = [], self.shape_links_all()
         s_index = 0
         for bi, b in enumerate(self.bodies):
             for s in b.shapes:
-                d = dict(body=bi, link=links[s_index], R=s.pose.R.copy(), t=s.pose.t.copy(), verts=None, f=None)
+                d = dict(body=bi, link=links[s_index], R=s.pose.R.copy(), t=s.pose.t.copy(), verts=None, f=None,
+                         pverts=None, pf=None)
                 if s.kind == SHAPE_SPHERE:
                     r = float(s.size[0])
                     d.update(kind=0, size=[r, 0.0, 0.0], margin=r, centre=s.pose.t.copy(), radius=r)
@@ -491,8 +509,10 @@ class Articulation:
                     dist = np.linalg.norm(v - c, axis=1)
                     half = 0.5 * (v.max(0) - v.min(0))
                     m = min(0.01, 0.25 * float(half.min()))
+                    f = np.where(dist > m, 1.0 - m / np.maximum(dist, 1e-12), 0.0)
+                    pi = farthest_point_sample(v, HULL_PAIR_VERTS)
                     d.update(kind=4, size=[0.0, 0.0, 0.0], margin=m, centre=c, radius=float(dist.max()),
-                             R=np.eye(3), t=np.zeros(3), verts=v, f=np.where(dist > m, 1.0 - m / np.maximum(dist, 1e-12), 0.0))
+                             R=np.eye(3), t=np.zeros(3), verts=v, f=f, pverts=v[pi], pf=f[pi])
                 out.append(d)
                 s_index += 1
         return out

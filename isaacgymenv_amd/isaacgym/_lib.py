@@ -28,7 +28,8 @@ class GsModelDesc(C.Structure):
                                   "shape_margin", "shape_sphere")] + [
         ("num_hull_verts", C.c_int32), ("hull_verts", C.c_void_p), ("shape_hv0", C.c_void_p),
         ("shape_hv1", C.c_void_p), ("num_pairs", C.c_int32), ("pair_a", C.c_void_p), ("pair_b", C.c_void_p),
-        ("pair_kind", C.c_void_p), ("pair_pool", C.c_int32)]
+        ("pair_kind", C.c_void_p), ("pair_pool", C.c_int32), ("num_pair_verts", C.c_int32), ("pair_verts", C.c_void_p),
+        ("shape_pv0", C.c_void_p), ("shape_pv1", C.c_void_p)]
 
 
 class GsSimParams(C.Structure):
@@ -136,11 +137,13 @@ def model_desc(flat: dict):
              ("shape_size", "shsize", np.float64), ("shape_margin", "shmargin", np.float64),
              ("shape_sphere", "shsphere", np.float64), ("hull_verts", "hverts", np.float64),
              ("shape_hv0", "shv0", np.int32), ("shape_hv1", "shv1", np.int32), ("pair_a", "pair_a", np.int32),
-             ("pair_b", "pair_b", np.int32), ("pair_kind", "pair_kind", np.int32)]
+             ("pair_b", "pair_b", np.int32), ("pair_kind", "pair_kind", np.int32), ("pair_verts", "pverts", np.float64),
+             ("shape_pv0", "shp0", np.int32), ("shape_pv1", "shp1", np.int32)]
     m.num_links = flat["nr"]
     m.num_hull_verts = len(flat["hverts"])
     m.num_pairs = int(flat["npair"])
     m.pair_pool = int(flat["npool"])
+    m.num_pair_verts = len(flat["pverts"])
     for field, key, dt in pairs:
         a = np.ascontiguousarray(flat[key], dtype=dt)
         if a.size == 0:

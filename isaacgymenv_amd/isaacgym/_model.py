@@ -14,7 +14,8 @@ The same flat arrays feed the product library (``gs_sim_set_model`` in
 * ``cdyn[nc]``: hull slot of a convex hull's dynamic ground candidate (0..3), -1 for fixed points
 * shapes (``Articulation.shape_table``): ``shkind``, ``shbody``, ``shlink`` [ns]; ``shpose[ns][12]`` (body
   frame); ``shsize[ns][3]``; ``shmargin[ns]``; ``shsphere[ns][4]`` (bounding sphere, body frame);
-  hull vertices ``hverts[nhv][4]`` (body frame xyz, core factor f) with ``shv0``/``shv1`` [ns] ranges
+  hull vertices ``hverts[nhv][4]`` (body frame xyz, core factor f) with ``shv0``/``shv1`` [ns] ranges, and the
+  self-collision core's subset ``pverts[npv][4]`` with ``shp0``/``shp1``
 * self-collision pairs (``Articulation.self_collision_pairs``): ``npair``, ``pair_a``, ``pair_b``,
   ``pair_kind`` [npair]; ``npool`` self-contact slots per env
 """
@@ -68,14 +69,17 @@ def flatten(art: Articulation, armature: float | None = None) -> dict:
     tab = art.shape_table()
     ns = len(tab)
     shpose = np.zeros((ns, 12))
-    hv, shv0, shv1 = [], [], []
+    hv, shv0, shv1, pv, shp0, shp1 = [], [], [], [], [], []
     for i, d in enumerate(tab):
         shpose[i, :9] = d["R"].reshape(-1)
         shpose[i, 9:] = d["t"]
         shv0.append(len(hv))
+        shp0.append(len(pv))
         if d["verts"] is not None:
             hv += [list(v) + [float(f)] for v, f in zip(d["verts"], d["f"])]
+            pv += [list(v) + [float(f)] for v, f in zip(d["pverts"], d["pf"])]
         shv1.append(len(hv))
+        shp1.append(len(pv))
     pairs = art.self_collision_pairs() if not art.fixed_base else []
     return dict(
         nb=nb, nd=nd, nc=nc, ns=art.num_shapes, fixed_base=int(art.fixed_base),
@@ -100,6 +104,8 @@ def flatten(art: Articulation, armature: float | None = None) -> dict:
         shsphere=np.array([list(d["centre"]) + [d["radius"]] for d in tab], dtype=np.float64).reshape(ns, 4),
         hverts=np.array(hv, dtype=np.float64).reshape(len(hv), 4),
         shv0=np.array(shv0, dtype=np.int32).reshape(ns), shv1=np.array(shv1, dtype=np.int32).reshape(ns),
+        pverts=np.array(pv, dtype=np.float64).reshape(len(pv), 4),
+        shp0=np.array(shp0, dtype=np.int32).reshape(ns), shp1=np.array(shp1, dtype=np.int32).reshape(ns),
         npair=len(pairs),
         pair_a=np.array([p[0] for p in pairs], dtype=np.int32).reshape(len(pairs)),
         pair_b=np.array([p[1] for p in pairs], dtype=np.int32).reshape(len(pairs)),

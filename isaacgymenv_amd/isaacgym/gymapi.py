@@ -388,7 +388,8 @@ class Sim:
         if len(filters) > 1:
             raise NotImplementedError("actors with and without self-collision (collision filter 0) in one sim "
                                       "(DESIGN.md section 6)")
-        self.self_collide = bool(filters.pop()) and int(flat["npair"]) > 0
+        # (GS_SELF_COLLIDE=0 turns the pairs off: an A/B knob for measurements, not a product setting)
+        self.self_collide = bool(filters.pop()) and int(flat["npair"]) > 0 and os.environ.get("GS_SELF_COLLIDE", "1") != "0"
         _lib.check(L.gs_sim_set_self_collision(self.handle, int(self.self_collide)), "gs_sim_set_self_collision")
         sens = [b for b, _ in self.asset.sensors]
         if sens:

@@ -178,10 +178,12 @@ class Ant(VecTask):
         if self._tail is not None:
             # the previous step's kernel published how many envs it flagged: look for them only then
             k = self._tail.done_count()
-            if k is None or k > 0:
+            if k is None:  # before the first launch: no ballots yet
                 env_ids = self.reset_buf.nonzero(as_tuple=False).flatten()
                 if len(env_ids) > 0:
                     self.reset_idx(env_ids)
+            elif k > 0:  # reset_idx fused (gt_ant_reset_flagged): no nonzero() host sync
+                self._tail.reset_flagged(k)
             self.gym.refresh_dof_state_tensor(self.sim)
             self.gym.refresh_actor_root_state_tensor(self.sim)
             self.gym.refresh_force_sensor_tensor(self.sim)

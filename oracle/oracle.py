@@ -28,7 +28,8 @@ class OModel(C.Structure):
         (n, C.c_void_p) for n in ("cdyn", "shkind", "shbody", "shlink", "shpose", "shsize", "shmargin", "shsphere",
                                   "hverts", "shv0", "shv1")] + [
         ("npair", C.c_int32), ("pair_a", C.c_void_p), ("pair_b", C.c_void_p), ("pair_kind", C.c_void_p),
-        ("npool", C.c_int32), ("self_collide", C.c_int32)]
+        ("npool", C.c_int32), ("self_collide", C.c_int32), ("pverts", C.c_void_p), ("shp0", C.c_void_p),
+        ("shp1", C.c_void_p)]
 
 
 class OParams(C.Structure):
@@ -90,12 +91,12 @@ class OracleSim:
             setattr(m, k, int(flat[k]))
         m.nr = int(flat.get("nr", flat["nb"]))
         for k in ("parent", "jkind", "bdof", "cbody", "cshape", "has_limits", "clink", "cdyn", "shkind", "shbody",
-                  "shlink", "shv0", "shv1", "pair_a", "pair_b", "pair_kind"):
+                  "shlink", "shv0", "shv1", "pair_a", "pair_b", "pair_kind", "shp0", "shp1"):
             a = np.ascontiguousarray(flat[k], dtype=np.int32)
             keep[k] = a
             setattr(m, k, a.ctypes.data)
         for k in ("jorigin", "jaxis", "mass", "com", "inertia", "cpoint", "cradius", "effort", "vmax", "armature",
-                  "lower", "upper", "shpose", "shsize", "shmargin", "shsphere", "hverts"):
+                  "lower", "upper", "shpose", "shsize", "shmargin", "shsphere", "hverts", "pverts"):
             a = np.ascontiguousarray(flat[k], dtype=np.float64)
             keep[k] = a
             setattr(m, k, a.ctypes.data)

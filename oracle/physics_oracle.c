@@ -95,6 +95,8 @@ typedef struct {
     const int32_t *pair_a, *pair_b, *pair_kind; /* [npair] shape a < shape b; 0 SS 1 SC 2 CC 3 GJK */
     int32_t npool;              /* self-contact slots per env (pair order, later contacts dropped) */
     int32_t self_collide;       /* filter-0 actor: self-collision pairs enabled */
+    const double *pverts;       /* [npv][4] a hull's self-collision core vertices (subset of hverts) */
+    const int32_t *shp0, *shp1; /* [ns] their range */
 } OModel;
 
 typedef struct {
@@ -341,8 +343,8 @@ static void core_support(const OModel *m, int sh, const ShapeW *W, const real *R
                   Rb[2] * d[0] + Rb[5] * d[1] + Rb[8] * d[2]};
     const double *cc = m->shsphere + 4 * sh;
     real best = -1e300, bv[3] = {0, 0, 0};
-    for (int k = m->shv0[sh]; k < m->shv1[sh]; ++k) {
-        const double *v = m->hverts + 4 * k;
+    for (int k = m->shp0[sh]; k < m->shp1[sh]; ++k) {
+        const double *v = m->pverts + 4 * k;
         const real f = (real)v[3];
         const real p[3] = {cc[0] + f * (v[0] - cc[0]), cc[1] + f * (v[1] - cc[1]), cc[2] + f * (v[2] - cc[2])};
         const real t = dot3(p, dl);
@@ -407,8 +409,8 @@ static real core_feature(const OModel *m, int sh, const ShapeW *W, const real *R
                         Rb[2] * d[0] + Rb[5] * d[1] + Rb[8] * d[2]};
     const double *cc = m->shsphere + 4 * sh;
     real hmax = -1e300;
-    for (int k = m->shv0[sh]; k < m->shv1[sh]; ++k) {
-        const double *v = m->hverts + 4 * k;
+    for (int k = m->shp0[sh]; k < m->shp1[sh]; ++k) {
+        const double *v = m->pverts + 4 * k;
         const real f = (real)v[3];
         const real p[3] = {cc[0] + f * (v[0] - cc[0]), cc[1] + f * (v[1] - cc[1]), cc[2] + f * (v[2] - cc[2])};
         const real h = dot3(p, dl);
@@ -416,16 +418,16 @@ static real core_feature(const OModel *m, int sh, const ShapeW *W, const real *R
     }
     real acc[3] = {0, 0, 0};
     int n = 0;
-    for (int k = m->shv0[sh]; k < m->shv1[sh]; ++k) {
-        const double *v = m->hverts + 4 * k;
+    for (int k = m->shp0[sh]; k < m->shp1[sh]; ++k) {
+        const double *v = m->pverts + 4 * k;
         const real f = (real)v[3];
         const real p[3] = {cc[0] + f * (v[0] - cc[0]), cc[1] + f * (v[1] - cc[1]), cc[2] + f * (v[2] - cc[2])};
         if (dot3(p, dl) >= hmax - FEATURE_EPS) { for (int t = 0; t < 3; ++t) acc[t] += p[t]; ++n; }
     }
     for (int t = 0; t < 3; ++t) acc[t] /= n;
     real ext = 0;
-    for (int k = m->shv0[sh]; k < m->shv1[sh]; ++k) {
-        const double *v = m->hverts + 4 * k;
+    for (int k = m->shp0[sh]; k < m->shp1[sh]; ++k) {
+        const double *v = m->pverts + 4 * k;
         const real f = (real)v[3];
         const real p[3] = {cc[0] + f * (v[0] - cc[0]), cc[1] + f * (v[1] - cc[1]), cc[2] + f * (v[2] - cc[2])};
         if (dot3(p, dl) >= hmax - FEATURE_EPS) {
@@ -451,7 +453,7 @@ static int simplex_closest(real W[4][3], int k, real *v, real *lam) {
         if (n == 1) {
             for (int a = 0; a < 3; ++a) p[a] = W[id[0]][a];
         } else {
-            real E[3][3], G[3][3], r[3], mu[3];
+            real E[3][3], G[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}}, r[3], mu[3];
             for (int j = 1; j < n; ++j) for (int a = 0; a < 3; ++a) E[j - 1][a] = W[id[j]][a] - W[id[0]][a];
             const int q = n - 1;
             for (int i = 0; i < q; ++i) {

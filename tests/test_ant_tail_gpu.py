@@ -109,3 +109,39 @@ def test_ant_tail_kernel_matches_reference_golden(monkeypatch):
                                    err_msg=f"reward step {t}")
         assert env._tail.done_count() == int(d["out_reset"][t].sum())
         np.testing.assert_array_equal(env._tail.true_objective.cpu().numpy(), d["in_root"][t][:, 7])
+
+
+def test_fused_reset_matches_torch_reset_idx(monkeypatch):
+    """gt_ant_reset_flagged (post_physics_step's reset, no nonzero() sync) vs the torch reset_idx of ant.py:252-279
+    from the same state and the same device generator position: the dof state, potentials, counters and the
+    sim state after the indexed sets are BIT-IDENTICAL, and the generator ends where torch_rand_float left it."""
+    n = 1024
+    env = _make(n, monkeypatch)
+    gen = torch.Generator(device="cuda:0").manual_seed(9)
+    for _ in range(30):
+        env.step(2 * torch.rand((n, 8), device="cuda:0", generator=gen) - 1)
+    env.progress_buf[: n // 16] = env.max_episode_length - 1   # more envs end their episode in the next tail
+    env._tail()
+    torch.cuda.synchronize()
+    k = env._tail.done_count()
+    flagged = env.reset_buf.nonzero(as_tuple=False).flatten()
+    assert k == len(flagged) >= n // 16
+    names = ("dof_state", "potentials", "prev_potentials", "progress_buf", "reset_buf")
+    snap = {a: getattr(env, a).clone() for a in names}
+    state0 = env.sim.state.clone()
+    rng = torch.cuda.get_rng_state()
+    env.reset_idx(flagged)
+    torch.cuda.synchronize()
+    want = {a: getattr(env, a).clone() for a in names}
+    want_state, want_rng = env.sim.state.clone(), torch.cuda.get_rng_state()
+    for a in names:
+        getattr(env, a).copy_(snap[a])
+    env.sim.state.copy_(state0)
+    torch.cuda.set_rng_state(rng)
+    ids = env._tail.reset_flagged(k)
+    torch.cuda.synchronize()
+    assert torch.equal(ids.long(), flagged)
+    for a in names:
+        assert torch.equal(getattr(env, a), want[a]), a
+    assert torch.equal(env.sim.state, want_state)
+    assert torch.equal(torch.cuda.get_rng_state(), want_rng)

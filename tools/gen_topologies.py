@@ -91,7 +91,9 @@ def topo_tables(flat: dict) -> dict:
     sh_body = [cbody[sh_c0[s]] if sh_c0[s] < nc else 0 for s in range(ns)]
     jkind = [int(k) for k in flat["jkind"]]
     team = team_tables(flat, parent, bdof, nbase)
-    return dict(cdyn=[int(k) for k in flat["cdyn"]], shkind=[int(k) for k in flat["shkind"]],
+    return dict(pair_a=[int(x) for x in flat["pair_a"]], pair_b=[int(x) for x in flat["pair_b"]],
+                pair_k=[int(x) for x in flat["pair_kind"]],
+                cdyn=[int(k) for k in flat["cdyn"]], shkind=[int(k) for k in flat["shkind"]],
                 NPK=int(flat["npool"]), NPAIR=int(flat["npair"]),
                 NR=int(flat["nr"]), clink=[int(l) for l in flat["clink"]], TEAM=team, NB=nb, ND=nd, NC=nc, NS=int(flat["ns"]), FIXED=fixed, NBASE=nbase, NV=nv, MAXDEP=maxdep,
                 parent=parent, bdof=bdof, jkind=jkind, dpar=dpar, depth=[len(a) for a in anc],
@@ -181,7 +183,8 @@ def emit() -> str:
         for k, n in (("parent", "NB"), ("bdof", "NB"), ("jkind", "NB"), ("bgdof", "NB"), ("subend", "NB"), ("dpar", "NV"),
                      ("depth", "NV"), ("gbody", "NV"), ("cbody", "NC"), ("clink", "NC"), ("cshape", "NC"), ("cleaf", "NC"), ("csupp", "NC"), ("cslot", "NC"),
                      ("lleaf", "ND"), ("lsupp", "ND"), ("lslot", "ND"), ("sh_c0", "NS"), ("sh_c1", "NS"),
-                     ("sh_body", "NS"), ("cdyn", "NC"), ("shkind", "NS")):
+                     ("sh_body", "NS"), ("cdyn", "NC"), ("shkind", "NS"), ("pair_a", "NPAIR"), ("pair_b", "NPAIR"),
+                     ("pair_k", "NPAIR")):
             vals = t[k] if len(t[k]) else [0]
             dim = n if len(t[k]) else "1"
             lines.append(f"  static constexpr int {k}[{dim}] = {carr(vals)};")

@@ -16,7 +16,8 @@ os.environ.setdefault("GS_LIBGYMSIM", "libgymsim_prof.so")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 PHASES = ["forward pass + contact Jacobians", "backward pass + L^T D L", "free velocity", "contact rows (Z, c)",
-          "PGS sweeps", "back-substitution + integrate", "PD torque", "kernel outputs"]
+          "PGS sweeps", "back-substitution + integrate", "PD torque", "kernel outputs", "(count)", "(count)", "(unused)",
+          "self-collision prepass"]
 
 
 def main():
@@ -43,13 +44,18 @@ def main():
     waves = (N * 4 + 63) // 64
     substeps = 5
     per = [buf[i] / (a.steps * waves) for i in range(16)]
-    total = sum(per[:8])
+    total = sum(per[:8]) + per[11]
     print(f"cycles per launch per wave (s_memtime), {waves} waves, {a.steps} launches:")
     for i, name in enumerate(PHASES):
+        if name.startswith("("):
+            continue
         print(f"  {name:36s} {per[i]:10.0f}  {100 * per[i] / total:5.1f} %")
     print(f"  {'total':36s} {total:10.0f}")
     print(f"chain contacts executed per wave per PGS sweep: {per[8] / (substeps * 5):.2f} of 12")
     print(f"root contacts executed per wave per PGS sweep:  {per[9] / (substeps * 5):.2f} of 2")
+    print(f"self-collision narrowphase entered per wave per substep: {buf[12] / (a.steps * waves * substeps):.4f}")
+    if buf[12]:
+        print(f"self-collision narrowphase cycles per entry (pose table + pairs): {buf[13] / buf[12]:.0f}")
 
 
 if __name__ == "__main__":
