@@ -480,25 +480,42 @@ constexpr int kUnrollPairs = 64;  // pair tables up to this size are unrolled at
 // separation, friction, bodies, links); returns the count.
 // (shape data at stride LB, pool entries at stride LBP with PE floats per entry: the one-env-per-lane solver
 // keeps both in its lane column; the lane team reads a per-team shape table and keeps a shorter entry)
+// Per-shape constants of the narrowphase: bounding-sphere radius, margin (core rounding), capsule half length.
+// ShapeConstsM reads the model; the lane team stages them in LDS once per launch (ShapeConstsTab, kShC floats
+// per shape), so a pair's test waits on no scalar-cache miss.
+struct ShapeConstsM {
+  const DevModel* __restrict__ M;
+  GS_HD float brad(int s) const { return M->shc[s][3]; }
+  GS_HD float margin(int s) const { return M->shm[s]; }
+  GS_HD float hlen(int s) const { return M->shsize[s][1]; }
+};
+constexpr int kShC = 4;
+struct ShapeConstsTab {
+  const float* __restrict__ t;
+  GS_HD float brad(int s) const { return t[kShC * s]; }
+  GS_HD float margin(int s) const { return t[kShC * s + 1]; }
+  GS_HD float hlen(int s) const { return t[kShC * s + 2]; }
+};
+
 // One pair (shapes a < b, pair kind) of self_contacts: appends its contacts to the pool (n counts them).
-template <class T, int LB, int LBP, int PE>
-GS_HD __attribute__((always_inline)) inline void self_pair(const DevModel* __restrict__ M, const DevParams& P,
-                                                           const float* __restrict__ mu_g, int N, int e,
-                                                           const float* shw, float* pool, int a, int b, int kind,
-                                                           int& n) {
+template <class T, int LB, int LBP, int PE, class SC>
+GS_HD __attribute__((always_inline)) inline void self_pair(const DevModel* __restrict__ M, const SC& sc,
+                                                           const DevParams& P, const float* __restrict__ mu_g, int N,
+                                                           int e, const float* shw, float* pool, int a, int b,
+                                                           int kind, int& n) {
   const float off = P.contact_offset;
   {
     const float* sa = shw + (kShW * a + 12) * LB;
     const float* sb = shw + (kShW * b + 12) * LB;
     const float d[3] = {sa[0] - sb[0], sa[LB] - sb[LB], sa[2 * LB] - sb[2 * LB]};
-    const float rr = M->shc[a][3] + M->shc[b][3] + off;
+    const float rr = sc.brad(a) + sc.brad(b) + off;
     if (!(dot3f(d, d) < rr * rr)) return;
   }
   {
     ShapeW Wa, Wb;
     load_shape_w<LB>(shw, a, Wa);
     load_shape_w<LB>(shw, b, Wb);
-    const float ra = M->shm[a], rb = M->shm[b];
+    const float ra = sc.margin(a), rb = sc.margin(b);
     float pa[2][3], pb[2][3];
     int nct = 1;
     bool gdeep = false;
@@ -506,10 +523,10 @@ GS_HD __attribute__((always_inline)) inline void self_pair(const DevModel* __res
 #pragma unroll
       for (int k = 0; k < 3; ++k) { pa[0][k] = Wa.c[k]; pb[0][k] = Wb.c[k]; }
     } else if (kind == 1) {
-      const bool a_sph = M->shkind[a] == 0;
+      const bool a_sph = T::shkind[a] == 0;  // (the compiled topology's kinds: gs_sim_set_model checks them)
       const ShapeW& Wc = a_sph ? Wb : Wa;
       const ShapeW& Ws = a_sph ? Wa : Wb;
-      const float hl = M->shsize[a_sph ? b : a][1];
+      const float hl = sc.hlen(a_sph ? b : a);
       const float ax[3] = {Wc.R[2], Wc.R[5], Wc.R[8]};
       float e0[3], e1[3], q3[3];
 #pragma unroll
@@ -521,7 +538,7 @@ GS_HD __attribute__((always_inline)) inline void self_pair(const DevModel* __res
         pb[0][k] = a_sph ? q3[k] : Ws.c[k];
       }
     } else if (kind == 2) {
-      const float ha = M->shsize[a][1], hb = M->shsize[b][1];
+      const float ha = sc.hlen(a), hb = sc.hlen(b);
       float p1[3], q1[3], p2[3], q2[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
@@ -622,24 +639,29 @@ GS_HD __attribute__((always_inline)) inline void self_pair(const DevModel* __res
   }
 }
 
-template <class T, int LB, int LBP = LB, int PE = PoolCfg<T>::PE>
+template <class T, int LB, int LBP = LB, int PE = PoolCfg<T>::PE, class SC = ShapeConstsM>
 GS_HD int self_contacts(const DevModel* __restrict__ M, const DevParams& P, const float* __restrict__ mu_g, int N,
-                        int e, const float* shw, float* pool) {
+                        int e, const float* shw, float* pool, const SC& sc) {
   int n = 0;
   if constexpr (T::NPAIR <= kUnrollPairs) {
     // the compiled topology's pair table (gs_sim_set_model checks it against the model's): shapes and pair
     // kinds fold into the code, the shapes' constants are independent loads
 #pragma unroll
     for (int q = 0; q < T::NPAIR; ++q)
-      if (n < T::NPK) self_pair<T, LB, LBP, PE>(M, P, mu_g, N, e, shw, pool, T::pair_a[q], T::pair_b[q], T::pair_k[q], n);
+      if (n < T::NPK) self_pair<T, LB, LBP, PE>(M, sc, P, mu_g, N, e, shw, pool, T::pair_a[q], T::pair_b[q], T::pair_k[q], n);
   } else {
     const int np = M->np;
     for (int q = 0; q < np; ++q) {
       if (n >= T::NPK) break;
-      self_pair<T, LB, LBP, PE>(M, P, mu_g, N, e, shw, pool, M->pa[q], M->pb[q], M->pk[q], n);
+      self_pair<T, LB, LBP, PE>(M, sc, P, mu_g, N, e, shw, pool, M->pa[q], M->pb[q], M->pk[q], n);
     }
   }
   return n;
+}
+template <class T, int LB, int LBP = LB, int PE = PoolCfg<T>::PE>
+GS_HD int self_contacts(const DevModel* __restrict__ M, const DevParams& P, const float* __restrict__ mu_g, int N,
+                        int e, const float* shw, float* pool) {
+  return self_contacts<T, LB, LBP, PE, ShapeConstsM>(M, P, mu_g, N, e, shw, pool, ShapeConstsM{M});
 }
 
 }  // namespace

@@ -23,7 +23,9 @@
 // Phase profiler (profiling build only, -DGS_PHASE_PROFILE -> libgymsim_prof.so): per-wave
 // s_memtime deltas per solver phase, summed over waves into gs_phase_cycles (gs_capi.hip).
 #ifdef GS_PHASE_PROFILE
-__device__ unsigned long long gs_phase_cycles[16];
+// [0, 16): phase sums over waves; [16, 32): histogram of a wave's launch total (25k-cycle bins);
+// [32, 48): phase sums over the slow waves (total above 250k cycles), [48]: their count
+__device__ unsigned long long gs_phase_cycles[64];
 #define GS_PROF_DECL long long gs_t_ = clock64(); long long gs_acc_[16] = {0};
 #define GS_PROF(i) { const long long t_ = clock64(); gs_acc_[i] += t_ - gs_t_; gs_t_ = t_; }
 #define GS_PROF_COUNT(i, n) { gs_acc_[i] += (n); }
@@ -31,7 +33,16 @@ __device__ unsigned long long gs_phase_cycles[16];
 #define GS_PROF_ARGS , gs_t_, gs_acc_
 #define GS_PROF_FLUSH                                                   \
   if ((threadIdx.x & 63) == 0) {                                        \
-    for (int i_ = 0; i_ < 16; ++i_) atomicAdd(&gs_phase_cycles[i_], (unsigned long long)gs_acc_[i_]); \
+    long long tot_ = 0;                                                 \
+    for (int i_ = 0; i_ < 16; ++i_) {                                   \
+      atomicAdd(&gs_phase_cycles[i_], (unsigned long long)gs_acc_[i_]); \
+      if (i_ < 8 || i_ == 11) tot_ += gs_acc_[i_];                      \
+    }                                                                   \
+    atomicAdd(&gs_phase_cycles[16 + (int)min(tot_ / 25000, 15ll)], 1ull); \
+    if (tot_ > 250000) {                                                \
+      for (int i_ = 0; i_ < 16; ++i_) atomicAdd(&gs_phase_cycles[32 + i_], (unsigned long long)gs_acc_[i_]); \
+      atomicAdd(&gs_phase_cycles[48], 1ull);                            \
+    }                                                                   \
   }
 #else
 #define GS_PROF_DECL
@@ -245,6 +256,46 @@ __device__ __forceinline__ void stage_chain_model(const DevModel* __restrict__ M
   }
 }
 
+// Team-uniform shape constants of the self-collision passes, staged once per launch: per shape
+// (ShapeConstsTab) bounding radius, margin, capsule half length; then per root shape the core segment in
+// the root frame (ends l0, l1), radius and half length (broadphase)
+template <class T>
+struct ShapeTab {
+  static constexpr int RS = T::HAS_TEAM ? T::T_RS : 0;
+  static constexpr int ROOT = kShC * T::NS;
+  static constexpr int POSE = ROOT + 8 * RS;  // per shape: local R (9), t (3), bounding-sphere centre (3)
+  static constexpr int SIZE = T::NPK > 0 ? POSE + 15 * T::NS : 1;
+};
+template <class T>
+__device__ __forceinline__ void stage_shape_consts(const DevModel* __restrict__ M, float* sct) {
+  if constexpr (T::NPK > 0) {
+    using S = ShapeTab<T>;
+    for (int i = threadIdx.x; i < S::SIZE; i += blockDim.x) {
+      float v = 0.f;
+      if (i < S::ROOT) {
+        const int sh = i / kShC, f = i - kShC * sh;
+        v = f == 0 ? M->shc[sh][3] : (f == 1 ? M->shm[sh] : (f == 2 ? M->shsize[sh][1] : 0.f));
+      } else if (i >= S::POSE) {
+        const int sh = (i - S::POSE) / 15, f = (i - S::POSE) - 15 * sh;
+        v = f < 9 ? M->shR[sh][f] : (f < 12 ? M->sht[sh][f - 9] : M->shc[sh][f - 12]);
+      } else {
+        const int sr = (i - S::ROOT) / 8, f = (i - S::ROOT) - 8 * sr;
+        const int kind = T::shkind[sr];
+        const bool seg = kind == 0 || kind == 1;
+        const float hl = kind == 1 ? M->shsize[sr][1] : 0.f;
+        if (f < 6) {
+          const int a = f % 3;
+          const float sg = f < 3 ? -hl : hl;
+          v = seg ? M->sht[sr][a] + sg * M->shR[sr][3 * a + 2] : M->shc[sr][a];
+        } else {
+          v = f == 6 ? (seg ? M->shm[sr] : M->shc[sr][3]) : hl;
+        }
+      }
+      sct[i] = v;
+    }
+  }
+}
+
 template <class T>
 __device__ __forceinline__ void team_load(const float* __restrict__ st, int N, int e, int lc, TeamState<T>& s) {
   constexpr int ND = T::ND, CL = T::T_CL;
@@ -367,7 +418,7 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
                                                   const DevParams& P, const float* __restrict__ mu_g, int N, int e,
                                                   int lc, const float (&R0)[9], const float (&R)[T::T_CL][9],
                                                   const float (&X)[T::T_CL][3], float* __restrict__ shw_tab,
-                                                  float* __restrict__ pool) {
+                                                  const float* __restrict__ sct, float* __restrict__ pool) {
   constexpr int TPW = kTeamsPerBlock, LN = T::T_LANES, SPC = T::T_SPC, RSH = T::T_RS;
   using C = CM<T>;
   // (conservative by a hair: the narrowphase recomputes the distance in another association order)
@@ -401,18 +452,12 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
   };
 #pragma unroll
   for (int sr = 0; sr < RSH; ++sr) {
-    const int kind = T::shkind[sr];
-    const bool seg = kind == 0 || kind == 1;
-    const float rhl = kind == 1 ? M->shsize[sr][1] : 0.f;
-    float l0[3], l1[3], r0[3], r1[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      l0[a] = seg ? M->sht[sr][a] - rhl * M->shR[sr][3 * a + 2] : M->shc[sr][a];
-      l1[a] = seg ? M->sht[sr][a] + rhl * M->shR[sr][3 * a + 2] : M->shc[sr][a];
-    }
+    const float* rt = sct + ShapeTab<T>::ROOT + 8 * sr;
+    const float l0[3] = {rt[0], rt[1], rt[2]}, l1[3] = {rt[3], rt[4], rt[5]};
+    const float rr = rt[6], rhl = rt[7];
+    float r0[3], r1[3];
     mat3vec(R0, l0, r0);
     mat3vec(R0, l1, r1);
-    const float rr = seg ? M->shm[sr] : M->shc[sr][3];
 #pragma unroll
     for (int j = 0; j < SPC; ++j)
       if (team_pair<T>(sr, RSH + j)) test(r0, r1, rr, rhl, p0[j], p1[j], rad[j], hl[j]);
@@ -455,10 +500,11 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
   for (int j = 0; j < T::T_SPC; ++j) {
     const int sh = T::T_RS + lc * T::T_SPC + j;
     const int k = T::sh_body[T::T_RS + j] - 1;
+    const float* ps = sct + ShapeTab<T>::POSE + 15 * sh;
     float Rs[9], t[3], c[3];
-    mat3mul(R[k], M->shR[sh], Rs);
-    mat3vec(R[k], M->sht[sh], t);
-    mat3vec(R[k], M->shc[sh], c);
+    mat3mul(R[k], ps, Rs);
+    mat3vec(R[k], ps + 9, t);
+    mat3vec(R[k], ps + 12, c);
 #pragma unroll
     for (int f = 0; f < 9; ++f) tab[(kShW * sh + f) * TPW] = Rs[f];
 #pragma unroll
@@ -470,10 +516,11 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
   if (lc == 0) {
 #pragma unroll
     for (int sh = 0; sh < T::T_RS; ++sh) {
+      const float* ps = sct + ShapeTab<T>::POSE + 15 * sh;
       float Rs[9], t[3], c[3];
-      mat3mul(R0, M->shR[sh], Rs);
-      mat3vec(R0, M->sht[sh], t);
-      mat3vec(R0, M->shc[sh], c);
+      mat3mul(R0, ps, Rs);
+      mat3vec(R0, ps + 9, t);
+      mat3vec(R0, ps + 12, c);
 #pragma unroll
       for (int f = 0; f < 9; ++f) tab[(kShW * sh + f) * TPW] = Rs[f];
 #pragma unroll
@@ -487,7 +534,7 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
   // any lane of the team near -> the team's narrowphase (replicated, team-uniform result)
   const bool tnear = quad_sum(near ? 1.f : 0.f) > 0.f;
   int cnt = 0;
-  if (tnear) cnt = self_contacts<T, TPW, RW, RowSlots<T>::PER_POOL>(M, P, mu_g, N, e, tab, pool);
+  if (tnear) cnt = self_contacts<T, TPW, RW, RowSlots<T>::PER_POOL>(M, P, mu_g, N, e, tab, pool, ShapeConstsTab{sct});
 #ifdef GS_PHASE_PROFILE
   if ((threadIdx.x & 63) == 0) atomicAdd(&gs_phase_cycles[13], (unsigned long long)(clock64() - np_t0));
 #endif
@@ -500,7 +547,8 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
                                              const float* __restrict__ mu_g, int N, int e, int lc,
                                              float* __restrict__ rows_own, const float* __restrict__ rows_team,
                                              float* __restrict__ cf_soa, bool collect,
-                                             float* __restrict__ cf_aos, float* __restrict__ shw_tab GS_PROF_PARAM) {
+                                             float* __restrict__ cf_aos, float* __restrict__ shw_tab,
+                                             const float* __restrict__ sct GS_PROF_PARAM) {
   constexpr int CL = T::T_CL, CC = T::T_CC, RC = T::T_RC, NCH = T::T_NCH, LN = T::T_LANES;
   static_assert(NCH == LN && LN == 4, "lane teams are DPP quads with one chain per lane");
   using C = CM<T>;
@@ -640,7 +688,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
   int npc = 0;
   float* pool = rows_own + RS::POOL * RW;
   if constexpr (T::NPK > 0) {
-    if (P.self_collide) npc = team_self_contacts<T>(M, cm, P, mu_g, N, e, lc, R0, R, X, shw_tab, pool);
+    if (P.self_collide) npc = team_self_contacts<T>(M, cm, P, mu_g, N, e, lc, R0, R, X, shw_tab, sct, pool);
   }
   GS_PROF(11)  // self-collision prepass
   // ================= chain backward pass: composite inertia / force, bias, chain rows of M
@@ -1335,7 +1383,9 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel*
   __shared__ float mdl[CM<T>::NP * LN];
   __shared__ float rows[RowSlots<T>::TOTAL * RW];
   __shared__ float shw_tab[T::NPK > 0 ? kShW * T::NS * kTeamsPerBlock : 1];
+  __shared__ float sct[ShapeTab<T>::SIZE];
   stage_chain_model<T>(M, mdl);
+  stage_shape_consts<T>(M, sct);
   __syncthreads();
   const int lc = threadIdx.x & (LN - 1);
   const int e = (blockIdx.x * kTeamBlock + threadIdx.x) / LN;
@@ -1351,7 +1401,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel*
   GS_PROF_DECL
   for (int sstep = 0; sstep < P.substeps; ++sstep) {
     const bool last = (sstep == P.substeps - 1) && P.collect;
-    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, nullptr, shw_tab GS_PROF_ARGS);
+    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, nullptr, shw_tab, sct GS_PROF_ARGS);
   }
   team_store<T>(B.state, N, e, lc, s);
   GS_PROF_FLUSH
@@ -1364,7 +1414,9 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
   __shared__ float mdl[CM<T>::NP * LN];
   __shared__ float rows[RowSlots<T>::TOTAL * RW];
   __shared__ float shw_tab[T::NPK > 0 ? kShW * T::NS * kTeamsPerBlock : 1];
+  __shared__ float sct[ShapeTab<T>::SIZE];
   stage_chain_model<T>(M, mdl);
+  stage_shape_consts<T>(M, sct);
   __syncthreads();
   const int lc = threadIdx.x & (LN - 1);
   const int e = (blockIdx.x * kTeamBlock + threadIdx.x) / LN;
@@ -1394,7 +1446,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
     const bool last = ((it % sub) == sub - 1) && P.collect;
     GS_PROF(6)  // PD torque
     float* cf_aos = (it == total - 1) ? A.cf_out : nullptr;
-    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, cf_aos, shw_tab GS_PROF_ARGS);
+    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, cf_aos, shw_tab, sct GS_PROF_ARGS);
     if (it == n_pd - 1 && A.dof_out) {
 #pragma unroll
       for (int k = 0; k < CL; ++k) {
@@ -1457,11 +1509,11 @@ const int g_num_team_kernels = sizeof(g_team_kernels) / sizeof(g_team_kernels[0]
 // Phase profile readout (include/gymsim.h); -1 outside the profiling build.
 extern "C" int gs_debug_phase_cycles(unsigned long long* out, int n, int reset) {
 #ifdef GS_PHASE_PROFILE
-  if (!out || n <= 0 || n > 16) return -1;
+  if (!out || n <= 0 || n > 64) return -1;
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gs_phase_cycles), sizeof(unsigned long long) * n) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[16] = {0};
+    unsigned long long z[64] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(gs_phase_cycles), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;

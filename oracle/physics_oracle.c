@@ -504,8 +504,13 @@ static int simplex_closest(real W[4][3], int k, real *v, real *lam) {
 
 /* GJK distance between the cores of shapes a and b: closest points pa, pb; returns the distance, 0 when
  * the cores overlap */
+/* narrowphase workload counters (analysis only: oracle_pair_stats): pairs tested, bounding spheres met,
+ * GJK calls, GJK iterations, contacts kept (not thread-safe: read them from single-threaded runs) */
+static long long g_pair_stats[5];
+
 static real gjk_cores(const OModel *m, int sa, int sb, const ShapeW *Wa, const ShapeW *Wb, const real *Ra,
                       const real *Pa, const real *Rb, const real *Pb, real *pa, real *pb) {
+    ++g_pair_stats[2];
     real v[3] = {Wa->sc[0] - Wb->sc[0], Wa->sc[1] - Wb->sc[1], Wa->sc[2] - Wb->sc[2]};
     if (dot3(v, v) < 1e-18) { v[0] = 1; v[1] = 0; v[2] = 0; }
     real W[4][3], A[4][3], B[4][3], lam[4] = {1, 0, 0, 0};
@@ -513,6 +518,7 @@ static real gjk_cores(const OModel *m, int sa, int sb, const ShapeW *Wa, const S
     for (int it = 0; it < 32; ++it) {
         const real nv[3] = {-v[0], -v[1], -v[2]};
         real a[3], b[3], w[3];
+        ++g_pair_stats[3];
         core_support(m, sa, Wa, Ra, Pa, nv, a);
         core_support(m, sb, Wb, Rb, Pb, v, b);
         for (int t = 0; t < 3; ++t) w[t] = a[t] - b[t];
@@ -593,7 +599,9 @@ static int self_contacts(const OModel *m, const OParams *p, real R[][9], real P[
         const int a = m->pair_a[q], b = m->pair_b[q], kind = m->pair_kind[q];
         const real d[3] = {W[a].sc[0] - W[b].sc[0], W[a].sc[1] - W[b].sc[1], W[a].sc[2] - W[b].sc[2]};
         const real rr = (real)m->shsphere[4 * a + 3] + (real)m->shsphere[4 * b + 3] + off;
+        ++g_pair_stats[0];
         if (!(dot3(d, d) < rr * rr)) continue;
+        ++g_pair_stats[1];
         const int ba = m->shbody[a], bb = m->shbody[b];
         const real ra = (real)m->shmargin[a], rb = (real)m->shmargin[b];
         real pa[2][3], pb[2][3];
@@ -678,6 +686,7 @@ static int self_contacts(const OModel *m, const OParams *p, real R[][9], real P[
             const real sep = dist - ra - rb;
             if (!(sep < off)) continue;
             PairContact *o = &out[n++];
+            ++g_pair_stats[4];
             for (int k = 0; k < 3; ++k) {
                 o->n[k] = nn[k];
                 o->x[k] = 0.5 * ((pa[c][k] - ra * nn[k]) + (pb[c][k] + rb * nn[k]));
@@ -1334,4 +1343,12 @@ int oracle_hull_select(const OModel *m, const OParams *p, int sh, const real *R,
     const int n = hull_ground_select(m, sh, R, P, rootz, (real)p->contact_offset, s4);
     for (int k = 0; k < n; ++k) sel[k] = s4[k];
     return n;
+}
+
+/* narrowphase workload counters since the last call (g_pair_stats); reset = 1 clears them */
+int oracle_pair_stats(long long *out, int reset) {
+    for (int i = 0; i < 5; ++i) out[i] = g_pair_stats[i];
+    if (reset)
+        for (int i = 0; i < 5; ++i) g_pair_stats[i] = 0;
+    return 0;
 }

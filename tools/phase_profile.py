@@ -36,11 +36,11 @@ def main():
     pool = torch.empty((64, N, A), device="cuda:0").uniform_(-1, 1)
     for i in range(a.warmup):
         env.step(pool[i % 64])
-    buf = (C.c_ulonglong * 16)()
-    assert L.gs_debug_phase_cycles(buf, 16, 1) == 0, "not the profiling build"
+    buf = (C.c_ulonglong * 64)()
+    assert L.gs_debug_phase_cycles(buf, 64, 1) == 0, "not the profiling build"
     for i in range(a.steps):
         env.step(pool[i % 64])
-    assert L.gs_debug_phase_cycles(buf, 16, 1) == 0
+    assert L.gs_debug_phase_cycles(buf, 64, 1) == 0
     waves = (N * 4 + 63) // 64
     substeps = 5
     per = [buf[i] / (a.steps * waves) for i in range(16)]
@@ -54,6 +54,15 @@ def main():
     print(f"chain contacts executed per wave per PGS sweep: {per[8] / (substeps * 5):.2f} of 12")
     print(f"root contacts executed per wave per PGS sweep:  {per[9] / (substeps * 5):.2f} of 2")
     print(f"self-collision narrowphase entered per wave per substep: {buf[12] / (a.steps * waves * substeps):.4f}")
+    hist = [buf[16 + i] for i in range(16)]
+    print("waves by launch total (25k-cycle bins):", " ".join(f"{25 * i}k:{h}" for i, h in enumerate(hist) if h))
+    if buf[48]:
+        ns = buf[48]
+        print(f"slow waves (> 250k cycles): {ns}; their mean phases:")
+        for i, name in enumerate(PHASES):
+            if not name.startswith("("):
+                print(f"  {name:36s} {buf[32 + i] / ns:10.0f}")
+        print(f"  PGS chain contacts per slow wave: {buf[32 + 8] / ns:.1f}")
     if buf[12]:
         print(f"self-collision narrowphase cycles per entry (pose table + pairs): {buf[13] / buf[12]:.0f}")
 
