@@ -639,16 +639,19 @@ GS_HD __attribute__((always_inline)) inline void self_pair(const DevModel* __res
   }
 }
 
+// (mask: a caller's broadphase may restrict the pairs to a superset of those that can touch -- bit q of pair q;
+// the result is the same as without it)
 template <class T, int LB, int LBP = LB, int PE = PoolCfg<T>::PE, class SC = ShapeConstsM>
 GS_HD int self_contacts(const DevModel* __restrict__ M, const DevParams& P, const float* __restrict__ mu_g, int N,
-                        int e, const float* shw, float* pool, const SC& sc) {
+                        int e, const float* shw, float* pool, const SC& sc, unsigned long long mask = ~0ull) {
   int n = 0;
   if constexpr (T::NPAIR <= kUnrollPairs) {
     // the compiled topology's pair table (gs_sim_set_model checks it against the model's): shapes and pair
     // kinds fold into the code, the shapes' constants are independent loads
 #pragma unroll
     for (int q = 0; q < T::NPAIR; ++q)
-      if (n < T::NPK) self_pair<T, LB, LBP, PE>(M, sc, P, mu_g, N, e, shw, pool, T::pair_a[q], T::pair_b[q], T::pair_k[q], n);
+      if (n < T::NPK && ((mask >> q) & 1ull))
+        self_pair<T, LB, LBP, PE>(M, sc, P, mu_g, N, e, shw, pool, T::pair_a[q], T::pair_b[q], T::pair_k[q], n);
   } else {
     const int np = M->np;
     for (int q = 0; q < np; ++q) {

@@ -404,6 +404,35 @@ __host__ __device__ constexpr bool team_pair(int a, int b) {
     if (T::pair_a[q] == a && T::pair_b[q] == b) return true;
   return false;
 }
+// index of the pair of shapes a, b in the pair table (-1: not a pair)
+template <class T>
+__host__ __device__ constexpr int team_pair_index(int a, int b) {
+  for (int q = 0; q < T::NPAIR; ++q)
+    if ((T::pair_a[q] == a && T::pair_b[q] == b) || (T::pair_a[q] == b && T::pair_b[q] == a)) return q;
+  return -1;
+}
+// a pair's bit in the team's near mask, for the lane's chain lc: shapes a_c = RS + c SPC + ja (or root shape
+// ra when ja < 0), b_c = RS + ((c + dl) & 3) SPC + jb, selected from the four compile-time candidates
+template <class T>
+__device__ __forceinline__ unsigned long long team_pair_bit(int lc, int ra, int ja, int dl, int jb) {
+  unsigned long long bit = 0ull;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int a = ja < 0 ? ra : T::T_RS + c * T::T_SPC + ja;
+    const int b = T::T_RS + ((c + dl) & 3) * T::T_SPC + jb;
+    const int q = team_pair_index<T>(a, b);
+    bit = lc == c ? (q >= 0 ? 1ull << q : 0ull) : bit;
+  }
+  return bit;
+}
+__device__ __forceinline__ unsigned long long quad_or64(unsigned long long m) {
+  int lo = (int)(unsigned)m, hi = (int)(unsigned)(m >> 32);
+  lo |= qperm_i<0xB1>(lo);
+  hi |= qperm_i<0xB1>(hi);
+  lo |= qperm_i<0x4E>(lo);
+  hi |= qperm_i<0x4E>(hi);
+  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
 
 // Self-collision prepass of a team.  Broadphase in registers, every substep: each lane holds its
 // chain's shapes as core segments + radius (a sphere is a point segment; boxes / hulls their bounding sphere) and
@@ -436,10 +465,11 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
     rad[j] = sp[6 * LN];
     hl[j] = sp[7 * LN];
   }
-  bool near = false;
+  static_assert(T::NPAIR <= 64, "the team's near-pair mask is 64 bits");
+  unsigned long long near = 0ull;  // bits of the pair table: the lane's tests that found a pair within reach
   // bounding spheres first (midpoint, half length + radius); the exact segment distance only where they meet
   auto test = [&](const float* a0, const float* a1, float ra, float ha, const float* b0, const float* b1, float rb,
-                  float hb) {
+                  float hb, unsigned long long bit) {
     const float rr = ra + rb + off;
     float dc = 0.f;
 #pragma unroll
@@ -448,7 +478,7 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
       dc += x * x;
     }
     const float rs = rr + ha + hb;
-    if (dc < rs * rs) near = near || (seg_seg_d2(a0, a1, b0, b1) < rr * rr);
+    if (dc < rs * rs && seg_seg_d2(a0, a1, b0, b1) < rr * rr) near |= bit;
   };
 #pragma unroll
   for (int sr = 0; sr < RSH; ++sr) {
@@ -460,13 +490,14 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
     mat3vec(R0, l1, r1);
 #pragma unroll
     for (int j = 0; j < SPC; ++j)
-      if (team_pair<T>(sr, RSH + j)) test(r0, r1, rr, rhl, p0[j], p1[j], rad[j], hl[j]);
+      if (team_pair<T>(sr, RSH + j)) test(r0, r1, rr, rhl, p0[j], p1[j], rad[j], hl[j], team_pair_bit<T>(lc, sr, -1, 0, j));
   }
 #pragma unroll
   for (int j = 0; j < SPC; ++j)
 #pragma unroll
     for (int j2 = j + 1; j2 < SPC; ++j2)
-      if (team_pair<T>(RSH + j, RSH + j2)) test(p0[j], p1[j], rad[j], hl[j], p0[j2], p1[j2], rad[j2], hl[j2]);
+      if (team_pair<T>(RSH + j, RSH + j2))
+        test(p0[j], p1[j], rad[j], hl[j], p0[j2], p1[j2], rad[j2], hl[j2], team_pair_bit<T>(lc, 0, j, 0, j2));
   // chains lc + 1 (every lane) and lc + 2 (lanes 0 and 1): each inter-chain pair exactly once
 #pragma unroll
   for (int dl = 1; dl <= 2; ++dl) {
@@ -484,10 +515,11 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
       for (int j = 0; j < SPC; ++j)
 #pragma unroll
         for (int j2 = 0; j2 < SPC; ++j2)
-          if (team_pair<T>(RSH + j, RSH + SPC + j2)) test(p0[j], p1[j], rad[j], hl[j], q0[j2], q1[j2], rad[j2], hl[j2]);
+          if (team_pair<T>(RSH + j, RSH + SPC + j2))
+            test(p0[j], p1[j], rad[j], hl[j], q0[j2], q1[j2], rad[j2], hl[j2], team_pair_bit<T>(lc, 0, j, dl, j2));
     }
   }
-  if (__ballot(near) == 0ull) return 0;  // wave-uniform: no team of the wave has a pair within contact_offset
+  if (__ballot(near != 0ull) == 0ull) return 0;  // wave-uniform: no team of the wave has a pair within reach
 #ifdef GS_PHASE_PROFILE
   if ((threadIdx.x & 63) == 0) atomicAdd(&gs_phase_cycles[12], 1ull);  // substeps a wave runs the narrowphase
   const long long np_t0 = clock64();
@@ -531,10 +563,11 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
     }
   }
   __syncthreads();
-  // any lane of the team near -> the team's narrowphase (replicated, team-uniform result)
-  const bool tnear = quad_sum(near ? 1.f : 0.f) > 0.f;
+  // the team's near pairs (team-uniform mask) -> the narrowphase of those pairs, replicated in the team's lanes
+  const unsigned long long tmask = quad_or64(near);
   int cnt = 0;
-  if (tnear) cnt = self_contacts<T, TPW, RW, RowSlots<T>::PER_POOL>(M, P, mu_g, N, e, tab, pool, ShapeConstsTab{sct});
+  if (tmask) cnt = self_contacts<T, TPW, RW, RowSlots<T>::PER_POOL>(M, P, mu_g, N, e, tab, pool, ShapeConstsTab{sct},
+                                                                    tmask);
 #ifdef GS_PHASE_PROFILE
   if ((threadIdx.x & 63) == 0) atomicAdd(&gs_phase_cycles[13], (unsigned long long)(clock64() - np_t0));
 #endif
