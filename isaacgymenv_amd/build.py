@@ -32,7 +32,7 @@ PROF_LIBS = {"libgymsim_prof.so": LIBS["libgymsim.so"]}
 SIM_FLAGS = ["-fno-slp-vectorize"]
 EXTRA_FLAGS = {"libgymtask.so": ["-ffp-contract=off"], "libgymrl.so": ["-ffp-contract=off"], "libgymsim.so": SIM_FLAGS,
                "libgymsim_prof.so": SIM_FLAGS + ["-DGS_PHASE_PROFILE"]}
-HEADERS = ["gs_internal.h", "gs_topologies.h", "gs_math.h", "gs_terrain.h", "gs_pairs.h", "gs_solver.h", "gs_kinematics.h",
+HEADERS = ["gs_internal.h", "gs_topologies.h", "gs_math.h", "gs_terrain.h", "gs_pairs.h", "gs_solver.h", "gs_kinematics.h", "gs_host_impl.h",
            "gs_physics_impl.h", "torch_philox.h"]
 # gs_phys_inst.hip is compiled once per (topology, kernel form): 0 simulate plane, 1 simulate terrain-mesh,
 # 2 fused PD step plane, 3 fused PD step terrain-mesh (gs_physics_impl.h)

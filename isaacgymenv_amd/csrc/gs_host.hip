@@ -18,67 +18,11 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "gs_solver.h"
+#include "gs_host_impl.h"
 #include "gs_kinematics.h"
 
-// ---------------------------------------------------------------- thread pool
-struct HostPool {
-  std::vector<std::thread> workers;
-  std::mutex m;
-  std::condition_variable wake, done;
-  const std::function<void(int, int)>* job = nullptr;  // (begin, end) of a chunk of envs
-  std::atomic<int> next{0};
-  int n = 0, chunk = 1;
-  unsigned long gen = 0;
-  int busy = 0;
-  bool stop = false;
-
-  void drain() {
-    for (;;) {
-      const int b = next.fetch_add(chunk);
-      if (b >= n) return;
-      (*job)(b, b + chunk < n ? b + chunk : n);
-    }
-  }
-  void worker() {
-    unsigned long seen = 0;
-    for (;;) {
-      {
-        std::unique_lock<std::mutex> lk(m);
-        wake.wait(lk, [&] { return stop || gen != seen; });
-        if (stop) return;
-        seen = gen;
-      }
-      drain();
-      std::lock_guard<std::mutex> lk(m);
-      if (--busy == 0) done.notify_one();
-    }
-  }
-  // run f over [0, n) in chunks; the calling thread works too; returns when every chunk is done
-  void run(int n_items, const std::function<void(int, int)>& f) {
-    if (n_items <= 0) return;
-    const int threads = (int)workers.size() + 1;
-    if (threads == 1 || n_items == 1) {
-      f(0, n_items);
-      return;
-    }
-    {
-      std::lock_guard<std::mutex> lk(m);
-      job = &f;
-      n = n_items;
-      // ~8 chunks per thread: envs differ in cost (contacts, terrain cells), so balance dynamically
-      chunk = n_items / (threads * 8) > 0 ? n_items / (threads * 8) : 1;
-      next.store(0);
-      busy = (int)workers.size();
-      ++gen;
-    }
-    wake.notify_all();
-    drain();
-    std::unique_lock<std::mutex> lk(m);
-    done.wait(lk, [&] { return busy == 0; });
-    job = nullptr;
-  }
-};
+using gs_hostimpl::host_sim;
+using gs_hostimpl::host_pd;
 
 HostPool* host_pool_create(int threads) {
   HostPool* p = new HostPool();
@@ -97,54 +41,6 @@ void host_pool_destroy(HostPool* p) {
 }
 int host_pool_threads(const HostPool* p) { return p ? (int)p->workers.size() + 1 : 0; }
 
-namespace {
-
-// per-thread contact-row scratch (the LDS column of one lane in the kernels, LB = 1).  GS_HOST_POISON=1 fills it
-// with NaN before every env (debug: any read of a slot the env did not write shows up as a NaN state)
-bool host_poison() {
-  static const bool on = [] { const char* v = std::getenv("GS_HOST_POISON"); return v && v[0] == '1'; }();
-  return on;
-}
-float* scratch(int slots) {
-  thread_local std::vector<float> buf;
-  if ((int)buf.size() < slots) buf.resize(slots);
-  return buf.data();
-}
-void poison(float* lds, int slots) {
-  if (host_poison()) std::fill(lds, lds + slots, std::numeric_limits<float>::quiet_NaN());
-}
-
-template <class T>
-void host_sim(const DevModel* M, const DevParams& P, const SimBuffers& B, const float* tau, HostPool* pool) {
-  if (P.has_terrain) {
-    pool->run(B.N, [&](int b, int e1) {
-      float* lds = scratch(LaneCfg<T, true>::SLOTS);
-      for (int e = b; e < e1; ++e) { poison(lds, LaneCfg<T, true>::SLOTS); simulate_env<T, true, 1>(M, P, B, tau, e, lds); }
-    });
-  } else {
-    pool->run(B.N, [&](int b, int e1) {
-      float* lds = scratch(LaneCfg<T, false>::SLOTS);
-      for (int e = b; e < e1; ++e) { poison(lds, LaneCfg<T, false>::SLOTS); simulate_env<T, false, 1>(M, P, B, tau, e, lds); }
-    });
-  }
-}
-
-template <class T>
-void host_pd(const DevModel* M, const DevParams& P, const SimBuffers& B, const PdDev& A, HostPool* pool) {
-  if (P.has_terrain) {
-    pool->run(B.N, [&](int b, int e1) {
-      float* lds = scratch(LaneCfg<T, true>::SLOTS);
-      for (int e = b; e < e1; ++e) { poison(lds, LaneCfg<T, true>::SLOTS); pd_step_env<T, true, 1>(M, P, B, A, e, lds); }
-    });
-  } else {
-    pool->run(B.N, [&](int b, int e1) {
-      float* lds = scratch(LaneCfg<T, false>::SLOTS);
-      for (int e = b; e < e1; ++e) { poison(lds, LaneCfg<T, false>::SLOTS); pd_step_env<T, false, 1>(M, P, B, A, e, lds); }
-    });
-  }
-}
-
-}  // namespace
 
 #define GS_HOST_TOPO_ENTRY(T, SIG) {SIG, &host_sim<T>, &host_pd<T>},
 HostTopoEntry g_host_topologies[] = {GS_FOR_EACH_TOPOLOGY(GS_HOST_TOPO_ENTRY)};

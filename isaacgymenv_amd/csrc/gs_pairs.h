@@ -99,6 +99,29 @@ struct PoolCfg {
   static constexpr int FLOATS = T::NPK > 0 ? T::NPK * PE : 0;
 };
 
+// a pair record's contact: x (3) n (3) sep -- the pool entry's first 6 floats plus the separation
+constexpr int kRecSep = 6, kRec = 7;
+
+// the rest of a pool entry whose x and n are written: tangents of n, separation stays, friction (PhysX average
+// of the two shapes'), bodies and links of shapes a and b
+template <int LBP>
+GS_HD void pool_entry_finish(const DevModel* __restrict__ M, const float* __restrict__ mu_g, int N, int e, int a, int b,
+                             float* o) {
+  const float nn[3] = {o[kPoolN * LBP], o[(kPoolN + 1) * LBP], o[(kPoolN + 2) * LBP]};
+  float t1[3], t2[3];
+  gs_terrain::tangents(nn, t1, t2);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    o[(kPoolT1 + k) * LBP] = t1[k];
+    o[(kPoolT2 + k) * LBP] = t2[k];
+  }
+  o[kPoolMu * LBP] = 0.5f * (mu_g[a * N + e] + mu_g[b * N + e]);
+  o[kPoolBA * LBP] = (float)M->shbody[a];
+  o[kPoolBB * LBP] = (float)M->shbody[b];
+  o[kPoolLA * LBP] = (float)M->shlink[a];
+  o[kPoolLB * LBP] = (float)M->shlink[b];
+}
+
 struct ShapeW {
   float R[9], c[3], sc[3];
 };
@@ -498,7 +521,9 @@ struct ShapeConstsTab {
 };
 
 // One pair (shapes a < b, pair kind) of self_contacts: appends its contacts to the pool (n counts them).
-template <class T, int LB, int LBP, int PE, class SC>
+// REC: a pair record of the wave-assisted lane kernels (gs_physics_impl.h pair_records) -- only x, n and the
+// separation (kRec floats per contact); pool_entry_finish completes the entry as the full form writes it.
+template <class T, int LB, int LBP, int PE, class SC, bool REC = false>
 GS_HD __attribute__((always_inline)) inline void self_pair(const DevModel* __restrict__ M, const SC& sc,
                                                            const DevParams& P, const float* __restrict__ mu_g, int N,
                                                            int e, const float* shw, float* pool, int a, int b,
@@ -619,21 +644,17 @@ GS_HD __attribute__((always_inline)) inline void self_pair(const DevModel* __res
       const float sep = gdeep ? -(ra + rb) : dist - ra - rb;
       if (!(sep < off)) continue;
       float* o = pool + PE * n * LBP;
-      float t1[3], t2[3];
-      gs_terrain::tangents(nn, t1, t2);
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         o[(kPoolX + k) * LBP] = 0.5f * ((pa[c][k] - ra * nn[k]) + (pb[c][k] + rb * nn[k]));
         o[(kPoolN + k) * LBP] = nn[k];
-        o[(kPoolT1 + k) * LBP] = t1[k];
-        o[(kPoolT2 + k) * LBP] = t2[k];
       }
-      o[kPoolSep * LBP] = sep;
-      o[kPoolMu * LBP] = 0.5f * (mu_g[a * N + e] + mu_g[b * N + e]);
-      o[kPoolBA * LBP] = (float)M->shbody[a];
-      o[kPoolBB * LBP] = (float)M->shbody[b];
-      o[kPoolLA * LBP] = (float)M->shlink[a];
-      o[kPoolLB * LBP] = (float)M->shlink[b];
+      if constexpr (REC) {
+        o[kRecSep * LBP] = sep;
+      } else {
+        o[kPoolSep * LBP] = sep;
+        pool_entry_finish<LBP>(M, mu_g, N, e, a, b, o);
+      }
       ++n;
     }
   }

@@ -196,15 +196,67 @@ GS_HD void body_poses(const DevModel* __restrict__ M, const EnvState<T>& s, floa
 // is complete (T::subend).  Contact Jacobian rows are written to LDS during the
 // same walk (they need the path's motion subspaces) and turned into scaled
 // Z rows after the factorisation.
+// Shape world data of env state s for the self-collision narrowphase (gs_pairs.h layout: [kShW * sh + f] at
+// stride LB): R (9), centre (3), bounding-sphere centre (3), relative to the root origin.  Written into the
+// contact-row area, which the substep fills only after its narrowphase.
+template <class T, int LB>
+GS_HD void shape_world(const DevModel* __restrict__ Min, const EnvState<T>& s, float* lds) {
+  constexpr int NB = T::NB;
+  const DevModel* __restrict__ M = gs_opaque(Min);
+  float Rb[NB][9], Xb[NB][3];
+  body_poses<T>(M, s, Rb, Xb);
+#pragma unroll
+  for (int sh = 0; sh < T::NS; ++sh) {
+    const int b = T::sh_body[sh];
+    float Rs[9], t[3];
+    mat3mul(Rb[b], M->shR[sh], Rs);
+    float* o = lds + kShW * sh * LB;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) o[k * LB] = Rs[k];
+    mat3vec(Rb[b], M->sht[sh], t);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) o[(9 + k) * LB] = Xb[b][k] + t[k];
+    mat3vec(Rb[b], M->shc[sh], t);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) o[(12 + k) * LB] = Xb[b][k] + t[k];
+  }
+}
+
+// Pair records (stride PR): per pair q its contact count at [q], contact c's x, n, separation at
+// [NPAIR + (2 q + c) kRec + f].  Gathered in pair order into the pool, at most T::NPK -- the entries
+// self_contacts writes for the same shapes.
+template <class T, int LB, int PR>
+GS_HD int pool_from_records(const DevModel* __restrict__ M, const float* __restrict__ mu_g, int N, int e,
+                            const float* __restrict__ prec, float* pool) {
+  constexpr int PE = PoolCfg<T>::PE;
+  int n = 0;
+  for (int q = 0; q < T::NPAIR && n < T::NPK; ++q) {
+    const int cnt = (int)prec[q * PR];
+    for (int c = 0; c < cnt && n < T::NPK; ++c) {
+      const float* r = prec + (T::NPAIR + (2 * q + c) * kRec) * PR;
+      float* o = pool + PE * n * LB;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) o[k * LB] = r[k * PR];
+      o[kPoolSep * LB] = r[kRecSep * PR];
+      pool_entry_finish<LB>(M, mu_g, N, e, M->pa[q], M->pb[q], o);
+      ++n;
+    }
+  }
+  return n;
+}
+
 // QS > 0 (TERR kernels): the terrain queries of this substep were already run by the whole workgroup
 // (terrain_queries, gs_physics.hip) and `qres` holds this env's results, [5 * c + k][QS] for
 // candidate c: (found, separation, normal xyz); QS == 0 runs each candidate's query inline.
 // SELF = false compiles the self-collision path out (kernels launched for sims without it)
-template <class T, bool TERR, int LB = LaneCfg<T, TERR>::LB, int QS = 0, bool SELF = true>
+// PR > 0 (wave-assisted kernels): the self-collision narrowphase of this substep was already run by the whole
+// workgroup (pair_records, gs_physics_impl.h) on the shape world data shape_world wrote, and `prec` holds this
+// env's pair records at stride PR (pair_records' layout); the prepass only gathers them into the pool.
+template <class T, bool TERR, int LB = LaneCfg<T, TERR>::LB, int QS = 0, bool SELF = true, int PR = 0>
 GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvState<T>& s,
                                         const float* tau, const float* __restrict__ mu_g, int N, int e, float* lds,
                                         float* __restrict__ cf_soa, bool collect, float* __restrict__ sens_soa,
-                   const float* __restrict__ qres = nullptr) {
+                   const float* __restrict__ qres = nullptr, const float* __restrict__ prec = nullptr) {
   constexpr int NB = T::NB, NV = T::NV, NB6 = T::NBASE, NC = T::NC, ND = T::ND;
   constexpr int MS = T::MAXDEP + 1;
   // Keep the model pointer opaque per substep: the constants are re-read with
@@ -221,24 +273,12 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
   int npc = 0;
   if constexpr (T::NPK > 0 && SELF) {
     if (P.self_collide) {
-      float Rb[NB][9], Xb[NB][3];
-      body_poses<T>(M, s, Rb, Xb);
-#pragma unroll
-      for (int sh = 0; sh < T::NS; ++sh) {
-        const int b = T::sh_body[sh];
-        float Rs[9], t[3];
-        mat3mul(Rb[b], M->shR[sh], Rs);
-        float* o = lds + kShW * sh * LB;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) o[k * LB] = Rs[k];
-        mat3vec(Rb[b], M->sht[sh], t);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) o[(9 + k) * LB] = Xb[b][k] + t[k];
-        mat3vec(Rb[b], M->shc[sh], t);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) o[(12 + k) * LB] = Xb[b][k] + t[k];
+      if constexpr (PR > 0) {
+        npc = pool_from_records<T, LB, PR>(M, mu_g, N, e, prec, pool);
+      } else {
+        shape_world<T, LB>(M, s, lds);
+        npc = self_contacts<T, LB>(M, P, mu_g, N, e, lds, pool);
       }
-      npc = self_contacts<T, LB>(M, P, mu_g, N, e, lds, pool);
       for (int p = 0; p < npc; ++p)
         for (int k = 0; k < 3 * NV; ++k) pool[(PE * p + kPoolJ + k) * LB] = 0.f;
     }
@@ -341,7 +381,11 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
     if constexpr (T::NPK > 0 && SELF) {
       if (i > 0) {
         const int col = NB6 + T::bdof[i];
-        for (int p = 0; p < npc; ++p) {
+        // (unrolled over the pool with a guard: a runtime loop here would carry the tree walk's registers
+        // across its back edge -- ~4 KB of scratch per lane measured)
+#pragma unroll
+        for (int p = 0; p < T::NPK; ++p) {
+          if (p >= npc) break;
           float* o = pool + PE * p * LB;
           const int ba = (int)o[kPoolBA * LB], bb = (int)o[kPoolBB * LB];
           const float coef = (float)((M->banc[ba] >> i) & 1u) - (float)((M->banc[bb] >> i) & 1u);
@@ -727,7 +771,9 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
 
   // ---------------- self-contact rows: dense J over the tree -> c = J nu_f, scaled Z = (L^-T J^T) D^-1/2, 1/diag
   if constexpr (T::NPK > 0 && SELF) {
-    for (int p = 0; p < npc; ++p) {
+#pragma unroll
+    for (int p = 0; p < T::NPK; ++p) {
+      if (p >= npc) break;
       float* o = pool + PE * p * LB;
 #pragma unroll
       for (int rr = 0; rr < 3; ++rr) {

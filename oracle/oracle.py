@@ -38,7 +38,8 @@ class OParams(C.Structure):
                 ("rest_offset", C.c_double), ("max_depen_vel", C.c_double), ("collect_contacts", C.c_int32),
                 ("has_ground", C.c_int32), ("ground_friction", C.c_double), ("limit_margin", C.c_double),
                 ("has_terrain", C.c_int32), ("trows", C.c_int32), ("tcols", C.c_int32), ("tverts", C.c_void_p),
-                ("tx0", C.c_double), ("ty0", C.c_double), ("ths", C.c_double), ("terrain_friction", C.c_double)]
+                ("tx0", C.c_double), ("ty0", C.c_double), ("ths", C.c_double), ("terrain_friction", C.c_double),
+                ("solver_type", C.c_int32)]
 
 
 def build(quiet: bool = True) -> None:
@@ -123,6 +124,7 @@ class OracleSim:
             p.gravity[i] = params["gravity"][i]
         p.pos_iters = params["pos_iters"]
         p.vel_iters = params["vel_iters"]
+        p.solver_type = int(params.get("solver_type", 0))
         p.contact_offset = params["contact_offset"]
         p.rest_offset = params["rest_offset"]
         p.max_depen_vel = params["max_depen_vel"]

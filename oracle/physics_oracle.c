@@ -117,6 +117,10 @@ typedef struct {
     const float *tverts;
     double tx0, ty0, ths;
     double terrain_friction;
+    /* physx.solver_type (cfg/config.yaml:31): 0 PGS (the kernels' solver), 1 TGS -- oracle only, the study of
+     * pos_iters sub-steps of h / pos_iters, each row's separation advanced by the displacement
+     * integrated so far, positions integrated with the sub-steps' velocities, no bias in the velocity phase */
+    int32_t solver_type;
 } OParams;
 
 /* ---------------------------------------------------------------- helpers */
@@ -1061,14 +1065,21 @@ static void env_substep(const OModel *m, const OParams *p, real h,
     real plam[3 * MAXPOOL];
     for (int k = 0; k < 3 * npc; ++k) plam[k] = 0;
     const int iters = p->pos_iters + p->vel_iters;
+    /* TGS (solver_type 1): displacement dq integrated over the position sub-steps of length hs; a row's
+     * separation is advanced by J dq (linearised), its target is set for the sub-step */
+    const int tgs = p->solver_type == 1 && p->pos_iters > 0;
+    const real hs = tgs ? h / p->pos_iters : h;
+    real dxs[MAXV];
+    for (int k = 0; k < nv; ++k) dxs[k] = 0;
     for (int it = 0; it < iters; ++it) {
         const int pos_phase = it < p->pos_iters;
+        const real hd = pos_phase ? hs : h;  /* a separated row may close its gap within hd */
         for (int a = 0; a < nlim; ++a) {
-            const real s = lsep[a];
+            const real s = lsep[a] + (tgs ? lsgn[a] * dxs[nbase + ldof[a]] : 0);
             const real u = lsgn[a] * v[nbase + ldof[a]];
             real target;
-            if (s >= 0) target = -s / h;
-            else if (pos_phase) { target = -s / h; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
+            if (s >= 0) target = -s / hd;
+            else if (pos_phase) { target = -s / hs; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
             else target = 0;
             real ln = laml[a] + (target - u) / LD[a];
             if (ln < 0) ln = 0;
@@ -1078,16 +1089,17 @@ static void env_substep(const OModel *m, const OParams *p, real h,
             for (int k = 0; k < nv; ++k) v[k] += Wr[k] * dl;
         }
         for (int a = 0; a < nact; ++a) {
-            const real s = cs[a];
+            real s = cs[a];
             /* normal */
             {
                 const int r = 3 * a;
                 const real *Jr = J + r * MAXV, *Wr = W + r * MAXV;
                 real u = 0;
                 for (int k = 0; k < nv; ++k) u += Jr[k] * v[k];
+                if (tgs) for (int k = 0; k < nv; ++k) s += Jr[k] * dxs[k];
                 real target;
-                if (s >= 0) target = -s / h;
-                else if (pos_phase) { target = -s / h; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
+                if (s >= 0) target = -s / hd;
+                else if (pos_phase) { target = -s / hs; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
                 else target = 0;
                 real ln = Dr[r] > MIN_RESPONSE ? lam[r] + (target - u) / Dr[r] : lam[r];
                 if (ln < 0) ln = 0;
@@ -1110,7 +1122,7 @@ static void env_substep(const OModel *m, const OParams *p, real h,
             }
         }
         for (int a = 0; a < npc; ++a) {
-            const real s = pc[a].sep;
+            real s = pc[a].sep;
             for (int t = 0; t < 3; ++t) {
                 const int r = 3 * a + t;
                 const real *Jr = PJ + r * MAXV, *Wr = PW + r * MAXV;
@@ -1118,9 +1130,10 @@ static void env_substep(const OModel *m, const OParams *p, real h,
                 for (int k = 0; k < nv; ++k) u += Jr[k] * v[k];
                 real ln;
                 if (t == 0) {
+                    if (tgs) for (int k = 0; k < nv; ++k) s += Jr[k] * dxs[k];
                     real target;
-                    if (s >= 0) target = -s / h;
-                    else if (pos_phase) { target = -s / h; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
+                    if (s >= 0) target = -s / hd;
+                    else if (pos_phase) { target = -s / hs; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
                     else target = 0;
                     ln = PD[r] > MIN_RESPONSE ? plam[r] + (target - u) / PD[r] : plam[r];
                     if (ln < 0) ln = 0;
@@ -1135,7 +1148,11 @@ static void env_substep(const OModel *m, const OParams *p, real h,
                 for (int k = 0; k < nv; ++k) v[k] += Wr[k] * dl;
             }
         }
-        if (it == p->pos_iters - 1) memcpy(nupos, v, sizeof(real) * nv);
+        if (tgs && pos_phase) for (int k = 0; k < nv; ++k) dxs[k] += hs * v[k];
+        if (it == p->pos_iters - 1) {
+            if (tgs) for (int k = 0; k < nv; ++k) nupos[k] = dxs[k] / h;  /* h * nupos = the sub-steps' displacement */
+            else memcpy(nupos, v, sizeof(real) * nv);
+        }
     }
     if (p->pos_iters == 0) memcpy(nupos, v, sizeof(real) * nv);
 
