@@ -40,7 +40,7 @@ def test_gae_kernel_rejects_oversized_horizon():
                         torch.zeros(N, dtype=torch.uint8, device="cuda"), 0.99, 0.95)
 
 
-def _agent(task, num_envs, **over):
+def _agent(task, num_envs, overrides=(), **over):
     from isaacgymenv_amd.isaacgymenvs.config import compose
     from isaacgymenv_amd.isaacgymenvs.tasks.base import vec_task
     from isaacgymenv_amd.rl import A2CAgent, PpoConfig
@@ -48,7 +48,7 @@ def _agent(task, num_envs, **over):
     vec_task.EXISTING_SIM = None
     cfg = compose("config", [f"task={task}"])
     env = isaacgymenvs.make(seed=42, task=task, num_envs=num_envs, sim_device="cuda:0", rl_device="cuda:0",
-                            headless=True, force_render=False)
+                            headless=True, force_render=False, overrides=list(overrides))
     pcfg = PpoConfig.from_train_cfg(cfg["train"], **over)
     return A2CAgent(env, pcfg, device="cuda:0", seed=42)
 
@@ -74,6 +74,19 @@ def test_anymal_terrain_ppo_epochs():
     assert np.isfinite(s["kl"]) and np.isfinite(s["a_loss"]) and np.isfinite(s["c_loss"])
     assert all(torch.isfinite(p).all() for p in agent.params)
     assert agent.frame == 2 * 24 * 4096
+
+
+def test_anymal_terrain_trimesh_ppo_epochs():
+    """BASELINE config 3: PPO on the trimesh heightfield (curriculum resets, mesh contacts, height probes)."""
+    agent = _agent("AnymalTerrain", 4096, overrides=["task.env.terrain.terrainType=trimesh"])
+    assert agent.env.cfg["env"]["terrain"]["terrainType"] == "trimesh" and agent.env.custom_origins
+    for _ in range(3):  # the third epoch replays the captured graphs
+        agent.train_epoch()
+    s = agent.epoch_stats()
+    assert np.isfinite(s["kl"]) and np.isfinite(s["a_loss"]) and np.isfinite(s["c_loss"])
+    assert all(torch.isfinite(p).all() for p in agent.params)
+    assert torch.isfinite(agent.env.obs_buf).all()
+    assert agent.frame == 3 * 24 * 4096
 
 
 def test_graph_replay_equals_eager_updates():
