@@ -171,8 +171,11 @@ __global__ __launch_bounds__(kTerrWave, 1) void k_pd_step_wave(const DevModel* _
 // launchers, one per kernel form (instantiated per topology in gs_phys_inst.hip).  Plane sims with
 // self-collision whose envs are LDS-starved (<= 4 env lanes per workgroup: UsefulHound) run the wave-assisted
 // kernels too, so their pair narrowphase is spread over the wave; mesh sims always do.
+#ifndef GS_WAVE_PLANE_SELF
+#define GS_WAVE_PLANE_SELF 1
+#endif
 template <class T>
-constexpr bool kWavePlaneSelf = T::NPK > 0 && LaneCfg<T, false>::LB <= 4 && !LaneCfg<T, false>::GLOBAL;
+constexpr bool kWavePlaneSelf = GS_WAVE_PLANE_SELF && T::NPK > 0 && LaneCfg<T, false>::LB <= 4 && !LaneCfg<T, false>::GLOBAL;
 
 template <class T>
 hipError_t launch_sim_plane(const DevModel* M, const DevParams& P, const SimBuffers& B, const float* tau, hipStream_t st) {

@@ -385,7 +385,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
         // across its back edge -- ~4 KB of scratch per lane measured)
 #pragma unroll
         for (int p = 0; p < T::NPK; ++p) {
-          if (p >= npc) break;
+          if (p >= npc) continue;  // (a guard, not an exit: the loop stays fully unrolled)
           float* o = pool + PE * p * LB;
           const int ba = (int)o[kPoolBA * LB], bb = (int)o[kPoolBB * LB];
           const float coef = (float)((M->banc[ba] >> i) & 1u) - (float)((M->banc[bb] >> i) & 1u);
@@ -773,7 +773,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
   if constexpr (T::NPK > 0 && SELF) {
 #pragma unroll
     for (int p = 0; p < T::NPK; ++p) {
-      if (p >= npc) break;
+      if (p >= npc) continue;
       float* o = pool + PE * p * LB;
 #pragma unroll
       for (int rr = 0; rr < 3; ++rr) {

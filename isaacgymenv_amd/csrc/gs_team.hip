@@ -397,6 +397,22 @@ __device__ __forceinline__ float seg_seg_d2(const float* p1, const float* q1, co
   return dd;
 }
 
+// squared distance from point p to segment s0 s1 (v_rcp: ~1 ulp, covered by the broadphase's slack)
+__device__ __forceinline__ float seg_pt_d2(const float* s0, const float* s1, const float* p) {
+  float d[3], r[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { d[k] = s1[k] - s0[k]; r[k] = p[k] - s0[k]; }
+  const float dd = dot3f(d, d);
+  const float t = dd > 1e-12f ? __builtin_amdgcn_fmed3f(dot3f(r, d) * __builtin_amdgcn_rcpf(dd), 0.f, 1.f) : 0.f;
+  float out = 0.f;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const float x = r[k] - t * d[k];
+    out += x * x;
+  }
+  return out;
+}
+
 // shapes a < b of a topology collide (its self-collision pair table, gs_topologies.h)
 template <class T>
 __host__ __device__ constexpr bool team_pair(int a, int b) {
@@ -468,8 +484,11 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
   static_assert(T::NPAIR <= 64, "the team's near-pair mask is 64 bits");
   unsigned long long near = 0ull;  // bits of the pair table: the lane's tests that found a pair within reach
   // bounding spheres first (midpoint, half length + radius); the exact segment distance only where they meet
-  auto test = [&](const float* a0, const float* a1, float ra, float ha, const float* b0, const float* b1, float rb,
-                  float hb, unsigned long long bit) {
+  // (sa / sb: the shape is a capsule core segment; spheres, boxes and hulls are points here -- compile-time
+  // kinds, so a point pair is exact on the midpoint test and a point-capsule pair takes the point-segment
+  // distance instead of the segment-segment one)
+  auto test = [&](const float* a0, const float* a1, float ra, float ha, bool sa, const float* b0, const float* b1,
+                  float rb, float hb, bool sb, unsigned long long bit) {
     const float rr = ra + rb + off;
     float dc = 0.f;
 #pragma unroll
@@ -477,8 +496,22 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
       const float x = 0.5f * ((a0[k] + a1[k]) - (b0[k] + b1[k]));
       dc += x * x;
     }
-    const float rs = rr + ha + hb;
-    if (dc < rs * rs && seg_seg_d2(a0, a1, b0, b1) < rr * rr) near |= bit;
+    if (!sa && !sb) {
+      if (dc < rr * rr) near |= bit;
+      return;
+    }
+    const float rs = rr + (sa ? ha : 0.f) + (sb ? hb : 0.f);
+    if (!(dc < rs * rs)) return;
+    float d2;
+    if (sa && sb) {
+      d2 = seg_seg_d2(a0, a1, b0, b1);
+    } else {
+      const float* s0 = sa ? a0 : b0;
+      const float* s1 = sa ? a1 : b1;
+      const float* pt = sa ? b0 : a0;
+      d2 = seg_pt_d2(s0, s1, pt);
+    }
+    if (d2 < rr * rr) near |= bit;
   };
 #pragma unroll
   for (int sr = 0; sr < RSH; ++sr) {
@@ -490,14 +523,17 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
     mat3vec(R0, l1, r1);
 #pragma unroll
     for (int j = 0; j < SPC; ++j)
-      if (team_pair<T>(sr, RSH + j)) test(r0, r1, rr, rhl, p0[j], p1[j], rad[j], hl[j], team_pair_bit<T>(lc, sr, -1, 0, j));
+      if (team_pair<T>(sr, RSH + j))
+        test(r0, r1, rr, rhl, T::shkind[sr] == 1, p0[j], p1[j], rad[j], hl[j], T::shkind[RSH + j] == 1,
+             team_pair_bit<T>(lc, sr, -1, 0, j));
   }
 #pragma unroll
   for (int j = 0; j < SPC; ++j)
 #pragma unroll
     for (int j2 = j + 1; j2 < SPC; ++j2)
       if (team_pair<T>(RSH + j, RSH + j2))
-        test(p0[j], p1[j], rad[j], hl[j], p0[j2], p1[j2], rad[j2], hl[j2], team_pair_bit<T>(lc, 0, j, 0, j2));
+        test(p0[j], p1[j], rad[j], hl[j], T::shkind[RSH + j] == 1, p0[j2], p1[j2], rad[j2], hl[j2],
+             T::shkind[RSH + j2] == 1, team_pair_bit<T>(lc, 0, j, 0, j2));
   // chains lc + 1 (every lane) and lc + 2 (lanes 0 and 1): each inter-chain pair exactly once
 #pragma unroll
   for (int dl = 1; dl <= 2; ++dl) {
@@ -516,7 +552,8 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
 #pragma unroll
         for (int j2 = 0; j2 < SPC; ++j2)
           if (team_pair<T>(RSH + j, RSH + SPC + j2))
-            test(p0[j], p1[j], rad[j], hl[j], q0[j2], q1[j2], rad[j2], hl[j2], team_pair_bit<T>(lc, 0, j, dl, j2));
+            test(p0[j], p1[j], rad[j], hl[j], T::shkind[RSH + j] == 1, q0[j2], q1[j2], rad[j2], hl[j2],
+                 T::shkind[RSH + j2] == 1, team_pair_bit<T>(lc, 0, j, dl, j2));
     }
   }
   if (__ballot(near != 0ull) == 0ull) return 0;  // wave-uniform: no team of the wave has a pair within reach
