@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 3
+#define RL_ABI_VERSION 4
 
 int rl_abi_version(void);
 const char *rl_last_error(void);
@@ -135,6 +135,30 @@ int rl_rollout_post(const float *rewards, const void *dones, int32_t dones_bytes
                     double gamma, int32_t num_envs, uint8_t *dones_out, float *rewards_out, float *current_rewards,
                     float *current_lengths, float *meter_rewards, float *meter_lengths, int32_t games_to_track,
                     void *stream);
+
+/*
+ * ABI 4 -- the minibatch optimizer step over the learner's flat buffers (rl_games a2c_common.py
+ * trancate_gradients_and_step: scaler.unscale_, clip_grad_norm_, scaler.step(Adam), scaler.update):
+ *   g = grad / scale (scale null: 1, no skipping, no update); found_inf = any non-finite g;
+ *   unless found_inf: g *= min(1, max_norm / (||g|| + 1e-6)) when max_norm > 0; g += weight_decay * p;
+ *   Adam with step t = *step + 1: m = lerp(m, g, 1 - beta1), v = beta2 v + (1 - beta2) g^2,
+ *   p -= lr / (1 - beta1^t) * m / (sqrt(v) / sqrt(1 - beta2^t) + eps); then *step = t.
+ *   GradScaler.update on (scale, growth_tracker): found_inf -> scale *= backoff, tracker = 0; else
+ *   tracker += 1, and at growth_interval scale *= growth, tracker = 0.
+ * param / grad / exp_avg / exp_avg_sq [n] f32; step, lr, scale: device f32 scalars; growth_tracker: device
+ * int32; partials >= rl_opt_partials_size() f32 scratch.  Three launches, no host synchronisation.
+ */
+typedef struct rl_opt_hyper {
+    float max_norm;       /* <= 0: no clipping */
+    float beta1, beta2, eps, weight_decay;
+    float backoff, growth;
+    int32_t growth_interval;
+} rl_opt_hyper;
+
+int rl_opt_step(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n, float *step,
+                const float *lr, float *scale, int32_t *growth_tracker, const rl_opt_hyper *hyper, float *partials,
+                void *stream);
+int rl_opt_partials_size(void);
 
 #ifdef __cplusplus
 }

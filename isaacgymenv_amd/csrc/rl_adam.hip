@@ -1,0 +1,158 @@
+// libgymrl.so -- the PPO minibatch optimizer step as three launches (include/gymrl.h rl_opt_step).
+//
+// rl_games a2c_common.py trancate_gradients_and_step with mixed precision: scaler.unscale_(optimizer),
+// clip_grad_norm_(params, grad_norm), scaler.step(optimizer) (torch.optim.Adam, skipped when a gradient
+// is not finite), scaler.update().  torch spends ~20 launches on it (per-tensor unscale and found-inf,
+// per-tensor norms and their norm, clip multiply, the fused Adam, the scale update); the parameters,
+// gradients and Adam moments of this learner are each ONE flat buffer (rl/a2c_continuous.py), so here:
+//   k_opt_norm  : per workgroup, sum of (g / scale)^2 over its slice (fixed order) and a non-finite flag
+//   k_opt_adam  : every workgroup sums the partials in the same fixed order (the norm, found-inf), then the
+//                 clip coefficient and Adam (torch's update: m.lerp_(g, 1 - b1), v = b2 v + (1 - b2) g^2,
+//                 p -= lr / bc1 * m / (sqrt(v) / sqrt(bc2) + eps)) on its slice; nothing when found-inf
+//   k_opt_finish: step += 1 unless found-inf; GradScaler.update (backoff on inf, growth every interval)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "gymrl.h"
+
+int rl_set_error(const char* msg);  // rl_gae.hip
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kBlocks = 256;  // partials: [kBlocks] sums, [kBlocks] non-finite flags
+
+__device__ __forceinline__ float block_sum(float x, float* sh) {
+  const int t = threadIdx.x;
+  sh[t] = x;
+  __syncthreads();
+  for (int s = kThreads / 2; s > 0; s >>= 1) {
+    if (t < s) sh[t] += sh[t + s];
+    __syncthreads();
+  }
+  const float r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ void slice(int64_t n, int64_t& b, int64_t& e) {
+  const int64_t chunk = (n + kBlocks - 1) / kBlocks;
+  b = (int64_t)blockIdx.x * chunk;
+  e = b + chunk < n ? b + chunk : n;
+}
+
+__global__ __launch_bounds__(kThreads) void k_opt_norm(const float* __restrict__ grad, int64_t n,
+                                                       const float* __restrict__ scale, float* __restrict__ part) {
+  __shared__ float sh[kThreads];
+  const float inv = scale ? 1.0f / *scale : 1.0f;
+  int64_t b, e;
+  slice(n, b, e);
+  float acc = 0.f, bad = 0.f;
+  for (int64_t i = b + threadIdx.x; i < e; i += kThreads) {
+    const float g = grad[i] * inv;
+    if (!isfinite(g)) bad = 1.f;
+    acc += g * g;
+  }
+  acc = block_sum(acc, sh);
+  bad = block_sum(bad, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = acc;
+    part[kBlocks + blockIdx.x] = bad;
+  }
+}
+
+// the partials, summed in the same order in every workgroup: (squared norm, found_inf)
+__device__ __forceinline__ void totals(const float* __restrict__ part, float* sh, float& sq, bool& found) {
+  sq = block_sum(threadIdx.x < kBlocks ? part[threadIdx.x] : 0.f, sh);
+  found = block_sum(threadIdx.x < kBlocks ? part[kBlocks + threadIdx.x] : 0.f, sh) > 0.f;
+}
+
+__global__ __launch_bounds__(kThreads) void k_opt_adam(float* __restrict__ param, const float* __restrict__ grad,
+                                                       float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                       const float* __restrict__ step, const float* __restrict__ lr,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ part, rl_opt_hyper h) {
+  __shared__ float sh[kThreads];
+  float sq;
+  bool found;
+  totals(part, sh, sq, found);
+  if (found) return;  // scaler.step skips the optimizer step
+  float coef = 1.f;
+  if (h.max_norm > 0.f) {  // clip_grad_norm_: max_norm / (total_norm + 1e-6), clamped to 1
+    const float c = h.max_norm / (sqrtf(sq) + 1e-6f);
+    coef = c < 1.f ? c : 1.f;
+  }
+  const float gs = (scale ? 1.0f / *scale : 1.0f) * coef;
+  const float t = *step + 1.f;
+  const float bc1 = 1.f - powf(h.beta1, t);
+  const float bc2 = 1.f - powf(h.beta2, t);
+  const float step_size = *lr / bc1;
+  const float bc2_sqrt = sqrtf(bc2);
+  int64_t b, e;
+  slice(n, b, e);
+  for (int64_t i = b + threadIdx.x; i < e; i += kThreads) {
+    float g = grad[i] * gs;
+    float p = param[i];
+    if (h.weight_decay != 0.f) g += h.weight_decay * p;
+    float mi = m[i], vi = v[i];
+    mi = mi + (1.f - h.beta1) * (g - mi);
+    vi = h.beta2 * vi + (1.f - h.beta2) * g * g;
+    const float denom = sqrtf(vi) / bc2_sqrt + h.eps;
+    p -= step_size * (mi / denom);
+    m[i] = mi;
+    v[i] = vi;
+    param[i] = p;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_opt_finish(float* __restrict__ step, float* __restrict__ scale,
+                                                         int32_t* __restrict__ tracker, const float* __restrict__ part,
+                                                         rl_opt_hyper h) {
+  __shared__ float sh[kThreads];
+  float sq;
+  bool found;
+  totals(part, sh, sq, found);
+  if (threadIdx.x != 0) return;
+  if (!found) *step += 1.f;
+  if (scale && tracker) {  // torch._amp_update_scale_
+    if (found) {
+      *scale *= h.backoff;
+      *tracker = 0;
+    } else {
+      const int32_t s = *tracker + 1;
+      if (s == h.growth_interval) {
+        *scale *= h.growth;
+        *tracker = 0;
+      } else {
+        *tracker = s;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int rl_opt_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float* step,
+                           const float* lr, float* scale, int32_t* growth_tracker, const rl_opt_hyper* hyper,
+                           float* partials, void* stream) {
+  if (n <= 0 || !param || !grad || !exp_avg || !exp_avg_sq || !step || !lr || !hyper || !partials)
+    return rl_set_error("rl_opt_step: null pointer or n <= 0");
+  if ((scale == nullptr) != (growth_tracker == nullptr))
+    return rl_set_error("rl_opt_step: scale and growth_tracker come together (both null: no loss scaling)");
+  hipStream_t st = (hipStream_t)stream;
+  const rl_opt_hyper h = *hyper;
+  hipLaunchKernelGGL(k_opt_norm, dim3(kBlocks), dim3(kThreads), 0, st, grad, n, scale, partials);
+  hipLaunchKernelGGL(k_opt_adam, dim3(kBlocks), dim3(kThreads), 0, st, param, grad, exp_avg, exp_avg_sq, n, step, lr,
+                     scale, partials, h);
+  hipLaunchKernelGGL(k_opt_finish, dim3(1), dim3(kThreads), 0, st, step, scale, growth_tracker, partials, h);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    char msg[256];
+    snprintf(msg, sizeof(msg), "rl_opt_step: launch failed: %s", hipGetErrorString(e));
+    return rl_set_error(msg) + 1;
+  }
+  return 0;
+}
+
+extern "C" int rl_opt_partials_size(void) { return 2 * kBlocks; }

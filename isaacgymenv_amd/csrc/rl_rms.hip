@@ -6,8 +6,8 @@
 // casts of the running moments.  torch spends ~25 launches on it (a Welford reduction of ~40 us at
 // 16384 x 188, ~15 float64 elementwise ops on [C], the normalisation chain); here:
 //   k_rms_part: workgroup b, lane c = column c: Welford over the workgroup's 64 rows (fp32, loads issued 8 ahead)
-//   k_rms_fin : 4 lanes per column merge the workgroups' (mean, M2) in fp64 (Chan et al.; lane j takes blocks
-//               j, j + 4, ... in order, then the 4 in lane order: fixed, deterministic), rounds the
+//   k_rms_fin : 64 lanes per column merge the workgroups' (mean, M2) in fp64 (Chan et al.; lane j takes blocks
+//               j, j + 64, ... in order, then a fixed pairwise tree: deterministic), rounds the
 //               batch mean / var to fp32 as torch's fp32 reductions return them, then updates the running
 //               moments with the reference formula in fp64, same operation order
 //   k_rms_norm: the normalisation (also the eval-mode path, update = 0); bumps the running count
@@ -24,8 +24,8 @@ namespace {
 constexpr int kCols = 256;     // columns <= 256
 constexpr int kRowBlock = 64;  // rows per partial
 constexpr int kPre = 8;        // loads issued ahead of the dependent Welford / merge chain
-constexpr int kFinCols = 64;   // finish: columns per workgroup, kFinSub lanes per column
-constexpr int kFinSub = 4;
+constexpr int kFinCols = 4;    // finish: columns per workgroup, kFinSub lanes per column
+constexpr int kFinSub = 64;
 
 __global__ __launch_bounds__(kCols) void k_rms_part(const float* __restrict__ x, int N, int C,
                                                     float* __restrict__ part) {
@@ -61,39 +61,37 @@ __device__ __forceinline__ void merge(double& na, double& mean, double& M2, doub
     na = tot;
 }
 
-// workgroup = kFinCols columns x kFinSub lanes; lane j merges the partials b = j, j + kFinSub, ... in order,
-// then lane 0 merges the kFinSub results in lane order (fixed: deterministic)
+// workgroup = kFinCols columns x kFinSub lanes; lane j merges the partials b = j, j + kFinSub, ... in order, then
+// the kFinSub lane results are merged pairwise in a fixed tree (lane j with lane j + s, s = 32, 16, ..., 1):
+// deterministic, and 47 workgroups of short fp64 chains instead of 3 workgroups of 64-long ones (34.5 -> ~2 us)
 __global__ __launch_bounds__(kFinCols * kFinSub) void k_rms_fin(const float* __restrict__ part, int blocks, int N,
                                                                 int C, double* __restrict__ rmean,
                                                                 double* __restrict__ rvar,
                                                                 const double* __restrict__ count) {
-    __shared__ double sh[kFinSub][kFinCols][3];
-    const int cl = threadIdx.x % kFinCols, j = threadIdx.x / kFinCols;
+    __shared__ double sh[kFinCols][kFinSub][3];
+    const int j = threadIdx.x % kFinSub, cl = threadIdx.x / kFinSub;
     const int c = blockIdx.x * kFinCols + cl;
     double na = 0.0, mean = 0.0, M2 = 0.0;
     if (c < C) {
-        for (int b0 = j; b0 < blocks; b0 += kFinSub * kPre) {
-            float pm[kPre], pm2[kPre];
-#pragma unroll
-            for (int k = 0; k < kPre; ++k) {
-                const int b = b0 + k * kFinSub;
-                pm[k] = b < blocks ? part[((size_t)b * C + c) * 2 + 0] : 0.f;
-                pm2[k] = b < blocks ? part[((size_t)b * C + c) * 2 + 1] : 0.f;
-            }
-#pragma unroll
-            for (int k = 0; k < kPre; ++k) {
-                const int b = b0 + k * kFinSub;
-                if (b < blocks) merge(na, mean, M2, (double)(min(N, (b + 1) * kRowBlock) - b * kRowBlock), pm[k], pm2[k]);
-            }
+        for (int b = j; b < blocks; b += kFinSub) {
+            const float pm = part[((size_t)b * C + c) * 2 + 0], pm2 = part[((size_t)b * C + c) * 2 + 1];
+            merge(na, mean, M2, (double)(min(N, (b + 1) * kRowBlock) - b * kRowBlock), pm, pm2);
         }
     }
-    sh[j][cl][0] = na;
-    sh[j][cl][1] = mean;
-    sh[j][cl][2] = M2;
+    sh[cl][j][0] = na;
+    sh[cl][j][1] = mean;
+    sh[cl][j][2] = M2;
     __syncthreads();
+    for (int st = kFinSub / 2; st > 0; st >>= 1) {
+        if (j < st && sh[cl][j + st][0] > 0.0) {
+            merge(na, mean, M2, sh[cl][j + st][0], sh[cl][j + st][1], sh[cl][j + st][2]);
+            sh[cl][j][0] = na;
+            sh[cl][j][1] = mean;
+            sh[cl][j][2] = M2;
+        }
+        __syncthreads();
+    }
     if (j != 0 || c >= C) return;
-    for (int q = 1; q < kFinSub; ++q)
-        if (sh[q][cl][0] > 0.0) merge(na, mean, M2, sh[q][cl][0], sh[q][cl][1], sh[q][cl][2]);
     const double cnt = *count;  // updated by k_rms_norm, after every column's update
     // torch: input.mean / input.var on float32 return float32
     const double bmean = (double)(float)mean;

@@ -212,6 +212,22 @@ class A2CAgent:
                                               weight_decay=cfg.weight_decay)
         self.mixed_precision = cfg.mixed_precision and on_gpu
         self.scaler = torch.amp.GradScaler("cuda", enabled=self.mixed_precision)
+        # the minibatch optimizer step as one HIP pass over the flat buffers (gae.opt_step, rl_opt_step):
+        # unscale, found-inf, norm clip, Adam, scaler update -- ~20 launches become 3.  The Adam moments
+        # are flat buffers too, and the optimizer's per-parameter state holds views into them, so
+        # checkpoints keep torch's Adam state layout.
+        self._fused_opt = on_gpu
+        if self._fused_opt:
+            self.flat_m = torch.zeros_like(self.flat_param)
+            self.flat_v = torch.zeros_like(self.flat_param)
+            self._opt_step_t = torch.zeros((), dtype=torch.float32, device=self.device)
+            self._opt_part = torch.empty(gae.lib().rl_opt_partials_size(), dtype=torch.float32, device=self.device)
+            self._bind_opt_state()
+            b1, b2 = self.optimizer.defaults["betas"]
+            self._opt_hyper = gae.OptHyper(cfg.grad_norm if cfg.truncate_grads else 0.0, b1, b2,
+                                           self.optimizer.defaults["eps"], cfg.weight_decay,
+                                           self.scaler.get_backoff_factor(), self.scaler.get_growth_factor(),
+                                           self.scaler.get_growth_interval())
         H, N, O, A = self.horizon, self.num_actors, self.obs_dim, self.actions_num
         dev = self.device
         # env-major experience (flattened batch = view); time-major GAE inputs
@@ -445,14 +461,35 @@ class A2CAgent:
         sigma = torch.exp(net.sigma.detach()).expand(mu.shape[0], -1)
         return (stats[0], stats[1], stats[2], stats[3], mu.detach(), sigma)
 
+    def _bind_opt_state(self):
+        """Adam state of every parameter as views into the flat moment buffers (after a checkpoint load
+        the loaded tensors are copied in first)."""
+        off = 0
+        for p in self.params:
+            n = p.numel()
+            st = self.optimizer.state.get(p)
+            m, v = self.flat_m[off:off + n].view_as(p), self.flat_v[off:off + n].view_as(p)
+            if st and "exp_avg" in st:
+                m.copy_(st["exp_avg"])
+                v.copy_(st["exp_avg_sq"])
+                self._opt_step_t.copy_(torch.as_tensor(st["step"], dtype=torch.float32))
+            self.optimizer.state[p] = {"step": self._opt_step_t, "exp_avg": m, "exp_avg_sq": v}
+            off += n
+
     def _mb_step(self, i, out):
         """Phase 2 (after the gradient all-reduce): unscale, clip, Adam, scaler update; KL of the
         new policy against the dataset's old mu/sigma."""
-        if self.cfg.truncate_grads:
-            self.scaler.unscale_(self.optimizer)
-            nn.utils.clip_grad_norm_(self.params, self.cfg.grad_norm)
-        self.scaler.step(self.optimizer)
-        self.scaler.update()
+        if self._fused_opt:
+            scale = self.scaler._scale if self.mixed_precision else None
+            tracker = self.scaler._growth_tracker if self.mixed_precision else None
+            gae.opt_step(self.flat_param, self.flat_grad, self.flat_m, self.flat_v, self._opt_step_t, self._opt_lr,
+                         scale, tracker, self._opt_hyper, self._opt_part)
+        else:
+            if self.cfg.truncate_grads:
+                self.scaler.unscale_(self.optimizer)
+                nn.utils.clip_grad_norm_(self.params, self.cfg.grad_norm)
+            self.scaler.step(self.optimizer)
+            self.scaler.update()
         mb = self._minibatch(i)
         with torch.no_grad():
             return self._policy_kl(out[4], out[5], mb["mu"], mb["sigma"])
@@ -624,6 +661,8 @@ class A2CAgent:
         self.frame = int(ckpt.get("frame", 0))
         if "optimizer" in ckpt:
             self.optimizer.load_state_dict(ckpt["optimizer"])
+            if self._fused_opt:
+                self._bind_opt_state()
         lr = float(ckpt.get("last_lr", self.cfg.learning_rate))
         self.lr.fill_(lr)
         if self._opt_lr is not None:

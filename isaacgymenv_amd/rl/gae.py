@@ -15,12 +15,19 @@ import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libgymrl.so")
 EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accum", "rl_colsum_accum", "rl_rollout_post",
-                    "rl_ppo_loss", "rl_ppo_loss_backward", "rl_rms_normalize",
+                    "rl_ppo_loss", "rl_ppo_loss_backward", "rl_rms_normalize", "rl_opt_step", "rl_opt_partials_size",
                     "rl_policy_head"]
 _lib = None
 
 
-RL_ABI_VERSION = 3  # include/gymrl.h
+RL_ABI_VERSION = 4  # include/gymrl.h
+
+
+class OptHyper(C.Structure):
+    """include/gymrl.h rl_opt_hyper"""
+    _fields_ = [("max_norm", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float),
+                ("weight_decay", C.c_float), ("backoff", C.c_float), ("growth", C.c_float),
+                ("growth_interval", C.c_int32)]
 
 
 def lib():
@@ -49,6 +56,9 @@ def lib():
         L.rl_ppo_loss_backward.restype = C.c_int
         L.rl_ppo_loss_backward.argtypes = [vp, vp, vp, vp, C.c_int32, C.c_int32, vp, C.c_int32, vp, C.c_int32, vp,
                                            vp]
+        L.rl_opt_step.restype = C.c_int
+        L.rl_opt_step.argtypes = [vp, vp, vp, vp, C.c_int64, vp, vp, vp, vp, C.POINTER(OptHyper), vp, vp]
+        L.rl_opt_partials_size.restype = C.c_int
         L.rl_rms_normalize.restype = C.c_int
         L.rl_rms_normalize.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp, C.c_double, C.c_int32, vp, vp, vp]
         L.rl_policy_head.restype = C.c_int
@@ -282,3 +292,15 @@ def policy_head(mu, noise, logstd, value, value_rms=None):
     if rc != 0:
         raise RuntimeError(f"rl_policy_head failed: {lib().rl_last_error().decode()}")
     return actions, sigmas, neglogp, vout
+
+
+def opt_step(param, grad, exp_avg, exp_avg_sq, step, lr, scale, growth_tracker, hyper: OptHyper, partials) -> None:
+    """The minibatch optimizer step on flat f32 buffers (include/gymrl.h rl_opt_step): unscale, found-inf,
+    norm clip, Adam, GradScaler update; scale / growth_tracker None = no loss scaling."""
+    rc = lib().rl_opt_step(param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
+                           param.numel(), step.data_ptr(), lr.data_ptr(),
+                           scale.data_ptr() if scale is not None else None,
+                           growth_tracker.data_ptr() if growth_tracker is not None else None, C.byref(hyper),
+                           partials.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"rl_opt_step failed: {lib().rl_last_error().decode()}")

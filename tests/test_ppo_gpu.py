@@ -271,6 +271,9 @@ def test_checkpoint_round_trip(tmp_path):
         for k in ("exp_avg", "exp_avg_sq", "step"):
             assert torch.equal(sa[i][k], sb[i][k]), (i, k)
     assert torch.equal(a.flat_param, b.flat_param)
+    if a._fused_opt:  # the restored moments are the fused step's flat buffers
+        assert torch.equal(a.flat_m, b.flat_m) and torch.equal(a.flat_v, b.flat_v)
+        assert b.optimizer.state[b.params[0]]["exp_avg"].data_ptr() == b.flat_m.data_ptr()
 
 
 def test_fused_ppo_loss_matches_torch_loss():
@@ -348,3 +351,57 @@ def test_policy_head_kernel_matches_torch_act_forward():
     assert torch.equal(fused["actions"], act) and torch.equal(fused["sigmas"], sigma)
     assert torch.equal(fused["values"], val) and torch.equal(fused["mus"], mu)
     torch.testing.assert_close(fused["neglogpacs"], nlp, rtol=1e-5, atol=1e-5)
+
+
+def test_fused_opt_step_matches_torch_adam():
+    """rl_opt_step (unscale, found-inf, clip_grad_norm_, Adam, GradScaler.update on flat buffers) against the
+    torch statement of rl_games' trancate_gradients_and_step on the same parameters, including a step with a
+    non-finite gradient (skipped, scale backed off) and a step the norm clip binds."""
+    from isaacgymenv_amd.rl import gae
+    torch.manual_seed(3)
+    sizes = [(512, 188), (512,), (256, 512), (256,), (12, 128), (12,), (1,)]
+    n = sum(int(np.prod(s)) for s in sizes)
+    flat0 = torch.randn(n, device="cuda") * 0.1
+    # torch reference: separate parameter tensors, fused capturable Adam, a manual GradScaler update
+    ref = [torch.nn.Parameter(t.clone().view(s)) for t, s in zip(torch.split(flat0, [int(np.prod(s)) for s in sizes]), sizes)]
+    lr = torch.tensor(3e-4, device="cuda")
+    opt = torch.optim.Adam(ref, lr=lr, eps=1e-8, fused=True, capturable=True)
+    scale_ref = torch.tensor(65536.0, device="cuda")
+    tracker_ref = 0
+    # fused: flat buffers
+    p, m, v = flat0.clone(), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    step = torch.zeros((), device="cuda")
+    scale = torch.tensor(65536.0, device="cuda")
+    tracker = torch.zeros((), dtype=torch.int32, device="cuda")
+    part = torch.empty(gae.lib().rl_opt_partials_size(), device="cuda")
+    hyper = gae.OptHyper(1.0, 0.9, 0.999, 1e-8, 0.0, 0.5, 2.0, 3)
+    for it in range(8):
+        g = torch.randn(n, device="cuda") * (0.05 if it % 2 else 5.0) * float(scale_ref)  # odd steps: clip inactive
+        if it == 4:
+            g[123] = float("inf")
+        for t, gg in zip(ref, torch.split(g, [t.numel() for t in ref])):
+            t.grad = gg.view_as(t).clone()
+        inv = 1.0 / float(scale_ref)
+        for t in ref:
+            t.grad.mul_(inv)
+        found = not all(torch.isfinite(t.grad).all() for t in ref)
+        if not found:
+            torch.nn.utils.clip_grad_norm_(ref, 1.0)
+            opt.step()
+            tracker_ref += 1
+            if tracker_ref == 3:
+                scale_ref *= 2.0
+                tracker_ref = 0
+        else:
+            scale_ref *= 0.5
+            tracker_ref = 0
+        gae.opt_step(p, g, m, v, step, lr, scale, tracker, hyper, part)
+        torch.cuda.synchronize()
+        assert float(scale) == float(scale_ref) and int(tracker) == tracker_ref, (it, float(scale), float(scale_ref))
+        flat_ref = torch.cat([t.detach().reshape(-1) for t in ref])
+        torch.testing.assert_close(p, flat_ref, rtol=1e-5, atol=1e-7)
+    assert float(step) == 7.0  # the inf step was skipped
+    m_ref = torch.cat([opt.state[t]["exp_avg"].reshape(-1) for t in ref])
+    v_ref = torch.cat([opt.state[t]["exp_avg_sq"].reshape(-1) for t in ref])
+    torch.testing.assert_close(m, m_ref, rtol=1e-5, atol=1e-9)
+    torch.testing.assert_close(v, v_ref, rtol=1e-5, atol=1e-12)
