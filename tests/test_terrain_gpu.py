@@ -49,12 +49,19 @@ def test_rough_terrain_one_simulate_matches_oracle():
     g_root, g_dof, g_cf, r, d, cf = _gpu_vs_oracle(ter, n, seed=2, steps=1)
     assert np.abs(cf).sum(axis=(1, 2)).astype(bool).mean() > 0.5, "most envs must touch the mesh"
     assert np.all(np.isfinite(g_root)) and np.all(np.isfinite(g_dof))
-    # contact activity / closest-triangle choices can switch on a last-bit difference (stair edges)
-    H.assert_mostly_close(g_root[:, 0:7], r[:, 0:7], atol=2e-5, max_frac=5e-3, what="root pose")
-    H.assert_mostly_close(g_dof[:, :, 0], d[:, :, 0], atol=2e-5, max_frac=5e-3, what="dof pos")
-    H.assert_mostly_close(g_root[:, 7:13], r[:, 7:13], atol=5e-3, rtol=5e-3, max_frac=5e-3, what="root vel")
-    H.assert_mostly_close(g_dof[:, :, 1], d[:, :, 1], atol=5e-3, rtol=5e-3, max_frac=5e-3, what="dof vel")
-    H.assert_mostly_close(g_cf, cf, atol=1.0, rtol=2e-2, max_frac=5e-3, what="contact forces")
+    # contact activity / closest-triangle choices can switch on a last-bit difference (stair edges): such an
+    # env must be one the oracle itself moves under an fp32-sized perturbation
+    art, flat = H.anymal()
+    params = dict(H.ANYMAL_PARAMS, has_ground=0)
+    root0, dof0, tau, mu = _terrain_states(n, ter, 2)
+
+    def rerun(idx, rng):
+        rr, dd = H.perturbed(root0, dof0, idx, rng)
+        c = np.zeros((len(idx), flat["nb"], 3))
+        OracleSim(flat, params, terrain=ter["oracle"]).simulate(rr, dd, np.ascontiguousarray(tau[idx]), mu[idx], c)
+        return H.state_fields(rr, dd, c)
+    print(H.assert_close_or_explained(H.state_fields(g_root, g_dof, g_cf), H.state_fields(r, d, cf), rerun,
+                                      what="rough terrain gpu"))
 
 
 def test_flat_mesh_gpu_equals_plane_gpu(monkeypatch):
