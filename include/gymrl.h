@@ -137,7 +137,7 @@ int rl_rollout_post(const float *rewards, const void *dones, int32_t dones_bytes
                     void *stream);
 
 /*
- * ABI 4 -- the minibatch optimizer step over the learner's flat buffers (rl_games a2c_common.py
+ * ABI 4 -- the act-forward MLP (rl_act_mlp, below) and the minibatch optimizer step over the learner's flat buffers (rl_games a2c_common.py
  * trancate_gradients_and_step: scaler.unscale_, clip_grad_norm_, scaler.step(Adam), scaler.update):
  *   g = grad / scale (scale null: 1, no skipping, no update); found_inf = any non-finite g;
  *   unless found_inf: g *= min(1, max_norm / (||g|| + 1e-6)) when max_norm > 0; g += weight_decay * p;
@@ -159,6 +159,27 @@ int rl_opt_step(float *param, const float *grad, float *exp_avg, float *exp_avg_
                 const float *lr, float *scale, int32_t *growth_tracker, const rl_opt_hyper *hyper, float *partials,
                 void *stream);
 int rl_opt_partials_size(void);
+
+/*
+ * The act forward of the actor-critic MLP as one kernel (rl_games ModelA2CContinuousLogStd eval forward of a
+ * fixed-sigma model: running_mean_std input normalisation -- running_mean / running_var [obs_dim] float64, both
+ * null for none -- then the actor MLP of Linear + ELU layers, the critic MLP when `critic` is not null (separate:
+ * True; null = shared trunk), mu = Linear(actor trunk) [rows][num_actions] and value = Linear(critic trunk)
+ * [rows] (the normalised value: rl_policy_head unnormalises it).  Layer l: weight [dims[l+1]][dims[l]] and bias
+ * [dims[l+1]] f32 (nn.Linear layout, 16-B aligned); widths multiples of 4 up to 512; f32 arithmetic.
+ */
+#define RL_MLP_MAX_LAYERS 4
+typedef struct rl_mlp {
+    int32_t num_layers;
+    int32_t dims[RL_MLP_MAX_LAYERS + 1];
+    const float *weight[RL_MLP_MAX_LAYERS];
+    const float *bias[RL_MLP_MAX_LAYERS];
+} rl_mlp;
+
+int rl_act_mlp(const float *obs, int32_t num_rows, int32_t obs_dim, const double *running_mean,
+               const double *running_var, double epsilon, const rl_mlp *actor, const rl_mlp *critic,
+               const float *mu_w, const float *mu_b, int32_t num_actions, const float *value_w, const float *value_b,
+               float *mu_out, float *value_out, void *stream);
 
 #ifdef __cplusplus
 }

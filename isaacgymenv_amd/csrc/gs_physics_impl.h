@@ -168,11 +168,14 @@ __global__ __launch_bounds__(kTerrWave, 1) void k_pd_step_wave(const DevModel* _
 
 }  // namespace gs_phys
 
-// launchers, one per kernel form (instantiated per topology in gs_phys_inst.hip).  Plane sims with
-// self-collision whose envs are LDS-starved (<= 4 env lanes per workgroup: UsefulHound) run the wave-assisted
-// kernels too, so their pair narrowphase is spread over the wave; mesh sims always do.
+// launchers, one per kernel form (instantiated per topology in gs_phys_inst.hip).  Mesh sims run the
+// wave-assisted kernels; with GS_WAVE_PLANE_SELF plane sims with self-collision whose envs are LDS-starved
+// (<= 4 env lanes per workgroup: UsefulHound) do too.
+// (off: measured slower for UsefulHound, the only such topology -- 4.68 vs 4.17 ms per substep: the pair records
+// cost it a workgroup per CU of LDS while its substep is bound by the solver lane's scratch latency, not by the
+// narrowphase; profiles/r03f_hound_ab.txt)
 #ifndef GS_WAVE_PLANE_SELF
-#define GS_WAVE_PLANE_SELF 1
+#define GS_WAVE_PLANE_SELF 0
 #endif
 template <class T>
 constexpr bool kWavePlaneSelf = GS_WAVE_PLANE_SELF && T::NPK > 0 && LaneCfg<T, false>::LB <= 4 && !LaneCfg<T, false>::GLOBAL;

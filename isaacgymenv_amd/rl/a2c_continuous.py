@@ -226,8 +226,9 @@ class A2CAgent:
             b1, b2 = self.optimizer.defaults["betas"]
             self._opt_hyper = gae.OptHyper(cfg.grad_norm if cfg.truncate_grads else 0.0, b1, b2,
                                            self.optimizer.defaults["eps"], cfg.weight_decay,
-                                           self.scaler.get_backoff_factor(), self.scaler.get_growth_factor(),
-                                           self.scaler.get_growth_interval())
+                                           *((self.scaler.get_backoff_factor(), self.scaler.get_growth_factor(),
+                                              self.scaler.get_growth_interval()) if self.scaler.is_enabled()
+                                             else (0.5, 2.0, 2000)))
         H, N, O, A = self.horizon, self.num_actors, self.obs_dim, self.actions_num
         dev = self.device
         # env-major experience (flattened batch = view); time-major GAE inputs

@@ -23,6 +23,8 @@ _ACT = {"elu": nn.ELU, "relu": nn.ReLU, "tanh": nn.Tanh, "selu": nn.SELU, "None"
 # library tiles only the small N x K output (24-48 workgroups for 512 x 188) and takes ~100 us on
 # MI355X; split, ~25 us (tools/probes/gemm_splitk.py).  The sum is one HIP kernel that accumulates
 # into weight.grad (rl_splitk_accum, csrc/rl_grad.hip).
+# the act forward's network as one HIP kernel (gae.act_mlp); False: the torch Linear / ELU statements
+USE_ACT_KERNEL = True
 SPLIT_K = 16
 SPLIT_K_MIN_ROWS = 4096
 
@@ -160,6 +162,22 @@ class ModelA2CContinuousLogStd(nn.Module):
         if normalize_input:
             self.running_mean_std = RunningMeanStd((obs_dim,))
 
+    def _act_mlps(self):
+        """(actor, critic or None) rl_mlp descriptors for gae.act_mlp, or None when the act kernel cannot run this
+        model (the parameter pointers are stable: the learner keeps them as views into its flat buffer)."""
+        if not USE_ACT_KERNEL:
+            return None
+        if getattr(self, "_act_desc", None) is None:
+            net = self.a2c_network
+            a = gae.mlp_desc(net.actor_mlp)
+            c = gae.mlp_desc(net.critic_mlp) if net.separate else None
+            ok = a is not None and (c is not None or not net.separate) and net.mu.weight.dtype == torch.float32
+            if ok and self.normalize_input:
+                rms = self.running_mean_std
+                ok = rms.running_mean.dtype == torch.float64 and not rms.norm_only
+            self._act_desc = (a, c) if ok else False
+        return self._act_desc or None
+
     def norm_obs(self, obs):
         with torch.no_grad():
             return self.running_mean_std(obs) if self.normalize_input else obs
@@ -176,19 +194,29 @@ class ModelA2CContinuousLogStd(nn.Module):
     def forward(self, input_dict: Dict[str, torch.Tensor]):
         is_train = input_dict.get("is_train", True)
         prev_actions = input_dict.get("prev_actions", None)
-        obs = self.norm_obs(input_dict["obs"])
+        raw = input_dict["obs"]
         net = self.a2c_network
-        if (not is_train and obs.is_cuda and obs.dtype == torch.float32 and net.fixed_sigma
+        if (not is_train and raw.is_cuda and raw.dtype == torch.float32 and net.fixed_sigma
                 and (not self.normalize_value or self.value_mean_std.running_mean.numel() == 1)):
-            # act forward on the device: the network, torch's normal_ draws, then one kernel for the head
-            a_out = net.actor_mlp(obs)
-            c_out = net.critic_mlp(obs) if net.separate else a_out
-            value = net.value(c_out).contiguous()
-            mu = net.mu(a_out).contiguous()
+            # act forward on the device: the network (one kernel, gae.act_mlp, when its layers allow it and the input
+            # statistics are frozen -- eval mode, as rl_games' play_steps sets), torch's normal_ draws, then one
+            # kernel for the head
+            frozen = not (self.normalize_input and self.running_mean_std.training)
+            mlps = self._act_mlps() if frozen and raw.is_contiguous() else None
+            if mlps is not None:
+                mu, value = gae.act_mlp(raw, self.running_mean_std if self.normalize_input else None,
+                                        mlps[0], mlps[1], net.mu, net.value)
+            else:
+                obs = self.norm_obs(raw)
+                a_out = net.actor_mlp(obs)
+                c_out = net.critic_mlp(obs) if net.separate else a_out
+                value = net.value(c_out).contiguous()
+                mu = net.mu(a_out).contiguous()
             noise = torch.empty_like(mu).normal_(0.0, 1.0)
             actions, sigmas, neglogp, values = gae.policy_head(
                 mu, noise, net.sigma.detach(), value, self.value_mean_std if self.normalize_value else None)
             return {"neglogpacs": neglogp, "values": values, "actions": actions, "mus": mu, "sigmas": sigmas}
+        obs = self.norm_obs(raw)
         mu, logstd, value = self.a2c_network(obs)
         sigma = torch.exp(logstd)
         distr = torch.distributions.Normal(mu, sigma, validate_args=False)

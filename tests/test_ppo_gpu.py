@@ -405,3 +405,42 @@ def test_fused_opt_step_matches_torch_adam():
     v_ref = torch.cat([opt.state[t]["exp_avg_sq"].reshape(-1) for t in ref])
     torch.testing.assert_close(m, m_ref, rtol=1e-5, atol=1e-9)
     torch.testing.assert_close(v, v_ref, rtol=1e-5, atol=1e-12)
+
+
+@pytest.mark.parametrize("units,separate,obs_dim,actions", [([512, 256, 128], True, 188, 12), ([32, 32], False, 4, 1),
+                                                             ([256, 128, 64], True, 60, 8)])
+def test_act_mlp_kernel_matches_torch_network(units, separate, obs_dim, actions):
+    """rl_act_mlp (normalisation, actor [+ critic] Linear + ELU layers, mu / value heads in one kernel) against the
+    torch statement of the same eval forward (AnymalTerrain, Cartpole and Ant network shapes)."""
+    from isaacgymenv_amd.rl import gae, network
+    from isaacgymenv_amd.rl.network import ActorCriticNetwork, ModelA2CContinuousLogStd
+    torch.manual_seed(5)
+    net = ActorCriticNetwork(obs_dim, actions, units, "elu", separate, True, 0.0)
+    model = ModelA2CContinuousLogStd(net, obs_dim, True, True).cuda().eval()
+    with torch.no_grad():
+        for p_ in model.parameters():
+            p_.normal_(0.0, 0.1)
+        model.running_mean_std.running_mean.normal_(0.0, 0.5)
+        model.running_mean_std.running_var.uniform_(0.5, 2.0)
+    obs = torch.randn(4096 + 3, obs_dim, device="cuda") * 2.0  # a partial last workgroup too
+    mlps = model._act_mlps()
+    assert mlps is not None
+    mu, value = gae.act_mlp(obs, model.running_mean_std, mlps[0], mlps[1], net.mu, net.value)
+    with torch.no_grad():
+        x = model.norm_obs(obs)
+        a = net.actor_mlp(x)
+        c = net.critic_mlp(x) if separate else a
+        mu_ref, v_ref = net.mu(a), net.value(c)
+    torch.testing.assert_close(mu, mu_ref, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(value, v_ref, rtol=1e-4, atol=1e-5)
+    # and through the model's act forward (same sampling stream either way)
+    network.USE_ACT_KERNEL = False
+    try:
+        torch.manual_seed(9)
+        ref = model({"is_train": False, "obs": obs})
+    finally:
+        network.USE_ACT_KERNEL = True
+    torch.manual_seed(9)
+    got = model({"is_train": False, "obs": obs})
+    for k in ("mus", "values", "actions", "neglogpacs"):
+        torch.testing.assert_close(got[k], ref[k], rtol=1e-4, atol=1e-4)
