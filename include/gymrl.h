@@ -166,7 +166,7 @@ int rl_opt_partials_size(void);
  * null for none -- then the actor MLP of Linear + ELU layers, the critic MLP when `critic` is not null (separate:
  * True; null = shared trunk), mu = Linear(actor trunk) [rows][num_actions] and value = Linear(critic trunk)
  * [rows] (the normalised value: rl_policy_head unnormalises it).  Layer l: weight [dims[l+1]][dims[l]] and bias
- * [dims[l+1]] f32 (nn.Linear layout, 16-B aligned); widths multiples of 4 up to 512; f32 arithmetic.
+ * [dims[l+1]] f32 (nn.Linear layout); widths multiples of 4 up to 512; f32 arithmetic.  Two launches.
  */
 #define RL_MLP_MAX_LAYERS 4
 typedef struct rl_mlp {
@@ -179,7 +179,9 @@ typedef struct rl_mlp {
 int rl_act_mlp(const float *obs, int32_t num_rows, int32_t obs_dim, const double *running_mean,
                const double *running_var, double epsilon, const rl_mlp *actor, const rl_mlp *critic,
                const float *mu_w, const float *mu_b, int32_t num_actions, const float *value_w, const float *value_b,
-               float *mu_out, float *value_out, void *stream);
+               float *mu_out, float *value_out, float *workspace, void *stream);
+/* f32 scratch rl_act_mlp needs (the hidden layers' weights transposed, refreshed by every call) */
+int rl_act_mlp_workspace_floats(const rl_mlp *actor, const rl_mlp *critic);
 
 #ifdef __cplusplus
 }

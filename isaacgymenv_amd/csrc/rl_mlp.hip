@@ -6,9 +6,10 @@
 // f32 GEMM and one ELU pass per layer, the heads), each latency-bound at 4096 rows (GEMMs of 8-16 us, 4-6 us
 // elementwise passes).  Here a workgroup takes R rows through every layer with the activations in LDS:
 //   * the normalised rows (the reference's clamp((x - float(mean)) / sqrt(float(var) + eps), -5, 5)) in LDS;
+//   * the layers' weights transposed into a workspace first (one launch, k_transpose: always the live weights);
 //   * a layer of J outputs: thread t owns column t (and t + 256 when J > 256) for the workgroup's rows (or a
-//     row group when J < 256); each 16-B weight load W[j][k..k+3] serves all its rows, the rows' inputs are
-//     16-B LDS broadcasts; bias + ELU (alpha 1: x > 0 ? x : exp(x) - 1) in f32, result to the other LDS buffer;
+//     row group when J < 256); a weight load Wt[k][j] is coalesced across the wave and serves all its rows,
+//     the rows' inputs are 16-B LDS broadcasts; bias + ELU (alpha 1: x > 0 ? x : exp(x) - 1) in f32, result to the other LDS buffer;
 //   * the heads: one thread per (row, output).
 // f32 throughout, accumulation in k order (not hipBLASLt's order: results agree with the torch statement to
 // float rounding, tests/test_ppo_gpu.py).
@@ -33,8 +34,9 @@ struct Mlp {
   int layers;
 };
 
-// one Linear + ELU layer on the workgroup's rows: in [R][K] (LDS, row stride ldi) -> out [R][J] (row stride ldo)
-__device__ __forceinline__ void layer(const float* __restrict__ W, const float* __restrict__ bias, int K, int J,
+// one Linear + ELU layer on the workgroup's rows: in [R][K] (LDS, row stride ldi) -> out [R][J] (row stride ldo);
+// Wt [K][J] is the layer's weight transposed (k_transpose), so a wave's weight load is 64 consecutive columns
+__device__ __forceinline__ void layer(const float* __restrict__ Wt, const float* __restrict__ bias, int K, int J,
                                       const float* in, int ldi, float* out, int ldo, bool elu) {
   const int t = threadIdx.x;
   const int Jt = J < kThreads ? J : kThreads;
@@ -42,25 +44,28 @@ __device__ __forceinline__ void layer(const float* __restrict__ W, const float* 
   const int j0 = t % Jt, g = t / Jt;
   if (g >= G) return;
   const bool two = J > kThreads && j0 + kThreads < J;
+  const int j1 = two ? j0 + kThreads : j0;
   float acc0[kRows], acc1[kRows];
 #pragma unroll
   for (int r = 0; r < kRows; ++r) { acc0[r] = 0.f; acc1[r] = 0.f; }
-  const float* w0 = W + (size_t)j0 * K;
-  const float* w1 = W + (size_t)(two ? j0 + kThreads : j0) * K;
   for (int k = 0; k < K; k += 4) {
-    const float4 a = *reinterpret_cast<const float4*>(w0 + k);
-    const float4 c = two ? *reinterpret_cast<const float4*>(w1 + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float a[4], c[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      a[q] = Wt[(size_t)(k + q) * J + j0];
+      c[q] = two ? Wt[(size_t)(k + q) * J + j1] : 0.f;
+    }
 #pragma unroll
     for (int rr = 0; rr < kRows; ++rr) {
       const int r = g + rr * G;
       if (r < kRows) {
         const float4 x = *reinterpret_cast<const float4*>(in + r * ldi + k);
-        acc0[rr] = fmaf(x.w, a.w, fmaf(x.z, a.z, fmaf(x.y, a.y, fmaf(x.x, a.x, acc0[rr]))));
-        acc1[rr] = fmaf(x.w, c.w, fmaf(x.z, c.z, fmaf(x.y, c.y, fmaf(x.x, c.x, acc1[rr]))));
+        acc0[rr] = fmaf(x.w, a[3], fmaf(x.z, a[2], fmaf(x.y, a[1], fmaf(x.x, a[0], acc0[rr]))));
+        if (two) acc1[rr] = fmaf(x.w, c[3], fmaf(x.z, c[2], fmaf(x.y, c[1], fmaf(x.x, c[0], acc1[rr]))));
       }
     }
   }
-  const float b0 = bias[j0], b1 = two ? bias[j0 + kThreads] : 0.f;
+  const float b0 = bias[j0], b1 = two ? bias[j1] : 0.f;
 #pragma unroll
   for (int rr = 0; rr < kRows; ++rr) {
     const int r = g + rr * G;
@@ -71,10 +76,35 @@ __device__ __forceinline__ void layer(const float* __restrict__ W, const float* 
       if (two) {
         float y1 = acc1[rr] + b1;
         if (elu) y1 = y1 > 0.f ? y1 : expf(y1) - 1.f;
-        out[r * ldo + j0 + kThreads] = y1;
+        out[r * ldo + j1] = y1;
       }
     }
   }
+}
+
+// every hidden layer's weight transposed into the workspace, one launch: workgroup b takes a 32 x 32 tile of the
+// layer whose tile range holds b (tile prefix in Tr)
+struct Tr {
+  const float* w[2 * RL_MLP_MAX_LAYERS];
+  float* wt[2 * RL_MLP_MAX_LAYERS];
+  int rows[2 * RL_MLP_MAX_LAYERS], cols[2 * RL_MLP_MAX_LAYERS];  // W [rows][cols]
+  int tile0[2 * RL_MLP_MAX_LAYERS + 1];
+  int n;
+};
+__global__ __launch_bounds__(256) void k_transpose(Tr T) {
+  __shared__ float tile[32][33];
+  int l = 0;
+  while (l + 1 < T.n && (int)blockIdx.x >= T.tile0[l + 1]) ++l;
+  const int b = blockIdx.x - T.tile0[l];
+  const int R = T.rows[l], Cc = T.cols[l];
+  const int tc = (Cc + 31) / 32;
+  const int r0 = (b / tc) * 32, c0 = (b % tc) * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int y = ty; y < 32; y += 8)
+    if (r0 + y < R && c0 + tx < Cc) tile[y][tx] = T.w[l][(size_t)(r0 + y) * Cc + c0 + tx];
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8)
+    if (c0 + y < Cc && r0 + tx < R) T.wt[l][(size_t)(c0 + y) * R + r0 + tx] = tile[tx][y];
 }
 
 // the hidden layers of one MLP from `x` (LDS); returns the buffer holding the last hidden layer
@@ -148,10 +178,19 @@ __global__ __launch_bounds__(kThreads) void k_act_mlp(const float* __restrict__ 
 
 }  // namespace
 
+extern "C" int rl_act_mlp_workspace_floats(const rl_mlp* actor, const rl_mlp* critic) {
+  int64_t n = 0;
+  const rl_mlp* src[2] = {actor, critic};
+  for (int s = 0; s < 2; ++s)
+    if (src[s])
+      for (int l = 0; l < src[s]->num_layers && l < RL_MLP_MAX_LAYERS; ++l) n += (int64_t)src[s]->dims[l] * src[s]->dims[l + 1];
+  return (int)n;
+}
+
 extern "C" int rl_act_mlp(const float* obs, int32_t num_rows, int32_t obs_dim, const double* running_mean,
                           const double* running_var, double epsilon, const rl_mlp* actor, const rl_mlp* critic,
                           const float* mu_w, const float* mu_b, int32_t num_actions, const float* value_w,
-                          const float* value_b, float* mu_out, float* value_out, void* stream) {
+                          const float* value_b, float* mu_out, float* value_out, float* workspace, void* stream) {
   if (!obs || !actor || !mu_w || !mu_b || !value_w || !value_b || !mu_out || !value_out || num_rows <= 0)
     return rl_set_error("rl_act_mlp: null pointer or num_rows <= 0");
   if ((running_mean == nullptr) != (running_var == nullptr))
@@ -170,14 +209,33 @@ extern "C" int rl_act_mlp(const float* obs, int32_t num_rows, int32_t obs_dim, c
       m[s].dims[l] = d.dims[l];
     }
     for (int l = 0; l < d.num_layers; ++l) {
-      if (!d.weight[l] || !d.bias[l] || (reinterpret_cast<uintptr_t>(d.weight[l]) & 15))
-        return rl_set_error("rl_act_mlp: null or unaligned layer weights");
+      if (!d.weight[l] || !d.bias[l]) return rl_set_error("rl_act_mlp: null layer weights");
       m[s].w[l] = d.weight[l];
       m[s].b[l] = d.bias[l];
     }
   }
   if (!critic) m[1] = m[0];
   if (num_actions <= 0 || num_actions > 256) return rl_set_error("rl_act_mlp: 0 < num_actions <= 256");
+  if (!workspace) return rl_set_error("rl_act_mlp: null workspace (rl_act_mlp_workspace_floats floats)");
+  // transposed weights into the workspace (the MLP kernel reads them), then the MLP
+  Tr T{};
+  float* ws = workspace;
+  T.tile0[0] = 0;
+  for (int s = 0; s < 2; ++s) {
+    if (!src[s]) continue;
+    for (int l = 0; l < m[s].layers; ++l) {
+      const int i = T.n++;
+      T.w[i] = m[s].w[l];
+      T.rows[i] = m[s].dims[l + 1];
+      T.cols[i] = m[s].dims[l];
+      T.wt[i] = ws;
+      ws += (size_t)T.rows[i] * T.cols[i];
+      T.tile0[i + 1] = T.tile0[i] + ((T.rows[i] + 31) / 32) * ((T.cols[i] + 31) / 32);
+      m[s].w[l] = T.wt[i];
+    }
+  }
+  if (!critic) m[1] = m[0];
+  hipLaunchKernelGGL(k_transpose, dim3(T.tile0[T.n]), dim3(256), 0, (hipStream_t)stream, T);
   hipLaunchKernelGGL(k_act_mlp, dim3((num_rows + kRows - 1) / kRows), dim3(kThreads), 0, (hipStream_t)stream, obs,
                      (int)num_rows, (int)obs_dim, running_mean, running_var, (float)epsilon, m[0], m[1],
                      critic ? 1 : 0, mu_w, mu_b, (int)num_actions, value_w, value_b, mu_out, value_out);

@@ -15,7 +15,7 @@ import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libgymrl.so")
 EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accum", "rl_colsum_accum", "rl_rollout_post",
-                    "rl_ppo_loss", "rl_ppo_loss_backward", "rl_rms_normalize", "rl_opt_step", "rl_opt_partials_size", "rl_act_mlp",
+                    "rl_ppo_loss", "rl_ppo_loss_backward", "rl_rms_normalize", "rl_opt_step", "rl_opt_partials_size", "rl_act_mlp", "rl_act_mlp_workspace_floats",
                     "rl_policy_head"]
 _lib = None
 
@@ -67,7 +67,9 @@ def lib():
                                            vp]
         L.rl_act_mlp.restype = C.c_int
         L.rl_act_mlp.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, C.c_double, C.POINTER(Mlp), C.POINTER(Mlp), vp, vp,
-                                 C.c_int32, vp, vp, vp, vp, vp]
+                                 C.c_int32, vp, vp, vp, vp, vp, vp]
+        L.rl_act_mlp_workspace_floats.restype = C.c_int
+        L.rl_act_mlp_workspace_floats.argtypes = [C.POINTER(Mlp), C.POINTER(Mlp)]
         L.rl_opt_step.restype = C.c_int
         L.rl_opt_step.argtypes = [vp, vp, vp, vp, C.c_int64, vp, vp, vp, vp, C.POINTER(OptHyper), vp, vp]
         L.rl_opt_partials_size.restype = C.c_int
@@ -342,7 +344,12 @@ def mlp_desc(seq) -> "Mlp | None":
     return d
 
 
-def act_mlp(obs, rms, actor: "Mlp", critic, mu_layer, value_layer):
+def act_mlp_workspace(actor: "Mlp", critic, device):
+    n = lib().rl_act_mlp_workspace_floats(C.byref(actor), C.byref(critic) if critic is not None else None)
+    return torch.empty(max(n, 1), dtype=torch.float32, device=device)
+
+
+def act_mlp(obs, rms, actor: "Mlp", critic, mu_layer, value_layer, workspace):
     """The act forward's network (include/gymrl.h rl_act_mlp): normalised obs -> (mu [N, A], value [N, 1])."""
     N, O = obs.shape
     A = mu_layer.out_features
@@ -355,7 +362,8 @@ def act_mlp(obs, rms, actor: "Mlp", critic, mu_layer, value_layer):
     rc = lib().rl_act_mlp(obs.data_ptr(), N, O, rm, rv, float(eps), C.byref(actor),
                           C.byref(critic) if critic is not None else None, mu_layer.weight.data_ptr(),
                           mu_layer.bias.data_ptr(), A, value_layer.weight.data_ptr(), value_layer.bias.data_ptr(),
-                          mu.data_ptr(), value.data_ptr(), torch.cuda.current_stream(obs.device).cuda_stream)
+                          mu.data_ptr(), value.data_ptr(), workspace.data_ptr(),
+                          torch.cuda.current_stream(obs.device).cuda_stream)
     if rc != 0:
         raise RuntimeError(f"rl_act_mlp failed: {lib().rl_last_error().decode()}")
     return mu, value

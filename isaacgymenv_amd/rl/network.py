@@ -175,7 +175,7 @@ class ModelA2CContinuousLogStd(nn.Module):
             if ok and self.normalize_input:
                 rms = self.running_mean_std
                 ok = rms.running_mean.dtype == torch.float64 and not rms.norm_only
-            self._act_desc = (a, c) if ok else False
+            self._act_desc = (a, c, gae.act_mlp_workspace(a, c, net.mu.weight.device)) if ok else False
         return self._act_desc or None
 
     def norm_obs(self, obs):
@@ -205,7 +205,7 @@ class ModelA2CContinuousLogStd(nn.Module):
             mlps = self._act_mlps() if frozen and raw.is_contiguous() else None
             if mlps is not None:
                 mu, value = gae.act_mlp(raw, self.running_mean_std if self.normalize_input else None,
-                                        mlps[0], mlps[1], net.mu, net.value)
+                                        mlps[0], mlps[1], net.mu, net.value, mlps[2])
             else:
                 obs = self.norm_obs(raw)
                 a_out = net.actor_mlp(obs)

@@ -425,7 +425,7 @@ def test_act_mlp_kernel_matches_torch_network(units, separate, obs_dim, actions)
     obs = torch.randn(4096 + 3, obs_dim, device="cuda") * 2.0  # a partial last workgroup too
     mlps = model._act_mlps()
     assert mlps is not None
-    mu, value = gae.act_mlp(obs, model.running_mean_std, mlps[0], mlps[1], net.mu, net.value)
+    mu, value = gae.act_mlp(obs, model.running_mean_std, mlps[0], mlps[1], net.mu, net.value, mlps[2])
     with torch.no_grad():
         x = model.norm_obs(obs)
         a = net.actor_mlp(x)
