@@ -23,8 +23,11 @@ _ACT = {"elu": nn.ELU, "relu": nn.ReLU, "tanh": nn.Tanh, "selu": nn.SELU, "None"
 # library tiles only the small N x K output (24-48 workgroups for 512 x 188) and takes ~100 us on
 # MI355X; split, ~25 us (tools/probes/gemm_splitk.py).  The sum is one HIP kernel that accumulates
 # into weight.grad (rl_splitk_accum, csrc/rl_grad.hip).
-# the act forward's network as one HIP kernel (gae.act_mlp); False: the torch Linear / ELU statements
-USE_ACT_KERNEL = True
+# the act forward's network as one HIP kernel (gae.act_mlp) instead of the torch Linear / ELU statements.  Off:
+# measured 365 us per call against ~0.14 ms for the whole torch act forward (profiles/r03h_kernel_stats.csv): its
+# f32 FMA chains wait on L2 weight loads with two waves per SIMD; kept (and parity-tested) as the base for a
+# staged-weight version
+USE_ACT_KERNEL = False
 SPLIT_K = 16
 SPLIT_K_MIN_ROWS = 4096
 

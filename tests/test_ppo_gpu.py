@@ -434,13 +434,15 @@ def test_act_mlp_kernel_matches_torch_network(units, separate, obs_dim, actions)
     torch.testing.assert_close(mu, mu_ref, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(value, v_ref, rtol=1e-4, atol=1e-5)
     # and through the model's act forward (same sampling stream either way)
-    network.USE_ACT_KERNEL = False
+    old = network.USE_ACT_KERNEL
     try:
+        network.USE_ACT_KERNEL = False
         torch.manual_seed(9)
         ref = model({"is_train": False, "obs": obs})
-    finally:
         network.USE_ACT_KERNEL = True
-    torch.manual_seed(9)
-    got = model({"is_train": False, "obs": obs})
+        torch.manual_seed(9)
+        got = model({"is_train": False, "obs": obs})
+    finally:
+        network.USE_ACT_KERNEL = old
     for k in ("mus", "values", "actions", "neglogpacs"):
         torch.testing.assert_close(got[k], ref[k], rtol=1e-4, atol=1e-4)
