@@ -409,11 +409,13 @@ def test_fused_opt_step_matches_torch_adam():
 
 @pytest.mark.parametrize("units,separate,obs_dim,actions", [([512, 256, 128], True, 188, 12), ([32, 32], False, 4, 1),
                                                              ([256, 128, 64], True, 60, 8)])
-def test_act_mlp_kernel_matches_torch_network(units, separate, obs_dim, actions):
+def test_act_mlp_kernel_matches_torch_network(units, separate, obs_dim, actions, monkeypatch):
     """rl_act_mlp (normalisation, actor [+ critic] Linear + ELU layers, mu / value heads in one kernel) against the
-    torch statement of the same eval forward (AnymalTerrain, Cartpole and Ant network shapes)."""
+    torch statement of the same eval forward (AnymalTerrain, Cartpole and Ant network shapes).  The kernel is off in
+    the learner by default (network.USE_ACT_KERNEL); the test switches it on for this model."""
     from isaacgymenv_amd.rl import gae, network
     from isaacgymenv_amd.rl.network import ActorCriticNetwork, ModelA2CContinuousLogStd
+    monkeypatch.setattr(network, "USE_ACT_KERNEL", True)
     torch.manual_seed(5)
     net = ActorCriticNetwork(obs_dim, actions, units, "elu", separate, True, 0.0)
     model = ModelA2CContinuousLogStd(net, obs_dim, True, True).cuda().eval()
