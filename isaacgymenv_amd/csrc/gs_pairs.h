@@ -16,6 +16,26 @@ namespace {
 
 GS_HD float dot3f(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
+// Visit rows k0 <= k < k1 of a model vertex table (4 floats per row) in index order, f(k, row).  The rows
+// are read 8 at a time before any is used: a hull's index range is wave-uniform, so the 8 rows are
+// independent scalar loads in flight together instead of one load-to-use wait per vertex (the tail
+// batch re-reads row k1 - 1 and skips it).  Same visits, same order as the plain loop.
+template <class F>
+GS_HD __attribute__((always_inline)) inline void for_rows8(const float (*tab)[4], int k0, int k1, F&& f) {
+  for (int kb = k0; kb < k1; kb += 8) {
+    float r[8][4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float* v = tab[kb + j < k1 ? kb + j : k1 - 1];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) r[j][t] = v[t];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (kb + j < k1) f(kb + j, r[j]);
+  }
+}
+
 // ---------------------------------------------------------------- hull vs ground
 // Vertices of hull shape sh (body pose R, X relative to the root origin; root height rootz) below
 // contact_offset, reduced to at most 4: the deepest; the farthest from it horizontally; the one spanning the
@@ -24,64 +44,63 @@ GS_HD float dot3f(const float* a, const float* b) { return a[0] * b[0] + a[1] * 
 GS_HD int hull_ground_select(const DevModel* __restrict__ M, int sh, const float* R, const float* X, float rootz,
                              float off, int* sel) {
   const int v0 = M->hv0[sh], v1 = M->hv1[sh];
-  auto world = [&](int k, float* w) {
-    const float* v = M->hv[k];
+  auto world = [&](const float* v, float* w) {
     w[0] = X[0] + R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
     w[1] = X[1] + R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
     w[2] = rootz + X[2] + R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
   };
   int i0 = -1;
   float zmin = 3.0e38f;
-  for (int k = v0; k < v1; ++k) {
+  for_rows8(M->hv, v0, v1, [&](int k, const float* v) {
     float w[3];
-    world(k, w);
+    world(v, w);
     if (w[2] < zmin) { zmin = w[2]; i0 = k; }
-  }
+  });
   if (i0 < 0 || !(zmin < off)) return 0;
   int n = 0;
   float p0[3];
-  world(i0, p0);
+  world(M->hv[i0], p0);
   sel[n++] = i0;
   int i1 = -1;
   float best = 1e-10f;
-  for (int k = v0; k < v1; ++k) {
+  for_rows8(M->hv, v0, v1, [&](int k, const float* v) {
     float w[3];
-    world(k, w);
-    if (!(w[2] < off)) continue;
+    world(v, w);
+    if (!(w[2] < off)) return;
     const float d2 = (w[0] - p0[0]) * (w[0] - p0[0]) + (w[1] - p0[1]) * (w[1] - p0[1]);
     if (d2 > best) { best = d2; i1 = k; }
-  }
+  });
   if (i1 < 0) return n;
   float p1[3];
-  world(i1, p1);
+  world(M->hv[i1], p1);
   sel[n++] = i1;
   const float ex = p1[0] - p0[0], ey = p1[1] - p0[1];
   int i2 = -1;
   best = 1e-10f;
-  for (int k = v0; k < v1; ++k) {
+  for_rows8(M->hv, v0, v1, [&](int k, const float* v) {
     float w[3];
-    world(k, w);
-    if (!(w[2] < off)) continue;
+    world(v, w);
+    if (!(w[2] < off)) return;
     const float a = fabsf(ex * (w[1] - p0[1]) - ey * (w[0] - p0[0]));
     if (a > best) { best = a; i2 = k; }
-  }
+  });
   if (i2 < 0) return n;
   float p2[3];
-  world(i2, p2);
+  world(M->hv[i2], p2);
   sel[n++] = i2;
   const float sg = (ex * (p2[1] - p0[1]) - ey * (p2[0] - p0[0])) > 0.f ? 1.f : -1.f;
   int i3 = -1;
   best = 1e-10f;
-  for (int k = v0; k < v1; ++k) {
+  for_rows8(M->hv, v0, v1, [&](int k, const float* v) {
     float w[3];
-    world(k, w);
-    if (!(w[2] < off)) continue;
+    world(v, w);
+    if (!(w[2] < off)) return;
     const float e0 = sg * ((p1[0] - p0[0]) * (w[1] - p0[1]) - (p1[1] - p0[1]) * (w[0] - p0[0]));
     const float e1 = sg * ((p2[0] - p1[0]) * (w[1] - p1[1]) - (p2[1] - p1[1]) * (w[0] - p1[0]));
     const float e2 = sg * ((p0[0] - p2[0]) * (w[1] - p2[1]) - (p0[1] - p2[1]) * (w[0] - p2[0]));
     const float mn = fminf(fminf(e0, e1), e2);
     if (-mn > best) { best = -mn; i3 = k; }
-  }
+  });
   if (i3 >= 0) sel[n++] = i3;
   return n;
 }
@@ -169,15 +188,14 @@ GS_HD void core_support(const DevModel* __restrict__ M, int sh, const ShapeW& W,
   } else {
     const float dl[3] = {W.R[0] * d[0] + W.R[3] * d[1] + W.R[6] * d[2], W.R[1] * d[0] + W.R[4] * d[1] + W.R[7] * d[2],
                          W.R[2] * d[0] + W.R[5] * d[1] + W.R[8] * d[2]};
-    const float* cc = M->shc[sh];
+    const float cc[3] = {M->shc[sh][0], M->shc[sh][1], M->shc[sh][2]};
     float best = -3.0e38f, bv[3] = {0.f, 0.f, 0.f};
-    for (int k = M->pv0[sh]; k < M->pv1[sh]; ++k) {
-      const float* v = M->pv[k];
+    for_rows8(M->pv, M->pv0[sh], M->pv1[sh], [&](int, const float* v) {
       const float f = v[3];
       const float p[3] = {cc[0] + f * (v[0] - cc[0]), cc[1] + f * (v[1] - cc[1]), cc[2] + f * (v[2] - cc[2])};
       const float t = dot3f(p, dl);
       if (t > best) { best = t; bv[0] = p[0]; bv[1] = p[1]; bv[2] = p[2]; }
-    }
+    });
     mat3vec(W.R, bv, out);
 #pragma unroll
     for (int k = 0; k < 3; ++k) out[k] += W.c[k];
@@ -249,39 +267,39 @@ GS_HD float core_feature(const DevModel* __restrict__ M, int sh, const ShapeW& W
   }
   const float dl[3] = {W.R[0] * d[0] + W.R[3] * d[1] + W.R[6] * d[2], W.R[1] * d[0] + W.R[4] * d[1] + W.R[7] * d[2],
                        W.R[2] * d[0] + W.R[5] * d[1] + W.R[8] * d[2]};
-  const float* cc = M->shc[sh];
-  auto corev = [&](int k, float* p) {
-    const float* v = M->pv[k];
+  const float cc[3] = {M->shc[sh][0], M->shc[sh][1], M->shc[sh][2]};
+  auto corev = [&](const float* v, float* p) {
     const float f = v[3];
     p[0] = cc[0] + f * (v[0] - cc[0]); p[1] = cc[1] + f * (v[1] - cc[1]); p[2] = cc[2] + f * (v[2] - cc[2]);
   };
+  const int k0 = M->pv0[sh], k1 = M->pv1[sh];
   float hmax = -3.0e38f;
-  for (int k = M->pv0[sh]; k < M->pv1[sh]; ++k) {
+  for_rows8(M->pv, k0, k1, [&](int, const float* v) {
     float p[3];
-    corev(k, p);
+    corev(v, p);
     hmax = fmaxf(hmax, dot3f(p, dl));
-  }
+  });
   float acc[3] = {0.f, 0.f, 0.f};
   int n = 0;
-  for (int k = M->pv0[sh]; k < M->pv1[sh]; ++k) {
+  for_rows8(M->pv, k0, k1, [&](int, const float* v) {
     float p[3];
-    corev(k, p);
+    corev(v, p);
     if (dot3f(p, dl) >= hmax - kFeatureEps) {
       acc[0] += p[0]; acc[1] += p[1]; acc[2] += p[2];
       ++n;
     }
-  }
+  });
   const float inv = 1.f / (float)n;
   acc[0] *= inv; acc[1] *= inv; acc[2] *= inv;
   float ext = 0.f;
-  for (int k = M->pv0[sh]; k < M->pv1[sh]; ++k) {
+  for_rows8(M->pv, k0, k1, [&](int, const float* v) {
     float p[3];
-    corev(k, p);
+    corev(v, p);
     if (dot3f(p, dl) >= hmax - kFeatureEps) {
       const float dd[3] = {p[0] - acc[0], p[1] - acc[1], p[2] - acc[2]};
       ext = fmaxf(ext, sqrtf(dot3f(dd, dd)));
     }
-  }
+  });
   mat3vec(W.R, acc, cen);
 #pragma unroll
   for (int k = 0; k < 3; ++k) cen[k] += W.c[k];
@@ -674,10 +692,33 @@ GS_HD int self_contacts(const DevModel* __restrict__ M, const DevParams& P, cons
       if (n < T::NPK && ((mask >> q) & 1ull))
         self_pair<T, LB, LBP, PE>(M, sc, P, mu_g, N, e, shw, pool, T::pair_a[q], T::pair_b[q], T::pair_k[q], n);
   } else {
+    // runtime pair table (UsefulHound: 253 pairs): 8 pairs' shapes and bounding spheres are read together
+    // and tested, then the near ones run self_pair in pair order (which repeats the same test)
     const int np = M->np;
-    for (int q = 0; q < np; ++q) {
+    const float off = P.contact_offset;
+    for (int q0 = 0; q0 < np; q0 += 8) {
       if (n >= T::NPK) break;
-      self_pair<T, LB, LBP, PE>(M, sc, P, mu_g, N, e, shw, pool, M->pa[q], M->pb[q], M->pk[q], n);
+      int pa[8], pb[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int q = q0 + j < np ? q0 + j : np - 1;
+        pa[j] = M->pa[q];
+        pb[j] = M->pb[q];
+      }
+      unsigned near = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float* sa = shw + (kShW * pa[j] + 12) * LB;
+        const float* sb = shw + (kShW * pb[j] + 12) * LB;
+        const float d[3] = {sa[0] - sb[0], sa[LB] - sb[LB], sa[2 * LB] - sb[2 * LB]};
+        const float rr = sc.brad(pa[j]) + sc.brad(pb[j]) + off;
+        if (q0 + j < np && dot3f(d, d) < rr * rr) near |= 1u << j;
+      }
+      // (one inlined narrowphase: j stays a uniform loop counter, the pair's shapes are re-read by index)
+#pragma unroll 1
+      for (int j = 0; j < 8; ++j)
+        if (((near >> j) & 1u) && n < T::NPK)
+          self_pair<T, LB, LBP, PE>(M, sc, P, mu_g, N, e, shw, pool, M->pa[q0 + j], M->pb[q0 + j], M->pk[q0 + j], n);
     }
   }
   return n;

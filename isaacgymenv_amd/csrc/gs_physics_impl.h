@@ -64,21 +64,59 @@ __device__ __forceinline__ void terrain_queries(const DevParams& P, int N, int e
   }
 }
 
-// pair records of the workgroup's envs (gs_solver.h pool_from_records layout, stride LB) from the shape world
-// data the env lanes wrote into their LDS columns (stride LB)
+// Near-pair records of the workgroup's envs (gs_solver.h NearRec layout, in each env's LDS column, stride LB)
+// from the shape world data the env lanes wrote there.  Two passes over the wave:
+//  1. broadphase, env by env, 64 pairs per round (lane = pair): the pairs within reach are ranked by a ballot
+//     prefix, so each env's list comes out in pair order;
+//  2. narrowphase of the listed pairs, one (env, pair) per lane -- the ~10-20 near pairs of every env of the
+//     workgroup run side by side instead of one after another in the env's lane.
+// The pair's shapes differ per lane in pass 2 (vector loads of their constants and hull vertices).
 template <class T, int LB>
 __device__ __forceinline__ void pair_records(const DevModel* __restrict__ M, const DevParams& P,
-                                             const float* __restrict__ mu_g, int N, int e0, const float* shw,
-                                             float* __restrict__ prec) {
-  constexpr int NI = T::NPAIR * LB;
-  for (int it = threadIdx.x; it < NI; it += kTerrWave) {
-    const int q = it / LB, l = it - q * LB;
+                                             const float* __restrict__ mu_g, int N, int e0, float* lds) {
+  using R = NearRec<T>;
+  const int lane = threadIdx.x;
+  const float off = P.contact_offset;
+  const ShapeConstsM sc{M};
+  int tot = 0;
+#pragma unroll
+  for (int l = 0; l < LB; ++l) {
+    float* col = lds + l;
+    const bool live = e0 + l < N;
+    int cnt = 0;
+    for (int q0 = 0; q0 < T::NPAIR; q0 += kTerrWave) {
+      const int q = q0 + lane;
+      bool near = false;
+      if (live && q < T::NPAIR) {
+        const int a = M->pa[q], b = M->pb[q];
+        const float* sa = col + (kShW * a + 12) * LB;
+        const float* sb = col + (kShW * b + 12) * LB;
+        const float d[3] = {sa[0] - sb[0], sa[LB] - sb[LB], sa[2 * LB] - sb[2 * LB]};
+        const float rr = sc.brad(a) + sc.brad(b) + off;
+        near = dot3f(d, d) < rr * rr;
+      }
+      const unsigned long long bal = __ballot(near);
+      if (near) col[(R::REC + R::RW * (cnt + __popcll(bal & ((1ull << lane) - 1ull)))) * LB] = (float)q;
+      cnt += __popcll(bal);
+    }
+    if (lane == 0) col[R::CNT * LB] = (float)cnt;
+    tot += cnt;
+  }
+  __syncthreads();  // the lists are read across lanes
+  for (int i = lane; i < tot; i += kTerrWave) {
+    int l = 0, r = i;
+#pragma unroll
+    for (int k = 0; k + 1 < LB; ++k) {
+      const int c = (int)lds[R::CNT * LB + l];
+      if (r >= c) { r -= c; ++l; }
+    }
+    float* col = lds + l;
+    float* rec = col + (R::REC + R::RW * r) * LB;
+    const int q = (int)rec[0];
     int n = 0;
-    if (e0 + l < N)
-      self_pair<T, LB, LB, kRec, ShapeConstsM, true>(M, ShapeConstsM{M}, P, mu_g, N, e0 + l, shw + l,
-                                                     prec + (T::NPAIR + 2 * q * kRec) * LB + l, M->pa[q], M->pb[q],
-                                                     M->pk[q], n);
-    prec[q * LB + l] = (float)n;
+    self_pair<T, LB, LB, kRec, ShapeConstsM, true>(M, sc, P, mu_g, N, e0 + l, col, rec + LB, M->pa[q], M->pb[q],
+                                                   M->pk[q], n);
+    rec[0] = (float)(q + kRecQ * n);
   }
 }
 
@@ -87,14 +125,15 @@ struct WaveCfg {
   static constexpr int LB = LaneCfg<T, TERR>::LB;
   static constexpr bool PAIRS = SELF && T::NPK > 0;
   static constexpr int QIN = TERR ? 4 * T::NC * LB : 1, QOUT = TERR ? 5 * T::NC * LB : 1;
-  static constexpr int PREC = PAIRS ? T::NPAIR * (1 + 2 * kRec) * LB : 1;
+  // the near-pair records live in the env columns' contact-row area (written after the records are read)
+  static_assert(!PAIRS || NearRec<T>::END <= LaneCfg<T, TERR>::X_POOL, "near-pair records exceed the env column");
 };
 
 // the work of the whole workgroup before an env substep: env lanes publish, every lane queries / tests
 template <class T, bool TERR, bool SELF>
 __device__ __forceinline__ void wave_prepass(const DevModel* __restrict__ M, const DevParams& P, const SimBuffers& B,
                                              int e0, bool env_lane, const EnvState<T>& s, float* lds, float* qin,
-                                             float* qout, float* prec) {
+                                             float* qout) {
   using W = WaveCfg<T, TERR, SELF>;
   constexpr int LB = W::LB;
   if (env_lane) {
@@ -104,7 +143,7 @@ __device__ __forceinline__ void wave_prepass(const DevModel* __restrict__ M, con
   __syncthreads();
   if constexpr (TERR) terrain_queries<T, LB>(P, B.N, e0, qin, qout);
 #ifndef GS_NO_PAIR_REC
-  if constexpr (W::PAIRS) if (P.self_collide) pair_records<T, LB>(M, P, B.mu, B.N, e0, lds, prec);
+  if constexpr (W::PAIRS) if (P.self_collide) pair_records<T, LB>(M, P, B.mu, B.N, e0, lds);
 #endif
   __syncthreads();
 }
@@ -115,7 +154,7 @@ __global__ __launch_bounds__(kTerrWave, 1) void k_simulate_wave(const DevModel* 
   using W = WaveCfg<T, TERR, SELF>;
   constexpr int LB = W::LB;
   __shared__ float lds[LaneCfg<T, TERR>::SLOTS * LB];
-  __shared__ float qin[W::QIN], qout[W::QOUT], prec[W::PREC];
+  __shared__ float qin[W::QIN], qout[W::QOUT];
   const int N = B.N, e0 = blockIdx.x * LB, e = e0 + threadIdx.x;
   const bool env_lane = threadIdx.x < LB && e < N;
   EnvState<T> s;
@@ -126,12 +165,12 @@ __global__ __launch_bounds__(kTerrWave, 1) void k_simulate_wave(const DevModel* 
     for (int j = 0; j < T::ND; ++j) tau[j] = tau_aos ? tau_aos[(size_t)e * T::ND + j] : 0.f;
   }
   for (int sstep = 0; sstep < P.substeps; ++sstep) {  // uniform trip count: every lane meets every barrier
-    wave_prepass<T, TERR, SELF>(M, P, B, e0, env_lane, s, lds, qin, qout, prec);
+    wave_prepass<T, TERR, SELF>(M, P, B, e0, env_lane, s, lds, qin, qout);
     if (env_lane) {
       const bool last = (sstep == P.substeps - 1) && P.collect;
       substep<T, TERR, LB, TERR ? LB : 0, SELF, W::PAIRS ? LB : 0>(
           M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last, sstep == P.substeps - 1 ? B.sens : nullptr,
-          qout + threadIdx.x, prec + threadIdx.x);
+          qout + threadIdx.x, lds + threadIdx.x);
     }
   }
   if (env_lane) store_state<T>(B.state, N, e, s);
@@ -143,7 +182,7 @@ __global__ __launch_bounds__(kTerrWave, 1) void k_pd_step_wave(const DevModel* _
   using W = WaveCfg<T, TERR, SELF>;
   constexpr int LB = W::LB;
   __shared__ float lds[LaneCfg<T, TERR>::SLOTS * LB];
-  __shared__ float qin[W::QIN], qout[W::QOUT], prec[W::PREC];
+  __shared__ float qin[W::QIN], qout[W::QOUT];
   const int N = B.N, e0 = blockIdx.x * LB, e = e0 + threadIdx.x;
   const bool env_lane = threadIdx.x < LB && e < N;
   EnvState<T> s;
@@ -154,12 +193,12 @@ __global__ __launch_bounds__(kTerrWave, 1) void k_pd_step_wave(const DevModel* _
   const int total = (A.decimation + A.extra) * sub;
   for (int it = 0; it < total; ++it) {  // uniform trip count: every lane meets every barrier
     if (env_lane && it < n_pd && (it % sub) == 0) pd_torques<T>(A, e, s, it == 0, tau);
-    wave_prepass<T, TERR, SELF>(M, P, B, e0, env_lane, s, lds, qin, qout, prec);
+    wave_prepass<T, TERR, SELF>(M, P, B, e0, env_lane, s, lds, qin, qout);
     if (env_lane) {
       const bool last = ((it % sub) == sub - 1) && P.collect;
       substep<T, TERR, LB, TERR ? LB : 0, SELF, W::PAIRS ? LB : 0>(
           M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last, it == total - 1 ? B.sens : nullptr,
-          qout + threadIdx.x, prec + threadIdx.x);
+          qout + threadIdx.x, lds + threadIdx.x);
       if (it == n_pd - 1) pd_dof_out<T>(A, e, s);
     }
   }
@@ -175,7 +214,7 @@ __global__ __launch_bounds__(kTerrWave, 1) void k_pd_step_wave(const DevModel* _
 // cost it a workgroup per CU of LDS while its substep is bound by the solver lane's scratch latency, not by the
 // narrowphase; profiles/r03f_hound_ab.txt)
 #ifndef GS_WAVE_PLANE_SELF
-#define GS_WAVE_PLANE_SELF 0
+#define GS_WAVE_PLANE_SELF 1
 #endif
 template <class T>
 constexpr bool kWavePlaneSelf = GS_WAVE_PLANE_SELF && T::NPK > 0 && LaneCfg<T, false>::LB <= 4 && !LaneCfg<T, false>::GLOBAL;

@@ -222,22 +222,36 @@ GS_HD void shape_world(const DevModel* __restrict__ Min, const EnvState<T>& s, f
   }
 }
 
-// Pair records (stride PR): per pair q its contact count at [q], contact c's x, n, separation at
-// [NPAIR + (2 q + c) kRec + f].  Gathered in pair order into the pool, at most T::NPK -- the entries
-// self_contacts writes for the same shapes.
+// Near-pair records of the wave-assisted kernels (gs_physics_impl.h pair_records), in each env's LDS column
+// (stride PR) behind the shape world data, written before the contact rows reuse that area: [CNT] the env's
+// count of pairs within reach of the broadphase; record r (its r-th such pair, in pair order) at REC + RW r:
+// q + kRecQ * (contact count), then contact c's x, n, separation at 1 + kRec c.
+constexpr int kRecQ = 1024;
+template <class T>
+struct NearRec {
+  static constexpr int CNT = kShW * T::NS, REC = CNT + 1, RW = 1 + 2 * kRec, END = REC + T::NPAIR * RW;
+  static_assert(T::NPAIR < kRecQ, "pair index must fit below kRecQ");
+};
+
+// the env's near-pair records gathered in pair order into the pool, at most T::NPK -- the entries
+// self_contacts writes for the same shapes
 template <class T, int LB, int PR>
 GS_HD int pool_from_records(const DevModel* __restrict__ M, const float* __restrict__ mu_g, int N, int e,
-                            const float* __restrict__ prec, float* pool) {
+                            const float* __restrict__ col, float* pool) {
+  using R = NearRec<T>;
   constexpr int PE = PoolCfg<T>::PE;
+  const int cnt = (int)col[R::CNT * PR];
   int n = 0;
-  for (int q = 0; q < T::NPAIR && n < T::NPK; ++q) {
-    const int cnt = (int)prec[q * PR];
-    for (int c = 0; c < cnt && n < T::NPK; ++c) {
-      const float* r = prec + (T::NPAIR + (2 * q + c) * kRec) * PR;
+  for (int r = 0; r < cnt && n < T::NPK; ++r) {
+    const float* rec = col + (R::REC + R::RW * r) * PR;
+    const int code = (int)rec[0];
+    const int q = code % kRecQ, nc = code / kRecQ;
+    for (int c = 0; c < nc && n < T::NPK; ++c) {
+      const float* x = rec + (1 + c * kRec) * PR;
       float* o = pool + PE * n * LB;
 #pragma unroll
-      for (int k = 0; k < 6; ++k) o[k * LB] = r[k * PR];
-      o[kPoolSep * LB] = r[kRecSep * PR];
+      for (int k = 0; k < 6; ++k) o[k * LB] = x[k * PR];
+      o[kPoolSep * LB] = x[kRecSep * PR];
       pool_entry_finish<LB>(M, mu_g, N, e, M->pa[q], M->pb[q], o);
       ++n;
     }
