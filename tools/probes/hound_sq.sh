@@ -8,7 +8,7 @@ ROOT=$PWD
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
-for sc in 1 0; do
+for sc in ${SCS:-1 0}; do
   GS_SELF_COLLIDE=$sc timeout -k 10 200 python3 $ROOT/tools/probes/hound_sq.py > $OUT/time_sc$sc.log 2>&1 || exit 1
   g=0
   for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM" \
