@@ -21,3 +21,20 @@ template hipError_t launch_pd_plane<GS_INST_TOPO>(const DevModel*, const DevPara
 template hipError_t launch_pd_terr<GS_INST_TOPO>(const DevModel*, const DevParams&, const SimBuffers&, const PdDev&,
                                                  hipStream_t);
 #endif
+
+#ifdef GS_PHASE_PROFILE
+// the wave-assisted kernels' phase cycles of this translation unit (gs_physics_impl.h gs_wave_cycles)
+#define GS_WCAT2(a, b, c) a##b##_##c
+#define GS_WCAT(a, b, c) GS_WCAT2(a, b, c)
+extern "C" __attribute__((visibility("default"))) int GS_WCAT(gs_debug_wave_cycles_, GS_INST_TOPO, GS_INST_FORM)(
+    unsigned long long* out, int n, int reset) {
+  if (n > 16) n = 16;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(gs_phys::gs_wave_cycles), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(gs_phys::gs_wave_cycles), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif

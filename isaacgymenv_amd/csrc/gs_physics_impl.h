@@ -17,7 +17,7 @@ __global__ __launch_bounds__((LaneCfg<T, TERR>::LB), 1) void k_simulate(const De
   const int e = blockIdx.x * LB + threadIdx.x;
   if (e >= B.N) return;
   float* rows = C::GLOBAL ? B.rows + (size_t)blockIdx.x * C::SLOTS * LB + threadIdx.x : lds + threadIdx.x;
-  simulate_env<T, TERR, LB, SELF>(M, P, B, tau_aos, e, rows);
+  simulate_env<T, TERR, LB, SELF, SELF && C::SPLIT>(M, P, B, tau_aos, e, rows);
 }
 
 template <class T, bool TERR, bool SELF>
@@ -45,6 +45,29 @@ __global__ __launch_bounds__((LaneCfg<T, TERR>::LB), 1) void k_pd_step(const Dev
 // code, so its register allocation is the plane solver's.
 constexpr int kTerrWave = 64;
 
+// Phase profiler of the wave-assisted kernels (profiling build only, -DGS_PHASE_PROFILE -> libgymsim_prof.so):
+// per-wave s_memtime cycles of 0 publish (shape world / candidate centres), 1 terrain queries, 2 pair broadphase,
+// 3 pair narrowphase, 4 env-lane substep; summed over waves into this translation unit's gs_wave_cycles, read by
+// gs_debug_wave_cycles_<topology>_<form> (gs_phys_inst.hip, tools/probes/wave_phases.py); [8] counts waves.
+#ifdef GS_PHASE_PROFILE
+static __device__ unsigned long long gs_wave_cycles[16];
+#define GS_WPROF_DECL long long wt_ = clock64(); long long wacc_[5] = {0, 0, 0, 0, 0};
+#define GS_WPROF(i) { const long long t_ = clock64(); wacc_[i] += t_ - wt_; wt_ = t_; }
+#define GS_WPROF_PARAM , long long &wt_, long long *wacc_
+#define GS_WPROF_ARGS , wt_, wacc_
+#define GS_WPROF_FLUSH                                                                      \
+  if (threadIdx.x == 0) {                                                                   \
+    for (int i_ = 0; i_ < 5; ++i_) atomicAdd(&gs_wave_cycles[i_], (unsigned long long)wacc_[i_]); \
+    atomicAdd(&gs_wave_cycles[8], 1ull);                                                    \
+  }
+#else
+#define GS_WPROF_DECL
+#define GS_WPROF(i)
+#define GS_WPROF_PARAM
+#define GS_WPROF_ARGS
+#define GS_WPROF_FLUSH
+#endif
+
 template <class T, int LB>
 __device__ __forceinline__ void terrain_queries(const DevParams& P, int N, int e0, const float* __restrict__ qin,
                                                 float* __restrict__ qout) {
@@ -71,9 +94,11 @@ __device__ __forceinline__ void terrain_queries(const DevParams& P, int N, int e
 //  2. narrowphase of the listed pairs, one (env, pair) per lane -- the ~10-20 near pairs of every env of the
 //     workgroup run side by side instead of one after another in the env's lane.
 // The pair's shapes differ per lane in pass 2 (vector loads of their constants and hull vertices).
-template <class T, int LB>
+// (shape world at stride LB from shw; env l's records at stride RS from rb0 + l * rstep)
+template <class T, int LB, int RS>
 __device__ __forceinline__ void pair_records(const DevModel* __restrict__ M, const DevParams& P,
-                                             const float* __restrict__ mu_g, int N, int e0, float* lds) {
+                                             const float* __restrict__ mu_g, int N, int e0, const float* shw,
+                                             float* rb0, size_t rstep GS_WPROF_PARAM) {
   using R = NearRec<T>;
   const int lane = threadIdx.x;
   const float off = P.contact_offset;
@@ -81,7 +106,8 @@ __device__ __forceinline__ void pair_records(const DevModel* __restrict__ M, con
   int tot = 0;
 #pragma unroll
   for (int l = 0; l < LB; ++l) {
-    float* col = lds + l;
+    const float* col = shw + l;
+    float* rb = rb0 + l * rstep;
     const bool live = e0 + l < N;
     int cnt = 0;
     for (int q0 = 0; q0 < T::NPAIR; q0 += kTerrWave) {
@@ -96,28 +122,49 @@ __device__ __forceinline__ void pair_records(const DevModel* __restrict__ M, con
         near = dot3f(d, d) < rr * rr;
       }
       const unsigned long long bal = __ballot(near);
-      if (near) col[(R::REC + R::RW * (cnt + __popcll(bal & ((1ull << lane) - 1ull)))) * LB] = (float)q;
+      if (near) rb[(1 + R::RW * (cnt + __popcll(bal & ((1ull << lane) - 1ull)))) * RS] = (float)q;
       cnt += __popcll(bal);
     }
-    if (lane == 0) col[R::CNT * LB] = (float)cnt;
+    if (lane == 0 && live) rb[0] = (float)cnt;
     tot += cnt;
   }
   __syncthreads();  // the lists are read across lanes
+  GS_WPROF(2)
   for (int i = lane; i < tot; i += kTerrWave) {
     int l = 0, r = i;
 #pragma unroll
     for (int k = 0; k + 1 < LB; ++k) {
-      const int c = (int)lds[R::CNT * LB + l];
+      const int c = (int)rb0[l * rstep];
       if (r >= c) { r -= c; ++l; }
     }
-    float* col = lds + l;
-    float* rec = col + (R::REC + R::RW * r) * LB;
+    float* rec = rb0 + l * rstep + (1 + R::RW * r) * RS;
     const int q = (int)rec[0];
     int n = 0;
-    self_pair<T, LB, LB, kRec, ShapeConstsM, true>(M, sc, P, mu_g, N, e0 + l, col, rec + LB, M->pa[q], M->pb[q],
+    self_pair<T, LB, RS, kRec, ShapeConstsM, true>(M, sc, P, mu_g, N, e0 + l, shw + l, rec + RS, M->pa[q], M->pb[q],
                                                    M->pk[q], n);
     rec[0] = (float)(q + kRecQ * n);
   }
+}
+
+// The split form's narrowphase kernel (LaneCfg::SPLIT): kPairEnvs envs per 64-lane workgroup publish their
+// shape world data to LDS, the wave runs pair_records, the records go to SimBuffers::rows for the solver kernel
+// (k_simulate, substep PR = 1) that follows on the stream.  Its own launch: a small register footprint and
+// several waves per SIMD to hide the narrowphase's load latency, which the solver kernel (512 VGPR, scratch,
+// 3 waves per CU) cannot.
+constexpr int kPairEnvs = 4;
+template <class T>
+__global__ __launch_bounds__(kTerrWave) void k_pair_records(const DevModel* __restrict__ M, DevParams P, SimBuffers B) {
+  __shared__ float shw[kShW * T::NS * kPairEnvs];
+  const int N = B.N, e0 = blockIdx.x * kPairEnvs, l = threadIdx.x;
+  if (l < kPairEnvs && e0 + l < N) {
+    EnvState<T> s;
+    load_state<T>(B.state, N, e0 + l, s);
+    shape_world<T, kPairEnvs>(M, s, shw + l);
+  }
+  __syncthreads();
+  GS_WPROF_DECL
+  constexpr int FL = LaneCfg<T, false>::ROW_FLOATS;
+  pair_records<T, kPairEnvs, 1>(M, P, B.mu, N, e0, shw, B.rows + (size_t)e0 * FL, FL GS_WPROF_ARGS);
 }
 
 template <class T, bool TERR, bool SELF>
@@ -133,7 +180,7 @@ struct WaveCfg {
 template <class T, bool TERR, bool SELF>
 __device__ __forceinline__ void wave_prepass(const DevModel* __restrict__ M, const DevParams& P, const SimBuffers& B,
                                              int e0, bool env_lane, const EnvState<T>& s, float* lds, float* qin,
-                                             float* qout) {
+                                             float* qout GS_WPROF_PARAM) {
   using W = WaveCfg<T, TERR, SELF>;
   constexpr int LB = W::LB;
   if (env_lane) {
@@ -141,11 +188,16 @@ __device__ __forceinline__ void wave_prepass(const DevModel* __restrict__ M, con
     if constexpr (W::PAIRS) if (P.self_collide) shape_world<T, LB>(M, s, lds + threadIdx.x);
   }
   __syncthreads();
+  GS_WPROF(0)
   if constexpr (TERR) terrain_queries<T, LB>(P, B.N, e0, qin, qout);
+  GS_WPROF(1)
 #ifndef GS_NO_PAIR_REC
-  if constexpr (W::PAIRS) if (P.self_collide) pair_records<T, LB>(M, P, B.mu, B.N, e0, lds);
+  if constexpr (W::PAIRS)
+    if (P.self_collide)
+      pair_records<T, LB, LB>(M, P, B.mu, B.N, e0, lds, lds + NearRec<T>::SHW * LB, 1 GS_WPROF_ARGS);
 #endif
   __syncthreads();
+  GS_WPROF(3)
 }
 
 template <class T, bool TERR, bool SELF>
@@ -164,15 +216,18 @@ __global__ __launch_bounds__(kTerrWave, 1) void k_simulate_wave(const DevModel* 
 #pragma unroll
     for (int j = 0; j < T::ND; ++j) tau[j] = tau_aos ? tau_aos[(size_t)e * T::ND + j] : 0.f;
   }
+  GS_WPROF_DECL
   for (int sstep = 0; sstep < P.substeps; ++sstep) {  // uniform trip count: every lane meets every barrier
-    wave_prepass<T, TERR, SELF>(M, P, B, e0, env_lane, s, lds, qin, qout);
+    wave_prepass<T, TERR, SELF>(M, P, B, e0, env_lane, s, lds, qin, qout GS_WPROF_ARGS);
     if (env_lane) {
       const bool last = (sstep == P.substeps - 1) && P.collect;
       substep<T, TERR, LB, TERR ? LB : 0, SELF, W::PAIRS ? LB : 0>(
           M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last, sstep == P.substeps - 1 ? B.sens : nullptr,
-          qout + threadIdx.x, lds + threadIdx.x);
+          qout + threadIdx.x, lds + threadIdx.x + NearRec<T>::SHW * LB);
     }
+    GS_WPROF(4)
   }
+  GS_WPROF_FLUSH
   if (env_lane) store_state<T>(B.state, N, e, s);
 }
 
@@ -191,17 +246,20 @@ __global__ __launch_bounds__(kTerrWave, 1) void k_pd_step_wave(const DevModel* _
   const int sub = P.substeps;
   const int n_pd = A.decimation * sub;
   const int total = (A.decimation + A.extra) * sub;
+  GS_WPROF_DECL
   for (int it = 0; it < total; ++it) {  // uniform trip count: every lane meets every barrier
     if (env_lane && it < n_pd && (it % sub) == 0) pd_torques<T>(A, e, s, it == 0, tau);
-    wave_prepass<T, TERR, SELF>(M, P, B, e0, env_lane, s, lds, qin, qout);
+    wave_prepass<T, TERR, SELF>(M, P, B, e0, env_lane, s, lds, qin, qout GS_WPROF_ARGS);
     if (env_lane) {
       const bool last = ((it % sub) == sub - 1) && P.collect;
       substep<T, TERR, LB, TERR ? LB : 0, SELF, W::PAIRS ? LB : 0>(
           M, P, s, tau, B.mu, N, e, lds + threadIdx.x, B.cf, last, it == total - 1 ? B.sens : nullptr,
-          qout + threadIdx.x, lds + threadIdx.x);
+          qout + threadIdx.x, lds + threadIdx.x + NearRec<T>::SHW * LB);
       if (it == n_pd - 1) pd_dof_out<T>(A, e, s);
     }
+    GS_WPROF(4)
   }
+  GS_WPROF_FLUSH
   if (env_lane) pd_outputs<T>(M, P, B, A, e, s, tau);
 }
 
@@ -224,10 +282,22 @@ hipError_t launch_sim_plane(const DevModel* M, const DevParams& P, const SimBuff
   constexpr int LB = LaneCfg<T, false>::LB;
   const dim3 grid((B.N + LB - 1) / LB);
   if (P.self_collide) {
-    if constexpr (kWavePlaneSelf<T>)
+    if constexpr (LaneCfg<T, false>::SPLIT) {
+      // narrowphase kernel, then the solver reading its records: one pair of launches per substep
+      if (!B.rows) return hipErrorInvalidValue;
+      const dim3 pgrid((B.N + gs_phys::kPairEnvs - 1) / gs_phys::kPairEnvs);
+      DevParams P1 = P;
+      P1.substeps = 1;
+      for (int ss = 0; ss < P.substeps; ++ss) {
+        P1.collect = P.collect && ss == P.substeps - 1;
+        hipLaunchKernelGGL((gs_phys::k_pair_records<T>), pgrid, dim3(gs_phys::kTerrWave), 0, st, M, P1, B);
+        hipLaunchKernelGGL((gs_phys::k_simulate<T, false, true>), grid, dim3(LB), 0, st, M, P1, B, tau);
+      }
+    } else if constexpr (kWavePlaneSelf<T>) {
       hipLaunchKernelGGL((gs_phys::k_simulate_wave<T, false, true>), grid, dim3(gs_phys::kTerrWave), 0, st, M, P, B, tau);
-    else
+    } else {
       hipLaunchKernelGGL((gs_phys::k_simulate<T, false, true>), grid, dim3(LB), 0, st, M, P, B, tau);
+    }
   } else {
     hipLaunchKernelGGL((gs_phys::k_simulate<T, false, false>), grid, dim3(LB), 0, st, M, P, B, tau);
   }

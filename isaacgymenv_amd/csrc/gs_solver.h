@@ -78,7 +78,10 @@ struct LaneCfg {
                                                                      : (FIT < GS_LANE_CAP ? FIT : GS_LANE_CAP);
   static_assert(GLOBAL || SLOTS * LB * 4 <= 160 * 1024, "contact rows exceed the LDS of a CU even at 8 lanes");
   // floats of SimBuffers::rows per env (0: the rows live in LDS)
-  static constexpr int ROW_FLOATS = GLOBAL ? SLOTS : 0;
+  // SPLIT (plane, self-collision, LDS-starved: UsefulHound): the pair narrowphase runs as its own kernel before the
+  // solver (gs_physics_impl.h k_pair_records) and hands over near-pair records in SimBuffers::rows, per env
+  static constexpr bool SPLIT = T::NPK > 0 && !TERR && !GLOBAL && LB <= 4;
+  static constexpr int ROW_FLOATS = GLOBAL ? SLOTS : SPLIT ? 1 + T::NPAIR * (1 + 2 * kRec) : 0;
 };
 
 // World-frame force of candidate c's impulses (normal from LDS, tangents rebuilt), / h.
@@ -222,14 +225,15 @@ GS_HD void shape_world(const DevModel* __restrict__ Min, const EnvState<T>& s, f
   }
 }
 
-// Near-pair records of the wave-assisted kernels (gs_physics_impl.h pair_records), in each env's LDS column
-// (stride PR) behind the shape world data, written before the contact rows reuse that area: [CNT] the env's
-// count of pairs within reach of the broadphase; record r (its r-th such pair, in pair order) at REC + RW r:
-// q + kRecQ * (contact count), then contact c's x, n, separation at 1 + kRec c.
+// Near-pair records of the wave-assisted kernels (gs_physics_impl.h pair_records), at stride PR from a base:
+// in each env's LDS column behind its shape world data (base SHW, written before the contact rows reuse that area),
+// or per env in SimBuffers::rows (LaneCfg::SPLIT, FLOATS per env).  [0] the env's count of pairs within reach of
+// the broadphase; record r (its r-th such pair, in pair order) at 1 + RW r: q + kRecQ * (contact count), then
+// contact c's x, n, separation at 1 + kRec c.
 constexpr int kRecQ = 1024;
 template <class T>
 struct NearRec {
-  static constexpr int CNT = kShW * T::NS, REC = CNT + 1, RW = 1 + 2 * kRec, END = REC + T::NPAIR * RW;
+  static constexpr int SHW = kShW * T::NS, RW = 1 + 2 * kRec, FLOATS = 1 + T::NPAIR * RW, END = SHW + FLOATS;
   static_assert(T::NPAIR < kRecQ, "pair index must fit below kRecQ");
 };
 
@@ -240,10 +244,10 @@ GS_HD int pool_from_records(const DevModel* __restrict__ M, const float* __restr
                             const float* __restrict__ col, float* pool) {
   using R = NearRec<T>;
   constexpr int PE = PoolCfg<T>::PE;
-  const int cnt = (int)col[R::CNT * PR];
+  const int cnt = (int)col[0];
   int n = 0;
   for (int r = 0; r < cnt && n < T::NPK; ++r) {
-    const float* rec = col + (R::REC + R::RW * r) * PR;
+    const float* rec = col + (1 + R::RW * r) * PR;
     const int code = (int)rec[0];
     const int q = code % kRecQ, nc = code / kRecQ;
     for (int c = 0; c < nc && n < T::NPK; ++c) {
@@ -1161,7 +1165,8 @@ GS_HD void candidate_centres(const DevModel* __restrict__ Min, const EnvState<T>
 
 // ---------------------------------------------------------------- per-env entry points
 // gym.simulate for env e: `substeps` substeps with constant dof forces [N][nd] (or zero)
-template <class T, bool TERR, int LB, bool SELF = true>
+// REC: the self-collision narrowphase already ran (k_pair_records), its near-pair records are in B.rows
+template <class T, bool TERR, int LB, bool SELF = true, bool REC = false>
 GS_HD void simulate_env(const DevModel* __restrict__ M, const DevParams& P, const SimBuffers& B,
                         const float* __restrict__ tau_aos, int e, float* lds) {
   const int N = B.N;
@@ -1172,7 +1177,12 @@ GS_HD void simulate_env(const DevModel* __restrict__ M, const DevParams& P, cons
   for (int j = 0; j < T::ND; ++j) tau[j] = tau_aos ? tau_aos[(size_t)e * T::ND + j] : 0.f;
   for (int sstep = 0; sstep < P.substeps; ++sstep) {
     const bool last = (sstep == P.substeps - 1) && P.collect;
-    substep<T, TERR, LB, 0, SELF>(M, P, s, tau, B.mu, N, e, lds, B.cf, last, sstep == P.substeps - 1 ? B.sens : nullptr);
+    if constexpr (SELF && REC)  // this substep's near-pair records
+      substep<T, TERR, LB, 0, SELF, 1>(M, P, s, tau, B.mu, N, e, lds, B.cf, last,
+                                       sstep == P.substeps - 1 ? B.sens : nullptr, nullptr,
+                                       B.rows + (size_t)e * LaneCfg<T, TERR>::ROW_FLOATS);
+    else
+      substep<T, TERR, LB, 0, SELF>(M, P, s, tau, B.mu, N, e, lds, B.cf, last, sstep == P.substeps - 1 ? B.sens : nullptr);
   }
   store_state<T>(B.state, N, e, s);
 }
