@@ -58,9 +58,9 @@ struct DevModel {
   int hv0[GS_MAXSH], hv1[GS_MAXSH];  // hull vertex range
   int np;                       // self-collision pairs
   int pa[GS_MAXP], pb[GS_MAXP], pk[GS_MAXP];  // shape a < shape b, kind 0 SS 1 SC 2 CC 3 GJK
-  float hv[GS_MAXHV][4];        // hull vertices, body frame xyz + core factor (core = c + f (v - c))
+  alignas(16) float hv[GS_MAXHV][4];  // (16-B rows: one dwordx4 load each) hull vertices, body frame xyz + core factor (core = c + f (v - c))
   int pv0[GS_MAXSH], pv1[GS_MAXSH];  // a hull's self-collision core vertices (subset of hv)
-  float pv[GS_MAXPV][4];
+  alignas(16) float pv[GS_MAXPV][4];
 };
 
 struct DevParams {

@@ -22,13 +22,13 @@ GS_HD float dot3f(const float* a, const float* b) { return a[0] * b[0] + a[1] * 
 // batch re-reads row k1 - 1 and skips it).  Same visits, same order as the plain loop.
 template <class F>
 GS_HD __attribute__((always_inline)) inline void for_rows8(const float (*tab)[4], int k0, int k1, F&& f) {
+  // (tab: a DevModel table declared alignas(16))
   for (int kb = k0; kb < k1; kb += 8) {
     float r[8][4];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float* v = tab[kb + j < k1 ? kb + j : k1 - 1];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) r[j][t] = v[t];
+      const float4 v = *reinterpret_cast<const float4*>(tab[kb + j < k1 ? kb + j : k1 - 1]);  // rows are 16-B aligned
+      r[j][0] = v.x; r[j][1] = v.y; r[j][2] = v.z; r[j][3] = v.w;
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j)
