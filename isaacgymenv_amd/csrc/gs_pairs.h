@@ -420,7 +420,10 @@ GS_HD float gjk_cores(const DevModel* __restrict__ M, int sa, int sb, const Shap
     for (int t = 0; t < 3; ++t) w[t] = a[t] - b[t];
     const float vv = dot3f(v, v), vw = dot3f(v, w);
     if (vw > 0.f && vw * vw > stop * stop * vv) return vw / sqrtf(vv);  // separated by more than stop
-    if (k > 0 && vv - vw <= 1e-10f * vv + 1e-14f) break;
+    // converged: the support plane is within 1e-6 |v| of the simplex's closest point (the distance to ~1e-6
+    // relative; the oracle's fp64 bound is 1e-10, which float arithmetic cannot resolve: below ~1e-7 vv the test
+    // reads rounding, so a converged float search ran on until a repeated support point or the iteration cap)
+    if (k > 0 && vv - vw <= 1e-6f * vv + 1e-14f) break;
     bool dup = false;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
