@@ -146,13 +146,14 @@ __device__ __forceinline__ void pair_records(const DevModel* __restrict__ M, con
   }
 }
 
-// The split form's narrowphase kernel (LaneCfg::SPLIT): kPairEnvs envs per 64-lane workgroup publish their
+// The split form's narrowphase kernel (LaneCfg::SPLIT): kPairEnvs envs per 64-lane workgroup (2: 0.60 ms per
+// UsefulHound launch vs 0.74 ms with 4, more waves in flight for the same pair tests) publish their
 // shape world data to LDS, the wave runs pair_records, the records go to SimBuffers::rows for the solver kernel
 // (k_simulate, substep PR = 1) that follows on the stream.  Its own launch: a small register footprint and
 // several waves per SIMD to hide the narrowphase's load latency, which the solver kernel (512 VGPR, scratch,
 // 3 waves per CU) cannot.  Two waves per SIMD (<= 256 VGPR): unbounded, the 4 publishing lanes' link poses (the
 // forward kinematics of shape_world) took the kernel to 383 VGPR + AGPR, one wave per SIMD.
-constexpr int kPairEnvs = 4;
+constexpr int kPairEnvs = 2;
 template <class T>
 __global__ __launch_bounds__(kTerrWave, 2) void k_pair_records(const DevModel* __restrict__ M, DevParams P, SimBuffers B) {
   __shared__ float shw[kShW * T::NS * kPairEnvs];
