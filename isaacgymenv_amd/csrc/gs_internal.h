@@ -15,8 +15,10 @@
 #define GS_MAXPV 512  // hull self-collision core vertices per articulation (UsefulHound: 7 x <= 48)
 #define GS_MAXPOOL 8  // self-contact slots per env
 #define GS_WAVE 64
-// a contact row whose J M^-1 J^T falls below this -- an effective mass above 1000 kg, an overlap no dof can
-// separate (UsefulHound's arm pinned on its trunk) -- takes no impulse; the oracle uses the same bound
+// a SELF-contact row whose J M^-1 J^T falls below this -- an effective mass above 1000 kg, an overlap no dof can
+// separate (UsefulHound's arm pinned on its trunk) -- takes no impulse; the oracle uses the same bound.  Ground
+// and terrain rows always respond (a body heavier than 1000 kg still rests on the plane:
+// tests/test_oracle_physics.py::test_heavy_body_rests_on_the_plane)
 #ifndef GS_MIN_RESPONSE
 #define GS_MIN_RESPONSE 1e-3f
 #endif

@@ -15,6 +15,11 @@
 namespace {
 
 GS_HD float dot3f(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+GS_HD void cross3f(const float* a, const float* b, float* o) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
 
 // Visit rows k0 <= k < k1 of a model vertex table (4 floats per row) in index order, f(k, row).  The rows
 // are read 8 at a time before any is used: a hull's index range is wave-uniform, so the 8 rows are
@@ -372,11 +377,29 @@ GS_HD void simplex_subset(const float (&W)[4][3], int k, float& best, int& bm, f
     }
     l[0] = l0;
     if (!ok || !(l0 > 1e-12f)) return;
+    // the closest point itself from cross products, not W0 + mu E: the normal equations' rounding leaves the
+    // point off the segment's perpendicular / the triangle's plane normal by ~cond(G) ulps, which turned
+    // into up to ~1e-2 rad of contact-normal error for near-parallel hull faces (the barycentrics above
+    // only decide validity and the closest points of the two cores)
+    if constexpr (q == 1) {
+      float c1[3], c2[3];
+      cross3f(E[0], W[id[0]], c1);
+      cross3f(c1, E[0], c2);
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      p[a] = W[id[0]][a];
+      for (int a = 0; a < 3; ++a) p[a] = c2[a] / G[0][0];
+    } else if constexpr (q == 2) {
+      float nr[3];
+      cross3f(E[0], E[1], nr);
+      const float s = dot3f(nr, W[id[0]]) / dot3f(nr, nr);
 #pragma unroll
-      for (int j = 0; j < q; ++j) p[a] += mu[j] * E[j][a];
+      for (int a = 0; a < 3; ++a) p[a] = s * nr[a];
+    } else {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        p[a] = W[id[0]][a];
+#pragma unroll
+        for (int j = 0; j < q; ++j) p[a] += mu[j] * E[j][a];
+      }
     }
   }
   const float d2 = dot3f(p, p);
@@ -397,12 +420,14 @@ GS_HD void simplex_all(const float (&W)[4][3], int k, float& best, int& bm, floa
   }
 }
 
-// GJK distance between the cores of shapes a and b: closest points pa, pb; returns the distance, 0 when the
-// cores overlap (same iteration and termination rules as the oracle's gjk_cores)
+// GJK distance between the cores of shapes a and b: closest points pa, pb and the separating vector
+// vout = pa - pb (from the final simplex's closest point: the contact normal's direction, more accurate than
+// the difference of the two closest points); returns the distance, 0 when the cores overlap (same iteration
+// and termination rules as the oracle's gjk_cores)
 // stop: a distance beyond which the caller has no use for the closest points -- once GJK's lower bound (the
 // support plane's offset v.w / |v|) exceeds it, the search ends and returns that bound (pa, pb unset)
 GS_HD float gjk_cores(const DevModel* __restrict__ M, int sa, int sb, const ShapeW& Wa, const ShapeW& Wb, float* pa,
-                      float* pb, float stop = 3.0e38f) {
+                      float* pb, float* vout, float stop = 3.0e38f) {
   float v[3] = {Wa.sc[0] - Wb.sc[0], Wa.sc[1] - Wb.sc[1], Wa.sc[2] - Wb.sc[2]};
   if (dot3f(v, v) < 1e-18f) { v[0] = 1.f; v[1] = 0.f; v[2] = 0.f; }
   float W[4][3], A[4][3], B[4][3], lam[4] = {1.f, 0.f, 0.f, 0.f};
@@ -475,6 +500,7 @@ GS_HD float gjk_cores(const DevModel* __restrict__ M, int sa, int sb, const Shap
     if (i < k)
 #pragma unroll
       for (int t = 0; t < 3; ++t) { pa[t] += lam[i] * A[i][t]; pb[t] += lam[i] * B[i][t]; }
+  vout[0] = v[0]; vout[1] = v[1]; vout[2] = v[2];
   return sqrtf(dot3f(v, v));
 }
 
@@ -564,7 +590,8 @@ GS_HD __attribute__((always_inline)) inline void self_pair(const DevModel* __res
     const float ra = sc.margin(a), rb = sc.margin(b);
     float pa[2][3], pb[2][3];
     int nct = 1;
-    bool gdeep = false;
+    bool gdeep = false, gnorm = false;
+    float gn[3] = {0.f, 0.f, 1.f}, gdist = 0.f;  // GJK pairs: the contact normal and the cores' distance
     if (kind == 0) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) { pa[0][k] = Wa.c[k]; pb[0][k] = Wb.c[k]; }
@@ -624,7 +651,8 @@ GS_HD __attribute__((always_inline)) inline void self_pair(const DevModel* __res
       // (a pair whose cores are farther apart than contact_offset + radii makes no contact: stop there, with a
       // hair of slack so the bound's rounding never drops a contact the full search would keep)
       const float stop = (off + ra + rb) * 1.001f + 1e-5f;
-      const float dist = gjk_cores(M, a, b, Wa, Wb, pa[0], pb[0], stop);
+      float vg[3];
+      const float dist = gjk_cores(M, a, b, Wa, Wb, pa[0], pb[0], vg, stop);
       if (dist > stop) return;
       if (!(dist > 1e-9f)) {
         gdeep = true;
@@ -634,7 +662,10 @@ GS_HD __attribute__((always_inline)) inline void self_pair(const DevModel* __res
         // the contact point: the centroid of the smaller of the two support features facing each other (a
         // face's, not GJK's arbitrary point of it), kept at the cores' distance
         const float inv = 1.f / dist;
-        const float nn[3] = {(pa[0][0] - pb[0][0]) * inv, (pa[0][1] - pb[0][1]) * inv, (pa[0][2] - pb[0][2]) * inv};
+        const float nn[3] = {vg[0] * inv, vg[1] * inv, vg[2] * inv};
+        gnorm = true;
+        gdist = dist;
+        gn[0] = nn[0]; gn[1] = nn[1]; gn[2] = nn[2];
         const float mn[3] = {-nn[0], -nn[1], -nn[2]};
         float ca[3], cb[3];
         const float ea = core_feature(M, a, Wa, mn, ca);
@@ -650,7 +681,11 @@ GS_HD __attribute__((always_inline)) inline void self_pair(const DevModel* __res
       if (n >= T::NPK) break;
       float nn[3] = {pa[c][0] - pb[c][0], pa[c][1] - pb[c][1], pa[c][2] - pb[c][2]};
       float dist = sqrtf(dot3f(nn, nn));
-      if (!(dist > 1e-9f)) {
+      if (gnorm) {  // (pa - pb of the feature construction is dist * n up to the rounding of |pa| ~ 0.5 m)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) nn[k] = gn[k];
+        dist = gdist;
+      } else if (!(dist > 1e-9f)) {
         float f[3] = {Wa.sc[0] - Wb.sc[0], Wa.sc[1] - Wb.sc[1], Wa.sc[2] - Wb.sc[2]};
         float l = sqrtf(dot3f(f, f));
         if (!(l > 1e-9f)) { f[0] = 0.f; f[1] = 0.f; f[2] = 1.f; l = 1.f; }

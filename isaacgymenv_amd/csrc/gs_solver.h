@@ -749,7 +749,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
           }
         }
         slot[(3 * SUP + rr) * LB] = cj;
-        slot[(3 * SUP + 3 + rr) * LB] = d > GS_MIN_RESPONSE ? 1.f / d : 0.f;
+        slot[(3 * SUP + 3 + rr) * LB] = 1.f / d;  // (ground rows: no response cutoff)
       }
     }
   });

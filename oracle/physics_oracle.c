@@ -49,8 +49,9 @@ typedef REAL real;
 #define MAXV 40
 #define MAXC 192
 #define MAXPOOL 16
-#define MIN_RESPONSE 1e-3 /* a contact row whose J M^-1 J^T falls below this (an effective mass above 1000 kg:
-                             an overlap no dof can separate) takes no impulse (GS_MIN_RESPONSE) */
+#define MIN_RESPONSE 1e-3 /* a self-contact row whose J M^-1 J^T falls below this (an effective mass above 1000 kg:
+                             an overlap no dof can separate) takes no impulse (GS_MIN_RESPONSE); ground rows
+                             always respond */
 
 typedef struct {
     int32_t nb, nd, nc, ns, fixed_base;
@@ -490,9 +491,23 @@ static int simplex_closest(real W[4][3], int k, real *v, real *lam) {
             for (int j = 0; j < q; ++j) { l0 -= mu[j]; l[j + 1] = mu[j]; if (!(mu[j] > 1e-12)) ok = 0; }
             l[0] = l0;
             if (!ok || !(l0 > 1e-12)) continue;
-            for (int a = 0; a < 3; ++a) {
-                p[a] = W[id[0]][a];
-                for (int j = 0; j < q; ++j) p[a] += mu[j] * E[j][a];
+            /* the closest point from cross products (same point as W0 + mu E in exact arithmetic; the kernels'
+             * float form needs it, gs_pairs.h simplex_subset) */
+            if (q == 1) {
+                real c1[3], c2[3];
+                cross3(E[0], W[id[0]], c1);
+                cross3(c1, E[0], c2);
+                for (int a = 0; a < 3; ++a) p[a] = c2[a] / G[0][0];
+            } else if (q == 2) {
+                real nr[3];
+                cross3(E[0], E[1], nr);
+                const real s = dot3(nr, W[id[0]]) / dot3(nr, nr);
+                for (int a = 0; a < 3; ++a) p[a] = s * nr[a];
+            } else {
+                for (int a = 0; a < 3; ++a) {
+                    p[a] = W[id[0]][a];
+                    for (int j = 0; j < q; ++j) p[a] += mu[j] * E[j][a];
+                }
             }
         }
         const real d2 = dot3(p, p);
@@ -506,14 +521,14 @@ static int simplex_closest(real W[4][3], int k, real *v, real *lam) {
     return bm;
 }
 
-/* GJK distance between the cores of shapes a and b: closest points pa, pb; returns the distance, 0 when
- * the cores overlap */
+/* GJK distance between the cores of shapes a and b: closest points pa, pb, separating vector vout (the final
+ * simplex's closest point, = pa - pb); returns the distance, 0 when the cores overlap */
 /* narrowphase workload counters (analysis only: oracle_pair_stats): pairs tested, bounding spheres met,
  * GJK calls, GJK iterations, contacts kept (not thread-safe: read them from single-threaded runs) */
 static long long g_pair_stats[5];
 
 static real gjk_cores(const OModel *m, int sa, int sb, const ShapeW *Wa, const ShapeW *Wb, const real *Ra,
-                      const real *Pa, const real *Rb, const real *Pb, real *pa, real *pb) {
+                      const real *Pa, const real *Rb, const real *Pb, real *pa, real *pb, real *vout) {
     ++g_pair_stats[2];
     real v[3] = {Wa->sc[0] - Wb->sc[0], Wa->sc[1] - Wb->sc[1], Wa->sc[2] - Wb->sc[2]};
     if (dot3(v, v) < 1e-18) { v[0] = 1; v[1] = 0; v[2] = 0; }
@@ -551,6 +566,7 @@ static real gjk_cores(const OModel *m, int sa, int sb, const ShapeW *Wa, const S
     for (int t = 0; t < 3; ++t) { pa[t] = 0; pb[t] = 0; }
     for (int i = 0; i < k; ++i)
         for (int t = 0; t < 3; ++t) { pa[t] += lam[i] * A[i][t]; pb[t] += lam[i] * B[i][t]; }
+    for (int t = 0; t < 3; ++t) vout[t] = v[t];
     return sqrt(dot3(v, v));
 }
 
@@ -609,7 +625,8 @@ static int self_contacts(const OModel *m, const OParams *p, real R[][9], real P[
         const int ba = m->shbody[a], bb = m->shbody[b];
         const real ra = (real)m->shmargin[a], rb = (real)m->shmargin[b];
         real pa[2][3], pb[2][3];
-        int nct = 1, gdeep = 0;
+        int nct = 1, gdeep = 0, gnorm = 0;
+        real gn[3] = {0, 0, 1}, gdist = 0; /* GJK pairs: the contact normal and the cores' distance */
         if (kind == 0) {
             for (int k = 0; k < 3; ++k) { pa[0][k] = W[a].c[k]; pb[0][k] = W[b].c[k]; }
         } else if (kind == 1) {
@@ -655,14 +672,17 @@ static int self_contacts(const OModel *m, const OParams *p, real R[][9], real P[
                 for (int k = 0; k < 3; ++k) { pa[0][k] = p1[k] + s * (q1[k] - p1[k]); pb[0][k] = p2[k] + t * (q2[k] - p2[k]); }
             }
         } else {
-            const real dist = gjk_cores(m, a, b, &W[a], &W[b], R[ba], P[ba], R[bb], P[bb], pa[0], pb[0]);
+            real vg[3];
+            const real dist = gjk_cores(m, a, b, &W[a], &W[b], R[ba], P[ba], R[bb], P[bb], pa[0], pb[0], vg);
             if (!(dist > 1e-9)) { /* overlapping cores: centres' direction, depth = both margins */
                 gdeep = 1;
                 for (int k = 0; k < 3; ++k) { pa[0][k] = W[a].sc[k]; pb[0][k] = W[b].sc[k]; }
             } else {
                 /* the contact point: the centroid of the smaller of the two support features facing each
                  * other (a face's, not GJK's arbitrary point of it), kept at the cores' distance */
-                const real nn[3] = {(pa[0][0] - pb[0][0]) / dist, (pa[0][1] - pb[0][1]) / dist, (pa[0][2] - pb[0][2]) / dist};
+                const real nn[3] = {vg[0] / dist, vg[1] / dist, vg[2] / dist};
+                gnorm = 1; gdist = dist;
+                for (int k = 0; k < 3; ++k) gn[k] = nn[k];
                 const real mn[3] = {-nn[0], -nn[1], -nn[2]};
                 real ca[3], cb[3];
                 const real ea = core_feature(m, a, &W[a], R[ba], P[ba], mn, ca);
@@ -677,7 +697,10 @@ static int self_contacts(const OModel *m, const OParams *p, real R[][9], real P[
             real nn[3] = {pa[c][0] - pb[c][0], pa[c][1] - pb[c][1], pa[c][2] - pb[c][2]};
             real dist = sqrt(dot3(nn, nn));
             const int deep = gdeep;
-            if (!(dist > 1e-9)) {
+            if (gnorm) {
+                for (int k = 0; k < 3; ++k) nn[k] = gn[k];
+                dist = gdist;
+            } else if (!(dist > 1e-9)) {
                 real f[3] = {W[a].sc[0] - W[b].sc[0], W[a].sc[1] - W[b].sc[1], W[a].sc[2] - W[b].sc[2]};
                 real l = sqrt(dot3(f, f));
                 if (!(l > 1e-9)) { f[0] = 0; f[1] = 0; f[2] = 1; l = 1; }
@@ -1101,7 +1124,7 @@ static void env_substep(const OModel *m, const OParams *p, real h,
                 if (s >= 0) target = -s / hd;
                 else if (pos_phase) { target = -s / hs; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
                 else target = 0;
-                real ln = Dr[r] > MIN_RESPONSE ? lam[r] + (target - u) / Dr[r] : lam[r];
+                real ln = lam[r] + (target - u) / Dr[r]; /* ground rows: no response cutoff */
                 if (ln < 0) ln = 0;
                 const real dl = ln - lam[r];
                 lam[r] = ln;
@@ -1113,7 +1136,7 @@ static void env_substep(const OModel *m, const OParams *p, real h,
                 real u = 0;
                 for (int k = 0; k < nv; ++k) u += Jr[k] * v[k];
                 const real lim = cmu[a] * lam[3 * a];
-                real lt = Dr[r] > MIN_RESPONSE ? lam[r] - u / Dr[r] : lam[r];
+                real lt = lam[r] - u / Dr[r];
                 if (lt > lim) lt = lim;
                 if (lt < -lim) lt = -lim;
                 const real dl = lt - lam[r];

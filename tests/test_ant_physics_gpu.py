@@ -48,12 +48,13 @@ def test_ant_one_simulate_matches_oracle():
     o_root, o_dof, o_sens = _oracle(flat, root, dof, tau, mu)
     assert np.all(np.isfinite(g_root)) and np.all(np.isfinite(g_dof)) and np.all(np.isfinite(g_sens))
 
-    def rerun(idx, rng):
+    def rerun(idx, rng, bits):
         r, d = H.perturbed(root, dof, idx, rng)
-        o_r, o_d, o_s = _oracle(flat, r, d, tau[idx], mu[idx])
+        o_r, o_d, _, o_s = H.oracle_run(flat, H.ANT_PARAMS, r, d, tau[idx], mu[idx], bits, nsens=4,
+                                        sensor_bodies=H.ANT_FEET)
         return H.state_fields(o_r, o_d, sens=o_s)
-    print(H.assert_close_or_explained(H.state_fields(g_root, g_dof, sens=g_sens), H.state_fields(o_root, o_dof, sens=o_sens),
-                                      rerun, what="ant gpu"))
+    H.assert_close_or_explained(H.state_fields(g_root, g_dof, sens=g_sens), H.state_fields(o_root, o_dof, sens=o_sens),
+                                rerun, what="ant gpu")
 
 
 def test_ant_limits_hold_on_gpu():

@@ -57,15 +57,12 @@ def _run_sim(kind, n, params, root, dof, tau, mu, ptgt, vtgt, drives, steps, hos
     return gym, sim, H.read_state(sim, dof.shape[1])
 
 
-def _run_oracle(flat, params, root, dof, tau, mu, ptgt, vtgt, drives, steps):
+def _run_oracle(flat, params, root, dof, tau, mu, ptgt, vtgt, drives, steps, bits=64):
     _, kp, kd = drives
     kp = np.where(drives[0] == DOF_MODE_POS, kp, 0.0)
     kd = np.where((drives[0] == DOF_MODE_POS) | (drives[0] == DOF_MODE_VEL), kd, 0.0)
-    o = OracleSim(flat, params, drives=(kp, kd))
-    r, d = root.copy(), dof.copy()
-    for _ in range(steps):
-        o.simulate(r, d, np.ascontiguousarray(tau), np.ascontiguousarray(mu),
-                   pos_targets=np.ascontiguousarray(ptgt), vel_targets=np.ascontiguousarray(vtgt))
+    r, d, _, _ = H.oracle_run(flat, params, root, dof, tau, mu, bits, steps, drives=(kp, kd), pos_targets=ptgt,
+                              vel_targets=vtgt)
     return r, d
 
 
@@ -99,10 +96,15 @@ def _hound_vs_oracle(host):
     gym, sim, (g_root, g_dof) = _run_sim("hound", n, H.HOUND_PARAMS, root, dof, tau, mu, ptgt, vtgt, drives, 1, host)
     o_root, o_dof = _run_oracle(flat, H.HOUND_PARAMS, root, dof, tau, mu, ptgt, vtgt, drives, 1)
     assert np.all(np.isfinite(g_root)) and np.all(np.isfinite(g_dof))
-    H.assert_mostly_close(g_root[:, 0:7], o_root[:, 0:7], atol=2e-5, max_frac=H.HOUND_SELF_FRAC, what="root pose")
-    H.assert_mostly_close(g_dof[:, :, 0], o_dof[:, :, 0], atol=2e-5, max_frac=H.HOUND_SELF_FRAC, what="dof pos")
-    H.assert_mostly_close(g_root[:, 7:13], o_root[:, 7:13], atol=5e-3, rtol=5e-3, max_frac=H.HOUND_SELF_FRAC, what="root vel")
-    H.assert_mostly_close(g_dof[:, :, 1], o_dof[:, :, 1], atol=5e-3, rtol=5e-3, max_frac=H.HOUND_SELF_FRAC, what="dof vel")
+
+    def rerun(idx, rng, bits):
+        r, d = H.perturbed(root, dof, idx, rng)
+        return H.state_fields(*_run_oracle(flat, H.HOUND_PARAMS, r, d, tau[idx], mu[idx], ptgt[idx], vtgt[idx],
+                                           drives, 1, bits))
+    # (Hound's arm-trunk / arm-leg hull contacts switch their support features on fp32 rounding, DESIGN.md 4:
+    # 2 of these 96 random states are off, both explained)
+    H.assert_close_or_explained(H.state_fields(g_root, g_dof), H.state_fields(o_root, o_dof), rerun,
+                                max_env_frac=0.03, what=f"hound arm drives {'host' if host else 'gpu'} vs oracle")
     return sim
 
 
@@ -227,5 +229,9 @@ def test_anymal_drives_leave_the_lane_team_kernel():
                                          np.zeros((n, 12)), drives, 1, False)
     assert sim.kernel_variant == 1
     o_root, o_dof = _run_oracle(flat, H.ANYMAL_PARAMS, root, dof, tau, mu, ptgt, np.zeros((n, 12)), drives, 1)
-    H.assert_mostly_close(g_dof[:, :, 0], o_dof[:, :, 0], atol=2e-5, max_frac=5e-3, what="dof pos")
-    H.assert_mostly_close(g_dof[:, :, 1], o_dof[:, :, 1], atol=5e-3, rtol=5e-3, max_frac=5e-3, what="dof vel")
+    def rerun(idx, rng, bits):
+        r, d = H.perturbed(root, dof, idx, rng)
+        return H.state_fields(*_run_oracle(flat, H.ANYMAL_PARAMS, r, d, tau[idx], mu[idx], ptgt[idx],
+                                           np.zeros((len(idx), 12)), drives, 1, bits))
+    H.assert_close_or_explained(H.state_fields(g_root, g_dof), H.state_fields(o_root, o_dof), rerun,
+                                max_env_frac=5e-3, what="anymal drives gpu (one env per lane) vs oracle")

@@ -56,22 +56,22 @@ def _host(kind, n, params, root, dof, tau, mu, nd, steps=1, terrain=None, thread
 def _explained(g, o, flat, params, root, dof, tau, mu, what, **kw):
     """Host results vs the oracle: every env within the GPU bars or its difference the oracle's own
     sensitivity (H.assert_close_or_explained)."""
-    def rerun(idx, rng):
+    def rerun(idx, rng, bits):
         r, d = H.perturbed(root, dof, idx, rng)
-        kw2 = dict(kw)
-        if "sens" in kw2:
-            kw2["sens"] = np.zeros((len(idx),) + kw2["sens"].shape[1:])
-        o_r, o_d, o_c = _oracle(flat, params, r, d, tau[idx], mu[idx], **kw2)
-        return H.state_fields(o_r, o_d, o_c if "cf" in g else None, kw2.get("sens") if "sens" in g else None)
-    print(H.assert_close_or_explained(g, o, rerun, what=what))
+        kw2 = {k: v for k, v in kw.items() if k in ("sensor_bodies", "terrain")}
+        nsens = kw["sens"].shape[1] if "sens" in kw else 0
+        o_r, o_d, o_c, o_s = H.oracle_run(flat, params, r, d, tau[idx], mu[idx], bits, nc=flat["nr"], nsens=nsens,
+                                          **kw2)
+        return H.state_fields(o_r, o_d, o_c if "cf" in g else None, o_s if "sens" in g else None)
+    H.assert_close_or_explained(g, o, rerun, what=what)
 
 
-def _check_state(g_root, g_dof, o_root, o_dof, max_frac=5e-3):
+def _check_state(g_root, g_dof, o_root, o_dof):
     assert np.all(np.isfinite(g_root)) and np.all(np.isfinite(g_dof))
-    H.assert_mostly_close(g_root[:, 0:7], o_root[:, 0:7], atol=2e-5, max_frac=max_frac, what="root pose")
-    H.assert_mostly_close(g_dof[:, :, 0], o_dof[:, :, 0], atol=2e-5, max_frac=max_frac, what="dof pos")
-    H.assert_mostly_close(g_root[:, 7:13], o_root[:, 7:13], atol=5e-3, rtol=5e-3, max_frac=max_frac, what="root vel")
-    H.assert_mostly_close(g_dof[:, :, 1], o_dof[:, :, 1], atol=5e-3, rtol=5e-3, max_frac=max_frac, what="dof vel")
+    np.testing.assert_allclose(g_root[:, 0:7], o_root[:, 0:7], atol=2e-5, rtol=0, err_msg="root pose")
+    np.testing.assert_allclose(g_dof[:, :, 0], o_dof[:, :, 0], atol=2e-5, rtol=0, err_msg="dof pos")
+    np.testing.assert_allclose(g_root[:, 7:13], o_root[:, 7:13], atol=5e-3, rtol=5e-3, err_msg="root vel")
+    np.testing.assert_allclose(g_dof[:, :, 1], o_dof[:, :, 1], atol=5e-3, rtol=5e-3, err_msg="dof vel")
 
 
 def test_no_gpu_is_used():
@@ -103,7 +103,7 @@ def test_anymal_one_simulate_matches_oracle():
     root, dof, tau, mu = H.anymal_states(n, seed=1)
     gym, sim, g_root, g_dof = _host("anymal", n, H.ANYMAL_PARAMS, root, dof, tau, mu, 12)
     o_root, o_dof, o_cf = _oracle(flat, H.ANYMAL_PARAMS, root, dof, tau, mu)
-    _check_state(g_root, g_dof, o_root, o_dof, max_frac=0.0)
+    _check_state(g_root, g_dof, o_root, o_dof)
     g_cf = sim.cf_soa.numpy().T.reshape(n, 13, 3)
     np.testing.assert_allclose(g_cf, o_cf, atol=1.0, rtol=2e-2)
     gym.refresh_net_contact_force_tensor(sim)

@@ -99,13 +99,12 @@ def test_hound_one_simulate_matches_oracle():
     osim.simulate(o_root, o_dof, np.ascontiguousarray(tau), mu, o_cf)
     assert np.all(np.isfinite(g_root)) and np.all(np.isfinite(g_dof))
     assert np.abs(o_cf).sum() > 0, "some feet / boxes must be in contact in the sampled states"
-    def rerun(idx, rng):
+    def rerun(idx, rng, bits):
         r, d = H.perturbed(root, dof, idx, rng)
-        c = np.zeros((len(idx), 24, 3))
-        OracleSim(flat, H.HOUND_PARAMS).simulate(r, d, np.ascontiguousarray(tau[idx]), mu[idx], c)
+        r, d, c, _ = H.oracle_run(flat, H.HOUND_PARAMS, r, d, tau[idx], mu[idx], bits, nc=24)
         return H.state_fields(r, d, c)
-    print(H.assert_close_or_explained(H.state_fields(g_root, g_dof, g_cf), H.state_fields(o_root, o_dof, o_cf), rerun,
-                                      what="hound gpu"))
+    H.assert_close_or_explained(H.state_fields(g_root, g_dof, g_cf), H.state_fields(o_root, o_dof, o_cf), rerun,
+                                what="hound gpu")
     # the foot spheres report at the foot links, never at the calves they are welded to
     names = art.link_names()
     feet = [names.index(f"{l}_foot") for l in ("FL", "FR", "RL", "RR")]

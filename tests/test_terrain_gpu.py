@@ -55,13 +55,12 @@ def test_rough_terrain_one_simulate_matches_oracle():
     params = dict(H.ANYMAL_PARAMS, has_ground=0)
     root0, dof0, tau, mu = _terrain_states(n, ter, 2)
 
-    def rerun(idx, rng):
+    def rerun(idx, rng, bits):
         rr, dd = H.perturbed(root0, dof0, idx, rng)
-        c = np.zeros((len(idx), flat["nb"], 3))
-        OracleSim(flat, params, terrain=ter["oracle"]).simulate(rr, dd, np.ascontiguousarray(tau[idx]), mu[idx], c)
+        rr, dd, c, _ = H.oracle_run(flat, params, rr, dd, tau[idx], mu[idx], bits, nc=flat["nb"], terrain=ter["oracle"])
         return H.state_fields(rr, dd, c)
-    print(H.assert_close_or_explained(H.state_fields(g_root, g_dof, g_cf), H.state_fields(r, d, cf), rerun,
-                                      what="rough terrain gpu"))
+    H.assert_close_or_explained(H.state_fields(g_root, g_dof, g_cf), H.state_fields(r, d, cf), rerun,
+                                what="rough terrain gpu")
 
 
 def test_flat_mesh_gpu_equals_plane_gpu(monkeypatch):
@@ -73,20 +72,27 @@ def test_flat_mesh_gpu_equals_plane_gpu(monkeypatch):
     n = 256
     root, dof, tau, mu = H.anymal_states(n, seed=6)
     root[:, 2] += 0.1
-    out = []
-    for kind in ("plane", "mesh"):
+
+    def run(kind, r0, d0):
         p = dict(H.ANYMAL_PARAMS, has_ground=int(kind == "plane"))
         gym, sim = H.make_gpu_sim("anymal", n, p, terrain=ter if kind == "mesh" else None)
-        H.load_state_into(sim, root, dof, mu)
+        H.load_state_into(sim, r0, d0, mu)
         sim.dof_force.copy_(torch.from_numpy(tau.astype(np.float32).reshape(-1)))
         for _ in range(3):
             gym.simulate(sim)
         torch.cuda.synchronize()
-        out.append(H.read_state(sim, 12) + (sim.cf_soa.cpu().numpy(),))
-    (r1, d1, c1), (r2, d2, c2) = out
-    H.assert_mostly_close(r2, r1, atol=1e-4, rtol=1e-4, max_frac=5e-3, what="root")
-    H.assert_mostly_close(d2, d1, atol=1e-3, rtol=1e-3, max_frac=5e-3, what="dof")
-    H.assert_mostly_close(c2, c1, atol=1.0, rtol=1e-2, max_frac=5e-3, what="contact forces")
+        r, d = H.read_state(sim, 12)
+        return H.state_fields(r, d, sim.cf_soa.cpu().numpy().T.reshape(n, 13, 3))
+
+    plane = run("plane", root, dof)
+    mesh = run("mesh", root, dof)
+
+    def rerun(idx, rng):
+        r, d = root.copy(), dof.copy()
+        r[idx], d[idx] = H.perturbed(root, dof, idx, rng)
+        return {k: v[idx] for k, v in run("plane", r, d).items()}
+    tol = {"pose": (1e-4, 1e-4), "vel": (1e-4, 1e-4), "q": (1e-3, 1e-3), "qd": (1e-3, 1e-3), "cf": (1.0, 1e-2)}
+    H.assert_close_or_explained(mesh, plane, rerun, tol=tol, max_env_frac=5e-3, what="flat mesh vs plane (3 substeps)")
 
 
 def test_anymal_trimesh_task_runs(monkeypatch):
