@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 5
+#define GS_ABI_VERSION 6
 
 typedef struct gs_sim gs_sim;
 
@@ -260,6 +260,14 @@ int gs_debug_phase_cycles(unsigned long long *out, int n, int reset);
  * for n spheres: centres [n][3] world, radii [n] (device pointers), threshold = r + contact_offset;
  * out [n][5] = (found, separation, normal xyz). */
 int gs_debug_terrain_query(gs_sim *sim, const float *centres, const float *radii, int n, float *out, void *stream);
+
+/* Test hook (ABI 6): each env's self-contact pool from the current sim state.
+ * mode 0: the inline narrowphase of the one-env-per-lane / host forms; mode 1 (device, split-form topologies
+ * such as UsefulHound): the near-pair records kernel then the records' gather, as the split simulate runs them.
+ * out [N][npk][10] = contact point (3, relative to the root origin), normal (3, from shape b to shape a),
+ * separation, friction, body a, body b; count [N] contacts kept (at most npk).  Device buffers on the GPU
+ * pipeline (synchronises `stream`), host buffers on the host backend. */
+int gs_debug_self_contacts(gs_sim *sim, int mode, float *out, int *count, void *stream);
 
 #ifdef __cplusplus
 }

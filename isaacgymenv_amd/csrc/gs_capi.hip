@@ -792,6 +792,18 @@ int gs_debug_terrain_query(gs_sim* s, const float* centres, const float* radii, 
   return e == hipSuccess ? 0 : hip_fail(e, "gs_debug_terrain_query");
 }
 
+int gs_debug_self_contacts(gs_sim* s, int mode, float* out, int* count, void* stream) {
+  if (ready(s, "gs_debug_self_contacts")) return -1;
+  if (!out || !count) return fail("gs_debug_self_contacts: bad buffers");
+  if (s->host) {
+    if (mode != 0) return fail("gs_debug_self_contacts: the host backend has the inline form only (mode 0)");
+    s->htopo->dbg_pool(&s->h_model, s->dp, buffers(s), out, count, s->pool);
+    return 0;
+  }
+  const hipError_t e = s->topo->dbg_pool(s->d_model, s->dp, buffers(s), mode, out, count, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "gs_debug_self_contacts (mode 1 needs a split-form topology)");
+}
+
 int gs_sim_kernel_variant(gs_sim* s) { return s ? s->variant : -1; }
 
 int gs_sim_enable_timing(gs_sim* s, int enable) {

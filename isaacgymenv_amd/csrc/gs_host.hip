@@ -23,6 +23,7 @@
 
 using gs_hostimpl::host_sim;
 using gs_hostimpl::host_pd;
+using gs_hostimpl::host_dbg_pool;
 
 HostPool* host_pool_create(int threads) {
   HostPool* p = new HostPool();
@@ -42,7 +43,7 @@ void host_pool_destroy(HostPool* p) {
 int host_pool_threads(const HostPool* p) { return p ? (int)p->workers.size() + 1 : 0; }
 
 
-#define GS_HOST_TOPO_ENTRY(T, SIG) {SIG, &host_sim<T>, &host_pd<T>},
+#define GS_HOST_TOPO_ENTRY(T, SIG) {SIG, &host_sim<T>, &host_pd<T>, &host_dbg_pool<T>},
 HostTopoEntry g_host_topologies[] = {GS_FOR_EACH_TOPOLOGY(GS_HOST_TOPO_ENTRY)};
 const int g_num_host_topologies = sizeof(g_host_topologies) / sizeof(g_host_topologies[0]);
 

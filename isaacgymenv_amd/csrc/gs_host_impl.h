@@ -157,4 +157,36 @@ void host_pd(const DevModel* M, const DevParams& P, const SimBuffers& B, const P
   }
 }
 
+// gs_debug_self_contacts on the host: each env's self-contact pool from the current state (the inline
+// narrowphase of the host substep); out [N][npk][10], count [N] as gs_physics_impl.h k_dbg_pool
+template <class T>
+void host_dbg_pool(const DevModel* M, const DevParams& P, const SimBuffers& B, float* out, int* count, HostPool* pool) {
+  using C = LaneCfg<T, false>;
+  pool->run(B.N, [&](int b, int e1) {
+    float* col = scratch(C::SLOTS);
+    for (int e = b; e < e1; ++e) {
+      int n = 0;
+      if constexpr (T::NPK > 0) {
+        constexpr int PE = PoolCfg<T>::PE;
+        poison(col, C::SLOTS);
+        EnvState<T> s;
+        load_state<T>(B.state, B.N, e, s);
+        shape_world<T, 1>(M, s, col);
+        float* pl = col + C::X_POOL;
+        n = self_contacts<T, 1>(M, P, B.mu, B.N, e, col, pl);
+        for (int p = 0; p < n; ++p) {
+          const float* o = pl + PE * p;
+          float* d = out + ((size_t)e * T::NPK + p) * 10;
+          for (int k = 0; k < 6; ++k) d[k] = o[kPoolX + k];
+          d[6] = o[kPoolSep];
+          d[7] = o[kPoolMu];
+          d[8] = o[kPoolBA];
+          d[9] = o[kPoolBB];
+        }
+      }
+      count[e] = n;
+    }
+  });
+}
+
 }  // namespace gs_hostimpl

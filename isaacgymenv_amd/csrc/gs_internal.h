@@ -114,11 +114,14 @@ typedef hipError_t (*launch_sim_fn)(const DevModel*, const DevParams&, const Sim
 typedef hipError_t (*launch_pd_fn)(const DevModel*, const DevParams&, const SimBuffers&, const PdDev&,
                                    hipStream_t);
 
+typedef hipError_t (*launch_dbg_pool_fn)(const DevModel*, const DevParams&, const SimBuffers&, int mode, float* out,
+                                        int* count, hipStream_t);
 struct TopoEntry {
   const char* sig;
   const char* name;
   launch_sim_fn sim;
   launch_pd_fn pd;
+  launch_dbg_pool_fn dbg_pool;  // gs_debug_self_contacts
   int nb, nd, nc, ns;
   int sens;  // force sensors compiled in (T::SENS)
   int row_floats, row_lanes;  // SimBuffers::rows of the plane one-env-per-lane kernels: floats per env
@@ -178,10 +181,12 @@ void host_pool_destroy(HostPool* p);
 int host_pool_threads(const HostPool* p);
 typedef void (*host_sim_fn)(const DevModel*, const DevParams&, const SimBuffers&, const float* tau, HostPool*);
 typedef void (*host_pd_fn)(const DevModel*, const DevParams&, const SimBuffers&, const PdDev&, HostPool*);
+typedef void (*host_dbg_pool_fn)(const DevModel*, const DevParams&, const SimBuffers&, float* out, int* count, HostPool*);
 struct HostTopoEntry {
   const char* sig;
   host_sim_fn sim;
   host_pd_fn pd;
+  host_dbg_pool_fn dbg_pool;  // gs_debug_self_contacts (inline narrowphase)
 };
 extern HostTopoEntry g_host_topologies[];
 extern const int g_num_host_topologies;

@@ -15,6 +15,15 @@
 namespace {
 
 GS_HD float dot3f(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+// GS_GJK_TRACE=<env> (debug builds only, tools/probes/hound_pool_probe.py): device printf of GJK's iterations
+// for that env in the one-thread-per-env debug kernel (gs_debug_self_contacts)
+#if defined(GS_GJK_TRACE) && defined(__HIP_DEVICE_COMPILE__)
+#define GS_GJK_TR(...) \
+  if ((int)(blockIdx.x * blockDim.x + threadIdx.x) == GS_GJK_TRACE) printf(__VA_ARGS__)
+#else
+#define GS_GJK_TR(...)
+#endif
+
 GS_HD void cross3f(const float* a, const float* b, float* o) {
   o[0] = a[1] * b[2] - a[2] * b[1];
   o[1] = a[2] * b[0] - a[0] * b[2];
@@ -377,29 +386,11 @@ GS_HD void simplex_subset(const float (&W)[4][3], int k, float& best, int& bm, f
     }
     l[0] = l0;
     if (!ok || !(l0 > 1e-12f)) return;
-    // the closest point itself from cross products, not W0 + mu E: the normal equations' rounding leaves the
-    // point off the segment's perpendicular / the triangle's plane normal by ~cond(G) ulps, which turned
-    // into up to ~1e-2 rad of contact-normal error for near-parallel hull faces (the barycentrics above
-    // only decide validity and the closest points of the two cores)
-    if constexpr (q == 1) {
-      float c1[3], c2[3];
-      cross3f(E[0], W[id[0]], c1);
-      cross3f(c1, E[0], c2);
 #pragma unroll
-      for (int a = 0; a < 3; ++a) p[a] = c2[a] / G[0][0];
-    } else if constexpr (q == 2) {
-      float nr[3];
-      cross3f(E[0], E[1], nr);
-      const float s = dot3f(nr, W[id[0]]) / dot3f(nr, nr);
+    for (int a = 0; a < 3; ++a) {
+      p[a] = W[id[0]][a];
 #pragma unroll
-      for (int a = 0; a < 3; ++a) p[a] = s * nr[a];
-    } else {
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        p[a] = W[id[0]][a];
-#pragma unroll
-        for (int j = 0; j < q; ++j) p[a] += mu[j] * E[j][a];
-      }
+      for (int j = 0; j < q; ++j) p[a] += mu[j] * E[j][a];
     }
   }
   const float d2 = dot3f(p, p);
@@ -444,6 +435,8 @@ GS_HD float gjk_cores(const DevModel* __restrict__ M, int sa, int sb, const Shap
 #pragma unroll
     for (int t = 0; t < 3; ++t) w[t] = a[t] - b[t];
     const float vv = dot3f(v, v), vw = dot3f(v, w);
+    GS_GJK_TR("gjk %d-%d it %d k %d v %.9g %.9g %.9g w %.9g %.9g %.9g vv %.9g vw %.9g\n", sa, sb, it, k, v[0], v[1],
+              v[2], w[0], w[1], w[2], vv, vw);
     if (vw > 0.f && vw * vw > stop * stop * vv) return vw / sqrtf(vv);  // separated by more than stop
     // converged: the support plane is within 1e-6 |v| of the simplex's closest point (the distance to ~1e-6
     // relative; the oracle's fp64 bound is 1e-10, which float arithmetic cannot resolve: below ~1e-7 vv the test
@@ -466,6 +459,7 @@ GS_HD float gjk_cores(const DevModel* __restrict__ M, int sa, int sb, const Shap
     float best = 3.0e38f, l4[4] = {0.f, 0.f, 0.f, 0.f};
     int mask = 0;
     simplex_all(W, k, best, mask, v, l4);
+    GS_GJK_TR("gjk %d-%d   mask %d best %.9g v %.9g %.9g %.9g\n", sa, sb, mask, best, v[0], v[1], v[2]);
     if (!mask) return 0.f;
     // keep the chosen subset, in order (compile-time moves under runtime conditions)
     float W2[4][3], A2[4][3], B2[4][3];
@@ -500,7 +494,42 @@ GS_HD float gjk_cores(const DevModel* __restrict__ M, int sa, int sb, const Shap
     if (i < k)
 #pragma unroll
       for (int t = 0; t < 3; ++t) { pa[t] += lam[i] * A[i][t]; pb[t] += lam[i] * B[i][t]; }
-  vout[0] = v[0]; vout[1] = v[1]; vout[2] = v[2];
+  // The separating direction from the final simplex's geometry: its affine closest point from cross products
+  // (the segment's perpendicular, the triangle's plane normal) instead of W0 + mu E, whose normal-equation
+  // rounding leaves it off the perpendicular by ~cond(G) ulps -- up to ~1e-2 rad of contact-normal error for
+  // near-parallel hull faces in float.  Only the direction is refined (GJK's subset choice above keeps the
+  // normal-equation points, which lie in the simplex's affine hull: a cross-product point of a near-degenerate
+  // subset could undercut the true distance and mislead the search), and only from a well-conditioned simplex.
+  float vr[3] = {v[0], v[1], v[2]};
+  if (k == 2 || k == 3) {
+    float E0[3], E1[3], pr[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) { E0[t] = W[1][t] - W[0][t]; E1[t] = W[2][t] - W[0][t]; }
+    bool ok = false;
+    if (k == 2) {
+      const float ee = dot3f(E0, E0);
+      float c1[3];
+      cross3f(E0, W[0], c1);
+      cross3f(c1, E0, pr);
+      ok = ee > 0.f;
+#pragma unroll
+      for (int t = 0; t < 3; ++t) pr[t] = ok ? pr[t] / ee : 0.f;
+    } else {
+      float nr[3];
+      cross3f(E0, E1, nr);
+      const float nn2 = dot3f(nr, nr);
+      ok = nn2 > 1e-8f * dot3f(E0, E0) * dot3f(E1, E1);  // the triangle's angles above ~1e-4 rad
+      const float s = ok ? dot3f(nr, W[0]) / nn2 : 0.f;
+#pragma unroll
+      for (int t = 0; t < 3; ++t) pr[t] = s * nr[t];
+    }
+    // (a refinement, not a new answer: it must agree with v to within a small angle)
+    const float vv = dot3f(v, v), pp = dot3f(pr, pr), vp = dot3f(v, pr);
+    if (ok && vp > 0.f && vp * vp >= 0.9999f * vv * pp) { vr[0] = pr[0]; vr[1] = pr[1]; vr[2] = pr[2]; }
+  }
+  vout[0] = vr[0]; vout[1] = vr[1]; vout[2] = vr[2];
+  GS_GJK_TR("gjk %d-%d done k %d pa %.9g %.9g %.9g pb %.9g %.9g %.9g\n", sa, sb, k, pa[0], pa[1], pa[2], pb[0], pb[1],
+            pb[2]);
   return sqrtf(dot3f(v, v));
 }
 

@@ -11,6 +11,8 @@
 #if GS_INST_FORM == 0
 template hipError_t launch_sim_plane<GS_INST_TOPO>(const DevModel*, const DevParams&, const SimBuffers&, const float*,
                                                    hipStream_t);
+template hipError_t launch_dbg_pool<GS_INST_TOPO>(const DevModel*, const DevParams&, const SimBuffers&, int, float*,
+                                                  int*, hipStream_t);
 #elif GS_INST_FORM == 1
 template hipError_t launch_sim_terr<GS_INST_TOPO>(const DevModel*, const DevParams&, const SimBuffers&, const float*,
                                                   hipStream_t);

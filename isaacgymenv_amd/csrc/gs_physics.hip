@@ -143,6 +143,9 @@ template <class T>
 hipError_t launch_pd_terr(const DevModel*, const DevParams&, const SimBuffers&, const PdDev&, hipStream_t);
 
 template <class T>
+hipError_t launch_dbg_pool(const DevModel*, const DevParams&, const SimBuffers&, int, float*, int*, hipStream_t);
+
+template <class T>
 hipError_t launch_sim(const DevModel* M, const DevParams& P, const SimBuffers& B, const float* tau, hipStream_t st) {
   return P.has_terrain ? launch_sim_terr<T>(M, P, B, tau, st) : launch_sim_plane<T>(M, P, B, tau, st);
 }
@@ -152,7 +155,7 @@ hipError_t launch_pd(const DevModel* M, const DevParams& P, const SimBuffers& B,
 }
 
 #define GS_TOPO_ENTRY(T, SIG)                                                                          \
-  {SIG, T::kName, &launch_sim<T>, &launch_pd<T>, T::NB, T::ND, T::NC, T::NS, T::SENS ? 1 : 0,            \
+  {SIG, T::kName, &launch_sim<T>, &launch_pd<T>, &launch_dbg_pool<T>, T::NB, T::ND, T::NC, T::NS, T::SENS ? 1 : 0,            \
    LaneCfg<T, false>::ROW_FLOATS, LaneCfg<T, false>::LB, T::NPK, T::cdyn, T::NPAIR, T::pair_a, T::pair_b,      \
    T::pair_k, T::shkind},
 TopoEntry g_topologies[] = {GS_FOR_EACH_TOPOLOGY(GS_TOPO_ENTRY)};

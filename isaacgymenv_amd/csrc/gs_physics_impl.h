@@ -305,6 +305,70 @@ hipError_t launch_sim_plane(const DevModel* M, const DevParams& P, const SimBuff
   }
   return hipGetLastError();
 }
+// ---------------------------------------------------------------- self-contact pool dump (test hook)
+// gs_debug_self_contacts: each env's self-contact pool from the current state, one env per thread with its
+// column in device memory (LB = 1).  MODE 0: the inline narrowphase (self_contacts, what the lane / host forms
+// run); MODE 1: the split form's route -- k_pair_records into SimBuffers::rows, then pool_from_records.
+// out [N][npk][10] = x (3, root-origin relative), n (3), separation, friction, body a, body b; count [N].
+namespace gs_phys {
+template <class T, int MODE>
+__global__ void k_dbg_pool(const DevModel* __restrict__ M, DevParams P, SimBuffers B, float* __restrict__ work,
+                           float* __restrict__ out, int* __restrict__ count) {
+  using C = LaneCfg<T, false>;
+  const int N = B.N, e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N) return;
+  int n = 0;
+  constexpr int NPK = T::NPK > 0 ? T::NPK : 1;
+  if constexpr (T::NPK > 0) {
+    constexpr int PE = PoolCfg<T>::PE;
+    float* col = work + (size_t)e * C::SLOTS;
+    float* pool = col + C::X_POOL;
+    if constexpr (MODE == 0) {
+      EnvState<T> s;
+      load_state<T>(B.state, N, e, s);
+      shape_world<T, 1>(M, s, col);
+      n = self_contacts<T, 1>(M, P, B.mu, N, e, col, pool);
+    } else {
+      n = pool_from_records<T, 1, 1>(M, B.mu, N, e, B.rows + (size_t)e * C::ROW_FLOATS, pool);
+    }
+    for (int p = 0; p < n; ++p) {
+      const float* o = pool + PE * p;
+      float* d = out + ((size_t)e * NPK + p) * 10;
+      for (int k = 0; k < 6; ++k) d[k] = o[kPoolX + k];
+      d[6] = o[kPoolSep];
+      d[7] = o[kPoolMu];
+      d[8] = o[kPoolBA];
+      d[9] = o[kPoolBB];
+    }
+  }
+  count[e] = n;
+}
+}  // namespace gs_phys
+
+template <class T>
+hipError_t launch_dbg_pool(const DevModel* M, const DevParams& P, const SimBuffers& B, int mode, float* out,
+                           int* count, hipStream_t st) {
+  using C = LaneCfg<T, false>;
+  if (mode != 0 && !(mode == 1 && C::SPLIT && B.rows)) return hipErrorInvalidValue;
+  float* work = nullptr;
+  hipError_t e = hipMalloc(&work, sizeof(float) * (size_t)B.N * C::SLOTS);
+  if (e != hipSuccess) return e;
+  DevParams P1 = P;
+  P1.substeps = 1;
+  if (mode == 1) {
+    if constexpr (C::SPLIT)
+      hipLaunchKernelGGL((gs_phys::k_pair_records<T>), dim3((B.N + gs_phys::kPairEnvs - 1) / gs_phys::kPairEnvs),
+                         dim3(gs_phys::kTerrWave), 0, st, M, P1, B);
+    hipLaunchKernelGGL((gs_phys::k_dbg_pool<T, 1>), dim3((B.N + 63) / 64), dim3(64), 0, st, M, P1, B, work, out, count);
+  } else {
+    hipLaunchKernelGGL((gs_phys::k_dbg_pool<T, 0>), dim3((B.N + 63) / 64), dim3(64), 0, st, M, P1, B, work, out, count);
+  }
+  e = hipGetLastError();
+  const hipError_t e2 = hipStreamSynchronize(st);
+  (void)hipFree(work);
+  return e != hipSuccess ? e : e2;
+}
+
 template <class T>
 hipError_t launch_sim_terr(const DevModel* M, const DevParams& P, const SimBuffers& B, const float* tau, hipStream_t st) {
   constexpr int LB = LaneCfg<T, true>::LB;

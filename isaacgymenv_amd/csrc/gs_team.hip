@@ -1446,6 +1446,17 @@ __device__ __forceinline__ void team_com_velocity(const DevModel* __restrict__ M
   v[0] = s.vo[0] + wc[0]; v[1] = s.vo[1] + wc[1]; v[2] = s.vo[2] + wc[2];
 }
 
+// XCD-aware workgroup -> env-block mapping.  The dispatcher hands workgroup b to XCD b % 8, and each XCD has
+// its own L2: with the identity mapping the two 64-B halves of every 128-B line of a SoA state row (16 envs x
+// 4 B per wave) were read by workgroups on two different XCDs, each fetching the line from HBM (2.2x the
+// algorithmic read bytes, profiles/pmc_pd_step.json r03).  Here the workgroups an XCD runs take consecutive env
+// blocks (a bijection on [0, G) for any G), so neighbouring halves meet in one L2.
+__device__ __forceinline__ int xcd_block(int b, int G) {
+  constexpr int kXcd = 8;
+  const int per = G / kXcd, rem = G % kXcd, x = b % kXcd, q = b / kXcd;
+  return x * per + (x < rem ? x : rem) + q;
+}
+
 template <class T>
 __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel* __restrict__ M, DevParams P,
                                                                  SimBuffers B, const float* __restrict__ tau_aos) {
@@ -1458,7 +1469,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel*
   stage_shape_consts<T>(M, sct);
   __syncthreads();
   const int lc = threadIdx.x & (LN - 1);
-  const int e = (blockIdx.x * kTeamBlock + threadIdx.x) / LN;
+  const int e = (xcd_block(blockIdx.x, gridDim.x) * kTeamBlock + threadIdx.x) / LN;
   if (e >= B.N) return;
   const int N = B.N;
   TeamState<T> s;
@@ -1489,7 +1500,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
   stage_shape_consts<T>(M, sct);
   __syncthreads();
   const int lc = threadIdx.x & (LN - 1);
-  const int e = (blockIdx.x * kTeamBlock + threadIdx.x) / LN;
+  const int e = (xcd_block(blockIdx.x, gridDim.x) * kTeamBlock + threadIdx.x) / LN;
   if (e >= B.N) return;
   const int N = B.N;
   TeamState<T> s;

@@ -90,6 +90,7 @@ def lib():
             "gs_sim_refresh_force_sensor": (i, [vp, vp, vp]),
             "gs_sim_add_triangle_mesh": (i, [vp, vp, C.c_int64, vp, C.c_int64, vp, d, d, d]),
             "gs_debug_terrain_query": (i, [vp, vp, vp, i, vp, vp]),
+            "gs_debug_self_contacts": (i, [vp, i, vp, vp, vp]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -112,6 +113,7 @@ EXPORTED_SYMBOLS = [
     "gs_sim_set_force_sensors", "gs_sim_bind_force_sensors", "gs_sim_refresh_force_sensor",
     "gs_sim_add_triangle_mesh", "gs_debug_terrain_query", "gs_sim_refresh_rigid_body", "gs_sim_refresh_jacobian",
     "gs_sim_refresh_mass_matrix", "gs_sim_set_dof_drives", "gs_sim_bind_dof_targets", "gs_sim_set_self_collision",
+    "gs_debug_self_contacts",
 ]
 
 

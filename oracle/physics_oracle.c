@@ -491,23 +491,9 @@ static int simplex_closest(real W[4][3], int k, real *v, real *lam) {
             for (int j = 0; j < q; ++j) { l0 -= mu[j]; l[j + 1] = mu[j]; if (!(mu[j] > 1e-12)) ok = 0; }
             l[0] = l0;
             if (!ok || !(l0 > 1e-12)) continue;
-            /* the closest point from cross products (same point as W0 + mu E in exact arithmetic; the kernels'
-             * float form needs it, gs_pairs.h simplex_subset) */
-            if (q == 1) {
-                real c1[3], c2[3];
-                cross3(E[0], W[id[0]], c1);
-                cross3(c1, E[0], c2);
-                for (int a = 0; a < 3; ++a) p[a] = c2[a] / G[0][0];
-            } else if (q == 2) {
-                real nr[3];
-                cross3(E[0], E[1], nr);
-                const real s = dot3(nr, W[id[0]]) / dot3(nr, nr);
-                for (int a = 0; a < 3; ++a) p[a] = s * nr[a];
-            } else {
-                for (int a = 0; a < 3; ++a) {
-                    p[a] = W[id[0]][a];
-                    for (int j = 0; j < q; ++j) p[a] += mu[j] * E[j][a];
-                }
+            for (int a = 0; a < 3; ++a) {
+                p[a] = W[id[0]][a];
+                for (int j = 0; j < q; ++j) p[a] += mu[j] * E[j][a];
             }
         }
         const real d2 = dot3(p, p);
@@ -566,7 +552,33 @@ static real gjk_cores(const OModel *m, int sa, int sb, const ShapeW *Wa, const S
     for (int t = 0; t < 3; ++t) { pa[t] = 0; pb[t] = 0; }
     for (int i = 0; i < k; ++i)
         for (int t = 0; t < 3; ++t) { pa[t] += lam[i] * A[i][t]; pb[t] += lam[i] * B[i][t]; }
-    for (int t = 0; t < 3; ++t) vout[t] = v[t];
+    /* the separating direction refined from the final simplex's geometry (the segment's perpendicular, the
+     * triangle's plane normal: the same direction as v in exact arithmetic; gs_pairs.h gjk_cores, where float
+     * needs it), only from a well-conditioned simplex and within a small angle of v */
+    real vr[3] = {v[0], v[1], v[2]};
+    if (k == 2 || k == 3) {
+        real E0[3], E1[3], pr[3];
+        for (int t = 0; t < 3; ++t) { E0[t] = W[1][t] - W[0][t]; E1[t] = W[2][t] - W[0][t]; }
+        int ok;
+        if (k == 2) {
+            const real ee = dot3(E0, E0);
+            real c1[3];
+            cross3(E0, W[0], c1);
+            cross3(c1, E0, pr);
+            ok = ee > 0;
+            for (int t = 0; t < 3; ++t) pr[t] = ok ? pr[t] / ee : 0;
+        } else {
+            real nr[3];
+            cross3(E0, E1, nr);
+            const real nn2 = dot3(nr, nr);
+            ok = nn2 > 1e-8 * dot3(E0, E0) * dot3(E1, E1);
+            const real s = ok ? dot3(nr, W[0]) / nn2 : 0;
+            for (int t = 0; t < 3; ++t) pr[t] = s * nr[t];
+        }
+        const real vv = dot3(v, v), pp = dot3(pr, pr), vp = dot3(v, pr);
+        if (ok && vp > 0 && vp * vp >= 0.9999 * vv * pp) for (int t = 0; t < 3; ++t) vr[t] = pr[t];
+    }
+    for (int t = 0; t < 3; ++t) vout[t] = vr[t];
     return sqrt(dot3(v, v));
 }
 

@@ -245,6 +245,21 @@ def upside_down_anymal(n):
     return root, dof
 
 
+def sim_self_contacts(sim, mode=0):
+    """The sim's self-contact pools from its current state (gs_debug_self_contacts): (contacts [n, npk, 10] float64
+    = x xyz, n xyz, separation, friction, body a, body b -- the oracle's self_contacts layout; counts [n])."""
+    import torch
+    from isaacgymenv_amd.isaacgym import _lib
+    n, npk = sim.num_envs, max(1, int(sim.asset.flat["npool"]))
+    dev = sim.state.device
+    out = torch.zeros((n, npk, 10), dtype=torch.float32, device=dev)
+    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    stream = None if dev.type == "cpu" else torch.cuda.current_stream().cuda_stream
+    _lib.check(_lib.lib().gs_debug_self_contacts(sim.handle, mode, out.data_ptr(), cnt.data_ptr(), stream),
+               "gs_debug_self_contacts")
+    return out.cpu().numpy().astype(np.float64), cnt.cpu().numpy()
+
+
 def load_state_into(sim, root, dof, mu):
     """Write oracle-layout numpy state ([N,13] internal root, [N,nd,2]) into the SoA sim state."""
     import torch

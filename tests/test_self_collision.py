@@ -211,3 +211,50 @@ def test_lane_kernel_self_contacts_match_oracle():
 @pytest.mark.gpu
 def test_team_kernel_self_contacts_match_oracle():
     _sim_vs_oracle(host=False, variant=2)
+
+
+def _pool_vs_oracle(pools, flat, root, dof, mu, what):
+    """Self-contact pools (gs_debug_self_contacts) against the oracle's from the same states: same contact count
+    in >= 98 % of the envs; where the counts agree, every contact's point, normal and separation within 1e-2
+    (the fp32 GJK's contact normal on near-parallel hull faces)."""
+    o_pool, o_cnt = OracleSim(flat, H.HOUND_PARAMS).self_contacts(root, dof, mu)
+    g_pool, g_cnt = pools
+    n = len(o_cnt)
+    same = g_cnt == o_cnt
+    assert same.mean() >= 0.98, (what, np.nonzero(~same)[0][:10])
+    assert o_cnt.sum() > n, "the states must have self-contacts"
+    worst = 0.0
+    for e in np.nonzero(same)[0]:
+        k = o_cnt[e]
+        if k:
+            assert np.array_equal(g_pool[e, :k, 8:10], o_pool[e, :k, 8:10]), (what, e)  # same pairs, same order
+            worst = max(worst, float(np.abs(g_pool[e, :k, :7] - o_pool[e, :k, :7]).max()))
+    assert worst <= 1e-2, (what, worst)
+    H.parity_report(f"{what}: self-contact pools vs oracle, {int(same.sum())} of {n} envs with equal counts, "
+                    f"worst point / normal / separation difference {worst:.3g}")
+
+
+def test_host_hound_self_contact_pools_match_oracle():
+    n = 96
+    art, flat = H.hound()
+    root, dof, tau, mu = H.hound_states(n, seed=9)
+    gym, sim = H.make_host_sim("hound", n, H.HOUND_PARAMS)
+    H.load_state_into(sim, root, dof, mu)
+    _pool_vs_oracle(H.sim_self_contacts(sim, 0), flat, root, dof, mu, "hound host")
+
+
+@pytest.mark.gpu
+def test_gpu_hound_self_contact_pools_match_oracle():
+    """Device pools in both forms -- inline narrowphase, and the split form's near-pair records kernel plus the
+    records' gather (what UsefulHound's simulate runs) -- against the oracle, and against each other."""
+    n = 256
+    art, flat = H.hound()
+    root, dof, tau, mu = H.hound_states(n, seed=9)
+    gym, sim = H.make_gpu_sim("hound", n, H.HOUND_PARAMS)
+    H.load_state_into(sim, root, dof, mu)
+    inline = H.sim_self_contacts(sim, 0)
+    records = H.sim_self_contacts(sim, 1)
+    _pool_vs_oracle(inline, flat, root, dof, mu, "hound gpu inline")
+    _pool_vs_oracle(records, flat, root, dof, mu, "hound gpu records")
+    np.testing.assert_array_equal(inline[1], records[1])
+    np.testing.assert_allclose(inline[0], records[0], rtol=0, atol=1e-6)
