@@ -268,11 +268,11 @@ __global__ __launch_bounds__(kTerrWave, 1) void k_pd_step_wave(const DevModel* _
 }  // namespace gs_phys
 
 // launchers, one per kernel form (instantiated per topology in gs_phys_inst.hip).  Mesh sims run the
-// wave-assisted kernels; with GS_WAVE_PLANE_SELF plane sims with self-collision whose envs are LDS-starved
-// (<= 4 env lanes per workgroup: UsefulHound) do too.
-// (off: measured slower for UsefulHound, the only such topology -- 4.68 vs 4.17 ms per substep: the pair records
-// cost it a workgroup per CU of LDS while its substep is bound by the solver lane's scratch latency, not by the
-// narrowphase; profiles/r03f_hound_ab.txt)
+// wave-assisted kernels.  Plane sims with self-collision whose envs are LDS-starved (<= 4 env lanes per
+// workgroup: UsefulHound): the simulate takes the split form when LaneCfg::SPLIT (k_pair_records, then
+// k_simulate reading the records; r03: 1.64 vs 2.05 ms per substep for the wave form), and the fused PD step
+// (gs_sim_pd_step) the wave-assisted form when GS_WAVE_PLANE_SELF (default 1) -- two narrowphase routes for one
+// topology, each pinned against the oracle on the GPU (test_hound_gpu.py: the simulate and the fused PD step).
 #ifndef GS_WAVE_PLANE_SELF
 #define GS_WAVE_PLANE_SELF 1
 #endif

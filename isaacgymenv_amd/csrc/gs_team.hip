@@ -600,13 +600,20 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
     }
   }
   __syncthreads();
+#ifdef GS_PHASE_PROFILE
+  if ((threadIdx.x & 63) == 0) atomicAdd(&gs_phase_cycles[14], (unsigned long long)(clock64() - np_t0));
+#endif
   // the team's near pairs (team-uniform mask) -> the narrowphase of those pairs, replicated in the team's lanes
   const unsigned long long tmask = quad_or64(near);
   int cnt = 0;
   if (tmask) cnt = self_contacts<T, TPW, RW, RowSlots<T>::PER_POOL>(M, P, mu_g, N, e, tab, pool, ShapeConstsTab{sct},
                                                                     tmask);
 #ifdef GS_PHASE_PROFILE
-  if ((threadIdx.x & 63) == 0) atomicAdd(&gs_phase_cycles[13], (unsigned long long)(clock64() - np_t0));
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&gs_phase_cycles[13], (unsigned long long)(clock64() - np_t0));
+    atomicAdd(&gs_phase_cycles[15], (unsigned long long)__popcll(__ballot(tmask != 0ull)));  // teams' lanes with pairs
+    atomicAdd(&gs_phase_cycles[10], (unsigned long long)__popcll(tmask));  // (lane 0's team) near pairs
+  }
 #endif
   return cnt;
 }

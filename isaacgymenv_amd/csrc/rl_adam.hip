@@ -77,11 +77,13 @@ __global__ __launch_bounds__(kThreads) void k_opt_adam(float* __restrict__ param
   float sq;
   bool found;
   totals(part, sh, sq, found);
-  if (found) return;  // scaler.step skips the optimizer step
+  // GradScaler.step skips the optimizer step on a non-finite gradient; without loss scaling torch's Adam steps
+  // anyway (and a non-finite gradient makes the parameters non-finite, as there)
+  if (found && scale) return;
   float coef = 1.f;
-  if (h.max_norm > 0.f) {  // clip_grad_norm_: max_norm / (total_norm + 1e-6), clamped to 1
+  if (h.max_norm > 0.f) {  // clip_grad_norm_: max_norm / (total_norm + 1e-6), clamp(max=1) (NaN stays NaN)
     const float c = h.max_norm / (sqrtf(sq) + 1e-6f);
-    coef = c < 1.f ? c : 1.f;
+    coef = c > 1.f ? 1.f : c;
   }
   const float gs = (scale ? 1.0f / *scale : 1.0f) * coef;
   const float t = *step + 1.f;
@@ -114,7 +116,7 @@ __global__ __launch_bounds__(kThreads) void k_opt_finish(float* __restrict__ ste
   bool found;
   totals(part, sh, sq, found);
   if (threadIdx.x != 0) return;
-  if (!found) *step += 1.f;
+  if (!found || !scale) *step += 1.f;  // (a skipped step exists only with loss scaling, k_opt_adam)
   if (scale && tracker) {  // torch._amp_update_scale_
     if (found) {
       *scale *= h.backoff;
@@ -122,7 +124,8 @@ __global__ __launch_bounds__(kThreads) void k_opt_finish(float* __restrict__ ste
     } else {
       const int32_t s = *tracker + 1;
       if (s == h.growth_interval) {
-        *scale *= h.growth;
+        const float grown = *scale * h.growth;
+        if (isfinite(grown)) *scale = grown;  // growth only while the scale stays finite
         *tracker = 0;
       } else {
         *tracker = s;

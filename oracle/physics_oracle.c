@@ -509,9 +509,10 @@ static int simplex_closest(real W[4][3], int k, real *v, real *lam) {
 
 /* GJK distance between the cores of shapes a and b: closest points pa, pb, separating vector vout (the final
  * simplex's closest point, = pa - pb); returns the distance, 0 when the cores overlap */
-/* narrowphase workload counters (analysis only: oracle_pair_stats): pairs tested, bounding spheres met,
- * GJK calls, GJK iterations, contacts kept (not thread-safe: read them from single-threaded runs) */
-static long long g_pair_stats[5];
+/* narrowphase workload counters (analysis only: oracle_pair_stats, tools/pool_overflow_study.py): pairs tested,
+ * bounding spheres met, GJK calls, GJK iterations, contacts kept, deep core overlaps skipped (GS_DEEP_SKIP),
+ * contacts dropped at the pool cap (not thread-safe: read them from single-threaded runs) */
+static long long g_pair_stats[7];
 
 static real gjk_cores(const OModel *m, int sa, int sb, const ShapeW *Wa, const ShapeW *Wb, const real *Ra,
                       const real *Pa, const real *Rb, const real *Pb, real *pa, real *pb, real *vout) {
@@ -721,7 +722,7 @@ static int self_contacts(const OModel *m, const OParams *p, real R[][9], real P[
             } else {
                 for (int k = 0; k < 3; ++k) nn[k] /= dist;
             }
-            if (deep) continue; /* overlapping cores: no contact */
+            if (deep) { ++g_pair_stats[5]; continue; } /* overlapping cores: no contact */
             const real sep = dist - ra - rb;
             if (!(sep < off)) continue;
             PairContact *o = &out[n++];
@@ -1399,8 +1400,8 @@ int oracle_hull_select(const OModel *m, const OParams *p, int sh, const real *R,
 
 /* narrowphase workload counters since the last call (g_pair_stats); reset = 1 clears them */
 int oracle_pair_stats(long long *out, int reset) {
-    for (int i = 0; i < 5; ++i) out[i] = g_pair_stats[i];
+    for (int i = 0; i < 7; ++i) out[i] = g_pair_stats[i];
     if (reset)
-        for (int i = 0; i < 5; ++i) g_pair_stats[i] = 0;
+        for (int i = 0; i < 7; ++i) g_pair_stats[i] = 0;
     return 0;
 }

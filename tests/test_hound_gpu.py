@@ -219,3 +219,59 @@ def test_hound_control_kernel_matches_reference(monkeypatch):
     scale = np.maximum(1.0, np.abs(ref))
     assert np.all(np.abs(got - ref) <= 1e-4 * scale), np.abs(got - ref).max()
     np.testing.assert_array_equal(f(env._effort_control[:, :6]), got)
+
+
+def _pd_sequence(flat, params, root, dof, dof_tensor, mu, act, default, kp, kd, scale, decimation, extra, bits=64):
+    """anymal_terrain.py:443-451's decimation loop (+ the extra simulate) on the oracle: the first PD torque from
+    the stale dof tensor, the next from the oracle's own state (the same sequence gs_sim_pd_step fuses)."""
+    dt = np.float64 if bits == 64 else np.float32
+    c = lambda a: np.ascontiguousarray(a, dtype=dt)  # noqa: E731
+    sim = OracleSim(flat, params, real_bits=bits)
+    r, d, mu = c(root), c(dof), c(mu)
+    cf = np.zeros((root.shape[0], flat["nr"], 3), dt)
+    q, qd = dof_tensor[:, :, 0], dof_tensor[:, :, 1]
+    tau = None
+    for i in range(decimation + extra):
+        if i < decimation:
+            tau = np.clip(kp * (scale * act + default - q) - kd * qd, -80.0, 80.0)
+        sim.simulate(r, d, c(tau), mu, cf)
+        q, qd = d[:, :, 0].copy(), d[:, :, 1].copy()
+    f = lambda a: np.asarray(a, np.float64)  # noqa: E731
+    return dict(q=f(d[:, :, 0]), qd=f(d[:, :, 1]), pose=f(r[:, :7]), vel=f(r[:, 7:]), tau=f(tau), cf=f(cf))
+
+
+def test_hound_fused_pd_step_with_self_collision_matches_oracle():
+    """gs_sim_pd_step on UsefulHound's topology runs the wave-assisted PD kernel (k_pd_step_wave: the
+    near-pair records in the env columns), a different narrowphase route than its simulate (the split
+    records kernel): 4 PD evaluations + 5 substeps from random states against the oracle's sequence
+    (this combination had no GPU test)."""
+    n = 256
+    art, flat = H.hound()
+    root, dof, tau, mu = H.hound_states(n, seed=13, spread=0.5)
+    gym, sim = H.make_gpu_sim("hound", n, H.HOUND_PARAMS)
+    H.load_state_into(sim, root, dof, mu)
+    gym.refresh_dof_state_tensor(sim)
+    torch.cuda.synchronize()
+    dof_tensor = sim.dof_tensor.view(n, 18, 2).double().cpu().numpy()
+    rng = np.random.RandomState(2)
+    act = rng.uniform(-1.0, 1.0, (n, 18))
+    default = np.array([0.0, 0.7854, -1.5708] * 4 + [0.0] * 6)
+    kp, kd, scale = 80.0, 2.0, 0.5
+    torques = torch.empty((n, 18), device="cuda:0")
+    gym.amd_pd_decimation_step(sim, torch.from_numpy(act.astype(np.float32)).cuda(),
+                               torch.from_numpy(default.astype(np.float32)).cuda(), kp, kd, scale, 80.0, 4, 1, torques)
+    torch.cuda.synchronize()
+    g_root, g_dof = H.read_state(sim, 18)
+    gpu = dict(q=g_dof[:, :, 0], qd=g_dof[:, :, 1], pose=g_root[:, :7], vel=g_root[:, 7:],
+               tau=torques.double().cpu().numpy(), cf=sim.contact_tensor.double().cpu().numpy().reshape(n, 24, 3))
+    ref = _pd_sequence(flat, H.HOUND_PARAMS, root, dof, dof_tensor, mu, act, default, kp, kd, scale, 4, 1)
+    assert np.abs(ref["cf"]).sum() > 0
+
+    def rerun(idx, rng_, bits):
+        r, d = H.perturbed(root, dof, idx, rng_)
+        return _pd_sequence(flat, H.HOUND_PARAMS, r, d, dof_tensor[idx], mu[idx], act[idx], default, kp, kd, scale, 4,
+                            1, bits)
+    tol = {"q": (1e-4, 0.0), "qd": (2.5e-2, 2.5e-2), "pose": (1e-4, 0.0), "vel": (2.5e-2, 2.5e-2), "tau": (0.5, 1e-2),
+           "cf": (2.0, 5e-2)}
+    H.assert_close_or_explained(gpu, ref, rerun, tol=tol, max_env_frac=0.03,
+                                what="hound fused pd step (wave-assisted self-collision) vs oracle")

@@ -407,6 +407,59 @@ def test_fused_opt_step_matches_torch_adam():
     torch.testing.assert_close(v, v_ref, rtol=1e-5, atol=1e-12)
 
 
+@pytest.mark.parametrize("clip,weight_decay", [(0.0, 0.0), (1.0, 1e-2), (0.0, 1e-3)])
+def test_fused_opt_step_without_scaler_matches_torch_adam(clip, weight_decay):
+    """rl_opt_step without loss scaling (scale / tracker None: configs with mixed_precision False), with and without
+    the norm clip (truncate_grads) and with weight decay, against torch Adam + clip_grad_norm_; a non-finite
+    gradient is NOT skipped here (torch's optimizer steps without a GradScaler)."""
+    from isaacgymenv_amd.rl import gae
+    torch.manual_seed(5)
+    sizes = [(64, 20), (64,), (8, 64), (8,)]
+    n = sum(int(np.prod(s)) for s in sizes)
+    flat0 = torch.randn(n, device="cuda") * 0.1
+    ref = [torch.nn.Parameter(t.clone().view(s)) for t, s in zip(torch.split(flat0, [int(np.prod(s)) for s in sizes]), sizes)]
+    lr = torch.tensor(1e-3, device="cuda")
+    opt = torch.optim.Adam(ref, lr=lr, eps=1e-8, weight_decay=weight_decay, fused=True, capturable=True)
+    p, m, v = flat0.clone(), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    step = torch.zeros((), device="cuda")
+    part = torch.empty(gae.lib().rl_opt_partials_size(), device="cuda")
+    hyper = gae.OptHyper(clip, 0.9, 0.999, 1e-8, weight_decay, 0.5, 2.0, 2000)
+    for it in range(6):
+        g = torch.randn(n, device="cuda") * (3.0 if it % 2 else 0.02)
+        for t, gg in zip(ref, torch.split(g, [t.numel() for t in ref])):
+            t.grad = gg.view_as(t).clone()
+        if clip > 0:
+            torch.nn.utils.clip_grad_norm_(ref, clip)
+        opt.step()
+        gae.opt_step(p, g, m, v, step, lr, None, None, hyper, part)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(p, torch.cat([t.detach().reshape(-1) for t in ref]), rtol=1e-5, atol=1e-7)
+    assert float(step) == 6.0
+    # a non-finite gradient: torch steps (NaN parameters follow), so does the fused pass
+    g = torch.randn(n, device="cuda")
+    g[7] = float("nan")
+    gae.opt_step(p, g, m, v, step, lr, None, None, hyper, part)
+    torch.cuda.synchronize()
+    assert float(step) == 7.0 and not bool(torch.isfinite(p).all())
+
+
+def test_fused_opt_step_scale_growth_stays_finite():
+    """GradScaler growth applies only while the grown scale is finite (torch._amp_update_scale_)."""
+    from isaacgymenv_amd.rl import gae
+    n = 64
+    p, m, v = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    step = torch.zeros((), device="cuda")
+    scale = torch.tensor(3.0e38, device="cuda")
+    s0 = float(scale)
+    tracker = torch.zeros((), dtype=torch.int32, device="cuda")
+    part = torch.empty(gae.lib().rl_opt_partials_size(), device="cuda")
+    hyper = gae.OptHyper(0.0, 0.9, 0.999, 1e-8, 0.0, 0.5, 2.0, 1)
+    gae.opt_step(p, torch.ones(n, device="cuda"), m, v, step, torch.tensor(1e-3, device="cuda"), scale, tracker, hyper,
+                 part)
+    torch.cuda.synchronize()
+    assert float(scale) == s0 and int(tracker) == 0 and float(step) == 1.0
+
+
 @pytest.mark.parametrize("units,separate,obs_dim,actions", [([512, 256, 128], True, 188, 12), ([32, 32], False, 4, 1),
                                                              ([256, 128, 64], True, 60, 8)])
 def test_act_mlp_kernel_matches_torch_network(units, separate, obs_dim, actions, monkeypatch):
