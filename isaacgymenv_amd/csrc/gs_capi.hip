@@ -451,10 +451,11 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
     const TeamEntry* te = nullptr;
     for (int i = 0; i < g_num_team_kernels; ++i)
       if (std::strcmp(g_team_kernels[i].sig, t->sig) == 0 && g_team_kernels[i].sim) te = &g_team_kernels[i];
-    // the lane team has no joint-limit rows and no mesh contacts: the one-env-per-lane kernel runs
-    if (te && (any_lim || s->dp.has_terrain)) te = nullptr;
+    // the lane team has no joint-limit rows: the one-env-per-lane kernel runs (a trimesh terrain runs the lane
+    // team's TERR form; kernel_variant 1 still selects the one-env-per-lane kernel)
+    if (te && any_lim) te = nullptr;
     if (want == 2 && !te)
-      return fail("gs_sim_set_model: no lane-team kernel for this topology / joint limits / terrain mesh");
+      return fail("gs_sim_set_model: no lane-team kernel for this topology / joint limits");
     if (te && want != 1) {
       sim_fn = te->sim;
       pd_fn = te->pd;

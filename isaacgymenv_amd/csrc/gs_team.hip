@@ -618,7 +618,26 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
   return cnt;
 }
 
-template <class T>
+// TERR (trimesh terrain): a candidate sphere at x (relative to the root origin p) against the
+// deepest of the ground plane and the terrain mesh, as the one-env-per-lane solver's TERR branch: returns the
+// distance, the contact normal and the surface friction (the plane's (0, 0, 1) and ground friction when no mesh
+// surface is nearer)
+__device__ __forceinline__ float terrain_candidate(const DevParams& P, const float* p, const float* x, float r,
+                                                   float* nrm, float& smu) {
+  const float cw[3] = {p[0] + x[0], p[1] + x[1], p[2] + x[2]};
+  float dist = P.has_ground ? cw[2] - r : 3.0e38f;
+  nrm[0] = 0.f; nrm[1] = 0.f; nrm[2] = 1.f;
+  smu = P.ground_mu;
+  float st, nt[3];
+  if (gs_terrain::sphere_contact(P.terr, cw, r, r + P.contact_offset, st, nt) && st < dist) {
+    dist = st;
+    nrm[0] = nt[0]; nrm[1] = nt[1]; nrm[2] = nt[2];
+    smu = P.terr.mu;
+  }
+  return dist;
+}
+
+template <class T, bool TERR>
 __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, const float* __restrict__ mdl,
                                              const DevParams& P, TeamState<T>& s, const float* tau,
                                              const float* __restrict__ mu_g, int N, int e, int lc,
@@ -664,6 +683,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
   SpI Ic[CL];
   bool act[CC];
   float sep[CC], cmu[CC];
+  float cnrm[TERR ? CC : 1][3];  // TERR: each chain candidate's contact normal (the force outputs)
 #pragma unroll
   for (int k = 0; k < CL; ++k) {
     const float* Rp = k == 0 ? R0 : R[k - 1];
@@ -731,10 +751,43 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         float x[3];
         mat3vec(R[k], pl, x);
         x[0] += X[k][0]; x[1] += X[k][1]; x[2] += X[k][2];
+        const int shape = T::T_RS + lc * T::T_SPC + T::T_ccs[j];
+        if constexpr (TERR) {
+          // deepest of the ground plane and the terrain mesh (gs_terrain.h), as the one-env-per-lane solver;
+          // the contact frame (n, t1, t2) replaces the plane's (z, x, y)
+          float nrm[3], smu;
+          const float dist = terrain_candidate(P, s.p, x, r, nrm, smu);
+          act[j] = dist < P.contact_offset;
+          sep[j] = dist - P.rest_offset;
+          cmu[j] = 0.5f * (mu_g[shape * N + e] + smu);
+          cnrm[j][0] = nrm[0]; cnrm[j][1] = nrm[1]; cnrm[j][2] = nrm[2];
+          if (act[j]) {
+            float dir[3][3];
+            dir[0][0] = nrm[0]; dir[0][1] = nrm[1]; dir[0][2] = nrm[2];
+            gs_terrain::tangents(nrm, dir[1], dir[2]);
+            const float xc[3] = {x[0] - r * nrm[0], x[1] - r * nrm[1], x[2] - r * nrm[2]};
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+              const float* d = dir[rr];
+              float xd[3];  // the row's angular part: d.(w x xc) = w.(xc x d)
+              cross3(xc, d, xd);
+              float* row = rows_own + RS::chain_row(j, rr) * RW;
+#pragma unroll
+              for (int b = 0; b < 6; ++b) row[RS::zslot(b) * RW] = b < 3 ? xd[b] : d[b - 3];
+#pragma unroll
+              for (int kk = 0; kk < CL; ++kk) {
+                float v = 0.f;
+                if (kk <= k)
+                  v = S[kk][3] * d[0] + S[kk][4] * d[1] + S[kk][5] * d[2] + S[kk][0] * xd[0] + S[kk][1] * xd[1] +
+                      S[kk][2] * xd[2];
+                row[RS::zslot(6 + kk) * RW] = v;
+              }
+            }
+          }
+        } else {
         const float dist = s.p[2] + x[2] - r;
         act[j] = P.has_ground && (dist < P.contact_offset);
         sep[j] = dist - P.rest_offset;
-        const int shape = T::T_RS + lc * T::T_SPC + T::T_ccs[j];
         cmu[j] = 0.5f * (mu_g[shape * N + e] + P.ground_mu);
         if (act[j]) {
           const float xc[3] = {x[0], x[1], x[2] - r};
@@ -756,6 +809,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
             }
           }
         }
+        }  // !TERR
       }
     }
   }
@@ -1002,25 +1056,47 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       rec[RS::C_MU * RW] = cmu[j];
     }
   }
-  // root candidates (replicated in every lane, own column)
+  // root candidates (replicated in every lane, own column; TERR: lane j % 4 runs root candidate j's mesh query
+  // and broadcasts its result to the team)
   bool ract[RC > 0 ? RC : 1];
+  float rnrm[TERR && RC > 0 ? RC : 1][3];
 #pragma unroll
   for (int j = 0; j < RC; ++j) {
     float x[3];
     mat3vec(R0, M->cpoint[j], x);
     const float r = M->cradius[j];
-    const float dist = s.p[2] + x[2] - r;
-    ract[j] = P.has_ground && (dist < P.contact_offset);
+    float dist, rmu_s = P.ground_mu;
+    float rdir[3][3];
+    if constexpr (TERR) {
+      float nq[3] = {0.f, 0.f, 1.f}, dq = 3.0e38f, mq = P.ground_mu;
+      if (lc == (j & (LN - 1))) dq = terrain_candidate(P, s.p, x, r, nq, mq);
+      dist = bcast(dq, j & (LN - 1));
+      rmu_s = bcast(mq, j & (LN - 1));
+#pragma unroll
+      for (int f = 0; f < 3; ++f) rnrm[j][f] = bcast(nq[f], j & (LN - 1));
+      ract[j] = dist < P.contact_offset;
+      rdir[0][0] = rnrm[j][0]; rdir[0][1] = rnrm[j][1]; rdir[0][2] = rnrm[j][2];
+      gs_terrain::tangents(rnrm[j], rdir[1], rdir[2]);
+    } else {
+      dist = s.p[2] + x[2] - r;
+      ract[j] = P.has_ground && (dist < P.contact_offset);
+    }
     if (ract[j]) {
       float* rec = rows_own + RS::root(j) * RW;
-      const float xc[3] = {x[0], x[1], x[2] - r};
+      const float xc[3] = {TERR ? x[0] - r * rdir[0][0] : x[0], TERR ? x[1] - r * rdir[0][1] : x[1],
+                           TERR ? x[2] - r * rdir[0][2] : x[2] - r};
       float zr[3][6], dir[3];
 #pragma unroll
       for (int rr = 0; rr < 3; ++rr) {
         const int ax3 = (rr == 0) ? 2 : (rr == 1 ? 0 : 1);
         float zb[6], cj = 0.f;
+        float xd[3] = {0.f, 0.f, 0.f};
+        if constexpr (TERR) cross3(xc, rdir[rr], xd);
 #pragma unroll
-        for (int b = 0; b < 6; ++b) { zb[b] = base_jac(xc, ax3, b); cj += zb[b] * nufb[b]; }
+        for (int b = 0; b < 6; ++b) {
+          zb[b] = TERR ? (b < 3 ? xd[b] : rdir[rr][b - 3]) : base_jac(xc, ax3, b);
+          cj += zb[b] * nufb[b];
+        }
 #pragma unroll
         for (int kk = 0; kk < 6; ++kk) {
           const int k = 5 - kk;
@@ -1062,7 +1138,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       const float tgt = -sc * inv_h;
       rec[RS::R_TP * RW] = (sc < 0.f ? fminf(tgt, P.max_depen_vel) : tgt) * dir[0];
       rec[RS::R_TV * RW] = (sc < 0.f ? 0.f : tgt) * dir[0];
-      rec[RS::R_MU * RW] = 0.5f * (mu_g[T::T_rcs[j] * N + e] + P.ground_mu);
+      rec[RS::R_MU * RW] = 0.5f * (mu_g[T::T_rcs[j] * N + e] + rmu_s);
     }
   }
   // self-contact pool rows: J = n.(v_A(x) - v_B(x)) has columns only on the two chains below
@@ -1385,9 +1461,17 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
             l1 = lc == c ? lamc[c][j][1] : l1;
             l2 = lc == c ? lamc[c][j][2] : l2;
           }
-          f0 += l1 * inv_h;
-          f1 += l2 * inv_h;
-          f2 += l0 * inv_h;
+          if constexpr (TERR) {  // f = (l0 n + l1 t1 + l2 t2) / h in the candidate's mesh frame
+            float t1[3], t2[3];
+            gs_terrain::tangents(cnrm[j], t1, t2);
+            f0 += (l0 * cnrm[j][0] + l1 * t1[0] + l2 * t2[0]) * inv_h;
+            f1 += (l0 * cnrm[j][1] + l1 * t1[1] + l2 * t2[1]) * inv_h;
+            f2 += (l0 * cnrm[j][2] + l1 * t1[2] + l2 * t2[2]) * inv_h;
+          } else {
+            f0 += l1 * inv_h;
+            f1 += l2 * inv_h;
+            f2 += l0 * inv_h;
+          }
         }
       }
       if constexpr (T::NPK > 0) {  // self-contacts: +f on body A, -f on body B
@@ -1416,9 +1500,18 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       float f0 = 0.f, f1 = 0.f, f2 = 0.f;
 #pragma unroll
       for (int j = 0; j < RC; ++j) {
-        f0 += lamr[j][1] * inv_h;
-        f1 += lamr[j][2] * inv_h;
-        f2 += lamr[j][0] * inv_h;
+        if constexpr (TERR) {
+          float t1[3], t2[3];
+          gs_terrain::tangents(rnrm[j], t1, t2);
+          const float g = ract[j] ? inv_h : 0.f;
+          f0 += (lamr[j][0] * rnrm[j][0] + lamr[j][1] * t1[0] + lamr[j][2] * t2[0]) * g;
+          f1 += (lamr[j][0] * rnrm[j][1] + lamr[j][1] * t1[1] + lamr[j][2] * t2[1]) * g;
+          f2 += (lamr[j][0] * rnrm[j][2] + lamr[j][1] * t1[2] + lamr[j][2] * t2[2]) * g;
+        } else {
+          f0 += lamr[j][1] * inv_h;
+          f1 += lamr[j][2] * inv_h;
+          f2 += lamr[j][0] * inv_h;
+        }
       }
       if constexpr (T::NPK > 0) {
         for (int p = 0; p < npc; ++p) {
@@ -1464,7 +1557,7 @@ __device__ __forceinline__ int xcd_block(int b, int G) {
   return x * per + (x < rem ? x : rem) + q;
 }
 
-template <class T>
+template <class T, bool TERR>
 __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel* __restrict__ M, DevParams P,
                                                                  SimBuffers B, const float* __restrict__ tau_aos) {
   constexpr int LN = T::T_LANES, CL = T::T_CL, ND = T::ND;
@@ -1489,13 +1582,13 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel*
   GS_PROF_DECL
   for (int sstep = 0; sstep < P.substeps; ++sstep) {
     const bool last = (sstep == P.substeps - 1) && P.collect;
-    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, nullptr, shw_tab, sct GS_PROF_ARGS);
+    substep_team<T, TERR>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, nullptr, shw_tab, sct GS_PROF_ARGS);
   }
   team_store<T>(B.state, N, e, lc, s);
   GS_PROF_FLUSH
 }
 
-template <class T>
+template <class T, bool TERR>
 __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* __restrict__ M, DevParams P,
                                                                 SimBuffers B, PdDev A) {
   constexpr int LN = T::T_LANES, CL = T::T_CL, ND = T::ND, NB = T::NB;
@@ -1534,7 +1627,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
     const bool last = ((it % sub) == sub - 1) && P.collect;
     GS_PROF(6)  // PD torque
     float* cf_aos = (it == total - 1) ? A.cf_out : nullptr;
-    substep_team<T>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, cf_aos, shw_tab, sct GS_PROF_ARGS);
+    substep_team<T, TERR>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, cf_aos, shw_tab, sct GS_PROF_ARGS);
     if (it == n_pd - 1 && A.dof_out) {
 #pragma unroll
       for (int k = 0; k < CL; ++k) {
@@ -1572,7 +1665,10 @@ hipError_t launch_sim_team(const DevModel* M, const DevParams& P, const SimBuffe
     static_assert(T::NR == T::NB, "the lane team reports contact forces per body (no kept fixed-joint links)");
     const long lanes = (long)B.N * T::T_LANES;
     const int blocks = (int)((lanes + kTeamBlock - 1) / kTeamBlock);
-    hipLaunchKernelGGL(k_simulate_team<T>, dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, tau);
+    if (P.has_terrain)  // trimesh terrain: mesh queries by the candidates' owner lanes
+      hipLaunchKernelGGL((k_simulate_team<T, true>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, tau);
+    else
+      hipLaunchKernelGGL((k_simulate_team<T, false>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, tau);
     return hipGetLastError();
   } else {
     return hipErrorInvalidConfiguration;
@@ -1583,7 +1679,10 @@ hipError_t launch_pd_team(const DevModel* M, const DevParams& P, const SimBuffer
   if constexpr (T::HAS_TEAM) {
     const long lanes = (long)B.N * T::T_LANES;
     const int blocks = (int)((lanes + kTeamBlock - 1) / kTeamBlock);
-    hipLaunchKernelGGL(k_pd_step_team<T>, dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, A);
+    if (P.has_terrain)
+      hipLaunchKernelGGL((k_pd_step_team<T, true>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, A);
+    else
+      hipLaunchKernelGGL((k_pd_step_team<T, false>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, A);
     return hipGetLastError();
   } else {
     return hipErrorInvalidConfiguration;

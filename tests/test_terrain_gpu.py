@@ -23,12 +23,16 @@ def _terrain_states(n, ter, seed):
     return root, dof, tau, mu
 
 
-def _gpu_vs_oracle(ter, n, seed, steps):
+KERNELS = {"lane": 1, "team": 2}
+
+
+def _gpu_vs_oracle(ter, n, seed, steps, kernel="team"):
     art, flat = H.anymal()
     params = dict(H.ANYMAL_PARAMS, has_ground=0)
     root, dof, tau, mu = _terrain_states(n, ter, seed)
     gym, sim = H.make_gpu_sim("anymal", n, params, terrain=ter)
-    assert sim.kernel_variant == 1  # mesh contacts run in the one-env-per-lane kernel
+    # mesh contacts: the lane team's TERR form (default) or the wave-assisted one-env-per-lane kernel
+    assert sim.kernel_variant == KERNELS[kernel]
     H.load_state_into(sim, root, dof, mu)
     sim.dof_force.copy_(torch.from_numpy(tau.astype(np.float32).reshape(-1)))
     osim = OracleSim(flat, params, terrain=ter["oracle"])
@@ -43,10 +47,12 @@ def _gpu_vs_oracle(ter, n, seed, steps):
     return g_root, g_dof, g_cf, r, d, cf
 
 
-def test_rough_terrain_one_simulate_matches_oracle():
+@pytest.mark.parametrize("kernel", sorted(KERNELS))
+def test_rough_terrain_one_simulate_matches_oracle(kernel, monkeypatch):
+    monkeypatch.setenv("GS_PHYSICS_KERNEL", kernel)
     ter = H.rough_terrain(seed=5)
     n = 512
-    g_root, g_dof, g_cf, r, d, cf = _gpu_vs_oracle(ter, n, seed=2, steps=1)
+    g_root, g_dof, g_cf, r, d, cf = _gpu_vs_oracle(ter, n, seed=2, steps=1, kernel=kernel)
     assert np.abs(cf).sum(axis=(1, 2)).astype(bool).mean() > 0.5, "most envs must touch the mesh"
     assert np.all(np.isfinite(g_root)) and np.all(np.isfinite(g_dof))
     # contact activity / closest-triangle choices can switch on a last-bit difference (stair edges): such an
@@ -60,12 +66,14 @@ def test_rough_terrain_one_simulate_matches_oracle():
         rr, dd, c, _ = H.oracle_run(flat, params, rr, dd, tau[idx], mu[idx], bits, nc=flat["nb"], terrain=ter["oracle"])
         return H.state_fields(rr, dd, c)
     H.assert_close_or_explained(H.state_fields(g_root, g_dof, g_cf), H.state_fields(r, d, cf), rerun,
-                                what="rough terrain gpu")
+                                what=f"rough terrain gpu ({kernel} kernel)")
 
 
-def test_flat_mesh_gpu_equals_plane_gpu(monkeypatch):
-    """A flat mesh at z = 0 and the ground plane give the same step on the GPU too (frames, rows)."""
-    monkeypatch.setenv("GS_PHYSICS_KERNEL", "lane")
+@pytest.mark.parametrize("kernel", sorted(KERNELS))
+def test_flat_mesh_gpu_equals_plane_gpu(kernel, monkeypatch):
+    """A flat mesh at z = 0 and the ground plane give the same step on the GPU too (frames, rows), in both kernel
+    forms."""
+    monkeypatch.setenv("GS_PHYSICS_KERNEL", kernel)
     from isaacgymenv_amd.isaacgym.terrain_utils import convert_heightfield_to_trimesh
     hf = np.zeros((121, 121), np.int16)
     ter = H.terrain_from_heights(hf, shift=(-6.0, -6.0, 0.0))
@@ -92,7 +100,8 @@ def test_flat_mesh_gpu_equals_plane_gpu(monkeypatch):
         r[idx], d[idx] = H.perturbed(root, dof, idx, rng)
         return {k: v[idx] for k, v in run("plane", r, d).items()}
     tol = {"pose": (1e-4, 1e-4), "vel": (1e-4, 1e-4), "q": (1e-3, 1e-3), "qd": (1e-3, 1e-3), "cf": (1.0, 1e-2)}
-    H.assert_close_or_explained(mesh, plane, rerun, tol=tol, max_env_frac=5e-3, what="flat mesh vs plane (3 substeps)")
+    H.assert_close_or_explained(mesh, plane, rerun, tol=tol, max_env_frac=5e-3,
+                                what=f"flat mesh vs plane (3 substeps, {kernel} kernel)")
 
 
 def test_anymal_trimesh_task_runs(monkeypatch):
@@ -105,7 +114,7 @@ def test_anymal_trimesh_task_runs(monkeypatch):
                             headless=True, force_render=False,
                             overrides=["task.env.terrain.terrainType=trimesh", "task.env.terrain.numLevels=4",
                                        "task.env.terrain.numTerrains=8"])
-    assert env.custom_origins and env.sim.kernel_variant == 1
+    assert env.custom_origins and env.sim.kernel_variant == 2  # the lane team's TERR form
     gen = torch.Generator(device="cuda:0").manual_seed(3)
     falls = 0
     for t in range(300):
