@@ -89,7 +89,7 @@ struct gs_sim {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   float4* d_tverts = nullptr;     // terrain mesh (gs_terrain.h)
-  uint2* d_tcells = nullptr;
+  uint4* d_tcells = nullptr;
   float* d_rows = nullptr;        // contact-row tiles of the GLOBAL-row kernels (TopoEntry::row_floats)
   size_t rows_cap = 0;            // floats allocated
   // host backend (device < 0)
@@ -98,7 +98,7 @@ struct gs_sim {
   const HostTopoEntry* htopo = nullptr;
   DevLinks h_links{};
   std::vector<float4> h_tverts;
-  std::vector<uint2> h_tcells;
+  std::vector<uint4> h_tcells;
   double host_ms = -1.0;          // wall time of the last simulate / pd_step (timing enabled)
   const DevModel* model() const { return host ? &h_model : d_model; }
   const DevLinks* links() const { return host ? &h_links : d_links; }
@@ -234,13 +234,14 @@ int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_verti
       hv[(size_t)(i * cols + j)] = make_float4((float)(v[0] + tx), (float)(v[1] + ty), (float)(v[2] + tz), 0.f);
     }
   }
-  std::vector<uint2> hc((size_t)((rows - 1) * (cols - 1)));
+  std::vector<uint4> hc((size_t)((rows - 1) * (cols - 1)));
   for (int64_t i = 0; i + 1 < rows; ++i) {
     for (int64_t j = 0; j + 1 < cols; ++j) {
       const float4 q[4] = {hv[i * cols + j], hv[i * cols + j + 1], hv[(i + 1) * cols + j], hv[(i + 1) * cols + j + 1]};
-      float zmax = q[0].z, xmin = q[0].x, xmax = q[0].x, ymin = q[0].y, ymax = q[0].y;
+      float zmax = q[0].z, zmin = q[0].z, xmin = q[0].x, xmax = q[0].x, ymin = q[0].y, ymax = q[0].y;
       for (int k = 1; k < 4; ++k) {
         zmax = std::max(zmax, q[k].z);
+        zmin = std::min(zmin, q[k].z);
         xmin = std::min(xmin, q[k].x); xmax = std::max(xmax, q[k].x);
         ymin = std::min(ymin, q[k].y); ymax = std::max(ymax, q[k].y);
       }
@@ -250,9 +251,10 @@ int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_verti
       if (xmax > cx0 + 1.25 * hs) f |= TCELL_XHI;
       if (ymin < cy0 - 0.25 * hs) f |= TCELL_YLO;
       if (ymax > cy0 + 1.25 * hs) f |= TCELL_YHI;
-      uint32_t zb;
+      uint32_t zb, zl;
       std::memcpy(&zb, &zmax, 4);
-      hc[(size_t)(i * (cols - 1) + j)] = make_uint2(zb, f);
+      std::memcpy(&zl, &zmin, 4);
+      hc[(size_t)(i * (cols - 1) + j)] = make_uint4(zb, f, zl, 0u);
     }
   }
   TerrainDev& T = s->dp.terr;
@@ -263,12 +265,12 @@ int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_verti
     T.cell = s->h_tcells.data();
   } else {
     float4* dv = nullptr;
-    uint2* dc = nullptr;
+    uint4* dc = nullptr;
     hipError_t e = hipSetDevice(s->device);
     if (e == hipSuccess) e = hipMalloc(&dv, hv.size() * sizeof(float4));
-    if (e == hipSuccess) e = hipMalloc(&dc, hc.size() * sizeof(uint2));
+    if (e == hipSuccess) e = hipMalloc(&dc, hc.size() * sizeof(uint4));
     if (e == hipSuccess) e = hipMemcpy(dv, hv.data(), hv.size() * sizeof(float4), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dc, hc.data(), hc.size() * sizeof(uint2), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dc, hc.data(), hc.size() * sizeof(uint4), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
       if (dv) (void)hipFree(dv);
       if (dc) (void)hipFree(dc);

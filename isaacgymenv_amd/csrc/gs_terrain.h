@@ -15,13 +15,17 @@
 //     * q on an edge or vertex: only from the front side (nf.(c - a) >= 0), normal = (c - q)/|c - q|,
 //       separation = |c - q| - r;
 //   the candidate keeps the surface of the triangle CLOSEST to its centre (|sd| for a face, |c - q|
-//   otherwise), first found on ties, scanning cells in (i, j) order and the two triangles of a
-//   cell in the order above (a foot pushed into a stair riser below the tread's edge is pushed
-//   back out of the riser, not lifted onto the tread, unless the tread is nearer).
+//   otherwise), first found on ties, visiting first the cell under the centre, then every cell in
+//   (i, j) order, the two triangles of a cell in the order above (a foot pushed into a stair riser
+//   below the tread's edge is pushed back out of the riser, not lifted onto the tread, unless the
+//   tread is nearer).
 // Cells are culled by their top height (a centre more than thr above every vertex of a cell
-// cannot touch it from the front nor lie behind one of its faces) and by their (move-extended)
-// footprint widened by the horizontal reach max(thr, r + TERRAIN_BACK); both tests are
-// conservative, so the result is that of a full scan.
+// cannot touch it from the front nor lie behind one of its faces), by their (move-extended)
+// footprint widened by the horizontal reach max(thr, r + TERRAIN_BACK), and -- once a surface is
+// found -- by their bounding box: a triangle's key is its distance to the centre, at least the box's,
+// so a cell whose box lies no nearer than the best key cannot win (strict < updates).  All three
+// tests are conservative, so the result is that of a full scan in the visiting order; on flat ground
+// the box test leaves the 1-4 cells around the centre of the 25-36 in the window.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -37,7 +41,8 @@
 
 struct TerrainDev {
   const float4* v;     // [rows*cols] world xyz (transform applied), w unused
-  const uint2* cell;   // [(rows-1)*(cols-1)]: x = top height (float bits), y = footprint flags
+  const uint4* cell;   // [(rows-1)*(cols-1)]: x = top height (float bits), y = footprint flags,
+                       // z = bottom height (float bits), w unused
   int rows, cols;
   float x0, y0, hs, inv_hs;
   float mu;            // static friction of the mesh
@@ -149,22 +154,31 @@ GS_HD bool sphere_contact(const TerrainDev& T, const float* p, float r, float th
   const int j0 = gs_imax((int)floorf(gy - gt) - 1, 0), j1 = gs_imin((int)floorf(gy + gt) + 1, T.cols - 2);
   float best = 3.0e38f, bkey = 3.0e38f;
   const float zlo = p[2] - thr;
-  for (int i = i0; i <= i1; ++i) {
-    const float cx0 = T.x0 + (float)i * T.hs;
-    for (int j = j0; j <= j1; ++j) {
-      const uint2 cinfo = T.cell[(size_t)i * (T.cols - 1) + j];
-      if (zlo > gs_bits_float(cinfo.x)) continue;
-      const uint32_t f = cinfo.y;
-      const float cy0 = T.y0 + (float)j * T.hs;
-      const float bx0 = cx0 - ((f & TCELL_XLO) ? T.hs : 0.f), bx1 = cx0 + ((f & TCELL_XHI) ? 2.f : 1.f) * T.hs;
-      const float by0 = cy0 - ((f & TCELL_YLO) ? T.hs : 0.f), by1 = cy0 + ((f & TCELL_YHI) ? 2.f : 1.f) * T.hs;
-      if (p[0] + reach < bx0 || p[0] - reach > bx1 || p[1] + reach < by0 || p[1] - reach > by1) continue;
-      const size_t v0 = (size_t)i * T.cols + j;
-      const float4 v00 = T.v[v0], v01 = T.v[v0 + 1], v10 = T.v[v0 + T.cols], v11 = T.v[v0 + T.cols + 1];
-      triangle(p, r, thr, v00, v11, v01, bkey, best, n);
-      triangle(p, r, thr, v00, v10, v11, bkey, best, n);
-    }
-  }
+  const float pad = 1e-4f * T.hs;  // (the footprint box is exact up to the coordinates' rounding)
+  auto visit = [&](int i, int j) {
+    const uint4 cinfo = T.cell[(size_t)i * (T.cols - 1) + j];
+    const float top = gs_bits_float(cinfo.x);
+    if (zlo > top) return;
+    const uint32_t f = cinfo.y;
+    const float cx0 = T.x0 + (float)i * T.hs, cy0 = T.y0 + (float)j * T.hs;
+    const float bx0 = cx0 - ((f & TCELL_XLO) ? T.hs : 0.f), bx1 = cx0 + ((f & TCELL_XHI) ? 2.f : 1.f) * T.hs;
+    const float by0 = cy0 - ((f & TCELL_YLO) ? T.hs : 0.f), by1 = cy0 + ((f & TCELL_YHI) ? 2.f : 1.f) * T.hs;
+    if (p[0] + reach < bx0 || p[0] - reach > bx1 || p[1] + reach < by0 || p[1] - reach > by1) return;
+    const float dx = fmaxf(fmaxf(bx0 - pad - p[0], p[0] - bx1 - pad), 0.f);
+    const float dy = fmaxf(fmaxf(by0 - pad - p[1], p[1] - by1 - pad), 0.f);
+    const float dz = fmaxf(fmaxf(gs_bits_float(cinfo.z) - pad - p[2], p[2] - top - pad), 0.f);
+    if (dx * dx + dy * dy + dz * dz >= bkey * bkey) return;
+    const size_t v0 = (size_t)i * T.cols + j;
+    const float4 v00 = T.v[v0], v01 = T.v[v0 + 1], v10 = T.v[v0 + T.cols], v11 = T.v[v0 + T.cols + 1];
+    triangle(p, r, thr, v00, v11, v01, bkey, best, n);
+    triangle(p, r, thr, v00, v10, v11, bkey, best, n);
+  };
+  const int ic = (int)floorf(gx), jc = (int)floorf(gy);
+  const bool centre = ic >= 0 && ic <= T.rows - 2 && jc >= 0 && jc <= T.cols - 2;
+  if (centre) visit(ic, jc);
+  for (int i = i0; i <= i1; ++i)
+    for (int j = j0; j <= j1; ++j)
+      if (!(centre && i == ic && j == jc)) visit(i, j);
   if (best >= thr - r) return false;
   sep = best;
   return true;

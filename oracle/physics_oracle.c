@@ -163,8 +163,8 @@ static void quat_to_mat(const real *q, real *R) { /* xyzw */
  * normal (also from behind, up to r + TERRAIN_BACK); otherwise the nearest point of the three
  * edges, from the front side only; triangles facing down (n_z < TERRAIN_DOWN_NZ, inverted by the
  * slope-threshold vertex moves) are skipped.  The triangle CLOSEST to the centre gives the contact (first
- * found on ties).  Full scan of a window 3 cells wider than any triangle of a grid cell can reach
- * (vertices move at most one cell). */
+ * found on ties, visiting the cell under the centre first, then every cell in (i, j) order).  Full scan of a
+ * window 3 cells wider than any triangle of a grid cell can reach (vertices move at most one cell). */
 #define TERRAIN_BACK 0.1
 #define TERRAIN_DOWN_NZ (-0.5) /* downward-facing (inverted) triangles generate no contact */
 static void seg_closest(const real *p, const real *a, const real *b, real *q) {
@@ -222,10 +222,13 @@ static int terrain_query(const OParams *pp, const real *p, real r, real thr, rea
     const real reach = thr > r + TERRAIN_BACK ? thr : r + TERRAIN_BACK;
     const int w = (int)ceil(reach / hs) + 3;
     real bkey = 1e300, best = 1e300;
-    for (int i = gi - w; i <= gi + w; ++i) {
+    const int centre = gi >= 0 && gi <= pp->trows - 2 && gj >= 0 && gj <= pp->tcols - 2;
+    for (int pass = centre ? 0 : 1; pass < 2; ++pass)
+    for (int i = pass ? gi - w : gi; i <= (pass ? gi + w : gi); ++i) {
         if (i < 0 || i > pp->trows - 2) continue;
-        for (int j = gj - w; j <= gj + w; ++j) {
+        for (int j = pass ? gj - w : gj; j <= (pass ? gj + w : gj); ++j) {
             if (j < 0 || j > pp->tcols - 2) continue;
+            if (pass && centre && i == gi && j == gj) continue;
             real v[4][3];
             const int64_t id[4] = {(int64_t)i * pp->tcols + j, (int64_t)i * pp->tcols + j + 1,
                                    (int64_t)(i + 1) * pp->tcols + j, (int64_t)(i + 1) * pp->tcols + j + 1};
