@@ -640,7 +640,7 @@ __device__ __forceinline__ float terrain_candidate(const DevParams& P, const flo
 template <class T, bool TERR>
 __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, const float* __restrict__ mdl,
                                              const DevParams& P, TeamState<T>& s, const float* tau,
-                                             const float* __restrict__ mu_g, int N, int e, int lc,
+                                             const float* __restrict__ mu_t, int N, int e, int lc,
                                              float* __restrict__ rows_own, const float* __restrict__ rows_team,
                                              float* __restrict__ cf_soa, bool collect,
                                              float* __restrict__ cf_aos, float* __restrict__ shw_tab,
@@ -759,7 +759,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
           const float dist = terrain_candidate(P, s.p, x, r, nrm, smu);
           act[j] = dist < P.contact_offset;
           sep[j] = dist - P.rest_offset;
-          cmu[j] = 0.5f * (mu_g[shape * N + e] + smu);
+          cmu[j] = 0.5f * (mu_t[shape * kTeamsPerBlock] + smu);
           cnrm[j][0] = nrm[0]; cnrm[j][1] = nrm[1]; cnrm[j][2] = nrm[2];
           if (act[j]) {
             float dir[3][3];
@@ -788,7 +788,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         const float dist = s.p[2] + x[2] - r;
         act[j] = P.has_ground && (dist < P.contact_offset);
         sep[j] = dist - P.rest_offset;
-        cmu[j] = 0.5f * (mu_g[shape * N + e] + P.ground_mu);
+        cmu[j] = 0.5f * (mu_t[shape * kTeamsPerBlock] + P.ground_mu);
         if (act[j]) {
           const float xc[3] = {x[0], x[1], x[2] - r};
 #pragma unroll
@@ -819,7 +819,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
   int npc = 0;
   float* pool = rows_own + RS::POOL * RW;
   if constexpr (T::NPK > 0) {
-    if (P.self_collide) npc = team_self_contacts<T>(M, cm, P, mu_g, N, e, lc, R0, R, X, shw_tab, sct, pool);
+    if (P.self_collide) npc = team_self_contacts<T>(M, cm, P, mu_t, kTeamsPerBlock, 0, lc, R0, R, X, shw_tab, sct, pool);
   }
   GS_PROF(11)  // self-collision prepass
   // ================= chain backward pass: composite inertia / force, bias, chain rows of M
@@ -1138,7 +1138,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       const float tgt = -sc * inv_h;
       rec[RS::R_TP * RW] = (sc < 0.f ? fminf(tgt, P.max_depen_vel) : tgt) * dir[0];
       rec[RS::R_TV * RW] = (sc < 0.f ? 0.f : tgt) * dir[0];
-      rec[RS::R_MU * RW] = 0.5f * (mu_g[T::T_rcs[j] * N + e] + rmu_s);
+      rec[RS::R_MU * RW] = 0.5f * (mu_t[T::T_rcs[j] * kTeamsPerBlock] + rmu_s);
     }
   }
   // self-contact pool rows: J = n.(v_A(x) - v_B(x)) has columns only on the two chains below
@@ -1565,12 +1565,18 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel*
   __shared__ float rows[RowSlots<T>::TOTAL * RW];
   __shared__ float shw_tab[T::NPK > 0 ? kShW * T::NS * kTeamsPerBlock : 1];
   __shared__ float sct[ShapeTab<T>::SIZE];
+  // the team's shape friction (constant over the launch), read by the contact records and the self-contact pool
+  // from LDS instead of device memory every substep: [shape][team]
+  __shared__ float mu_tab[T::NS * kTeamsPerBlock];
   stage_chain_model<T>(M, mdl);
   stage_shape_consts<T>(M, sct);
-  __syncthreads();
   const int lc = threadIdx.x & (LN - 1);
   const int e = (xcd_block(blockIdx.x, gridDim.x) * kTeamBlock + threadIdx.x) / LN;
+  for (int sh = lc; sh < T::NS; sh += LN)
+    mu_tab[sh * kTeamsPerBlock + (threadIdx.x >> 2)] = e < B.N ? B.mu[(size_t)sh * B.N + e] : 1.f;
+  __syncthreads();
   if (e >= B.N) return;
+  const float* mu_t = mu_tab + (threadIdx.x >> 2);
   const int N = B.N;
   TeamState<T> s;
   team_load<T>(B.state, N, e, lc, s);
@@ -1582,7 +1588,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel*
   GS_PROF_DECL
   for (int sstep = 0; sstep < P.substeps; ++sstep) {
     const bool last = (sstep == P.substeps - 1) && P.collect;
-    substep_team<T, TERR>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, nullptr, shw_tab, sct GS_PROF_ARGS);
+    substep_team<T, TERR>(M, mdl, P, s, tau, mu_t, N, e, lc, own, team, B.cf, last, nullptr, shw_tab, sct GS_PROF_ARGS);
   }
   team_store<T>(B.state, N, e, lc, s);
   GS_PROF_FLUSH
@@ -1596,12 +1602,18 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
   __shared__ float rows[RowSlots<T>::TOTAL * RW];
   __shared__ float shw_tab[T::NPK > 0 ? kShW * T::NS * kTeamsPerBlock : 1];
   __shared__ float sct[ShapeTab<T>::SIZE];
+  // the team's shape friction (constant over the launch), read by the contact records and the self-contact pool
+  // from LDS instead of device memory every substep: [shape][team]
+  __shared__ float mu_tab[T::NS * kTeamsPerBlock];
   stage_chain_model<T>(M, mdl);
   stage_shape_consts<T>(M, sct);
-  __syncthreads();
   const int lc = threadIdx.x & (LN - 1);
   const int e = (xcd_block(blockIdx.x, gridDim.x) * kTeamBlock + threadIdx.x) / LN;
+  for (int sh = lc; sh < T::NS; sh += LN)
+    mu_tab[sh * kTeamsPerBlock + (threadIdx.x >> 2)] = e < B.N ? B.mu[(size_t)sh * B.N + e] : 1.f;
+  __syncthreads();
   if (e >= B.N) return;
+  const float* mu_t = mu_tab + (threadIdx.x >> 2);
   const int N = B.N;
   TeamState<T> s;
   team_load<T>(B.state, N, e, lc, s);
@@ -1627,7 +1639,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
     const bool last = ((it % sub) == sub - 1) && P.collect;
     GS_PROF(6)  // PD torque
     float* cf_aos = (it == total - 1) ? A.cf_out : nullptr;
-    substep_team<T, TERR>(M, mdl, P, s, tau, B.mu, N, e, lc, own, team, B.cf, last, cf_aos, shw_tab, sct GS_PROF_ARGS);
+    substep_team<T, TERR>(M, mdl, P, s, tau, mu_t, N, e, lc, own, team, B.cf, last, cf_aos, shw_tab, sct GS_PROF_ARGS);
     if (it == n_pd - 1 && A.dof_out) {
 #pragma unroll
       for (int k = 0; k < CL; ++k) {

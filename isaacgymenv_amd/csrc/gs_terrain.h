@@ -154,9 +154,9 @@ GS_HD bool sphere_contact(const TerrainDev& T, const float* p, float r, float th
   const int j0 = gs_imax((int)floorf(gy - gt) - 1, 0), j1 = gs_imin((int)floorf(gy + gt) + 1, T.cols - 2);
   float best = 3.0e38f, bkey = 3.0e38f;
   const float zlo = p[2] - thr;
-  const float pad = 1e-4f * T.hs;  // (the footprint box is exact up to the coordinates' rounding)
-  auto visit = [&](int i, int j) {
-    const uint4 cinfo = T.cell[(size_t)i * (T.cols - 1) + j];
+  const float pad = 1e-4f * T.hs;
+  // one cell given its info word: the culling tests, then its two triangles
+  auto cell = [&](int i, int j, const uint4& cinfo) {
     const float top = gs_bits_float(cinfo.x);
     if (zlo > top) return;
     const uint32_t f = cinfo.y;
@@ -175,10 +175,23 @@ GS_HD bool sphere_contact(const TerrainDev& T, const float* p, float r, float th
   };
   const int ic = (int)floorf(gx), jc = (int)floorf(gy);
   const bool centre = ic >= 0 && ic <= T.rows - 2 && jc >= 0 && jc <= T.cols - 2;
-  if (centre) visit(ic, jc);
-  for (int i = i0; i <= i1; ++i)
-    for (int j = j0; j <= j1; ++j)
-      if (!(centre && i == ic && j == jc)) visit(i, j);
+  if (centre) cell(ic, jc, T.cell[(size_t)ic * (T.cols - 1) + jc]);
+  // the rest in (i, j) order; a row's cell words are loaded together before any is tested (one load latency
+  // per row instead of one per cell: the scan is a chain of dependent loads otherwise)
+  constexpr int kRowBatch = 8;
+  for (int i = i0; i <= i1; ++i) {
+    const uint4* crow = T.cell + (size_t)i * (T.cols - 1);
+    for (int jb = j0; jb <= j1; jb += kRowBatch) {
+      uint4 cw[kRowBatch];
+#pragma unroll
+      for (int k = 0; k < kRowBatch; ++k) cw[k] = crow[jb + k <= j1 ? jb + k : j1];
+#pragma unroll
+      for (int k = 0; k < kRowBatch; ++k) {
+        const int j = jb + k;
+        if (j <= j1 && !(centre && i == ic && j == jc)) cell(i, j, cw[k]);
+      }
+    }
+  }
   if (best >= thr - r) return false;
   sep = best;
   return true;

@@ -25,13 +25,15 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--num-envs", type=int, default=4096)
+    ap.add_argument("--trimesh", action="store_true", help="terrainType=trimesh (the lane team's TERR form)")
     a = ap.parse_args()
     import torch
     import isaacgymenvs
     from isaacgymenv_amd.isaacgym import _lib
     L = _lib.lib()
     env = isaacgymenvs.make(seed=42, task="AnymalTerrain", num_envs=a.num_envs, sim_device="cuda:0",
-                            rl_device="cuda:0", headless=True, force_render=False)
+                            rl_device="cuda:0", headless=True, force_render=False,
+                            overrides=["task.env.terrain.terrainType=trimesh"] if a.trimesh else [])
     N, A = env.num_envs, env.num_actions
     pool = torch.empty((64, N, A), device="cuda:0").uniform_(-1, 1)
     for i in range(a.warmup):
