@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 4
+#define RL_ABI_VERSION 5
 
 int rl_abi_version(void);
 const char *rl_last_error(void);
@@ -137,7 +137,7 @@ int rl_rollout_post(const float *rewards, const void *dones, int32_t dones_bytes
                     void *stream);
 
 /*
- * ABI 4 -- the act-forward MLP (rl_act_mlp, below) and the minibatch optimizer step over the learner's flat buffers (rl_games a2c_common.py
+ * ABI 4 -- the minibatch optimizer step over the learner's flat buffers (rl_games a2c_common.py
  * trancate_gradients_and_step: scaler.unscale_, clip_grad_norm_, scaler.step(Adam), scaler.update):
  *   g = grad / scale (scale null: 1, no skipping, no update); found_inf = any non-finite g;
  *   unless found_inf: g *= min(1, max_norm / (||g|| + 1e-6)) when max_norm > 0; g += weight_decay * p;
@@ -161,27 +161,24 @@ int rl_opt_step(float *param, const float *grad, float *exp_avg, float *exp_avg_
 int rl_opt_partials_size(void);
 
 /*
- * The act forward of the actor-critic MLP as one kernel (rl_games ModelA2CContinuousLogStd eval forward of a
- * fixed-sigma model: running_mean_std input normalisation -- running_mean / running_var [obs_dim] float64, both
- * null for none -- then the actor MLP of Linear + ELU layers, the critic MLP when `critic` is not null (separate:
- * True; null = shared trunk), mu = Linear(actor trunk) [rows][num_actions] and value = Linear(critic trunk)
- * [rows] (the normalised value: rl_policy_head unnormalises it).  Layer l: weight [dims[l+1]][dims[l]] and bias
- * [dims[l+1]] f32 (nn.Linear layout); widths multiples of 4 up to 512; f32 arithmetic.  Two launches.
+ * ABI 5 -- the hidden Linear + ELU layers of the actor / critic MLPs on the matrix cores (rl_linear.hip; rl_games
+ * network_builder.py A2CBuilder mlp, trained under fp16 autocast: AnymalTerrainPPO.yaml mixed_precision).  fp16
+ * operands, f32 accumulation (v_mfma_f32_32x32x16_f16).  The act-forward MLP kernel of ABI 4 (rl_act_mlp: f32 FMA
+ * chains on L2-resident weights, slower than the library GEMMs it replaced) is gone.
+ *
+ * rl_linear_fwd: y [M][N] fp16 = act(x [M][K] (row stride ldx) . w[N][K]^T + bias [N] fp16 (null: none)), act 1 =
+ *   ELU (alpha 1), 0 = none.  M % 64 == 0, N % 128 == 0, K and ldx % 4 == 0, 8-byte aligned rows.
+ * rl_linear_transpose: w [N][K] fp16 -> wt [K][N] fp16.
+ * rl_linear_bwd: the backward of rl_linear_fwd with ELU from its output y: dZ = dy * (y > 0 ? 1 : y + 1);
+ *   dx [M][K] fp16 = dZ . w (from wt = w^T; null dx: skipped; needs K % 128 == 0);
+ *   wpart [splits][N][K] f32 = per row block of M / splits rows, dZ^T . x; bpart [splits][N] f32 = column sums of
+ *   dZ (null: skipped).  Finish with rl_splitk_accum (fixed order).  M % 128 == 0, M % (32 splits) == 0.
  */
-#define RL_MLP_MAX_LAYERS 4
-typedef struct rl_mlp {
-    int32_t num_layers;
-    int32_t dims[RL_MLP_MAX_LAYERS + 1];
-    const float *weight[RL_MLP_MAX_LAYERS];
-    const float *bias[RL_MLP_MAX_LAYERS];
-} rl_mlp;
-
-int rl_act_mlp(const float *obs, int32_t num_rows, int32_t obs_dim, const double *running_mean,
-               const double *running_var, double epsilon, const rl_mlp *actor, const rl_mlp *critic,
-               const float *mu_w, const float *mu_b, int32_t num_actions, const float *value_w, const float *value_b,
-               float *mu_out, float *value_out, float *workspace, void *stream);
-/* f32 scratch rl_act_mlp needs (the hidden layers' weights transposed, refreshed by every call) */
-int rl_act_mlp_workspace_floats(const rl_mlp *actor, const rl_mlp *critic);
+int rl_linear_fwd(const void *x, int32_t M, int32_t K, int32_t ldx, const void *w, int32_t N, const void *bias,
+                  int32_t act, void *y, void *stream);
+int rl_linear_transpose(const void *w, int32_t N, int32_t K, void *wt, void *stream);
+int rl_linear_bwd(const void *dy, const void *y, int32_t M, int32_t N, const void *x, int32_t K, int32_t ldx,
+                  const void *wt, void *dx, int32_t splits, float *wpart, float *bpart, void *stream);
 
 #ifdef __cplusplus
 }

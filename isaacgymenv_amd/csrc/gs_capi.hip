@@ -90,6 +90,7 @@ struct gs_sim {
   bool timed = false;
   float4* d_tverts = nullptr;     // terrain mesh (gs_terrain.h)
   uint4* d_tcells = nullptr;
+  float* d_tblk = nullptr;        // highest cell top per TERRAIN_BLK x TERRAIN_BLK block of cells
   float* d_rows = nullptr;        // contact-row tiles of the GLOBAL-row kernels (TopoEntry::row_floats)
   size_t rows_cap = 0;            // floats allocated
   // host backend (device < 0)
@@ -99,6 +100,7 @@ struct gs_sim {
   DevLinks h_links{};
   std::vector<float4> h_tverts;
   std::vector<uint4> h_tcells;
+  std::vector<float> h_tblk;
   double host_ms = -1.0;          // wall time of the last simulate / pd_step (timing enabled)
   const DevModel* model() const { return host ? &h_model : d_model; }
   const DevLinks* links() const { return host ? &h_links : d_links; }
@@ -165,6 +167,7 @@ void gs_sim_destroy(gs_sim* s) {
   if (s->d_links) (void)hipFree(s->d_links);
   if (s->d_tverts) (void)hipFree(s->d_tverts);
   if (s->d_tcells) (void)hipFree(s->d_tcells);
+  if (s->d_tblk) (void)hipFree(s->d_tblk);
   if (s->d_rows) (void)hipFree(s->d_rows);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -257,30 +260,49 @@ int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_verti
       hc[(size_t)(i * (cols - 1) + j)] = make_uint4(zb, f, zl, 0u);
     }
   }
+  // block summary for the query's first cull (gs_terrain.h sphere_contact): the highest cell top of each block
+  const int64_t brows = (rows - 1 + TERRAIN_BLK - 1) / TERRAIN_BLK, bcols = (cols - 1 + TERRAIN_BLK - 1) / TERRAIN_BLK;
+  std::vector<float> hb((size_t)(brows * bcols), -3.0e38f);
+  for (int64_t i = 0; i + 1 < rows; ++i)
+    for (int64_t j = 0; j + 1 < cols; ++j) {
+      float top;
+      std::memcpy(&top, &hc[(size_t)(i * (cols - 1) + j)].x, 4);
+      float& b = hb[(size_t)((i / TERRAIN_BLK) * bcols + j / TERRAIN_BLK)];
+      b = std::max(b, top);
+    }
   TerrainDev& T = s->dp.terr;
   if (s->host) {
     s->h_tverts = std::move(hv);
     s->h_tcells = std::move(hc);
+    s->h_tblk = std::move(hb);
     T.v = s->h_tverts.data();
     T.cell = s->h_tcells.data();
+    T.blk = s->h_tblk.data();
   } else {
     float4* dv = nullptr;
     uint4* dc = nullptr;
+    float* db = nullptr;
     hipError_t e = hipSetDevice(s->device);
     if (e == hipSuccess) e = hipMalloc(&dv, hv.size() * sizeof(float4));
     if (e == hipSuccess) e = hipMalloc(&dc, hc.size() * sizeof(uint4));
+    if (e == hipSuccess) e = hipMalloc(&db, hb.size() * sizeof(float));
     if (e == hipSuccess) e = hipMemcpy(dv, hv.data(), hv.size() * sizeof(float4), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(dc, hc.data(), hc.size() * sizeof(uint4), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(db, hb.data(), hb.size() * sizeof(float), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
       if (dv) (void)hipFree(dv);
       if (dc) (void)hipFree(dc);
+      if (db) (void)hipFree(db);
       return hip_fail(e, "gs_sim_add_triangle_mesh");
     }
     s->d_tverts = dv;
     s->d_tcells = dc;
+    s->d_tblk = db;
     T.v = s->d_tverts;
     T.cell = s->d_tcells;
+    T.blk = s->d_tblk;
   }
+  T.bcols = (int)bcols;
   T.rows = (int)rows;
   T.cols = (int)cols;
   T.x0 = (float)(x0 + tx);

@@ -33,6 +33,7 @@
 #include "gs_math.h"
 
 #define TERRAIN_BACK 0.1f
+#define TERRAIN_BLK 8  // cells per side of a block in TerrainDev::blk
 // faces whose unit normal points down (z below this) generate no contact: a heightfield's surface
 // faces up or sideways, and the slope-threshold vertex moves can invert a triangle, whose back face
 // would otherwise admit a sphere centre lying inside the terrain and push it down along the
@@ -43,7 +44,8 @@ struct TerrainDev {
   const float4* v;     // [rows*cols] world xyz (transform applied), w unused
   const uint4* cell;   // [(rows-1)*(cols-1)]: x = top height (float bits), y = footprint flags,
                        // z = bottom height (float bits), w unused
-  int rows, cols;
+  const float* blk;    // [ceil((rows-1)/TERRAIN_BLK)][bcols]: the highest top of each block of cells
+  int rows, cols, bcols;
   float x0, y0, hs, inv_hs;
   float mu;            // static friction of the mesh
 };
@@ -173,22 +175,59 @@ GS_HD bool sphere_contact(const TerrainDev& T, const float* p, float r, float th
     triangle(p, r, thr, v00, v11, v01, bkey, best, n);
     triangle(p, r, thr, v00, v10, v11, bkey, best, n);
   };
+  if (i0 > i1 || j0 > j1) return false;
+  // Everything below skips only cells the per-cell tests above would skip, so the result is the full scan's.
+  // (1) the sphere's lowest reach above the highest top of every block the range touches: no cell can contact
+  //     (a lifted foot, the knees, the base: most queries end here after one batch of loads)
+  {
+    const int bi0 = i0 / TERRAIN_BLK, bi1 = i1 / TERRAIN_BLK, bj0 = j0 / TERRAIN_BLK, bj1 = j1 / TERRAIN_BLK;
+    bool reach_any = false;
+    if (bi1 - bi0 <= 1 && bj1 - bj0 <= 1) {
+      const float* b0 = T.blk + (size_t)bi0 * T.bcols;
+      const float* b1 = T.blk + (size_t)bi1 * T.bcols;
+      const float t00 = b0[bj0], t01 = b0[bj1], t10 = b1[bj0], t11 = b1[bj1];
+      reach_any = !(zlo > t00) || !(zlo > t01) || !(zlo > t10) || !(zlo > t11);
+    } else {
+      for (int bi = bi0; bi <= bi1; ++bi)
+        for (int bj = bj0; bj <= bj1; ++bj) reach_any |= !(zlo > T.blk[(size_t)bi * T.bcols + bj]);
+    }
+    if (!reach_any) return false;
+  }
   const int ic = (int)floorf(gx), jc = (int)floorf(gy);
   const bool centre = ic >= 0 && ic <= T.rows - 2 && jc >= 0 && jc <= T.cols - 2;
   if (centre) cell(ic, jc, T.cell[(size_t)ic * (T.cols - 1) + jc]);
-  // the rest in (i, j) order; a row's cell words are loaded together before any is tested (one load latency
-  // per row instead of one per cell: the scan is a chain of dependent loads otherwise)
+  // (2) the rest in (i, j) order.  Before loading a cell's word, its widest possible footprint (one cell further
+  //     on every side, plus a margin far above the float rounding of the coordinates) is tested against the
+  //     reach and the best key: cells beyond it are skipped unread, whole rows at once.  A row's remaining cell
+  //     words are loaded together before any is tested (one load latency per row, not one per cell).
+  const float marg = pad + 0.01f * T.hs;
+  const float kscale = 1.f + 1e-5f;  // the key test on the widest footprint, safely on the skipping side
   constexpr int kRowBatch = 8;
   for (int i = i0; i <= i1; ++i) {
+    const float cx0 = T.x0 + (float)i * T.hs;
+    const float wx0 = cx0 - T.hs - marg, wx1 = cx0 + 2.f * T.hs + marg;
+    if (p[0] + reach < wx0 || p[0] - reach > wx1) continue;
+    const float dxw = fmaxf(fmaxf(wx0 - p[0], p[0] - wx1), 0.f);
+    const float dx2 = dxw * dxw;
+    auto unread = [&](int j) {
+      const float cy0 = T.y0 + (float)j * T.hs;
+      const float wy0 = cy0 - T.hs - marg, wy1 = cy0 + 2.f * T.hs + marg;
+      if (p[1] + reach < wy0 || p[1] - reach > wy1) return true;
+      const float dyw = fmaxf(fmaxf(wy0 - p[1], p[1] - wy1), 0.f);
+      return dx2 + dyw * dyw >= bkey * bkey * kscale;
+    };
+    int ja = j0, jz = j1;
+    while (ja <= jz && unread(ja)) ++ja;
+    while (jz >= ja && unread(jz)) --jz;
     const uint4* crow = T.cell + (size_t)i * (T.cols - 1);
-    for (int jb = j0; jb <= j1; jb += kRowBatch) {
+    for (int jb = ja; jb <= jz; jb += kRowBatch) {
       uint4 cw[kRowBatch];
 #pragma unroll
-      for (int k = 0; k < kRowBatch; ++k) cw[k] = crow[jb + k <= j1 ? jb + k : j1];
+      for (int k = 0; k < kRowBatch; ++k) cw[k] = crow[jb + k <= jz ? jb + k : jz];
 #pragma unroll
       for (int k = 0; k < kRowBatch; ++k) {
         const int j = jb + k;
-        if (j <= j1 && !(centre && i == ic && j == jc)) cell(i, j, cw[k]);
+        if (j <= jz && !(centre && i == ic && j == jc)) cell(i, j, cw[k]);
       }
     }
   }

@@ -1,0 +1,360 @@
+// libgymrl.so -- the PPO learner's hidden Linear + ELU layers on the matrix cores (include/gymrl.h ABI 5).
+//
+// rl_games' actor / critic MLPs (network_builder.py A2CBuilder: Linear -> ELU per hidden layer; AnymalTerrainPPO.yaml
+// units 512-256-128, separate networks, fp16 autocast under mixed_precision) train on 16384-row minibatches.  On
+// hipBLASLt each hidden layer was a GEMM (~12 us at these skinny shapes), an ELU pass and its backward, and a
+// split-K weight-gradient GEMM with its finish (network.py).  Here a layer is:
+//   forward   Y  = ELU(X W^T + b)                     one kernel (k_gemm_nt<ELU>), bias and ELU in the epilogue
+//   backward  dZ = dY * ELU'(Y)  (ELU' = 1 for Y > 0, Y + 1 otherwise: torch's elu_backward on the result)
+//             dX = dZ W                               k_gemm_nt<prologue dZ> on W^T (k_transpose_f16)
+//             dW = dZ^T X, db = colsum dZ             k_gemm_tn: S row-block partials [S][N][K] / [S][N] in f32,
+//                                                     finished in a fixed order by rl_splitk_accum (rl_grad.hip)
+// Operands fp16, accumulation f32 (v_mfma_f32_32x32x16_f16), outputs rounded once to fp16 (Y, dX) or kept f32
+// (weight / bias partials).  Tiles: 256 threads = 4 waves in 2 x 2, each wave 2 x 2 (or 1 x 2) MFMA tiles of
+// 32 x 32; the reduction in steps of 32 through double-buffered LDS.  NT: both operands are contiguous along the
+// reduction index (X rows, W rows; dZ rows, W^T rows) and go to LDS as they are; TN (weight gradient): both
+// operands are [M][*] row-major and the reduction runs over M, so each 16-B global chunk is written to LDS
+// transposed (8 scalar stores) and the fragments read contiguous along M.
+//
+// MFMA 32x32x16 operand / result maps (gfx950): lane l, r = l & 31, h = l >> 5 holds A[row r][k = 8h + j] and
+// B[k = 8h + j][col r] (j = 0..7); result register i of lane l is C[row (i & 3) + 8 (i >> 2) + 4 h][col r].
+// (tests/test_ppo_gpu.py test_linear_kernels_exact_on_integers pins them with exact integer data.)
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "gymrl.h"
+
+int rl_set_error(const char* msg);  // rl_gae.hip
+
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+constexpr int kThreads = 256;
+constexpr int kStep = 32;          // reduction step per LDS stage (two MFMA k-steps)
+constexpr int kLd = kStep + 8;     // LDS row stride in halves (80 B): the 32 rows of a fragment read spread banks
+
+__device__ __forceinline__ float elu_f(float z) { return z > 0.f ? z : expm1f(z); }
+// torch elu_backward with is_result: y > 0 -> 1, else y + 1 (= exp(z))
+__device__ __forceinline__ float elu_d(float y) { return y > 0.f ? 1.f : y + 1.f; }
+
+// 8 consecutive halves of a row from global memory: 16 B as two 8-B loads (rows are 8-B aligned: host check),
+// zero beyond `valid`
+__device__ __forceinline__ h8 load8(const _Float16* __restrict__ p, int valid) {
+  h8 v;
+  if (valid >= 8) {
+    const uint2 a = *reinterpret_cast<const uint2*>(p);
+    const uint2 b = *reinterpret_cast<const uint2*>(p + 4);
+    uint4 u = make_uint4(a.x, a.y, b.x, b.y);
+    v = __builtin_bit_cast(h8, u);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = j < valid ? p[j] : (_Float16)0.f;
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------- NT: C[m][c] = sum_r A[m][r] Bt[c][r]
+// APRO: A is dZ = dY * elu'(Y) formed on load (A = dY, Ay = Y, both [M][R]).  ACT: ELU epilogue.  bias: fp16 [C]
+// or null.  C fp16 [M][ldc].  M % BM == 0, Cn % BN == 0 (host).
+template <int BM, int BN, bool ACT, bool APRO>
+__global__ __launch_bounds__(kThreads) void k_gemm_nt(const _Float16* __restrict__ A, const _Float16* __restrict__ Ay,
+                                                      int lda, const _Float16* __restrict__ Bt, int ldb,
+                                                      const _Float16* __restrict__ bias, _Float16* __restrict__ C,
+                                                      int ldc, int R) {
+  constexpr int TM = BM / 64, TN = BN / 64;                  // MFMA tiles per wave
+  constexpr int CA = BM * kStep / 8 / kThreads, CB = BN * kStep / 8 / kThreads;  // 16-B chunks per thread
+  static_assert(CA >= 1 && CB >= 1, "tile too small for the thread block");
+  __shared__ _Float16 sA[2][BM * kLd];
+  __shared__ _Float16 sB[2][BN * kLd];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * BM, c0 = blockIdx.y * BN;
+  const int r = lane & 31, hh = lane >> 5;
+  f16v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  h8 ra[CA], rb[CB];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int c = tid + i * kThreads, row = c >> 2, kc = (c & 3) * 8;
+      const int valid = R - (k0 + kc);
+      const size_t off = (size_t)(m0 + row) * lda + k0 + kc;
+      h8 v = load8(A + off, valid);
+      if constexpr (APRO) {
+        const h8 y = load8(Ay + off, valid);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (_Float16)((float)v[j] * elu_d((float)y[j]));
+      }
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const int c = tid + i * kThreads, row = c >> 2, kc = (c & 3) * 8;
+      rb[i] = load8(Bt + (size_t)(c0 + row) * ldb + k0 + kc, R - (k0 + kc));
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int c = tid + i * kThreads, row = c >> 2, kc = (c & 3) * 8;
+      *reinterpret_cast<h8*>(&sA[buf][row * kLd + kc]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const int c = tid + i * kThreads, row = c >> 2, kc = (c & 3) * 8;
+      *reinterpret_cast<h8*>(&sB[buf][row * kLd + kc]) = rb[i];
+    }
+  };
+  const int steps = (R + kStep - 1) / kStep;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int s = 0; s < steps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < steps) gload((s + 1) * kStep);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      h8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const h8*>(&sA[buf][(wm * (BM / 2) + i * 32 + r) * kLd + ks * 16 + 8 * hh]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[j] = *reinterpret_cast<const h8*>(&sB[buf][(wn * (BN / 2) + j * 32 + r) * kLd + ks * 16 + 8 * hh]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (s + 1 < steps) lstore(buf ^ 1);
+    __syncthreads();
+  }
+  // epilogue: + bias, ELU, one rounding to fp16
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = c0 + wn * (BN / 2) + j * 32 + r;
+    const float bv = bias ? (float)bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int row = m0 + wm * (BM / 2) + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * hh;
+        float z = acc[i][j][q] + bv;
+        if constexpr (ACT) z = elu_f(z);
+        C[(size_t)row * ldc + col] = (_Float16)z;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- TN: weight / bias gradient partials
+// part[s][n][k] = sum_{m in block s} dZ[m][n] X[m][k] with dZ = dY * elu'(Y) (dY, Y [M][N], X [M][K]);
+// bpart[s][n] = sum_{m in block s} dZ[m][n] (written by the blocks of k-tile 0).  Tiles 128 (n) x 128 (k);
+// the rows of a block in steps of 32.
+constexpr int kTN = 128;
+__global__ __launch_bounds__(kThreads) void k_gemm_tn(const _Float16* __restrict__ dY, const _Float16* __restrict__ Y,
+                                                      int N, const _Float16* __restrict__ X, int ldx, int K,
+                                                      int rows_per_split, float* __restrict__ part,
+                                                      float* __restrict__ bpart) {
+  __shared__ _Float16 sA[2][kTN * kLd];  // [n][m]
+  __shared__ _Float16 sB[2][kTN * kLd];  // [k][m]
+  __shared__ float sbias[16][kTN / 8 * 8 + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int n0 = blockIdx.x * kTN, k0 = blockIdx.y * kTN, s = blockIdx.z;
+  const int mb = s * rows_per_split;
+  const int r = lane & 31, hh = lane >> 5;
+  const bool do_bias = blockIdx.y == 0 && bpart != nullptr;
+  f16v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+  // each thread: 2 chunks of 8 along n (resp. k) at rows m = tid / 16 and tid / 16 + 16 of the step
+  const int crow = tid >> 4, ccol = (tid & 15) * 8;
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  h8 ra[2], rb[2];
+  auto gload = [&](int m) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const size_t row = (size_t)(m + crow + 16 * i);
+      const size_t off = row * N + n0 + ccol;
+      const h8 g = load8(dY + off, N - (n0 + ccol));
+      const h8 y = load8(Y + off, N - (n0 + ccol));
+      h8 z;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float zf = (float)g[j] * elu_d((float)y[j]);
+        z[j] = (_Float16)zf;
+        bsum[j] += (float)z[j];  // the bias gradient sums the same rounded dZ the weight gradient uses
+      }
+      ra[i] = z;
+      rb[i] = load8(X + row * ldx + k0 + ccol, K - (k0 + ccol));
+    }
+  };
+  auto lstore = [&](int buf) {  // transposed: element j of the chunk to row (col + j), column m
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = crow + 16 * i;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sA[buf][(ccol + j) * kLd + m] = ra[i][j];
+        sB[buf][(ccol + j) * kLd + m] = rb[i][j];
+      }
+    }
+  };
+  const int steps = rows_per_split / kStep;
+  gload(mb);
+  lstore(0);
+  __syncthreads();
+  for (int st = 0; st < steps; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < steps) gload(mb + (st + 1) * kStep);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      h8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        fa[i] = *reinterpret_cast<const h8*>(&sA[buf][(wm * 64 + i * 32 + r) * kLd + ks * 16 + 8 * hh]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        fb[j] = *reinterpret_cast<const h8*>(&sB[buf][(wn * 64 + j * 32 + r) * kLd + ks * 16 + 8 * hh]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (st + 1 < steps) lstore(buf ^ 1);
+    __syncthreads();
+  }
+  float* out = part + (size_t)s * N * K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = k0 + wn * 64 + j * 32 + r;
+      if (k < K) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int n = n0 + wm * 64 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * hh;
+          out[(size_t)n * K + k] = acc[i][j][q];
+        }
+      }
+    }
+  if (do_bias) {  // the 16 row groups' sums of each column, added in a fixed order
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sbias[crow][ccol + j] = bsum[j];
+    __syncthreads();
+    if (tid < kTN && n0 + tid < N) {
+      float t = 0.f;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) t += sbias[g][tid];
+      bpart[(size_t)s * N + n0 + tid] = t;
+    }
+  }
+}
+
+// W [N][K] fp16 -> W^T [K][N] fp16 (32 x 32 tiles through LDS)
+__global__ __launch_bounds__(256) void k_transpose_f16(const _Float16* __restrict__ w, int N, int K,
+                                                       _Float16* __restrict__ wt) {
+  __shared__ _Float16 t[32][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int bk = blockIdx.x * 32, bn = blockIdx.y * 32;
+#pragma unroll
+  for (int i = 0; i < 32; i += 8) {
+    const int n = bn + ty + i, k = bk + tx;
+    if (n < N && k < K) t[ty + i][tx] = w[(size_t)n * K + k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 32; i += 8) {
+    const int k = bk + ty + i, n = bn + tx;
+    if (n < N && k < K) wt[(size_t)k * N + n] = t[tx][ty + i];
+  }
+}
+
+bool aligned8(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 7u) == 0; }
+
+int launch_fail(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess) return 0;
+  char msg[256];
+  snprintf(msg, sizeof(msg), "%s: launch failed: %s", what, hipGetErrorString(e));
+  return rl_set_error(msg) + 1;
+}
+
+}  // namespace
+
+extern "C" int rl_linear_fwd(const void* x, int32_t M, int32_t K, int32_t ldx, const void* w, int32_t N,
+                             const void* bias, int32_t act, void* y, void* stream) {
+  if (!x || !w || !y || M <= 0 || K <= 0 || N <= 0) return rl_set_error("rl_linear_fwd: null pointer or empty shape");
+  if (M % 64 || N % 128 || ldx % 4 || K % 4 || !aligned8(x) || !aligned8(w))
+    return rl_set_error("rl_linear_fwd: M % 64, N % 128, K % 4 and 8-byte aligned rows required");
+  hipStream_t st = (hipStream_t)stream;
+  const auto* X = static_cast<const _Float16*>(x);
+  const auto* W = static_cast<const _Float16*>(w);
+  const auto* B = static_cast<const _Float16*>(bias);
+  auto* Y = static_cast<_Float16*>(y);
+  // 128 x 128 tiles when that still gives >= 256 workgroups, else 64-row tiles
+  if ((M / 128) * (N / 128) >= 256 && M % 128 == 0) {
+    const dim3 g(M / 128, N / 128);
+    if (act) hipLaunchKernelGGL((k_gemm_nt<128, 128, true, false>), g, dim3(kThreads), 0, st, X, nullptr, ldx, W, K, B, Y, N, K);
+    else hipLaunchKernelGGL((k_gemm_nt<128, 128, false, false>), g, dim3(kThreads), 0, st, X, nullptr, ldx, W, K, B, Y, N, K);
+  } else {
+    const dim3 g(M / 64, N / 128);
+    if (act) hipLaunchKernelGGL((k_gemm_nt<64, 128, true, false>), g, dim3(kThreads), 0, st, X, nullptr, ldx, W, K, B, Y, N, K);
+    else hipLaunchKernelGGL((k_gemm_nt<64, 128, false, false>), g, dim3(kThreads), 0, st, X, nullptr, ldx, W, K, B, Y, N, K);
+  }
+  return launch_fail("rl_linear_fwd");
+}
+
+extern "C" int rl_linear_transpose(const void* w, int32_t N, int32_t K, void* wt, void* stream) {
+  if (!w || !wt || N <= 0 || K <= 0) return rl_set_error("rl_linear_transpose: null pointer or empty shape");
+  hipLaunchKernelGGL(k_transpose_f16, dim3((K + 31) / 32, (N + 31) / 32), dim3(256), 0, (hipStream_t)stream,
+                     static_cast<const _Float16*>(w), N, K, static_cast<_Float16*>(wt));
+  return launch_fail("rl_linear_transpose");
+}
+
+extern "C" int rl_linear_bwd(const void* dy, const void* y, int32_t M, int32_t N, const void* x, int32_t K,
+                             int32_t ldx, const void* wt, void* dx, int32_t splits, float* wpart, float* bpart,
+                             void* stream) {
+  if (!dy || !y || !x || M <= 0 || N <= 0 || K <= 0) return rl_set_error("rl_linear_bwd: null pointer or empty shape");
+  if (M % 128 || N % 128 || K % 4 || ldx % 4 || !aligned8(dy) || !aligned8(y) || !aligned8(x))
+    return rl_set_error("rl_linear_bwd: M % 128, N % 128, K % 4 and 8-byte aligned rows required");
+  if (splits <= 0 || M % (splits * kStep) != 0) return rl_set_error("rl_linear_bwd: M must split into multiples of 32 rows");
+  hipStream_t st = (hipStream_t)stream;
+  const auto* DY = static_cast<const _Float16*>(dy);
+  const auto* Yv = static_cast<const _Float16*>(y);
+  const auto* X = static_cast<const _Float16*>(x);
+  if (dx) {
+    if (!wt || !aligned8(wt) || K % 128) return rl_set_error("rl_linear_bwd: dX needs W^T and K % 128");
+    const auto* WT = static_cast<const _Float16*>(wt);
+    auto* DX = static_cast<_Float16*>(dx);
+    if ((M / 128) * (K / 128) >= 256) {
+      hipLaunchKernelGGL((k_gemm_nt<128, 128, false, true>), dim3(M / 128, K / 128), dim3(kThreads), 0, st, DY, Yv, N,
+                         WT, N, nullptr, DX, K, N);
+    } else {
+      hipLaunchKernelGGL((k_gemm_nt<64, 128, false, true>), dim3(M / 64, K / 128), dim3(kThreads), 0, st, DY, Yv, N,
+                         WT, N, nullptr, DX, K, N);
+    }
+    if (int rc = launch_fail("rl_linear_bwd (dX)")) return rc;
+  }
+  if (wpart) {
+    hipLaunchKernelGGL(k_gemm_tn, dim3(N / kTN, (K + kTN - 1) / kTN, splits), dim3(kThreads), 0, st, DY, Yv, N, X, ldx,
+                       K, M / splits, wpart, bpart);
+    return launch_fail("rl_linear_bwd (dW)");
+  }
+  return 0;
+}

@@ -15,21 +15,12 @@ import torch
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libgymrl.so")
 EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accum", "rl_colsum_accum", "rl_rollout_post",
-                    "rl_ppo_loss", "rl_ppo_loss_backward", "rl_rms_normalize", "rl_opt_step", "rl_opt_partials_size", "rl_act_mlp", "rl_act_mlp_workspace_floats",
-                    "rl_policy_head"]
+                    "rl_ppo_loss", "rl_ppo_loss_backward", "rl_rms_normalize", "rl_opt_step", "rl_opt_partials_size",
+                    "rl_linear_fwd", "rl_linear_transpose", "rl_linear_bwd", "rl_policy_head"]
 _lib = None
 
 
-RL_ABI_VERSION = 4  # include/gymrl.h
-
-
-MLP_MAX_LAYERS = 4
-
-
-class Mlp(C.Structure):
-    """include/gymrl.h rl_mlp"""
-    _fields_ = [("num_layers", C.c_int32), ("dims", C.c_int32 * (MLP_MAX_LAYERS + 1)),
-                ("weight", C.c_void_p * MLP_MAX_LAYERS), ("bias", C.c_void_p * MLP_MAX_LAYERS)]
+RL_ABI_VERSION = 5  # include/gymrl.h
 
 
 class OptHyper(C.Structure):
@@ -65,11 +56,12 @@ def lib():
         L.rl_ppo_loss_backward.restype = C.c_int
         L.rl_ppo_loss_backward.argtypes = [vp, vp, vp, vp, C.c_int32, C.c_int32, vp, C.c_int32, vp, C.c_int32, vp,
                                            vp]
-        L.rl_act_mlp.restype = C.c_int
-        L.rl_act_mlp.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, C.c_double, C.POINTER(Mlp), C.POINTER(Mlp), vp, vp,
-                                 C.c_int32, vp, vp, vp, vp, vp, vp]
-        L.rl_act_mlp_workspace_floats.restype = C.c_int
-        L.rl_act_mlp_workspace_floats.argtypes = [C.POINTER(Mlp), C.POINTER(Mlp)]
+        for f in ("rl_linear_fwd", "rl_linear_transpose", "rl_linear_bwd"):
+            getattr(L, f).restype = C.c_int
+        L.rl_linear_fwd.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int32, vp, C.c_int32, vp, vp]
+        L.rl_linear_transpose.argtypes = [vp, C.c_int32, C.c_int32, vp, vp]
+        L.rl_linear_bwd.argtypes = [vp, vp, C.c_int32, C.c_int32, vp, C.c_int32, C.c_int32, vp, vp, C.c_int32, vp, vp,
+                                    vp]
         L.rl_opt_step.restype = C.c_int
         L.rl_opt_step.argtypes = [vp, vp, vp, vp, C.c_int64, vp, vp, vp, vp, C.POINTER(OptHyper), vp, vp]
         L.rl_opt_partials_size.restype = C.c_int
@@ -320,50 +312,32 @@ def opt_step(param, grad, exp_avg, exp_avg_sq, step, lr, scale, growth_tracker, 
         raise RuntimeError(f"rl_opt_step failed: {lib().rl_last_error().decode()}")
 
 
-def mlp_desc(seq) -> "Mlp | None":
-    """rl_mlp of an nn.Sequential of (Linear, ELU) pairs with f32 weights (None when the act kernel cannot run it:
-    another activation, more than MLP_MAX_LAYERS layers, widths not multiples of 4 or above 512)."""
-    mods = list(seq)
-    if len(mods) % 2 or not mods or len(mods) // 2 > MLP_MAX_LAYERS:
-        return None
-    d = Mlp()
-    d.num_layers = len(mods) // 2
-    for l in range(d.num_layers):
-        lin, act = mods[2 * l], mods[2 * l + 1]
-        if not isinstance(lin, torch.nn.Linear) or not isinstance(act, torch.nn.ELU) or act.alpha != 1.0:
-            return None
-        if lin.weight.dtype != torch.float32 or lin.bias is None or not lin.weight.is_contiguous():
-            return None
-        if l == 0:
-            d.dims[0] = lin.in_features
-        d.dims[l + 1] = lin.out_features
-        d.weight[l] = lin.weight.data_ptr()
-        d.bias[l] = lin.bias.data_ptr()
-    if any(d.dims[i] % 4 or d.dims[i] > 512 for i in range(d.num_layers + 1)):
-        return None
-    return d
-
-
-def act_mlp_workspace(actor: "Mlp", critic, device):
-    n = lib().rl_act_mlp_workspace_floats(C.byref(actor), C.byref(critic) if critic is not None else None)
-    return torch.empty(max(n, 1), dtype=torch.float32, device=device)
-
-
-def act_mlp(obs, rms, actor: "Mlp", critic, mu_layer, value_layer, workspace):
-    """The act forward's network (include/gymrl.h rl_act_mlp): normalised obs -> (mu [N, A], value [N, 1])."""
-    N, O = obs.shape
-    A = mu_layer.out_features
-    mu = torch.empty(N, A, dtype=torch.float32, device=obs.device)
-    value = torch.empty(N, 1, dtype=torch.float32, device=obs.device)
-    rm = rv = None
-    eps = 0.0
-    if rms is not None:
-        rm, rv, eps = rms.running_mean.data_ptr(), rms.running_var.data_ptr(), rms.epsilon
-    rc = lib().rl_act_mlp(obs.data_ptr(), N, O, rm, rv, float(eps), C.byref(actor),
-                          C.byref(critic) if critic is not None else None, mu_layer.weight.data_ptr(),
-                          mu_layer.bias.data_ptr(), A, value_layer.weight.data_ptr(), value_layer.bias.data_ptr(),
-                          mu.data_ptr(), value.data_ptr(), workspace.data_ptr(),
-                          torch.cuda.current_stream(obs.device).cuda_stream)
+def _check(rc, what):
     if rc != 0:
-        raise RuntimeError(f"rl_act_mlp failed: {lib().rl_last_error().decode()}")
-    return mu, value
+        raise RuntimeError(f"{what} failed: {lib().rl_last_error().decode()}")
+
+
+def linear_fwd(x, w_half, b_half, act: bool, out):
+    """rl_linear_fwd: out [M, N] fp16 = act(x [M, K] fp16 . w_half[N, K]^T + b_half) on the matrix cores."""
+    M, K = x.shape
+    N = w_half.shape[0]
+    _check(lib().rl_linear_fwd(x.data_ptr(), M, K, x.stride(0), w_half.data_ptr(), N,
+                               b_half.data_ptr() if b_half is not None else None, int(act), out.data_ptr(),
+                               torch.cuda.current_stream().cuda_stream), "rl_linear_fwd")
+
+
+def linear_transpose(w_half, out):
+    N, K = w_half.shape
+    _check(lib().rl_linear_transpose(w_half.data_ptr(), N, K, out.data_ptr(), torch.cuda.current_stream().cuda_stream),
+           "rl_linear_transpose")
+
+
+def linear_bwd(dy, y, x, wt, dx, splits: int, wpart, bpart):
+    """rl_linear_bwd: dx = (dy * elu'(y)) . w (wt = w^T, dx None: skipped); wpart [splits, N, K] / bpart [splits, N]
+    f32 row-block partials of the weight / bias gradients (finish with splitk_accum)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    _check(lib().rl_linear_bwd(dy.data_ptr(), y.data_ptr(), M, N, x.data_ptr(), K, x.stride(0),
+                               wt.data_ptr() if wt is not None else None, dx.data_ptr() if dx is not None else None,
+                               splits, wpart.data_ptr(), bpart.data_ptr() if bpart is not None else None,
+                               torch.cuda.current_stream().cuda_stream), "rl_linear_bwd")

@@ -23,11 +23,10 @@ _ACT = {"elu": nn.ELU, "relu": nn.ReLU, "tanh": nn.Tanh, "selu": nn.SELU, "None"
 # library tiles only the small N x K output (24-48 workgroups for 512 x 188) and takes ~100 us on
 # MI355X; split, ~25 us (tools/probes/gemm_splitk.py).  The sum is one HIP kernel that accumulates
 # into weight.grad (rl_splitk_accum, csrc/rl_grad.hip).
-# the act forward's network as one HIP kernel (gae.act_mlp) instead of the torch Linear / ELU statements.  Off:
-# measured 365 us per call against ~0.14 ms for the whole torch act forward (profiles/r03h_kernel_stats.csv): its
-# f32 FMA chains wait on L2 weight loads with two waves per SIMD; kept (and parity-tested) as the base for a
-# staged-weight version
-USE_ACT_KERNEL = False
+# The hidden Linear + ELU layers under fp16 autocast (the learner's minibatch forward / backward) run on the matrix
+# cores as libgymrl's rl_linear_* kernels (csrc/rl_linear.hip): bias and ELU fused into the GEMM epilogue, ELU's
+# backward fused into the dX / dW GEMMs' operand loads.  Off: the torch Linear / ELU statements above.
+USE_MFMA_LAYERS = True
 SPLIT_K = 16
 SPLIT_K_MIN_ROWS = 4096
 
@@ -110,12 +109,115 @@ class Linear(nn.Linear):
         return super().forward(x)
 
 
+def _splits(M: int, tiles: int) -> int:
+    """Row blocks of the weight-gradient partials: enough workgroups for the 256 CUs (>= 256 with the layer's
+    128 x 128 output tiles), each block a multiple of 128 rows."""
+    s = 1
+    while s * tiles < 256 and M % (2 * s * 128) == 0:
+        s *= 2
+    return s
+
+
+class _LinearELUFn(torch.autograd.Function):
+    """One hidden layer, Y = ELU(X W^T + b), on the matrix cores (include/gymrl.h rl_linear_fwd / rl_linear_bwd):
+    fp16 operands as torch's autocast would cast them, f32 accumulation, Y rounded once to fp16.  The backward
+    takes ELU's derivative from Y (torch's elu_backward on the result), writes dX (fp16) and the weight / bias
+    gradients as f32 row-block partials that rl_splitk_accum adds in a fixed order -- into ``.grad`` directly
+    under the learner (``direct``, as _SplitKLinearFn), else into fresh tensors autograd returns."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda")
+    def forward(ctx, x, w, b, w_half=None, b_half=None, direct=False):
+        h = torch.float16
+        xc = x.to(h)
+        if xc.stride(1) != 1 or xc.stride(0) % 4 or xc.data_ptr() % 8:
+            xc = xc.contiguous()
+        wc = w_half if w_half is not None else w.to(h)
+        bc = None if b is None else (b_half if b_half is not None and w_half is not None else b.to(h))
+        y = torch.empty(xc.shape[0], wc.shape[0], dtype=h, device=x.device)
+        gae.linear_fwd(xc, wc, bc, True, y)
+        ctx.save_for_backward(xc, wc, y)
+        ctx.w, ctx.b = w, b
+        ctx.direct = bool(direct)
+        return y
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, gy):
+        xc, wc, y = ctx.saved_tensors
+        gy = gy.to(torch.float16).contiguous()
+        M, N = y.shape
+        K = xc.shape[1]
+        dev = y.device
+        dx = wt = None
+        if ctx.needs_input_grad[0]:
+            wt = torch.empty(K, N, dtype=torch.float16, device=dev)
+            gae.linear_transpose(wc, wt)
+            dx = torch.empty(M, K, dtype=torch.float16, device=dev)
+        want_w = ctx.needs_input_grad[1]
+        want_b = ctx.b is not None and ctx.needs_input_grad[2]
+        splits = _splits(M, (N // 128) * ((K + 127) // 128))
+        wpart = torch.empty(splits, N, K, dtype=torch.float32, device=dev) if want_w or want_b else None
+        bpart = torch.empty(splits, N, dtype=torch.float32, device=dev) if want_b else None
+        if dx is not None or wpart is not None:
+            gae.linear_bwd(gy, y, xc, wt, dx, splits, wpart, bpart)
+        gw = gb = None
+        for want, p, part, slot in ((want_w, ctx.w, wpart, 0), (want_b, ctx.b, bpart, 1)):
+            if not want:
+                continue
+            if ctx.direct:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p, dtype=torch.float32)
+                gae.splitk_accum(part, p.grad)
+            else:
+                t = torch.zeros_like(p, dtype=torch.float32)
+                gae.splitk_accum(part, t)
+                if slot == 0:
+                    gw = t
+                else:
+                    gb = t
+        return dx, gw, gb, None, None, None
+
+
+class _MLP(nn.Sequential):
+    """rl_games' mlp (Linear, activation per hidden layer; same modules and state_dict as nn.Sequential).  Under
+    fp16 autocast on the GPU, with ELU layers whose widths the kernels tile (multiples of 128) and a row count in
+    multiples of 128, each Linear + ELU pair is one _LinearELUFn."""
+
+    def _fused(self, x) -> bool:
+        if not (USE_MFMA_LAYERS and x.is_cuda and x.dim() == 2 and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.float16 and x.shape[0] % 128 == 0 and x.shape[0] > 0):
+            return False
+        mods = list(self)
+        if len(mods) % 2 or not mods:
+            return False
+        for i in range(0, len(mods), 2):
+            lin, act = mods[i], mods[i + 1]
+            if not (isinstance(lin, Linear) and type(act) is nn.ELU and act.alpha == 1.0 and not act.inplace
+                    and lin.weight.dtype == torch.float32 and lin.out_features % 128 == 0
+                    and lin.in_features % 4 == 0):
+                return False
+            # dX needs the input width in multiples of 128 (every layer after the first: a previous width)
+            if i == 0 and x.requires_grad and lin.in_features % 128:
+                return False
+        return True
+
+    def forward(self, x):
+        if not self._fused(x):
+            return super().forward(x)
+        mods = list(self)
+        for i in range(0, len(mods), 2):
+            lin = mods[i]
+            x = _LinearELUFn.apply(x, lin.weight, lin.bias, lin.half_weight, lin.half_bias, lin.direct_grad)
+        return x
+
+
 def _mlp(in_size: int, units: List[int], activation: str) -> nn.Sequential:
     layers = []
     for u in units:
         layers += [Linear(in_size, u), _ACT[activation]()]
         in_size = u
-    return nn.Sequential(*layers)
+    return _MLP(*layers)
 
 
 class ActorCriticNetwork(nn.Module):
@@ -165,22 +267,6 @@ class ModelA2CContinuousLogStd(nn.Module):
         if normalize_input:
             self.running_mean_std = RunningMeanStd((obs_dim,))
 
-    def _act_mlps(self):
-        """(actor, critic or None) rl_mlp descriptors for gae.act_mlp, or None when the act kernel cannot run this
-        model (the parameter pointers are stable: the learner keeps them as views into its flat buffer)."""
-        if not USE_ACT_KERNEL:
-            return None
-        if getattr(self, "_act_desc", None) is None:
-            net = self.a2c_network
-            a = gae.mlp_desc(net.actor_mlp)
-            c = gae.mlp_desc(net.critic_mlp) if net.separate else None
-            ok = a is not None and (c is not None or not net.separate) and net.mu.weight.dtype == torch.float32
-            if ok and self.normalize_input:
-                rms = self.running_mean_std
-                ok = rms.running_mean.dtype == torch.float64 and not rms.norm_only
-            self._act_desc = (a, c, gae.act_mlp_workspace(a, c, net.mu.weight.device)) if ok else False
-        return self._act_desc or None
-
     def norm_obs(self, obs):
         with torch.no_grad():
             return self.running_mean_std(obs) if self.normalize_input else obs
@@ -201,20 +287,12 @@ class ModelA2CContinuousLogStd(nn.Module):
         net = self.a2c_network
         if (not is_train and raw.is_cuda and raw.dtype == torch.float32 and net.fixed_sigma
                 and (not self.normalize_value or self.value_mean_std.running_mean.numel() == 1)):
-            # act forward on the device: the network (one kernel, gae.act_mlp, when its layers allow it and the input
-            # statistics are frozen -- eval mode, as rl_games' play_steps sets), torch's normal_ draws, then one
-            # kernel for the head
-            frozen = not (self.normalize_input and self.running_mean_std.training)
-            mlps = self._act_mlps() if frozen and raw.is_contiguous() else None
-            if mlps is not None:
-                mu, value = gae.act_mlp(raw, self.running_mean_std if self.normalize_input else None,
-                                        mlps[0], mlps[1], net.mu, net.value, mlps[2])
-            else:
-                obs = self.norm_obs(raw)
-                a_out = net.actor_mlp(obs)
-                c_out = net.critic_mlp(obs) if net.separate else a_out
-                value = net.value(c_out).contiguous()
-                mu = net.mu(a_out).contiguous()
+            # act forward on the device: the network, torch's normal_ draws, then one kernel for the head
+            obs = self.norm_obs(raw)
+            a_out = net.actor_mlp(obs)
+            c_out = net.critic_mlp(obs) if net.separate else a_out
+            value = net.value(c_out).contiguous()
+            mu = net.mu(a_out).contiguous()
             noise = torch.empty_like(mu).normal_(0.0, 1.0)
             actions, sigmas, neglogp, values = gae.policy_head(
                 mu, noise, net.sigma.detach(), value, self.value_mean_std if self.normalize_value else None)

@@ -460,44 +460,122 @@ def test_fused_opt_step_scale_growth_stays_finite():
     assert float(scale) == s0 and int(tracker) == 0 and float(step) == 1.0
 
 
-@pytest.mark.parametrize("units,separate,obs_dim,actions", [([512, 256, 128], True, 188, 12), ([32, 32], False, 4, 1),
-                                                             ([256, 128, 64], True, 60, 8)])
-def test_act_mlp_kernel_matches_torch_network(units, separate, obs_dim, actions, monkeypatch):
-    """rl_act_mlp (normalisation, actor [+ critic] Linear + ELU layers, mu / value heads in one kernel) against the
-    torch statement of the same eval forward (AnymalTerrain, Cartpole and Ant network shapes).  The kernel is off in
-    the learner by default (network.USE_ACT_KERNEL); the test switches it on for this model."""
-    from isaacgymenv_amd.rl import gae, network
-    from isaacgymenv_amd.rl.network import ActorCriticNetwork, ModelA2CContinuousLogStd
-    monkeypatch.setattr(network, "USE_ACT_KERNEL", True)
-    torch.manual_seed(5)
-    net = ActorCriticNetwork(obs_dim, actions, units, "elu", separate, True, 0.0)
-    model = ModelA2CContinuousLogStd(net, obs_dim, True, True).cuda().eval()
+@pytest.mark.parametrize("M", [256, 16384])
+def test_linear_kernels_exact_on_integers(M):
+    """rl_linear_fwd / rl_linear_bwd on small integers (and halves), where fp16 operands, f32 accumulation and
+    the fp16 outputs are all exact: the results must equal float64 matmuls bit for bit.  Pins the MFMA operand /
+    result lane maps, the tile edges (K = 188 is no multiple of the 32-wide reduction step), both tile sizes
+    (M = 256: 64-row tiles) and the split row blocks of the weight-gradient partials."""
+    from isaacgymenv_amd.rl import gae
+    g = torch.Generator(device="cpu").manual_seed(M)
+    ri = lambda lo, hi, *shape: torch.randint(lo, hi + 1, shape, generator=g).to(torch.float16).cuda()  # noqa: E731
+    # forward, no activation: |y| <= 188 * 9 + 3 < 2048
+    x, w, b = ri(-3, 3, M, 188), ri(-3, 3, 512, 188), ri(-3, 3, 512)
+    y = torch.empty(M, 512, dtype=torch.float16, device="cuda")
+    gae.linear_fwd(x, w, b, False, y)
+    ref = x.double() @ w.double().T + b.double()
+    assert torch.equal(y.double(), ref)
+    # ELU epilogue on the same sums: only the rounding of expm1 to fp16 differs from torch's fp16 ELU
+    gae.linear_fwd(x, w, b, True, y)
+    torch.testing.assert_close(y.float(), torch.nn.functional.elu(ref).half().float(), rtol=1e-3, atol=1e-3)
+    # backward: y in {-0.5, 0.5, 1, 2} (ELU' = 0.5 or 1), dy in {-1, 0, 1}, w in [-2, 2]
+    for N, K, want_dx in ((256, 512, True), (512, 188, False)):
+        yv = torch.tensor([-0.5, 0.5, 1.0, 2.0], dtype=torch.float16)[torch.randint(0, 4, (M, N), generator=g)].cuda()
+        dy, xw, wv = ri(-1, 1, M, N), ri(-3, 3, M, K), ri(-2, 2, N, K)
+        dz = dy.double() * torch.where(yv > 0, 1.0, yv.double() + 1.0)
+        splits = 8 if M % (8 * 128) == 0 else 2
+        wt = torch.empty(K, N, dtype=torch.float16, device="cuda")
+        gae.linear_transpose(wv, wt)
+        assert torch.equal(wt, wv.T)
+        dx = torch.empty(M, K, dtype=torch.float16, device="cuda") if want_dx else None
+        wpart = torch.empty(splits, N, K, device="cuda")
+        bpart = torch.empty(splits, N, device="cuda")
+        gae.linear_bwd(dy, yv, xw, wt if want_dx else None, dx, splits, wpart, bpart)
+        rows = M // splits
+        if want_dx:
+            assert torch.equal(dx.double(), dz @ wv.double())
+        for s_ in range(splits):
+            blk = slice(s_ * rows, (s_ + 1) * rows)
+            assert torch.equal(wpart[s_].double(), dz[blk].T @ xw[blk].double()), s_
+            assert torch.equal(bpart[s_].double(), dz[blk].sum(0)), s_
+
+
+def test_linear_kernels_reject_untileable_shapes():
+    from isaacgymenv_amd.rl import gae
+    x = torch.zeros(100, 64, dtype=torch.float16, device="cuda")
+    w = torch.zeros(128, 64, dtype=torch.float16, device="cuda")
+    with pytest.raises(RuntimeError, match="M % 64"):
+        gae.linear_fwd(x, w, None, True, torch.empty(100, 128, dtype=torch.float16, device="cuda"))
+    y = torch.zeros(128, 128, dtype=torch.float16, device="cuda")
+    with pytest.raises(RuntimeError, match="K % 128"):
+        gae.linear_bwd(y, y, torch.zeros(128, 64, dtype=torch.float16, device="cuda"), w.T.contiguous(), torch.empty(128, 64, dtype=torch.float16,
+                       device="cuda"), 1, torch.empty(1, 128, 64, device="cuda"), None)
+
+
+def _mlp_pair(obs_dim, units):
+    from isaacgymenv_amd.rl import network
+    mlp = network._mlp(obs_dim, units, "elu").cuda()
+    layers, d = [], obs_dim
+    for u in units:
+        layers += [torch.nn.Linear(d, u), torch.nn.ELU()]
+        d = u
+    ref = torch.nn.Sequential(*layers).cuda()
+    ref.load_state_dict(mlp.state_dict())
+    return mlp, ref
+
+
+@pytest.mark.parametrize("direct", [False, True])
+def test_mfma_mlp_matches_torch_fp32_within_fp16_error(direct, monkeypatch):
+    """The actor MLP of AnymalTerrainPPO (188 -> 512 -> 256 -> 128, ELU) on 16384 rows under fp16 autocast through
+    the rl_linear kernels, against the same network in fp32 torch.  Bar: the output, the input gradient and every
+    parameter gradient lie within 2x (+ a floor of 1e-3 of the field's scale) of the error torch's own fp16 autocast
+    path makes against that fp32 reference."""
+    from isaacgymenv_amd.rl import network
+    torch.manual_seed(3)
+    mlp, ref = _mlp_pair(188, [512, 256, 128])
+    for m in mlp:
+        if isinstance(m, network.Linear):
+            m.direct_grad = direct
     with torch.no_grad():
-        for p_ in model.parameters():
-            p_.normal_(0.0, 0.1)
-        model.running_mean_std.running_mean.normal_(0.0, 0.5)
-        model.running_mean_std.running_var.uniform_(0.5, 2.0)
-    obs = torch.randn(4096 + 3, obs_dim, device="cuda") * 2.0  # a partial last workgroup too
-    mlps = model._act_mlps()
-    assert mlps is not None
-    mu, value = gae.act_mlp(obs, model.running_mean_std, mlps[0], mlps[1], net.mu, net.value, mlps[2])
-    with torch.no_grad():
-        x = model.norm_obs(obs)
-        a = net.actor_mlp(x)
-        c = net.critic_mlp(x) if separate else a
-        mu_ref, v_ref = net.mu(a), net.value(c)
-    torch.testing.assert_close(mu, mu_ref, rtol=1e-4, atol=1e-5)
-    torch.testing.assert_close(value, v_ref, rtol=1e-4, atol=1e-5)
-    # and through the model's act forward (same sampling stream either way)
-    old = network.USE_ACT_KERNEL
-    try:
-        network.USE_ACT_KERNEL = False
-        torch.manual_seed(9)
-        ref = model({"is_train": False, "obs": obs})
-        network.USE_ACT_KERNEL = True
-        torch.manual_seed(9)
-        got = model({"is_train": False, "obs": obs})
-    finally:
-        network.USE_ACT_KERNEL = old
-    for k in ("mus", "values", "actions", "neglogpacs"):
-        torch.testing.assert_close(got[k], ref[k], rtol=1e-4, atol=1e-4)
+        for p_ in mlp.parameters():
+            p_.normal_(0.0, 0.08)
+    ref.load_state_dict(mlp.state_dict())
+    x = torch.randn(16384, 188, device="cuda") * 1.5
+    gout = torch.randn(16384, 128, device="cuda")
+
+    def run(model, autocast, fused):
+        monkeypatch.setattr(network, "USE_MFMA_LAYERS", fused)
+        model.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.float16, enabled=autocast):
+            if fused:
+                assert model._fused(x)
+            y = model(x)
+        (y.float() * gout).sum().backward()
+        return [y.float()] + [p_.grad.clone() for p_ in model.parameters()]
+
+    want = run(ref, False, False)
+    fp16 = run(mlp, True, False)
+    got = run(mlp, True, True)
+    for i, (g_, t_, w_) in enumerate(zip(got, fp16, want)):
+        scale = float(w_.abs().max())
+        err, base = float((g_ - w_).abs().max()), float((t_ - w_).abs().max())
+        assert err <= 2.0 * base + 1e-3 * scale, (i, err, base, scale)
+
+
+def test_mfma_mlp_input_gradient_and_autograd_grad():
+    """A grad-requiring input of a 128-multiple width gets its gradient through rl_linear_bwd's dX, and
+    torch.autograd.grad (direct off) receives the weight / bias gradients without touching .grad."""
+    from isaacgymenv_amd.rl import network
+    torch.manual_seed(4)
+    mlp, ref = _mlp_pair(256, [256, 128])
+    x = torch.randn(4096, 256, device="cuda")
+    with torch.autocast("cuda", dtype=torch.float16):
+        xi = x.clone().requires_grad_(True)
+        assert mlp._fused(xi)
+        y = mlp(xi)
+        got = torch.autograd.grad(y.float().sum(), [xi] + list(mlp.parameters()))
+    xr = x.clone().requires_grad_(True)
+    want = torch.autograd.grad(ref(xr).sum(), [xr] + list(ref.parameters()))
+    assert all(p_.grad is None for p_ in mlp.parameters())
+    for g_, w_ in zip(got, want):
+        assert float((g_.float() - w_).abs().max()) <= 5e-3 * float(w_.abs().max()) + 1e-4
