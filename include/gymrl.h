@@ -172,13 +172,16 @@ int rl_opt_partials_size(void);
  * rl_linear_bwd: the backward of rl_linear_fwd with ELU from its output y: dZ = dy * (y > 0 ? 1 : y + 1);
  *   dx [M][K] fp16 = dZ . w (from wt = w^T; null dx: skipped; needs K % 128 == 0);
  *   wpart [splits][N][K] f32 = per row block of M / splits rows, dZ^T . x; bpart [splits][N] f32 = column sums of
- *   dZ (null: skipped).  Finish with rl_splitk_accum (fixed order).  M % 128 == 0, M % (32 splits) == 0.
+ *   dZ (null: skipped); pstride 0 = those layouts, else block s of both starts s * pstride floats in (the merged
+ *   layout bpart = wpart + N*K, pstride = N*K + N: one rl_splitk_accum finishes a weight and its bias when their
+ *   gradients are adjacent).  wpart 16-byte aligned.  Finish with rl_splitk_accum (fixed order).  M % 128 == 0,
+ *   M % (64 splits) == 0.
  */
 int rl_linear_fwd(const void *x, int32_t M, int32_t K, int32_t ldx, const void *w, int32_t N, const void *bias,
                   int32_t act, void *y, void *stream);
 int rl_linear_transpose(const void *w, int32_t N, int32_t K, void *wt, void *stream);
 int rl_linear_bwd(const void *dy, const void *y, int32_t M, int32_t N, const void *x, int32_t K, int32_t ldx,
-                  const void *wt, void *dx, int32_t splits, float *wpart, float *bpart, void *stream);
+                  const void *wt, void *dx, int32_t splits, float *wpart, float *bpart, int64_t pstride, void *stream);
 
 #ifdef __cplusplus
 }

@@ -15,6 +15,8 @@
 // Rows are processed in the oracle's global order (root candidates, then chain 0, 1, ...), so
 // the iterates are the same projected Gauss-Seidel sequence, only the rounding order of the base
 // sums differs.  4096 envs -> 256 waves; per-chain model constants are staged in LDS.
+#include <type_traits>
+
 #include "gs_internal.h"
 #include "gs_topologies.h"
 #include "gs_math.h"
@@ -678,6 +680,74 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     for (int k = 0; k < 6; ++k) F0[k] = ia[k] + x6[k];
   }
 
+  // ================= TERR: the mesh queries first, while little else is live (run inside the forward pass, where
+  // the chain's spatial quantities are live, the query code spilled ~1 KB of registers per lane to scratch).  The
+  // chain's body poses are walked here by the forward pass's own statements; results: distance, normal, friction.
+  // (held in a type that is empty for plane scenes: dead arrays there cost the plane kernel 0.5 KB of scratch)
+  struct TerrQ {
+    float d[CC], n[CC][3], m[CC];                                        // chain candidates
+    float rd[RC > 0 ? RC : 1], rn[RC > 0 ? RC : 1][3], rm[RC > 0 ? RC : 1];  // root candidates
+  };
+  struct NoTerrQ {};
+  [[maybe_unused]] std::conditional_t<TERR, TerrQ, NoTerrQ> tq;
+  if constexpr (TERR) {
+    float Rk[9], Xk[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < 9; ++f) Rk[f] = R0[f];
+#pragma unroll
+    for (int k = 0; k < CL; ++k) {
+      const float* bp = cm + (k * C::BODY) * LN;
+      float jR[9], jt[3], ax[3];
+#pragma unroll
+      for (int f = 0; f < 9; ++f) jR[f] = bp[f * LN];
+#pragma unroll
+      for (int f = 0; f < 3; ++f) { jt[f] = bp[(9 + f) * LN]; ax[f] = bp[(12 + f) * LN]; }
+      float RJ[9], t[3], aw[3];
+      mat3mul(Rk, jR, RJ);
+      mat3vec(Rk, jt, t);
+      Xk[0] += t[0]; Xk[1] += t[1]; Xk[2] += t[2];
+      mat3vec(RJ, ax, aw);
+      const float qj = s.q[k];
+      if (T::jkind[1 + k] == 1) {
+        float sn, cs;
+        sincosf(qj, &sn, &cs);
+        const float Cc = 1.f - cs;
+        float Rq[9];
+        Rq[0] = cs + ax[0] * ax[0] * Cc;         Rq[1] = ax[0] * ax[1] * Cc - ax[2] * sn; Rq[2] = ax[0] * ax[2] * Cc + ax[1] * sn;
+        Rq[3] = ax[1] * ax[0] * Cc + ax[2] * sn; Rq[4] = cs + ax[1] * ax[1] * Cc;         Rq[5] = ax[1] * ax[2] * Cc - ax[0] * sn;
+        Rq[6] = ax[2] * ax[0] * Cc - ax[1] * sn; Rq[7] = ax[2] * ax[1] * Cc + ax[0] * sn; Rq[8] = cs + ax[2] * ax[2] * Cc;
+        mat3mul(RJ, Rq, Rk);
+      } else {
+#pragma unroll
+        for (int f = 0; f < 9; ++f) Rk[f] = RJ[f];
+        Xk[0] += aw[0] * qj; Xk[1] += aw[1] * qj; Xk[2] += aw[2] * qj;
+      }
+#pragma unroll
+      for (int j = 0; j < CC; ++j) {
+        if (T::T_ccb[j] == k) {
+          const float* cp = cm + (C::CAND + 4 * j) * LN;
+          const float pl[3] = {cp[0], cp[LN], cp[2 * LN]};
+          float x[3];
+          mat3vec(Rk, pl, x);
+          x[0] += Xk[0]; x[1] += Xk[1]; x[2] += Xk[2];
+          tq.d[j] = terrain_candidate(P, s.p, x, cp[3 * LN], tq.n[j], tq.m[j]);
+        }
+      }
+    }
+    // root candidates: lane j % 4 runs root candidate j's query and broadcasts the result to the team
+#pragma unroll
+    for (int j = 0; j < RC; ++j) {
+      float x[3];
+      mat3vec(R0, M->cpoint[j], x);
+      float nq[3] = {0.f, 0.f, 1.f}, dq = 3.0e38f, mq = P.ground_mu;
+      if (lc == (j & (LN - 1))) dq = terrain_candidate(P, s.p, x, M->cradius[j], nq, mq);
+      tq.rd[j] = bcast(dq, j & (LN - 1));
+      tq.rm[j] = bcast(mq, j & (LN - 1));
+#pragma unroll
+      for (int f = 0; f < 3; ++f) tq.rn[j][f] = bcast(nq[f], j & (LN - 1));
+    }
+  }
+
   // ================= chain forward pass (lane-local)
   float R[CL][9], X[CL][3], S[CL][6], V[CL][6], A[CL][6], Fc[CL][6];
   SpI Ic[CL];
@@ -755,8 +825,8 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         if constexpr (TERR) {
           // deepest of the ground plane and the terrain mesh (gs_terrain.h), as the one-env-per-lane solver;
           // the contact frame (n, t1, t2) replaces the plane's (z, x, y)
-          float nrm[3], smu;
-          const float dist = terrain_candidate(P, s.p, x, r, nrm, smu);
+          const float* nrm = tq.n[j];
+          const float dist = tq.d[j], smu = tq.m[j];
           act[j] = dist < P.contact_offset;
           sep[j] = dist - P.rest_offset;
           cmu[j] = 0.5f * (mu_t[shape * kTeamsPerBlock] + smu);
@@ -1068,12 +1138,10 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     float dist, rmu_s = P.ground_mu;
     float rdir[3][3];
     if constexpr (TERR) {
-      float nq[3] = {0.f, 0.f, 1.f}, dq = 3.0e38f, mq = P.ground_mu;
-      if (lc == (j & (LN - 1))) dq = terrain_candidate(P, s.p, x, r, nq, mq);
-      dist = bcast(dq, j & (LN - 1));
-      rmu_s = bcast(mq, j & (LN - 1));
+      dist = tq.rd[j];
+      rmu_s = tq.rm[j];
 #pragma unroll
-      for (int f = 0; f < 3; ++f) rnrm[j][f] = bcast(nq[f], j & (LN - 1));
+      for (int f = 0; f < 3; ++f) rnrm[j][f] = tq.rn[j][f];
       ract[j] = dist < P.contact_offset;
       rdir[0][0] = rnrm[j][0]; rdir[0][1] = rnrm[j][1]; rdir[0][2] = rnrm[j][2];
       gs_terrain::tangents(rnrm[j], rdir[1], rdir[2]);

@@ -33,14 +33,25 @@ __global__ __launch_bounds__(kBlock) void k_splitk_accum(const void* __restrict_
     if (i0 >= n) return;
     float acc[kVec] = {0.f, 0.f, 0.f, 0.f};
     if (vec) {
-        for (int p = 0; p < P; ++p) {
-            if constexpr (HALF) {
-                const __half2* src = reinterpret_cast<const __half2*>(static_cast<const __half*>(parts) + p * n + i0);
-                const float2 a = __half22float2(src[0]), b = __half22float2(src[1]);
-                acc[0] += a.x; acc[1] += a.y; acc[2] += b.x; acc[3] += b.y;
-            } else {
-                const float4 v = *reinterpret_cast<const float4*>(static_cast<const float*>(parts) + p * n + i0);
-                acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
+        // the partials in batches of 8 loads issued before any is added (one load latency per batch, not per
+        // partial); the additions stay in ascending partial order
+        constexpr int kBatch = 8;
+        for (int p0 = 0; p0 < P; p0 += kBatch) {
+            float4 v[kBatch];
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b) {
+                const int p = p0 + b < P ? p0 + b : P - 1;
+                if constexpr (HALF) {
+                    const __half2* src = reinterpret_cast<const __half2*>(static_cast<const __half*>(parts) + p * n + i0);
+                    const float2 a = __half22float2(src[0]), c = __half22float2(src[1]);
+                    v[b] = make_float4(a.x, a.y, c.x, c.y);
+                } else {
+                    v[b] = *reinterpret_cast<const float4*>(static_cast<const float*>(parts) + p * n + i0);
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b) {
+                if (p0 + b < P) { acc[0] += v[b].x; acc[1] += v[b].y; acc[2] += v[b].z; acc[3] += v[b].w; }
             }
         }
         float4 g = *reinterpret_cast<float4*>(grad + i0);

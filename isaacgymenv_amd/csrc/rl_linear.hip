@@ -34,8 +34,8 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 
 constexpr int kThreads = 256;
-constexpr int kStep = 32;          // reduction step per LDS stage (two MFMA k-steps)
-constexpr int kLd = kStep + 8;     // LDS row stride in halves (80 B): the 32 rows of a fragment read spread banks
+constexpr int kTnStep = 64;        // TN: rows of the reduction per LDS stage (four MFMA k-steps)
+constexpr int kNtStep = 64;        // NT: reduction step per LDS stage (four MFMA k-steps); LDS rows of 72 halves
 
 __device__ __forceinline__ float elu_f(float z) { return z > 0.f ? z : expm1f(z); }
 // torch elu_backward with is_result: y > 0 -> 1, else y + 1 (= exp(z))
@@ -59,34 +59,36 @@ __device__ __forceinline__ h8 load8(const _Float16* __restrict__ p, int valid) {
 
 // ---------------------------------------------------------------- NT: C[m][c] = sum_r A[m][r] Bt[c][r]
 // APRO: A is dZ = dY * elu'(Y) formed on load (A = dY, Ay = Y, both [M][R]).  ACT: ELU epilogue.  bias: fp16 [C]
-// or null.  C fp16 [M][ldc].  M % BM == 0, Cn % BN == 0 (host).
+// or null.  C fp16 [M][ldc].  M % BM == 0, Cn % BN == 0 (host).  The MFMA takes the Bt tile as its row operand,
+// so a lane's result registers 4g .. 4g+3 are 4 consecutive columns c of one row m: one 8-byte store each.
 template <int BM, int BN, bool ACT, bool APRO>
 __global__ __launch_bounds__(kThreads) void k_gemm_nt(const _Float16* __restrict__ A, const _Float16* __restrict__ Ay,
                                                       int lda, const _Float16* __restrict__ Bt, int ldb,
                                                       const _Float16* __restrict__ bias, _Float16* __restrict__ C,
                                                       int ldc, int R) {
   constexpr int TM = BM / 64, TN = BN / 64;                  // MFMA tiles per wave
-  constexpr int CA = BM * kStep / 8 / kThreads, CB = BN * kStep / 8 / kThreads;  // 16-B chunks per thread
+  constexpr int KS = kNtStep, LD = KS + 8, CPR = KS / 8;      // reduction step, LDS row stride, chunks per row
+  constexpr int CA = BM * KS / 8 / kThreads, CB = BN * KS / 8 / kThreads;  // 16-B chunks per thread
   static_assert(CA >= 1 && CB >= 1, "tile too small for the thread block");
-  __shared__ _Float16 sA[2][BM * kLd];
-  __shared__ _Float16 sB[2][BN * kLd];
+  __shared__ _Float16 sA[2][BM * LD];
+  __shared__ _Float16 sB[2][BN * LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.x * BM, c0 = blockIdx.y * BN;
   const int r = lane & 31, hh = lane >> 5;
-  f16v acc[TM][TN];
+  f16v acc[TN][TM];
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int j = 0; j < TN; ++j)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+      for (int q = 0; q < 16; ++q) acc[j][i][q] = 0.f;
 
   h8 ra[CA], rb[CB];
   auto gload = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < CA; ++i) {
-      const int c = tid + i * kThreads, row = c >> 2, kc = (c & 3) * 8;
+      const int c = tid + i * kThreads, row = c / CPR, kc = (c % CPR) * 8;
       const int valid = R - (k0 + kc);
       const size_t off = (size_t)(m0 + row) * lda + k0 + kc;
       h8 v = load8(A + off, valid);
@@ -99,59 +101,70 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(const _Float16* __restrict
     }
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
-      const int c = tid + i * kThreads, row = c >> 2, kc = (c & 3) * 8;
+      const int c = tid + i * kThreads, row = c / CPR, kc = (c % CPR) * 8;
       rb[i] = load8(Bt + (size_t)(c0 + row) * ldb + k0 + kc, R - (k0 + kc));
     }
   };
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < CA; ++i) {
-      const int c = tid + i * kThreads, row = c >> 2, kc = (c & 3) * 8;
-      *reinterpret_cast<h8*>(&sA[buf][row * kLd + kc]) = ra[i];
+      const int c = tid + i * kThreads, row = c / CPR, kc = (c % CPR) * 8;
+      *reinterpret_cast<h8*>(&sA[buf][row * LD + kc]) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
-      const int c = tid + i * kThreads, row = c >> 2, kc = (c & 3) * 8;
-      *reinterpret_cast<h8*>(&sB[buf][row * kLd + kc]) = rb[i];
+      const int c = tid + i * kThreads, row = c / CPR, kc = (c % CPR) * 8;
+      *reinterpret_cast<h8*>(&sB[buf][row * LD + kc]) = rb[i];
     }
   };
-  const int steps = (R + kStep - 1) / kStep;
+  const int steps = (R + KS - 1) / KS;
   gload(0);
   lstore(0);
   __syncthreads();
   for (int s = 0; s < steps; ++s) {
     const int buf = s & 1;
-    if (s + 1 < steps) gload((s + 1) * kStep);
+    if (s + 1 < steps) gload((s + 1) * KS);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KS / 16; ++ks) {
       h8 fa[TM], fb[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        fa[i] = *reinterpret_cast<const h8*>(&sA[buf][(wm * (BM / 2) + i * 32 + r) * kLd + ks * 16 + 8 * hh]);
+        fa[i] = *reinterpret_cast<const h8*>(&sA[buf][(wm * (BM / 2) + i * 32 + r) * LD + ks * 16 + 8 * hh]);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        fb[j] = *reinterpret_cast<const h8*>(&sB[buf][(wn * (BN / 2) + j * 32 + r) * kLd + ks * 16 + 8 * hh]);
+        fb[j] = *reinterpret_cast<const h8*>(&sB[buf][(wn * (BN / 2) + j * 32 + r) * LD + ks * 16 + 8 * hh]);
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < TM; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[j], fa[i], acc[j][i], 0, 0, 0);
     }
     if (s + 1 < steps) lstore(buf ^ 1);
     __syncthreads();
   }
-  // epilogue: + bias, ELU, one rounding to fp16
+  // epilogue: + bias, ELU, one rounding to fp16; registers 4g .. 4g+3 -> columns cg .. cg+3 of row m
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int col = c0 + wn * (BN / 2) + j * 32 + r;
-    const float bv = bias ? (float)bias[col] : 0.f;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+    for (int g = 0; g < 4; ++g) {
+      const int cg = c0 + wn * (BN / 2) + j * 32 + 8 * g + 4 * hh;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (bias) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int row = m0 + wm * (BM / 2) + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * hh;
-        float z = acc[i][j][q] + bv;
-        if constexpr (ACT) z = elu_f(z);
-        C[(size_t)row * ldc + col] = (_Float16)z;
+        for (int e = 0; e < 4; ++e) bv[e] = (float)bias[cg + e];
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm * (BM / 2) + i * 32 + r;
+        _Float16 o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float z = acc[j][i][4 * g + e] + bv[e];
+          if constexpr (ACT) z = elu_f(z);
+          o[e] = (_Float16)z;
+        }
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        const h4 ov = {o[0], o[1], o[2], o[3]};
+        *reinterpret_cast<h4*>(C + (size_t)m * ldc + cg) = ov;
       }
     }
   }
@@ -159,36 +172,56 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(const _Float16* __restrict
 
 // ---------------------------------------------------------------- TN: weight / bias gradient partials
 // part[s][n][k] = sum_{m in block s} dZ[m][n] X[m][k] with dZ = dY * elu'(Y) (dY, Y [M][N], X [M][K]);
-// bpart[s][n] = sum_{m in block s} dZ[m][n] (written by the blocks of k-tile 0).  Tiles 128 (n) x 128 (k);
-// the rows of a block in steps of 32.
+// bpart[s][n] = sum_{m in block s} dZ[m][n] (written by the blocks of k-tile 0); consecutive blocks wstride /
+// bstride floats apart.  Tiles 128 (k) x 128 (n); the rows of a block in stages of 64.  Both operands sum over their ROW
+// index m, so they are staged in LDS as they lie in memory ([m][n], [m][k]: 16-byte stores) and the MFMA fragments
+// (8 consecutive m of one column) come from the hardware transpose read ds_read_b64_tr_b16: lane 4q + p of each
+// 16-lane group addresses row q, columns 4p .. 4p+3 of a 4 x 16 block and receives one column of it.  Row stride
+// 160 halves (320 B): the four rows of a block fall on disjoint bank ranges.  X^T is the MFMA's row operand, so a
+// lane's result registers 4g .. 4g+3 are 4 consecutive k of one n: one 16-byte store each.
 constexpr int kTN = 128;
+constexpr int kTLd = kTN + 32;
+typedef short s4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ h8 tr_frag(const _Float16* tile, int lane) {
+  // the 8 consecutive rows (8h .. 8h+7, h = lane >> 5) of column (lane & 31) of `tile` ([row][kTLd] halves)
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const _Float16* a = tile + (8 * (g >> 1) + q) * kTLd + 16 * (g & 1) + 4 * p;
+  typedef __attribute__((address_space(3))) s4 lds_s4;
+  const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(a));
+  const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(a + 4 * kTLd));
+  const s4 v[2] = {lo, hi};
+  return __builtin_bit_cast(h8, v);
+}
+
 __global__ __launch_bounds__(kThreads) void k_gemm_tn(const _Float16* __restrict__ dY, const _Float16* __restrict__ Y,
                                                       int N, const _Float16* __restrict__ X, int ldx, int K,
                                                       int rows_per_split, float* __restrict__ part,
-                                                      float* __restrict__ bpart) {
-  __shared__ _Float16 sA[2][kTN * kLd];  // [n][m]
-  __shared__ _Float16 sB[2][kTN * kLd];  // [k][m]
-  __shared__ float sbias[16][kTN / 8 * 8 + 1];
+                                                      float* __restrict__ bpart, int64_t wstride, int64_t bstride) {
+  constexpr int TS = kTnStep, CH = TS / 16;  // rows per stage, 16-B chunks per thread per operand
+  __shared__ _Float16 sZ[2][TS * kTLd];  // [m][n]
+  __shared__ _Float16 sX[2][TS * kTLd];  // [m][k]
+  __shared__ float sbias[16][kTN + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wk = wave >> 1, wn = wave & 1;
   const int n0 = blockIdx.x * kTN, k0 = blockIdx.y * kTN, s = blockIdx.z;
   const int mb = s * rows_per_split;
   const int r = lane & 31, hh = lane >> 5;
   const bool do_bias = blockIdx.y == 0 && bpart != nullptr;
-  f16v acc[2][2];
+  f16v acc[2][2];  // [k tile][n tile]
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
-  // each thread: 2 chunks of 8 along n (resp. k) at rows m = tid / 16 and tid / 16 + 16 of the step
+  // each thread: CH chunks of 8 along n (resp. k) at rows m = tid / 16 + 16 i of the stage
   const int crow = tid >> 4, ccol = (tid & 15) * 8;
   float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  h8 ra[2], rb[2];
+  h8 ra[CH], rb[CH];
   auto gload = [&](int m) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < CH; ++i) {
       const size_t row = (size_t)(m + crow + 16 * i);
       const size_t off = row * N + n0 + ccol;
       const h8 g = load8(dY + off, N - (n0 + ccol));
@@ -196,72 +229,66 @@ __global__ __launch_bounds__(kThreads) void k_gemm_tn(const _Float16* __restrict
       h8 z;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float zf = (float)g[j] * elu_d((float)y[j]);
-        z[j] = (_Float16)zf;
+        z[j] = (_Float16)((float)g[j] * elu_d((float)y[j]));
         bsum[j] += (float)z[j];  // the bias gradient sums the same rounded dZ the weight gradient uses
       }
       ra[i] = z;
       rb[i] = load8(X + row * ldx + k0 + ccol, K - (k0 + ccol));
     }
   };
-  auto lstore = [&](int buf) {  // transposed: element j of the chunk to row (col + j), column m
+  auto lstore = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < CH; ++i) {
       const int m = crow + 16 * i;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        sA[buf][(ccol + j) * kLd + m] = ra[i][j];
-        sB[buf][(ccol + j) * kLd + m] = rb[i][j];
-      }
+      *reinterpret_cast<h8*>(&sZ[buf][m * kTLd + ccol]) = ra[i];
+      *reinterpret_cast<h8*>(&sX[buf][m * kTLd + ccol]) = rb[i];
     }
   };
-  const int steps = rows_per_split / kStep;
+  const int steps = rows_per_split / TS;
   gload(mb);
   lstore(0);
   __syncthreads();
   for (int st = 0; st < steps; ++st) {
     const int buf = st & 1;
-    if (st + 1 < steps) gload(mb + (st + 1) * kStep);
+    if (st + 1 < steps) gload(mb + (st + 1) * TS);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      h8 fa[2], fb[2];
+    for (int ks = 0; ks < TS / 16; ++ks) {
+      h8 fx[2], fz[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        fa[i] = *reinterpret_cast<const h8*>(&sA[buf][(wm * 64 + i * 32 + r) * kLd + ks * 16 + 8 * hh]);
+      for (int i = 0; i < 2; ++i) fx[i] = tr_frag(&sX[buf][ks * 16 * kTLd + wk * 64 + i * 32], lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        fb[j] = *reinterpret_cast<const h8*>(&sB[buf][(wn * 64 + j * 32 + r) * kLd + ks * 16 + 8 * hh]);
+      for (int j = 0; j < 2; ++j) fz[j] = tr_frag(&sZ[buf][ks * 16 * kTLd + wn * 64 + j * 32], lane);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fx[i], fz[j], acc[i][j], 0, 0, 0);
     }
     if (st + 1 < steps) lstore(buf ^ 1);
     __syncthreads();
   }
-  float* out = part + (size_t)s * N * K;
+  float* out = part + (size_t)s * wstride;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wn * 64 + j * 32 + r;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int k = k0 + wn * 64 + j * 32 + r;
-      if (k < K) {
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int n = n0 + wm * 64 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * hh;
-          out[(size_t)n * K + k] = acc[i][j][q];
-        }
+      for (int g = 0; g < 4; ++g) {
+        const int k = k0 + wk * 64 + i * 32 + 8 * g + 4 * hh;
+        if (k < K)  // K % 4 == 0: a group of 4 is wholly inside or outside
+          *reinterpret_cast<float4*>(out + (size_t)n * K + k) =
+              make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
       }
-    }
+  }
   if (do_bias) {  // the 16 row groups' sums of each column, added in a fixed order
 #pragma unroll
     for (int j = 0; j < 8; ++j) sbias[crow][ccol + j] = bsum[j];
     __syncthreads();
-    if (tid < kTN && n0 + tid < N) {
+    if (tid < kTN) {
       float t = 0.f;
 #pragma unroll
       for (int g = 0; g < 16; ++g) t += sbias[g][tid];
-      bpart[(size_t)s * N + n0 + tid] = t;
+      bpart[(size_t)s * bstride + n0 + tid] = t;
     }
   }
 }
@@ -300,7 +327,7 @@ int launch_fail(const char* what) {
 extern "C" int rl_linear_fwd(const void* x, int32_t M, int32_t K, int32_t ldx, const void* w, int32_t N,
                              const void* bias, int32_t act, void* y, void* stream) {
   if (!x || !w || !y || M <= 0 || K <= 0 || N <= 0) return rl_set_error("rl_linear_fwd: null pointer or empty shape");
-  if (M % 64 || N % 128 || ldx % 4 || K % 4 || !aligned8(x) || !aligned8(w))
+  if (M % 64 || N % 128 || ldx % 4 || K % 4 || !aligned8(x) || !aligned8(w) || !aligned8(y))
     return rl_set_error("rl_linear_fwd: M % 64, N % 128, K % 4 and 8-byte aligned rows required");
   hipStream_t st = (hipStream_t)stream;
   const auto* X = static_cast<const _Float16*>(x);
@@ -329,17 +356,19 @@ extern "C" int rl_linear_transpose(const void* w, int32_t N, int32_t K, void* wt
 
 extern "C" int rl_linear_bwd(const void* dy, const void* y, int32_t M, int32_t N, const void* x, int32_t K,
                              int32_t ldx, const void* wt, void* dx, int32_t splits, float* wpart, float* bpart,
-                             void* stream) {
+                             int64_t pstride, void* stream) {
   if (!dy || !y || !x || M <= 0 || N <= 0 || K <= 0) return rl_set_error("rl_linear_bwd: null pointer or empty shape");
   if (M % 128 || N % 128 || K % 4 || ldx % 4 || !aligned8(dy) || !aligned8(y) || !aligned8(x))
     return rl_set_error("rl_linear_bwd: M % 128, N % 128, K % 4 and 8-byte aligned rows required");
-  if (splits <= 0 || M % (splits * kStep) != 0) return rl_set_error("rl_linear_bwd: M must split into multiples of 32 rows");
+  if (splits <= 0 || M % (splits * kTnStep) != 0)
+    return rl_set_error("rl_linear_bwd: M must split into row blocks of multiples of 64");
   hipStream_t st = (hipStream_t)stream;
   const auto* DY = static_cast<const _Float16*>(dy);
   const auto* Yv = static_cast<const _Float16*>(y);
   const auto* X = static_cast<const _Float16*>(x);
   if (dx) {
-    if (!wt || !aligned8(wt) || K % 128) return rl_set_error("rl_linear_bwd: dX needs W^T and K % 128");
+    if (!wt || !aligned8(wt) || !aligned8(dx) || K % 128)
+      return rl_set_error("rl_linear_bwd: dX needs W^T, 8-byte aligned rows and K % 128");
     const auto* WT = static_cast<const _Float16*>(wt);
     auto* DX = static_cast<_Float16*>(dx);
     if ((M / 128) * (K / 128) >= 256) {
@@ -352,8 +381,13 @@ extern "C" int rl_linear_bwd(const void* dy, const void* y, int32_t M, int32_t N
     if (int rc = launch_fail("rl_linear_bwd (dX)")) return rc;
   }
   if (wpart) {
+    // pstride 0: wpart [splits][N][K], bpart [splits][N]; else both advance pstride floats per block (the merged
+    // layout: each block's bias partials right behind its weight partials, pstride = N*K + N)
+    const int64_t ws = pstride ? pstride : (int64_t)N * K, bs = pstride ? pstride : (int64_t)N;
+    if ((reinterpret_cast<uintptr_t>(wpart) & 15) || ws % 4 || ws < (int64_t)N * K)
+      return rl_set_error("rl_linear_bwd: weight partials need 16-byte alignment and a block stride >= N*K, % 4");
     hipLaunchKernelGGL(k_gemm_tn, dim3(N / kTN, (K + kTN - 1) / kTN, splits), dim3(kThreads), 0, st, DY, Yv, N, X, ldx,
-                       K, M / splits, wpart, bpart);
+                       K, M / splits, wpart, bpart, ws, bs);
     return launch_fail("rl_linear_bwd (dW)");
   }
   return 0;

@@ -8,6 +8,7 @@ default init (rl_games ``default`` initializer = identity), biases are zeroed, a
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List
 
 import torch
@@ -26,7 +27,7 @@ _ACT = {"elu": nn.ELU, "relu": nn.ReLU, "tanh": nn.Tanh, "selu": nn.SELU, "None"
 # The hidden Linear + ELU layers under fp16 autocast (the learner's minibatch forward / backward) run on the matrix
 # cores as libgymrl's rl_linear_* kernels (csrc/rl_linear.hip): bias and ELU fused into the GEMM epilogue, ELU's
 # backward fused into the dX / dW GEMMs' operand loads.  Off: the torch Linear / ELU statements above.
-USE_MFMA_LAYERS = True
+USE_MFMA_LAYERS = os.environ.get("IGE_MFMA_LAYERS", "1") != "0"  # (an A/B switch for the bench)
 SPLIT_K = 16
 SPLIT_K_MIN_ROWS = 4096
 
@@ -157,12 +158,27 @@ class _LinearELUFn(torch.autograd.Function):
         want_w = ctx.needs_input_grad[1]
         want_b = ctx.b is not None and ctx.needs_input_grad[2]
         splits = _splits(M, (N // 128) * ((K + 127) // 128))
+        gw = gb = None
+        w, b = ctx.w, ctx.b
+        if ctx.direct and want_w and want_b:
+            for p in (w, b):
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p, dtype=torch.float32)
+        merged = (ctx.direct and want_w and want_b and w.grad.is_contiguous() and b.grad.is_contiguous()
+                  and b.grad.data_ptr() == w.grad.data_ptr() + 4 * N * K)
+        if merged:
+            # the learner's flat gradient keeps a Linear's weight and bias adjacent: ONE partial buffer [S][N*K + N]
+            # and one finish over both (rl_linear_bwd's merged layout)
+            part = torch.empty(splits, N * K + N, dtype=torch.float32, device=dev)
+            gae.linear_bwd(gy, y, xc, wt, dx, splits, part, part[:, N * K:], pstride=N * K + N)
+            span = w.grad.new_empty(0).set_(w.grad.untyped_storage(), w.grad.storage_offset(), (N * K + N,), (1,))
+            gae.splitk_accum(part, span)
+            return dx, None, None, None, None, None
         wpart = torch.empty(splits, N, K, dtype=torch.float32, device=dev) if want_w or want_b else None
         bpart = torch.empty(splits, N, dtype=torch.float32, device=dev) if want_b else None
         if dx is not None or wpart is not None:
             gae.linear_bwd(gy, y, xc, wt, dx, splits, wpart, bpart)
-        gw = gb = None
-        for want, p, part, slot in ((want_w, ctx.w, wpart, 0), (want_b, ctx.b, bpart, 1)):
+        for want, p, part, slot in ((want_w, w, wpart, 0), (want_b, b, bpart, 1)):
             if not want:
                 continue
             if ctx.direct:

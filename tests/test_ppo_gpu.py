@@ -498,6 +498,11 @@ def test_linear_kernels_exact_on_integers(M):
             blk = slice(s_ * rows, (s_ + 1) * rows)
             assert torch.equal(wpart[s_].double(), dz[blk].T @ xw[blk].double()), s_
             assert torch.equal(bpart[s_].double(), dz[blk].sum(0)), s_
+        # the merged layout: each block's bias partials right behind its weight partials
+        part = torch.full((splits, N * K + N), float("nan"), device="cuda")
+        gae.linear_bwd(dy, yv, xw, None, None, splits, part, part[:, N * K:], pstride=N * K + N)
+        assert torch.equal(part[:, :N * K].reshape(splits, N, K), wpart)
+        assert torch.equal(part[:, N * K:], bpart)
 
 
 def test_linear_kernels_reject_untileable_shapes():

@@ -86,12 +86,17 @@ def main():
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--out", default=None)
     ap.add_argument("--self-collide", type=int, default=1, help="0: ANYmal's self-collision pairs off")
+    ap.add_argument("--no-velocity-limit", action="store_true",
+                    help="drop the URDF joint velocity limit (20 rad/s): the round-4 diagnosis of the TGS divergence")
     a = ap.parse_args()
     art, flat = H.anymal()
     flat["self_collide"] = a.self_collide
+    if a.no_velocity_limit:
+        flat["vmax"] = np.zeros_like(np.asarray(flat["vmax"], dtype=np.float64))  # <= 0: unlimited
     base = dict(H.ANYMAL_PARAMS)
     out = {"config": dict(envs=a.envs, env_steps=a.steps, dt=base["dt"], pos_iters=base["pos_iters"],
-                          vel_iters=base["vel_iters"], decimation=DECIMATION, self_collide=int(flat["self_collide"]))}
+                          vel_iters=base["vel_iters"], decimation=DECIMATION, self_collide=int(flat["self_collide"]),
+                          joint_velocity_limit=not a.no_velocity_limit)}
     t0 = time.time()
     for scen in ("standing", "locomotion"):
         root, dof, mu, default = start_states(art, flat, a.envs, seed=3)
