@@ -168,9 +168,9 @@ int rl_opt_partials_size(void);
  *
  * rl_linear_fwd: y [M][N] fp16 = act(x [M][K] (row stride ldx) . w[N][K]^T + bias [N] fp16 (null: none)), act 1 =
  *   ELU (alpha 1), 0 = none.  M % 64 == 0, N % 128 == 0, K and ldx % 4 == 0, 8-byte aligned rows.
- * rl_linear_transpose: w [N][K] fp16 -> wt [K][N] fp16.
+ * rl_linear_transpose: w [N][K] fp16 -> wt [K][N] fp16 (a utility; the backward reads w itself).
  * rl_linear_bwd: the backward of rl_linear_fwd with ELU from its output y: dZ = dy * (y > 0 ? 1 : y + 1);
- *   dx [M][K] fp16 = dZ . w (from wt = w^T; null dx: skipped; needs K % 128 == 0);
+ *   dx [M][K] fp16 = dZ . w (w [N][K] as in rl_linear_fwd; null dx: skipped; needs K % 128 == 0);
  *   wpart [splits][N][K] f32 = per row block of M / splits rows, dZ^T . x; bpart [splits][N] f32 = column sums of
  *   dZ (null: skipped); pstride 0 = those layouts, else block s of both starts s * pstride floats in (the merged
  *   layout bpart = wpart + N*K, pstride = N*K + N: one rl_splitk_accum finishes a weight and its bias when their
@@ -181,7 +181,7 @@ int rl_linear_fwd(const void *x, int32_t M, int32_t K, int32_t ldx, const void *
                   int32_t act, void *y, void *stream);
 int rl_linear_transpose(const void *w, int32_t N, int32_t K, void *wt, void *stream);
 int rl_linear_bwd(const void *dy, const void *y, int32_t M, int32_t N, const void *x, int32_t K, int32_t ldx,
-                  const void *wt, void *dx, int32_t splits, float *wpart, float *bpart, int64_t pstride, void *stream);
+                  const void *w, void *dx, int32_t splits, float *wpart, float *bpart, int64_t pstride, void *stream);
 
 #ifdef __cplusplus
 }

@@ -6,7 +6,7 @@
 // split-K weight-gradient GEMM with its finish (network.py).  Here a layer is:
 //   forward   Y  = ELU(X W^T + b)                     one kernel (k_gemm_nt<ELU>), bias and ELU in the epilogue
 //   backward  dZ = dY * ELU'(Y)  (ELU' = 1 for Y > 0, Y + 1 otherwise: torch's elu_backward on the result)
-//             dX = dZ W                               k_gemm_nt<prologue dZ> on W^T (k_transpose_f16)
+//             dX = dZ W                               k_gemm_nn (dZ formed on load, W through transpose reads)
 //             dW = dZ^T X, db = colsum dZ             k_gemm_tn: S row-block partials [S][N][K] / [S][N] in f32,
 //                                                     finished in a fixed order by rl_splitk_accum (rl_grad.hip)
 // Operands fp16, accumulation f32 (v_mfma_f32_32x32x16_f16), outputs rounded once to fp16 (Y, dX) or kept f32
@@ -58,11 +58,10 @@ __device__ __forceinline__ h8 load8(const _Float16* __restrict__ p, int valid) {
 }
 
 // ---------------------------------------------------------------- NT: C[m][c] = sum_r A[m][r] Bt[c][r]
-// APRO: A is dZ = dY * elu'(Y) formed on load (A = dY, Ay = Y, both [M][R]).  ACT: ELU epilogue.  bias: fp16 [C]
-// or null.  C fp16 [M][ldc].  M % BM == 0, Cn % BN == 0 (host).  The MFMA takes the Bt tile as its row operand,
+// ACT: ELU epilogue.  bias: fp16 [C] or null.  C fp16 [M][ldc].  M % BM == 0, Cn % BN == 0 (host).  The MFMA takes the Bt tile as its row operand,
 // so a lane's result registers 4g .. 4g+3 are 4 consecutive columns c of one row m: one 8-byte store each.
-template <int BM, int BN, bool ACT, bool APRO>
-__global__ __launch_bounds__(kThreads) void k_gemm_nt(const _Float16* __restrict__ A, const _Float16* __restrict__ Ay,
+template <int BM, int BN, bool ACT>
+__global__ __launch_bounds__(kThreads) void k_gemm_nt(const _Float16* __restrict__ A,
                                                       int lda, const _Float16* __restrict__ Bt, int ldb,
                                                       const _Float16* __restrict__ bias, _Float16* __restrict__ C,
                                                       int ldc, int R) {
@@ -91,13 +90,7 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(const _Float16* __restrict
       const int c = tid + i * kThreads, row = c / CPR, kc = (c % CPR) * 8;
       const int valid = R - (k0 + kc);
       const size_t off = (size_t)(m0 + row) * lda + k0 + kc;
-      h8 v = load8(A + off, valid);
-      if constexpr (APRO) {
-        const h8 y = load8(Ay + off, valid);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (_Float16)((float)v[j] * elu_d((float)y[j]));
-      }
-      ra[i] = v;
+      ra[i] = load8(A + off, valid);
     }
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
@@ -293,6 +286,101 @@ __global__ __launch_bounds__(kThreads) void k_gemm_tn(const _Float16* __restrict
   }
 }
 
+// ---------------------------------------------------------------- NN: dX[m][k] = sum_n dZ[m][n] W[n][k]
+// dZ = dY * elu'(Y) formed on load (dY, Y [M][N]); W [N][K] as the forward uses it, staged in LDS as it lies
+// ([n][k], 16-byte stores) and read with the transpose read (8 consecutive n of one k per lane), so no W^T copy
+// is needed.  As in k_gemm_nt the k rows are the MFMA's row operand: registers 4g .. 4g+3 are 4 consecutive k of
+// one row m, one 8-byte store.  M % BM == 0, K % 128 == 0 (host).
+template <int BM>
+__global__ __launch_bounds__(kThreads) void k_gemm_nn(const _Float16* __restrict__ dY, const _Float16* __restrict__ Y,
+                                                      int N, const _Float16* __restrict__ W, int K,
+                                                      _Float16* __restrict__ dX) {
+  constexpr int BN = 128, TM = BM / 64, TN = BN / 64;
+  constexpr int KS = kNtStep, LD = KS + 8, CPR = KS / 8;
+  constexpr int CA = BM * KS / 8 / kThreads, CB = KS * BN / 8 / kThreads;
+  __shared__ _Float16 sA[2][BM * LD];     // [m][n]
+  __shared__ _Float16 sB[2][KS * kTLd];   // [n][k]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * BM, c0 = blockIdx.y * BN;
+  const int r = lane & 31, hh = lane >> 5;
+  f16v acc[TN][TM];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[j][i][q] = 0.f;
+  h8 ra[CA], rb[CB];
+  auto gload = [&](int n0) {
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int c = tid + i * kThreads, row = c / CPR, kc = (c % CPR) * 8;
+      const int valid = N - (n0 + kc);
+      const size_t off = (size_t)(m0 + row) * N + n0 + kc;
+      h8 v = load8(dY + off, valid);
+      const h8 y = load8(Y + off, valid);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (_Float16)((float)v[j] * elu_d((float)y[j]));
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const int c = tid + i * kThreads, row = c >> 4, kc = (c & 15) * 8;
+      rb[i] = n0 + row < N ? load8(W + (size_t)(n0 + row) * K + c0 + kc, 8) : h8{};
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int c = tid + i * kThreads, row = c / CPR, kc = (c % CPR) * 8;
+      *reinterpret_cast<h8*>(&sA[buf][row * LD + kc]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const int c = tid + i * kThreads, row = c >> 4, kc = (c & 15) * 8;
+      *reinterpret_cast<h8*>(&sB[buf][row * kTLd + kc]) = rb[i];
+    }
+  };
+  const int steps = (N + KS - 1) / KS;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int s = 0; s < steps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < steps) gload((s + 1) * KS);
+#pragma unroll
+    for (int ks = 0; ks < KS / 16; ++ks) {
+      h8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const h8*>(&sA[buf][(wm * (BM / 2) + i * 32 + r) * LD + ks * 16 + 8 * hh]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = tr_frag(&sB[buf][ks * 16 * kTLd + wn * (BN / 2) + j * 32], lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[j], fa[i], acc[j][i], 0, 0, 0);
+    }
+    if (s + 1 < steps) lstore(buf ^ 1);
+    __syncthreads();
+  }
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int cg = c0 + wn * (BN / 2) + j * 32 + 8 * g + 4 * hh;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm * (BM / 2) + i * 32 + r;
+        const h4 ov = {(_Float16)acc[j][i][4 * g], (_Float16)acc[j][i][4 * g + 1], (_Float16)acc[j][i][4 * g + 2],
+                       (_Float16)acc[j][i][4 * g + 3]};
+        *reinterpret_cast<h4*>(dX + (size_t)m * K + cg) = ov;
+      }
+    }
+}
+
 // W [N][K] fp16 -> W^T [K][N] fp16 (32 x 32 tiles through LDS)
 __global__ __launch_bounds__(256) void k_transpose_f16(const _Float16* __restrict__ w, int N, int K,
                                                        _Float16* __restrict__ wt) {
@@ -337,12 +425,12 @@ extern "C" int rl_linear_fwd(const void* x, int32_t M, int32_t K, int32_t ldx, c
   // 128 x 128 tiles when that still gives >= 256 workgroups, else 64-row tiles
   if ((M / 128) * (N / 128) >= 256 && M % 128 == 0) {
     const dim3 g(M / 128, N / 128);
-    if (act) hipLaunchKernelGGL((k_gemm_nt<128, 128, true, false>), g, dim3(kThreads), 0, st, X, nullptr, ldx, W, K, B, Y, N, K);
-    else hipLaunchKernelGGL((k_gemm_nt<128, 128, false, false>), g, dim3(kThreads), 0, st, X, nullptr, ldx, W, K, B, Y, N, K);
+    if (act) hipLaunchKernelGGL((k_gemm_nt<128, 128, true>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, N, K);
+    else hipLaunchKernelGGL((k_gemm_nt<128, 128, false>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, N, K);
   } else {
     const dim3 g(M / 64, N / 128);
-    if (act) hipLaunchKernelGGL((k_gemm_nt<64, 128, true, false>), g, dim3(kThreads), 0, st, X, nullptr, ldx, W, K, B, Y, N, K);
-    else hipLaunchKernelGGL((k_gemm_nt<64, 128, false, false>), g, dim3(kThreads), 0, st, X, nullptr, ldx, W, K, B, Y, N, K);
+    if (act) hipLaunchKernelGGL((k_gemm_nt<64, 128, true>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, N, K);
+    else hipLaunchKernelGGL((k_gemm_nt<64, 128, false>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, N, K);
   }
   return launch_fail("rl_linear_fwd");
 }
@@ -355,7 +443,7 @@ extern "C" int rl_linear_transpose(const void* w, int32_t N, int32_t K, void* wt
 }
 
 extern "C" int rl_linear_bwd(const void* dy, const void* y, int32_t M, int32_t N, const void* x, int32_t K,
-                             int32_t ldx, const void* wt, void* dx, int32_t splits, float* wpart, float* bpart,
+                             int32_t ldx, const void* w, void* dx, int32_t splits, float* wpart, float* bpart,
                              int64_t pstride, void* stream) {
   if (!dy || !y || !x || M <= 0 || N <= 0 || K <= 0) return rl_set_error("rl_linear_bwd: null pointer or empty shape");
   if (M % 128 || N % 128 || K % 4 || ldx % 4 || !aligned8(dy) || !aligned8(y) || !aligned8(x))
@@ -367,17 +455,14 @@ extern "C" int rl_linear_bwd(const void* dy, const void* y, int32_t M, int32_t N
   const auto* Yv = static_cast<const _Float16*>(y);
   const auto* X = static_cast<const _Float16*>(x);
   if (dx) {
-    if (!wt || !aligned8(wt) || !aligned8(dx) || K % 128)
-      return rl_set_error("rl_linear_bwd: dX needs W^T, 8-byte aligned rows and K % 128");
-    const auto* WT = static_cast<const _Float16*>(wt);
+    if (!w || !aligned8(w) || !aligned8(dx) || K % 128)
+      return rl_set_error("rl_linear_bwd: dX needs W, 8-byte aligned rows and K % 128");
+    const auto* Wp = static_cast<const _Float16*>(w);
     auto* DX = static_cast<_Float16*>(dx);
-    if ((M / 128) * (K / 128) >= 256) {
-      hipLaunchKernelGGL((k_gemm_nt<128, 128, false, true>), dim3(M / 128, K / 128), dim3(kThreads), 0, st, DY, Yv, N,
-                         WT, N, nullptr, DX, K, N);
-    } else {
-      hipLaunchKernelGGL((k_gemm_nt<64, 128, false, true>), dim3(M / 64, K / 128), dim3(kThreads), 0, st, DY, Yv, N,
-                         WT, N, nullptr, DX, K, N);
-    }
+    if ((M / 128) * (K / 128) >= 256)
+      hipLaunchKernelGGL((k_gemm_nn<128>), dim3(M / 128, K / 128), dim3(kThreads), 0, st, DY, Yv, N, Wp, K, DX);
+    else
+      hipLaunchKernelGGL((k_gemm_nn<64>), dim3(M / 64, K / 128), dim3(kThreads), 0, st, DY, Yv, N, Wp, K, DX);
     if (int rc = launch_fail("rl_linear_bwd (dX)")) return rc;
   }
   if (wpart) {

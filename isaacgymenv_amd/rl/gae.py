@@ -332,14 +332,14 @@ def linear_transpose(w_half, out):
            "rl_linear_transpose")
 
 
-def linear_bwd(dy, y, x, wt, dx, splits: int, wpart, bpart, pstride: int = 0):
-    """rl_linear_bwd: dx = (dy * elu'(y)) . w (wt = w^T, dx None: skipped); wpart [splits, N, K] / bpart [splits, N]
+def linear_bwd(dy, y, x, w, dx, splits: int, wpart, bpart, pstride: int = 0):
+    """rl_linear_bwd: dx = (dy * elu'(y)) . w (w [N, K] fp16, dx None: skipped); wpart [splits, N, K] / bpart [splits, N]
     f32 row-block partials of the weight / bias gradients (finish with splitk_accum); pstride != 0: both are
     tensors / views whose blocks lie pstride floats apart (the merged [splits, N*K + N] layout)."""
     M, N = dy.shape
     K = x.shape[1]
     _check(lib().rl_linear_bwd(dy.data_ptr(), y.data_ptr(), M, N, x.data_ptr(), K, x.stride(0),
-                               wt.data_ptr() if wt is not None else None, dx.data_ptr() if dx is not None else None,
+                               w.data_ptr() if w is not None else None, dx.data_ptr() if dx is not None else None,
                                splits, wpart.data_ptr() if wpart is not None else None,
                                bpart.data_ptr() if bpart is not None else None, int(pstride),
                                torch.cuda.current_stream().cuda_stream), "rl_linear_bwd")

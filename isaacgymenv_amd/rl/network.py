@@ -150,10 +150,8 @@ class _LinearELUFn(torch.autograd.Function):
         M, N = y.shape
         K = xc.shape[1]
         dev = y.device
-        dx = wt = None
+        dx = None
         if ctx.needs_input_grad[0]:
-            wt = torch.empty(K, N, dtype=torch.float16, device=dev)
-            gae.linear_transpose(wc, wt)
             dx = torch.empty(M, K, dtype=torch.float16, device=dev)
         want_w = ctx.needs_input_grad[1]
         want_b = ctx.b is not None and ctx.needs_input_grad[2]
@@ -170,14 +168,14 @@ class _LinearELUFn(torch.autograd.Function):
             # the learner's flat gradient keeps a Linear's weight and bias adjacent: ONE partial buffer [S][N*K + N]
             # and one finish over both (rl_linear_bwd's merged layout)
             part = torch.empty(splits, N * K + N, dtype=torch.float32, device=dev)
-            gae.linear_bwd(gy, y, xc, wt, dx, splits, part, part[:, N * K:], pstride=N * K + N)
+            gae.linear_bwd(gy, y, xc, wc, dx, splits, part, part[:, N * K:], pstride=N * K + N)
             span = w.grad.new_empty(0).set_(w.grad.untyped_storage(), w.grad.storage_offset(), (N * K + N,), (1,))
             gae.splitk_accum(part, span)
             return dx, None, None, None, None, None
         wpart = torch.empty(splits, N, K, dtype=torch.float32, device=dev) if want_w or want_b else None
         bpart = torch.empty(splits, N, dtype=torch.float32, device=dev) if want_b else None
         if dx is not None or wpart is not None:
-            gae.linear_bwd(gy, y, xc, wt, dx, splits, wpart, bpart)
+            gae.linear_bwd(gy, y, xc, wc, dx, splits, wpart, bpart)
         for want, p, part, slot in ((want_w, w, wpart, 0), (want_b, b, bpart, 1)):
             if not want:
                 continue

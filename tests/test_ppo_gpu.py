@@ -490,7 +490,7 @@ def test_linear_kernels_exact_on_integers(M):
         dx = torch.empty(M, K, dtype=torch.float16, device="cuda") if want_dx else None
         wpart = torch.empty(splits, N, K, device="cuda")
         bpart = torch.empty(splits, N, device="cuda")
-        gae.linear_bwd(dy, yv, xw, wt if want_dx else None, dx, splits, wpart, bpart)
+        gae.linear_bwd(dy, yv, xw, wv if want_dx else None, dx, splits, wpart, bpart)
         rows = M // splits
         if want_dx:
             assert torch.equal(dx.double(), dz @ wv.double())
@@ -513,7 +513,7 @@ def test_linear_kernels_reject_untileable_shapes():
         gae.linear_fwd(x, w, None, True, torch.empty(100, 128, dtype=torch.float16, device="cuda"))
     y = torch.zeros(128, 128, dtype=torch.float16, device="cuda")
     with pytest.raises(RuntimeError, match="K % 128"):
-        gae.linear_bwd(y, y, torch.zeros(128, 64, dtype=torch.float16, device="cuda"), w.T.contiguous(), torch.empty(128, 64, dtype=torch.float16,
+        gae.linear_bwd(y, y, torch.zeros(128, 64, dtype=torch.float16, device="cuda"), w, torch.empty(128, 64, dtype=torch.float16,
                        device="cuda"), 1, torch.empty(1, 128, 64, device="cuda"), None)
 
 

@@ -51,7 +51,7 @@ def main():
         r["fwd_torch"] = timed(lambda: torch.nn.functional.elu(torch.nn.functional.linear(x, w, b)))
         r["transpose"] = timed(lambda: gae.linear_transpose(w, wt))
         if K % 128 == 0:
-            r["dx_mfma"] = timed(lambda: gae.linear_bwd(dy, y, x, wt, dx, splits, None, None))
+            r["dx_mfma"] = timed(lambda: gae.linear_bwd(dy, y, x, w, dx, splits, None, None))
         r["dw_mfma"] = timed(lambda: gae.linear_bwd(dy, y, x, None, None, splits, part, part[:, N * K:], N * K + N))
         r["accum"] = timed(lambda: gae.splitk_accum(part, gacc))
 
@@ -63,7 +63,7 @@ def main():
             p.sum(0, dtype=torch.float32)
             dz.sum(0, dtype=torch.float32)
         r["bwd_torch"] = timed(torch_bwd)
-        r["bwd_mfma_total"] = r["transpose"] * (K % 128 == 0) + r.get("dx_mfma", 0.0) + r["dw_mfma"] + r["accum"]
+        r["bwd_mfma_total"] = r.get("dx_mfma", 0.0) + r["dw_mfma"] + r["accum"]
         flops = 2 * M * N * K
         r["fwd_mfma_tflops"] = flops / r["fwd_mfma"] / 1e6
         r["dw_mfma_tflops"] = flops / r["dw_mfma"] / 1e6
