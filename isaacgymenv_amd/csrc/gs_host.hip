@@ -100,7 +100,7 @@ void host_terrain_query(const DevParams& P, const float* c, const float* r, int 
   for (int t = 0; t < n; ++t) {
     const float p[3] = {c[3 * t], c[3 * t + 1], c[3 * t + 2]};
     float sep = 0.f, nn[3] = {0.f, 0.f, 0.f};
-    const bool f = gs_terrain::sphere_contact<true>(P.terr, p, r[t], r[t] + P.contact_offset, sep, nn);
+    const bool f = gs_terrain::sphere_contact(P.terr, p, r[t], r[t] + P.contact_offset, sep, nn);
     out[5 * t] = f ? 1.f : 0.f;
     out[5 * t + 1] = sep;
     out[5 * t + 2] = nn[0]; out[5 * t + 3] = nn[1]; out[5 * t + 4] = nn[2];

@@ -631,7 +631,7 @@ __device__ __forceinline__ float terrain_candidate(const DevParams& P, const flo
   nrm[0] = 0.f; nrm[1] = 0.f; nrm[2] = 1.f;
   smu = P.ground_mu;
   float st, nt[3];
-  if (gs_terrain::sphere_contact<true>(P.terr, cw, r, r + P.contact_offset, st, nt) && st < dist) {
+  if (gs_terrain::sphere_contact(P.terr, cw, r, r + P.contact_offset, st, nt) && st < dist) {
     dist = st;
     nrm[0] = nt[0]; nrm[1] = nt[1]; nrm[2] = nt[2];
     smu = P.terr.mu;

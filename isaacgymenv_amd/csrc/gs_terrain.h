@@ -147,11 +147,6 @@ GS_HD void triangle(const float* p, float r, float thr, const float4& A, const f
 }
 
 // Closest admissible mesh surface for sphere (p, r); false when none lies within thr.
-// PATCH (the lane-team kernel, whose queries run while little else is live): when the 3 x 3 cells around the
-// centre lie inside the grid, their cell words and the 4 x 4 vertices they use are loaded in two batches up front,
-// and the cells of that neighbourhood are tested from registers -- same tests, same order, so the same result; a
-// wave pays two load latencies per query instead of one per row and one per tested cell.
-template <bool PATCH = false>
 GS_HD bool sphere_contact(const TerrainDev& T, const float* p, float r, float thr, float& sep,
                                                float* n) {
   // horizontal reach: a face can be admitted from behind up to r + TERRAIN_BACK away (walls)
@@ -162,23 +157,19 @@ GS_HD bool sphere_contact(const TerrainDev& T, const float* p, float r, float th
   float best = 3.0e38f, bkey = 3.0e38f;
   const float zlo = p[2] - thr;
   const float pad = 1e-4f * T.hs;
-  // one cell given its info word: the culling tests (false: skipped), then its two triangles
-  auto cell_tests = [&](int i, int j, const uint4& cinfo) -> bool {
+  // one cell given its info word: the culling tests, then its two triangles
+  auto cell = [&](int i, int j, const uint4& cinfo) {
     const float top = gs_bits_float(cinfo.x);
-    if (zlo > top) return false;
+    if (zlo > top) return;
     const uint32_t f = cinfo.y;
     const float cx0 = T.x0 + (float)i * T.hs, cy0 = T.y0 + (float)j * T.hs;
     const float bx0 = cx0 - ((f & TCELL_XLO) ? T.hs : 0.f), bx1 = cx0 + ((f & TCELL_XHI) ? 2.f : 1.f) * T.hs;
     const float by0 = cy0 - ((f & TCELL_YLO) ? T.hs : 0.f), by1 = cy0 + ((f & TCELL_YHI) ? 2.f : 1.f) * T.hs;
-    if (p[0] + reach < bx0 || p[0] - reach > bx1 || p[1] + reach < by0 || p[1] - reach > by1) return false;
+    if (p[0] + reach < bx0 || p[0] - reach > bx1 || p[1] + reach < by0 || p[1] - reach > by1) return;
     const float dx = fmaxf(fmaxf(bx0 - pad - p[0], p[0] - bx1 - pad), 0.f);
     const float dy = fmaxf(fmaxf(by0 - pad - p[1], p[1] - by1 - pad), 0.f);
     const float dz = fmaxf(fmaxf(gs_bits_float(cinfo.z) - pad - p[2], p[2] - top - pad), 0.f);
-    if (dx * dx + dy * dy + dz * dz >= bkey * bkey) return false;
-    return true;
-  };
-  auto cell = [&](int i, int j, const uint4& cinfo) {
-    if (!cell_tests(i, j, cinfo)) return;
+    if (dx * dx + dy * dy + dz * dz >= bkey * bkey) return;
     const size_t v0 = (size_t)i * T.cols + j;
     const float4 v00 = T.v[v0], v01 = T.v[v0 + 1], v10 = T.v[v0 + T.cols], v11 = T.v[v0 + T.cols + 1];
     triangle(p, r, thr, v00, v11, v01, bkey, best, n);
@@ -204,31 +195,7 @@ GS_HD bool sphere_contact(const TerrainDev& T, const float* p, float r, float th
   }
   const int ic = (int)floorf(gx), jc = (int)floorf(gy);
   const bool centre = ic >= 0 && ic <= T.rows - 2 && jc >= 0 && jc <= T.cols - 2;
-  // the 3 x 3 neighbourhood from registers (PATCH): w[a][b] = word of cell (ic-1+a, jc-1+b), pv[a][b] = vertex
-  // (ic-1+a, jc-1+b)
-  const bool patch = PATCH && ic >= 1 && jc >= 1 && ic + 1 <= T.rows - 2 && jc + 1 <= T.cols - 2;
-  uint4 w[PATCH ? 3 : 1][PATCH ? 3 : 1];
-  float4 pv[PATCH ? 4 : 1][PATCH ? 4 : 1];
-  // (a, b) compile-time after unrolling: the patch stays in registers
-  auto patch_cell = [&](int a, int b) {
-    if (!cell_tests(ic - 1 + a, jc - 1 + b, w[a][b])) return;
-    triangle(p, r, thr, pv[a][b], pv[a + 1][b + 1], pv[a][b + 1], bkey, best, n);
-    triangle(p, r, thr, pv[a][b], pv[a + 1][b], pv[a + 1][b + 1], bkey, best, n);
-  };
-  if constexpr (PATCH) {
-    if (patch) {
-#pragma unroll
-      for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b) w[a][b] = T.cell[(size_t)(ic - 1 + a) * (T.cols - 1) + jc - 1 + b];
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) pv[a][b] = T.v[(size_t)(ic - 1 + a) * T.cols + jc - 1 + b];
-      patch_cell(1, 1);
-    }
-  }
-  if (centre && !patch) cell(ic, jc, T.cell[(size_t)ic * (T.cols - 1) + jc]);
+  if (centre) cell(ic, jc, T.cell[(size_t)ic * (T.cols - 1) + jc]);
   // (2) the rest in (i, j) order.  Before loading a cell's word, its widest possible footprint (one cell further
   //     on every side, plus a margin far above the float rounding of the coordinates) is tested against the
   //     reach and the best key: cells beyond it are skipped unread, whole rows at once.  A row's remaining cell
@@ -252,21 +219,6 @@ GS_HD bool sphere_contact(const TerrainDev& T, const float* p, float r, float th
     int ja = j0, jz = j1;
     while (ja <= jz && unread(ja)) ++ja;
     while (jz >= ja && unread(jz)) --jz;
-    if constexpr (PATCH) {
-      if (patch && i >= ic - 1 && i <= ic + 1 && ja >= jc - 1 && jz <= jc + 1) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-          if (i == ic - 1 + a) {
-#pragma unroll
-            for (int b = 0; b < 3; ++b) {
-              const int j = jc - 1 + b;
-              if (j >= ja && j <= jz && !(a == 1 && b == 1)) patch_cell(a, b);
-            }
-          }
-        }
-        continue;
-      }
-    }
     const uint4* crow = T.cell + (size_t)i * (T.cols - 1);
     for (int jb = ja; jb <= jz; jb += kRowBatch) {
       uint4 cw[kRowBatch];

@@ -159,45 +159,6 @@ def test_rough_trimesh_matches_oracle():
                mu, "rough trimesh host", terrain=ter["oracle"])
 
 
-def test_terrain_query_register_patch_matches_oracle():
-    """The terrain query's register-patch form (gs_terrain.h sphere_contact<PATCH>: the lane-team kernel's form,
-    also behind the host debug hook) against the oracle's independent statement, 200k spheres over the rough mesh
-    including its borders and a 0.3 m radius (the patch is skipped at the grid edge and its neighbourhood is
-    left for the outer rows when the reach grows).  Same bar as the GPU test of the plain form.  (The patch form
-    gave bit-identical outputs to the plain form on 300k such queries on the host.)"""
-    from isaacgymenv_amd.isaacgym import _lib
-    ter = H.rough_terrain(seed=5)
-    art, flat = H.anymal()
-    params = dict(H.ANYMAL_PARAMS, has_ground=0)
-    gym, sim = H.make_host_sim("anymal", 1, params, terrain=ter)
-    rng = np.random.RandomState(1)
-    n = 200000
-    o = ter["oracle"]
-    grid = o["vertices"].reshape(o["rows"], o["cols"], 3)
-    c = np.zeros((n, 3))
-    c[:, 0] = rng.uniform(o["x0"] - 0.2, o["x0"] + (o["rows"] - 1) * o["hs"] + 0.2, n)
-    c[:, 1] = rng.uniform(o["y0"] - 0.2, o["y0"] + (o["cols"] - 1) * o["hs"] + 0.2, n)
-    gi = np.clip(np.round((c[:, 0] - o["x0"]) / o["hs"]).astype(int), 0, o["rows"] - 1)
-    gj = np.clip(np.round((c[:, 1] - o["y0"]) / o["hs"]).astype(int), 0, o["cols"] - 1)
-    c[:, 2] = grid[gi, gj, 2] + rng.uniform(-0.15, 0.25, n)
-    r = rng.choice([0.02, 0.03, 0.06, 0.1, 0.3], n)
-    out = torch.zeros(n, 5)
-    cd, rd = torch.from_numpy(c.astype(np.float32)), torch.from_numpy(r.astype(np.float32))
-    _lib.check(_lib.lib().gs_debug_terrain_query(sim.handle, cd.data_ptr(), rd.data_ptr(), n, out.data_ptr(), None),
-               "terrain query")
-    g = out.numpy().astype(np.float64)
-    ref = OracleSim(flat, params, terrain=o).terrain_query(c.astype(np.float32).astype(np.float64),
-                                                         r.astype(np.float32).astype(np.float64))
-    found_g, found_o = g[:, 0] > 0.5, ref[:, 0] > 0.5
-    assert found_o.mean() > 0.3
-    assert (found_g != found_o).mean() < 2e-4
-    both = found_g & found_o
-    dsep = np.abs(g[both, 1] - ref[both, 1])
-    dn = np.abs(g[both, 2:5] - ref[both, 2:5]).max(axis=1)
-    assert (dsep > 1e-4).mean() < 5e-4, ((dsep > 1e-4).mean(), dsep.max())
-    assert (dn > 1e-3).mean() < 5e-4, ((dn > 1e-3).mean(), dn.max())
-
-
 @pytest.mark.parametrize("kind", ["hound", "anymal", "cartpole"])
 def test_link_kinematics_match_oracle(kind):
     n = 40
