@@ -734,17 +734,24 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         }
       }
     }
-    // root candidates: lane j % 4 runs root candidate j's query and broadcasts the result to the team
+    // root candidates: the team's lanes run up to four of them side by side (lane c: root candidate g + c), each
+    // result broadcast to the team -- one query slot of the wave per four root candidates, not one per candidate
 #pragma unroll
-    for (int j = 0; j < RC; ++j) {
-      float x[3];
-      mat3vec(R0, M->cpoint[j], x);
+    for (int g = 0; g < RC; g += LN) {
+      const int jj = g + lc;
       float nq[3] = {0.f, 0.f, 1.f}, dq = 3.0e38f, mq = P.ground_mu;
-      if (lc == (j & (LN - 1))) dq = terrain_candidate(P, s.p, x, M->cradius[j], nq, mq);
-      tq.rd[j] = bcast(dq, j & (LN - 1));
-      tq.rm[j] = bcast(mq, j & (LN - 1));
+      if (jj < RC) {
+        float x[3];
+        mat3vec(R0, M->cpoint[jj], x);
+        dq = terrain_candidate(P, s.p, x, M->cradius[jj], nq, mq);
+      }
 #pragma unroll
-      for (int f = 0; f < 3; ++f) tq.rn[j][f] = bcast(nq[f], j & (LN - 1));
+      for (int j = g; j < (g + LN < RC ? g + LN : RC); ++j) {
+        tq.rd[j] = bcast(dq, j - g);
+        tq.rm[j] = bcast(mq, j - g);
+#pragma unroll
+        for (int f = 0; f < 3; ++f) tq.rn[j][f] = bcast(nq[f], j - g);
+      }
     }
   }
 
