@@ -26,16 +26,18 @@ constexpr int kVec = 4;
 
 // vec: n % 4 == 0 and both pointers aligned for the 4-wide accesses (host-checked; a gradient view inside
 // the flat buffer may sit at any float offset), else the scalar path, same order of additions
+// 64-thread workgroups: a layer's gradient is 33-131 k floats, i.e. 8-32 k lanes -- spread over every CU
+constexpr int kAccBlock = 64;
 template <bool HALF>
-__global__ __launch_bounds__(kBlock) void k_splitk_accum(const void* __restrict__ parts, int P, int64_t n,
-                                                         float* __restrict__ grad, bool vec) {
-    const int64_t i0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kVec;
+__global__ __launch_bounds__(kAccBlock) void k_splitk_accum(const void* __restrict__ parts, int P, int64_t n,
+                                                            float* __restrict__ grad, bool vec) {
+    const int64_t i0 = ((int64_t)blockIdx.x * kAccBlock + threadIdx.x) * kVec;
     if (i0 >= n) return;
     float acc[kVec] = {0.f, 0.f, 0.f, 0.f};
     if (vec) {
         // the partials in batches of 8 loads issued before any is added (one load latency per batch, not per
         // partial); the additions stay in ascending partial order
-        constexpr int kBatch = 8;
+        constexpr int kBatch = 16;
         for (int p0 = 0; p0 < P; p0 += kBatch) {
             float4 v[kBatch];
 #pragma unroll
@@ -79,12 +81,12 @@ extern "C" int rl_splitk_accum(const void* parts, int32_t num_parts, int64_t n, 
     const uintptr_t align = parts_are_f16 ? 8 : 16;
     const bool vec = (n % kVec) == 0 && ((uintptr_t)parts % align) == 0 && ((uintptr_t)grad % 16) == 0;
     const int64_t lanes = (n + kVec - 1) / kVec;
-    const dim3 grid((unsigned)((lanes + kBlock - 1) / kBlock));
+    const dim3 grid((unsigned)((lanes + kAccBlock - 1) / kAccBlock));
     if (parts_are_f16)
-        hipLaunchKernelGGL(k_splitk_accum<true>, grid, dim3(kBlock), 0, (hipStream_t)stream, parts, (int)num_parts, n,
+        hipLaunchKernelGGL(k_splitk_accum<true>, grid, dim3(kAccBlock), 0, (hipStream_t)stream, parts, (int)num_parts, n,
                            grad, vec);
     else
-        hipLaunchKernelGGL(k_splitk_accum<false>, grid, dim3(kBlock), 0, (hipStream_t)stream, parts, (int)num_parts,
+        hipLaunchKernelGGL(k_splitk_accum<false>, grid, dim3(kAccBlock), 0, (hipStream_t)stream, parts, (int)num_parts,
                            n, grad, vec);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

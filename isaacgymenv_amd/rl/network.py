@@ -162,7 +162,10 @@ class _LinearELUFn(torch.autograd.Function):
             for p in (w, b):
                 if p.grad is None:
                     p.grad = torch.zeros_like(p, dtype=torch.float32)
+        # (adjacent views of ONE storage: two separate allocations may also sit back to back, and a span over them
+        # would reach past the weight gradient's storage)
         merged = (ctx.direct and want_w and want_b and w.grad.is_contiguous() and b.grad.is_contiguous()
+                  and b.grad.untyped_storage().data_ptr() == w.grad.untyped_storage().data_ptr()
                   and b.grad.data_ptr() == w.grad.data_ptr() + 4 * N * K)
         if merged:
             # the learner's flat gradient keeps a Linear's weight and bias adjacent: ONE partial buffer [S][N*K + N]

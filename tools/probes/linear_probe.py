@@ -31,6 +31,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=None)
     ap.add_argument("--rows", type=int, default=16384)
+    ap.add_argument("--splits-sweep", action="store_true", help="also time dW + finish at 8 ... 128 row blocks")
     a = ap.parse_args()
     M = a.rows
     h = torch.float16
@@ -54,6 +55,13 @@ def main():
             r["dx_mfma"] = timed(lambda: gae.linear_bwd(dy, y, x, w, dx, splits, None, None))
         r["dw_mfma"] = timed(lambda: gae.linear_bwd(dy, y, x, None, None, splits, part, part[:, N * K:], N * K + N))
         r["accum"] = timed(lambda: gae.splitk_accum(part, gacc))
+        if a.splits_sweep:
+            for S in (8, 16, 32, 64, 128):
+                if M % (S * 64):
+                    continue
+                pt = torch.empty(S, N * K + N, device="cuda")
+                r[f"dw_s{S}"] = timed(lambda: gae.linear_bwd(dy, y, x, None, None, S, pt, pt[:, N * K:], N * K + N))
+                r[f"acc_s{S}"] = timed(lambda: gae.splitk_accum(pt, gacc))
 
         def torch_bwd():
             dz = torch.ops.aten.elu_backward(dy, 1.0, 1.0, 1.0, True, y)
