@@ -211,22 +211,27 @@ __global__ __launch_bounds__(kThreads) void k_gemm_tn(const _Float16* __restrict
   // each thread: CH chunks of 8 along n (resp. k) at rows m = tid / 16 + 16 i of the stage
   const int crow = tid >> 4, ccol = (tid & 15) * 8;
   float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  h8 ra[CH], rb[CH];
+  h8 ra[CH], rb[CH], ry[CH];
+  // the loads of a stage are issued before the previous stage's MFMAs and consumed after them (dZ and the bias
+  // sums formed in gfinish), so their latency hides behind the matrix work
   auto gload = [&](int m) {
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const size_t row = (size_t)(m + crow + 16 * i);
       const size_t off = row * N + n0 + ccol;
-      const h8 g = load8(dY + off, N - (n0 + ccol));
-      const h8 y = load8(Y + off, N - (n0 + ccol));
-      h8 z;
+      ra[i] = load8(dY + off, N - (n0 + ccol));
+      ry[i] = load8(Y + off, N - (n0 + ccol));
+      rb[i] = load8(X + row * ldx + k0 + ccol, K - (k0 + ccol));
+    }
+  };
+  auto gfinish = [&]() {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        z[j] = (_Float16)((float)g[j] * elu_d((float)y[j]));
-        bsum[j] += (float)z[j];  // the bias gradient sums the same rounded dZ the weight gradient uses
+        ra[i][j] = (_Float16)((float)ra[i][j] * elu_d((float)ry[i][j]));
+        bsum[j] += (float)ra[i][j];  // the bias gradient sums the same rounded dZ the weight gradient uses
       }
-      ra[i] = z;
-      rb[i] = load8(X + row * ldx + k0 + ccol, K - (k0 + ccol));
     }
   };
   auto lstore = [&](int buf) {
@@ -239,6 +244,7 @@ __global__ __launch_bounds__(kThreads) void k_gemm_tn(const _Float16* __restrict
   };
   const int steps = rows_per_split / TS;
   gload(mb);
+  gfinish();
   lstore(0);
   __syncthreads();
   for (int st = 0; st < steps; ++st) {
@@ -256,7 +262,10 @@ __global__ __launch_bounds__(kThreads) void k_gemm_tn(const _Float16* __restrict
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fx[i], fz[j], acc[i][j], 0, 0, 0);
     }
-    if (st + 1 < steps) lstore(buf ^ 1);
+    if (st + 1 < steps) {
+      gfinish();
+      lstore(buf ^ 1);
+    }
     __syncthreads();
   }
   float* out = part + (size_t)s * wstride;
@@ -311,24 +320,28 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nn(const _Float16* __restrict
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[j][i][q] = 0.f;
-  h8 ra[CA], rb[CB];
+  h8 ra[CA], ry[CA], rb[CB];
+  // loads issued before the previous step's MFMAs, dZ formed after them (gfinish): the latency hides behind them
   auto gload = [&](int n0) {
 #pragma unroll
     for (int i = 0; i < CA; ++i) {
       const int c = tid + i * kThreads, row = c / CPR, kc = (c % CPR) * 8;
       const int valid = N - (n0 + kc);
       const size_t off = (size_t)(m0 + row) * N + n0 + kc;
-      h8 v = load8(dY + off, valid);
-      const h8 y = load8(Y + off, valid);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (_Float16)((float)v[j] * elu_d((float)y[j]));
-      ra[i] = v;
+      ra[i] = load8(dY + off, valid);
+      ry[i] = load8(Y + off, valid);
     }
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
       const int c = tid + i * kThreads, row = c >> 4, kc = (c & 15) * 8;
       rb[i] = n0 + row < N ? load8(W + (size_t)(n0 + row) * K + c0 + kc, 8) : h8{};
     }
+  };
+  auto gfinish = [&]() {
+#pragma unroll
+    for (int i = 0; i < CA; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ra[i][j] = (_Float16)((float)ra[i][j] * elu_d((float)ry[i][j]));
   };
   auto lstore = [&](int buf) {
 #pragma unroll
@@ -344,6 +357,7 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nn(const _Float16* __restrict
   };
   const int steps = (N + KS - 1) / KS;
   gload(0);
+  gfinish();
   lstore(0);
   __syncthreads();
   for (int s = 0; s < steps; ++s) {
@@ -362,7 +376,10 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nn(const _Float16* __restrict
 #pragma unroll
         for (int i = 0; i < TM; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fb[j], fa[i], acc[j][i], 0, 0, 0);
     }
-    if (s + 1 < steps) lstore(buf ^ 1);
+    if (s + 1 < steps) {
+      gfinish();
+      lstore(buf ^ 1);
+    }
     __syncthreads();
   }
   typedef _Float16 h4 __attribute__((ext_vector_type(4)));
