@@ -691,6 +691,12 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
   struct NoTerrQ {};
   [[maybe_unused]] std::conditional_t<TERR, TerrQ, NoTerrQ> tq;
   if constexpr (TERR) {
+    // each lane's queries: its chain's CC candidates, and root candidate lc (lanes lc < RC); world centres as
+    // terrain_candidate forms them (root origin + the candidate's offset)
+    constexpr int NQ = CC + 1;
+    static_assert(RC <= LN, "one root candidate per lane of the team");
+    float qc[NQ][3], qr[NQ];
+    bool qv[NQ];
     float Rk[9], Xk[3] = {0.f, 0.f, 0.f};
 #pragma unroll
     for (int f = 0; f < 9; ++f) Rk[f] = R0[f];
@@ -730,28 +736,91 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
           float x[3];
           mat3vec(Rk, pl, x);
           x[0] += Xk[0]; x[1] += Xk[1]; x[2] += Xk[2];
-          tq.d[j] = terrain_candidate(P, s.p, x, cp[3 * LN], tq.n[j], tq.m[j]);
+#pragma unroll
+          for (int f = 0; f < 3; ++f) qc[j][f] = s.p[f] + x[f];
+          qr[j] = cp[3 * LN];
+          qv[j] = true;
         }
       }
     }
-    // root candidates: the team's lanes run up to four of them side by side (lane c: root candidate g + c), each
-    // result broadcast to the team -- one query slot of the wave per four root candidates, not one per candidate
+    qv[CC] = lc < RC;
+    qr[CC] = 0.f;
+    qc[CC][0] = qc[CC][1] = qc[CC][2] = 0.f;
+    if (lc < RC) {
+      float x[3];
+      mat3vec(R0, M->cpoint[lc], x);
 #pragma unroll
-    for (int g = 0; g < RC; g += LN) {
-      const int jj = g + lc;
-      float nq[3] = {0.f, 0.f, 1.f}, dq = 3.0e38f, mq = P.ground_mu;
-      if (jj < RC) {
-        float x[3];
-        mat3vec(R0, M->cpoint[jj], x);
-        dq = terrain_candidate(P, s.p, x, M->cradius[jj], nq, mq);
+      for (int f = 0; f < 3; ++f) qc[CC][f] = s.p[f] + x[f];
+      qr[CC] = M->cradius[lc];
+    }
+    // the queries the block summary cannot rule out (gs_terrain::may_contact: sphere_contact's own first test) go
+    // into one list for the whole wave -- typically a minority (knees, the base, lifted feet end here) -- and the
+    // wave's 64 lanes run them side by side, instead of every lane running its NQ queries one after another (a
+    // wave pays for a query slot whenever ANY of its lanes has a query in it).  The list lives in the self-collision
+    // pose table (rewritten before each use there), kQItem floats per query: centre, radius, found, sep, normal.
+    constexpr int kQItem = 9;
+    static_assert(T::NPK > 0 && kShW * T::NS >= kQItem * (CC * LN + RC), "query list fits the pose table");
+    float* ql = shw_tab;  // (the workgroup's table; a workgroup is one wave)
+    const int wl = threadIdx.x & 63;
+    const unsigned long long below = (1ull << wl) - 1ull;
+    int slot[NQ];
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const bool need = qv[q] && gs_terrain::may_contact(P.terr, qc[q], qr[q], qr[q] + P.contact_offset);
+      const unsigned long long bal = __ballot(need);
+      slot[q] = need ? cnt + __popcll(bal & below) : -1;
+      if (need) {
+        float* it = ql + slot[q] * kQItem;
+        it[0] = qc[q][0]; it[1] = qc[q][1]; it[2] = qc[q][2]; it[3] = qr[q];
       }
+      cnt += __popcll(bal);
+    }
+    __syncthreads();
+    // (the live lanes only: the lanes of envs past N left the kernel before the substep loop)
+    const unsigned long long live = __ballot(true);
+    const int nlive = __popcll(live);
+    for (int i = __popcll(live & below); i < cnt; i += nlive) {
+      float* it = ql + i * kQItem;
+      const float cw[3] = {it[0], it[1], it[2]};
+      const float r = it[3];
+      float st = 0.f, nt[3] = {0.f, 0.f, 1.f};
+      const bool found = gs_terrain::sphere_contact(P.terr, cw, r, r + P.contact_offset, st, nt);
+      it[4] = found ? 1.f : 0.f;
+      it[5] = st;
+      it[6] = nt[0]; it[7] = nt[1]; it[8] = nt[2];
+    }
+    __syncthreads();
+    // terrain_candidate's result: the deepest of the ground plane and the mesh surface
+    float rd = 3.0e38f, rn[3] = {0.f, 0.f, 1.f}, rm = P.ground_mu;
 #pragma unroll
-      for (int j = g; j < (g + LN < RC ? g + LN : RC); ++j) {
-        tq.rd[j] = bcast(dq, j - g);
-        tq.rm[j] = bcast(mq, j - g);
-#pragma unroll
-        for (int f = 0; f < 3; ++f) tq.rn[j][f] = bcast(nq[f], j - g);
+    for (int q = 0; q < NQ; ++q) {
+      float dist = P.has_ground ? qc[q][2] - qr[q] : 3.0e38f;
+      float nrm[3] = {0.f, 0.f, 1.f};
+      float smu = P.ground_mu;
+      if (slot[q] >= 0) {
+        const float* it = ql + slot[q] * kQItem;
+        if (it[4] != 0.f && it[5] < dist) {
+          dist = it[5];
+          nrm[0] = it[6]; nrm[1] = it[7]; nrm[2] = it[8];
+          smu = P.terr.mu;
+        }
       }
+      if (q < CC) {
+        tq.d[q] = dist; tq.m[q] = smu;
+        tq.n[q][0] = nrm[0]; tq.n[q][1] = nrm[1]; tq.n[q][2] = nrm[2];
+      } else {
+        rd = dist; rm = smu;
+        rn[0] = nrm[0]; rn[1] = nrm[1]; rn[2] = nrm[2];
+      }
+    }
+    // root candidate j's result lives in lane j of the team
+#pragma unroll
+    for (int j = 0; j < RC; ++j) {
+      tq.rd[j] = bcast(rd, j);
+      tq.rm[j] = bcast(rm, j);
+#pragma unroll
+      for (int f = 0; f < 3; ++f) tq.rn[j][f] = bcast(rn[f], j);
     }
   }
 

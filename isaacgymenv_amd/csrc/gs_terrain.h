@@ -146,9 +146,38 @@ GS_HD void triangle(const float* p, float r, float thr, const float4& A, const f
   }
 }
 
+// false when no cell around sphere (p, r) can hold a surface within thr: the range of cells within the horizontal
+// reach is empty, or the sphere's lowest reach lies above the highest top of every block the range touches (the
+// block summary).  sphere_contact starts with exactly this test; the lane team runs it alone first to hand only
+// the remaining queries to the wave (gs_team.hip).
+GS_HD bool may_contact(const TerrainDev& T, const float* p, float r, float thr) {
+  const float reach = fmaxf(thr, r + TERRAIN_BACK);
+  const float gx = (p[0] - T.x0) * T.inv_hs, gy = (p[1] - T.y0) * T.inv_hs, gt = reach * T.inv_hs;
+  const int i0 = gs_imax((int)floorf(gx - gt) - 1, 0), i1 = gs_imin((int)floorf(gx + gt) + 1, T.rows - 2);
+  const int j0 = gs_imax((int)floorf(gy - gt) - 1, 0), j1 = gs_imin((int)floorf(gy + gt) + 1, T.cols - 2);
+  if (i0 > i1 || j0 > j1) return false;
+  const float zlo = p[2] - thr;
+  const int bi0 = i0 / TERRAIN_BLK, bi1 = i1 / TERRAIN_BLK, bj0 = j0 / TERRAIN_BLK, bj1 = j1 / TERRAIN_BLK;
+  bool reach_any = false;
+  if (bi1 - bi0 <= 1 && bj1 - bj0 <= 1) {
+    const float* b0 = T.blk + (size_t)bi0 * T.bcols;
+    const float* b1 = T.blk + (size_t)bi1 * T.bcols;
+    const float t00 = b0[bj0], t01 = b0[bj1], t10 = b1[bj0], t11 = b1[bj1];
+    reach_any = !(zlo > t00) || !(zlo > t01) || !(zlo > t10) || !(zlo > t11);
+  } else {
+    for (int bi = bi0; bi <= bi1; ++bi)
+      for (int bj = bj0; bj <= bj1; ++bj) reach_any |= !(zlo > T.blk[(size_t)bi * T.bcols + bj]);
+  }
+  return reach_any;
+}
+
 // Closest admissible mesh surface for sphere (p, r); false when none lies within thr.
 GS_HD bool sphere_contact(const TerrainDev& T, const float* p, float r, float thr, float& sep,
                                                float* n) {
+  // (1) the range of cells and the block summary: no cell can contact (a lifted foot, the knees, the base: most
+  //     queries end here after one batch of loads).  Everything below skips only cells the per-cell tests would
+  //     skip, so the result is the full scan's.
+  if (!may_contact(T, p, r, thr)) return false;
   // horizontal reach: a face can be admitted from behind up to r + TERRAIN_BACK away (walls)
   const float reach = fmaxf(thr, r + TERRAIN_BACK);
   const float gx = (p[0] - T.x0) * T.inv_hs, gy = (p[1] - T.y0) * T.inv_hs, gt = reach * T.inv_hs;
@@ -175,24 +204,6 @@ GS_HD bool sphere_contact(const TerrainDev& T, const float* p, float r, float th
     triangle(p, r, thr, v00, v11, v01, bkey, best, n);
     triangle(p, r, thr, v00, v10, v11, bkey, best, n);
   };
-  if (i0 > i1 || j0 > j1) return false;
-  // Everything below skips only cells the per-cell tests above would skip, so the result is the full scan's.
-  // (1) the sphere's lowest reach above the highest top of every block the range touches: no cell can contact
-  //     (a lifted foot, the knees, the base: most queries end here after one batch of loads)
-  {
-    const int bi0 = i0 / TERRAIN_BLK, bi1 = i1 / TERRAIN_BLK, bj0 = j0 / TERRAIN_BLK, bj1 = j1 / TERRAIN_BLK;
-    bool reach_any = false;
-    if (bi1 - bi0 <= 1 && bj1 - bj0 <= 1) {
-      const float* b0 = T.blk + (size_t)bi0 * T.bcols;
-      const float* b1 = T.blk + (size_t)bi1 * T.bcols;
-      const float t00 = b0[bj0], t01 = b0[bj1], t10 = b1[bj0], t11 = b1[bj1];
-      reach_any = !(zlo > t00) || !(zlo > t01) || !(zlo > t10) || !(zlo > t11);
-    } else {
-      for (int bi = bi0; bi <= bi1; ++bi)
-        for (int bj = bj0; bj <= bj1; ++bj) reach_any |= !(zlo > T.blk[(size_t)bi * T.bcols + bj]);
-    }
-    if (!reach_any) return false;
-  }
   const int ic = (int)floorf(gx), jc = (int)floorf(gy);
   const bool centre = ic >= 0 && ic <= T.rows - 2 && jc >= 0 && jc <= T.cols - 2;
   if (centre) cell(ic, jc, T.cell[(size_t)ic * (T.cols - 1) + jc]);
