@@ -91,6 +91,7 @@ struct gs_sim {
   float4* d_tverts = nullptr;     // terrain mesh (gs_terrain.h)
   uint4* d_tcells = nullptr;
   float* d_tblk = nullptr;        // highest cell top per TERRAIN_BLK x TERRAIN_BLK block of cells
+  float* d_tsq4 = nullptr;        // highest cell top of the 4 x 4 cells starting at each cell
   float* d_rows = nullptr;        // contact-row tiles of the GLOBAL-row kernels (TopoEntry::row_floats)
   size_t rows_cap = 0;            // floats allocated
   // host backend (device < 0)
@@ -101,6 +102,7 @@ struct gs_sim {
   std::vector<float4> h_tverts;
   std::vector<uint4> h_tcells;
   std::vector<float> h_tblk;
+  std::vector<float> h_tsq4;
   double host_ms = -1.0;          // wall time of the last simulate / pd_step (timing enabled)
   const DevModel* model() const { return host ? &h_model : d_model; }
   const DevLinks* links() const { return host ? &h_links : d_links; }
@@ -168,6 +170,7 @@ void gs_sim_destroy(gs_sim* s) {
   if (s->d_tverts) (void)hipFree(s->d_tverts);
   if (s->d_tcells) (void)hipFree(s->d_tcells);
   if (s->d_tblk) (void)hipFree(s->d_tblk);
+  if (s->d_tsq4) (void)hipFree(s->d_tsq4);
   if (s->d_rows) (void)hipFree(s->d_rows);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -270,37 +273,64 @@ int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_verti
       float& b = hb[(size_t)((i / TERRAIN_BLK) * bcols + j / TERRAIN_BLK)];
       b = std::max(b, top);
     }
+  // 4 x 4 square maxima (clipped at the grid's end): row-wise maxima of 4, then column-wise
+  const int64_t cr = rows - 1, cc = cols - 1;
+  std::vector<float> h4((size_t)(cr * cc)), hq((size_t)(cr * cc));
+  for (int64_t i = 0; i < cr; ++i)
+    for (int64_t j = 0; j < cc; ++j) {
+      float m = -3.0e38f;
+      for (int64_t d = 0; d < 4 && j + d < cc; ++d) {
+        float top;
+        std::memcpy(&top, &hc[(size_t)(i * cc + j + d)].x, 4);
+        m = std::max(m, top);
+      }
+      h4[(size_t)(i * cc + j)] = m;
+    }
+  for (int64_t i = 0; i < cr; ++i)
+    for (int64_t j = 0; j < cc; ++j) {
+      float m = -3.0e38f;
+      for (int64_t d = 0; d < 4 && i + d < cr; ++d) m = std::max(m, h4[(size_t)((i + d) * cc + j)]);
+      hq[(size_t)(i * cc + j)] = m;
+    }
   TerrainDev& T = s->dp.terr;
   if (s->host) {
     s->h_tverts = std::move(hv);
     s->h_tcells = std::move(hc);
     s->h_tblk = std::move(hb);
+    s->h_tsq4 = std::move(hq);
     T.v = s->h_tverts.data();
     T.cell = s->h_tcells.data();
     T.blk = s->h_tblk.data();
+    T.sq4 = s->h_tsq4.data();
   } else {
     float4* dv = nullptr;
     uint4* dc = nullptr;
     float* db = nullptr;
+    float* dq = nullptr;
     hipError_t e = hipSetDevice(s->device);
     if (e == hipSuccess) e = hipMalloc(&dv, hv.size() * sizeof(float4));
     if (e == hipSuccess) e = hipMalloc(&dc, hc.size() * sizeof(uint4));
     if (e == hipSuccess) e = hipMalloc(&db, hb.size() * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&dq, hq.size() * sizeof(float));
     if (e == hipSuccess) e = hipMemcpy(dv, hv.data(), hv.size() * sizeof(float4), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(dc, hc.data(), hc.size() * sizeof(uint4), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(db, hb.data(), hb.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dq, hq.data(), hq.size() * sizeof(float), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
       if (dv) (void)hipFree(dv);
       if (dc) (void)hipFree(dc);
       if (db) (void)hipFree(db);
+      if (dq) (void)hipFree(dq);
       return hip_fail(e, "gs_sim_add_triangle_mesh");
     }
     s->d_tverts = dv;
     s->d_tcells = dc;
     s->d_tblk = db;
+    s->d_tsq4 = dq;
     T.v = s->d_tverts;
     T.cell = s->d_tcells;
     T.blk = s->d_tblk;
+    T.sq4 = s->d_tsq4;
   }
   T.bcols = (int)bcols;
   T.rows = (int)rows;

@@ -45,6 +45,7 @@ struct TerrainDev {
   const uint4* cell;   // [(rows-1)*(cols-1)]: x = top height (float bits), y = footprint flags,
                        // z = bottom height (float bits), w unused
   const float* blk;    // [ceil((rows-1)/TERRAIN_BLK)][bcols]: the highest top of each block of cells
+  const float* sq4;    // [(rows-1)*(cols-1)]: the highest top of the 4 x 4 cells starting at each cell (clipped)
   int rows, cols, bcols;
   float x0, y0, hs, inv_hs;
   float mu;            // static friction of the mesh
@@ -147,8 +148,8 @@ GS_HD void triangle(const float* p, float r, float thr, const float4& A, const f
 }
 
 // false when no cell around sphere (p, r) can hold a surface within thr: the range of cells within the horizontal
-// reach is empty, or the sphere's lowest reach lies above the highest top of every block the range touches (the
-// block summary).  sphere_contact starts with exactly this test; the lane team runs it alone first to hand only
+// reach is empty, or the sphere's lowest reach lies above the highest cell top of the range (from the 4 x 4
+// square maxima; ranges wider than 8 cells from the 8 x 8 block summary).  sphere_contact starts with exactly this test; the lane team runs it alone first to hand only
 // the remaining queries to the wave (gs_team.hip).
 GS_HD bool may_contact(const TerrainDev& T, const float* p, float r, float thr) {
   const float reach = fmaxf(thr, r + TERRAIN_BACK);
@@ -157,6 +158,14 @@ GS_HD bool may_contact(const TerrainDev& T, const float* p, float r, float thr) 
   const int j0 = gs_imax((int)floorf(gy - gt) - 1, 0), j1 = gs_imin((int)floorf(gy + gt) + 1, T.cols - 2);
   if (i0 > i1 || j0 > j1) return false;
   const float zlo = p[2] - thr;
+  if (i1 - i0 <= 7 && j1 - j0 <= 7) {
+    // the range's highest top exactly-or-above from four overlapping 4 x 4 squares (their union covers a range
+    // up to 8 cells wide; a narrower, clipped range is covered with room to spare): one batch of loads
+    const int ib = gs_imax(i0, i1 - 3), jb = gs_imax(j0, j1 - 3);
+    const size_t C = (size_t)(T.cols - 1);
+    const float t00 = T.sq4[i0 * C + j0], t01 = T.sq4[i0 * C + jb], t10 = T.sq4[ib * C + j0], t11 = T.sq4[ib * C + jb];
+    return !(zlo > t00) || !(zlo > t01) || !(zlo > t10) || !(zlo > t11);
+  }
   const int bi0 = i0 / TERRAIN_BLK, bi1 = i1 / TERRAIN_BLK, bj0 = j0 / TERRAIN_BLK, bj1 = j1 / TERRAIN_BLK;
   bool reach_any = false;
   if (bi1 - bi0 <= 1 && bj1 - bj0 <= 1) {
