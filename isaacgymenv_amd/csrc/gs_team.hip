@@ -785,7 +785,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       const float cw[3] = {it[0], it[1], it[2]};
       const float r = it[3];
       float st = 0.f, nt[3] = {0.f, 0.f, 1.f};
-      const bool found = gs_terrain::sphere_contact(P.terr, cw, r, r + P.contact_offset, st, nt);
+      const bool found = gs_terrain::sphere_contact_scan(P.terr, cw, r, r + P.contact_offset, st, nt);
       it[4] = found ? 1.f : 0.f;
       it[5] = st;
       it[6] = nt[0]; it[7] = nt[1]; it[8] = nt[2];

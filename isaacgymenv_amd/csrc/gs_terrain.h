@@ -180,13 +180,18 @@ GS_HD bool may_contact(const TerrainDev& T, const float* p, float r, float thr) 
   return reach_any;
 }
 
+// The scan of sphere_contact past its first cull (callers that ran may_contact themselves: gs_team.hip).
+GS_HD bool sphere_contact_scan(const TerrainDev& T, const float* p, float r, float thr, float& sep, float* n);
+
 // Closest admissible mesh surface for sphere (p, r); false when none lies within thr.
-GS_HD bool sphere_contact(const TerrainDev& T, const float* p, float r, float thr, float& sep,
-                                               float* n) {
-  // (1) the range of cells and the block summary: no cell can contact (a lifted foot, the knees, the base: most
-  //     queries end here after one batch of loads).  Everything below skips only cells the per-cell tests would
-  //     skip, so the result is the full scan's.
-  if (!may_contact(T, p, r, thr)) return false;
+// (1) the range of cells and its highest top: no cell can contact (a lifted foot, the knees, the base: most
+//     queries end here after one batch of loads).  Everything after it skips only cells the per-cell tests would
+//     skip, so the result is the full scan's.
+GS_HD bool sphere_contact(const TerrainDev& T, const float* p, float r, float thr, float& sep, float* n) {
+  return may_contact(T, p, r, thr) && sphere_contact_scan(T, p, r, thr, sep, n);
+}
+
+GS_HD bool sphere_contact_scan(const TerrainDev& T, const float* p, float r, float thr, float& sep, float* n) {
   // horizontal reach: a face can be admitted from behind up to r + TERRAIN_BACK away (walls)
   const float reach = fmaxf(thr, r + TERRAIN_BACK);
   const float gx = (p[0] - T.x0) * T.inv_hs, gy = (p[1] - T.y0) * T.inv_hs, gt = reach * T.inv_hs;
