@@ -200,8 +200,8 @@ GS_HD bool sphere_contact_scan(const TerrainDev& T, const float* p, float r, flo
   float best = 3.0e38f, bkey = 3.0e38f;
   const float zlo = p[2] - thr;
   const float pad = 1e-4f * T.hs;
-  // one cell given its info word: the culling tests, then its two triangles
-  auto cell = [&](int i, int j, const uint4& cinfo) {
+  // one cell given its info word: the culling tests, then its two triangles (vertices loaded here unless given)
+  auto cell = [&](int i, int j, const uint4& cinfo, const float4* pre = nullptr) {
     const float top = gs_bits_float(cinfo.x);
     if (zlo > top) return;
     const uint32_t f = cinfo.y;
@@ -214,13 +214,19 @@ GS_HD bool sphere_contact_scan(const TerrainDev& T, const float* p, float r, flo
     const float dz = fmaxf(fmaxf(gs_bits_float(cinfo.z) - pad - p[2], p[2] - top - pad), 0.f);
     if (dx * dx + dy * dy + dz * dz >= bkey * bkey) return;
     const size_t v0 = (size_t)i * T.cols + j;
-    const float4 v00 = T.v[v0], v01 = T.v[v0 + 1], v10 = T.v[v0 + T.cols], v11 = T.v[v0 + T.cols + 1];
+    const float4 v00 = pre ? pre[0] : T.v[v0], v01 = pre ? pre[1] : T.v[v0 + 1];
+    const float4 v10 = pre ? pre[2] : T.v[v0 + T.cols], v11 = pre ? pre[3] : T.v[v0 + T.cols + 1];
     triangle(p, r, thr, v00, v11, v01, bkey, best, n);
     triangle(p, r, thr, v00, v10, v11, bkey, best, n);
   };
   const int ic = (int)floorf(gx), jc = (int)floorf(gy);
   const bool centre = ic >= 0 && ic <= T.rows - 2 && jc >= 0 && jc <= T.cols - 2;
-  if (centre) cell(ic, jc, T.cell[(size_t)ic * (T.cols - 1) + jc]);
+  if (centre) {  // the centre cell's word and vertices in one batch (it is nearly always tested)
+    const size_t v0 = (size_t)ic * T.cols + jc;
+    const uint4 cw = T.cell[(size_t)ic * (T.cols - 1) + jc];
+    const float4 pre[4] = {T.v[v0], T.v[v0 + 1], T.v[v0 + T.cols], T.v[v0 + T.cols + 1]};
+    cell(ic, jc, cw, pre);
+  }
   // (2) the rest in (i, j) order.  Before loading a cell's word, its widest possible footprint (one cell further
   //     on every side, plus a margin far above the float rounding of the coordinates) is tested against the
   //     reach and the best key: cells beyond it are skipped unread, whole rows at once.  A row's remaining cell
