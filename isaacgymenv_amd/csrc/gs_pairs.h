@@ -16,10 +16,12 @@ namespace {
 
 GS_HD float dot3f(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 // GS_GJK_TRACE=<env> (debug builds only, tools/probes/hound_pool_probe.py): device printf of GJK's iterations
-// for that env in the one-thread-per-env debug kernel (gs_debug_self_contacts)
+// for that env in the one-thread-per-env debug kernel (gs_debug_self_contacts); on the host backend every call
 #if defined(GS_GJK_TRACE) && defined(__HIP_DEVICE_COMPILE__)
 #define GS_GJK_TR(...) \
   if ((int)(blockIdx.x * blockDim.x + threadIdx.x) == GS_GJK_TRACE) printf(__VA_ARGS__)
+#elif defined(GS_GJK_TRACE)
+#define GS_GJK_TR(...) printf(__VA_ARGS__)  // host backend: every call (run a one-env sim)
 #else
 #define GS_GJK_TR(...)
 #endif
@@ -183,7 +185,14 @@ GS_HD void core_support(const DevModel* __restrict__ M, int sh, const ShapeW& W,
     const float mg = M->shm[sh];
     const float ax[3] = {W.R[2], W.R[5], W.R[8]};
     const float da = dot3f(ax, d);
-    const float pp[3] = {d[0] - da * ax[0], d[1] - da * ax[1], d[2] - da * ax[2]};
+    float pp[3] = {d[0] - da * ax[0], d[1] - da * ax[1], d[2] - da * ax[2]};
+    // projected once more: for d nearly along the axis (an end disc facing the other core) the subtraction
+    // cancels, and the rounding left in pp -- not orthogonal to the axis -- tilted the normalised rim direction
+    // off the disc (UsefulHound, a hull face on a leg cylinder's end: the rim point 2.8 mm beyond the disc and a
+    // 1.7 mm separation error, round 5)
+    const float pa = dot3f(ax, pp);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) pp[k] -= pa * ax[k];
     const float lp = sqrtf(dot3f(pp, pp));
     const float s = da >= 0.f ? sz[1] - mg : -(sz[1] - mg);
     const float rs = lp > 1e-12f ? (sz[0] - mg) / lp : 0.f;
@@ -427,6 +436,9 @@ GS_HD float gjk_cores(const DevModel* __restrict__ M, int sa, int sb, const Shap
 #pragma unroll
     for (int t = 0; t < 3; ++t) W[i][t] = A[i][t] = B[i][t] = 0.f;
   int k = 0;
+  // a support plane with v.w > 1e-4 vv has certified a positive distance (at least v.w / |v|, far above rounding):
+  // from then on a subset search that reads the origin as enclosed is a rounding failure, not an overlap
+  bool sepd = false;
   for (int it = 0; it < 32; ++it) {
     const float nv[3] = {-v[0], -v[1], -v[2]};
     float a[3], b[3], w[3];
@@ -438,17 +450,58 @@ GS_HD float gjk_cores(const DevModel* __restrict__ M, int sa, int sb, const Shap
     GS_GJK_TR("gjk %d-%d it %d k %d v %.9g %.9g %.9g w %.9g %.9g %.9g vv %.9g vw %.9g\n", sa, sb, it, k, v[0], v[1],
               v[2], w[0], w[1], w[2], vv, vw);
     if (vw > 0.f && vw * vw > stop * stop * vv) return vw / sqrtf(vv);  // separated by more than stop
+    sepd = sepd || vw > 1e-4f * vv;
     // converged: the support plane is within 1e-6 |v| of the simplex's closest point (the distance to ~1e-6
     // relative; the oracle's fp64 bound is 1e-10, which float arithmetic cannot resolve: below ~1e-7 vv the test
     // reads rounding, so a converged float search ran on until a repeated support point or the iteration cap)
     if (k > 0 && vv - vw <= 1e-6f * vv + 1e-14f) break;
+    // Step along the segment from the closest point of the first kold simplex points -- a point of the Minkowski
+    // difference whose witness points are the same combination of A and B -- to w: a strict decrease whenever
+    // v.w < v.v, and the next simplex {that point, w} is well conditioned.  Returns false (the simplex cut back to
+    // kold points, v its closest point) when rounding leaves no progress.
+    auto segment_step = [&](int kold) -> bool {
+      float Av[3] = {0.f, 0.f, 0.f}, Bv[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (i < kold)
+#pragma unroll
+          for (int t = 0; t < 3; ++t) { Av[t] += lam[i] * A[i][t]; Bv[t] += lam[i] * B[i][t]; }
+      const float Wv[3] = {Av[0] - Bv[0], Av[1] - Bv[1], Av[2] - Bv[2]};
+      const float d[3] = {w[0] - Wv[0], w[1] - Wv[1], w[2] - Wv[2]};
+      const float dd = dot3f(d, d);
+      float t = dd > 0.f ? -dot3f(Wv, d) / dd : 0.f;
+      t = t > 1.f ? 1.f : t;
+      GS_GJK_TR("gjk %d-%d   segment step from %d points t %.9g\n", sa, sb, kold, t);
+      if (!(t > 0.f)) {
+        k = kold;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) v[s] = Wv[s];
+        return false;
+      }
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        W[0][s] = Wv[s]; A[0][s] = Av[s]; B[0][s] = Bv[s];
+        W[1][s] = w[s]; A[1][s] = a[s]; B[1][s] = b[s];
+        v[s] = Wv[s] + t * d[s];
+      }
+      lam[0] = 1.f - t; lam[1] = t; lam[2] = 0.f; lam[3] = 0.f;
+      k = 2;
+      return true;
+    };
     bool dup = false;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float d[3] = {W[i][0] - w[0], W[i][1] - w[1], W[i][2] - w[2]};
       dup = dup || (i < k && dot3f(d, d) < 1e-16f);
     }
-    if (dup) break;
+    // A support point already in the simplex although the search has not converged (v.w < v.v beyond the
+    // tolerance): in exact arithmetic v is the simplex's closest point and v.p >= v.v for every vertex p, so v is
+    // off by the rounding of the subset solve -- sliver triangles of two finely tessellated hulls (UsefulHound's
+    // trunk against an arm link: 0.7 degrees of contact normal, round 5).  Step instead of stopping.
+    if (dup) {
+      if (segment_step(k)) continue;
+      break;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if (i == k) {
@@ -460,7 +513,18 @@ GS_HD float gjk_cores(const DevModel* __restrict__ M, int sa, int sb, const Shap
     int mask = 0;
     simplex_all(W, k, best, mask, v, l4);
     GS_GJK_TR("gjk %d-%d   mask %d best %.9g v %.9g %.9g %.9g\n", sa, sb, mask, best, v[0], v[1], v[2]);
-    if (!mask) return 0.f;
+    if (!mask && !sepd) return 0.f;
+    if (!((mask >> (k - 1)) & 1) || (sepd && (mask == 15 || !(best >= 1e-18f)))) {
+      // The subset search dropped the new support point w although w lies beyond the old closest point's support
+      // plane (vv - vw above the tolerance) -- in exact arithmetic the grown simplex's closest point involves w --
+      // or it read the origin as enclosed after a support plane had certified a positive distance.  Only rounding
+      // does either: the case of a curved core (a cylinder's rim), whose support points crowd together into
+      // sliver triangles and tetrahedra as the search converges.  Left alone the search re-added w until the
+      // iteration cap and returned the old point, or reported overlapping cores (UsefulHound env 111 of the r04f
+      // failure: a 4e-3 rad contact-normal error; the fp32 oracle dropped the contact).
+      if (segment_step(k - 1)) continue;
+      break;
+    }
     // keep the chosen subset, in order (compile-time moves under runtime conditions)
     float W2[4][3], A2[4][3], B2[4][3];
     int n = 0;

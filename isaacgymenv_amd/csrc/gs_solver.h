@@ -749,7 +749,9 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
           }
         }
         slot[(3 * SUP + rr) * LB] = cj;
-        slot[(3 * SUP + 3 + rr) * LB] = 1.f / d;  // (ground rows: no response cutoff)
+        // (ground rows: no response cutoff; a row the articulation cannot move along -- d == 0, e.g. a
+        // fixed-base planar chain's off-plane tangent -- takes no impulse instead of 0 * inf)
+        slot[(3 * SUP + 3 + rr) * LB] = d > 0.f ? 1.f / d : 0.f;
       }
     }
   });
@@ -783,7 +785,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
         }
       }
       slot[SUP * LB] = lsgn[j] * nuf[leaf];
-      slot[(SUP + 1) * LB] = 1.f / d;
+      slot[(SUP + 1) * LB] = d > 0.f ? 1.f / d : 0.f;
     }
   }
 

@@ -1182,7 +1182,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         row[13 * RW] = 0.f;
         row[14 * RW] = 0.f;
         row[RS::CSLOT * RW] = cj;
-        dir[rr] = __builtin_amdgcn_rcpf(d);
+        dir[rr] = d > 0.f ? __builtin_amdgcn_rcpf(d) : 0.f;  // (d == 0: a row the chain cannot move along)
         rec[(RS::C_DI + rr) * RW] = dir[rr];
       }
       float g10 = 0.f, g20 = 0.f, g21 = 0.f;
@@ -1265,7 +1265,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         rz[13 * RW] = 0.f;
         rz[14 * RW] = 0.f;
         rz[RS::CSLOT * RW] = cj;
-        dir[rr] = __builtin_amdgcn_rcpf(d);
+        dir[rr] = d > 0.f ? __builtin_amdgcn_rcpf(d) : 0.f;  // (d == 0: a row the chain cannot move along)
         rec[(RS::R_DI + rr) * RW] = dir[rr];
       }
       float g10 = 0.f, g20 = 0.f, g21 = 0.f;

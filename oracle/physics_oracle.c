@@ -34,6 +34,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -44,6 +45,10 @@
 #define REAL double
 #endif
 typedef REAL real;
+/* GJK's convergence bound on vv - v.w relative to vv: 1e-10 in fp64; the fp32 build uses the float kernels' 1e-6
+ * (gs_pairs.h gjk_cores: below ~1e-7 vv a float test reads rounding, and a search that cannot stop runs into a
+ * degenerate 4-point simplex that reads as overlapping cores -- not the rounding of the spec, a failure of it) */
+#define GJK_TOL (sizeof(real) == sizeof(double) ? 1e-10 : 1e-6)
 
 #define MAXB 32
 #define MAXV 40
@@ -331,6 +336,9 @@ static void core_support(const OModel *m, int sh, const ShapeW *W, const real *R
         const real ax[3] = {W->R[2], W->R[5], W->R[8]};
         const real da = dot3(ax, d);
         real pp[3] = {d[0] - da * ax[0], d[1] - da * ax[1], d[2] - da * ax[2]};
+        /* projected once more (d nearly along the axis: the subtraction cancels; gs_pairs.h core_support) */
+        const real pa = dot3(ax, pp);
+        for (int k = 0; k < 3; ++k) pp[k] -= pa * ax[k];
         const real lp = sqrt(dot3(pp, pp));
         const real s = da >= 0 ? sz[1] - mg : -(sz[1] - mg);
         for (int k = 0; k < 3; ++k) out[k] = W->c[k] + s * ax[k] + (lp > 1e-12 ? (sz[0] - mg) * pp[k] / lp : 0);
@@ -524,6 +532,7 @@ static real gjk_cores(const OModel *m, int sa, int sb, const ShapeW *Wa, const S
     if (dot3(v, v) < 1e-18) { v[0] = 1; v[1] = 0; v[2] = 0; }
     real W[4][3], A[4][3], B[4][3], lam[4] = {1, 0, 0, 0};
     int k = 0;
+    int sepd = 0; /* a support plane with v.w > 1e-4 vv certified a positive distance (gs_pairs.h gjk_cores) */
     for (int it = 0; it < 32; ++it) {
         const real nv[3] = {-v[0], -v[1], -v[2]};
         real a[3], b[3], w[3];
@@ -532,18 +541,58 @@ static real gjk_cores(const OModel *m, int sa, int sb, const ShapeW *Wa, const S
         core_support(m, sb, Wb, Rb, Pb, v, b);
         for (int t = 0; t < 3; ++t) w[t] = a[t] - b[t];
         const real vv = dot3(v, v);
-        if (k > 0 && vv - dot3(v, w) <= 1e-10 * vv + 1e-14) break;
+#ifdef ORACLE_GJK_TRACE  /* debug builds only */
+        fprintf(stderr, "ogjk %d-%d it %d k %d v %.9g %.9g %.9g w %.9g %.9g %.9g vv %.9g vw %.9g\n", sa, sb, it, k,
+                (double)v[0], (double)v[1], (double)v[2], (double)w[0], (double)w[1], (double)w[2], (double)vv,
+                (double)dot3(v, w));
+#endif
+        if (dot3(v, w) > (real)1e-4 * vv) sepd = 1;
+        if (k > 0 && vv - dot3(v, w) <= (real)GJK_TOL * vv + (real)1e-14) break;
+        /* a step along the segment from the closest point of the first kold simplex points (a point of the
+         * Minkowski difference, witnesses the same combination of A and B) to w; the simplex becomes {that point,
+         * w}; 0 when rounding leaves no progress (the simplex cut back to kold points) -- gs_pairs.h gjk_cores */
+        int step = -1; /* -1: none; otherwise kold */
         int dup = 0;
         for (int i = 0; i < k; ++i) {
             const real d[3] = {W[i][0] - w[0], W[i][1] - w[1], W[i][2] - w[2]};
             if (dot3(d, d) < 1e-16) dup = 1;
         }
-        if (dup) break;
-        for (int t = 0; t < 3; ++t) { W[k][t] = w[t]; A[k][t] = a[t]; B[k][t] = b[t]; }
-        ++k;
+        /* a repeated support point before convergence: v is off by the subset solve's rounding */
+        if (dup) step = k;
+        int mask = 0;
         real l4[4];
-        const int mask = simplex_closest(W, k, v, l4);
-        if (!mask) return 0;
+        if (step < 0) {
+            for (int t = 0; t < 3; ++t) { W[k][t] = w[t]; A[k][t] = a[t]; B[k][t] = b[t]; }
+            ++k;
+            mask = simplex_closest(W, k, v, l4);
+            if (!mask && !sepd) return 0;
+            /* rounding rejected every subset with the new support point w although w lies beyond the old closest
+             * point's support plane, or read the origin as enclosed after a positive distance was certified */
+            if (!(mask >> (k - 1) & 1) || (sepd && (mask == 15 || !(dot3(v, v) >= 1e-18)))) step = k - 1;
+        }
+        if (step >= 0) {
+            real Av[3] = {0, 0, 0}, Bv[3] = {0, 0, 0};
+            for (int i = 0; i < step; ++i)
+                for (int t = 0; t < 3; ++t) { Av[t] += lam[i] * A[i][t]; Bv[t] += lam[i] * B[i][t]; }
+            const real Wv[3] = {Av[0] - Bv[0], Av[1] - Bv[1], Av[2] - Bv[2]};
+            const real d[3] = {w[0] - Wv[0], w[1] - Wv[1], w[2] - Wv[2]};
+            const real dd = dot3(d, d);
+            real t = dd > 0 ? -dot3(Wv, d) / dd : 0;
+            t = t > 1 ? 1 : t;
+            if (!(t > 0)) {
+                k = step;
+                for (int s = 0; s < 3; ++s) v[s] = Wv[s];
+                break;
+            }
+            for (int s = 0; s < 3; ++s) {
+                W[0][s] = Wv[s]; A[0][s] = Av[s]; B[0][s] = Bv[s];
+                W[1][s] = w[s]; A[1][s] = a[s]; B[1][s] = b[s];
+                v[s] = Wv[s] + t * d[s];
+            }
+            lam[0] = 1 - t; lam[1] = t; lam[2] = 0; lam[3] = 0;
+            k = 2;
+            continue;
+        }
         int n = 0;
         for (int i = 0; i < k; ++i)
             if (mask >> i & 1) {
@@ -1140,7 +1189,8 @@ static void env_substep(const OModel *m, const OParams *p, real h,
                 if (s >= 0) target = -s / hd;
                 else if (pos_phase) { target = -s / hs; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
                 else target = 0;
-                real ln = lam[r] + (target - u) / Dr[r]; /* ground rows: no response cutoff */
+                real ln = Dr[r] > 0 ? lam[r] + (target - u) / Dr[r] : lam[r]; /* ground rows: no response cutoff; Dr == 0: a
+                                                                                  * row the articulation cannot move along */
                 if (ln < 0) ln = 0;
                 const real dl = ln - lam[r];
                 lam[r] = ln;
@@ -1152,7 +1202,7 @@ static void env_substep(const OModel *m, const OParams *p, real h,
                 real u = 0;
                 for (int k = 0; k < nv; ++k) u += Jr[k] * v[k];
                 const real lim = cmu[a] * lam[3 * a];
-                real lt = lam[r] - u / Dr[r];
+                real lt = Dr[r] > 0 ? lam[r] - u / Dr[r] : lam[r];
                 if (lt > lim) lt = lim;
                 if (lt < -lim) lt = -lim;
                 const real dl = lt - lam[r];

@@ -41,7 +41,7 @@ def _make(monkeypatch):
 def _oracle_sequence(flat, root, dof, dof_tensor, mu, act, default, kp, kd, scale, decimation=4, extra=1, bits=64):
     """anymal_terrain.py:443-451 then vec_task's extra simulate, in fp64 (bits=32: the same restatement in float)."""
     dt = np.float64 if bits == 64 else np.float32
-    c = lambda a: np.ascontiguousarray(a, dtype=dt)  # noqa: E731
+    c = lambda a: np.array(a, dtype=dt, order="C")  # a copy: the oracle steps it in place  # noqa: E731
     sim = OracleSim(flat, H.ANYMAL_PARAMS, real_bits=bits)
     r, d, mu = c(root), c(dof), c(mu)
     cf = np.zeros((root.shape[0], flat["nb"], 3), dt)
