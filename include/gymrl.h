@@ -172,7 +172,7 @@ int rl_opt_partials_size(void);
  * rl_linear_bwd: the backward of rl_linear_fwd with ELU from its output y: dZ = dy * (y > 0 ? 1 : y + 1);
  *   dx [M][K] fp16 = dZ . w (w [N][K] as in rl_linear_fwd; null dx: skipped; needs K % 128 == 0);
  *   wpart [splits][N][K] f32 = per row block of M / splits rows, dZ^T . x; bpart [splits][N] f32 = column sums of
- *   dZ (null: skipped); pstride 0 = those layouts, else block s of both starts s * pstride floats in (the merged
+ *   dZ (null: skipped; bpart needs wpart, computed in the same pass); pstride 0 = those layouts, else block s of both starts s * pstride floats in (the merged
  *   layout bpart = wpart + N*K, pstride = N*K + N: one rl_splitk_accum finishes a weight and its bias when their
  *   gradients are adjacent).  wpart 16-byte aligned.  Finish with rl_splitk_accum (fixed order).  M % 128 == 0,
  *   M % (64 splits) == 0.

@@ -257,10 +257,16 @@ int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_verti
       if (xmax > cx0 + 1.25 * hs) f |= TCELL_XHI;
       if (ymin < cy0 - 0.25 * hs) f |= TCELL_YLO;
       if (ymax > cy0 + 1.25 * hs) f |= TCELL_YHI;
+      // the extents beyond the cell square, rounded up to hs / TCELL_EXT_UNITS (gs_terrain.h)
+      auto ext = [&](double d) -> uint32_t {
+        return (uint32_t)std::min(255.0, std::ceil(std::max(0.0, d) / hs * TCELL_EXT_UNITS));
+      };
+      const uint32_t ew = ext(cx0 - xmin) | ext(xmax - (cx0 + hs)) << 8 | ext(cy0 - ymin) << 16 |
+                          ext(ymax - (cy0 + hs)) << 24;
       uint32_t zb, zl;
       std::memcpy(&zb, &zmax, 4);
       std::memcpy(&zl, &zmin, 4);
-      hc[(size_t)(i * (cols - 1) + j)] = make_uint4(zb, f, zl, 0u);
+      hc[(size_t)(i * (cols - 1) + j)] = make_uint4(zb, f, zl, ew);
     }
   }
   // block summary for the query's first cull (gs_terrain.h sphere_contact): the highest cell top of each block

@@ -43,7 +43,7 @@
 struct TerrainDev {
   const float4* v;     // [rows*cols] world xyz (transform applied), w unused
   const uint4* cell;   // [(rows-1)*(cols-1)]: x = top height (float bits), y = footprint flags,
-                       // z = bottom height (float bits), w unused
+                       // z = bottom height (float bits), w = footprint extents (TCELL_EXT_*)
   const float* blk;    // [ceil((rows-1)/TERRAIN_BLK)][bcols]: the highest top of each block of cells
   const float* sq4;    // [(rows-1)*(cols-1)]: the highest top of the 4 x 4 cells starting at each cell (clipped)
   int rows, cols, bcols;
@@ -56,6 +56,11 @@ struct TerrainDev {
 #define TCELL_XHI 2u
 #define TCELL_YLO 4u
 #define TCELL_YHI 8u
+// footprint extents of a cell (its word's w): how far its vertices reach beyond the cell square towards -x, +x,
+// -y, +y, one byte each, in units of hs / 64 rounded up (the flags alone bounded a vertex moved by
+// less than a quarter cell -- set only past 0.25 hs -- by the bare cell square; the extents bound every vertex the
+// input check admits, up to 1.001 hs = 65 units)
+#define TCELL_EXT_UNITS 64.0f
 
 namespace gs_terrain {
 
@@ -204,10 +209,10 @@ GS_HD bool sphere_contact_scan(const TerrainDev& T, const float* p, float r, flo
   auto cell = [&](int i, int j, const uint4& cinfo, const float4* pre = nullptr) {
     const float top = gs_bits_float(cinfo.x);
     if (zlo > top) return;
-    const uint32_t f = cinfo.y;
-    const float cx0 = T.x0 + (float)i * T.hs, cy0 = T.y0 + (float)j * T.hs;
-    const float bx0 = cx0 - ((f & TCELL_XLO) ? T.hs : 0.f), bx1 = cx0 + ((f & TCELL_XHI) ? 2.f : 1.f) * T.hs;
-    const float by0 = cy0 - ((f & TCELL_YLO) ? T.hs : 0.f), by1 = cy0 + ((f & TCELL_YHI) ? 2.f : 1.f) * T.hs;
+    const uint32_t x = cinfo.w;
+    const float cx0 = T.x0 + (float)i * T.hs, cy0 = T.y0 + (float)j * T.hs, u = T.hs * (1.f / TCELL_EXT_UNITS);
+    const float bx0 = cx0 - u * (float)(x & 255u), bx1 = cx0 + T.hs + u * (float)((x >> 8) & 255u);
+    const float by0 = cy0 - u * (float)((x >> 16) & 255u), by1 = cy0 + T.hs + u * (float)(x >> 24);
     if (p[0] + reach < bx0 || p[0] - reach > bx1 || p[1] + reach < by0 || p[1] - reach > by1) return;
     const float dx = fmaxf(fmaxf(bx0 - pad - p[0], p[0] - bx1 - pad), 0.f);
     const float dy = fmaxf(fmaxf(by0 - pad - p[1], p[1] - by1 - pad), 0.f);

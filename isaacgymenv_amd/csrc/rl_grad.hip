@@ -35,8 +35,9 @@ __global__ __launch_bounds__(kAccBlock) void k_splitk_accum(const void* __restri
     if (i0 >= n) return;
     float acc[kVec] = {0.f, 0.f, 0.f, 0.f};
     if (vec) {
-        // the partials in batches of 8 loads issued before any is added (one load latency per batch, not per
-        // partial); the additions stay in ascending partial order
+        // the partials in batches of 16 loads issued before any is added (one load latency per batch, not per
+        // partial); the additions stay in ascending partial order (a last batch past P reloads partial P - 1 in
+        // its spare slots and never adds them)
         constexpr int kBatch = 16;
         for (int p0 = 0; p0 < P; p0 += kBatch) {
             float4 v[kBatch];

@@ -467,6 +467,8 @@ extern "C" int rl_linear_bwd(const void* dy, const void* y, int32_t M, int32_t N
     return rl_set_error("rl_linear_bwd: M % 128, N % 128, K % 4 and 8-byte aligned rows required");
   if (splits <= 0 || M % (splits * kTnStep) != 0)
     return rl_set_error("rl_linear_bwd: M must split into row blocks of multiples of 64");
+  // (the bias partials come out of the weight-gradient kernel's pass: bpart alone would be left unwritten)
+  if (bpart && !wpart) return rl_set_error("rl_linear_bwd: bias partials (bpart) need the weight partials (wpart)");
   hipStream_t st = (hipStream_t)stream;
   const auto* DY = static_cast<const _Float16*>(dy);
   const auto* Yv = static_cast<const _Float16*>(y);

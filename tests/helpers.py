@@ -278,7 +278,7 @@ def read_state(sim, nd):
     st = sim.state.cpu().numpy().astype(np.float64)
     n = st.shape[1]
     root = st[0:13].T.copy()
-    dof = np.stack([st[13:13 + nd].T, st[13 + nd:].T], axis=-1)
+    dof = np.ascontiguousarray(np.stack([st[13:13 + nd].T, st[13 + nd:].T], axis=-1))
     return root, dof
 
 
@@ -366,7 +366,7 @@ def oracle_run(flat, params, root, dof, tau, mu, bits=64, steps=1, nc=None, nsen
     sim_kw = {k: c(kw[k]) for k in ("pos_targets", "vel_targets") if k in kw}
     o = OracleSim(flat, params, real_bits=bits, **ctor)
     n = root.shape[0]
-    r, d = np.array(root, dtype=dt), np.array(dof, dtype=dt)  # copies: the oracle steps them in place
+    r, d = np.array(root, dtype=dt, order="C"), np.array(dof, dtype=dt, order="C")  # copies: stepped in place
     cf = np.zeros((n, nc, 3), dt) if nc else None
     sens = np.zeros((n, nsens, 6), dt) if nsens else None
     for _ in range(steps):

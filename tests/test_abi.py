@@ -105,3 +105,15 @@ def test_ctypes_struct_layouts_match_the_headers(tmp_path):
 
 def C_sizeof(py):
     return ctypes.sizeof(py)
+
+
+def test_linear_bwd_rejects_bias_partials_without_weight_partials():
+    """rl_linear_bwd computes the bias partials in the weight-gradient pass, so bpart without wpart
+    is refused before any launch (no GPU needed) instead of returning 0 with bpart unwritten."""
+    from isaacgymenv_amd.rl import gae
+    L = gae.lib()
+    buf = (ctypes.c_double * 4096)()
+    p = ctypes.addressof(buf)
+    rc = L.rl_linear_bwd(p, p, 128, 128, p, 128, 128, p, None, 1, None, p, 0, None)
+    assert rc != 0
+    assert b"wpart" in L.rl_last_error()

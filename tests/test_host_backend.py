@@ -397,3 +397,48 @@ def test_fixed_base_planar_chain_on_ground_stays_finite():
     assert np.isfinite(g_cf).all()
     np.testing.assert_array_equal(g_cf[:, 1], 0.0)  # the cart (body 1): every row has zero response
     np.testing.assert_array_equal(o_cf[:, 1], 0.0)
+
+
+def test_terrain_query_on_jittered_mesh_matches_oracle():
+    """the cell cull of gs_terrain.h must bound every vertex the mesh check admits, not only the
+    terrain_utils moves of exactly one cell.  A heightfield-grid mesh whose vertices are jittered off their grid
+    points by up to 0.2 cells in x and y (and a few by a whole cell), queried at 100k random spheres on the host
+    backend (the same gs_terrain.h source as the kernels) against the oracle's scan of every cell in range, which
+    culls nothing."""
+    from isaacgymenv_amd.isaacgym import _lib, terrain_utils
+    rng = np.random.RandomState(9)
+    rows, cols, hs = 60, 60, 0.1
+    hf = (rng.randint(-12, 12, (rows, cols)) * 4).astype(np.int16)
+    v, t = terrain_utils.convert_heightfield_to_trimesh(hf, hs, 0.005, None)
+    v = v.astype(np.float64)
+    v[:, :2] += rng.uniform(-0.2, 0.2, (v.shape[0], 2)) * hs
+    whole = rng.rand(v.shape[0]) < 0.02
+    v[whole, 0] += np.where(rng.rand(whole.sum()) < 0.5, -1.0, 1.0) * hs * 0.75
+    grid = v.reshape(rows, cols, 3)
+    # the outer rows' x and columns' y on their grid lines: they define the grid origin and spacing
+    grid[0, :, 0], grid[-1, :, 0] = 0.0, (rows - 1) * hs
+    grid[:, 0, 1], grid[:, -1, 1] = 0.0, (cols - 1) * hs
+    ter = H.mesh_terrain(v.astype(np.float32), t, rows, cols, hs, shift=(-3.0, -3.0, 0.0))
+    art, flat = H.anymal()
+    params = dict(H.ANYMAL_PARAMS, has_ground=0)
+    gym, sim = H.make_host_sim("anymal", 1, params, terrain=ter)
+    o = ter["oracle"]
+    n = 100000
+    c = np.zeros((n, 3))
+    c[:, 0] = rng.uniform(o["x0"] + 0.2, o["x0"] + (rows - 2) * hs - 0.2, n)
+    c[:, 1] = rng.uniform(o["y0"] + 0.2, o["y0"] + (cols - 2) * hs - 0.2, n)
+    gi = np.clip(np.round((c[:, 0] - o["x0"]) / hs).astype(int), 0, rows - 1)
+    gj = np.clip(np.round((c[:, 1] - o["y0"]) / hs).astype(int), 0, cols - 1)
+    c[:, 2] = o["vertices"].reshape(rows, cols, 3)[gi, gj, 2] + rng.uniform(-0.1, 0.15, n)
+    r = rng.choice([0.02, 0.05, 0.1], n)
+    cf, rf = c.astype(np.float32), r.astype(np.float32)
+    out = np.zeros((n, 5), np.float32)
+    _lib.check(_lib.lib().gs_debug_terrain_query(sim.handle, cf.ctypes.data, rf.ctypes.data, n, out.ctypes.data,
+                                                 None), "terrain query")
+    ref = OracleSim(flat, params, terrain=o).terrain_query(cf.astype(np.float64), rf.astype(np.float64))
+    found_g, found_o = out[:, 0] > 0.5, ref[:, 0] > 0.5
+    assert found_o.mean() > 0.3
+    assert (found_g != found_o).mean() < 2e-4
+    both = found_g & found_o
+    dsep = np.abs(out[both, 1] - ref[both, 1])
+    assert (dsep > 1e-4).mean() < 5e-4, ((dsep > 1e-4).mean(), dsep.max())

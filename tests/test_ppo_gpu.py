@@ -584,3 +584,52 @@ def test_mfma_mlp_input_gradient_and_autograd_grad():
     assert all(p_.grad is None for p_ in mlp.parameters())
     for g_, w_ in zip(got, want):
         assert float((g_.float() - w_).abs().max()) <= 5e-3 * float(w_.abs().max()) + 1e-4
+
+
+def test_mfma_mlp_merged_weight_bias_gradient_path(monkeypatch):
+    """with direct gradients and each Linear's weight and bias gradients adjacent in ONE flat buffer
+    (the learner's layout, a2c_continuous.A2CAgent), _LinearELUFn takes the merged partial buffer and one
+    rl_splitk_accum over the span; with separate gradient tensors the two-finish path.  Both are the same fixed-order
+    sums of the same partials, so the gradients agree bit for bit."""
+    from isaacgymenv_amd.rl import gae, network
+    monkeypatch.setattr(network, "USE_MFMA_LAYERS", True)
+    torch.manual_seed(5)
+    mlp, _ = _mlp_pair(256, [256, 128])
+    lins = [m for m in mlp if isinstance(m, network.Linear)]
+    for m in lins:
+        m.direct_grad = True
+    x = torch.randn(8192, 256, device="cuda")
+    gout = torch.randn(8192, 128, device="cuda")
+    seen = []
+    orig = gae.linear_bwd
+
+    def spy(*a, **kw):
+        seen.append(kw.get("pstride", 0))
+        return orig(*a, **kw)
+    monkeypatch.setattr(gae, "linear_bwd", spy)
+
+    def run(flat_layout):
+        if flat_layout:  # weight then bias of each layer, back to back in one buffer (as the learner's flat grad)
+            n = sum(p_.numel() for p_ in mlp.parameters())
+            flat = torch.zeros(n, device="cuda")
+            o = 0
+            for m in lins:
+                for p_ in (m.weight, m.bias):
+                    p_.grad = flat[o:o + p_.numel()].view_as(p_)
+                    o += p_.numel()
+        else:
+            for p_ in mlp.parameters():
+                p_.grad = None
+        seen.clear()
+        with torch.autocast("cuda", dtype=torch.float16):
+            assert mlp._fused(x)
+            y = mlp(x)
+        (y.float() * gout).sum().backward()
+        return [p_.grad.clone() for p_ in mlp.parameters()], list(seen)
+
+    merged, pstrides_m = run(True)
+    separate, pstrides_s = run(False)
+    assert pstrides_m and all(s > 0 for s in pstrides_m), pstrides_m  # the merged layout on every layer
+    assert pstrides_s and all(s == 0 for s in pstrides_s), pstrides_s
+    for a, b in zip(merged, separate):
+        assert torch.equal(a, b)
