@@ -416,7 +416,23 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
     return fail("gs_sim_set_model: hull vertices / self-collision pairs exceed compiled maxima");
   for (int sh = 0; sh < m->num_shapes; ++sh) {
     for (int k = 0; k < 3; ++k) h.shc[sh][k] = (float)m->shape_sphere[4 * sh + k];
-    h.shc[sh][3] = (float)(m->shape_sphere[4 * sh + 3] * (1.0 + 1e-4) + 1e-5);
+    // the sphere must hold the shape's ground candidates too (the solver skips a shape whose sphere clears the
+    // ground): a cylinder's candidates are its end points with the cylinder's radius (a capsule to the plane
+    // test), which reach hl + r along the axis, beyond the cylinder's own bounding sphere
+    // sqrt(hl^2 + r^2) (round 5: a UsefulHound leg cylinder's end 10 mm from the ground was skipped at a 42 mm
+    // sphere clearance; the pair broadphase only gets looser by it)
+    double reach = m->shape_sphere[4 * sh + 3];
+    for (int c = 0; c < m->num_candidates; ++c) {
+      if (m->cand_shape && m->cand_shape[c] == sh && m->cand_dyn[c] < 0) {
+        double d2 = 0.0;
+        for (int k = 0; k < 3; ++k) {
+          const double d = m->cand_point[3 * c + k] - m->shape_sphere[4 * sh + k];
+          d2 += d * d;
+        }
+        reach = std::max(reach, std::sqrt(d2) + m->cand_radius[c]);
+      }
+    }
+    h.shc[sh][3] = (float)(reach * (1.0 + 1e-4) + 1e-5);
     h.shkind[sh] = m->shape_kind[sh];
     h.shbody[sh] = m->shape_body[sh];
     h.shlink[sh] = m->shape_link[sh];

@@ -452,6 +452,64 @@ __device__ __forceinline__ unsigned long long quad_or64(unsigned long long m) {
   return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
 }
 
+// The replicated narrowphase (the round-4 path, now the fallback of team_self_contacts when a lane holds more
+// contacts than it stages): every lane publishes its chain's shapes' full poses (lane 0 also the root's) to the
+// team's LDS table, and each lane of a team runs gs_pairs.h self_contacts over the team's near pairs.
+template <class T>
+__device__ __forceinline__ int team_narrow_replicated(const DevModel* __restrict__ M, const DevParams& P,
+                                                   const float* __restrict__ mu_g, int N, int e, int lc,
+                                                   const float (&R0)[9], const float (&R)[T::T_CL][9],
+                                                   const float (&X)[T::T_CL][3], unsigned long long near,
+                                                   float* __restrict__ shw_tab, const float* __restrict__ sct,
+                                                   float* __restrict__ pool) {
+  constexpr int TPW = kTeamsPerBlock;
+  const int team = threadIdx.x >> 2;
+  float* tab = shw_tab + team;
+  __syncthreads();  // the staging above may still be read
+  // full shape poses for the narrowphase: R (9), centre (3), bounding-sphere centre (3)
+#pragma unroll
+  for (int j = 0; j < T::T_SPC; ++j) {
+    const int sh = T::T_RS + lc * T::T_SPC + j;
+    const int k = T::sh_body[T::T_RS + j] - 1;
+    const float* ps = sct + ShapeTab<T>::POSE + 15 * sh;
+    float Rs[9], t[3], c[3];
+    mat3mul(R[k], ps, Rs);
+    mat3vec(R[k], ps + 9, t);
+    mat3vec(R[k], ps + 12, c);
+#pragma unroll
+    for (int f = 0; f < 9; ++f) tab[(kShW * sh + f) * TPW] = Rs[f];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      tab[(kShW * sh + 9 + f) * TPW] = X[k][f] + t[f];
+      tab[(kShW * sh + 12 + f) * TPW] = X[k][f] + c[f];
+    }
+  }
+  if (lc == 0) {
+#pragma unroll
+    for (int sh = 0; sh < T::T_RS; ++sh) {
+      const float* ps = sct + ShapeTab<T>::POSE + 15 * sh;
+      float Rs[9], t[3], c[3];
+      mat3mul(R0, ps, Rs);
+      mat3vec(R0, ps + 9, t);
+      mat3vec(R0, ps + 12, c);
+#pragma unroll
+      for (int f = 0; f < 9; ++f) tab[(kShW * sh + f) * TPW] = Rs[f];
+#pragma unroll
+      for (int f = 0; f < 3; ++f) {
+        tab[(kShW * sh + 9 + f) * TPW] = t[f];
+        tab[(kShW * sh + 12 + f) * TPW] = c[f];
+      }
+    }
+  }
+  __syncthreads();
+  // the team's near pairs (team-uniform mask) -> the narrowphase of those pairs, replicated in the team's lanes
+  const unsigned long long tmask = quad_or64(near);
+  int cnt = 0;
+  if (tmask) cnt = self_contacts<T, TPW, RW, RowSlots<T>::PER_POOL>(M, P, mu_g, N, e, tab, pool, ShapeConstsTab{sct},
+                                                                    tmask);
+  return cnt;
+}
+
 // Self-collision prepass of a team.  Broadphase in registers, every substep: each lane holds its
 // chain's shapes as core segments + radius (a sphere is a point segment; boxes / hulls their bounding sphere) and
 // the root's; it tests the pairs root x own chain, own chain x itself, own chain x chain lc+1 and (lanes 0, 1)
@@ -489,8 +547,8 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
   // (sa / sb: the shape is a capsule core segment; spheres, boxes and hulls are points here -- compile-time
   // kinds, so a point pair is exact on the midpoint test and a point-capsule pair takes the point-segment
   // distance instead of the segment-segment one)
-  auto test = [&](const float* a0, const float* a1, float ra, float ha, bool sa, const float* b0, const float* b1,
-                  float rb, float hb, bool sb, unsigned long long bit) {
+  auto test = [&](const float* a0, const float* a1, float ra, float ha, bool sa, int, const float* b0, const float* b1,
+                  float rb, float hb, bool sb, int, unsigned long long bit) {
     const float rr = ra + rb + off;
     float dc = 0.f;
 #pragma unroll
@@ -515,109 +573,237 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
     }
     if (d2 < rr * rr) near |= bit;
   };
+  // every pair site of the lane, in a fixed order: f(segment a, radius, half length, capsule?, shape, segment b, ...,
+  // the pair's bit); the root shapes' and the neighbour chains' segments are formed here
+  auto visit = [&](auto&& f) {
 #pragma unroll
-  for (int sr = 0; sr < RSH; ++sr) {
-    const float* rt = sct + ShapeTab<T>::ROOT + 8 * sr;
-    const float l0[3] = {rt[0], rt[1], rt[2]}, l1[3] = {rt[3], rt[4], rt[5]};
-    const float rr = rt[6], rhl = rt[7];
-    float r0[3], r1[3];
-    mat3vec(R0, l0, r0);
-    mat3vec(R0, l1, r1);
-#pragma unroll
-    for (int j = 0; j < SPC; ++j)
-      if (team_pair<T>(sr, RSH + j))
-        test(r0, r1, rr, rhl, T::shkind[sr] == 1, p0[j], p1[j], rad[j], hl[j], T::shkind[RSH + j] == 1,
-             team_pair_bit<T>(lc, sr, -1, 0, j));
-  }
-#pragma unroll
-  for (int j = 0; j < SPC; ++j)
-#pragma unroll
-    for (int j2 = j + 1; j2 < SPC; ++j2)
-      if (team_pair<T>(RSH + j, RSH + j2))
-        test(p0[j], p1[j], rad[j], hl[j], T::shkind[RSH + j] == 1, p0[j2], p1[j2], rad[j2], hl[j2],
-             T::shkind[RSH + j2] == 1, team_pair_bit<T>(lc, 0, j, 0, j2));
-  // chains lc + 1 (every lane) and lc + 2 (lanes 0 and 1): each inter-chain pair exactly once
-#pragma unroll
-  for (int dl = 1; dl <= 2; ++dl) {
-    float q0[SPC][3], q1[SPC][3];
-#pragma unroll
-    for (int j = 0; j < SPC; ++j) {
-#pragma unroll
-      for (int f = 0; f < 3; ++f) {
-        q0[j][f] = dl == 1 ? qperm<0x39>(p0[j][f]) : qperm<0x4E>(p0[j][f]);
-        q1[j][f] = dl == 1 ? qperm<0x39>(p1[j][f]) : qperm<0x4E>(p1[j][f]);
-      }
-    }
-    if (dl == 1 || lc < 2) {
+    for (int sr = 0; sr < RSH; ++sr) {
+      const float* rt = sct + ShapeTab<T>::ROOT + 8 * sr;
+      const float l0[3] = {rt[0], rt[1], rt[2]}, l1[3] = {rt[3], rt[4], rt[5]};
+      const float rr = rt[6], rhl = rt[7];
+      float r0[3], r1[3];
+      mat3vec(R0, l0, r0);
+      mat3vec(R0, l1, r1);
 #pragma unroll
       for (int j = 0; j < SPC; ++j)
-#pragma unroll
-        for (int j2 = 0; j2 < SPC; ++j2)
-          if (team_pair<T>(RSH + j, RSH + SPC + j2))
-            test(p0[j], p1[j], rad[j], hl[j], T::shkind[RSH + j] == 1, q0[j2], q1[j2], rad[j2], hl[j2],
-                 T::shkind[RSH + j2] == 1, team_pair_bit<T>(lc, 0, j, dl, j2));
+        if (team_pair<T>(sr, RSH + j))
+          f(r0, r1, rr, rhl, T::shkind[sr] == 1, sr, p0[j], p1[j], rad[j], hl[j], T::shkind[RSH + j] == 1,
+            RSH + lc * SPC + j, team_pair_bit<T>(lc, sr, -1, 0, j));
     }
-  }
+#pragma unroll
+    for (int j = 0; j < SPC; ++j)
+#pragma unroll
+      for (int j2 = j + 1; j2 < SPC; ++j2)
+        if (team_pair<T>(RSH + j, RSH + j2))
+          f(p0[j], p1[j], rad[j], hl[j], T::shkind[RSH + j] == 1, RSH + lc * SPC + j, p0[j2], p1[j2], rad[j2], hl[j2],
+            T::shkind[RSH + j2] == 1, RSH + lc * SPC + j2, team_pair_bit<T>(lc, 0, j, 0, j2));
+    // chains lc + 1 (every lane) and lc + 2 (lanes 0 and 1): each inter-chain pair exactly once
+#pragma unroll
+    for (int dl = 1; dl <= 2; ++dl) {
+      float q0[SPC][3], q1[SPC][3];
+#pragma unroll
+      for (int j = 0; j < SPC; ++j) {
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          q0[j][g] = dl == 1 ? qperm<0x39>(p0[j][g]) : qperm<0x4E>(p0[j][g]);
+          q1[j][g] = dl == 1 ? qperm<0x39>(p1[j][g]) : qperm<0x4E>(p1[j][g]);
+        }
+      }
+      if (dl == 1 || lc < 2) {
+        const int lo = (lc + dl) & 3;
+#pragma unroll
+        for (int j = 0; j < SPC; ++j)
+#pragma unroll
+          for (int j2 = 0; j2 < SPC; ++j2)
+            if (team_pair<T>(RSH + j, RSH + SPC + j2))
+              f(p0[j], p1[j], rad[j], hl[j], T::shkind[RSH + j] == 1, RSH + lc * SPC + j, q0[j2], q1[j2], rad[j2],
+                hl[j2], T::shkind[RSH + j2] == 1, RSH + lo * SPC + j2, team_pair_bit<T>(lc, 0, j, dl, j2));
+      }
+    }
+  };
+  visit(test);
   if (__ballot(near != 0ull) == 0ull) return 0;  // wave-uniform: no team of the wave has a pair within reach
 #ifdef GS_PHASE_PROFILE
   if ((threadIdx.x & 63) == 0) atomicAdd(&gs_phase_cycles[12], 1ull);  // substeps a wave runs the narrowphase
   const long long np_t0 = clock64();
 #endif
+  // ---- narrowphase (round 5).  Each near pair's contacts are formed by the lane whose broadphase found it, from
+  // the segments it holds in registers -- the closed-form sphere / capsule rules of gs_pairs.h self_pair (the
+  // pair's a = the lower shape index, n from b to a, up to 2 contacts for a parallel capsule overlap), so the
+  // pool is the one-env-per-lane solver's -- into the lane's own LDS slots; the team then ranks its contacts
+  // by (pair, contact) through DPP, keeps the first NPK in pair order (self_contacts' cap) and every lane of the
+  // team copies them into its pool column.  Before, every lane of the team published its shapes' full poses
+  // and re-ran the whole narrowphase of the team's near pairs (10.5 k cycles per wave-substep entered: the slow
+  // waves' tail).  A lane with more than kLC contacts (not seen in the pool study) takes the
+  // replicated path below for the whole wave.
+  constexpr int kLC = 2, kSt = 9;  // contacts per lane; floats per staged contact: x (3) n (3) sep, shapes a, b
+  const int wl = threadIdx.x & 63;
   const int team = threadIdx.x >> 2;
-  float* tab = shw_tab + team;
-  __syncthreads();  // an earlier substep's narrowphase may still be reading the table
-  // full shape poses for the narrowphase: R (9), centre (3), bounding-sphere centre (3)
+  float* lslot = shw_tab + wl;                        // [f + kSt * slot][64 lanes]
+  float* tstg = shw_tab + kLC * kSt * 64 + team;      // [f + kSt * rank][TPW teams]
+  static_assert(kLC * kSt * 64 + T::NPK * kSt * TPW <= kShW * T::NS * TPW, "contact staging fits the pose table");
+  __syncthreads();  // an earlier user of the table (the TERR query list, a previous substep) is done with it
+  const float coff = P.contact_offset;
+  int cnt = 0, key0 = 0x7fffffff, key1 = 0x7fffffff;
+  bool over = false;
+  auto narrow = [&](const float* a0_, const float* a1_, float ra_, float, bool sa, int ia, const float* b0_,
+                    const float* b1_, float rb_, float, bool sb, int ib, unsigned long long bit) {
+    if (!(near & bit)) return;
+    const int q = __builtin_ctzll(bit);
+    // the pair table's orientation: a = the lower shape index
+    const bool sw = ia > ib;
+    float a0[3], a1[3], b0[3], b1[3];
 #pragma unroll
-  for (int j = 0; j < T::T_SPC; ++j) {
-    const int sh = T::T_RS + lc * T::T_SPC + j;
-    const int k = T::sh_body[T::T_RS + j] - 1;
-    const float* ps = sct + ShapeTab<T>::POSE + 15 * sh;
-    float Rs[9], t[3], c[3];
-    mat3mul(R[k], ps, Rs);
-    mat3vec(R[k], ps + 9, t);
-    mat3vec(R[k], ps + 12, c);
-#pragma unroll
-    for (int f = 0; f < 9; ++f) tab[(kShW * sh + f) * TPW] = Rs[f];
-#pragma unroll
-    for (int f = 0; f < 3; ++f) {
-      tab[(kShW * sh + 9 + f) * TPW] = X[k][f] + t[f];
-      tab[(kShW * sh + 12 + f) * TPW] = X[k][f] + c[f];
+    for (int k = 0; k < 3; ++k) {
+      a0[k] = sw ? b0_[k] : a0_[k]; a1[k] = sw ? b1_[k] : a1_[k];
+      b0[k] = sw ? a0_[k] : b0_[k]; b1[k] = sw ? a1_[k] : b1_[k];
     }
-  }
-  if (lc == 0) {
+    const float ra = sw ? rb_ : ra_, rb = sw ? ra_ : rb_;
+    const int sha = sw ? ib : ia, shb = sw ? ia : ib;
+    float pa[2][3], pb[2][3];
+    int nct = 1;
+    if (!sa && !sb) {  // sphere pair: the centres
 #pragma unroll
-    for (int sh = 0; sh < T::T_RS; ++sh) {
-      const float* ps = sct + ShapeTab<T>::POSE + 15 * sh;
-      float Rs[9], t[3], c[3];
-      mat3mul(R0, ps, Rs);
-      mat3vec(R0, ps + 9, t);
-      mat3vec(R0, ps + 12, c);
+      for (int k = 0; k < 3; ++k) { pa[0][k] = a0[k]; pb[0][k] = b0[k]; }
+    } else if (sa && sb) {  // capsule pair: the segments' closest points, both ends of a parallel overlap
+      float s, t, den, aa, ee;
+      seg_seg(a0, a1, b0, b1, s, t, den, aa, ee);
+      bool two = false;
+      float lo = 0.f, hi = 0.f;
+      if (aa > 1e-12f && ee > 1e-12f && den <= 1e-4f * aa * ee) {
+        float d1[3], w0[3], w1[3];
 #pragma unroll
-      for (int f = 0; f < 9; ++f) tab[(kShW * sh + f) * TPW] = Rs[f];
+        for (int k = 0; k < 3; ++k) { d1[k] = a1[k] - a0[k]; w0[k] = b0[k] - a0[k]; w1[k] = b1[k] - a0[k]; }
+        const float s0 = dot3f(w0, d1) / aa, s1 = dot3f(w1, d1) / aa;
+        lo = fminf(s0, s1);
+        hi = fmaxf(s0, s1);
+        lo = lo < 0.f ? 0.f : lo;
+        hi = hi > 1.f ? 1.f : hi;
+        two = hi - lo > 1e-3f;
+      }
+      if (two) {
+        nct = 2;
 #pragma unroll
-      for (int f = 0; f < 3; ++f) {
-        tab[(kShW * sh + 9 + f) * TPW] = t[f];
-        tab[(kShW * sh + 12 + f) * TPW] = c[f];
+        for (int c = 0; c < 2; ++c) {
+          const float sc2 = c == 0 ? lo : hi;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) pa[c][k] = a0[k] + sc2 * (a1[k] - a0[k]);
+          seg_closest_pt(pa[c], b0, b1, pb[c]);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { pa[0][k] = a0[k] + s * (a1[k] - a0[k]); pb[0][k] = b0[k] + t * (b1[k] - b0[k]); }
+      }
+    } else {  // sphere - capsule: the sphere centre's closest point on the core segment
+      const bool capa = sw ? sb : sa;  // side a (oriented) is the capsule
+      float e0[3], e1[3], pt[3], q3[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        e0[k] = capa ? a0[k] : b0[k]; e1[k] = capa ? a1[k] : b1[k]; pt[k] = capa ? b0[k] : a0[k];
+      }
+      seg_closest_pt(pt, e0, e1, q3);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { pa[0][k] = capa ? q3[k] : a0[k]; pb[0][k] = capa ? b0[k] : q3[k]; }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      if (c >= nct) break;
+      float nn[3] = {pa[c][0] - pb[c][0], pa[c][1] - pb[c][1], pa[c][2] - pb[c][2]};
+      float dist = sqrtf(dot3f(nn, nn));
+      if (!(dist > 1e-9f)) {  // coincident cores: the centres' direction
+        float f[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) f[k] = 0.5f * ((a0[k] + a1[k]) - (b0[k] + b1[k]));
+        float l = sqrtf(dot3f(f, f));
+        if (!(l > 1e-9f)) { f[0] = 0.f; f[1] = 0.f; f[2] = 1.f; l = 1.f; }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) nn[k] = f[k] / l;
+        dist = 0.f;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) nn[k] /= dist;
+      }
+      const float sep = dist - ra - rb;
+      if (!(sep < coff)) continue;
+      if (cnt < kLC) {
+        float* o = lslot + kSt * cnt * 64;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          o[k * 64] = 0.5f * ((pa[c][k] - ra * nn[k]) + (pb[c][k] + rb * nn[k]));
+          o[(3 + k) * 64] = nn[k];
+        }
+        o[6 * 64] = sep;
+        o[7 * 64] = __int_as_float(sha);
+        o[8 * 64] = __int_as_float(shb);
+        const int key = 2 * q + c;
+        if (cnt == 0) key0 = key; else key1 = key;
+      } else {
+        over = true;
+      }
+      ++cnt;
+    }
+  };
+  visit(narrow);
+  int cnt_team = 0;
+  if (__ballot(over) == 0ull) {
+    // the team's contacts in pair order: each contact's rank among the team's (at most 4 x kLC) keys
+    constexpr int kNone = 0x7fffffff;
+    int r0 = 0, r1 = 0;
+    auto tally = [&](int k) {
+      r0 += k < key0;
+      r1 += k < key1;
+      cnt_team += k != kNone;
+    };
+    tally(key0); tally(key1);
+    {
+      const int a = qperm_i<0x39>(key0), b = qperm_i<0x39>(key1);
+      tally(a); tally(b);
+    }
+    {
+      const int a = qperm_i<0x4E>(key0), b = qperm_i<0x4E>(key1);
+      tally(a); tally(b);
+    }
+    {
+      const int a = qperm_i<0x93>(key0), b = qperm_i<0x93>(key1);
+      tally(a); tally(b);
+    }
+#pragma unroll
+    for (int i = 0; i < kLC; ++i) {
+      const int rk = i == 0 ? r0 : r1;
+      if (i < cnt && rk < T::NPK) {
+        const float* src = lslot + kSt * i * 64;
+        float* dst = tstg + kSt * rk * TPW;
+#pragma unroll
+        for (int f = 0; f < kSt; ++f) dst[f * TPW] = src[f * 64];
       }
     }
+    __syncthreads();
+    cnt_team = cnt_team < T::NPK ? cnt_team : T::NPK;
+#pragma unroll
+    for (int r = 0; r < T::NPK; ++r) {
+      if (r < cnt_team) {
+        const float* src = tstg + kSt * r * TPW;
+        float* o = pool + RowSlots<T>::PER_POOL * r * RW;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          o[(kPoolX + k) * RW] = src[k * TPW];
+          o[(kPoolN + k) * RW] = src[(3 + k) * TPW];
+        }
+        o[kPoolSep * RW] = src[6 * TPW];
+        pool_entry_finish<RW>(M, mu_g, N, e, __float_as_int(src[7 * TPW]), __float_as_int(src[8 * TPW]), o);
+      }
+    }
+  } else {
+    cnt_team = team_narrow_replicated<T>(M, P, mu_g, N, e, lc, R0, R, X, near, shw_tab, sct, pool);
   }
-  __syncthreads();
-#ifdef GS_PHASE_PROFILE
-  if ((threadIdx.x & 63) == 0) atomicAdd(&gs_phase_cycles[14], (unsigned long long)(clock64() - np_t0));
-#endif
-  // the team's near pairs (team-uniform mask) -> the narrowphase of those pairs, replicated in the team's lanes
-  const unsigned long long tmask = quad_or64(near);
-  int cnt = 0;
-  if (tmask) cnt = self_contacts<T, TPW, RW, RowSlots<T>::PER_POOL>(M, P, mu_g, N, e, tab, pool, ShapeConstsTab{sct},
-                                                                    tmask);
 #ifdef GS_PHASE_PROFILE
   if ((threadIdx.x & 63) == 0) {
     atomicAdd(&gs_phase_cycles[13], (unsigned long long)(clock64() - np_t0));
-    atomicAdd(&gs_phase_cycles[15], (unsigned long long)__popcll(__ballot(tmask != 0ull)));  // teams' lanes with pairs
-    atomicAdd(&gs_phase_cycles[10], (unsigned long long)__popcll(tmask));  // (lane 0's team) near pairs
+    atomicAdd(&gs_phase_cycles[15], (unsigned long long)__popcll(__ballot(quad_or64(near) != 0ull)));
+    atomicAdd(&gs_phase_cycles[10], (unsigned long long)__popcll(quad_or64(near)));  // (lane 0's team) near pairs
   }
 #endif
-  return cnt;
+  return cnt_team;
 }
 
 // TERR (trimesh terrain): a candidate sphere at x (relative to the root origin p) against the

@@ -344,6 +344,15 @@ def parity_report(line):
             f.write(line + "\n")
 
 
+def parity_dump(name, **arrays):
+    """On a failing parity check, keep its inputs and outputs for a CPU replay: an .npz under $PARITY_DUMP when set
+    (the GPU round scripts point it into gpurun_out/, which comes back from the box)."""
+    path = os.environ.get("PARITY_DUMP")
+    if path:
+        os.makedirs(path, exist_ok=True)
+        np.savez_compressed(os.path.join(path, name + ".npz"), **arrays)
+
+
 def _field_ratios(a, d, tol, n):
     """{field: [n]} -- per env, the largest |a - d| / (atol + rtol |d|) over the field's elements."""
     out = {}

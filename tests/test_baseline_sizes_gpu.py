@@ -20,6 +20,10 @@ from tests import helpers as H
 pytestmark = pytest.mark.gpu
 
 N = 4096
+# the one-simulate tolerances with the float32 resolution of a world position added to the
+# pose: the tasks place their envs on a grid hundreds of metres wide, where one ulp of a coordinate is up to
+# 3e-5 m (2 ulp = 2.4e-7 relative)
+TOL = dict(H.STATE_TOL, pose=(2e-5, 2.4e-7))
 
 
 def _make(task, monkeypatch):
@@ -71,8 +75,13 @@ def test_ant_4096_one_simulate_matches_oracle(monkeypatch):
         o_r, o_d, _, o_s = H.oracle_run(flat, H.ANT_PARAMS, r, d, tau[idx], mu[idx], bits, nsens=4,
                                         sensor_bodies=H.ANT_FEET)
         return H.state_fields(o_r, o_d, sens=o_s)
-    H.assert_close_or_explained(H.state_fields(g_root, g_dof, sens=g_sens), H.state_fields(o_root, o_dof, sens=o_sens),
-                                rerun, what=f"ant {N} envs (30 task steps), one simulate vs oracle")
+    try:
+        H.assert_close_or_explained(H.state_fields(g_root, g_dof, sens=g_sens),
+                                    H.state_fields(o_root, o_dof, sens=o_sens), rerun, tol=TOL,
+                                    what=f"ant {N} envs (30 task steps), one simulate vs oracle")
+    except AssertionError:
+        H.parity_dump("ant4096", root=root, dof=dof, mu=mu, tau=tau, g_root=g_root, g_dof=g_dof, g_sens=g_sens)
+        raise
 
 
 def test_hound_4096_split_simulate_matches_oracle(monkeypatch):
@@ -97,5 +106,9 @@ def test_hound_4096_split_simulate_matches_oracle(monkeypatch):
         r, d = H.perturbed(root, dof, idx, rng_)
         r, d, c, _ = H.oracle_run(flat, H.HOUND_PARAMS, r, d, tau[idx], mu[idx], bits, nc=24)
         return H.state_fields(r, d, c)
-    H.assert_close_or_explained(H.state_fields(g_root, g_dof, g_cf), H.state_fields(o_root, o_dof, o_cf), rerun,
-                                what=f"hound {N} envs (30 task steps), split simulate vs oracle")
+    try:
+        H.assert_close_or_explained(H.state_fields(g_root, g_dof, g_cf), H.state_fields(o_root, o_dof, o_cf), rerun,
+                                    tol=TOL, what=f"hound {N} envs (30 task steps), split simulate vs oracle")
+    except AssertionError:
+        H.parity_dump("hound4096", root=root, dof=dof, mu=mu, tau=tau, g_root=g_root, g_dof=g_dof, g_cf=g_cf)
+        raise

@@ -442,3 +442,21 @@ def test_terrain_query_on_jittered_mesh_matches_oracle():
     both = found_g & found_o
     dsep = np.abs(out[both, 1] - ref[both, 1])
     assert (dsep > 1e-4).mean() < 5e-4, ((dsep > 1e-4).mean(), dsep.max())
+
+
+def test_cylinder_end_near_ground_is_not_skipped():
+    """Round 5, found by the 4096-env UsefulHound parity test (tests/test_baseline_sizes_gpu.py, env 680 of a state
+    the task reached after 30 steps, fixture tests/golden/hound_cylinder_ground_case.npz): the solver skips a shape
+    whose bounding sphere clears the ground, but a cylinder's ground candidates are capsule ends (hl + r from the
+    centre) that reach beyond the cylinder's own bounding sphere sqrt(hl^2 + r^2).  A leg cylinder's end 10 mm from
+    the ground was skipped at a 42 mm sphere clearance; the spinning robot's contact impulse was lost (q off by
+    8e-4 rad in one simulate).  gs_sim_set_model now widens each shape's sphere to its candidates."""
+    z = np.load(os.path.join(GOLDEN, "hound_cylinder_ground_case.npz"))
+    root, dof, mu, tau = z["root"], z["dof"], z["mu"], z["tau"]
+    art, flat = H.hound()
+    for params in (H.HOUND_PARAMS, dict(H.HOUND_PARAMS, pos_iters=1, vel_iters=0)):
+        _, sim, g_root, g_dof = _host("hound", 1, params, root, dof, tau, mu, 18)
+        o_root, o_dof, _, _ = H.oracle_run(flat, params, root, dof, tau, mu, nc=24)
+        np.testing.assert_allclose(g_dof[:, :, 0], o_dof[:, :, 0], atol=2e-6)
+        np.testing.assert_allclose(g_dof[:, :, 1], o_dof[:, :, 1], atol=5e-4, rtol=1e-4)
+        np.testing.assert_allclose(g_root[:, 7:], o_root[:, 7:], atol=5e-4, rtol=1e-4)

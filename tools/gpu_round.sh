@@ -8,6 +8,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 ROOT=$PWD
 export PARITY_REPORT=$OUT/parity.txt
+export PARITY_DUMP=$OUT/dump
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && echo "pytest ok" &&
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && echo "smoke ok" &&
 timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err && cat $OUT/bench.json &&
