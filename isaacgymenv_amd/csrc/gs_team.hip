@@ -259,7 +259,7 @@ __device__ __forceinline__ void stage_chain_model(const DevModel* __restrict__ M
 }
 
 // Team-uniform shape constants of the self-collision passes, staged once per launch: per shape
-// (ShapeConstsTab) bounding radius, margin, capsule half length; then per root shape the core segment in
+// (ShapeConstsTab) bounding radius, margin, capsule half length, 256 body + link; then per root shape the core segment in
 // the root frame (ends l0, l1), radius and half length (broadphase)
 template <class T>
 struct ShapeTab {
@@ -276,7 +276,10 @@ __device__ __forceinline__ void stage_shape_consts(const DevModel* __restrict__ 
       float v = 0.f;
       if (i < S::ROOT) {
         const int sh = i / kShC, f = i - kShC * sh;
-        v = f == 0 ? M->shc[sh][3] : (f == 1 ? M->shm[sh] : (f == 2 ? M->shsize[sh][1] : 0.f));
+        // (slot 3: the shape's body and link, 256 body + link -- the team narrowphase's pool entries, no global
+        // load on that path)
+        v = f == 0 ? M->shc[sh][3]
+                   : (f == 1 ? M->shm[sh] : (f == 2 ? M->shsize[sh][1] : (float)(256 * M->shbody[sh] + M->shlink[sh])));
       } else if (i >= S::POSE) {
         const int sh = (i - S::POSE) / 15, f = (i - S::POSE) - 15 * sh;
         v = f < 9 ? M->shR[sh][f] : (f < 12 ? M->sht[sh][f - 9] : M->shc[sh][f - 12]);
@@ -413,6 +416,44 @@ __device__ __forceinline__ float seg_pt_d2(const float* s0, const float* s1, con
     out += x * x;
   }
   return out;
+}
+
+// gs_pairs.h seg_seg / seg_closest_pt with v_rcp for the divisions (~1 ulp): the team narrowphase is a serial
+// chain of them inside a wave-divergent block, where each IEEE division costs ~10 dependent instructions
+__device__ __forceinline__ void seg_seg_rcp(const float* p1, const float* q1, const float* p2, const float* q2, float& s,
+                                            float& t, float& den, float& a, float& e) {
+  float d1[3], d2[3], r[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { d1[k] = q1[k] - p1[k]; d2[k] = q2[k] - p2[k]; r[k] = p1[k] - p2[k]; }
+  a = dot3f(d1, d1);
+  e = dot3f(d2, d2);
+  const float f = dot3f(d2, r);
+  s = 0.f; t = 0.f; den = 0.f;
+  const float ia = __builtin_amdgcn_rcpf(a), ie = __builtin_amdgcn_rcpf(e);
+  auto cl = [](float x) { return __builtin_amdgcn_fmed3f(x, 0.f, 1.f); };
+  if (a <= 1e-12f && e <= 1e-12f) {
+  } else if (a <= 1e-12f) {
+    t = cl(f * ie);
+  } else {
+    const float c = dot3f(d1, r);
+    if (e <= 1e-12f) {
+      s = cl(-c * ia);
+    } else {
+      const float b = dot3f(d1, d2);
+      den = a * e - b * b;
+      s = den > 0.f ? cl((b * f - c * e) * __builtin_amdgcn_rcpf(den)) : 0.f;
+      t = (b * s + f) * ie;
+      if (t < 0.f) { t = 0.f; s = cl(-c * ia); }
+      else if (t > 1.f) { t = 1.f; s = cl((b - c) * ia); }
+    }
+  }
+}
+__device__ __forceinline__ void seg_closest_pt_rcp(const float* p, const float* a, const float* b, float* q) {
+  const float ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, ap[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
+  const float l2 = dot3f(ab, ab);
+  const float t = l2 > 0.f ? __builtin_amdgcn_fmed3f(dot3f(ap, ab) * __builtin_amdgcn_rcpf(l2), 0.f, 1.f) : 0.f;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) q[k] = a[k] + t * ab[k];
 }
 
 // shapes a < b of a topology collide (its self-collision pair table, gs_topologies.h)
@@ -667,14 +708,15 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
       for (int k = 0; k < 3; ++k) { pa[0][k] = a0[k]; pb[0][k] = b0[k]; }
     } else if (sa && sb) {  // capsule pair: the segments' closest points, both ends of a parallel overlap
       float s, t, den, aa, ee;
-      seg_seg(a0, a1, b0, b1, s, t, den, aa, ee);
+      seg_seg_rcp(a0, a1, b0, b1, s, t, den, aa, ee);
       bool two = false;
       float lo = 0.f, hi = 0.f;
       if (aa > 1e-12f && ee > 1e-12f && den <= 1e-4f * aa * ee) {
         float d1[3], w0[3], w1[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) { d1[k] = a1[k] - a0[k]; w0[k] = b0[k] - a0[k]; w1[k] = b1[k] - a0[k]; }
-        const float s0 = dot3f(w0, d1) / aa, s1 = dot3f(w1, d1) / aa;
+        const float ia = __builtin_amdgcn_rcpf(aa);
+        const float s0 = dot3f(w0, d1) * ia, s1 = dot3f(w1, d1) * ia;
         lo = fminf(s0, s1);
         hi = fmaxf(s0, s1);
         lo = lo < 0.f ? 0.f : lo;
@@ -688,7 +730,7 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
           const float sc2 = c == 0 ? lo : hi;
 #pragma unroll
           for (int k = 0; k < 3; ++k) pa[c][k] = a0[k] + sc2 * (a1[k] - a0[k]);
-          seg_closest_pt(pa[c], b0, b1, pb[c]);
+          seg_closest_pt_rcp(pa[c], b0, b1, pb[c]);
         }
       } else {
 #pragma unroll
@@ -701,7 +743,7 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
       for (int k = 0; k < 3; ++k) {
         e0[k] = capa ? a0[k] : b0[k]; e1[k] = capa ? a1[k] : b1[k]; pt[k] = capa ? b0[k] : a0[k];
       }
-      seg_closest_pt(pt, e0, e1, q3);
+      seg_closest_pt_rcp(pt, e0, e1, q3);
 #pragma unroll
       for (int k = 0; k < 3; ++k) { pa[0][k] = capa ? q3[k] : a0[k]; pb[0][k] = capa ? b0[k] : q3[k]; }
     }
@@ -709,7 +751,8 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
     for (int c = 0; c < 2; ++c) {
       if (c >= nct) break;
       float nn[3] = {pa[c][0] - pb[c][0], pa[c][1] - pb[c][1], pa[c][2] - pb[c][2]};
-      float dist = sqrtf(dot3f(nn, nn));
+      const float d2 = dot3f(nn, nn);
+      float dist = sqrtf(d2);
       if (!(dist > 1e-9f)) {  // coincident cores: the centres' direction
         float f[3];
 #pragma unroll
@@ -720,8 +763,9 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
         for (int k = 0; k < 3; ++k) nn[k] = f[k] / l;
         dist = 0.f;
       } else {
+        const float idist = __builtin_amdgcn_rsqf(d2);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) nn[k] /= dist;
+        for (int k = 0; k < 3; ++k) nn[k] *= idist;
       }
       const float sep = dist - ra - rb;
       if (!(sep < coff)) continue;
@@ -744,6 +788,9 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
     }
   };
   visit(narrow);
+#ifdef GS_PHASE_PROFILE
+  if ((threadIdx.x & 63) == 0) atomicAdd(&gs_phase_cycles[14], (unsigned long long)(clock64() - np_t0));
+#endif
   int cnt_team = 0;
   if (__ballot(over) == 0ull) {
     // the team's contacts in pair order: each contact's rank among the team's (at most 4 x kLC) keys
@@ -790,17 +837,36 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
           o[(kPoolN + k) * RW] = src[(3 + k) * TPW];
         }
         o[kPoolSep * RW] = src[6 * TPW];
-        pool_entry_finish<RW>(M, mu_g, N, e, __float_as_int(src[7 * TPW]), __float_as_int(src[8 * TPW]), o);
+        // pool_entry_finish's fields, the bodies and links from the LDS shape table
+        const int a = __float_as_int(src[7 * TPW]), b = __float_as_int(src[8 * TPW]);
+        const float nn[3] = {src[3 * TPW], src[4 * TPW], src[5 * TPW]};
+        float t1[3], t2[3];
+        gs_terrain::tangents(nn, t1, t2);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          o[(kPoolT1 + k) * RW] = t1[k];
+          o[(kPoolT2 + k) * RW] = t2[k];
+        }
+        o[kPoolMu * RW] = 0.5f * (mu_g[a * N + e] + mu_g[b * N + e]);
+        const int bla = (int)sct[kShC * a + 3], blb = (int)sct[kShC * b + 3];
+        o[kPoolBA * RW] = (float)(bla >> 8);
+        o[kPoolBB * RW] = (float)(blb >> 8);
+        o[kPoolLA * RW] = (float)(bla & 255);
+        o[kPoolLB * RW] = (float)(blb & 255);
       }
     }
   } else {
     cnt_team = team_narrow_replicated<T>(M, P, mu_g, N, e, lc, R0, R, X, near, shw_tab, sct, pool);
   }
 #ifdef GS_PHASE_PROFILE
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&gs_phase_cycles[13], (unsigned long long)(clock64() - np_t0));
-    atomicAdd(&gs_phase_cycles[15], (unsigned long long)__popcll(__ballot(quad_or64(near) != 0ull)));
-    atomicAdd(&gs_phase_cycles[10], (unsigned long long)__popcll(quad_or64(near)));  // (lane 0's team) near pairs
+  {
+    const unsigned long long tm = quad_or64(near);
+    const unsigned long long lanes = __ballot(tm != 0ull);
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&gs_phase_cycles[13], (unsigned long long)(clock64() - np_t0));
+      atomicAdd(&gs_phase_cycles[15], (unsigned long long)__popcll(lanes));  // lanes of teams with a near pair
+      atomicAdd(&gs_phase_cycles[10], (unsigned long long)__popcll(tm));  // (lane 0's team) near pairs
+    }
   }
 #endif
   return cnt_team;

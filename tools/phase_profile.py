@@ -66,9 +66,10 @@ def main():
                 print(f"  {name:36s} {buf[32 + i] / ns:10.0f}")
         print(f"  PGS chain contacts per slow wave: {buf[32 + 8] / ns:.1f}")
     if buf[12]:
-        print(f"self-collision narrowphase cycles per entry (pose table + pairs): {buf[13] / buf[12]:.0f}, of which "
-              f"the pose table + its barriers {buf[14] / buf[12]:.0f}; lanes of teams with a near pair per entry "
-              f"{buf[15] / buf[12]:.1f} of 64; lane 0's team near pairs per entry {buf[10] / buf[12]:.2f}")
+        print(f"self-collision narrowphase cycles per entry: {buf[13] / buf[12]:.0f}, of which the near pairs' "
+              f"contacts in their lanes {buf[14] / buf[12]:.0f} (the rest: ranking, staging, pool entries); lanes of "
+              f"teams with a near pair per entry {buf[15] / buf[12]:.1f} of 64; lane 0's team near pairs per entry "
+              f"{buf[10] / buf[12]:.2f}")
 
 
 if __name__ == "__main__":
