@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 5
+#define RL_ABI_VERSION 6
 
 int rl_abi_version(void);
 const char *rl_last_error(void);
@@ -182,6 +182,27 @@ int rl_linear_fwd(const void *x, int32_t M, int32_t K, int32_t ldx, const void *
 int rl_linear_transpose(const void *w, int32_t N, int32_t K, void *wt, void *stream);
 int rl_linear_bwd(const void *dy, const void *y, int32_t M, int32_t N, const void *x, int32_t K, int32_t ldx,
                   const void *w, void *dx, int32_t splits, float *wpart, float *bpart, int64_t pstride, void *stream);
+
+/*
+ * ABI 6 -- grouped layers: G equal-shaped layers in one launch (the actor and critic MLPs of rl_games' separate
+ * network, AnymalTerrainPPO.yaml `separate: True`; network.py _GroupedMLPFn).  Group g reads x + g x_gstride,
+ * w + g w_gstride, bias + g b_gstride, y / dy + g y_gstride (row stride ldy, 0: N) and writes dx + g dx_gstride
+ * (row stride lddx, 0: K) and its weight / bias partials at + g part_gstride / bpart_gstride within each block of
+ * pstride floats.  Strides in elements, multiples of 4.  groups = 1 with all strides 0 is the ungrouped call; every
+ * group computes exactly what its own ungrouped call would (same tiles, same reduction order).
+ */
+typedef struct rl_linear_groups {
+    int32_t groups;
+    int32_t ldy;
+    int32_t lddx;
+    int32_t reserved;
+    int64_t x_gstride, w_gstride, b_gstride, y_gstride, dx_gstride, part_gstride, bpart_gstride;
+} rl_linear_groups;
+int rl_linear_fwd_g(const void *x, int32_t M, int32_t K, int32_t ldx, const void *w, int32_t N, const void *bias,
+                    int32_t act, void *y, const rl_linear_groups *groups, void *stream);
+int rl_linear_bwd_g(const void *dy, const void *y, int32_t M, int32_t N, const void *x, int32_t K, int32_t ldx,
+                    const void *w, void *dx, int32_t splits, float *wpart, float *bpart, int64_t pstride,
+                    const rl_linear_groups *groups, void *stream);
 
 #ifdef __cplusplus
 }

@@ -60,11 +60,21 @@ __device__ __forceinline__ h8 load8(const _Float16* __restrict__ p, int valid) {
 // ---------------------------------------------------------------- NT: C[m][c] = sum_r A[m][r] Bt[c][r]
 // ACT: ELU epilogue.  bias: fp16 [C] or null.  C fp16 [M][ldc].  M % BM == 0, Cn % BN == 0 (host).  The MFMA takes the Bt tile as its row operand,
 // so a lane's result registers 4g .. 4g+3 are 4 consecutive columns c of one row m: one 8-byte store each.
+// Groups (blockIdx.z = g): group g reads A + g gA, Bt + g gB, bias + g gBias and writes C + g gC -- the actor and
+// critic MLPs' equal-shaped layers in one launch (rl_linear_fwd_g).
 template <int BM, int BN, bool ACT>
 __global__ __launch_bounds__(kThreads) void k_gemm_nt(const _Float16* __restrict__ A,
                                                       int lda, const _Float16* __restrict__ Bt, int ldb,
                                                       const _Float16* __restrict__ bias, _Float16* __restrict__ C,
-                                                      int ldc, int R) {
+                                                      int ldc, int R, int64_t gA, int64_t gB, int64_t gBias,
+                                                      int64_t gC) {
+  {
+    const int64_t g = blockIdx.z;
+    A += g * gA;
+    Bt += g * gB;
+    if (bias) bias += g * gBias;
+    C += g * gC;
+  }
   constexpr int TM = BM / 64, TN = BN / 64;                  // MFMA tiles per wave
   constexpr int KS = kNtStep, LD = KS + 8, CPR = KS / 8;      // reduction step, LDS row stride, chunks per row
   constexpr int CA = BM * KS / 8 / kThreads, CB = BN * KS / 8 / kThreads;  // 16-B chunks per thread
@@ -187,17 +197,28 @@ __device__ __forceinline__ h8 tr_frag(const _Float16* tile, int lane) {
   return __builtin_bit_cast(h8, v);
 }
 
+// Groups: blockIdx.z = g * splits + s; group g reads dY / Y + g gY (row stride ldy), X + g gX and writes its
+// partials at + g gP / + g gBP within each block.
 __global__ __launch_bounds__(kThreads) void k_gemm_tn(const _Float16* __restrict__ dY, const _Float16* __restrict__ Y,
-                                                      int N, const _Float16* __restrict__ X, int ldx, int K,
+                                                      int N, int ldy, const _Float16* __restrict__ X, int ldx, int K,
                                                       int rows_per_split, float* __restrict__ part,
-                                                      float* __restrict__ bpart, int64_t wstride, int64_t bstride) {
+                                                      float* __restrict__ bpart, int64_t wstride, int64_t bstride,
+                                                      int splits, int64_t gY, int64_t gX, int64_t gP, int64_t gBP) {
+  {
+    const int64_t g = blockIdx.z / splits;
+    dY += g * gY;
+    Y += g * gY;
+    X += g * gX;
+    part += g * gP;
+    if (bpart) bpart += g * gBP;
+  }
   constexpr int TS = kTnStep, CH = TS / 16;  // rows per stage, 16-B chunks per thread per operand
   __shared__ _Float16 sZ[2][TS * kTLd];  // [m][n]
   __shared__ _Float16 sX[2][TS * kTLd];  // [m][k]
   __shared__ float sbias[16][kTN + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wk = wave >> 1, wn = wave & 1;
-  const int n0 = blockIdx.x * kTN, k0 = blockIdx.y * kTN, s = blockIdx.z;
+  const int n0 = blockIdx.x * kTN, k0 = blockIdx.y * kTN, s = blockIdx.z % splits;
   const int mb = s * rows_per_split;
   const int r = lane & 31, hh = lane >> 5;
   const bool do_bias = blockIdx.y == 0 && bpart != nullptr;
@@ -218,7 +239,7 @@ __global__ __launch_bounds__(kThreads) void k_gemm_tn(const _Float16* __restrict
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const size_t row = (size_t)(m + crow + 16 * i);
-      const size_t off = row * N + n0 + ccol;
+      const size_t off = row * ldy + n0 + ccol;
       ra[i] = load8(dY + off, N - (n0 + ccol));
       ry[i] = load8(Y + off, N - (n0 + ccol));
       rb[i] = load8(X + row * ldx + k0 + ccol, K - (k0 + ccol));
@@ -300,10 +321,19 @@ __global__ __launch_bounds__(kThreads) void k_gemm_tn(const _Float16* __restrict
 // ([n][k], 16-byte stores) and read with the transpose read (8 consecutive n of one k per lane), so no W^T copy
 // is needed.  As in k_gemm_nt the k rows are the MFMA's row operand: registers 4g .. 4g+3 are 4 consecutive k of
 // one row m, one 8-byte store.  M % BM == 0, K % 128 == 0 (host).
+// Groups (blockIdx.z = g): dY / Y + g gY (row stride ldy), W + g gW, dX + g gDX (row stride lddx).
 template <int BM>
 __global__ __launch_bounds__(kThreads) void k_gemm_nn(const _Float16* __restrict__ dY, const _Float16* __restrict__ Y,
-                                                      int N, const _Float16* __restrict__ W, int K,
-                                                      _Float16* __restrict__ dX) {
+                                                      int N, int ldy, const _Float16* __restrict__ W, int K,
+                                                      _Float16* __restrict__ dX, int lddx, int64_t gY, int64_t gW,
+                                                      int64_t gDX) {
+  {
+    const int64_t g = blockIdx.z;
+    dY += g * gY;
+    Y += g * gY;
+    W += g * gW;
+    dX += g * gDX;
+  }
   constexpr int BN = 128, TM = BM / 64, TN = BN / 64;
   constexpr int KS = kNtStep, LD = KS + 8, CPR = KS / 8;
   constexpr int CA = BM * KS / 8 / kThreads, CB = KS * BN / 8 / kThreads;
@@ -327,7 +357,7 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nn(const _Float16* __restrict
     for (int i = 0; i < CA; ++i) {
       const int c = tid + i * kThreads, row = c / CPR, kc = (c % CPR) * 8;
       const int valid = N - (n0 + kc);
-      const size_t off = (size_t)(m0 + row) * N + n0 + kc;
+      const size_t off = (size_t)(m0 + row) * ldy + n0 + kc;
       ra[i] = load8(dY + off, valid);
       ry[i] = load8(Y + off, valid);
     }
@@ -393,7 +423,7 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nn(const _Float16* __restrict
         const int m = m0 + wm * (BM / 2) + i * 32 + r;
         const h4 ov = {(_Float16)acc[j][i][4 * g], (_Float16)acc[j][i][4 * g + 1], (_Float16)acc[j][i][4 * g + 2],
                        (_Float16)acc[j][i][4 * g + 3]};
-        *reinterpret_cast<h4*>(dX + (size_t)m * K + cg) = ov;
+        *reinterpret_cast<h4*>(dX + (size_t)m * lddx + cg) = ov;
       }
     }
 }
@@ -429,27 +459,38 @@ int launch_fail(const char* what) {
 
 }  // namespace
 
-extern "C" int rl_linear_fwd(const void* x, int32_t M, int32_t K, int32_t ldx, const void* w, int32_t N,
-                             const void* bias, int32_t act, void* y, void* stream) {
+extern "C" int rl_linear_fwd_g(const void* x, int32_t M, int32_t K, int32_t ldx, const void* w, int32_t N,
+                               const void* bias, int32_t act, void* y, const rl_linear_groups* grp, void* stream) {
   if (!x || !w || !y || M <= 0 || K <= 0 || N <= 0) return rl_set_error("rl_linear_fwd: null pointer or empty shape");
+  const int G = grp ? grp->groups : 1;
+  const int ldy = grp && grp->ldy ? grp->ldy : N;
+  if (G < 1 || G > 65535 || ldy < N || ldy % 4) return rl_set_error("rl_linear_fwd: bad groups or output row stride");
   if (M % 64 || N % 128 || ldx % 4 || K % 4 || !aligned8(x) || !aligned8(w) || !aligned8(y))
     return rl_set_error("rl_linear_fwd: M % 64, N % 128, K % 4 and 8-byte aligned rows required");
+  const int64_t gx = grp ? grp->x_gstride : 0, gw = grp ? grp->w_gstride : 0, gb = grp ? grp->b_gstride : 0,
+                gy = grp ? grp->y_gstride : 0;
+  if (G > 1 && ((gx | gw | gb | gy) % 4 != 0)) return rl_set_error("rl_linear_fwd: group strides must be % 4");
   hipStream_t st = (hipStream_t)stream;
   const auto* X = static_cast<const _Float16*>(x);
   const auto* W = static_cast<const _Float16*>(w);
   const auto* B = static_cast<const _Float16*>(bias);
   auto* Y = static_cast<_Float16*>(y);
-  // 128 x 128 tiles when that still gives >= 256 workgroups, else 64-row tiles
-  if ((M / 128) * (N / 128) >= 256 && M % 128 == 0) {
-    const dim3 g(M / 128, N / 128);
-    if (act) hipLaunchKernelGGL((k_gemm_nt<128, 128, true>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, N, K);
-    else hipLaunchKernelGGL((k_gemm_nt<128, 128, false>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, N, K);
+  // 128 x 128 tiles when that still gives >= 256 workgroups (over all groups), else 64-row tiles
+  if ((M / 128) * (N / 128) * G >= 256 && M % 128 == 0) {
+    const dim3 g(M / 128, N / 128, G);
+    if (act) hipLaunchKernelGGL((k_gemm_nt<128, 128, true>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, ldy, K, gx, gw, gb, gy);
+    else hipLaunchKernelGGL((k_gemm_nt<128, 128, false>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, ldy, K, gx, gw, gb, gy);
   } else {
-    const dim3 g(M / 64, N / 128);
-    if (act) hipLaunchKernelGGL((k_gemm_nt<64, 128, true>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, N, K);
-    else hipLaunchKernelGGL((k_gemm_nt<64, 128, false>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, N, K);
+    const dim3 g(M / 64, N / 128, G);
+    if (act) hipLaunchKernelGGL((k_gemm_nt<64, 128, true>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, ldy, K, gx, gw, gb, gy);
+    else hipLaunchKernelGGL((k_gemm_nt<64, 128, false>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, ldy, K, gx, gw, gb, gy);
   }
   return launch_fail("rl_linear_fwd");
+}
+
+extern "C" int rl_linear_fwd(const void* x, int32_t M, int32_t K, int32_t ldx, const void* w, int32_t N,
+                             const void* bias, int32_t act, void* y, void* stream) {
+  return rl_linear_fwd_g(x, M, K, ldx, w, N, bias, act, y, nullptr, stream);
 }
 
 extern "C" int rl_linear_transpose(const void* w, int32_t N, int32_t K, void* wt, void* stream) {
@@ -459,16 +500,23 @@ extern "C" int rl_linear_transpose(const void* w, int32_t N, int32_t K, void* wt
   return launch_fail("rl_linear_transpose");
 }
 
-extern "C" int rl_linear_bwd(const void* dy, const void* y, int32_t M, int32_t N, const void* x, int32_t K,
-                             int32_t ldx, const void* w, void* dx, int32_t splits, float* wpart, float* bpart,
-                             int64_t pstride, void* stream) {
+extern "C" int rl_linear_bwd_g(const void* dy, const void* y, int32_t M, int32_t N, const void* x, int32_t K,
+                               int32_t ldx, const void* w, void* dx, int32_t splits, float* wpart, float* bpart,
+                               int64_t pstride, const rl_linear_groups* grp, void* stream) {
   if (!dy || !y || !x || M <= 0 || N <= 0 || K <= 0) return rl_set_error("rl_linear_bwd: null pointer or empty shape");
+  const int G = grp ? grp->groups : 1;
+  const int ldy = grp && grp->ldy ? grp->ldy : N, lddx = grp && grp->lddx ? grp->lddx : K;
+  if (G < 1 || G > 65535 || ldy < N || ldy % 4 || lddx < K || lddx % 4)
+    return rl_set_error("rl_linear_bwd: bad groups or row strides");
   if (M % 128 || N % 128 || K % 4 || ldx % 4 || !aligned8(dy) || !aligned8(y) || !aligned8(x))
     return rl_set_error("rl_linear_bwd: M % 128, N % 128, K % 4 and 8-byte aligned rows required");
-  if (splits <= 0 || M % (splits * kTnStep) != 0)
+  if (splits <= 0 || M % (splits * kTnStep) != 0 || (int64_t)splits * G > 65535)
     return rl_set_error("rl_linear_bwd: M must split into row blocks of multiples of 64");
   // (the bias partials come out of the weight-gradient kernel's pass: bpart alone would be left unwritten)
   if (bpart && !wpart) return rl_set_error("rl_linear_bwd: bias partials (bpart) need the weight partials (wpart)");
+  const int64_t gx = grp ? grp->x_gstride : 0, gw = grp ? grp->w_gstride : 0, gy = grp ? grp->y_gstride : 0,
+                gdx = grp ? grp->dx_gstride : 0, gp = grp ? grp->part_gstride : 0, gbp = grp ? grp->bpart_gstride : 0;
+  if (G > 1 && ((gx | gw | gy | gdx | gp | gbp) % 4 != 0)) return rl_set_error("rl_linear_bwd: group strides must be % 4");
   hipStream_t st = (hipStream_t)stream;
   const auto* DY = static_cast<const _Float16*>(dy);
   const auto* Yv = static_cast<const _Float16*>(y);
@@ -478,21 +526,30 @@ extern "C" int rl_linear_bwd(const void* dy, const void* y, int32_t M, int32_t N
       return rl_set_error("rl_linear_bwd: dX needs W, 8-byte aligned rows and K % 128");
     const auto* Wp = static_cast<const _Float16*>(w);
     auto* DX = static_cast<_Float16*>(dx);
-    if ((M / 128) * (K / 128) >= 256)
-      hipLaunchKernelGGL((k_gemm_nn<128>), dim3(M / 128, K / 128), dim3(kThreads), 0, st, DY, Yv, N, Wp, K, DX);
+    if ((M / 128) * (K / 128) * G >= 256)
+      hipLaunchKernelGGL((k_gemm_nn<128>), dim3(M / 128, K / 128, G), dim3(kThreads), 0, st, DY, Yv, N, ldy, Wp, K, DX,
+                         lddx, gy, gw, gdx);
     else
-      hipLaunchKernelGGL((k_gemm_nn<64>), dim3(M / 64, K / 128), dim3(kThreads), 0, st, DY, Yv, N, Wp, K, DX);
+      hipLaunchKernelGGL((k_gemm_nn<64>), dim3(M / 64, K / 128, G), dim3(kThreads), 0, st, DY, Yv, N, ldy, Wp, K, DX,
+                         lddx, gy, gw, gdx);
     if (int rc = launch_fail("rl_linear_bwd (dX)")) return rc;
   }
   if (wpart) {
     // pstride 0: wpart [splits][N][K], bpart [splits][N]; else both advance pstride floats per block (the merged
-    // layout: each block's bias partials right behind its weight partials, pstride = N*K + N)
+    // layout: each block's bias partials right behind its weight partials, pstride = N*K + N; grouped: the groups'
+    // weight partials then their bias partials within a block, pstride = G (N*K + N))
     const int64_t ws = pstride ? pstride : (int64_t)N * K, bs = pstride ? pstride : (int64_t)N;
     if ((reinterpret_cast<uintptr_t>(wpart) & 15) || ws % 4 || ws < (int64_t)N * K)
       return rl_set_error("rl_linear_bwd: weight partials need 16-byte alignment and a block stride >= N*K, % 4");
-    hipLaunchKernelGGL(k_gemm_tn, dim3(N / kTN, (K + kTN - 1) / kTN, splits), dim3(kThreads), 0, st, DY, Yv, N, X, ldx,
-                       K, M / splits, wpart, bpart, ws, bs);
+    hipLaunchKernelGGL(k_gemm_tn, dim3(N / kTN, (K + kTN - 1) / kTN, splits * G), dim3(kThreads), 0, st, DY, Yv, N,
+                       ldy, X, ldx, K, M / splits, wpart, bpart, ws, bs, splits, gy, gx, gp, gbp);
     return launch_fail("rl_linear_bwd (dW)");
   }
   return 0;
+}
+
+extern "C" int rl_linear_bwd(const void* dy, const void* y, int32_t M, int32_t N, const void* x, int32_t K,
+                             int32_t ldx, const void* w, void* dx, int32_t splits, float* wpart, float* bpart,
+                             int64_t pstride, void* stream) {
+  return rl_linear_bwd_g(dy, y, M, N, x, K, ldx, w, dx, splits, wpart, bpart, pstride, nullptr, stream);
 }

@@ -41,6 +41,7 @@ import isaacgymenv_amd
 
 from . import gae
 from .gae import discount_values
+from . import network as network_mod
 from .network import ActorCriticNetwork, Linear, ModelA2CContinuousLogStd
 
 
@@ -165,22 +166,31 @@ class A2CAgent:
                                  cfg.fixed_sigma, cfg.sigma_init_val)
         self.model = ModelA2CContinuousLogStd(net, self.obs_dim, cfg.normalize_input, cfg.normalize_value)
         self.model.to(self.device)
-        self.params = [p for p in self.model.parameters()]
+        self.params = [p for p in self.model.parameters()]  # (the optimizer's order: model.parameters())
         self.num_params = sum(p.numel() for p in self.params)
+        # the flat layout: model order, except that with separate actor / critic MLPs of equal widths on the fp16
+        # matrix-core update, each hidden layer's two weights and then its two biases come first and adjacent, so
+        # both networks' layer runs as one launch per GEMM (network.GroupedMLPSpec)
+        grouped = (cfg.separate and cfg.mixed_precision and self.device.type == "cuda" and network_mod.USE_MFMA_LAYERS
+                   and self._mlps_groupable(net))
+        self._flat_params = self.params
+        if grouped:
+            head = []
+            for la, lc in zip(*[[m for m in mlp if isinstance(m, Linear)] for mlp in (net.actor_mlp, net.critic_mlp)]):
+                head += [la.weight, lc.weight, la.bias, lc.bias]
+            ids = {id(p) for p in head}
+            self._flat_params = head + [p for p in self.params if id(p) not in ids]
         # one flat parameter buffer (every parameter a view into it) and, for the fp16 update, its fp16
         # shadow: one cast per minibatch refreshes the fp16 weights every Linear layer reads
-        self.flat_param = torch.cat([p.detach().reshape(-1) for p in self.params]).to(self.device)
-        off = 0
-        for p in self.params:
+        self.flat_param = torch.cat([p.detach().reshape(-1) for p in self._flat_params]).to(self.device)
+        offs, off = {}, 0
+        for p in self._flat_params:
             p.data = self.flat_param[off:off + p.numel()].view_as(p)
+            offs[id(p)] = off
             off += p.numel()
         self.flat_param_half = None
         if cfg.mixed_precision and self.device.type == "cuda":
             self.flat_param_half = torch.empty(self.num_params, dtype=torch.float16, device=self.device)
-            offs, off = {}, 0
-            for p in self.params:
-                offs[id(p)] = off
-                off += p.numel()
             for m in self.model.modules():
                 if isinstance(m, Linear):
                     o = offs[id(m.weight)]
@@ -191,9 +201,11 @@ class A2CAgent:
         # one flat gradient buffer; .grad of every parameter is a view into it
         self.flat_grad = torch.zeros(self.num_params, dtype=torch.float32, device=self.device)
         off = 0
-        for p in self.params:
+        for p in self._flat_params:
             p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
             off += p.numel()
+        net.grouped = (network_mod.GroupedMLPSpec([net.actor_mlp, net.critic_mlp], self.flat_param_half, self.flat_grad,
+                                                  lambda p: offs[id(p)]) if grouped else None)
         # the learner's .backward() lets the split-K Linear layers accumulate straight into these views
         for m in self.model.modules():
             if isinstance(m, Linear):
@@ -278,13 +290,32 @@ class A2CAgent:
         net = self.model.a2c_network
         self._fused_loss = on_gpu and net.fixed_sigma and self.actions_num <= 32
 
+    @staticmethod
+    def _mlps_groupable(net) -> bool:
+        """Actor and critic MLPs of Linear + ELU layers with equal shapes, widths the MFMA kernels tile."""
+        if net.critic_mlp is None:
+            return False
+        mods = [list(net.actor_mlp), list(net.critic_mlp)]
+        if len(mods[0]) != len(mods[1]) or not mods[0] or len(mods[0]) % 2:
+            return False
+        for a, c in zip(*mods):
+            if type(a) is not type(c):
+                return False
+            if isinstance(a, Linear):
+                if (a.in_features, a.out_features) != (c.in_features, c.out_features) or a.out_features % 128 \
+                        or a.bias is None or c.bias is None:
+                    return False
+            elif not (type(a) is nn.ELU and a.alpha == 1.0 and c.alpha == 1.0):
+                return False
+        return True
+
     # ------------------------------------------------------------------ multi-GPU
     def _broadcast_params(self):
-        flat = torch.cat([p.detach().reshape(-1) for p in self.params])
+        flat = torch.cat([p.detach().reshape(-1) for p in self._flat_params])
         dist.broadcast(flat, 0)
         off = 0
         with torch.no_grad():
-            for p in self.params:
+            for p in self._flat_params:
                 p.copy_(flat[off:off + p.numel()].view_as(p))
                 off += p.numel()
 
@@ -450,8 +481,7 @@ class A2CAgent:
         net = self.model.a2c_network
         obs = self.model.norm_obs(mb["obs"])
         with torch.autocast("cuda", dtype=torch.float16, enabled=self.mixed_precision, cache_enabled=False):
-            a_out = net.actor_mlp(obs)
-            c_out = net.critic_mlp(obs) if net.separate else a_out
+            a_out, c_out = net.hidden(obs)
             values = net.value(c_out)
             mu = net.mu(a_out)
         loss, stats = gae.PpoLossFn.apply(mu, values, net.sigma, mb["actions"], mb["old_logp_actions"],
@@ -466,7 +496,7 @@ class A2CAgent:
         """Adam state of every parameter as views into the flat moment buffers (after a checkpoint load
         the loaded tensors are copied in first)."""
         off = 0
-        for p in self.params:
+        for p in self._flat_params:
             n = p.numel()
             st = self.optimizer.state.get(p)
             m, v = self.flat_m[off:off + n].view_as(p), self.flat_v[off:off + n].view_as(p)

@@ -16,11 +16,19 @@ import torch
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libgymrl.so")
 EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accum", "rl_colsum_accum", "rl_rollout_post",
                     "rl_ppo_loss", "rl_ppo_loss_backward", "rl_rms_normalize", "rl_opt_step", "rl_opt_partials_size",
-                    "rl_linear_fwd", "rl_linear_transpose", "rl_linear_bwd", "rl_policy_head"]
+                    "rl_linear_fwd", "rl_linear_transpose", "rl_linear_bwd", "rl_policy_head", "rl_linear_fwd_g",
+                    "rl_linear_bwd_g"]
 _lib = None
 
 
-RL_ABI_VERSION = 5  # include/gymrl.h
+RL_ABI_VERSION = 6  # include/gymrl.h
+
+
+class LinearGroups(C.Structure):
+    """include/gymrl.h rl_linear_groups"""
+    _fields_ = [("groups", C.c_int32), ("ldy", C.c_int32), ("lddx", C.c_int32), ("reserved", C.c_int32),
+                ("x_gstride", C.c_int64), ("w_gstride", C.c_int64), ("b_gstride", C.c_int64), ("y_gstride", C.c_int64),
+                ("dx_gstride", C.c_int64), ("part_gstride", C.c_int64), ("bpart_gstride", C.c_int64)]
 
 
 class OptHyper(C.Structure):
@@ -62,6 +70,12 @@ def lib():
         L.rl_linear_transpose.argtypes = [vp, C.c_int32, C.c_int32, vp, vp]
         L.rl_linear_bwd.argtypes = [vp, vp, C.c_int32, C.c_int32, vp, C.c_int32, C.c_int32, vp, vp, C.c_int32, vp, vp,
                                     C.c_int64, vp]
+        for f in ("rl_linear_fwd_g", "rl_linear_bwd_g"):
+            getattr(L, f).restype = C.c_int
+        L.rl_linear_fwd_g.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int32, vp, C.c_int32, vp,
+                                      C.POINTER(LinearGroups), vp]
+        L.rl_linear_bwd_g.argtypes = [vp, vp, C.c_int32, C.c_int32, vp, C.c_int32, C.c_int32, vp, vp, C.c_int32, vp,
+                                      vp, C.c_int64, C.POINTER(LinearGroups), vp]
         L.rl_opt_step.restype = C.c_int
         L.rl_opt_step.argtypes = [vp, vp, vp, vp, C.c_int64, vp, vp, vp, vp, C.POINTER(OptHyper), vp, vp]
         L.rl_opt_partials_size.restype = C.c_int
@@ -343,3 +357,25 @@ def linear_bwd(dy, y, x, w, dx, splits: int, wpart, bpart, pstride: int = 0):
                                splits, wpart.data_ptr() if wpart is not None else None,
                                bpart.data_ptr() if bpart is not None else None, int(pstride),
                                torch.cuda.current_stream().cuda_stream), "rl_linear_bwd")
+
+
+def linear_fwd_grouped(x, ldx: int, K: int, w_half, N: int, b_half, act: bool, y, ldy: int, groups: int, x_gstride: int,
+                       w_gstride: int, b_gstride: int, y_gstride: int, M: int):
+    """rl_linear_fwd_g: `groups` equal-shaped layers in one launch.  Tensors are base pointers (group 0); group g's
+    operands lie the given element strides further (include/gymrl.h rl_linear_groups)."""
+    g = LinearGroups(groups, ldy, 0, 0, x_gstride, w_gstride, b_gstride, y_gstride, 0, 0, 0)
+    _check(lib().rl_linear_fwd_g(x.data_ptr(), M, K, ldx, w_half.data_ptr(), N,
+                                 b_half.data_ptr() if b_half is not None else None, int(act), y.data_ptr(), C.byref(g),
+                                 torch.cuda.current_stream().cuda_stream), "rl_linear_fwd_g")
+
+
+def linear_bwd_grouped(dy, y, ldy: int, y_gstride: int, M: int, N: int, x, ldx: int, x_gstride: int, K: int, w,
+                       w_gstride: int, dx, lddx: int, dx_gstride: int, splits: int, wpart, bpart, pstride: int,
+                       part_gstride: int, bpart_gstride: int, groups: int):
+    """rl_linear_bwd_g: the backward of `groups` equal-shaped layers in one launch per GEMM (dX, dW + db)."""
+    g = LinearGroups(groups, ldy, lddx, 0, x_gstride, w_gstride, 0, y_gstride, dx_gstride, part_gstride, bpart_gstride)
+    _check(lib().rl_linear_bwd_g(dy.data_ptr(), y.data_ptr(), M, N, x.data_ptr(), K, ldx,
+                                 w.data_ptr() if w is not None else None, dx.data_ptr() if dx is not None else None,
+                                 splits, wpart.data_ptr() if wpart is not None else None,
+                                 bpart.data_ptr() if bpart is not None else None, int(pstride), C.byref(g),
+                                 torch.cuda.current_stream().cuda_stream), "rl_linear_bwd_g")

@@ -196,6 +196,93 @@ class _LinearELUFn(torch.autograd.Function):
         return dx, gw, gb, None, None, None
 
 
+class GroupedMLPSpec:
+    """G equal-shaped Linear + ELU MLPs on one input -- rl_games' separate actor and critic (AnymalTerrainPPO.yaml
+    `separate: True`, mlp 512-256-128 elu) -- laid out by the learner (A2CAgent) so that layer l's G weights
+    [G][N][K] and then its G biases [G][N] are contiguous in the flat parameter buffer, its fp16 shadow and the flat
+    gradient buffer.  _GroupedMLPFn then runs each layer of all G networks as ONE launch per GEMM: layer 0 (one
+    shared input) as a single GEMM over the stacked [G*N][K] weight, the later layers as grouped launches
+    (include/gymrl.h rl_linear_*_g, ABI 6), and one rl_splitk_accum finishes a layer's G weight and bias gradients."""
+
+    def __init__(self, mlps, flat_half, flat_grad, offset_of):
+        self.G = len(mlps)
+        lins = [[m for m in mlp if isinstance(m, Linear)] for mlp in mlps]
+        self.params = [p for ls in lins for lin in ls for p in (lin.weight, lin.bias)]
+        self.layers = []
+        for l, lin0 in enumerate(lins[0]):
+            N, K = lin0.out_features, lin0.in_features
+            o = offset_of(lin0.weight)
+            for g in range(self.G):
+                lin = lins[g][l]
+                assert (lin.out_features, lin.in_features) == (N, K), "grouped MLPs must have equal shapes"
+                assert offset_of(lin.weight) == o + g * N * K and offset_of(lin.bias) == o + self.G * N * K + g * N, \
+                    "grouped layout: a layer's G weights, then its G biases"
+            G = self.G
+            self.layers.append((N, K, flat_half[o:o + G * N * K].view(G * N, K),
+                                flat_half[o + G * N * K:o + G * (N * K + N)], flat_grad[o:o + G * (N * K + N)]))
+
+    def applies(self, x) -> bool:
+        if not (USE_MFMA_LAYERS and x.is_cuda and x.dim() == 2 and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.float16 and x.shape[0] % 128 == 0 and x.shape[0] > 0):
+            return False
+        return all(N % 128 == 0 and K % 4 == 0 and (l == 0 or K % 128 == 0) for l, (N, K, *_) in enumerate(self.layers))
+
+
+class _GroupedMLPFn(torch.autograd.Function):
+    """G equal-shaped MLPs (GroupedMLPSpec) forward / backward, one launch per GEMM for all G.  Each group computes
+    exactly what _LinearELUFn computes for its network alone (same tiles, same reduction order, same split row
+    blocks), so the outputs and gradients are bit-identical to the per-network path
+    (tests/test_ppo_gpu.py test_grouped_mlp_matches_separate_networks_bit_for_bit).  The learner's direct
+    gradients: the weight and bias gradients go straight into the flat gradient buffer, none is returned."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda")
+    def forward(ctx, x, spec, *params):
+        h = torch.float16
+        xc = x.to(h)
+        if xc.stride(1) != 1 or xc.stride(0) % 4 or xc.data_ptr() % 8:
+            xc = xc.contiguous()
+        G, M = spec.G, xc.shape[0]
+        ys = []
+        inp = xc
+        for l, (N, K, wh, bh, _) in enumerate(spec.layers):
+            y = torch.empty(M, G * N, dtype=h, device=x.device)
+            if l == 0:  # one shared input: the stacked [G*N][K] weight is one GEMM
+                gae.linear_fwd(xc, wh, bh, True, y)
+            else:
+                gae.linear_fwd_grouped(inp, G * K, K, wh, N, bh, True, y, G * N, G, K, N * K, N, N, M)
+            ys.append(y)
+            inp = y
+        ctx.save_for_backward(xc, *ys)
+        ctx.spec = spec
+        n_last = spec.layers[-1][0]
+        return tuple(ys[-1][:, g * n_last:(g + 1) * n_last] for g in range(G))
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, *gouts):
+        xc, *ys = ctx.saved_tensors
+        spec = ctx.spec
+        G, M = spec.G, xc.shape[0]
+        n_last = spec.layers[-1][0]
+        dy = torch.cat([(g if g is not None else torch.zeros(M, n_last, device=xc.device)).to(torch.float16)
+                        for g in gouts], dim=1)
+        for l in reversed(range(len(spec.layers))):
+            N, K, wh, _, span = spec.layers[l]
+            # the per-network path's row blocks (network._LinearELUFn): the same fixed-order partial sums
+            splits = _splits(M, (N // 128) * ((K + 127) // 128))
+            part = torch.empty(splits, G * (N * K + N), dtype=torch.float32, device=xc.device)
+            if l == 0:
+                gae.linear_bwd(dy, ys[0], xc, None, None, splits, part, part[:, G * N * K:], pstride=G * (N * K + N))
+            else:
+                dx = torch.empty(M, G * K, dtype=torch.float16, device=xc.device)
+                gae.linear_bwd_grouped(dy, ys[l], G * N, N, M, N, ys[l - 1], G * K, K, K, wh, N * K, dx, G * K, K,
+                                       splits, part, part[:, G * N * K:], G * (N * K + N), N * K, N, G)
+                dy = dx
+            gae.splitk_accum(part, span)
+        return (None, None) + (None,) * len(spec.params)
+
+
 class _MLP(nn.Sequential):
     """rl_games' mlp (Linear, activation per hidden layer; same modules and state_dict as nn.Sequential).  Under
     fp16 autocast on the GPU, with ELU layers whose widths the kernels tile (multiples of 128) and a row count in
@@ -261,9 +348,17 @@ class ActorCriticNetwork(nn.Module):
             else:
                 self.sigma.weight.fill_(sigma_init_val)
 
-    def forward(self, obs):
+    grouped = None  # GroupedMLPSpec, set by the learner when its flat layout groups the actor and critic layers
+
+    def hidden(self, obs):
+        """(actor MLP output, critic MLP output): under the learner's grouped layout one launch per GEMM for both."""
+        if self.separate and self.grouped is not None and self.grouped.applies(obs):
+            return _GroupedMLPFn.apply(obs, self.grouped, *self.grouped.params)
         a_out = self.actor_mlp(obs)
-        c_out = self.critic_mlp(obs) if self.separate else a_out
+        return a_out, (self.critic_mlp(obs) if self.separate else a_out)
+
+    def forward(self, obs):
+        a_out, c_out = self.hidden(obs)
         value = self.value(c_out)
         mu = self.mu(a_out)
         logstd = mu * 0.0 + self.sigma if self.fixed_sigma else self.sigma(a_out)

@@ -41,7 +41,7 @@ def test_python_bindings_cover_the_abi():
     assert sorted(gymtask.EXPORTED_SYMBOLS) == _declared("gymtask.h")
     from isaacgymenv_amd.rl import gae
     assert sorted(gae.EXPORTED_SYMBOLS) == _declared("gymrl.h")
-    assert gae.lib().rl_abi_version() == 5
+    assert gae.lib().rl_abi_version() == 6
 
 
 def test_abi_version_and_topology_query():
@@ -79,13 +79,15 @@ def test_ctypes_struct_layouts_match_the_headers(tmp_path):
         pytest.skip("no gcc")
     from isaacgymenv_amd.isaacgym import _lib
     from isaacgymenv_amd import gymtask
+    from isaacgymenv_amd.rl import gae
     mirrors = {"gs_model_desc": _lib.GsModelDesc, "gs_sim_params": _lib.GsSimParams, "gs_pd_args": _lib.GsPdArgs,
                "gt_torch_rand_plan": gymtask.GtTorchRandPlan, "gt_anymal_params": gymtask.GtAnymalParams,
                "gt_anymal_buffers": gymtask.GtAnymalBuffers, "gt_anymal_reset_draws": gymtask.GtAnymalResetDraws,
                "gt_hound_control_params": gymtask.GtHoundControlParams, "gt_ant_params": gymtask.GtAntParams,
                "gt_ant_buffers": gymtask.GtAntBuffers, "gt_anymal_terrain_reset": gymtask.GtAnymalTerrainReset,
-               "gt_anymal_hound": gymtask.GtAnymalHound}
-    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gymsim.h"', '#include "gymtask.h"',
+               "gt_anymal_hound": gymtask.GtAnymalHound, "rl_linear_groups": gae.LinearGroups,
+               "rl_opt_hyper": gae.OptHyper}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gymsim.h"', '#include "gymtask.h"', '#include "gymrl.h"',
              "int main(void) {"]
     expect = []
     for cname, py in mirrors.items():

@@ -633,3 +633,75 @@ def test_mfma_mlp_merged_weight_bias_gradient_path(monkeypatch):
     assert pstrides_s and all(s == 0 for s in pstrides_s), pstrides_s
     for a, b in zip(merged, separate):
         assert torch.equal(a, b)
+
+
+def _flat_net(net, order, grouped):
+    """The learner's flat buffers over `order` (A2CAgent): parameters, their fp16 shadow and the gradients as views
+    of three flat tensors, direct gradients; grouped: the actor / critic layer spec (network.GroupedMLPSpec)."""
+    from isaacgymenv_amd.rl import network
+    offs, off = {}, 0
+    flat = torch.cat([p.detach().reshape(-1) for p in order])
+    for p in order:
+        p.data = flat[off:off + p.numel()].view_as(p)
+        offs[id(p)] = off
+        off += p.numel()
+    half = torch.empty(off, dtype=torch.float16, device="cuda")
+    grad = torch.zeros(off, device="cuda")
+    for p in order:
+        p.grad = grad[offs[id(p)]:offs[id(p)] + p.numel()].view_as(p)
+    for m in net.modules():
+        if isinstance(m, network.Linear):
+            m.half_weight = half[offs[id(m.weight)]:offs[id(m.weight)] + m.weight.numel()].view_as(m.weight)
+            m.half_bias = half[offs[id(m.bias)]:offs[id(m.bias)] + m.bias.numel()].view_as(m.bias)
+            m.direct_grad = True
+    net.grouped = (network.GroupedMLPSpec([net.actor_mlp, net.critic_mlp], half, grad, lambda p: offs[id(p)])
+                   if grouped else None)
+    half.copy_(flat)
+    return grad
+
+
+def test_grouped_mlp_matches_separate_networks_bit_for_bit(monkeypatch):
+    """ABI 6: the actor and critic MLPs of AnymalTerrainPPO (188 -> 512 -> 256 -> 128 ELU, separate) as one launch per
+    GEMM (network._GroupedMLPFn: layer 0 one GEMM over the stacked weights, layers 1-2 grouped launches, one gradient
+    finish per layer) against each network on its own (_LinearELUFn): hidden outputs and every weight / bias gradient
+    bit-identical (same tiles, same reduction order, same split row blocks)."""
+    import copy
+    from isaacgymenv_amd.rl import network
+    monkeypatch.setattr(network, "USE_MFMA_LAYERS", True)
+    torch.manual_seed(7)
+    base = network.ActorCriticNetwork(188, 12, [512, 256, 128], "elu", separate=True).cuda()
+    with torch.no_grad():
+        for p_ in base.parameters():
+            p_.normal_(0.0, 0.08)
+    nets = {}
+    for grouped in (True, False):
+        net = copy.deepcopy(base)
+        order = list(net.parameters())
+        if grouped:
+            head = []
+            lins = [[m for m in mlp if isinstance(m, network.Linear)] for mlp in (net.actor_mlp, net.critic_mlp)]
+            for la, lc in zip(*lins):
+                head += [la.weight, lc.weight, la.bias, lc.bias]
+            ids = {id(p_) for p_ in head}
+            order = head + [p_ for p_ in order if id(p_) not in ids]
+        _flat_net(net, order, grouped)
+        nets[grouped] = net
+    x = torch.randn(16384, 188, device="cuda")
+    ga, gc = torch.randn(16384, 128, device="cuda"), torch.randn(16384, 128, device="cuda")
+    outs = {}
+    for grouped, net in nets.items():
+        launches = []
+        if grouped:
+            orig = network._GroupedMLPFn.apply
+            monkeypatch.setattr(network._GroupedMLPFn, "apply", lambda *a: (launches.append(1), orig(*a))[1])
+        with torch.autocast("cuda", dtype=torch.float16):
+            assert net.grouped is None or net.grouped.applies(x)
+            a_out, c_out = net.hidden(x)
+        ((a_out.float() * ga).sum() + (c_out.float() * gc).sum()).backward()
+        assert bool(launches) == grouped
+        outs[grouped] = (a_out.detach().clone(), c_out.detach().clone(),
+                         {n: p_.grad.clone() for n, p_ in net.named_parameters() if "mlp" in n})
+    for a, b in zip(outs[True][:2], outs[False][:2]):
+        assert torch.equal(a, b)
+    for n, g in outs[False][2].items():
+        assert torch.equal(outs[True][2][n], g), n
