@@ -204,6 +204,23 @@ int rl_linear_bwd_g(const void *dy, const void *y, int32_t M, int32_t N, const v
                     const void *w, void *dx, int32_t splits, float *wpart, float *bpart, int64_t pstride,
                     const rl_linear_groups *groups, void *stream);
 
+/*
+ * ABI 6 -- the minibatch's policy bookkeeping (rl_policy.hip; rl_games a2c_common.py after the optimizer step:
+ * torch_ext.policy_kl, dataset.update_mu_sigma, schedulers.AdaptiveScheduler, the loss / kl meters).
+ * rl_policy_kl: kl (f32 scalar) = mean over M rows of the sum over A of log(s1/s0 + 1e-5) + (s0^2 + (m1 - m0)^2) /
+ *   (2 (s1^2 + 1e-5)) - 0.5 with m0 = mu_new [M][A] (mu_half: fp16, else f32), s0 = sigma_new (row r at
+ *   r * sigma_row_stride: 0 = one [A] row for all), m1 / s1 = mu_old / sigma_old [M][A] f32; write_back: mu_old /
+ *   sigma_old receive the new values (update_mu_sigma).  Fixed-order sums; partials >= rl_kl_partials_size() f32.
+ * rl_adaptive_lr: kl = kl * inv_world (the rank average after a summing all-reduce); adaptive: lr (f64) /= 1.5 if kl >
+ *   2 kl_threshold (>= 1e-6), *= 1.5 if kl < kl_threshold / 2 (<= 1e-2), opt_lr (f32, nullable) = lr; stats (nullable):
+ *   stats[0..3] += a_loss, c_loss, kl, entropy.  One thread, no host synchronisation.
+ */
+int rl_kl_partials_size(void);
+int rl_policy_kl(const void *mu_new, int32_t mu_half, const float *sigma_new, int64_t sigma_row_stride, float *mu_old,
+                 float *sigma_old, int32_t M, int32_t A, int32_t write_back, float *kl, float *partials, void *stream);
+int rl_adaptive_lr(float *kl, float inv_world, int32_t adaptive, double kl_threshold, double *lr, float *opt_lr,
+                   float *stats, const float *a_loss, const float *c_loss, const float *entropy, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -142,7 +142,10 @@ typedef struct gs_pd_args {
     int32_t decimation;
     int32_t extra_simulates;
     float *torques_out;          /* [N][nd]  last applied torque */
-    float *dof_state_out;        /* [N*nd][2] or NULL            */
+    float *dof_state_out;        /* [N*nd][2] in/out, required: the first PD torque reads q, qd
+                                    from it (the task's refreshed dof_pos / dof_vel views,
+                                    anymal_terrain.py:444-445), it receives the state after
+                                    the decimation loop */
     float *root_state_out;       /* [N][13]   or NULL            */
     float *contact_out;          /* [N*nb][3] or NULL            */
     float *actions_copy_out;     /* [N][nd] or NULL: receives `actions` (the task's

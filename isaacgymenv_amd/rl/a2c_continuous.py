@@ -205,7 +205,7 @@ class A2CAgent:
             p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
             off += p.numel()
         net.grouped = (network_mod.GroupedMLPSpec([net.actor_mlp, net.critic_mlp], self.flat_param_half, self.flat_grad,
-                                                  lambda p: offs[id(p)]) if grouped else None)
+                                                  lambda p: offs[id(p)], self.flat_param) if grouped else None)
         # the learner's .backward() lets the split-K Linear layers accumulate straight into these views
         for m in self.model.modules():
             if isinstance(m, Linear):
@@ -289,6 +289,11 @@ class A2CAgent:
         # config); a learned-sigma head keeps the torch statement of the loss
         net = self.model.a2c_network
         self._fused_loss = on_gpu and net.fixed_sigma and self.actions_num <= 32
+        # KL of the minibatch, dataset.update_mu_sigma, adaptive LR and the meters as three HIP launches
+        # (gae.policy_kl / gae.adaptive_lr, rl_policy.hip) instead of ~14 torch ones
+        self._fused_kl = self._fused_loss and self._opt_lr is not None
+        if self._fused_kl:
+            self._kl_part = torch.zeros(gae.lib().rl_kl_partials_size(), dtype=torch.float32, device=dev)
 
     @staticmethod
     def _mlps_groupable(net) -> bool:
@@ -523,11 +528,20 @@ class A2CAgent:
             self.scaler.update()
         mb = self._minibatch(i)
         with torch.no_grad():
+            if self._fused_kl:  # KL + update_mu_sigma: the dataset rows take the new values in the same pass
+                kl = torch.empty((), dtype=torch.float32, device=self.device)
+                gae.policy_kl(out[4], out[5][0] if out[5].stride(0) == 0 else out[5], mb["mu"], mb["sigma"], kl,
+                              self._kl_part, write_back=True)
+                return kl
             return self._policy_kl(out[4], out[5], mb["mu"], mb["sigma"])
 
     def _mb_finish(self, i, out, kl):
         """Phase 3 (after the KL all-reduce, which sums): dataset.update_mu_sigma, adaptive LR,
         diagnostics."""
+        if self._fused_kl:
+            gae.adaptive_lr(kl, 1.0 / self.world_size if self.multi_gpu else 1.0, self.cfg.lr_schedule == "adaptive",
+                            self.cfg.kl_threshold, self.lr, self._opt_lr, self._stats_acc, out[0], out[1], out[2])
+            return
         s = slice(i * self.cfg.minibatch_size, (i + 1) * self.cfg.minibatch_size)
         with torch.no_grad():
             self.dataset["mu"][s] = out[4]

@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accum", "rl_colsum_accum", "rl_rollout_post",
                     "rl_ppo_loss", "rl_ppo_loss_backward", "rl_rms_normalize", "rl_opt_step", "rl_opt_partials_size",
                     "rl_linear_fwd", "rl_linear_transpose", "rl_linear_bwd", "rl_policy_head", "rl_linear_fwd_g",
-                    "rl_linear_bwd_g"]
+                    "rl_linear_bwd_g", "rl_kl_partials_size", "rl_policy_kl", "rl_adaptive_lr"]
 _lib = None
 
 
@@ -76,6 +76,11 @@ def lib():
                                       C.POINTER(LinearGroups), vp]
         L.rl_linear_bwd_g.argtypes = [vp, vp, C.c_int32, C.c_int32, vp, C.c_int32, C.c_int32, vp, vp, C.c_int32, vp,
                                       vp, C.c_int64, C.POINTER(LinearGroups), vp]
+        L.rl_kl_partials_size.restype = C.c_int
+        L.rl_policy_kl.restype = C.c_int
+        L.rl_policy_kl.argtypes = [vp, C.c_int32, vp, C.c_int64, vp, vp, C.c_int32, C.c_int32, C.c_int32, vp, vp, vp]
+        L.rl_adaptive_lr.restype = C.c_int
+        L.rl_adaptive_lr.argtypes = [vp, C.c_float, C.c_int32, C.c_double, vp, vp, vp, vp, vp, vp, vp]
         L.rl_opt_step.restype = C.c_int
         L.rl_opt_step.argtypes = [vp, vp, vp, vp, C.c_int64, vp, vp, vp, vp, C.POINTER(OptHyper), vp, vp]
         L.rl_opt_partials_size.restype = C.c_int
@@ -379,3 +384,26 @@ def linear_bwd_grouped(dy, y, ldy: int, y_gstride: int, M: int, N: int, x, ldx: 
                                  splits, wpart.data_ptr() if wpart is not None else None,
                                  bpart.data_ptr() if bpart is not None else None, int(pstride), C.byref(g),
                                  torch.cuda.current_stream().cuda_stream), "rl_linear_bwd_g")
+
+
+def policy_kl(mu_new, sigma_row, mu_old, sigma_old, kl_out, partials, write_back: bool = True) -> None:
+    """rl_policy_kl: kl_out (f32 0-d) = policy_kl(mu_new, sigma, mu_old, sigma_old) (rl_games torch_ext.policy_kl),
+    sigma_new one [A] row for all rows (fixed sigma) or [M, A]; write_back: mu_old / sigma_old (the dataset's
+    rows) receive the new values (dataset.update_mu_sigma)."""
+    M, A = mu_new.shape
+    assert mu_new.is_contiguous() and mu_old.is_contiguous() and sigma_old.is_contiguous()
+    assert mu_old.dtype == torch.float32 and sigma_old.dtype == torch.float32 and sigma_row.dtype == torch.float32
+    stride = 0 if sigma_row.dim() == 1 else sigma_row.stride(0)
+    _check(lib().rl_policy_kl(mu_new.data_ptr(), int(mu_new.dtype == torch.float16), sigma_row.data_ptr(), stride,
+                              mu_old.data_ptr(), sigma_old.data_ptr(), M, A, int(write_back), kl_out.data_ptr(),
+                              partials.data_ptr(), torch.cuda.current_stream().cuda_stream), "rl_policy_kl")
+
+
+def adaptive_lr(kl, inv_world: float, adaptive: bool, kl_threshold: float, lr, opt_lr, stats, a_loss, c_loss,
+                entropy) -> None:
+    """rl_adaptive_lr: the rank-averaged kl, AdaptiveScheduler on the f64 lr (and its f32 optimizer copy), the
+    epoch meters stats[0..3] += a_loss, c_loss, kl, entropy."""
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    _check(lib().rl_adaptive_lr(kl.data_ptr(), float(inv_world), int(adaptive), float(kl_threshold), ptr(lr),
+                                ptr(opt_lr), ptr(stats), ptr(a_loss), ptr(c_loss), ptr(entropy),
+                                torch.cuda.current_stream().cuda_stream), "rl_adaptive_lr")

@@ -204,11 +204,11 @@ class GroupedMLPSpec:
     shared input) as a single GEMM over the stacked [G*N][K] weight, the later layers as grouped launches
     (include/gymrl.h rl_linear_*_g, ABI 6), and one rl_splitk_accum finishes a layer's G weight and bias gradients."""
 
-    def __init__(self, mlps, flat_half, flat_grad, offset_of):
+    def __init__(self, mlps, flat_half, flat_grad, offset_of, flat_param=None):
         self.G = len(mlps)
         lins = [[m for m in mlp if isinstance(m, Linear)] for mlp in mlps]
         self.params = [p for ls in lins for lin in ls for p in (lin.weight, lin.bias)]
-        self.layers = []
+        self.layers, self.layers32 = [], []
         for l, lin0 in enumerate(lins[0]):
             N, K = lin0.out_features, lin0.in_features
             o = offset_of(lin0.weight)
@@ -220,6 +220,28 @@ class GroupedMLPSpec:
             G = self.G
             self.layers.append((N, K, flat_half[o:o + G * N * K].view(G * N, K),
                                 flat_half[o + G * N * K:o + G * (N * K + N)], flat_grad[o:o + G * (N * K + N)]))
+            if flat_param is not None:  # the f32 weights and biases of the layer, [G][N][K] and [G][N]
+                self.layers32.append((flat_param[o:o + G * N * K].view(G, N, K),
+                                      flat_param[o + G * N * K:o + G * (N * K + N)].view(G, N)))
+
+    def act_forward(self, x):
+        """The G MLPs in f32 without autograd (the rollout's act forward, rl_games play_steps: no autocast): layer 0
+        one library GEMM over the stacked weights, the later layers one batched GEMM, one ELU per layer for all G
+        networks.  Returns the G hidden outputs."""
+        import torch.nn.functional as F
+        G, M = self.G, x.shape[0]
+        w0, b0 = self.layers32[0]
+        y = torch.addmm(b0.reshape(-1), x, w0.reshape(-1, w0.shape[2]).t())
+        F.elu(y, inplace=True)
+        y = y.view(M, G, -1).transpose(0, 1)
+        for w, b in self.layers32[1:]:
+            y = torch.baddbmm(b.unsqueeze(1), y, w.transpose(1, 2))
+            F.elu(y, inplace=True)
+        return tuple(y[g] for g in range(G))
+
+    def act_applies(self, x) -> bool:
+        return (bool(self.layers32) and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2
+                and not torch.is_grad_enabled() and not torch.is_autocast_enabled("cuda"))
 
     def applies(self, x) -> bool:
         if not (USE_MFMA_LAYERS and x.is_cuda and x.dim() == 2 and torch.is_autocast_enabled("cuda")
@@ -352,8 +374,11 @@ class ActorCriticNetwork(nn.Module):
 
     def hidden(self, obs):
         """(actor MLP output, critic MLP output): under the learner's grouped layout one launch per GEMM for both."""
-        if self.separate and self.grouped is not None and self.grouped.applies(obs):
-            return _GroupedMLPFn.apply(obs, self.grouped, *self.grouped.params)
+        if self.separate and self.grouped is not None:
+            if self.grouped.applies(obs):
+                return _GroupedMLPFn.apply(obs, self.grouped, *self.grouped.params)
+            if self.grouped.act_applies(obs):
+                return self.grouped.act_forward(obs)
         a_out = self.actor_mlp(obs)
         return a_out, (self.critic_mlp(obs) if self.separate else a_out)
 
@@ -401,8 +426,7 @@ class ModelA2CContinuousLogStd(nn.Module):
                 and (not self.normalize_value or self.value_mean_std.running_mean.numel() == 1)):
             # act forward on the device: the network, torch's normal_ draws, then one kernel for the head
             obs = self.norm_obs(raw)
-            a_out = net.actor_mlp(obs)
-            c_out = net.critic_mlp(obs) if net.separate else a_out
+            a_out, c_out = net.hidden(obs)
             value = net.value(c_out).contiguous()
             mu = net.mu(a_out).contiguous()
             noise = torch.empty_like(mu).normal_(0.0, 1.0)

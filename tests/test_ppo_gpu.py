@@ -654,7 +654,7 @@ def _flat_net(net, order, grouped):
             m.half_weight = half[offs[id(m.weight)]:offs[id(m.weight)] + m.weight.numel()].view_as(m.weight)
             m.half_bias = half[offs[id(m.bias)]:offs[id(m.bias)] + m.bias.numel()].view_as(m.bias)
             m.direct_grad = True
-    net.grouped = (network.GroupedMLPSpec([net.actor_mlp, net.critic_mlp], half, grad, lambda p: offs[id(p)])
+    net.grouped = (network.GroupedMLPSpec([net.actor_mlp, net.critic_mlp], half, grad, lambda p: offs[id(p)], flat)
                    if grouped else None)
     half.copy_(flat)
     return grad
@@ -705,3 +705,91 @@ def test_grouped_mlp_matches_separate_networks_bit_for_bit(monkeypatch):
         assert torch.equal(a, b)
     for n, g in outs[False][2].items():
         assert torch.equal(outs[True][2][n], g), n
+
+
+def test_grouped_act_forward_matches_separate_networks():
+    """The rollout's act forward (f32, no autograd, no autocast) under the grouped layout: layer 0 one addmm over the
+    stacked actor / critic weights, later layers one baddbmm (GroupedMLPSpec.act_forward) against each torch MLP on
+    its own; same f32 GEMMs in a different grouping, so within f32 rounding (1e-5)."""
+    import copy
+    from isaacgymenv_amd.rl import network
+    torch.manual_seed(11)
+    base = network.ActorCriticNetwork(188, 12, [512, 256, 128], "elu", separate=True).cuda()
+    net = copy.deepcopy(base)
+    head = []
+    lins = [[m for m in mlp if isinstance(m, network.Linear)] for mlp in (net.actor_mlp, net.critic_mlp)]
+    for la, lc in zip(*lins):
+        head += [la.weight, lc.weight, la.bias, lc.bias]
+    ids = {id(p_) for p_ in head}
+    _flat_net(net, head + [p_ for p_ in net.parameters() if id(p_) not in ids], True)
+    x = torch.randn(4096, 188, device="cuda")
+    with torch.no_grad():
+        assert net.grouped.act_applies(x)
+        a_g, c_g = net.hidden(x)
+        a_r, c_r = base.actor_mlp(x), base.critic_mlp(x)
+        mu_g, logstd_g, v_g = net(x)
+        mu_r, logstd_r, v_r = base(x)
+    torch.testing.assert_close(a_g, a_r, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(c_g, c_r, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(mu_g, mu_r, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(v_g, v_r, rtol=1e-5, atol=1e-5)
+    assert torch.equal(logstd_g, logstd_r)
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+        assert not net.grouped.act_applies(x)  # the train forward keeps the fp16 MFMA path
+
+
+@pytest.mark.parametrize("half,M,A", [(True, 16384, 12), (False, 16384, 12), (True, 1000, 8), (False, 3, 1)])
+def test_policy_kl_kernel_matches_torch_policy_kl(half, M, A):
+    """rl_policy_kl against the torch statement (A2CAgent._policy_kl, rl_games torch_ext.policy_kl) on the same
+    tensors: kl within f32 summation-order error; write_back leaves the dataset rows equal to the new mu / sigma
+    (dataset.update_mu_sigma)."""
+    from isaacgymenv_amd.rl import gae
+    from isaacgymenv_amd.rl.a2c_continuous import A2CAgent
+    g = torch.Generator(device="cuda").manual_seed(M + A)
+    mu_new = torch.randn(M, A, device="cuda", generator=g).to(torch.float16 if half else torch.float32)
+    sig_row = torch.exp(0.3 * torch.randn(A, device="cuda", generator=g))
+    mu_old = mu_new.float() + 0.05 * torch.randn(M, A, device="cuda", generator=g)
+    sg_old = sig_row.expand(M, -1) * torch.exp(0.02 * torch.randn(M, A, device="cuda", generator=g))
+    want = A2CAgent._policy_kl(mu_new, sig_row.expand(M, -1), mu_old, sg_old)
+    part = torch.zeros(gae.lib().rl_kl_partials_size(), device="cuda")
+    for write_back in (False, True):
+        kl = torch.empty((), device="cuda")
+        mo, so = mu_old.clone(), sg_old.clone()
+        gae.policy_kl(mu_new, sig_row, mo, so, kl, part, write_back=write_back)
+        torch.testing.assert_close(kl, want, rtol=2e-5, atol=1e-7)
+        if write_back:
+            assert torch.equal(mo, mu_new.float()) and torch.equal(so, sig_row.expand(M, -1))
+        else:
+            assert torch.equal(mo, mu_old) and torch.equal(so, sg_old)
+    # a per-row sigma [M, A] (row stride A)
+    sg_rows = sig_row.expand(M, -1).contiguous() * 1.01
+    kl = torch.empty((), device="cuda")
+    gae.policy_kl(mu_new, sg_rows, mu_old.clone(), sg_old.clone(), kl, part, write_back=False)
+    torch.testing.assert_close(kl, A2CAgent._policy_kl(mu_new, sg_rows, mu_old, sg_old), rtol=2e-5, atol=1e-7)
+
+
+def test_adaptive_lr_kernel_matches_torch_scheduler():
+    """rl_adaptive_lr against A2CAgent._update_lr + the meters of _mb_finish: lr down above 2 thr, up below thr / 2,
+    unchanged between, clamps at 1e-6 / 1e-2, the rank average, the f32 optimizer copy; stats bit-identical."""
+    from isaacgymenv_amd.rl import gae
+    thr = 0.008
+    cases = [(0.5, 3e-4), (0.001, 3e-4), (0.008, 3e-4), (0.5, 1.2e-6), (0.0, 9e-3), (0.0161, 5e-4), (0.0039, 5e-4)]
+    for world in (1, 4):
+        for kl_v, lr_v in cases:
+            kl = torch.tensor(kl_v * world, device="cuda")
+            lr = torch.tensor(lr_v, dtype=torch.float64, device="cuda")
+            opt_lr = torch.tensor(lr_v, device="cuda")
+            stats = torch.tensor([1.0, 2.0, 3.0, 4.0], device="cuda")
+            losses = torch.tensor([0.25, 0.5, 0.125], device="cuda")
+            gae.adaptive_lr(kl, 1.0 / world, True, thr, lr, opt_lr, stats, losses[0], losses[1], losses[2])
+            k = torch.tensor(kl_v * world, device="cuda") / world if world > 1 else torch.tensor(kl_v, device="cuda")
+            kd, cur = k.double(), torch.tensor(lr_v, dtype=torch.float64, device="cuda")
+            want = torch.where(kd > 2.0 * thr, torch.clamp(cur / 1.5, min=1e-6), cur)
+            want = torch.where(kd < 0.5 * thr, torch.clamp(cur * 1.5, max=1e-2), want)
+            assert torch.equal(kl, k) and torch.equal(lr, want), (kl_v, lr_v, world)
+            assert torch.equal(opt_lr, want.float())
+            exp = torch.tensor([1.0, 2.0, 3.0, 4.0], device="cuda") + torch.stack([losses[0], losses[1], k, losses[2]])
+            assert torch.equal(stats, exp)
+    lr = torch.tensor(3e-4, dtype=torch.float64, device="cuda")
+    gae.adaptive_lr(torch.tensor(0.5, device="cuda"), 1.0, False, thr, lr, None, None, None, None, None)
+    assert float(lr) == 3e-4  # fixed schedule: lr untouched

@@ -5,7 +5,8 @@
 The case is the r04f UsefulHound failure by default: random Hound states (seed 13, spread
 0.5), actions RandomState(2), the fused 4 x PD + 1 step on the host backend.  Format (little endian): a
 magic, the gs_model_desc arrays in model_desc() order (each: int64 count, int32 kind 0 int32 / 1 float64, data),
-the scalar model fields, gs_sim_params, then N, nd, ns, the SoA state, shape frictions, actions, default pose and
+the scalar model fields, gs_sim_params, then N, nd, ns, self-collision, ground flag, the ground's frictions and
+restitution, the SoA state, shape frictions, actions, default pose and
 the PD gains.  The driver also writes its outputs next to it (<out.bin>.out) for compare().
 """
 import argparse
@@ -44,9 +45,14 @@ def case(name, n):
 
 
 def write(path, name, n):
+    """The case as the drop-in gymapi hands it to the library: the sim built by tests/helpers.make_host_sim (the
+    loaded asset's model, its gs_sim_params, self-collision flag and ground), then the case's state and actions."""
     flat, params, root, dof, mu, act, default = case(name, n)
+    N, nd = root.shape[0], dof.shape[1]
+    gym, sim = H.make_host_sim({"hound111": "hound"}.get(name, name), N, params, threads=1)
+    flat, p = sim.asset.flat, sim.cparams
     desc, keep = _lib.model_desc(flat)
-    N, nd, ns = root.shape[0], dof.shape[1], int(flat["ns"])
+    ns = int(flat["ns"])
     with open(path, "wb") as f:
         f.write(struct.pack("<I", MAGIC))
         for field, _ in _FIELDS:
@@ -56,11 +62,14 @@ def write(path, name, n):
         f.write(struct.pack("<10i", desc.num_bodies, desc.num_dofs, desc.num_candidates, desc.num_shapes,
                             desc.fixed_base, desc.num_links, desc.num_hull_verts, desc.num_pairs, desc.pair_pool,
                             desc.num_pair_verts))
-        f.write(struct.pack("<di3dii4dii", params["dt"], params["substeps"], *params["gravity"], params["pos_iters"],
-                            params["vel_iters"], params["contact_offset"], params["rest_offset"], 0.2,
-                            params["max_depen_vel"], params.get("collect_contacts", 1), 0))
-        f.write(struct.pack("<d", params.get("limit_margin", 0.1)))
-        f.write(struct.pack("<5i", N, nd, ns, int(flat.get("self_collide", 0)), 1 if params.get("has_ground", 1) else 0))
+        f.write(struct.pack("<di3dii4dii", p.dt, p.substeps, *p.gravity, p.num_position_iterations,
+                            p.num_velocity_iterations, p.contact_offset, p.rest_offset, p.bounce_threshold_velocity,
+                            p.max_depenetration_velocity, p.contact_collection, p.kernel_variant))
+        f.write(struct.pack("<d", p.joint_limit_margin))
+        g = sim.ground
+        f.write(struct.pack("<5i", N, nd, ns, int(sim.self_collide), 0 if g is None else 1))
+        f.write(struct.pack("<3d", *((g.static_friction, g.dynamic_friction, g.restitution) if g is not None
+                                     else (0.0, 0.0, 0.0))))
         st = np.zeros((13 + 2 * nd, N), np.float32)
         st[0:13], st[13:13 + nd], st[13 + nd:] = root.T, dof[:, :, 0].T, dof[:, :, 1].T
         f.write(st.tobytes())

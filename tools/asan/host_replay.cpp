@@ -83,6 +83,8 @@ int main(int argc, char** argv) {
   p.num_threads = 1;
   int32_t hdr[5];
   rd(hdr, 5);
+  double gnd[3];
+  rd(gnd, 3);
   const int N = hdr[0], nd = hdr[1], ns = hdr[2], self_collide = hdr[3], ground = hdr[4];
   std::vector<float> state((size_t)(13 + 2 * nd) * N), mu((size_t)ns * N), act((size_t)N * nd), def(nd), g(4);
   rd(state.data(), state.size());
@@ -99,11 +101,16 @@ int main(int argc, char** argv) {
   }
   check(gs_sim_set_model(sim, &m), "gs_sim_set_model");
   check(gs_sim_set_self_collision(sim, self_collide), "gs_sim_set_self_collision");
-  if (ground) check(gs_sim_add_ground(sim, 1.0, 1.0, 0.0), "gs_sim_add_ground");
+  if (ground) check(gs_sim_add_ground(sim, gnd[0], gnd[1], gnd[2]), "gs_sim_add_ground");
   std::vector<float> cf((size_t)3 * m.num_links * N, 0.f);
   check(gs_sim_prepare(sim, N, state.data(), mu.data(), cf.data()), "gs_sim_prepare");
   std::vector<float> tau((size_t)N * nd, 0.f), dof_out((size_t)N * nd * 2, 0.f), root_out((size_t)N * 13, 0.f),
       contact_out((size_t)N * m.num_links * 3, 0.f);
+  for (int i = 0; i < N; ++i)  // the refreshed dof state tensor the first PD torque reads (gs_pd_args)
+    for (int d = 0; d < nd; ++d) {
+      dof_out[((size_t)i * nd + d) * 2] = state[(size_t)(13 + d) * N + i];
+      dof_out[((size_t)i * nd + d) * 2 + 1] = state[(size_t)(13 + nd + d) * N + i];
+    }
   gs_pd_args pd{};
   pd.actions = act.data();
   pd.default_pos = def.data();
