@@ -98,6 +98,34 @@ int rl_ppo_loss_backward(const float *grad_loss, const float *dmu, const float *
                          int32_t dvalues_is_f16, float *dlogstd_out, void *stream);
 
 /*
+ * ABI 6 -- the heads and the loss in one pass (rl_games network_builder's mu / value heads, fp16 under autocast,
+ * then rl_ppo_loss).  hidden: fp16 [rows][ld] holding the actor MLP's output in columns [actor_col, +hidden_size)
+ * and the critic's in [critic_col, +hidden_size) (disjoint; even columns, even ld, 4-byte aligned; hidden_size even
+ * and <= 256); w_mu [A][hidden_size], b_mu [A], w_v [hidden_size], b_v [1] fp16 (the parameters' fp16 shadows).
+ * mu = fp16(hidden_a w_mu^T + b_mu), value = fp16(hidden_c w_v + b_v) (fp32 accumulation), then rl_ppo_loss's
+ * statements: loss, stats[4], the unscaled dmu [rows][A], dvalues [rows], dlogstd [A] f32; mu_out fp16 [rows][A].
+ * partials >= rl_ppo_heads_partials_size(rows, hidden_size, A) f32 (shared by both passes).  Two launches.
+ */
+int rl_ppo_heads_partials_size(int32_t rows, int32_t hidden_size, int32_t num_actions);
+int rl_ppo_heads_loss(const void *hidden, int64_t ld, int32_t actor_col, int32_t critic_col, int32_t hidden_size,
+                      const void *w_mu, const void *b_mu, const void *w_v, const void *b_v, const float *logstd,
+                      const float *actions, const float *old_neglogp, const float *advantages, const float *old_values,
+                      const float *returns, int32_t rows, int32_t num_actions, double e_clip, int32_t clip_value,
+                      double critic_coef, double entropy_coef, double bounds_loss_coef, void *mu_out, float *dmu,
+                      float *dvalues, float *partials, float *loss, float *stats, float *dlogstd, void *stream);
+/*
+ * Backward: s = grad_loss[0]; d mu = fp16(dmu s), d v = fp16(dvalues s) (the fp16 head gradients), then
+ * dhidden (fp16, same layout as hidden; the two column ranges written) = d mu w_mu | d v w_v, and the head
+ * parameters' gradients ADDED to grad_w_mu [A][hidden_size], grad_b_mu [A], grad_w_v [hidden_size], grad_b_v [1],
+ * grad_logstd [A] += dlogstd s (f32; fixed-order sums over row blocks).  Two launches.
+ */
+int rl_ppo_heads_loss_backward(const float *grad_loss, const float *dmu, const float *dvalues, const float *dlogstd,
+                               const void *hidden, int64_t ld, int32_t actor_col, int32_t critic_col,
+                               int32_t hidden_size, const void *w_mu, const void *w_v, int32_t rows,
+                               int32_t num_actions, void *dhidden, float *partials, float *grad_w_mu, float *grad_b_mu,
+                               float *grad_w_v, float *grad_b_v, float *grad_logstd, void *stream);
+
+/*
  * RunningMeanStd of the model input (rl_games algos_torch/running_mean_std.py): with update != 0 the
  * batch mean / unbiased var of x [rows][cols] (cols <= 256) are merged into the float64 running moments
  * running_mean / running_var [cols] and count (0-d) as the reference does in train mode; then

@@ -292,6 +292,8 @@ class A2CAgent:
         # KL of the minibatch, dataset.update_mu_sigma, adaptive LR and the meters as three HIP launches
         # (gae.policy_kl / gae.adaptive_lr, rl_policy.hip) instead of ~14 torch ones
         self._fused_kl = self._fused_loss and self._opt_lr is not None
+        # ... and with the grouped actor / critic layout the heads join the loss pass (network.stacked_hidden)
+        self._fused_heads = self._fused_loss
         if self._fused_kl:
             self._kl_part = torch.zeros(gae.lib().rl_kl_partials_size(), dtype=torch.float32, device=dev)
 
@@ -485,6 +487,19 @@ class A2CAgent:
         cfg = self.cfg
         net = self.model.a2c_network
         obs = self.model.norm_obs(mb["obs"])
+        if self._fused_heads:
+            with torch.autocast("cuda", dtype=torch.float16, enabled=self.mixed_precision, cache_enabled=False):
+                st = net.stacked_hidden(obs)
+            if st is not None:  # the heads and the loss as one pass (gae.PpoHeadsLossFn, rl_ppo_heads_loss)
+                y, heads = st
+                loss, stats, mu = gae.PpoHeadsLossFn.apply(y, heads, net.sigma.detach(), mb["actions"],
+                                                           mb["old_logp_actions"], mb["advantages"], mb["old_values"],
+                                                           mb["returns"], cfg.e_clip, cfg.clip_value, cfg.critic_coef,
+                                                           self.entropy_coef, cfg.bounds_loss_coef)
+                self.flat_grad.zero_()
+                self.scaler.scale(loss).backward()
+                sigma = torch.exp(net.sigma.detach()).expand(mu.shape[0], -1)
+                return (stats[0], stats[1], stats[2], stats[3], mu, sigma)
         with torch.autocast("cuda", dtype=torch.float16, enabled=self.mixed_precision, cache_enabled=False):
             a_out, c_out = net.hidden(obs)
             values = net.value(c_out)

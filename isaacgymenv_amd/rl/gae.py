@@ -17,7 +17,8 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accum", "rl_colsum_accum", "rl_rollout_post",
                     "rl_ppo_loss", "rl_ppo_loss_backward", "rl_rms_normalize", "rl_opt_step", "rl_opt_partials_size",
                     "rl_linear_fwd", "rl_linear_transpose", "rl_linear_bwd", "rl_policy_head", "rl_linear_fwd_g",
-                    "rl_linear_bwd_g", "rl_kl_partials_size", "rl_policy_kl", "rl_adaptive_lr"]
+                    "rl_linear_bwd_g", "rl_kl_partials_size", "rl_policy_kl", "rl_adaptive_lr",
+                    "rl_ppo_heads_partials_size", "rl_ppo_heads_loss", "rl_ppo_heads_loss_backward"]
 _lib = None
 
 
@@ -76,6 +77,15 @@ def lib():
                                       C.POINTER(LinearGroups), vp]
         L.rl_linear_bwd_g.argtypes = [vp, vp, C.c_int32, C.c_int32, vp, C.c_int32, C.c_int32, vp, vp, C.c_int32, vp,
                                       vp, C.c_int64, C.POINTER(LinearGroups), vp]
+        L.rl_ppo_heads_partials_size.restype = C.c_int
+        L.rl_ppo_heads_partials_size.argtypes = [C.c_int32, C.c_int32, C.c_int32]
+        L.rl_ppo_heads_loss.restype = C.c_int
+        L.rl_ppo_heads_loss.argtypes = [vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, vp, vp, vp, vp, vp, vp, vp, vp,
+                                        vp, vp, C.c_int32, C.c_int32, C.c_double, C.c_int32, C.c_double, C.c_double,
+                                        C.c_double, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.rl_ppo_heads_loss_backward.restype = C.c_int
+        L.rl_ppo_heads_loss_backward.argtypes = [vp, vp, vp, vp, vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, vp, vp,
+                                                 C.c_int32, C.c_int32, vp, vp, vp, vp, vp, vp, vp, vp]
         L.rl_kl_partials_size.restype = C.c_int
         L.rl_policy_kl.restype = C.c_int
         L.rl_policy_kl.argtypes = [vp, C.c_int32, vp, C.c_int64, vp, vp, C.c_int32, C.c_int32, C.c_int32, vp, vp, vp]
@@ -271,6 +281,82 @@ class PpoLossFn(torch.autograd.Function):
         if rc != 0:
             raise RuntimeError(f"rl_ppo_loss_backward failed: {lib().rl_last_error().decode()}")
         return (dmu_out, dv_out, dls_out) + (None,) * 10
+
+
+class HeadsSpec:
+    """The mu / value heads of a separate actor-critic network for PpoHeadsLossFn: their fp16 parameter shadows and
+    the f32 gradient views the learner's flat buffers give them (direct gradients), the sigma parameter's gradient,
+    and where the actor / critic outputs sit in the grouped MLP's [rows][G*H] output."""
+
+    def __init__(self, actor_col, critic_col, hidden, w_mu, b_mu, w_v, b_v, gw_mu, gb_mu, gw_v, gb_v, g_logstd):
+        self.actor_col, self.critic_col, self.hidden = int(actor_col), int(critic_col), int(hidden)
+        self.w_mu, self.b_mu, self.w_v, self.b_v = w_mu, b_mu, w_v, b_v
+        self.gw_mu, self.gb_mu, self.gw_v, self.gb_v, self.g_logstd = gw_mu, gb_mu, gw_v, gb_v, g_logstd
+        for t in (w_mu, b_mu, w_v, b_v):
+            assert t.dtype == torch.float16 and t.is_contiguous()
+        for t in (gw_mu, gb_mu, gw_v, gb_v, g_logstd):
+            assert t.dtype == torch.float32 and t.is_contiguous()
+        self.num_actions = w_mu.shape[0]
+        assert w_mu.shape == (self.num_actions, self.hidden) and w_v.numel() == self.hidden and b_v.numel() == 1
+
+
+class PpoHeadsLossFn(torch.autograd.Function):
+    """The mu / value heads and the PPO loss in one pass (rl_ppo_heads_loss): hidden fp16 [B][ld] is the grouped
+    actor / critic MLP output (network._GroupedMLPFn stacked); returns (loss 0-d, stats [4], mu fp16 [B][A]).  The
+    backward (rl_ppo_heads_loss_backward) returns d hidden and adds the heads' and sigma's gradients straight into
+    the learner's flat gradient views (HeadsSpec) -- six hipBLASLt GEMMs, two reductions, a concatenation and the
+    loss's launches become four."""
+
+    @staticmethod
+    def forward(ctx, hidden, heads, logstd, actions, old_neglogp, advantages, old_values, returns, e_clip: float,
+                clip_value: bool, critic_coef: float, entropy_coef: float, bounds_loss_coef: float):
+        B, ld = hidden.shape
+        A, H = heads.num_actions, heads.hidden
+        dev = hidden.device
+        assert hidden.dtype == torch.float16 and hidden.stride(1) == 1 and hidden.data_ptr() % 4 == 0
+        for t in (logstd, actions, old_neglogp, advantages, old_values, returns):
+            assert t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
+        assert actions.shape == (B, A) and logstd.numel() == A and old_neglogp.numel() == B
+        assert advantages.numel() == B and old_values.numel() == B and returns.numel() == B
+        f32 = torch.float32
+        mu = torch.empty(B, A, dtype=torch.float16, device=dev)
+        dmu = torch.empty(B, A, dtype=f32, device=dev)
+        dv = torch.empty(B, dtype=f32, device=dev)
+        part = torch.empty(lib().rl_ppo_heads_partials_size(B, H, A), dtype=f32, device=dev)
+        loss = torch.empty((), dtype=f32, device=dev)
+        stats = torch.empty(4, dtype=f32, device=dev)
+        dls = torch.empty(A, dtype=f32, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _check(lib().rl_ppo_heads_loss(hidden.data_ptr(), hidden.stride(0), heads.actor_col, heads.critic_col, H,
+                                       heads.w_mu.data_ptr(), heads.b_mu.data_ptr(), heads.w_v.data_ptr(),
+                                       heads.b_v.data_ptr(), logstd.data_ptr(), actions.data_ptr(),
+                                       old_neglogp.data_ptr(), advantages.data_ptr(), old_values.data_ptr(),
+                                       returns.data_ptr(), B, A, float(e_clip), int(bool(clip_value)),
+                                       float(critic_coef), float(entropy_coef), float(bounds_loss_coef), mu.data_ptr(),
+                                       dmu.data_ptr(), dv.data_ptr(), part.data_ptr(), loss.data_ptr(),
+                                       stats.data_ptr(), dls.data_ptr(), stream), "rl_ppo_heads_loss")
+        ctx.save_for_backward(hidden, dmu, dv, dls, part)
+        ctx.heads = heads
+        ctx.mark_non_differentiable(stats, mu)
+        return loss, stats, mu
+
+    @staticmethod
+    def backward(ctx, g_loss, g_stats, g_mu):
+        hidden, dmu, dv, dls, part = ctx.saved_tensors
+        hd = ctx.heads
+        B, A = dmu.shape
+        g = (g_loss if g_loss is not None else torch.ones((), device=hidden.device)).float().contiguous()
+        dh = torch.empty_like(hidden)
+        if hd.hidden * 2 != hidden.shape[1]:
+            dh.zero_()  # columns outside the two ranges get no gradient
+        _check(lib().rl_ppo_heads_loss_backward(g.data_ptr(), dmu.data_ptr(), dv.data_ptr(), dls.data_ptr(),
+                                                hidden.data_ptr(), hidden.stride(0), hd.actor_col, hd.critic_col,
+                                                hd.hidden, hd.w_mu.data_ptr(), hd.w_v.data_ptr(), B, A, dh.data_ptr(),
+                                                part.data_ptr(), hd.gw_mu.data_ptr(), hd.gb_mu.data_ptr(),
+                                                hd.gw_v.data_ptr(), hd.gb_v.data_ptr(), hd.g_logstd.data_ptr(),
+                                                torch.cuda.current_stream(hidden.device).cuda_stream),
+               "rl_ppo_heads_loss_backward")
+        return (dh,) + (None,) * 12
 
 
 def rms_supported(x: torch.Tensor) -> bool:

@@ -259,7 +259,7 @@ class _GroupedMLPFn(torch.autograd.Function):
 
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda")
-    def forward(ctx, x, spec, *params):
+    def forward(ctx, x, spec, stacked, *params):
         h = torch.float16
         xc = x.to(h)
         if xc.stride(1) != 1 or xc.stride(0) % 4 or xc.data_ptr() % 8:
@@ -278,6 +278,8 @@ class _GroupedMLPFn(torch.autograd.Function):
         ctx.save_for_backward(xc, *ys)
         ctx.spec = spec
         n_last = spec.layers[-1][0]
+        if stacked:  # the [M][G*N] output itself (PpoHeadsLossFn reads both groups' columns from it)
+            return ys[-1]
         return tuple(ys[-1][:, g * n_last:(g + 1) * n_last] for g in range(G))
 
     @staticmethod
@@ -287,8 +289,11 @@ class _GroupedMLPFn(torch.autograd.Function):
         spec = ctx.spec
         G, M = spec.G, xc.shape[0]
         n_last = spec.layers[-1][0]
-        dy = torch.cat([(g if g is not None else torch.zeros(M, n_last, device=xc.device)).to(torch.float16)
-                        for g in gouts], dim=1)
+        if len(gouts) == 1:  # stacked output: the gradient already has the [M][G*N] layout
+            dy = gouts[0].to(torch.float16).contiguous()
+        else:
+            dy = torch.cat([(g if g is not None else torch.zeros(M, n_last, device=xc.device)).to(torch.float16)
+                            for g in gouts], dim=1)
         for l in reversed(range(len(spec.layers))):
             N, K, wh, _, span = spec.layers[l]
             # the per-network path's row blocks (network._LinearELUFn): the same fixed-order partial sums
@@ -302,7 +307,7 @@ class _GroupedMLPFn(torch.autograd.Function):
                                        splits, part, part[:, G * N * K:], G * (N * K + N), N * K, N, G)
                 dy = dx
             gae.splitk_accum(part, span)
-        return (None, None) + (None,) * len(spec.params)
+        return (None, None, None) + (None,) * len(spec.params)
 
 
 class _MLP(nn.Sequential):
@@ -376,11 +381,28 @@ class ActorCriticNetwork(nn.Module):
         """(actor MLP output, critic MLP output): under the learner's grouped layout one launch per GEMM for both."""
         if self.separate and self.grouped is not None:
             if self.grouped.applies(obs):
-                return _GroupedMLPFn.apply(obs, self.grouped, *self.grouped.params)
+                return _GroupedMLPFn.apply(obs, self.grouped, False, *self.grouped.params)
             if self.grouped.act_applies(obs):
                 return self.grouped.act_forward(obs)
         a_out = self.actor_mlp(obs)
         return a_out, (self.critic_mlp(obs) if self.separate else a_out)
+
+    def stacked_hidden(self, obs):
+        """The grouped actor / critic output as one fp16 [rows][2 * H] tensor (actor columns first) and the heads'
+        spec for gae.PpoHeadsLossFn, or None where the grouped MFMA path does not apply (fp16 autocast, learner
+        layout, fixed sigma, heads' fp16 shadows and flat gradient views bound)."""
+        if not (self.separate and self.fixed_sigma and self.grouped is not None and self.grouped.G == 2
+                and self.grouped.applies(obs)):
+            return None
+        mu, val = self.mu, self.value
+        if (mu.half_weight is None or mu.half_bias is None or val.half_weight is None or val.half_bias is None
+                or val.out_features != 1 or mu.weight.grad is None or val.weight.grad is None
+                or self.sigma.grad is None or mu.in_features % 2):
+            return None
+        H = mu.in_features
+        heads = gae.HeadsSpec(0, H, H, mu.half_weight, mu.half_bias, val.half_weight, val.half_bias, mu.weight.grad,
+                              mu.bias.grad, val.weight.grad, val.bias.grad, self.sigma.grad)
+        return _GroupedMLPFn.apply(obs, self.grouped, True, *self.grouped.params), heads
 
     def forward(self, obs):
         a_out, c_out = self.hidden(obs)
