@@ -64,6 +64,21 @@ int rl_splitk_accum(const void *parts, int32_t num_parts, int64_t n, int32_t par
                     void *stream);
 
 /*
+ * ABI 6: up to RL_SPLITK_MAX_JOBS rl_splitk_accum finishes in one launch (the learner's layers at the end of the
+ * backward); store != 0: grad = sum (no read of grad; the fused learner writes each gradient once and skips
+ * zeroing the flat buffer), else grad += sum.  Same per-job arithmetic and order as rl_splitk_accum.
+ */
+#define RL_SPLITK_MAX_JOBS 8
+typedef struct rl_splitk_job {
+    const void *parts;
+    float *grad;
+    int64_t n;
+    int32_t num_parts;
+    int32_t parts_are_f16;
+} rl_splitk_job;
+int rl_splitk_accum_multi(const rl_splitk_job *jobs, int32_t num_jobs, int32_t store, void *stream);
+
+/*
  * grad[c] += sum_r g[r * cols + c]   (the bias gradient of a Linear layer: column sums of its output
  * gradient; fp32 sums, deterministic: fixed-order row-block partials, then the partials added in a
  * fixed order; two launches on `stream`)
@@ -117,13 +132,15 @@ int rl_ppo_heads_loss(const void *hidden, int64_t ld, int32_t actor_col, int32_t
  * Backward: s = grad_loss[0]; d mu = fp16(dmu s), d v = fp16(dvalues s) (the fp16 head gradients), then
  * dhidden (fp16, same layout as hidden; the two column ranges written) = d mu w_mu | d v w_v, and the head
  * parameters' gradients ADDED to grad_w_mu [A][hidden_size], grad_b_mu [A], grad_w_v [hidden_size], grad_b_v [1],
- * grad_logstd [A] += dlogstd s (f32; fixed-order sums over row blocks).  Two launches.
+ * grad_logstd [A] += dlogstd s (f32; fixed-order sums over row blocks; store_grads: = instead of +=, the fused
+ * learner's zero-free flat gradient).  Two launches.
  */
 int rl_ppo_heads_loss_backward(const float *grad_loss, const float *dmu, const float *dvalues, const float *dlogstd,
                                const void *hidden, int64_t ld, int32_t actor_col, int32_t critic_col,
                                int32_t hidden_size, const void *w_mu, const void *w_v, int32_t rows,
                                int32_t num_actions, void *dhidden, float *partials, float *grad_w_mu, float *grad_b_mu,
-                               float *grad_w_v, float *grad_b_v, float *grad_logstd, void *stream);
+                               float *grad_w_v, float *grad_b_v, float *grad_logstd, int32_t store_grads,
+                               void *stream);
 
 /*
  * RunningMeanStd of the model input (rl_games algos_torch/running_mean_std.py): with update != 0 the
@@ -134,6 +151,9 @@ int rl_ppo_heads_loss_backward(const float *grad_loss, const float *dmu, const f
  */
 int rl_rms_normalize(const float *x, int32_t rows, int32_t cols, double *running_mean, double *running_var,
                      double *count, double epsilon, int32_t update, float *partials, float *y, void *stream);
+/* ABI 6: the same with y written as fp16 (the learner's first-layer operand; the value autocast would cast to). */
+int rl_rms_normalize_h(const float *x, int32_t rows, int32_t cols, double *running_mean, double *running_var,
+                       double *count, double epsilon, int32_t update, float *partials, void *y_half, void *stream);
 
 /*
  * Act-forward head of the fixed-sigma continuous model (rl_games ModelA2CContinuousLogStd eval forward):
@@ -187,6 +207,14 @@ int rl_opt_step(float *param, const float *grad, float *exp_avg, float *exp_avg_
                 const float *lr, float *scale, int32_t *growth_tracker, const rl_opt_hyper *hyper, float *partials,
                 void *stream);
 int rl_opt_partials_size(void);
+/*
+ * ABI 6: rl_opt_step that also writes the updated parameters' fp16 shadow param_half [n] (the next minibatch's
+ * GEMM operands, instead of a separate cast), with the step / scale bookkeeping in the Adam launch's last workgroup:
+ * two launches.  partials (rl_opt_partials_size() f32) zero-initialised once.
+ */
+int rl_opt_step_h(float *param, void *param_half, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+                  float *step, const float *lr, float *scale, int32_t *growth_tracker, const rl_opt_hyper *hyper,
+                  float *partials, void *stream);
 
 /*
  * ABI 5 -- the hidden Linear + ELU layers of the actor / critic MLPs on the matrix cores (rl_linear.hip; rl_games
@@ -237,17 +265,25 @@ int rl_linear_bwd_g(const void *dy, const void *y, int32_t M, int32_t N, const v
  * torch_ext.policy_kl, dataset.update_mu_sigma, schedulers.AdaptiveScheduler, the loss / kl meters).
  * rl_policy_kl: kl (f32 scalar) = mean over M rows of the sum over A of log(s1/s0 + 1e-5) + (s0^2 + (m1 - m0)^2) /
  *   (2 (s1^2 + 1e-5)) - 0.5 with m0 = mu_new [M][A] (mu_half: fp16, else f32), s0 = sigma_new (row r at
- *   r * sigma_row_stride: 0 = one [A] row for all), m1 / s1 = mu_old / sigma_old [M][A] f32; write_back: mu_old /
- *   sigma_old receive the new values (update_mu_sigma).  Fixed-order sums; partials >= rl_kl_partials_size() f32.
+ *   r * sigma_row_stride: 0 = one [A] row for all; sigma_is_log: the row holds log sigma, s0 = exp of it),
+ *   m1 / s1 = mu_old / sigma_old [M][A] f32; write_back: mu_old / sigma_old receive the new values
+ *   (update_mu_sigma).  Fixed-order sums; partials >= rl_kl_partials_size() f32, zero-initialised once.
  * rl_adaptive_lr: kl = kl * inv_world (the rank average after a summing all-reduce); adaptive: lr (f64) /= 1.5 if kl >
  *   2 kl_threshold (>= 1e-6), *= 1.5 if kl < kl_threshold / 2 (<= 1e-2), opt_lr (f32, nullable) = lr; stats (nullable):
  *   stats[0..3] += a_loss, c_loss, kl, entropy.  One thread, no host synchronisation.
+ * rl_policy_kl_step: rl_policy_kl then rl_adaptive_lr (inv_world 1) in ONE launch, the single-rank minibatch (the
+ *   last workgroup to finish sums the partials -- same order -- and steps the scheduler).
  */
 int rl_kl_partials_size(void);
-int rl_policy_kl(const void *mu_new, int32_t mu_half, const float *sigma_new, int64_t sigma_row_stride, float *mu_old,
-                 float *sigma_old, int32_t M, int32_t A, int32_t write_back, float *kl, float *partials, void *stream);
+int rl_policy_kl(const void *mu_new, int32_t mu_half, const float *sigma_new, int64_t sigma_row_stride,
+                 int32_t sigma_is_log, float *mu_old, float *sigma_old, int32_t M, int32_t A, int32_t write_back,
+                 float *kl, float *partials, void *stream);
 int rl_adaptive_lr(float *kl, float inv_world, int32_t adaptive, double kl_threshold, double *lr, float *opt_lr,
                    float *stats, const float *a_loss, const float *c_loss, const float *entropy, void *stream);
+int rl_policy_kl_step(const void *mu_new, int32_t mu_half, const float *sigma_new, int64_t sigma_row_stride,
+                      int32_t sigma_is_log, float *mu_old, float *sigma_old, int32_t M, int32_t A, int32_t write_back,
+                      float *kl, float *partials, int32_t adaptive, double kl_threshold, double *lr, float *opt_lr,
+                      float *stats, const float *a_loss, const float *c_loss, const float *entropy, void *stream);
 
 #ifdef __cplusplus
 }

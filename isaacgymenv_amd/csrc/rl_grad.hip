@@ -72,7 +72,103 @@ __global__ __launch_bounds__(kAccBlock) void k_splitk_accum(const void* __restri
     }
 }
 
+// several layers' finishes in one launch (rl_splitk_accum_multi): blocks [first[j], first[j + 1]) finish job j;
+// store: grad = sum instead of grad += sum (the learner's fused path writes every gradient exactly once, so the
+// flat gradient buffer needs no zeroing)
+struct MultiJobs {
+    const void* parts[RL_SPLITK_MAX_JOBS];
+    float* grad[RL_SPLITK_MAX_JOBS];
+    int64_t n[RL_SPLITK_MAX_JOBS];
+    int32_t P[RL_SPLITK_MAX_JOBS];
+    int32_t half[RL_SPLITK_MAX_JOBS];
+    int32_t vec[RL_SPLITK_MAX_JOBS];
+    int32_t first[RL_SPLITK_MAX_JOBS + 1];
+    int32_t njobs, store;
+};
+
+template <bool HALF>
+__device__ __forceinline__ void accum_lanes(const void* __restrict__ parts, int P, int64_t n, float* __restrict__ grad,
+                                            bool vec, int64_t i0, bool store) {
+    float acc[kVec] = {0.f, 0.f, 0.f, 0.f};
+    if (vec) {
+        constexpr int kBatch = 16;
+        for (int p0 = 0; p0 < P; p0 += kBatch) {
+            float4 v[kBatch];
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b) {
+                const int p = p0 + b < P ? p0 + b : P - 1;
+                if constexpr (HALF) {
+                    const __half2* src = reinterpret_cast<const __half2*>(static_cast<const __half*>(parts) + p * n + i0);
+                    const float2 a = __half22float2(src[0]), c = __half22float2(src[1]);
+                    v[b] = make_float4(a.x, a.y, c.x, c.y);
+                } else {
+                    v[b] = *reinterpret_cast<const float4*>(static_cast<const float*>(parts) + p * n + i0);
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b) {
+                if (p0 + b < P) { acc[0] += v[b].x; acc[1] += v[b].y; acc[2] += v[b].z; acc[3] += v[b].w; }
+            }
+        }
+        float4 g = store ? make_float4(0.f, 0.f, 0.f, 0.f) : *reinterpret_cast<float4*>(grad + i0);
+        g.x += acc[0]; g.y += acc[1]; g.z += acc[2]; g.w += acc[3];
+        *reinterpret_cast<float4*>(grad + i0) = g;
+        return;
+    }
+    for (int k = 0; k < kVec && i0 + k < n; ++k) {
+        float a = 0.f;
+        for (int p = 0; p < P; ++p) {
+            if constexpr (HALF) a += __half2float(static_cast<const __half*>(parts)[p * n + i0 + k]);
+            else a += static_cast<const float*>(parts)[p * n + i0 + k];
+        }
+        grad[i0 + k] = store ? a : grad[i0 + k] + a;
+    }
+}
+
+__global__ __launch_bounds__(kAccBlock) void k_splitk_accum_multi(MultiJobs J) {
+    int j = 0;
+    while (j + 1 < J.njobs && (int)blockIdx.x >= J.first[j + 1]) ++j;
+    const int64_t i0 = ((int64_t)(blockIdx.x - J.first[j]) * kAccBlock + threadIdx.x) * kVec;
+    if (i0 >= J.n[j]) return;
+    if (J.half[j]) accum_lanes<true>(J.parts[j], J.P[j], J.n[j], J.grad[j], J.vec[j], i0, J.store);
+    else accum_lanes<false>(J.parts[j], J.P[j], J.n[j], J.grad[j], J.vec[j], i0, J.store);
+}
+
 }  // namespace
+
+extern "C" int rl_splitk_accum_multi(const rl_splitk_job* jobs, int32_t num_jobs, int32_t store, void* stream) {
+    if (!jobs || num_jobs <= 0 || num_jobs > RL_SPLITK_MAX_JOBS)
+        return rl_set_error("rl_splitk_accum_multi: 1 <= num_jobs <= RL_SPLITK_MAX_JOBS jobs required");
+    MultiJobs J{};
+    int64_t blocks = 0;
+    for (int j = 0; j < num_jobs; ++j) {
+        const rl_splitk_job& q = jobs[j];
+        if (q.num_parts <= 0 || q.n < 0 || (q.n > 0 && (!q.parts || !q.grad)))
+            return rl_set_error("rl_splitk_accum_multi: a job has a null pointer, num_parts <= 0 or n < 0");
+        const uintptr_t align = q.parts_are_f16 ? 8 : 16;
+        J.parts[j] = q.parts;
+        J.grad[j] = q.grad;
+        J.n[j] = q.n;
+        J.P[j] = q.num_parts;
+        J.half[j] = q.parts_are_f16 ? 1 : 0;
+        J.vec[j] = (q.n % kVec) == 0 && ((uintptr_t)q.parts % align) == 0 && ((uintptr_t)q.grad % 16) == 0;
+        J.first[j] = (int32_t)blocks;
+        blocks += ((q.n + kVec - 1) / kVec + kAccBlock - 1) / kAccBlock;
+        if (blocks > INT32_MAX) return rl_set_error("rl_splitk_accum_multi: too many elements");
+    }
+    J.first[num_jobs] = (int32_t)blocks;
+    J.njobs = num_jobs;
+    J.store = store ? 1 : 0;
+    if (blocks == 0) return 0;
+    hipLaunchKernelGGL(k_splitk_accum_multi, dim3((unsigned)blocks), dim3(kAccBlock), 0, (hipStream_t)stream, J);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        char msg[256];
+        snprintf(msg, sizeof(msg), "rl_splitk_accum_multi: launch failed: %s", hipGetErrorString(e));
+        return rl_set_error(msg) + 1;
+    }
+    return 0;
+}
 
 extern "C" int rl_splitk_accum(const void* parts, int32_t num_parts, int64_t n, int32_t parts_are_f16, float* grad,
                                void* stream) {

@@ -357,79 +357,94 @@ __global__ __launch_bounds__(256) void k_heads_fwd(const __half* __restrict__ hi
     if (t < 4 + A) part[(size_t)blockIdx.x * kNT + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
 }
 
-// one thread per hidden column (actor column c and critic column c) and row group: 256 / H groups of kHRB * H / 256
-// rows, loads RC rows at a time
+// one thread per column pair (actor columns 2p, 2p + 1 and the critic's) and row group: 512 / H groups of
+// kHRB * H / 512 rows (16 for H = 128), every row's loads issued before the math
 template <int AM>
 __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ g, const float* __restrict__ dmu,
                                                    const float* __restrict__ dv, const __half* __restrict__ hid,
                                                    int ld, int acol, int ccol, int H, const __half* __restrict__ wmu,
                                                    const __half* __restrict__ wv, int B, int A,
                                                    __half* __restrict__ dhid, float* __restrict__ part) {
-    constexpr int RC = 16, SDW = (AM + 4) & ~3;  // row stride of sd: 16-byte aligned rows
-    __shared__ float sd[kHRB][SDW];               // the rows' fp16 d mu (as float) and, in column AM, d v
-    __shared__ float comb[256 * (AM + 1)];        // the row groups' weight partials
+    constexpr int SDW = (AM + 4) & ~3, NS = 2 * AM + 2, RMAX = 64;  // sd row stride; partial slots per thread
+    __shared__ float sd[kHRB][SDW];  // the rows' fp16 d mu (as float) and, in column AM, d v
+    __shared__ float comb[NS * 256];  // the row groups' weight partials
     const int t = threadIdx.x, row0 = blockIdx.x * kHRB;
     const int nrow = min(kHRB, B - row0);
     const float s = *g;
+    const int H2 = H / 2, GR = 256 / H2, grp = t / H2, p = t - grp * H2, RPG = kHRB / GR;
+    // the gradient rows (scaled, rounded to fp16 as the torch path's head gradients) and this thread's weights
     if (t < kHRB) {
 #pragma unroll
         for (int a = 0; a < AM; ++a) sd[t][a] = (a < A && t < nrow) ? rnd_h(dmu[(size_t)(row0 + t) * A + a] * s) : 0.f;
         sd[t][AM] = t < nrow ? rnd_h(dv[row0 + t] * s) : 0.f;
     }
-    const int GR = 256 / H, grp = t / H, c = t - grp * H, RPG = kHRB / GR;
-    float w[AM], acc[AM];
+    float w0[AM], w1[AM], acc0[AM], acc1[AM];
 #pragma unroll
     for (int a = 0; a < AM; ++a) {
-        w[a] = a < A ? h2f(wmu[(size_t)a * H + c]) : 0.f;
-        acc[a] = 0.f;
+        w0[a] = a < A ? h2f(wmu[(size_t)a * H + 2 * p]) : 0.f;  // (the fp16 shadow: 2-byte aligned only)
+        w1[a] = a < A ? h2f(wmu[(size_t)a * H + 2 * p + 1]) : 0.f;
+        acc0[a] = 0.f;
+        acc1[a] = 0.f;
     }
-    const float wvc = h2f(wv[c]);
-    float accv = 0.f;
-    __syncthreads();
+    const float wv0 = h2f(wv[2 * p]), wv1 = h2f(wv[2 * p + 1]);
+    float av0 = 0.f, av1 = 0.f;
     const int r0 = grp * RPG, r1 = min(r0 + RPG, nrow);
-    for (int rb = r0; rb < r1; rb += RC) {
-        __half xa[RC], xc[RC];
+    __half2 xa[RMAX / 4], xc[RMAX / 4];  // RPG <= 16 for H <= 128; H = 256 takes two passes below
+    __syncthreads();
+    for (int rb = r0; rb < r1; rb += RMAX / 4) {
 #pragma unroll
-        for (int k = 0; k < RC; ++k) {
+        for (int k = 0; k < RMAX / 4; ++k) {
             const size_t o = (size_t)(row0 + rb + k) * ld;
-            xa[k] = rb + k < r1 ? hid[o + acol + c] : __float2half(0.f);
-            xc[k] = rb + k < r1 ? hid[o + ccol + c] : __float2half(0.f);
+            const bool in = rb + k < r1;
+            xa[k] = in ? *reinterpret_cast<const __half2*>(hid + o + acol + 2 * p) : __half2{};
+            xc[k] = in ? *reinterpret_cast<const __half2*>(hid + o + ccol + 2 * p) : __half2{};
         }
 #pragma unroll
-        for (int k = 0; k < RC; ++k) {
+        for (int k = 0; k < RMAX / 4; ++k) {
             const int r = rb + k;
             if (r < r1) {
-                const float x = h2f(xa[k]);
-                float dx = 0.f;
+                const float x0 = __low2float(xa[k]), x1 = __high2float(xa[k]);
+                float d0 = 0.f, d1 = 0.f;
 #pragma unroll
                 for (int a = 0; a < AM; ++a) {
                     if (a < A) {
                         const float d = sd[r][a];
-                        dx += d * w[a];
-                        acc[a] += d * x;
+                        d0 += d * w0[a];
+                        d1 += d * w1[a];
+                        acc0[a] += d * x0;
+                        acc1[a] += d * x1;
                     }
                 }
-                const float d = sd[r][AM];
+                const float dvr = sd[r][AM];
                 const size_t o = (size_t)(row0 + r) * ld;
-                dhid[o + acol + c] = __float2half(dx);
-                dhid[o + ccol + c] = __float2half(d * wvc);
-                accv += d * h2f(xc[k]);
+                *reinterpret_cast<__half2*>(dhid + o + acol + 2 * p) = __floats2half2_rn(d0, d1);
+                *reinterpret_cast<__half2*>(dhid + o + ccol + 2 * p) = __floats2half2_rn(dvr * wv0, dvr * wv1);
+                av0 += dvr * __low2float(xc[k]);
+                av1 += dvr * __high2float(xc[k]);
             }
         }
     }
     // the row groups' partials in a fixed order (group 0 adds 1, 2, ...)
 #pragma unroll
-    for (int a = 0; a < AM; ++a) comb[a * 256 + t] = acc[a];
-    comb[AM * 256 + t] = accv;
+    for (int a = 0; a < AM; ++a) {
+        comb[(2 * a) * 256 + t] = acc0[a];
+        comb[(2 * a + 1) * 256 + t] = acc1[a];
+    }
+    comb[(2 * AM) * 256 + t] = av0;
+    comb[(2 * AM + 1) * 256 + t] = av1;
     __syncthreads();
     const size_t P = (size_t)A * H + H + A + 1;
     float* pb = part + (size_t)blockIdx.x * P;
     if (grp == 0) {
         for (int a = 0; a <= A; ++a) {
-            const int sl = a < A ? a : AM;
-            float sum = comb[sl * 256 + c];
-            for (int g2 = 1; g2 < GR; ++g2) sum += comb[sl * 256 + g2 * H + c];
-            pb[(size_t)a * H + c] = sum;  // a == A: w_v's slot, right after W_mu's
+            const int sl = a < A ? 2 * a : 2 * AM;  // a == A: w_v, right after W_mu's slots
+            float s0 = comb[sl * 256 + p], s1 = comb[(sl + 1) * 256 + p];
+            for (int g2 = 1; g2 < GR; ++g2) {
+                s0 += comb[sl * 256 + g2 * H2 + p];
+                s1 += comb[(sl + 1) * 256 + g2 * H2 + p];
+            }
+            pb[(size_t)a * H + 2 * p] = s0;
+            pb[(size_t)a * H + 2 * p + 1] = s1;
         }
     }
     if (t <= A) {  // bias partials: d b_mu (t < A), d b_v (t == A)
@@ -462,17 +477,19 @@ __global__ __launch_bounds__(256) void k_heads_bfin(const float* __restrict__ pa
                                                     const float* __restrict__ g, const float* __restrict__ dls,
                                                     float* __restrict__ gw_mu, float* __restrict__ gb_mu,
                                                     float* __restrict__ gw_v, float* __restrict__ gb_v,
-                                                    float* __restrict__ g_logstd) {
+                                                    float* __restrict__ g_logstd, int store) {
     __shared__ float sh[4][64];
     const int P = A * H + H + A + 1;
     const int i = blockIdx.x * 64 + (threadIdx.x & 63);
     const float sum = sum_partials(part, blocks, (size_t)P, i, i < P, sh);
     if (threadIdx.x >= 64) return;
-    if (i < A * H) gw_mu[i] += sum;
-    else if (i < A * H + H) gw_v[i - A * H] += sum;
-    else if (i < A * H + H + A) gb_mu[i - A * H - H] += sum;
-    else if (i < P) gb_v[0] += sum;
-    else if (i < P + A) g_logstd[i - P] += dls[i - P] * *g;  // the sigma parameter (AccumulateGrad's add)
+    float* dst = i < A * H ? gw_mu + i
+                 : i < A * H + H ? gw_v + (i - A * H)
+                 : i < A * H + H + A ? gb_mu + (i - A * H - H)
+                 : i < P ? gb_v : i < P + A ? g_logstd + (i - P) : nullptr;
+    if (!dst) return;
+    const float val = i < P ? sum : dls[i - P] * *g;  // the sigma parameter: d logstd times the scale
+    *dst = store ? val : *dst + val;  // AccumulateGrad's add, or the first write of a zero-free flat buffer
 }
 
 int launch_err(const char* where) {
@@ -626,7 +643,7 @@ extern "C" int rl_ppo_heads_loss_backward(const float* grad_loss, const float* d
                                           int32_t critic_col, int32_t hidden_size, const void* w_mu, const void* w_v,
                                           int32_t rows, int32_t num_actions, void* dhidden, float* partials,
                                           float* grad_w_mu, float* grad_b_mu, float* grad_w_v, float* grad_b_v,
-                                          float* grad_logstd, void* stream) {
+                                          float* grad_logstd, int32_t store_grads, void* stream) {
     if (int rc = heads_check("rl_ppo_heads_loss_backward", ld, actor_col, critic_col, hidden_size, rows, num_actions))
         return rc;
     if (!grad_loss || !dmu || !dvalues || !dlogstd || !hidden || !w_mu || !w_v || !dhidden || !partials ||
@@ -642,6 +659,6 @@ extern "C" int rl_ppo_heads_loss_backward(const float* grad_loss, const float* d
     if (int rc = launch_err("rl_ppo_heads_loss_backward")) return rc;
     const int P = A * H + H + A + 1 + A;
     hipLaunchKernelGGL(k_heads_bfin, dim3((P + 63) / 64), dim3(256), 0, st, partials, blocks, A, H, grad_loss, dlogstd,
-                       grad_w_mu, grad_b_mu, grad_w_v, grad_b_v, grad_logstd);
+                       grad_w_mu, grad_b_mu, grad_w_v, grad_b_v, grad_logstd, (int)store_grads);
     return launch_err("rl_ppo_heads_loss_backward finish");
 }

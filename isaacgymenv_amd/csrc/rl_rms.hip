@@ -11,6 +11,7 @@
 //               batch mean / var to fp32 as torch's fp32 reductions return them, then updates the running
 //               moments with the reference formula in fp64, same operation order
 //   k_rms_norm: the normalisation (also the eval-mode path, update = 0); bumps the running count
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -108,9 +109,10 @@ __global__ __launch_bounds__(kFinCols * kFinSub) void k_rms_fin(const float* __r
     rvar[c] = m2 / tot;
 }
 
+template <class TY>  // float, or __half: the fp16 operand the learner's first layer casts it to anyway
 __global__ __launch_bounds__(256) void k_rms_norm(const float* __restrict__ x, int64_t n, int C,
                                                   const double* __restrict__ rmean, const double* __restrict__ rvar,
-                                                  float eps, float* __restrict__ y, double* __restrict__ count,
+                                                  float eps, TY* __restrict__ y, double* __restrict__ count,
                                                   double add) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (count && i == 0) *count += add;  // the running count, after k_rms_fin read it
@@ -118,14 +120,16 @@ __global__ __launch_bounds__(256) void k_rms_norm(const float* __restrict__ x, i
     const int c = (int)(i % C);
     const float m = (float)rmean[c];
     const float d = sqrtf((float)rvar[c] + eps);
-    y[i] = fminf(fmaxf((x[i] - m) / d, -5.f), 5.f);
+    const float v = fminf(fmaxf((x[i] - m) / d, -5.f), 5.f);
+    if constexpr (sizeof(TY) == 2) y[i] = __float2half(v);
+    else y[i] = v;
 }
 
 }  // namespace
 
-extern "C" int rl_rms_normalize(const float* x, int32_t rows, int32_t cols, double* running_mean, double* running_var,
-                                double* count, double epsilon, int32_t update, float* partials, float* y,
-                                void* stream) {
+static int rms_normalize(const float* x, int32_t rows, int32_t cols, double* running_mean, double* running_var,
+                         double* count, double epsilon, int32_t update, float* partials, void* y, bool half,
+                         void* stream) {
     if (rows <= 0 || cols <= 0 || cols > kCols) return rl_set_error("rl_rms_normalize: rows > 0, 0 < cols <= 256");
     if (!x || !running_mean || !running_var || !y || (update && (!count || !partials)))
         return rl_set_error("rl_rms_normalize: null pointer");
@@ -137,8 +141,12 @@ extern "C" int rl_rms_normalize(const float* x, int32_t rows, int32_t cols, doub
                            blocks, (int)rows, (int)cols, running_mean, running_var, count);
     }
     const int64_t n = (int64_t)rows * cols;
-    hipLaunchKernelGGL(k_rms_norm, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, (int)cols,
-                       running_mean, running_var, (float)epsilon, y, update ? count : nullptr, (double)rows);
+    if (half)
+        hipLaunchKernelGGL(k_rms_norm<__half>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, (int)cols,
+                           running_mean, running_var, (float)epsilon, (__half*)y, update ? count : nullptr, (double)rows);
+    else
+        hipLaunchKernelGGL(k_rms_norm<float>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, n, (int)cols,
+                           running_mean, running_var, (float)epsilon, (float*)y, update ? count : nullptr, (double)rows);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         char msg[256];
@@ -146,4 +154,17 @@ extern "C" int rl_rms_normalize(const float* x, int32_t rows, int32_t cols, doub
         return rl_set_error(msg) + 1;
     }
     return 0;
+}
+
+extern "C" int rl_rms_normalize(const float* x, int32_t rows, int32_t cols, double* running_mean, double* running_var,
+                                double* count, double epsilon, int32_t update, float* partials, float* y,
+                                void* stream) {
+    return rms_normalize(x, rows, cols, running_mean, running_var, count, epsilon, update, partials, y, false, stream);
+}
+
+extern "C" int rl_rms_normalize_h(const float* x, int32_t rows, int32_t cols, double* running_mean,
+                                  double* running_var, double* count, double epsilon, int32_t update, float* partials,
+                                  void* y_half, void* stream) {
+    return rms_normalize(x, rows, cols, running_mean, running_var, count, epsilon, update, partials, y_half, true,
+                         stream);
 }

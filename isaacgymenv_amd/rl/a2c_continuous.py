@@ -224,6 +224,8 @@ class A2CAgent:
                                               weight_decay=cfg.weight_decay)
         self.mixed_precision = cfg.mixed_precision and on_gpu
         self.scaler = torch.amp.GradScaler("cuda", enabled=self.mixed_precision)
+        if self.mixed_precision:  # the scale / growth tracker tensors now (the fused path never calls scale())
+            self.scaler._lazy_init_scale_growth_tracker(self.device)
         # the minibatch optimizer step as one HIP pass over the flat buffers (gae.opt_step, rl_opt_step):
         # unscale, found-inf, norm clip, Adam, scaler update -- ~20 launches become 3.  The Adam moments
         # are flat buffers too, and the optimizer's per-parameter state holds views into them, so
@@ -233,7 +235,7 @@ class A2CAgent:
             self.flat_m = torch.zeros_like(self.flat_param)
             self.flat_v = torch.zeros_like(self.flat_param)
             self._opt_step_t = torch.zeros((), dtype=torch.float32, device=self.device)
-            self._opt_part = torch.empty(gae.lib().rl_opt_partials_size(), dtype=torch.float32, device=self.device)
+            self._opt_part = torch.zeros(gae.lib().rl_opt_partials_size(), dtype=torch.float32, device=self.device)
             self._bind_opt_state()
             b1, b2 = self.optimizer.defaults["betas"]
             self._opt_hyper = gae.OptHyper(cfg.grad_norm if cfg.truncate_grads else 0.0, b1, b2,
@@ -293,7 +295,13 @@ class A2CAgent:
         # (gae.policy_kl / gae.adaptive_lr, rl_policy.hip) instead of ~14 torch ones
         self._fused_kl = self._fused_loss and self._opt_lr is not None
         # ... and with the grouped actor / critic layout the heads join the loss pass (network.stacked_hidden)
-        self._fused_heads = self._fused_loss
+        self._fused_heads = self._fused_loss and net.grouped is not None and self.mixed_precision
+        # that path writes every parameter's gradient exactly once (MLP layers, heads, sigma): no zeroing needed
+        covered = (sum(p.numel() for p in net.grouped.params) + net.mu.weight.numel() + net.mu.bias.numel()
+                   + net.value.weight.numel() + net.value.bias.numel() + net.sigma.numel()) if self._fused_heads else -1
+        self._grad_store_covers_all = covered == self.flat_grad.numel()
+        # the optimizer writes the fp16 parameter shadow with its update (rl_opt_step_h)
+        self._shadow_by_opt = self._fused_opt and self.flat_param_half is not None
         if self._fused_kl:
             self._kl_part = torch.zeros(gae.lib().rl_kl_partials_size(), dtype=torch.float32, device=dev)
 
@@ -454,8 +462,10 @@ class A2CAgent:
         cfg = self.cfg
         e = cfg.e_clip
         mb = self._minibatch(i)
-        if self.mixed_precision and self.flat_param_half is not None:
-            self.flat_param_half.copy_(self.flat_param)  # the fp16 weights of this minibatch, one cast
+        if self.mixed_precision and self.flat_param_half is not None and (i == 0 or not self._shadow_by_opt):
+            # the fp16 weights of this minibatch, one cast (with rl_opt_step_h the optimizer writes them after each
+            # minibatch: only a mini-epoch's first minibatch refreshes them, after whatever changed them outside)
+            self.flat_param_half.copy_(self.flat_param)
         if self._fused_loss:
             return self._mb_forward_backward_fused(mb)
         with torch.autocast("cuda", dtype=torch.float16, enabled=self.mixed_precision, cache_enabled=False):
@@ -486,20 +496,29 @@ class A2CAgent:
         loss statements and their autograd become three.  Same terms, same autograd rules."""
         cfg = self.cfg
         net = self.model.a2c_network
-        obs = self.model.norm_obs(mb["obs"])
-        if self._fused_heads:
-            with torch.autocast("cuda", dtype=torch.float16, enabled=self.mixed_precision, cache_enabled=False):
-                st = net.stacked_hidden(obs)
-            if st is not None:  # the heads and the loss as one pass (gae.PpoHeadsLossFn, rl_ppo_heads_loss)
+        if self._fused_heads and self.mixed_precision:
+            # the heads and the loss as one pass (gae.PpoHeadsLossFn, rl_ppo_heads_loss) after the grouped MLPs;
+            # the normalised obs written as fp16 (the first layer's operand); every gradient stored by its one
+            # writer (no zeroing of the flat buffer); the GradScaler scale fed as the loss's gradient (what
+            # scaler.scale(loss).backward() computes, minus its two elementwise launches)
+            obs_h = self.model.norm_obs_half(mb["obs"])
+            with torch.autocast("cuda", dtype=torch.float16, cache_enabled=False):
+                st = net.stacked_hidden(obs_h)
+            if st is not None:
                 y, heads = st
                 loss, stats, mu = gae.PpoHeadsLossFn.apply(y, heads, net.sigma.detach(), mb["actions"],
                                                            mb["old_logp_actions"], mb["advantages"], mb["old_values"],
                                                            mb["returns"], cfg.e_clip, cfg.clip_value, cfg.critic_coef,
                                                            self.entropy_coef, cfg.bounds_loss_coef)
-                self.flat_grad.zero_()
-                self.scaler.scale(loss).backward()
-                sigma = torch.exp(net.sigma.detach()).expand(mu.shape[0], -1)
-                return (stats[0], stats[1], stats[2], stats[3], mu, sigma)
+                if not self._grad_store_covers_all:
+                    self.flat_grad.zero_()
+                if self.scaler._scale is None:  # a GradScaler swapped in after construction
+                    self.scaler._lazy_init_scale_growth_tracker(self.device)
+                torch.autograd.backward(loss, grad_tensors=self.scaler._scale.reshape(()))
+                # sigma as the log row (the KL pass takes exp of it)
+                return (stats[0], stats[1], stats[2], stats[3], mu, net.sigma.detach())
+            raise RuntimeError("fused heads path selected but network.stacked_hidden does not apply")
+        obs = self.model.norm_obs(mb["obs"])
         with torch.autocast("cuda", dtype=torch.float16, enabled=self.mixed_precision, cache_enabled=False):
             a_out, c_out = net.hidden(obs)
             values = net.value(c_out)
@@ -533,8 +552,12 @@ class A2CAgent:
         if self._fused_opt:
             scale = self.scaler._scale if self.mixed_precision else None
             tracker = self.scaler._growth_tracker if self.mixed_precision else None
-            gae.opt_step(self.flat_param, self.flat_grad, self.flat_m, self.flat_v, self._opt_step_t, self._opt_lr,
-                         scale, tracker, self._opt_hyper, self._opt_part)
+            if self._shadow_by_opt:  # + the fp16 shadow of the updated parameters, 2 launches
+                gae.opt_step_h(self.flat_param, self.flat_param_half, self.flat_grad, self.flat_m, self.flat_v,
+                               self._opt_step_t, self._opt_lr, scale, tracker, self._opt_hyper, self._opt_part)
+            else:
+                gae.opt_step(self.flat_param, self.flat_grad, self.flat_m, self.flat_v, self._opt_step_t,
+                             self._opt_lr, scale, tracker, self._opt_hyper, self._opt_part)
         else:
             if self.cfg.truncate_grads:
                 self.scaler.unscale_(self.optimizer)
@@ -543,19 +566,26 @@ class A2CAgent:
             self.scaler.update()
         mb = self._minibatch(i)
         with torch.no_grad():
+            log_row = out[5].dim() == 1  # the fused heads path hands over log sigma (one row for all)
             if self._fused_kl:  # KL + update_mu_sigma: the dataset rows take the new values in the same pass
                 kl = torch.empty((), dtype=torch.float32, device=self.device)
-                gae.policy_kl(out[4], out[5][0] if out[5].stride(0) == 0 else out[5], mb["mu"], mb["sigma"], kl,
-                              self._kl_part, write_back=True)
+                sig = out[5] if log_row else (out[5][0] if out[5].stride(0) == 0 else out[5])
+                # single rank: the scheduler step and the meters in the same launch (no KL all-reduce between)
+                lr_step = None if self.multi_gpu else (self.cfg.lr_schedule == "adaptive", self.cfg.kl_threshold,
+                                                       self.lr, self._opt_lr, self._stats_acc, out[0], out[1], out[2])
+                gae.policy_kl(out[4], sig, mb["mu"], mb["sigma"], kl, self._kl_part, write_back=True,
+                              sigma_is_log=log_row, lr_step=lr_step)
                 return kl
-            return self._policy_kl(out[4], out[5], mb["mu"], mb["sigma"])
+            sig = torch.exp(out[5]).expand(out[4].shape[0], -1) if log_row else out[5]
+            return self._policy_kl(out[4], sig, mb["mu"], mb["sigma"])
 
     def _mb_finish(self, i, out, kl):
         """Phase 3 (after the KL all-reduce, which sums): dataset.update_mu_sigma, adaptive LR,
         diagnostics."""
         if self._fused_kl:
-            gae.adaptive_lr(kl, 1.0 / self.world_size if self.multi_gpu else 1.0, self.cfg.lr_schedule == "adaptive",
-                            self.cfg.kl_threshold, self.lr, self._opt_lr, self._stats_acc, out[0], out[1], out[2])
+            if self.multi_gpu:  # (single rank: done in the KL launch, _mb_step)
+                gae.adaptive_lr(kl, 1.0 / self.world_size, self.cfg.lr_schedule == "adaptive", self.cfg.kl_threshold,
+                                self.lr, self._opt_lr, self._stats_acc, out[0], out[1], out[2])
             return
         s = slice(i * self.cfg.minibatch_size, (i + 1) * self.cfg.minibatch_size)
         with torch.no_grad():

@@ -18,7 +18,8 @@ EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accu
                     "rl_ppo_loss", "rl_ppo_loss_backward", "rl_rms_normalize", "rl_opt_step", "rl_opt_partials_size",
                     "rl_linear_fwd", "rl_linear_transpose", "rl_linear_bwd", "rl_policy_head", "rl_linear_fwd_g",
                     "rl_linear_bwd_g", "rl_kl_partials_size", "rl_policy_kl", "rl_adaptive_lr",
-                    "rl_ppo_heads_partials_size", "rl_ppo_heads_loss", "rl_ppo_heads_loss_backward"]
+                    "rl_ppo_heads_partials_size", "rl_ppo_heads_loss", "rl_ppo_heads_loss_backward",
+                    "rl_splitk_accum_multi", "rl_policy_kl_step", "rl_opt_step_h", "rl_rms_normalize_h"]
 _lib = None
 
 
@@ -30,6 +31,15 @@ class LinearGroups(C.Structure):
     _fields_ = [("groups", C.c_int32), ("ldy", C.c_int32), ("lddx", C.c_int32), ("reserved", C.c_int32),
                 ("x_gstride", C.c_int64), ("w_gstride", C.c_int64), ("b_gstride", C.c_int64), ("y_gstride", C.c_int64),
                 ("dx_gstride", C.c_int64), ("part_gstride", C.c_int64), ("bpart_gstride", C.c_int64)]
+
+
+SPLITK_MAX_JOBS = 8  # include/gymrl.h RL_SPLITK_MAX_JOBS
+
+
+class SplitkJob(C.Structure):
+    """include/gymrl.h rl_splitk_job."""
+    _fields_ = [("parts", C.c_void_p), ("grad", C.c_void_p), ("n", C.c_int64), ("num_parts", C.c_int32),
+                ("parts_are_f16", C.c_int32)]
 
 
 class OptHyper(C.Structure):
@@ -85,10 +95,20 @@ def lib():
                                         C.c_double, vp, vp, vp, vp, vp, vp, vp, vp]
         L.rl_ppo_heads_loss_backward.restype = C.c_int
         L.rl_ppo_heads_loss_backward.argtypes = [vp, vp, vp, vp, vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, vp, vp,
-                                                 C.c_int32, C.c_int32, vp, vp, vp, vp, vp, vp, vp, vp]
+                                                 C.c_int32, C.c_int32, vp, vp, vp, vp, vp, vp, vp, C.c_int32, vp]
+        L.rl_splitk_accum_multi.restype = C.c_int
+        L.rl_splitk_accum_multi.argtypes = [C.POINTER(SplitkJob), C.c_int32, C.c_int32, vp]
+        L.rl_policy_kl_step.restype = C.c_int
+        L.rl_policy_kl_step.argtypes = [vp, C.c_int32, vp, C.c_int64, C.c_int32, vp, vp, C.c_int32, C.c_int32,
+                                        C.c_int32, vp, vp, C.c_int32, C.c_double, vp, vp, vp, vp, vp, vp, vp]
+        L.rl_opt_step_h.restype = C.c_int
+        L.rl_opt_step_h.argtypes = [vp, vp, vp, vp, vp, C.c_int64, vp, vp, vp, vp, C.POINTER(OptHyper), vp, vp]
+        L.rl_rms_normalize_h.restype = C.c_int
+        L.rl_rms_normalize_h.argtypes = [vp, C.c_int32, C.c_int32, vp, vp, vp, C.c_double, C.c_int32, vp, vp, vp]
         L.rl_kl_partials_size.restype = C.c_int
         L.rl_policy_kl.restype = C.c_int
-        L.rl_policy_kl.argtypes = [vp, C.c_int32, vp, C.c_int64, vp, vp, C.c_int32, C.c_int32, C.c_int32, vp, vp, vp]
+        L.rl_policy_kl.argtypes = [vp, C.c_int32, vp, C.c_int64, C.c_int32, vp, vp, C.c_int32, C.c_int32, C.c_int32, vp,
+                                   vp, vp]
         L.rl_adaptive_lr.restype = C.c_int
         L.rl_adaptive_lr.argtypes = [vp, C.c_float, C.c_int32, C.c_double, vp, vp, vp, vp, vp, vp, vp]
         L.rl_opt_step.restype = C.c_int
@@ -288,8 +308,10 @@ class HeadsSpec:
     the f32 gradient views the learner's flat buffers give them (direct gradients), the sigma parameter's gradient,
     and where the actor / critic outputs sit in the grouped MLP's [rows][G*H] output."""
 
-    def __init__(self, actor_col, critic_col, hidden, w_mu, b_mu, w_v, b_v, gw_mu, gb_mu, gw_v, gb_v, g_logstd):
+    def __init__(self, actor_col, critic_col, hidden, w_mu, b_mu, w_v, b_v, gw_mu, gb_mu, gw_v, gb_v, g_logstd,
+                 store: bool = False):
         self.actor_col, self.critic_col, self.hidden = int(actor_col), int(critic_col), int(hidden)
+        self.store = bool(store)  # gradients written (=), not added: the learner's zero-free flat buffer
         self.w_mu, self.b_mu, self.w_v, self.b_v = w_mu, b_mu, w_v, b_v
         self.gw_mu, self.gb_mu, self.gw_v, self.gb_v, self.g_logstd = gw_mu, gb_mu, gw_v, gb_v, g_logstd
         for t in (w_mu, b_mu, w_v, b_v):
@@ -337,6 +359,7 @@ class PpoHeadsLossFn(torch.autograd.Function):
                                        stats.data_ptr(), dls.data_ptr(), stream), "rl_ppo_heads_loss")
         ctx.save_for_backward(hidden, dmu, dv, dls, part)
         ctx.heads = heads
+        ctx.set_materialize_grads(False)  # stats / mu take no gradient: no zero tensors for them
         ctx.mark_non_differentiable(stats, mu)
         return loss, stats, mu
 
@@ -354,7 +377,7 @@ class PpoHeadsLossFn(torch.autograd.Function):
                                                 hd.hidden, hd.w_mu.data_ptr(), hd.w_v.data_ptr(), B, A, dh.data_ptr(),
                                                 part.data_ptr(), hd.gw_mu.data_ptr(), hd.gb_mu.data_ptr(),
                                                 hd.gw_v.data_ptr(), hd.gb_v.data_ptr(), hd.g_logstd.data_ptr(),
-                                                torch.cuda.current_stream(hidden.device).cuda_stream),
+                                                int(hd.store), torch.cuda.current_stream(hidden.device).cuda_stream),
                "rl_ppo_heads_loss_backward")
         return (dh,) + (None,) * 12
 
@@ -364,17 +387,19 @@ def rms_supported(x: torch.Tensor) -> bool:
         and x.shape[0] > 0
 
 
-def rms_normalize(x, running_mean, running_var, count, epsilon: float, update: bool) -> torch.Tensor:
+def rms_normalize(x, running_mean, running_var, count, epsilon: float, update: bool,
+                  out_half: bool = False) -> torch.Tensor:
     """RunningMeanStd forward (include/gymrl.h rl_rms_normalize): x f32 [N, C] (rms_supported), float64
     running_mean / running_var [C] and count 0-d updated in place when ``update``; returns y f32 [N, C]."""
     assert rms_supported(x)
     for t in (running_mean, running_var, count):
         assert t.dtype == torch.float64 and t.is_contiguous() and t.device == x.device
     N, Cc = x.shape
-    y = torch.empty_like(x)
+    y = torch.empty_like(x, dtype=torch.float16 if out_half else torch.float32)
     part = torch.empty(((N + 63) // 64) * Cc * 2, dtype=torch.float32, device=x.device) if update else None
     stream = torch.cuda.current_stream(x.device).cuda_stream
-    rc = lib().rl_rms_normalize(x.data_ptr(), N, Cc, running_mean.data_ptr(), running_var.data_ptr(),
+    fn = lib().rl_rms_normalize_h if out_half else lib().rl_rms_normalize
+    rc = fn(x.data_ptr(), N, Cc, running_mean.data_ptr(), running_var.data_ptr(),
                                 count.data_ptr(), float(epsilon), int(bool(update)),
                                 part.data_ptr() if part is not None else None, y.data_ptr(), stream)
     if rc != 0:
@@ -472,17 +497,30 @@ def linear_bwd_grouped(dy, y, ldy: int, y_gstride: int, M: int, N: int, x, ldx: 
                                  torch.cuda.current_stream().cuda_stream), "rl_linear_bwd_g")
 
 
-def policy_kl(mu_new, sigma_row, mu_old, sigma_old, kl_out, partials, write_back: bool = True) -> None:
+def policy_kl(mu_new, sigma_row, mu_old, sigma_old, kl_out, partials, write_back: bool = True,
+              sigma_is_log: bool = False, lr_step=None) -> None:
     """rl_policy_kl: kl_out (f32 0-d) = policy_kl(mu_new, sigma, mu_old, sigma_old) (rl_games torch_ext.policy_kl),
-    sigma_new one [A] row for all rows (fixed sigma) or [M, A]; write_back: mu_old / sigma_old (the dataset's
-    rows) receive the new values (dataset.update_mu_sigma)."""
+    sigma_new one [A] row for all rows (fixed sigma) or [M, A]; sigma_is_log: the row holds log sigma (the sigma
+    parameter); write_back: mu_old / sigma_old (the dataset's rows) receive the new values
+    (dataset.update_mu_sigma).  lr_step = (adaptive, kl_threshold, lr, opt_lr, stats, a_loss, c_loss, entropy):
+    the single-rank minibatch's scheduler step and meters in the same launch (rl_policy_kl_step)."""
     M, A = mu_new.shape
     assert mu_new.is_contiguous() and mu_old.is_contiguous() and sigma_old.is_contiguous()
     assert mu_old.dtype == torch.float32 and sigma_old.dtype == torch.float32 and sigma_row.dtype == torch.float32
     stride = 0 if sigma_row.dim() == 1 else sigma_row.stride(0)
-    _check(lib().rl_policy_kl(mu_new.data_ptr(), int(mu_new.dtype == torch.float16), sigma_row.data_ptr(), stride,
-                              mu_old.data_ptr(), sigma_old.data_ptr(), M, A, int(write_back), kl_out.data_ptr(),
-                              partials.data_ptr(), torch.cuda.current_stream().cuda_stream), "rl_policy_kl")
+    stream = torch.cuda.current_stream().cuda_stream
+    half = int(mu_new.dtype == torch.float16)
+    if lr_step is None:
+        _check(lib().rl_policy_kl(mu_new.data_ptr(), half, sigma_row.data_ptr(), stride, int(sigma_is_log),
+                                  mu_old.data_ptr(), sigma_old.data_ptr(), M, A, int(write_back), kl_out.data_ptr(),
+                                  partials.data_ptr(), stream), "rl_policy_kl")
+        return
+    adaptive, thr, lr, opt_lr, stats, a_loss, c_loss, entropy = lr_step
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    _check(lib().rl_policy_kl_step(mu_new.data_ptr(), half, sigma_row.data_ptr(), stride, int(sigma_is_log),
+                                   mu_old.data_ptr(), sigma_old.data_ptr(), M, A, int(write_back), kl_out.data_ptr(),
+                                   partials.data_ptr(), int(adaptive), float(thr), ptr(lr), ptr(opt_lr), ptr(stats),
+                                   ptr(a_loss), ptr(c_loss), ptr(entropy), stream), "rl_policy_kl_step")
 
 
 def adaptive_lr(kl, inv_world: float, adaptive: bool, kl_threshold: float, lr, opt_lr, stats, a_loss, c_loss,
@@ -493,3 +531,27 @@ def adaptive_lr(kl, inv_world: float, adaptive: bool, kl_threshold: float, lr, o
     _check(lib().rl_adaptive_lr(kl.data_ptr(), float(inv_world), int(adaptive), float(kl_threshold), ptr(lr),
                                 ptr(opt_lr), ptr(stats), ptr(a_loss), ptr(c_loss), ptr(entropy),
                                 torch.cuda.current_stream().cuda_stream), "rl_adaptive_lr")
+
+
+def splitk_accum_multi(jobs, store: bool = False) -> None:
+    """rl_splitk_accum_multi: [(parts [P, ...] f32 / fp16, grad f32)] finished in one launch (grad = / += sum)."""
+    assert 0 < len(jobs) <= SPLITK_MAX_JOBS
+    arr = (SplitkJob * len(jobs))()
+    for k, (parts, grad) in enumerate(jobs):
+        assert parts.is_contiguous() and grad.is_contiguous() and grad.dtype == torch.float32
+        assert parts.dtype in (torch.float16, torch.float32) and parts[0].numel() == grad.numel()
+        arr[k] = SplitkJob(parts.data_ptr(), grad.data_ptr(), grad.numel(), parts.shape[0],
+                           int(parts.dtype == torch.float16))
+    _check(lib().rl_splitk_accum_multi(arr, len(jobs), int(store), torch.cuda.current_stream().cuda_stream),
+           "rl_splitk_accum_multi")
+
+
+def opt_step_h(param, param_half, grad, exp_avg, exp_avg_sq, step, lr, scale, growth_tracker, hyper: OptHyper,
+               partials) -> None:
+    """rl_opt_step_h: opt_step that also writes the fp16 parameter shadow (two launches); partials zero-initialised."""
+    assert param_half.dtype == torch.float16 and param_half.numel() == param.numel()
+    _check(lib().rl_opt_step_h(param.data_ptr(), param_half.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(),
+                               exp_avg_sq.data_ptr(), param.numel(), step.data_ptr(), lr.data_ptr(),
+                               scale.data_ptr() if scale is not None else None,
+                               growth_tracker.data_ptr() if growth_tracker is not None else None, C.byref(hyper),
+                               partials.data_ptr(), torch.cuda.current_stream().cuda_stream), "rl_opt_step_h")

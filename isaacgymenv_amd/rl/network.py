@@ -277,6 +277,7 @@ class _GroupedMLPFn(torch.autograd.Function):
             inp = y
         ctx.save_for_backward(xc, *ys)
         ctx.spec = spec
+        ctx.stacked = stacked
         n_last = spec.layers[-1][0]
         if stacked:  # the [M][G*N] output itself (PpoHeadsLossFn reads both groups' columns from it)
             return ys[-1]
@@ -294,6 +295,7 @@ class _GroupedMLPFn(torch.autograd.Function):
         else:
             dy = torch.cat([(g if g is not None else torch.zeros(M, n_last, device=xc.device)).to(torch.float16)
                             for g in gouts], dim=1)
+        jobs = []
         for l in reversed(range(len(spec.layers))):
             N, K, wh, _, span = spec.layers[l]
             # the per-network path's row blocks (network._LinearELUFn): the same fixed-order partial sums
@@ -306,7 +308,10 @@ class _GroupedMLPFn(torch.autograd.Function):
                 gae.linear_bwd_grouped(dy, ys[l], G * N, N, M, N, ys[l - 1], G * K, K, K, wh, N * K, dx, G * K, K,
                                        splits, part, part[:, G * N * K:], G * (N * K + N), N * K, N, G)
                 dy = dx
-            gae.splitk_accum(part, span)
+            jobs.append((part, span))
+        # every layer's weight / bias gradients finished in one launch; the stacked form (the learner's fused heads
+        # path, which writes every gradient exactly once) stores them into the unzeroed flat buffer
+        gae.splitk_accum_multi(jobs, store=ctx.stacked)
         return (None, None, None) + (None,) * len(spec.params)
 
 
@@ -390,7 +395,9 @@ class ActorCriticNetwork(nn.Module):
     def stacked_hidden(self, obs):
         """The grouped actor / critic output as one fp16 [rows][2 * H] tensor (actor columns first) and the heads'
         spec for gae.PpoHeadsLossFn, or None where the grouped MFMA path does not apply (fp16 autocast, learner
-        layout, fixed sigma, heads' fp16 shadows and flat gradient views bound)."""
+        layout, fixed sigma, heads' fp16 shadows and flat gradient views bound).  The backward of this form STORES
+        the MLP, head and sigma gradients into their flat-buffer views (each written once): the learner skips
+        zeroing the buffer."""
         if not (self.separate and self.fixed_sigma and self.grouped is not None and self.grouped.G == 2
                 and self.grouped.applies(obs)):
             return None
@@ -401,7 +408,7 @@ class ActorCriticNetwork(nn.Module):
             return None
         H = mu.in_features
         heads = gae.HeadsSpec(0, H, H, mu.half_weight, mu.half_bias, val.half_weight, val.half_bias, mu.weight.grad,
-                              mu.bias.grad, val.weight.grad, val.bias.grad, self.sigma.grad)
+                              mu.bias.grad, val.weight.grad, val.bias.grad, self.sigma.grad, store=True)
         return _GroupedMLPFn.apply(obs, self.grouped, True, *self.grouped.params), heads
 
     def forward(self, obs):
@@ -429,6 +436,14 @@ class ModelA2CContinuousLogStd(nn.Module):
     def norm_obs(self, obs):
         with torch.no_grad():
             return self.running_mean_std(obs) if self.normalize_input else obs
+
+    def norm_obs_half(self, obs):
+        """norm_obs rounded to fp16 -- the operand the first fp16 layer casts it to -- written by the normalisation
+        pass itself where the device path applies (rl_rms_normalize_h)."""
+        with torch.no_grad():
+            if self.normalize_input:
+                return self.running_mean_std.forward_half(obs)
+            return obs.to(torch.float16)
 
     def denorm_value(self, value):
         with torch.no_grad():

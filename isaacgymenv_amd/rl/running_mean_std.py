@@ -34,6 +34,13 @@ class RunningMeanStd(nn.Module):
         new_var = m2 / tot_count
         return new_mean, new_var, tot_count
 
+    def forward_half(self, input):
+        """forward(input) rounded to fp16 (train or eval mode as forward)."""
+        if not self.norm_only and gae.rms_supported(input):
+            return gae.rms_normalize(input, self.running_mean, self.running_var, self.count, self.epsilon,
+                                     update=self.training, out_half=True)
+        return self.forward(input).to(torch.float16)
+
     def forward(self, input, unnorm: bool = False):
         if not unnorm and not self.norm_only and gae.rms_supported(input):
             # device path: the moment update and the normalisation as one HIP pass (rl_rms_normalize)

@@ -303,6 +303,8 @@ def test_fused_ppo_loss_matches_torch_loss():
             assert torch.equal(m0, m1)
         else:  # the fused heads' fp32 dot products in another order: within one fp16 ulp
             assert float((m1 - m0).abs().max()) <= 2e-3 * max(1.0, float(m0.abs().max()))
+        if s1.dim() == 1:  # the fused heads path hands over log sigma
+            s1 = torch.exp(s1).expand_as(s0)
         assert torch.allclose(s0, s1)
         scale = float(g0.abs().max())
         assert scale > 0 and float((g1 - g0).abs().max()) <= 1e-2 * scale, (mode, float((g1 - g0).abs().max()), scale)
@@ -858,3 +860,111 @@ def test_fused_heads_loss_matches_torch_heads_and_loss():
         assert float(ref.abs().max()) > 0, n
         err = float((got - ref).abs().max())
         assert err <= 1e-2 * float(ref.abs().max()) + 1e-6, (n, err, float(ref.abs().max()))
+
+
+def test_policy_kl_step_matches_separate_launches():
+    """rl_policy_kl_step (KL + scheduler + meters in one launch, last workgroup finishes) against rl_policy_kl +
+    rl_adaptive_lr: kl, lr, the optimizer lr, the meters and the written-back dataset rows bit-identical; the log-sigma
+    row (sigma_is_log) against the exp'd row; repeated launches (the counter resets)."""
+    from isaacgymenv_amd.rl import gae
+    M, A = 16384, 12
+    g = torch.Generator(device="cuda").manual_seed(4)
+    mu_new = torch.randn(M, A, device="cuda", generator=g).half()
+    logstd = 0.2 * torch.randn(A, device="cuda", generator=g)
+    mu_old = mu_new.float() + 0.05 * torch.randn(M, A, device="cuda", generator=g)
+    sg_old = torch.exp(logstd).expand(M, -1) * torch.exp(0.02 * torch.randn(M, A, device="cuda", generator=g))
+    res = {}
+    for fused in (False, True):
+        part = torch.zeros(gae.lib().rl_kl_partials_size(), device="cuda")
+        lr = torch.tensor(3e-4, dtype=torch.float64, device="cuda")
+        opt_lr = torch.tensor(3e-4, device="cuda")
+        stats = torch.zeros(4, device="cuda")
+        losses = torch.tensor([0.25, 0.5, 0.125], device="cuda")
+        mo, so = mu_old.clone(), sg_old.clone()
+        kls = []
+        for rep in range(3):
+            kl = torch.empty((), device="cuda")
+            if fused:
+                gae.policy_kl(mu_new, logstd, mo, so, kl, part, write_back=rep == 0, sigma_is_log=True,
+                              lr_step=(True, 0.008, lr, opt_lr, stats, losses[0], losses[1], losses[2]))
+            else:
+                gae.policy_kl(mu_new, torch.exp(logstd), mo, so, kl, part, write_back=rep == 0)
+                gae.adaptive_lr(kl, 1.0, True, 0.008, lr, opt_lr, stats, losses[0], losses[1], losses[2])
+            kls.append(kl.clone())
+        res[fused] = (torch.stack(kls), lr.clone(), opt_lr.clone(), stats.clone(), mo, so)
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
+
+
+def test_opt_step_h_matches_opt_step_and_writes_the_shadow():
+    """rl_opt_step_h (shadow write, finish in the Adam launch's last workgroup) against rl_opt_step over several
+    steps incl. a non-finite gradient (skipped, scale backed off) and a growth step: parameters, moments, step, scale,
+    tracker bit-identical; the shadow equals the parameters rounded to fp16."""
+    from isaacgymenv_amd.rl import gae
+    n = 300001
+    g = torch.Generator(device="cuda").manual_seed(8)
+    p0 = torch.randn(n, device="cuda", generator=g)
+    grads = [torch.randn(n, device="cuda", generator=g) * 100.0 for _ in range(5)]
+    grads[2][17] = float("inf")
+    hyper = gae.OptHyper(1.0, 0.9, 0.999, 1e-8, 0.0, 0.5, 2.0, 2)
+    res = {}
+    for h in (False, True):
+        p, m, v = p0.clone(), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+        half = torch.zeros(n, dtype=torch.float16, device="cuda")
+        step, lr = torch.zeros((), device="cuda"), torch.tensor(3e-4, device="cuda")
+        scale, tracker = torch.tensor([128.0], device="cuda"), torch.zeros(1, dtype=torch.int32, device="cuda")
+        part = torch.zeros(gae.lib().rl_opt_partials_size(), device="cuda")
+        for gr in grads:
+            if h:
+                gae.opt_step_h(p, half, gr, m, v, step, lr, scale, tracker, hyper, part)
+            else:
+                gae.opt_step(p, gr, m, v, step, lr, scale, tracker, hyper, part)
+        res[h] = (p, m, v, step, scale, tracker, half)
+    for a, b in zip(res[False][:6], res[True][:6]):
+        assert torch.equal(a, b)
+    assert float(res[True][3]) == 4.0 and float(res[True][4]) == 256.0  # grow, skip (back off), grow
+    assert torch.equal(res[True][6], res[True][0].half())
+
+
+def test_splitk_accum_multi_matches_per_layer_finishes():
+    """rl_splitk_accum_multi: three layers' partials (incl. an unaligned span, an fp16 job) in one launch against
+    rl_splitk_accum per layer -- bit-identical; store mode writes the sums into garbage-filled gradients."""
+    from isaacgymenv_amd.rl import gae
+    g = torch.Generator(device="cuda").manual_seed(2)
+    shapes = [(16, 96256 + 1024), (8, 131072 + 512), (4, 32768 + 257)]
+    parts = [torch.randn(P, n, device="cuda", generator=g) for P, n in shapes]
+    parts[1] = parts[1].half()
+    flat = torch.randn(sum(n for _, n in shapes) + 1, device="cuda", generator=g)
+    spans, o = [], 1  # offset 1: the first span is not 16-byte aligned
+    for _, n in shapes:
+        spans.append((o, n))
+        o += n
+    ref = flat.clone()
+    for pt, (o, n) in zip(parts, spans):
+        gae.splitk_accum(pt, ref[o:o + n])
+    got = flat.clone()
+    gae.splitk_accum_multi([(pt, got[o:o + n]) for pt, (o, n) in zip(parts, spans)])
+    assert torch.equal(got, ref)
+    stored = torch.full_like(flat, float("nan"))
+    gae.splitk_accum_multi([(pt, stored[o:o + n]) for pt, (o, n) in zip(parts, spans)], store=True)
+    zero = torch.zeros_like(flat)
+    for pt, (o, n) in zip(parts, spans):
+        gae.splitk_accum(pt, zero[o:o + n])
+    assert torch.equal(stored[1:], zero[1:])
+
+
+def test_rms_normalize_half_output_is_the_rounded_f32_output():
+    """rl_rms_normalize_h: the same normalisation (and running-moment update) as rl_rms_normalize, y rounded to fp16."""
+    from isaacgymenv_amd.rl import gae
+    x = torch.randn(16384, 188, device="cuda") * 3.0 + 1.0
+    outs = []
+    for half in (False, True):
+        mean = torch.zeros(188, dtype=torch.float64, device="cuda")
+        var = torch.ones(188, dtype=torch.float64, device="cuda")
+        count = torch.tensor(1e-4, dtype=torch.float64, device="cuda")
+        y = gae.rms_normalize(x, mean, var, count, 1e-5, True, out_half=half)
+        outs.append((y, mean, var, count))
+    (y0, *m0), (y1, *m1) = outs
+    assert y1.dtype == torch.float16 and torch.equal(y1, y0.half())
+    for a, b in zip(m0, m1):
+        assert torch.equal(a, b)
