@@ -137,14 +137,12 @@ __global__ __launch_bounds__(kThreads) void k_opt_adam(float* __restrict__ param
     }
   }
   if (!counter) return;
-  __syncthreads();  // every lane of the workgroup has read step / scale
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(counter, 1u) == gridDim.x - 1;
-  }
+  // nothing is handed over (each workgroup has its own found / norm): the counter only orders the last
+  // workgroup's step / scale update after every workgroup's reads of them, which completed before its add
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(counter, 1u) == gridDim.x - 1;
   __syncthreads();
   if (last && threadIdx.x == 0) {
-    __threadfence();
     opt_finish(step, scale, tracker, found, h);
     *counter = 0u;  // ready for the next launch
   }

@@ -57,6 +57,61 @@ __device__ __forceinline__ h8 load8(const _Float16* __restrict__ p, int valid) {
   return v;
 }
 
+// XCD-aware tile order (MI355X_MICROARCH.md, workgroup dispatch: blocks are dealt round-robin over the 8 XCDs):
+// the 1-D grid's block b is renumbered so that each XCD takes a contiguous run of the row-major (group, m, n) tile
+// order -- n fastest: the blocks resident on an XCD at once cover whole rows of the output (full-line, page-local
+// writes) and share their A row tiles in that XCD's L2.  Bijective for any tile count.
+__device__ __forceinline__ void tile_of(int MT, int NT, int& g, int& mt, int& nt) {
+  const int T = gridDim.x, id = blockIdx.x, q = T / 8, r = T % 8, xcd = id % 8;
+  const int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + id / 8;
+  g = w / (MT * NT);
+  const int rem = w - g * (MT * NT);
+  mt = rem / NT;
+  nt = rem - mt * NT;
+}
+
+// The output tile through LDS: a lane's fp16 results (4 consecutive columns of one row per register group) are
+// written to `stage` ([BM][BN + 8] halves, the K loop's buffers reused), then the workgroup stores whole rows with
+// 16-byte stores -- each wave store a contiguous 1 KB of 4 rows.  Stored straight from the registers (8-byte
+// stores, 32 rows apart per wave instruction) the 32 MB of the first layer's output went out at ~1 TB/s.
+// o(j, i, g) gives the 4 halves of register group g of fragment (j, i).  Falls back to the direct stores when C
+// or its row stride is not 16-byte aligned.
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+template <int BM, int BN, class F>
+__device__ __forceinline__ void store_tile(_Float16* __restrict__ stage, _Float16* __restrict__ C, int ldc, int m0,
+                                           int c0, int wm, int wn, int r, int hh, F&& o) {
+  constexpr int TM = BM / 64, TN = BN / 64, SLD = BN + 8;
+  if (((reinterpret_cast<uintptr_t>(C) | (uintptr_t)(ldc * 2)) & 15) != 0) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int m = m0 + wm * (BM / 2) + i * 32 + r, cg = c0 + wn * (BN / 2) + j * 32 + 8 * g + 4 * hh;
+          *reinterpret_cast<h4*>(C + (size_t)m * ldc + cg) = o(j, i, g);
+        }
+    return;
+  }
+  __syncthreads();  // every wave is done with the K loop's buffers
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int ml = wm * (BM / 2) + i * 32 + r, cl = wn * (BN / 2) + j * 32 + 8 * g + 4 * hh;
+        *reinterpret_cast<h4*>(stage + ml * SLD + cl) = o(j, i, g);
+      }
+  __syncthreads();
+  constexpr int CPR = BN / 8, IT = BM * CPR / kThreads;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int c = threadIdx.x + it * kThreads, row = c / CPR, cc = (c % CPR) * 8;
+    *reinterpret_cast<uint4*>(C + (size_t)(m0 + row) * ldc + c0 + cc) = *reinterpret_cast<const uint4*>(stage + row * SLD + cc);
+  }
+}
+
 // ---------------------------------------------------------------- NT: C[m][c] = sum_r A[m][r] Bt[c][r]
 // ACT: ELU epilogue.  bias: fp16 [C] or null.  C fp16 [M][ldc].  M % BM == 0, Cn % BN == 0 (host).  The MFMA takes the Bt tile as its row operand,
 // so a lane's result registers 4g .. 4g+3 are 4 consecutive columns c of one row m: one 8-byte store each.
@@ -67,9 +122,11 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(const _Float16* __restrict
                                                       int lda, const _Float16* __restrict__ Bt, int ldb,
                                                       const _Float16* __restrict__ bias, _Float16* __restrict__ C,
                                                       int ldc, int R, int64_t gA, int64_t gB, int64_t gBias,
-                                                      int64_t gC) {
+                                                      int64_t gC, int MT, int NT) {
+  int gi, mt, nt;
+  tile_of(MT, NT, gi, mt, nt);
   {
-    const int64_t g = blockIdx.z;
+    const int64_t g = gi;
     A += g * gA;
     Bt += g * gB;
     if (bias) bias += g * gBias;
@@ -83,7 +140,7 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(const _Float16* __restrict
   __shared__ _Float16 sB[2][BN * LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.x * BM, c0 = blockIdx.y * BN;
+  const int m0 = mt * BM, c0 = nt * BN;
   const int r = lane & 31, hh = lane >> 5;
   f16v acc[TN][TM];
 #pragma unroll
@@ -93,6 +150,16 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(const _Float16* __restrict
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[j][i][q] = 0.f;
 
+  // the bias of this lane's output columns, loaded before the K loop (its latency hides there): columns
+  // c0 + wn BN/2 + 32 j + 8 g + 4 hh + e
+  float bcol[TN][4][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        bcol[j][g][e] = bias ? (float)bias[c0 + wn * (BN / 2) + j * 32 + 8 * g + 4 * hh + e] : 0.f;
   h8 ra[CA], rb[CB];
   auto gload = [&](int k0) {
 #pragma unroll
@@ -145,32 +212,17 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(const _Float16* __restrict
     __syncthreads();
   }
   // epilogue: + bias, ELU, one rounding to fp16; registers 4g .. 4g+3 -> columns cg .. cg+3 of row m
+  static_assert(BM * (BN + 8) <= 2 * BM * LD, "the output stage fits the A buffers");
+  store_tile<BM, BN>(&sA[0][0], C, ldc, m0, c0, wm, wn, r, hh, [&](int j, int i, int g) {
+    h4 ov;
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int cg = c0 + wn * (BN / 2) + j * 32 + 8 * g + 4 * hh;
-      float bv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (bias) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bv[e] = (float)bias[cg + e];
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int m = m0 + wm * (BM / 2) + i * 32 + r;
-        _Float16 o[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float z = acc[j][i][4 * g + e] + bv[e];
-          if constexpr (ACT) z = elu_f(z);
-          o[e] = (_Float16)z;
-        }
-        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-        const h4 ov = {o[0], o[1], o[2], o[3]};
-        *reinterpret_cast<h4*>(C + (size_t)m * ldc + cg) = ov;
-      }
+    for (int e = 0; e < 4; ++e) {
+      float z = acc[j][i][4 * g + e] + bcol[j][g][e];
+      if constexpr (ACT) z = elu_f(z);
+      ov[e] = (_Float16)z;
     }
-  }
+    return ov;
+  });
 }
 
 // ---------------------------------------------------------------- TN: weight / bias gradient partials
@@ -326,9 +378,11 @@ template <int BM>
 __global__ __launch_bounds__(kThreads) void k_gemm_nn(const _Float16* __restrict__ dY, const _Float16* __restrict__ Y,
                                                       int N, int ldy, const _Float16* __restrict__ W, int K,
                                                       _Float16* __restrict__ dX, int lddx, int64_t gY, int64_t gW,
-                                                      int64_t gDX) {
+                                                      int64_t gDX, int MT, int NT) {
+  int gi, mt, nt;
+  tile_of(MT, NT, gi, mt, nt);
   {
-    const int64_t g = blockIdx.z;
+    const int64_t g = gi;
     dY += g * gY;
     Y += g * gY;
     W += g * gW;
@@ -341,7 +395,7 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nn(const _Float16* __restrict
   __shared__ _Float16 sB[2][KS * kTLd];   // [n][k]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.x * BM, c0 = blockIdx.y * BN;
+  const int m0 = mt * BM, c0 = nt * BN;
   const int r = lane & 31, hh = lane >> 5;
   f16v acc[TN][TM];
 #pragma unroll
@@ -412,20 +466,13 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nn(const _Float16* __restrict
     }
     __syncthreads();
   }
-  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int cg = c0 + wn * (BN / 2) + j * 32 + 8 * g + 4 * hh;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int m = m0 + wm * (BM / 2) + i * 32 + r;
-        const h4 ov = {(_Float16)acc[j][i][4 * g], (_Float16)acc[j][i][4 * g + 1], (_Float16)acc[j][i][4 * g + 2],
-                       (_Float16)acc[j][i][4 * g + 3]};
-        *reinterpret_cast<h4*>(dX + (size_t)m * lddx + cg) = ov;
-      }
-    }
+  static_assert(BM * (BN + 8) <= 2 * BM * LD, "the output stage fits the A buffers");
+  store_tile<BM, BN>(&sA[0][0], dX, lddx, m0, c0, wm, wn, r, hh,
+                     [&](int j, int i, int g) {
+                       const h4 ov = {(_Float16)acc[j][i][4 * g], (_Float16)acc[j][i][4 * g + 1],
+                                      (_Float16)acc[j][i][4 * g + 2], (_Float16)acc[j][i][4 * g + 3]};
+                       return ov;
+                     });
 }
 
 // W [N][K] fp16 -> W^T [K][N] fp16 (32 x 32 tiles through LDS)
@@ -477,13 +524,15 @@ extern "C" int rl_linear_fwd_g(const void* x, int32_t M, int32_t K, int32_t ldx,
   auto* Y = static_cast<_Float16*>(y);
   // 128 x 128 tiles when that still gives >= 256 workgroups (over all groups), else 64-row tiles
   if ((M / 128) * (N / 128) * G >= 256 && M % 128 == 0) {
-    const dim3 g(M / 128, N / 128, G);
-    if (act) hipLaunchKernelGGL((k_gemm_nt<128, 128, true>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, ldy, K, gx, gw, gb, gy);
-    else hipLaunchKernelGGL((k_gemm_nt<128, 128, false>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, ldy, K, gx, gw, gb, gy);
+    const int MT = M / 128, NT = N / 128;
+    const dim3 g(MT * NT * G);
+    if (act) hipLaunchKernelGGL((k_gemm_nt<128, 128, true>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, ldy, K, gx, gw, gb, gy, MT, NT);
+    else hipLaunchKernelGGL((k_gemm_nt<128, 128, false>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, ldy, K, gx, gw, gb, gy, MT, NT);
   } else {
-    const dim3 g(M / 64, N / 128, G);
-    if (act) hipLaunchKernelGGL((k_gemm_nt<64, 128, true>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, ldy, K, gx, gw, gb, gy);
-    else hipLaunchKernelGGL((k_gemm_nt<64, 128, false>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, ldy, K, gx, gw, gb, gy);
+    const int MT = M / 64, NT = N / 128;
+    const dim3 g(MT * NT * G);
+    if (act) hipLaunchKernelGGL((k_gemm_nt<64, 128, true>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, ldy, K, gx, gw, gb, gy, MT, NT);
+    else hipLaunchKernelGGL((k_gemm_nt<64, 128, false>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, ldy, K, gx, gw, gb, gy, MT, NT);
   }
   return launch_fail("rl_linear_fwd");
 }
@@ -527,11 +576,11 @@ extern "C" int rl_linear_bwd_g(const void* dy, const void* y, int32_t M, int32_t
     const auto* Wp = static_cast<const _Float16*>(w);
     auto* DX = static_cast<_Float16*>(dx);
     if ((M / 128) * (K / 128) * G >= 256)
-      hipLaunchKernelGGL((k_gemm_nn<128>), dim3(M / 128, K / 128, G), dim3(kThreads), 0, st, DY, Yv, N, ldy, Wp, K, DX,
-                         lddx, gy, gw, gdx);
+      hipLaunchKernelGGL((k_gemm_nn<128>), dim3((M / 128) * (K / 128) * G), dim3(kThreads), 0, st, DY, Yv, N, ldy, Wp,
+                         K, DX, lddx, gy, gw, gdx, M / 128, K / 128);
     else
-      hipLaunchKernelGGL((k_gemm_nn<64>), dim3(M / 64, K / 128, G), dim3(kThreads), 0, st, DY, Yv, N, ldy, Wp, K, DX,
-                         lddx, gy, gw, gdx);
+      hipLaunchKernelGGL((k_gemm_nn<64>), dim3((M / 64) * (K / 128) * G), dim3(kThreads), 0, st, DY, Yv, N, ldy, Wp,
+                         K, DX, lddx, gy, gw, gdx, M / 64, K / 128);
     if (int rc = launch_fail("rl_linear_bwd (dX)")) return rc;
   }
   if (wpart) {

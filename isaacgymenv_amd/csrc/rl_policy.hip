@@ -100,14 +100,21 @@ __global__ __launch_bounds__(kThreads) void k_kl_part(const void* __restrict__ m
     if (threadIdx.x == 0) part[blockIdx.x] = total;
     return;
   }
+  // the hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): the partial stored, waited for, released at agent
+  // scope, then the agent-scope counter add; the last workgroup acquires before anyone of it loads the partials
   if (threadIdx.x == 0) {
     part[blockIdx.x] = total;
-    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     last = atomicAdd(L.counter, 1u) == (unsigned)(gridDim.x - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   __syncthreads();
   if (!last) return;
-  __threadfence();
   sh[threadIdx.x] = threadIdx.x < kBlocks ? part[threadIdx.x] : 0.f;
   __syncthreads();
   const float k = tree_sum(sh) / (float)M;
