@@ -1017,6 +1017,9 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     const unsigned long long below = (1ull << wl) - 1ull;
     int slot[NQ];
     int cnt = 0;
+#ifdef GS_PHASE_PROFILE
+    const long long tq0 = clock64();
+#endif
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const bool need = qv[q] && gs_terrain::may_contact(P.terr, qc[q], qr[q], qr[q] + P.contact_offset);
@@ -1029,6 +1032,9 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       cnt += __popcll(bal);
     }
     __syncthreads();
+#ifdef GS_PHASE_PROFILE
+    const long long tq1 = clock64();
+#endif
     // (the live lanes only: the lanes of envs past N left the kernel before the substep loop)
     const unsigned long long live = __ballot(true);
     const int nlive = __popcll(live);
@@ -1043,6 +1049,14 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       it[6] = nt[0]; it[7] = nt[1]; it[8] = nt[2];
     }
     __syncthreads();
+#ifdef GS_PHASE_PROFILE
+    if ((threadIdx.x & 63) == 0) {  // mesh query phases: [50] the may_contact culls, [51] the scans, [52] queries
+      const long long tq2 = clock64();
+      atomicAdd(&gs_phase_cycles[50], (unsigned long long)(tq1 - tq0));
+      atomicAdd(&gs_phase_cycles[51], (unsigned long long)(tq2 - tq1));
+      atomicAdd(&gs_phase_cycles[52], (unsigned long long)cnt);
+    }
+#endif
     // terrain_candidate's result: the deepest of the ground plane and the mesh surface
     float rd = 3.0e38f, rn[3] = {0.f, 0.f, 1.f}, rm = P.ground_mu;
 #pragma unroll

@@ -123,7 +123,8 @@ typedef struct {
     const float *tverts;
     double tx0, ty0, ths;
     double terrain_friction;
-    /* physx.solver_type (cfg/config.yaml:31): 0 PGS (the kernels' solver), 1 TGS -- oracle only, the study of
+    /* physx.solver_type (cfg/config.yaml:31): 0 PGS (the kernels' solver), 1 TGS, 2 TGS with the joint velocity
+     * limit applied in each position sub-step -- 1 and 2 oracle only, the study of
      * pos_iters sub-steps of h / pos_iters, each row's separation advanced by the displacement
      * integrated so far, positions integrated with the sub-steps' velocities, no bias in the velocity phase */
     int32_t solver_type;
@@ -1155,7 +1156,16 @@ static void env_substep(const OModel *m, const OParams *p, real h,
     const int iters = p->pos_iters + p->vel_iters;
     /* TGS (solver_type 1): displacement dq integrated over the position sub-steps of length hs; a row's
      * separation is advanced by J dq (linearised), its target is set for the sub-step */
-    const int tgs = p->solver_type == 1 && p->pos_iters > 0;
+    const int tgs = p->solver_type >= 1 && p->solver_type <= 3 && p->pos_iters > 0;
+    /* solver_type 3 (round 5): TGS whose position sub-steps push a penetration out at -s / h (the whole step, as
+     * PGS) instead of -s / hs: the sub-steps share the push-out rather than each demanding all of it */
+    const real hpush = p->solver_type == 3 ? h : (p->solver_type >= 1 && p->pos_iters > 0 ? h / p->pos_iters : h);
+    /* solver_type 2 (round 5): TGS whose position sub-steps integrate the joint velocities
+     * clamped to the joint velocity limits (PhysX applies maxJointVelocity in every TGS sub-step integration):
+     * a row's linearised separation then advances by the displacement the clamped joints actually deliver, so
+     * a sub-step push-out target the limit cannot meet is not counted as met (the round-4 divergence:
+     * profiles/r04_tgs_divergence.txt) */
+    const int tgs_clamp = p->solver_type == 2;
     const real hs = tgs ? h / p->pos_iters : h;
     real dxs[MAXV];
     for (int k = 0; k < nv; ++k) dxs[k] = 0;
@@ -1167,7 +1177,7 @@ static void env_substep(const OModel *m, const OParams *p, real h,
             const real u = lsgn[a] * v[nbase + ldof[a]];
             real target;
             if (s >= 0) target = -s / hd;
-            else if (pos_phase) { target = -s / hs; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
+            else if (pos_phase) { target = -s / hpush; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
             else target = 0;
             real ln = laml[a] + (target - u) / LD[a];
             if (ln < 0) ln = 0;
@@ -1187,7 +1197,7 @@ static void env_substep(const OModel *m, const OParams *p, real h,
                 if (tgs) for (int k = 0; k < nv; ++k) s += Jr[k] * dxs[k];
                 real target;
                 if (s >= 0) target = -s / hd;
-                else if (pos_phase) { target = -s / hs; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
+                else if (pos_phase) { target = -s / hpush; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
                 else target = 0;
                 real ln = Dr[r] > 0 ? lam[r] + (target - u) / Dr[r] : lam[r]; /* ground rows: no response cutoff; Dr == 0: a
                                                                                   * row the articulation cannot move along */
@@ -1222,7 +1232,7 @@ static void env_substep(const OModel *m, const OParams *p, real h,
                     if (tgs) for (int k = 0; k < nv; ++k) s += Jr[k] * dxs[k];
                     real target;
                     if (s >= 0) target = -s / hd;
-                    else if (pos_phase) { target = -s / hs; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
+                    else if (pos_phase) { target = -s / hpush; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
                     else target = 0;
                     ln = PD[r] > MIN_RESPONSE ? plam[r] + (target - u) / PD[r] : plam[r];
                     if (ln < 0) ln = 0;
@@ -1237,7 +1247,18 @@ static void env_substep(const OModel *m, const OParams *p, real h,
                 for (int k = 0; k < nv; ++k) v[k] += Wr[k] * dl;
             }
         }
-        if (tgs && pos_phase) for (int k = 0; k < nv; ++k) dxs[k] += hs * v[k];
+        if (tgs && pos_phase) {
+            if (tgs_clamp)
+                for (int j = 0; j < nd; ++j) {
+                    const real vm = (real)m->vmax[j];
+                    if (vm > 0) {
+                        real *a = &v[nbase + j];
+                        if (*a > vm) *a = vm;
+                        if (*a < -vm) *a = -vm;
+                    }
+                }
+            for (int k = 0; k < nv; ++k) dxs[k] += hs * v[k];
+        }
         if (it == p->pos_iters - 1) {
             if (tgs) for (int k = 0; k < nv; ++k) nupos[k] = dxs[k] / h;  /* h * nupos = the sub-steps' displacement */
             else memcpy(nupos, v, sizeof(real) * nv);

@@ -65,6 +65,10 @@ def main():
             if not name.startswith("("):
                 print(f"  {name:36s} {buf[32 + i] / ns:10.0f}")
         print(f"  PGS chain contacts per slow wave: {buf[32 + 8] / ns:.1f}")
+    if a.trimesh:
+        w = a.steps * waves
+        print(f"mesh queries (inside the forward pass): may_contact culls {buf[50] / w:.0f} cycles per wave per launch, "
+              f"the scans {buf[51] / w:.0f}; queries scanned per wave per substep {buf[52] / (w * substeps):.1f}")
     if buf[12]:
         print(f"self-collision narrowphase cycles per entry: {buf[13] / buf[12]:.0f}, of which the near pairs' "
               f"contacts in their lanes {buf[14] / buf[12]:.0f} (the rest: ranking, staging, pool entries); lanes of "

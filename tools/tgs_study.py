@@ -1,7 +1,8 @@
 """PGS vs TGS on the fp64 oracle.
 
 The reference configs ask PhysX for TGS (`solver_type: 1`, cfg/config.yaml:31); the MI355X kernels run PGS
-with split impulse.  The oracle (oracle/physics_oracle.c) has both: solver_type 0 is the kernels' PGS, 1 is
+with split impulse.  The oracle (oracle/physics_oracle.c) has both: solver_type 0 is the kernels' PGS, 1 (and 2: the
+joint velocity limit applied in every position sub-step, round 5) is
 TGS restated -- num_position_iterations sub-steps of h / n, each row's separation advanced by the displacement
 integrated so far (linearised, J dq), positions integrated with the sub-steps' velocities, no bias in the
 velocity iterations.  This script runs AnymalTerrain's physics (plane, the task's PD at 4 x decimation + 1
@@ -104,7 +105,7 @@ def main():
         acts = np.zeros((a.steps, a.envs, 12)) if scen == "standing" else rng.uniform(-1, 1, (a.steps, a.envs, 12))
         res = {}
         trajs = {}
-        for name, st in (("pgs", 0), ("tgs", 1)):
+        for name, st in (("pgs", 0), ("tgs", 1), ("tgs_substep_vlimit", 2), ("tgs_step_pushout", 3)):
             p = dict(base, solver_type=st)
             traj, info = rollout(flat, p, root, dof, mu, default, acts, a.threads)
             trajs[name] = traj
@@ -120,9 +121,13 @@ def main():
         traj_p, _ = rollout(flat, dict(base, solver_type=0), pr, dof, mu, default, acts, a.threads)
         sep = lambda x, y: np.linalg.norm(x[:, :, :3] - y[:, :, :3], axis=2).mean(axis=1)  # noqa: E731
         d_solver = sep(trajs["pgs"], trajs["tgs"])
+        d_solver2 = sep(trajs["pgs"], trajs["tgs_substep_vlimit"])
+        d_solver3 = sep(trajs["pgs"], trajs["tgs_step_pushout"])
         d_chaos = sep(trajs["pgs"], traj_p)
         marks = sorted(k for k in {0, 4, 19, a.steps // 2, a.steps - 1} if k < a.steps)
         res["pgs_vs_tgs_base_pos_sep_m"] = {str(k + 1): float(d_solver[k]) for k in marks}
+        res["pgs_vs_tgs_substep_vlimit_base_pos_sep_m"] = {str(k + 1): float(d_solver2[k]) for k in marks}
+        res["pgs_vs_tgs_step_pushout_base_pos_sep_m"] = {str(k + 1): float(d_solver3[k]) for k in marks}
         res["pgs_vs_perturbed_pgs_sep_m"] = {str(k + 1): float(d_chaos[k]) for k in marks}
         out[scen] = res
         print(scen, json.dumps(res, indent=1))
