@@ -80,6 +80,8 @@ def parse():
                     help="timed steps of each other BASELINE config (Ant, trimesh AnymalTerrain, UsefulHound); 0 = skip")
     ap.add_argument("--ppo-epochs", type=int, default=5,
                     help="timed PPO epochs (AnymalTerrainPPO.yaml: horizon 24 x envs samples each); 0 = skip")
+    ap.add_argument("--physx-solver-type", type=int, default=None,
+                    help="override task.sim.physx.solver_type for an A/B (default: the config's, TGS)")
     return ap.parse_args()
 
 
@@ -323,8 +325,9 @@ def _main():
     import isaacgymenvs
     from isaacgymenv_amd.isaacgymenvs.utils.utils import set_seed
     set_seed(42, rank=rank)
+    ov = [] if args.physx_solver_type is None else [f"task.sim.physx.solver_type={args.physx_solver_type}"]
     env = isaacgymenvs.make(seed=42 + rank, task="AnymalTerrain", num_envs=args.num_envs, sim_device=device,
-                            rl_device=device, graphics_device_id=-1, headless=True, force_render=False)
+                            rl_device=device, graphics_device_id=-1, headless=True, force_render=False, overrides=ov)
     N, A = env.num_envs, env.num_actions
     gen = torch.Generator(device=device)
     gen.manual_seed(1234 + rank)
@@ -364,6 +367,8 @@ def _main():
     kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
     variant = env.gym.amd_kernel_variant(env.sim)
     kernel_name = {1: "k_pd_step<Topo_anymal_c>", 2: "k_pd_step_team<Topo_anymal_c>"}.get(variant, str(variant))
+    solver_type = int(env.sim.cparams.solver_type)
+    solver = ("TGS" if solver_type == 1 and variant == 2 else "PGS") + f" (physx.solver_type {solver_type}, cfg/config.yaml:31)"
     # roofline basis: SURVEY.md 8(d)'s step-scoped algorithmic bytes (2,434 B per env step) per launch of
     # the dominant kernel; the kernel-scoped bytes (what gs_sim_pd_step alone moves) beside it
     bytes_per_launch = STEP_BYTES_PER_ENV * N
@@ -422,7 +427,8 @@ def _main():
             "data": "synthetic (uniform random actions in [-1,1) pre-generated in HBM, seed 1234+rank; random-init sim state via reset_idx)",
             "config": {"workload": "AnymalTerrain VecTask.step, terrainType plane (AnymalTerrain.yaml default), "
                                    "5 physics substeps/step, obs noise on",
-                       "num_envs_per_gpu": N, "global_num_envs": N * world, "parallelism": f"dp{world}"},
+                       "num_envs_per_gpu": N, "global_num_envs": N * world, "parallelism": f"dp{world}",
+                       "solver": solver},
             "roofline": {"bound": "hbm", "kernel": f"gs_sim_pd_step ({kernel_name})",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_note": traffic_note, "kernel_ms": kernel_ms,

@@ -148,6 +148,7 @@ gs_sim* gs_sim_create(int device, const gs_sim_params* p) {
   s->dp.contact_offset = (float)p->contact_offset;
   s->dp.rest_offset = (float)p->rest_offset;
   s->dp.max_depen_vel = (float)p->max_depenetration_velocity;
+  s->dp.tgs = p->solver_type == 1 && p->num_position_iterations > 0 ? 1 : 0;
   s->dp.collect = p->contact_collection != 0;
   s->dp.limit_margin = (float)(p->joint_limit_margin > 0 ? p->joint_limit_margin : 0.0);
   s->dp.any_limits = 0;

@@ -142,10 +142,11 @@ struct RowSlots {
   static constexpr int RZROW = 16;
   static constexpr int CSLOT = 15;
   __device__ static constexpr int zslot(int comp) { return comp < 6 ? 4 * (comp >> 1) + (comp & 1) : 4 * (comp - 6) + 2; }
+  // (C_SEP / R_SEP: the row's separation at the substep's start, for TGS's per-sub-step targets)
   static constexpr int C_DI = 3 * ZROW, C_G = C_DI + 3, C_TP = C_G + 3, C_TV = C_TP + 1,
-                       C_MU = C_TV + 1, C_ACT = C_MU + 1, PER_CONTACT = C_ACT + 1;
+                       C_MU = C_TV + 1, C_ACT = C_MU + 1, C_SEP = C_ACT + 1, PER_CONTACT = C_SEP + 1;
   static constexpr int R_DI = 3 * RZROW, R_G = R_DI + 3, R_TP = R_G + 3, R_TV = R_TP + 1,
-                       R_MU = R_TV + 1, PER_ROOT = R_MU + 1;
+                       R_MU = R_TV + 1, R_SEP = R_MU + 1, PER_ROOT = R_SEP + 1;
   static constexpr int CHAIN = PER_CONTACT * T::T_CC;
   static constexpr int ROOT = PER_ROOT * (T::T_RC > 0 ? T::T_RC : 1);
   // self-contact pool, replicated in every lane's column of a team: the entry's geometry
@@ -1466,6 +1467,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       rec[RS::C_TP * RW] = (sc < 0.f ? fminf(tgt, P.max_depen_vel) : tgt) * dir[0];
       rec[RS::C_TV * RW] = (sc < 0.f ? 0.f : tgt) * dir[0];
       rec[RS::C_MU * RW] = cmu[j];
+      rec[RS::C_SEP * RW] = sc;
     }
   }
   // root candidates (replicated in every lane, own column; TERR: lane j % 4 runs root candidate j's mesh query
@@ -1549,6 +1551,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       rec[RS::R_TP * RW] = (sc < 0.f ? fminf(tgt, P.max_depen_vel) : tgt) * dir[0];
       rec[RS::R_TV * RW] = (sc < 0.f ? 0.f : tgt) * dir[0];
       rec[RS::R_MU * RW] = 0.5f * (mu_t[T::T_rcs[j] * kTeamsPerBlock] + rmu_s);
+      rec[RS::R_SEP * RW] = sc;
     }
   }
   // self-contact pool rows: J = n.(v_A(x) - v_B(x)) has columns only on the two chains below
@@ -1684,9 +1687,27 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
   for (int j = 0; j < RC; ++j) lamr[j][0] = lamr[j][1] = lamr[j][2] = 0.f;
   float wbp[6], wcp[CL];
   const int iters = P.pos_iters + P.vel_iters;
+  // TGS (physx.solver_type 1; oracle/physics_oracle.c solver_type 3): the position iterations are
+  // sub-steps of hs = h / pos_iters; a row's separation is advanced by J dq, dq = hs (v_0 + ... + v_{k-1}) the
+  // displacement of the sub-steps done (in w space: Z (w_0 + ... + w_{k-1}) + k c, the sums kept in aA / aA2 /
+  // aC); its target: a gap closes within the sub-step (-s / hs), a penetration is pushed out at -s / h (capped),
+  // over the whole step; the velocity iterations target the gap left after the sub-steps; the positions integrate
+  // the sub-steps' mean velocity.  PGS (0): the split-impulse targets precomputed in the records.
+  const bool tgs = P.tgs != 0;
+  const float hs = tgs ? h / (float)P.pos_iters : h, inv_hs = 1.f / hs;
+  float aA = 0.f, aA2 = 0.f, aC[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) aC[c] = 0.f;
+  auto tgs_tdi = [&](float sc, float su, bool pos, float di0) {
+    const float sep = fmaf(hs, su, sc);
+    const float t = sep >= 0.f ? -sep * (pos ? inv_hs : inv_h) : (pos ? fminf(-sep * inv_h, P.max_depen_vel) : 0.f);
+    return t * di0;
+  };
   for (int it = 0; it < iters; ++it) {
     const int tsel = it < P.pos_iters ? RS::C_TP : RS::C_TV;
     const int rsel = it < P.pos_iters ? RS::R_TP : RS::R_TV;
+    const bool pos = it < P.pos_iters;
+    const float na = (float)(it < P.pos_iters ? it : P.pos_iters);  // sub-steps done
 #pragma unroll
     for (int j = 0; j < RC; ++j) {
       if (ract[j]) {
@@ -1698,9 +1719,12 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
 #pragma unroll
         for (int rr = 0; rr < 3; ++rr) u[rr] = fmaf(z[4 * rr], wA, fmaf(z[4 * rr + 1], wA2, z[4 * rr + 3]));
         quad_sum3(u);
+        float tdi = rec[rsel * RW];
+        if (tgs) tdi = tgs_tdi(rec[RS::R_SEP * RW], quad_sum(fmaf(z[0], aA, fmaf(z[1], aA2, na * z[3]))), pos,
+                               rec[RS::R_DI * RW]);
         float dl0, dl1, dl2;
         contact_block(u[0], u[1], u[2], rec[RS::R_DI * RW], rec[(RS::R_DI + 1) * RW], rec[(RS::R_DI + 2) * RW],
-                      rec[RS::R_G * RW], rec[(RS::R_G + 1) * RW], rec[(RS::R_G + 2) * RW], rec[rsel * RW],
+                      rec[RS::R_G * RW], rec[(RS::R_G + 1) * RW], rec[(RS::R_G + 2) * RW], tdi,
                       rec[RS::R_MU * RW], lamr[j], dl0, dl1, dl2);
         wA = fmaf(z[8], dl2, fmaf(z[4], dl1, fmaf(z[0], dl0, wA)));
         wA2 = fmaf(z[9], dl2, fmaf(z[5], dl1, fmaf(z[1], dl0, wA2)));
@@ -1709,7 +1733,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     // software-pipelined over the NCH*CC chain contacts: the next contact's whole record (activity,
     // this lane's Z components and c, the Delassus block, target, mu) is loaded before this
     // contact's (divergent) block, so its LDS latency overlaps the block
-    float nact, nz[12], nk[8];  // nk: 1/G_rr (3) | scaled couplings (3) | target | mu
+    float nact, nz[12], nk[8];  // nk: 1/G_rr (3) | scaled couplings (3) | target (TGS: separation) | mu
     auto fetch = [&](int n) {
       const int cc = n / CC, j = n - (n / CC) * CC;
       const float* rec = rows_team + cc + RS::chain(j) * RW;
@@ -1719,7 +1743,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       for (int i = 0; i < 12; ++i) nz[i] = recl[((i >> 2) * RS::ZROW + (i & 3)) * RW];
 #pragma unroll
       for (int i = 0; i < 6; ++i) nk[i] = rec[(RS::C_DI + i) * RW];
-      nk[6] = rec[tsel * RW];
+      nk[6] = rec[(tgs ? RS::C_SEP : tsel) * RW];
       nk[7] = rec[RS::C_MU * RW];
     };
     fetch(0);
@@ -1746,8 +1770,11 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         for (int rr = 0; rr < 3; ++rr)  // the w terms last (they carry the Gauss-Seidel chain)
           u[rr] = fmaf(z[4 * rr], wA, fmaf(z[4 * rr + 1], wA2, fmaf(z[4 * rr + 2], wC[cc], z[4 * rr + 3])));
         quad_sum3(u);
+        float tdi = k8[6];
+        if (tgs)
+          tdi = tgs_tdi(k8[6], quad_sum(fmaf(z[0], aA, fmaf(z[1], aA2, fmaf(z[2], aC[cc], na * z[3])))), pos, k8[0]);
         float dl0, dl1, dl2;
-        contact_block(u[0], u[1], u[2], k8[0], k8[1], k8[2], k8[3], k8[4], k8[5], k8[6], k8[7], lamc[cc][j], dl0,
+        contact_block(u[0], u[1], u[2], k8[0], k8[1], k8[2], k8[3], k8[4], k8[5], tdi, k8[7], lamc[cc][j], dl0,
                       dl1, dl2);
         wA = fmaf(z[8], dl2, fmaf(z[4], dl1, fmaf(z[0], dl0, wA)));
         wA2 = fmaf(z[9], dl2, fmaf(z[5], dl1, fmaf(z[1], dl0, wA2)));
@@ -1759,11 +1786,13 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       for (int p = 0; p < npc; ++p) {
         float* o = pool + RS::PER_POOL * p * RW;
         const int ca = (int)o[RS::P_CA * RW], cb = (int)o[RS::P_CB * RW];
-        float wa = 0.f, wb = 0.f;
+        float wa = 0.f, wb = 0.f, ana = 0.f, anb = 0.f;
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
           wa = c == ca ? wC[c] : wa;
           wb = c == cb ? wC[c] : wb;
+          ana = c == ca ? aC[c] : ana;
+          anb = c == cb ? aC[c] : anb;
         }
         float z[15], u[3];
 #pragma unroll
@@ -1773,9 +1802,14 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
           u[rr] = fmaf(z[5 * rr], wA, fmaf(z[5 * rr + 1], wA2, fmaf(z[5 * rr + 2], wa, fmaf(z[5 * rr + 3], wb, z[5 * rr + 4]))));
         quad_sum3(u);
         float lam[3] = {o[kPoolLam * RW], o[(kPoolLam + 1) * RW], o[(kPoolLam + 2) * RW]};
+        float tdi = o[psel * RW];
+        if (tgs)
+          tdi = tgs_tdi(o[kPoolSep * RW],
+                        quad_sum(fmaf(z[0], aA, fmaf(z[1], aA2, fmaf(z[2], ana, fmaf(z[3], anb, na * z[4]))))), pos,
+                        o[RS::P_DI * RW]);
         float dl0, dl1, dl2;
         contact_block(u[0], u[1], u[2], o[RS::P_DI * RW], o[(RS::P_DI + 1) * RW], o[(RS::P_DI + 2) * RW],
-                      o[RS::P_G * RW], o[(RS::P_G + 1) * RW], o[(RS::P_G + 2) * RW], o[psel * RW], o[kPoolMu * RW], lam,
+                      o[RS::P_G * RW], o[(RS::P_G + 1) * RW], o[(RS::P_G + 2) * RW], tdi, o[kPoolMu * RW], lam,
                       dl0, dl1, dl2);
         o[kPoolLam * RW] = lam[0];
         o[(kPoolLam + 1) * RW] = lam[1];
@@ -1792,7 +1826,23 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     for (int j = 0; j < RC; ++j)
       if (__ballot(ract[j]) != 0ull) GS_PROF_COUNT(9, 1)  // root contacts the wave executes
 #endif
-    if (it == P.pos_iters - 1) gather_w<T>(lc, wA, wA2, wC, wbp, wcp);
+    if (tgs && pos) {  // the sub-step's velocity joins the displacement
+      aA += wA;
+      aA2 += wA2;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) aC[c] += wC[c];
+    }
+    if (it == P.pos_iters - 1) {
+      if (tgs) {  // positions integrate the sub-steps' mean velocity (w space is linear)
+        const float inv_n = 1.f / (float)P.pos_iters;
+        float mC[NCH];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) mC[c] = aC[c] * inv_n;
+        gather_w<T>(lc, aA * inv_n, aA2 * inv_n, mC, wbp, wcp);
+      } else {
+        gather_w<T>(lc, wA, wA2, wC, wbp, wcp);
+      }
+    }
   }
   float wb[6], wc[CL];
   gather_w<T>(lc, wA, wA2, wC, wb, wc);

@@ -38,7 +38,8 @@ class GsSimParams(C.Structure):
                 ("contact_offset", C.c_double), ("rest_offset", C.c_double),
                 ("bounce_threshold_velocity", C.c_double), ("max_depenetration_velocity", C.c_double),
                 ("contact_collection", C.c_int32), ("kernel_variant", C.c_int32),
-                ("joint_limit_margin", C.c_double), ("num_threads", C.c_int32)]
+                ("joint_limit_margin", C.c_double), ("num_threads", C.c_int32),
+                ("solver_type", C.c_int32)]
 
 
 class GsPdArgs(C.Structure):

@@ -170,6 +170,8 @@ def make_gpu_sim(kind: str, n: int, params: dict, terrain=None, host: bool = Fal
     sp.physx.rest_offset = params["rest_offset"]
     sp.physx.max_depenetration_velocity = params["max_depen_vel"]
     sp.physx.contact_collection = gymapi.ContactCollection(params["collect_contacts"])
+    # the oracle's parameter dicts mean PGS unless they say otherwise (gymapi's own default is TGS, as Isaac Gym's)
+    sp.physx.solver_type = int(params.get("solver_type", 0))
     sim = gym.create_sim(0, -1, gymapi.SIM_PHYSX, sp)
     assert sim is not None
     if params.get("has_ground", 1):

@@ -38,11 +38,14 @@ def _make(monkeypatch):
                              headless=True, force_render=False)
 
 
-def _oracle_sequence(flat, root, dof, dof_tensor, mu, act, default, kp, kd, scale, decimation=4, extra=1, bits=64):
-    """anymal_terrain.py:443-451 then vec_task's extra simulate, in fp64 (bits=32: the same restatement in float)."""
+def _oracle_sequence(flat, root, dof, dof_tensor, mu, act, default, kp, kd, scale, decimation=4, extra=1, bits=64,
+                     solver_type=0):
+    """anymal_terrain.py:443-451 then vec_task's extra simulate, in fp64 (bits=32: the same restatement in float).
+    solver_type: the sim's physx.solver_type (the bench config asks TGS, cfg/config.yaml:31: the oracle's TGS
+    restatement is its solver_type 3)."""
     dt = np.float64 if bits == 64 else np.float32
     c = lambda a: np.array(a, dtype=dt, order="C")  # a copy: the oracle steps it in place  # noqa: E731
-    sim = OracleSim(flat, H.ANYMAL_PARAMS, real_bits=bits)
+    sim = OracleSim(flat, dict(H.ANYMAL_PARAMS, solver_type=3 if solver_type == 1 else 0), real_bits=bits)
     r, d, mu = c(root), c(dof), c(mu)
     cf = np.zeros((root.shape[0], flat["nb"], 3), dt)
     q, qd = dof_tensor[:, :, 0], dof_tensor[:, :, 1]
@@ -86,13 +89,15 @@ def test_fused_headline_step_matches_oracle_at_bench_config(monkeypatch):
                tau=torques.double().cpu().numpy(), cf=env.contact_forces.double().cpu().numpy())
     assert all(np.all(np.isfinite(v)) for v in gpu.values())
 
+    st = env.sim.cparams.solver_type
+    assert st == 1, "AnymalTerrain asks TGS (cfg/config.yaml:31) and the lane team runs it"
     ref = _oracle_sequence(flat, root, dof, dof_tensor, mu, act, default, kp, kd, scale, env.decimation,
-                           env.control_freq_inv)
+                           env.control_freq_inv, solver_type=st)
 
     def rerun(idx, rng, bits):
         pr, pd_ = H.perturbed(root, dof, idx, rng)
         out = _oracle_sequence(flat, pr, pd_, dof_tensor[idx], mu[idx], act[idx], default, kp, kd, scale,
-                               env.decimation, env.control_freq_inv, bits)
+                               env.decimation, env.control_freq_inv, bits, solver_type=st)
         return {k: np.asarray(v, np.float64) for k, v in out.items()}
     # a contact-switch env is rare at this state mix; a systematic error would make many envs "sensitive"
     H.assert_close_or_explained(gpu, ref, rerun, tol=TOL, max_env_frac=0.02,

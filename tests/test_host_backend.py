@@ -460,3 +460,17 @@ def test_cylinder_end_near_ground_is_not_skipped():
         np.testing.assert_allclose(g_dof[:, :, 0], o_dof[:, :, 0], atol=2e-6)
         np.testing.assert_allclose(g_dof[:, :, 1], o_dof[:, :, 1], atol=5e-4, rtol=1e-4)
         np.testing.assert_allclose(g_root[:, 7:], o_root[:, 7:], atol=5e-4, rtol=1e-4)
+
+
+def test_tgs_on_a_pgs_kernel_form_warns():
+    """physx.solver_type 1 on a kernel form without TGS (here the host backend) solves PGS and says so."""
+    import warnings
+    from isaacgymenv_amd.isaacgym.gymapi import PhysicsDeviationWarning
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        gym, sim = H.make_host_sim("anymal", 2, dict(H.ANYMAL_PARAMS, solver_type=1), threads=1)
+    assert any(issubclass(x.category, PhysicsDeviationWarning) and "TGS" in str(x.message) for x in w)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        gym, sim = H.make_host_sim("anymal", 2, H.ANYMAL_PARAMS, threads=1)
+    assert not any(issubclass(x.category, PhysicsDeviationWarning) for x in w)
