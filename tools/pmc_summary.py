@@ -65,7 +65,7 @@ def main():
     hbm = (2.0 * fetch_kb + write_kb) * 1024.0
     alg = bench.physics_kernel_bytes_per_env() * args.num_envs
     out = {
-        "kernel": re.search(r"k_pd_step\w*<\w+>", fr[0]["Kernel"]).group(0) + " (gs_sim_pd_step)",
+        "kernel": re.search(r"k_pd_step\w*<[^>]+>", fr[0]["Kernel"]).group(0) + " (gs_sim_pd_step)",
         "num_envs": args.num_envs,
         "round": args.round,
         "counters": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, --kernel-trace",
