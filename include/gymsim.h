@@ -124,10 +124,9 @@ typedef struct gs_sim_params {
     double joint_limit_margin;          /* a limit row is active within this distance of the limit */
     int32_t num_threads;                /* ABI 3, host backend: physx.num_threads (cfg/config.yaml:30)
                                            solver threads including the caller; <= 1 = caller only */
-    int32_t solver_type;                /* ABI 7: physx.solver_type (cfg/config.yaml:31): 0 PGS, 1 TGS --
-                                           the position iterations as sub-steps of h / num_position_
-                                           iterations; TGS runs in the lane-team kernel
-                                           (gs_sim_kernel_variant 2), every other form solves PGS */
+    int32_t solver_type;                /* ABI 7: physx.solver_type (cfg/config.yaml:31): 0 PGS with split
+                                           impulse, 1 TGS -- the position iterations as sub-steps of
+                                           h / num_position_iterations; every kernel form */
 } gs_sim_params;
 
 /* Fused PD decimation step (AnymalTerrain.pre_physics_step + VecTask.step's

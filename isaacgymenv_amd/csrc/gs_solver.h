@@ -837,8 +837,29 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
   });
   const float inv_h = 1.f / h;
   const int iters = P.pos_iters + P.vel_iters;
+  // TGS (physx.solver_type 1; DESIGN.md 3.5, the lane team's rule, oracle solver_type 3): the position iterations
+  // are sub-steps of hs = h / pos_iters; a row's separation is advanced by J dq, dq the sub-steps' displacement --
+  // in w space the row's c + z.w summed over the sub-steps done (wacc: the sum of their w); a gap closes within
+  // its sub-step, a penetration is pushed out over the step (-s / h, capped); the velocity iterations target the
+  // gap the sub-steps left; the positions integrate the sub-steps' mean velocity.  PGS: split impulse.
+  const bool tgs = P.tgs != 0;
+  const float hs = tgs ? h / (float)P.pos_iters : h, inv_hs = 1.f / hs;
+  float wacc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) wacc[k] = 0.f;
   for (int it = 0; it < iters; ++it) {
     const bool pos_phase = it < P.pos_iters;
+    const float na = (float)(it < P.pos_iters ? it : P.pos_iters);  // sub-steps done
+    // the row's target from its separation at the sub-step (TGS) or the step's start (PGS)
+    auto row_target = [&](float sc, float su) {
+      if (!tgs) {
+        const float t = -sc * inv_h;
+        return sc < 0.f ? (pos_phase ? fminf(t, P.max_depen_vel) : 0.f) : t;
+      }
+      const float sep = sc + hs * su;
+      return sep >= 0.f ? -sep * (pos_phase ? inv_hs : inv_h)
+                        : (pos_phase ? fminf(-sep * inv_h, P.max_depen_vel) : 0.f);
+    };
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
       if (lsgn[j] != 0.f) {
@@ -846,17 +867,17 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
         const int leaf = T::lleaf[j];
         const float* slot = lds + T::lslot[j] * LB;
         const float sc = lsep[j];
-        float target = -sc * inv_h;
-        if (sc < 0.f) target = pos_phase ? fminf(target, P.max_depen_vel) : 0.f;
         float z[MS];
-        float u = slot[SUP * LB];
+        float u = slot[SUP * LB], su = na * slot[SUP * LB];
 #pragma unroll
         for (int si = 0; si < MS; ++si) {
           if (si < SUP) {
             z[si] = slot[si * LB];
             u += z[si] * wt[supp_node<T>(leaf, si)];
+            if (tgs) su += z[si] * wacc[supp_node<T>(leaf, si)];
           }
         }
+        const float target = row_target(sc, su);
         const float nl = fmaxf(laml[j] + (target - u) * slot[(SUP + 1) * LB], 0.f);
         const float dl = nl - laml[j];
         laml[j] = nl;
@@ -873,22 +894,22 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
         const float sc = lds[(X_SEP + c) * LB];
         const float cmu = lds[(X_MU + c) * LB];
         float lam[3] = {lamc[(3 * c) * LB], lamc[(3 * c + 1) * LB], lamc[(3 * c + 2) * LB]};
-        float target = -sc * inv_h;
-        if (sc < 0.f) target = pos_phase ? fminf(target, P.max_depen_vel) : 0.f;
 #pragma unroll
         for (int rr = 0; rr < 3; ++rr) {
           float z[MS];
-          float u = slot[(3 * SUP + rr) * LB];
+          float u = slot[(3 * SUP + rr) * LB], su = na * slot[(3 * SUP + rr) * LB];
 #pragma unroll
           for (int si = 0; si < MS; ++si) {
             if (si < SUP) {
               z[si] = slot[(rr * SUP + si) * LB];
               u += z[si] * wt[supp_node<T>(leaf, si)];
+              if (tgs && rr == 0) su += z[si] * wacc[supp_node<T>(leaf, si)];
             }
           }
           const float dinv = slot[(3 * SUP + 3 + rr) * LB];  // 0 below GS_MIN_RESPONSE (no impulse)
           float nl;
           if (rr == 0) {
+            const float target = row_target(sc, su);
             nl = fmaxf(lam[0] + (target - u) * dinv, 0.f);
           } else {
             const float lim = cmu * lam[0];
@@ -909,17 +930,19 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
       for (int p = 0; p < npc; ++p) {
         float* o = pool + PE * p * LB;
         const float sc = o[kPoolSep * LB];
-        float target = -sc * inv_h;
-        if (sc < 0.f) target = pos_phase ? fminf(target, P.max_depen_vel) : 0.f;
         float lam[3] = {o[kPoolLam * LB], o[(kPoolLam + 1) * LB], o[(kPoolLam + 2) * LB]};
 #pragma unroll
         for (int rr = 0; rr < 3; ++rr) {
-          float u = o[(kPoolC + rr) * LB];
+          float u = o[(kPoolC + rr) * LB], su = na * o[(kPoolC + rr) * LB];
 #pragma unroll
-          for (int k = 0; k < NV; ++k) u += o[(kPoolJ + rr * NV + k) * LB] * wt[k];
+          for (int k = 0; k < NV; ++k) {
+            u += o[(kPoolJ + rr * NV + k) * LB] * wt[k];
+            if (tgs && rr == 0) su += o[(kPoolJ + rr * NV + k) * LB] * wacc[k];
+          }
           const float dinv = o[(kPoolDi + rr) * LB];
           float nl;
           if (rr == 0) {
+            const float target = row_target(sc, su);
             nl = fmaxf(lam[0] + (target - u) * dinv, 0.f);
           } else {
             const float lim = o[kPoolMu * LB] * lam[0];
@@ -935,9 +958,14 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
         o[(kPoolLam + 2) * LB] = lam[2];
       }
     }
-    if (it == P.pos_iters - 1) {
+    if (tgs && pos_phase) {  // the sub-step's velocity joins the displacement
 #pragma unroll
-      for (int k = 0; k < NV; ++k) wpos[k] = wt[k];
+      for (int k = 0; k < NV; ++k) wacc[k] += wt[k];
+    }
+    if (it == P.pos_iters - 1) {
+      const float inv_n = 1.f / (float)P.pos_iters;  // TGS: the sub-steps' mean (w space is linear)
+#pragma unroll
+      for (int k = 0; k < NV; ++k) wpos[k] = tgs ? wacc[k] * inv_n : wt[k];
     }
   }
   if (P.pos_iters <= 0) {

@@ -340,8 +340,8 @@ class Sim:
         p.joint_limit_margin = JOINT_LIMIT_MARGIN
         # PhysX CPU worker threads (cfg/config.yaml:30 num_threads: 4); 0 = the calling thread only
         p.num_threads = max(1, int(getattr(px, "num_threads", 0) or 0))
-        # physx.solver_type (cfg/config.yaml:31): 1 = TGS, solved by the lane-team kernel; the
-        # other kernel forms solve PGS and prepare_sim warns when one of them is chosen for a TGS sim
+        # physx.solver_type (cfg/config.yaml:31): 1 = TGS (position iterations as sub-steps), 0 = PGS with split
+        # impulse -- every kernel form and the host backend solve both
         p.solver_type = 1 if int(getattr(px, "solver_type", 0)) == 1 else 0
         self.cparams = p
         L = _lib.lib()
@@ -422,11 +422,6 @@ class Sim:
                                     self.cf_soa.data_ptr()), "gs_sim_prepare")
         self._keep = keep
         self.kernel_variant = L.gs_sim_kernel_variant(self.handle)
-        if self.cparams.solver_type == 1 and (self.host or self.kernel_variant != 2):
-            warnings.warn("physx.solver_type=1 (TGS) requested: this sim's kernel form (%s) solves projected "
-                          "Gauss-Seidel with split impulse; TGS runs in the lane-team kernel only (DESIGN.md 3.5)"
-                          % ("host backend" if self.host else "variant %d" % self.kernel_variant),
-                          PhysicsDeviationWarning, stacklevel=3)
         self.num_sensors = len(sens)
         self.sens_soa = torch.zeros(max(1, 6 * len(sens)), N, dtype=f32, device=dev)
         if sens:

@@ -65,14 +65,16 @@ def test_ant_4096_one_simulate_matches_oracle(monkeypatch):
     g_root, g_dof = H.read_state(env.sim, 8)
     g_sens = env.sim.sens_soa.cpu().numpy().astype(np.float64).T.reshape(N, 4, 6)
     assert np.all(np.isfinite(g_root)) and np.all(np.isfinite(g_dof)) and np.all(np.isfinite(g_sens))
-    o_root, o_dof, _, o_sens = H.oracle_run(flat, H.ANT_PARAMS, root, dof, tau, mu, nsens=4, sensor_bodies=H.ANT_FEET)
+    # the config's physx.solver_type (Ant.yaml asks TGS): the oracle's TGS restatement is its solver_type 3
+    ap = dict(H.ANT_PARAMS, solver_type=3 if env.sim.cparams.solver_type == 1 else 0)
+    o_root, o_dof, _, o_sens = H.oracle_run(flat, ap, root, dof, tau, mu, nsens=4, sensor_bodies=H.ANT_FEET)
     near_limit = ((dof[:, :, 0] < flat["lower"] + 0.1) | (dof[:, :, 0] > flat["upper"] - 0.1)).any(axis=1)
     assert near_limit.mean() > 0.05, "the sampled states must exercise the joint-limit rows"
     assert np.abs(o_sens).sum() > 0
 
     def rerun(idx, rng, bits):
         r, d = H.perturbed(root, dof, idx, rng)
-        o_r, o_d, _, o_s = H.oracle_run(flat, H.ANT_PARAMS, r, d, tau[idx], mu[idx], bits, nsens=4,
+        o_r, o_d, _, o_s = H.oracle_run(flat, ap, r, d, tau[idx], mu[idx], bits, nsens=4,
                                         sensor_bodies=H.ANT_FEET)
         return H.state_fields(o_r, o_d, sens=o_s)
     try:
@@ -99,12 +101,13 @@ def test_hound_4096_split_simulate_matches_oracle(monkeypatch):
     g_root, g_dof = H.read_state(env.sim, 18)
     g_cf = env.sim.contact_tensor.cpu().numpy().astype(np.float64).reshape(N, 24, 3)
     assert np.all(np.isfinite(g_root)) and np.all(np.isfinite(g_dof)) and np.all(np.isfinite(g_cf))
-    o_root, o_dof, o_cf, _ = H.oracle_run(flat, H.HOUND_PARAMS, root, dof, tau, mu, nc=24)
+    hp = dict(H.HOUND_PARAMS, solver_type=3 if env.sim.cparams.solver_type == 1 else 0)  # UsefulHound.yaml: TGS
+    o_root, o_dof, o_cf, _ = H.oracle_run(flat, hp, root, dof, tau, mu, nc=24)
     assert np.abs(o_cf).sum() > 0
 
     def rerun(idx, rng_, bits):
         r, d = H.perturbed(root, dof, idx, rng_)
-        r, d, c, _ = H.oracle_run(flat, H.HOUND_PARAMS, r, d, tau[idx], mu[idx], bits, nc=24)
+        r, d, c, _ = H.oracle_run(flat, hp, r, d, tau[idx], mu[idx], bits, nc=24)
         return H.state_fields(r, d, c)
     try:
         H.assert_close_or_explained(H.state_fields(g_root, g_dof, g_cf), H.state_fields(o_root, o_dof, o_cf), rerun,

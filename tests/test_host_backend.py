@@ -462,15 +462,33 @@ def test_cylinder_end_near_ground_is_not_skipped():
         np.testing.assert_allclose(g_root[:, 7:], o_root[:, 7:], atol=5e-4, rtol=1e-4)
 
 
-def test_tgs_on_a_pgs_kernel_form_warns():
-    """physx.solver_type 1 on a kernel form without TGS (here the host backend) solves PGS and says so."""
+def test_host_tgs_matches_oracle_tgs_and_warns_nothing():
+    """physx.solver_type 1 on the host backend (the lane solver source, gs_solver.h): one simulate from random ANYmal
+    states and from Ant states (joint limits + force sensors) against the oracle's TGS (solver_type 3), the GPU
+    tolerances through the explained-env rule; no PhysicsDeviationWarning (TGS is simulated)."""
     import warnings
     from isaacgymenv_amd.isaacgym.gymapi import PhysicsDeviationWarning
-    with warnings.catch_warnings(record=True) as w:
-        warnings.simplefilter("always")
-        gym, sim = H.make_host_sim("anymal", 2, dict(H.ANYMAL_PARAMS, solver_type=1), threads=1)
-    assert any(issubclass(x.category, PhysicsDeviationWarning) and "TGS" in str(x.message) for x in w)
-    with warnings.catch_warnings(record=True) as w:
-        warnings.simplefilter("always")
-        gym, sim = H.make_host_sim("anymal", 2, H.ANYMAL_PARAMS, threads=1)
-    assert not any(issubclass(x.category, PhysicsDeviationWarning) for x in w)
+    for kind, mk, states, params, nd in (("anymal", H.anymal, H.anymal_states, H.ANYMAL_PARAMS, 12),
+                                         ("ant", H.ant, H.ant_states, H.ANT_PARAMS, 8)):
+        n = 64
+        art, flat = mk()
+        root, dof, tau, mu = states(n, seed=6)
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            gym, sim = H.make_host_sim(kind, n, dict(params, solver_type=1), threads=2)
+        assert not any(issubclass(x.category, PhysicsDeviationWarning) for x in w), kind
+        assert sim.cparams.solver_type == 1
+        H.load_state_into(sim, root, dof, mu)
+        sim.dof_force.copy_(torch.from_numpy(tau.astype(np.float32).reshape(-1)))
+        gym.simulate(sim)
+        g_root, g_dof = H.read_state(sim, nd)
+        op = dict(params, solver_type=3)
+        o_root, o_dof, _, _ = H.oracle_run(flat, op, root, dof, tau, mu)
+
+        def rerun(idx, rng, bits=64):
+            r, d = H.perturbed(root, dof, idx, rng)
+            rr, dd, _, _ = H.oracle_run(flat, op, r, d, tau[idx], mu[idx], bits=bits)
+            return H.state_fields(rr, dd)
+
+        H.assert_close_or_explained(H.state_fields(g_root, g_dof), H.state_fields(o_root, o_dof), rerun,
+                                    what=f"host TGS one simulate vs the oracle's TGS ({kind}, {n} random states)")
