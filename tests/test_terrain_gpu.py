@@ -26,11 +26,13 @@ def _terrain_states(n, ter, seed):
 KERNELS = {"lane": 1, "team": 2}
 
 
-def _gpu_vs_oracle(ter, n, seed, steps, kernel="team"):
+def _gpu_vs_oracle(ter, n, seed, steps, kernel="team", solver="pgs"):
     art, flat = H.anymal()
     params = dict(H.ANYMAL_PARAMS, has_ground=0)
     root, dof, tau, mu = _terrain_states(n, ter, seed)
-    gym, sim = H.make_gpu_sim("anymal", n, params, terrain=ter)
+    gym, sim = H.make_gpu_sim("anymal", n, dict(params, solver_type=1 if solver == "tgs" else 0), terrain=ter)
+    if solver == "tgs":
+        params = dict(params, solver_type=3)  # the oracle's TGS restatement
     # mesh contacts: the lane team's TERR form (default) or the wave-assisted one-env-per-lane kernel
     assert sim.kernel_variant == KERNELS[kernel]
     H.load_state_into(sim, root, dof, mu)
@@ -47,18 +49,18 @@ def _gpu_vs_oracle(ter, n, seed, steps, kernel="team"):
     return g_root, g_dof, g_cf, r, d, cf
 
 
-@pytest.mark.parametrize("kernel", sorted(KERNELS))
-def test_rough_terrain_one_simulate_matches_oracle(kernel, monkeypatch):
+@pytest.mark.parametrize("kernel,solver", [("lane", "pgs"), ("team", "pgs"), ("lane", "tgs"), ("team", "tgs")])
+def test_rough_terrain_one_simulate_matches_oracle(kernel, solver, monkeypatch):
     monkeypatch.setenv("GS_PHYSICS_KERNEL", kernel)
     ter = H.rough_terrain(seed=5)
     n = 512
-    g_root, g_dof, g_cf, r, d, cf = _gpu_vs_oracle(ter, n, seed=2, steps=1, kernel=kernel)
+    g_root, g_dof, g_cf, r, d, cf = _gpu_vs_oracle(ter, n, seed=2, steps=1, kernel=kernel, solver=solver)
     assert np.abs(cf).sum(axis=(1, 2)).astype(bool).mean() > 0.5, "most envs must touch the mesh"
     assert np.all(np.isfinite(g_root)) and np.all(np.isfinite(g_dof))
     # contact activity / closest-triangle choices can switch on a last-bit difference (stair edges): such an
     # env must be one the oracle itself moves under an fp32-sized perturbation
     art, flat = H.anymal()
-    params = dict(H.ANYMAL_PARAMS, has_ground=0)
+    params = dict(H.ANYMAL_PARAMS, has_ground=0, solver_type=3 if solver == "tgs" else 0)
     root0, dof0, tau, mu = _terrain_states(n, ter, 2)
 
     def rerun(idx, rng, bits):
@@ -66,7 +68,7 @@ def test_rough_terrain_one_simulate_matches_oracle(kernel, monkeypatch):
         rr, dd, c, _ = H.oracle_run(flat, params, rr, dd, tau[idx], mu[idx], bits, nc=flat["nb"], terrain=ter["oracle"])
         return H.state_fields(rr, dd, c)
     H.assert_close_or_explained(H.state_fields(g_root, g_dof, g_cf), H.state_fields(r, d, cf), rerun,
-                                what=f"rough terrain gpu ({kernel} kernel)")
+                                what=f"rough terrain gpu ({kernel} kernel, {solver.upper()})")
 
 
 @pytest.mark.parametrize("kernel", sorted(KERNELS))

@@ -16,13 +16,15 @@ TGS_GPU = dict(H.ANYMAL_PARAMS, solver_type=1)
 TGS_ORACLE = dict(H.ANYMAL_PARAMS, solver_type=3)
 
 
-def test_team_tgs_one_simulate_matches_oracle(monkeypatch):
-    monkeypatch.setenv("GS_PHYSICS_KERNEL", "team")
+@pytest.mark.parametrize("kernel", ["lane", "team"])
+def test_team_tgs_one_simulate_matches_oracle(kernel, monkeypatch):
+    """Both kernel forms: the lane team (gs_team.hip) and one env per lane (gs_solver.h, also the host backend's)."""
+    monkeypatch.setenv("GS_PHYSICS_KERNEL", kernel)
     n = 512
     art, flat = H.anymal()
     root, dof, tau, mu = H.anymal_states(n, seed=5)
     gym, sim = H.make_gpu_sim("anymal", n, TGS_GPU)
-    assert sim.kernel_variant == 2 and sim.cparams.solver_type == 1
+    assert sim.kernel_variant == {"lane": 1, "team": 2}[kernel] and sim.cparams.solver_type == 1
     H.load_state_into(sim, root, dof, mu)
     sim.dof_force.copy_(torch.from_numpy(tau.astype(np.float32).reshape(-1)))
     gym.simulate(sim)
@@ -37,7 +39,7 @@ def test_team_tgs_one_simulate_matches_oracle(monkeypatch):
         return H.state_fields(rr, dd, cc)
 
     H.assert_close_or_explained(H.state_fields(g_root, g_dof, g_cf), H.state_fields(o_root, o_dof, o_cf), rerun,
-                                what="team TGS one simulate vs the oracle's TGS (512 random ANYmal states)")
+                                what=f"{kernel} TGS one simulate vs the oracle's TGS (512 random ANYmal states)")
 
 
 def test_team_tgs_standing_rollout_tracks_oracle(monkeypatch):
