@@ -82,8 +82,9 @@ typedef struct gt_anymal_buffers {
     int32_t *reset_count;        /* [3] device, zero-initialised: post_a's accumulator and
                                     workgroup counter (re-armed by post_a itself), and [2] =
                                     the number of envs post_a flagged for reset               */
-    int32_t *host_count;         /* [2] host-mapped words (gt_host_alloc) or NULL: post_a's last
-                                    workgroup stores {count, seq} with system scope            */
+    int32_t *host_count;         /* [2] host-mapped words (gt_host_alloc, 8-byte aligned) or NULL:
+                                    post_a's last workgroup stores {count, seq} as ONE 8-byte
+                                    system-scope store                                         */
     int32_t seq;                 /* sequence number post_a publishes in host_count[1]        */
     uint64_t *reset_masks;       /* [ceil(N/64)] post_a's per-wave reset ballots (bit l of word w =
                                     env 64w+l), read by gt_anymal_reset_flagged                */

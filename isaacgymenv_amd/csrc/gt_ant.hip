@@ -161,8 +161,11 @@ __global__ void __launch_bounds__(64) k_ant_tail(gt_ant_params p, gt_ant_buffers
       atomicExch(acc, 0ull);
       b.reset_count[2] = total;
       if (b.host_count) {
-        __hip_atomic_store(&b.host_count[0], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&b.host_count[1], b.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // {count, seq} as ONE 8-byte store: the host reads only this word, so no release fence
+        // (a system-scope release writes back the whole L2, microseconds at the end of the tail)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(b.host_count),
+                           ((unsigned long long)(uint32_t)b.seq << 32) | (uint32_t)total, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
   }

@@ -276,8 +276,11 @@ __global__ void __launch_bounds__(64) k_post_a(gt_anymal_params p, gt_anymal_buf
       *acc = 0ull;
       b.reset_count[2] = total;
       if (b.host_count) {
-        __hip_atomic_store(&b.host_count[0], total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&b.host_count[1], b.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // {count, seq} as ONE 8-byte store: the host reads only this word, so no release fence
+        // (a system-scope release writes back the whole L2, microseconds at the end of the tail)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(b.host_count),
+                           ((unsigned long long)(uint32_t)b.seq << 32) | (uint32_t)total, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
   }
@@ -469,7 +472,11 @@ __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_any
   }
   // Episode means, deterministic: every wave publishes its 13 wave sums (zeros when nothing was
   // flagged) to its own slot of `partial`; the last wave to finish adds the slots in wave order.
-  // Agent-scope atomic stores / loads: the waves run on different XCDs, whose L2s are not coherent.
+  // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1 table): the
+  // slots are stored and loaded sc1 (relaxed agent-scope atomics, L2-served, so no L1 staleness),
+  // each wave waits for its own stores before ONE lane adds to the unsharded counter, and the wave
+  // whose add returned last loads.  No __threadfence(): two of those per wave (~3.5 us each) were
+  // most of this kernel's time.
   // slot NT (terrain): the wave's sum of terrain levels after the update, for mean(terrain_levels)
   constexpr int NT = GT_ANYMAL_NUM_TERMS + 1;
 #pragma unroll
@@ -484,23 +491,41 @@ __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_any
       __hip_atomic_store(&partial[(size_t)w * NT + GT_ANYMAL_NUM_TERMS], lv, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   unsigned old = 0;
-  __threadfence();
-  if (lane == 0) old = atomicAdd(done, 1u);
+  if (lane == 0) old = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   old = __shfl(old, 0, 64);
   if (old == gridDim.x - 1) {  // last wave: finalise the 13 terms in parallel lanes
-    __threadfence();
+    // The slots are staged through LDS 64 waves at a time, every lane issuing its NT loads at
+    // once; lane `term` then adds its column in wave order from LDS (the order of the sum is
+    // fixed, so extras["episode"] does not depend on wave scheduling).
+    static_assert(NT <= kMaxDraws, "partial staging reuses u_lds");
+    float v = 0.0f;
+    for (int q0 = 0; q0 < (int)gridDim.x; q0 += 64) {
+      const int nq = min(64, (int)gridDim.x - q0);
+      float r[NT];
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const int s = lane + 64 * i;
+        r[i] = s < nq * NT ? __hip_atomic_load(&partial[(size_t)q0 * NT + s], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                           : 0.0f;
+      }
+      __syncthreads();  // u_lds (draws, or the previous chunk) is no longer read
+#pragma unroll
+      for (int i = 0; i < NT; ++i) u_lds[lane + 64 * i] = r[i];
+      __syncthreads();
+      if (lane < NT)
+        for (int q = 0; q < nq; ++q) v += u_lds[q * NT + lane];
+    }
     if (lane < GT_ANYMAL_NUM_TERMS + (has_terrain ? 1 : 0)) {
-      float v = 0.0f;
-      for (int q = 0; q < (int)gridDim.x; ++q)
-        v += __hip_atomic_load(&partial[(size_t)q * NT + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (lane < GT_ANYMAL_NUM_TERMS)
         // torch.mean(sums[env_ids]) / max_episode_length_s: mean = sum * (1/k), / scalar = * (1/scalar)
         ep_out[lane] = (v * (1.0f / (float)k)) * (1.0f / len_s);
       else
         ep_out[lane] = v * (1.0f / (float)p.num_envs);  // torch.mean(terrain_levels.float())
     }
-    if (lane == 0) *done = 0u;
+    if (lane == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -816,8 +841,10 @@ int gt_wait_host_seq(const int32_t* words, int32_t seq, int32_t timeout_ms, int3
   // event wake-up.  Yield after the first ~50k polls (~1 ms) so a long wait does not hog a core.
   const auto t0 = std::chrono::steady_clock::now();
   for (uint64_t i = 0;; ++i) {
-    if (__atomic_load_n(&words[1], __ATOMIC_ACQUIRE) == seq) {
-      *value = __atomic_load_n(&words[0], __ATOMIC_RELAXED);
+    // {count, seq} arrive as one 8-byte store (words is hipHostMalloc'd, so 8-byte aligned)
+    const uint64_t w = __atomic_load_n(reinterpret_cast<const uint64_t*>(words), __ATOMIC_ACQUIRE);
+    if ((int32_t)(uint32_t)(w >> 32) == seq) {
+      *value = (int32_t)(uint32_t)w;
       return 0;
     }
     if ((i & 4095) == 4095) {
