@@ -18,6 +18,7 @@
  *   rl_rms_normalize : the model's running mean / std input normalisation.
  *   rl_policy_head : the act forward's sampling / neglogp / value unnormalisation.
  *   rl_rollout_post : the rollout bookkeeping after each env step (play_steps).
+ *   rl_rollout_pre : the experience slot written before each env step (play_steps).
  *
  * All pointers are device pointers; calls are ordered on `stream` (a hipStream_t,
  * NULL = legacy default stream) and return 0 on success, otherwise a nonzero
@@ -32,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 6
+#define RL_ABI_VERSION 7
 
 int rl_abi_version(void);
 const char *rl_last_error(void);
@@ -183,6 +184,21 @@ int rl_rollout_post(const float *rewards, const void *dones, int32_t dones_bytes
                     double gamma, int32_t num_envs, uint8_t *dones_out, float *rewards_out, float *current_rewards,
                     float *current_lengths, float *meter_rewards, float *meter_lengths, int32_t games_to_track,
                     void *stream);
+
+/*
+ * ABI 7 -- play_steps' experience of horizon slot `slot` before env.step (rl_games a2c_common.py
+ * update_data('obses' / 'dones' / 'values' / 'actions' / 'neglogpacs' / 'mus' / 'sigmas')), one launch:
+ *   b_obs[e][slot][:] = obs[e][:]            obs [N][obs_dim] f32, b_obs [N][horizon][obs_dim]
+ *   t_dones[slot][e] = dones[e]              dones [N] u8, t_dones [horizon][N] u8
+ *   t_values[slot][e] = values[e * values_stride]                      t_values [horizon][N] f32
+ *   b_actions / b_mu / b_sigma[e][slot][:] = actions / mu / sigma[e][:]  ([N][A] in, [N][horizon][A] out)
+ *   b_neglogp[e][slot] = neglogp[e]          neglogp [N], b_neglogp [N][horizon]
+ * Inputs contiguous as shown; num_actions <= 64.  Plain copies (bit-identical).
+ */
+int rl_rollout_pre(const float *obs, int32_t obs_dim, const uint8_t *dones, const float *values, int32_t values_stride,
+                   const float *actions, const float *neglogp, const float *mu, const float *sigma, int32_t num_envs,
+                   int32_t num_actions, int32_t horizon, int32_t slot, float *b_obs, uint8_t *t_dones, float *t_values,
+                   float *b_actions, float *b_neglogp, float *b_mu, float *b_sigma, void *stream);
 
 /*
  * ABI 4 -- the minibatch optimizer step over the learner's flat buffers (rl_games a2c_common.py

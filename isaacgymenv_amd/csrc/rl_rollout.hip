@@ -110,6 +110,64 @@ extern "C" int rl_rollout_post(const float* rewards, const void* dones, int32_t 
     return 0;
 }
 
+// ---------------------------------------------------------------- experience slot (before env.step)
+// play_steps' update_data calls of horizon slot n (rl_games a2c_common.py: obses, dones, values,
+// actions, neglogpacs, mus, sigmas), one launch instead of seven strided copies: 64 lanes per env,
+// four envs per workgroup; plain copies, bit-identical to the torch statements.
+namespace {
+
+__global__ __launch_bounds__(256) void k_rollout_pre(const float* __restrict__ obs, int O, const uint8_t* __restrict__ dones,
+                                                     const float* __restrict__ values, int vstride,
+                                                     const float* __restrict__ actions, const float* __restrict__ neglogp,
+                                                     const float* __restrict__ mu, const float* __restrict__ sigma, int N,
+                                                     int A, int H, int n, float* __restrict__ b_obs,
+                                                     uint8_t* __restrict__ t_dones, float* __restrict__ t_values,
+                                                     float* __restrict__ b_actions, float* __restrict__ b_neglogp,
+                                                     float* __restrict__ b_mu, float* __restrict__ b_sigma) {
+    const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int l = threadIdx.x & 63;
+    if (e >= N) return;
+    const float* src = obs + (size_t)e * O;
+    float* dst = b_obs + ((size_t)e * H + n) * O;
+    for (int k = l; k < O; k += 64) dst[k] = src[k];
+    const size_t ra = (size_t)e * A, wa = ((size_t)e * H + n) * A;
+    if (l < A) {
+        b_actions[wa + l] = actions[ra + l];
+        b_mu[wa + l] = mu[ra + l];
+        b_sigma[wa + l] = sigma[ra + l];
+    }
+    if (l == 0) {
+        t_dones[(size_t)n * N + e] = dones[e];
+        t_values[(size_t)n * N + e] = values[(size_t)e * vstride];
+        b_neglogp[(size_t)e * H + n] = neglogp[e];
+    }
+}
+
+}  // namespace
+
+extern "C" int rl_rollout_pre(const float* obs, int32_t obs_dim, const uint8_t* dones, const float* values,
+                              int32_t values_stride, const float* actions, const float* neglogp, const float* mu,
+                              const float* sigma, int32_t num_envs, int32_t num_actions, int32_t horizon, int32_t slot,
+                              float* b_obs, uint8_t* t_dones, float* t_values, float* b_actions, float* b_neglogp,
+                              float* b_mu, float* b_sigma, void* stream) {
+    if (num_envs <= 0 || obs_dim <= 0 || num_actions <= 0 || num_actions > 64 || horizon <= 0 || slot < 0 ||
+        slot >= horizon || values_stride <= 0)
+        return rl_set_error("rl_rollout_pre: bad sizes (num_actions <= 64, 0 <= slot < horizon)");
+    if (!obs || !dones || !values || !actions || !neglogp || !mu || !sigma || !b_obs || !t_dones || !t_values ||
+        !b_actions || !b_neglogp || !b_mu || !b_sigma)
+        return rl_set_error("rl_rollout_pre: null pointer");
+    hipLaunchKernelGGL(k_rollout_pre, dim3((num_envs + 3) / 4), dim3(256), 0, (hipStream_t)stream, obs, (int)obs_dim,
+                       dones, values, (int)values_stride, actions, neglogp, mu, sigma, (int)num_envs, (int)num_actions,
+                       (int)horizon, (int)slot, b_obs, t_dones, t_values, b_actions, b_neglogp, b_mu, b_sigma);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        char msg[256];
+        snprintf(msg, sizeof(msg), "rl_rollout_pre: launch failed: %s", hipGetErrorString(e));
+        return rl_set_error(msg) + 1;
+    }
+    return 0;
+}
+
 // ---------------------------------------------------------------- act forward head
 // models.ModelA2CContinuousLogStd eval forward after the network (fixed sigma), rl/network.py:
 //   sigma = exp(logstd); action = normal(0, 1) * sigma + mu  (the standard normals drawn by torch's

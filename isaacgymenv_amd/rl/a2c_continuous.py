@@ -287,6 +287,7 @@ class A2CAgent:
         self._has_timeouts = False
         # after env.step on the GPU: one fused kernel instead of the static copies + post graph
         self._fused_post = on_gpu
+        self._pre_ok = None  # rl_rollout_pre fits the experience layouts (decided on first use)
         # minibatch loss + gradient as one HIP pass for the fixed-sigma models (every in-scope train
         # config); a learned-sigma head keeps the torch statement of the loss
         net = self.model.a2c_network
@@ -389,35 +390,58 @@ class A2CAgent:
         self.current_rewards *= not_done
         self.current_lengths *= not_done
 
-    def _store_post_fused(self, n, res, rewards, dones, time_outs):
+    def _store_post_fused(self, n, values, rewards, dones, time_outs):
         """_store_post as one HIP kernel (libgymrl rl_rollout_post) reading the env's own output
         buffers: same fp32 arithmetic for the experience rewards, dones and episode counters; the
-        meters' masked sums in the kernel's fixed reduction order."""
+        meters' masked sums in the kernel's fixed reduction order.  values: slot n's value
+        estimates (t_values[n], stored before env.step), for the time-out bootstrap."""
         cfg = self.cfg
         boot = cfg.value_bootstrap and time_outs is not None
-        gae.rollout_post(rewards, dones, time_outs if boot else None, res["values"] if boot else None,
+        gae.rollout_post(rewards, dones, time_outs if boot else None, values if boot else None,
                          cfg.reward_shift, cfg.reward_scale, cfg.gamma, self.dones, self.t_rewards[n],
                          self.current_rewards, self.current_lengths, self.game_rewards.state,
                          self.game_lengths.state, cfg.games_to_track)
+
+    def _store_pre_fused(self, n, obs, res) -> bool:
+        """_store_pre as one HIP kernel (libgymrl rl_rollout_pre); False when the layouts do not fit it."""
+        args = (obs, self.dones, res["values"], res["actions"], res["neglogpacs"], res["mus"], res["sigmas"],
+                self.b_obs, self.t_dones, self.t_values, self.b_actions, self.b_neglogp, self.b_mu, self.b_sigma)
+        if self._pre_ok is None:
+            self._pre_ok = gae.rollout_pre_applies(*args)
+        elif self._pre_ok:  # the act forward's outputs keep their layout; re-check only what varies
+            self._pre_ok = obs.is_contiguous() and obs.shape == self.b_obs.shape[::2] and obs.dtype == torch.float32
+        if not self._pre_ok:
+            return False
+        gae.rollout_pre(n, *args)
+        return True
 
     def play_steps(self):
         cfg = self.cfg
         if self.obs is None:
             self.env_reset()
         graphs = self._step_graphs is not None
+        # The fused bookkeeping of slot n-1 (rl_rollout_post) is issued after slot n's act forward: it
+        # reads only the env's outputs and t_values[n-1], and the forward reads neither, so the GPU gets
+        # the forward one host call sooner.  It must precede slot n's experience (which stores dones).
+        pending = None
         for n in range(self.horizon):
             res = self.get_action_values(self.obs)
-            if graphs:
-                self._step_graphs[n][0].replay()
-            else:
-                self._store_pre(n, self._obs(self.obs), res)
+            if pending is not None:
+                self._store_post_fused(*pending)
+                pending = None
+            obs = self._obs(self.obs)
+            if not (self._fused_post and self._store_pre_fused(n, obs, res)):
+                if graphs:
+                    self._step_graphs[n][0].replay()
+                else:
+                    self._store_pre(n, obs, res)
             actions = res["actions"]
             if cfg.clip_actions:
                 actions = torch.clamp(actions, -1.0, 1.0)  # action space is [-1, 1]: rescale is identity
             self.obs, rewards, dones, infos = self.env.step(actions)
             self._has_timeouts = "time_outs" in infos
             if self._fused_post:
-                self._store_post_fused(n, res, rewards, dones, infos.get("time_outs"))
+                pending = (n, self.t_values[n], rewards, dones, infos.get("time_outs"))
                 continue
             self._s_rew.copy_(rewards)
             self._s_dones.copy_(dones)
@@ -427,6 +451,8 @@ class A2CAgent:
                 self._step_graphs[n][1].replay()
             else:
                 self._store_post(n, res)
+        if pending is not None:
+            self._store_post_fused(*pending)
         last_values = self.get_values(self.obs)[:, 0].contiguous()
         returns, advs, values = discount_values(self.t_rewards, self.t_values, self.t_dones, last_values,
                                                 self.dones.contiguous(), cfg.gamma, cfg.tau)

@@ -19,11 +19,11 @@ EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accu
                     "rl_linear_fwd", "rl_linear_transpose", "rl_linear_bwd", "rl_policy_head", "rl_linear_fwd_g",
                     "rl_linear_bwd_g", "rl_kl_partials_size", "rl_policy_kl", "rl_adaptive_lr",
                     "rl_ppo_heads_partials_size", "rl_ppo_heads_loss", "rl_ppo_heads_loss_backward",
-                    "rl_splitk_accum_multi", "rl_policy_kl_step", "rl_opt_step_h", "rl_rms_normalize_h"]
+                    "rl_splitk_accum_multi", "rl_policy_kl_step", "rl_opt_step_h", "rl_rms_normalize_h", "rl_rollout_pre"]
 _lib = None
 
 
-RL_ABI_VERSION = 6  # include/gymrl.h
+RL_ABI_VERSION = 7  # include/gymrl.h
 
 
 class LinearGroups(C.Structure):
@@ -121,6 +121,9 @@ def lib():
         L.rl_rollout_post.restype = C.c_int
         L.rl_rollout_post.argtypes = [vp, vp, C.c_int32, vp, C.c_int32, vp, C.c_double, C.c_double, C.c_double,
                                       C.c_int32, vp, vp, vp, vp, vp, vp, C.c_int32, vp]
+        L.rl_rollout_pre.restype = C.c_int
+        L.rl_rollout_pre.argtypes = [vp, C.c_int32, vp, vp, C.c_int32, vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_int32,
+                                     C.c_int32, vp, vp, vp, vp, vp, vp, vp, vp]
         L.rl_last_error.restype = C.c_char_p
         L.rl_abi_version.restype = C.c_int
         _lib = L
@@ -209,6 +212,41 @@ def colsum_accum(g: torch.Tensor, grad: torch.Tensor) -> None:
 
 
 _FLAG_BYTES = {torch.bool: 1, torch.uint8: 1, torch.int64: 8}
+
+
+def rollout_pre(n: int, obs, dones, values, actions, neglogp, mu, sigma, b_obs, t_dones, t_values, b_actions,
+                b_neglogp, b_mu, b_sigma) -> None:
+    """play_steps' experience of horizon slot n before env.step as one kernel (include/gymrl.h
+    rl_rollout_pre): b_obs[:, n] = obs, t_dones[n] = dones, t_values[n] = values[:, 0], b_actions /
+    b_neglogp / b_mu / b_sigma[:, n] = actions / neglogp / mu / sigma.  The caller checks layouts
+    once (rollout_pre_applies); this is the per-step call."""
+    N, O = obs.shape
+    H, A = b_obs.shape[1], actions.shape[1]
+    stream = torch.cuda.current_stream(obs.device).cuda_stream
+    rc = lib().rl_rollout_pre(obs.data_ptr(), O, dones.data_ptr(), values.data_ptr(), values.stride(0),
+                              actions.data_ptr(), neglogp.data_ptr(), mu.data_ptr(), sigma.data_ptr(), N, A, H, int(n),
+                              b_obs.data_ptr(), t_dones.data_ptr(), t_values.data_ptr(), b_actions.data_ptr(),
+                              b_neglogp.data_ptr(), b_mu.data_ptr(), b_sigma.data_ptr(), stream)
+    if rc != 0:
+        raise RuntimeError(lib().rl_last_error().decode())
+
+
+def rollout_pre_applies(obs, dones, values, actions, neglogp, mu, sigma, b_obs, t_dones, t_values, b_actions, b_neglogp,
+                        b_mu, b_sigma) -> bool:
+    """The layouts rl_rollout_pre assumes (all on one GPU; the experience buffers as A2CAgent allocates them)."""
+    ts = (obs, dones, values, actions, neglogp, mu, sigma, b_obs, t_dones, t_values, b_actions, b_neglogp, b_mu, b_sigma)
+    if not all(isinstance(t, torch.Tensor) and t.is_cuda and t.device == obs.device for t in ts):
+        return False
+    N, A = actions.shape if actions.dim() == 2 else (-1, -1)
+    f32 = torch.float32
+    return (obs.dim() == 2 and obs.is_contiguous() and obs.dtype == f32 and dones.dtype == torch.uint8
+            and dones.is_contiguous() and dones.numel() == N and values.dtype == f32 and values.dim() == 2
+            and values.shape[0] == N and values.stride(1) == 1 and 0 < A <= 64
+            and all(t.dtype == f32 and t.is_contiguous() and t.shape == (N, A) for t in (actions, mu, sigma))
+            and neglogp.dtype == f32 and neglogp.is_contiguous() and neglogp.numel() == N
+            and all(t.is_contiguous() for t in (b_obs, t_dones, t_values, b_actions, b_neglogp, b_mu, b_sigma))
+            and b_obs.shape[0] == N and b_obs.shape[2] == obs.shape[1] and t_dones.dtype == torch.uint8
+            and b_actions.shape == b_mu.shape == b_sigma.shape == (N, b_obs.shape[1], A))
 
 
 def rollout_post(rewards, dones, time_outs, values, reward_shift: float, reward_scale: float, gamma: float,

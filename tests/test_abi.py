@@ -41,7 +41,7 @@ def test_python_bindings_cover_the_abi():
     assert sorted(gymtask.EXPORTED_SYMBOLS) == _declared("gymtask.h")
     from isaacgymenv_amd.rl import gae
     assert sorted(gae.EXPORTED_SYMBOLS) == _declared("gymrl.h")
-    assert gae.lib().rl_abi_version() == 6
+    assert gae.lib().rl_abi_version() == 7
 
 
 def test_abi_version_and_topology_query():

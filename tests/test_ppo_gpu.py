@@ -217,7 +217,7 @@ def test_rollout_post_kernel_matches_torch_bookkeeping(dones_dtype, boot):
         for n, (rew, dn, to, res) in enumerate(steps):
             h = n % agent.horizon
             if mode == "fused":
-                agent._store_post_fused(h, res, rew, dn, to)
+                agent._store_post_fused(h, res["values"][:, 0], rew, dn, to)
             else:
                 agent._s_rew.copy_(rew)
                 agent._s_dones.copy_(dn)
@@ -232,6 +232,59 @@ def test_rollout_post_kernel_matches_torch_bookkeeping(dones_dtype, boot):
     for k in (3, 4):
         torch.testing.assert_close(f[k], r[k], rtol=1e-5, atol=1e-6)
     assert float(r[4][1]) > 0  # the meters were updated
+
+
+def test_fused_rollout_bookkeeping_equals_torch_statements():
+    """play_steps with the two bookkeeping kernels (rl_rollout_pre before env.step; rl_rollout_post
+    deferred behind the next act forward, bootstrapping from t_values) fills the same experience,
+    bit for bit, as the torch statements in their original order (Cartpole, value bootstrap on)."""
+    runs = []
+    for fused in (False, True):
+        torch.manual_seed(0)
+        agent = _agent("Cartpole", 512, value_bootstrap=True)
+        agent.use_graphs = False
+        agent._fused_post = fused
+        returns, values = agent.play_steps()
+        torch.cuda.synchronize()
+        assert agent._pre_ok is (True if fused else None)
+        runs.append([t.clone() for t in (agent.b_obs, agent.t_dones, agent.t_values, agent.t_rewards, agent.b_actions,
+                                         agent.b_neglogp, agent.b_mu, agent.b_sigma, agent.dones,
+                                         agent.current_rewards, agent.current_lengths, returns, values)])
+    assert float(runs[0][1].float().sum()) > 0  # some episodes ended inside the rollout
+    for k, (a, b) in enumerate(zip(*runs)):
+        assert torch.equal(a, b), k
+
+
+def test_rollout_pre_kernel_matches_torch_experience_copies():
+    """rl_rollout_pre (one kernel before env.step) = the seven torch statements of _store_pre, bit-exact,
+    for every horizon slot of a ragged env count (4096 - 37 envs, 12 actions, 188-wide obs)."""
+    from isaacgymenv_amd.rl import gae
+    N, H, O, A = 4096 - 37, 24, 188, 12
+    gen = torch.Generator(device="cuda").manual_seed(11)
+    mk = lambda *shape: torch.randn(*shape, device="cuda", generator=gen)  # noqa: E731
+    bufs = {"b_obs": torch.zeros(N, H, O, device="cuda"), "t_dones": torch.zeros(H, N, dtype=torch.uint8, device="cuda"),
+            "t_values": torch.zeros(H, N, device="cuda"), "b_actions": torch.zeros(N, H, A, device="cuda"),
+            "b_neglogp": torch.zeros(N, H, device="cuda"), "b_mu": torch.zeros(N, H, A, device="cuda"),
+            "b_sigma": torch.zeros(N, H, A, device="cuda")}
+    want = {k: v.clone() for k, v in bufs.items()}
+    for n in range(H):
+        obs, dones = mk(N, O), (torch.rand(N, device="cuda", generator=gen) < 0.3).to(torch.uint8)
+        res = {"values": mk(N, 1), "actions": mk(N, A), "neglogpacs": mk(N), "mus": mk(N, A), "sigmas": mk(N, A).exp()}
+        args = (obs, dones, res["values"], res["actions"], res["neglogpacs"], res["mus"], res["sigmas"], *bufs.values())
+        assert gae.rollout_pre_applies(*args)
+        gae.rollout_pre(n, *args)
+        want["b_obs"][:, n] = obs
+        want["t_dones"][n] = dones
+        want["t_values"][n] = res["values"][:, 0]
+        want["b_actions"][:, n] = res["actions"]
+        want["b_neglogp"][:, n] = res["neglogpacs"]
+        want["b_mu"][:, n] = res["mus"]
+        want["b_sigma"][:, n] = res["sigmas"]
+    torch.cuda.synchronize()
+    for k in bufs:
+        assert torch.equal(bufs[k], want[k]), k
+    # a layout the kernel does not take is refused (the caller then runs the torch statements)
+    assert not gae.rollout_pre_applies(obs.t(), *args[1:])
 
 
 @pytest.mark.parametrize("rows,cols,dtype,offset", [(16384, 512, torch.float16, 0), (16384, 256, torch.float16, 1),
