@@ -186,6 +186,19 @@ int rl_rollout_post(const float *rewards, const void *dones, int32_t dones_bytes
                     void *stream);
 
 /*
+ * ABI 7 -- the act forward's heads and head in one launch: mu = a W_mu^T + b_mu (W_mu [A][H]), value =
+ * c w_v^T + b_v (w_v [H], b_v [1]) from the actor / critic MLP outputs a, c (rows of H f32, row strides
+ * ld_actor / ld_critic), then rl_policy_head's statements on them (noise [N][A] = torch's normal_ draws,
+ * logstd [A]; value unnormalised when value_mean / value_var are given).  Outputs mu, actions, sigmas
+ * [N][A], neglogp [N], value_out [N].  Each head output is a sequential f32 FMA chain over H.
+ */
+int rl_act_heads(const float *hidden_actor, int32_t ld_actor, const float *hidden_critic, int32_t ld_critic,
+                 int32_t H, const float *w_mu, const float *b_mu, const float *w_v, const float *b_v, const float *noise,
+                 const float *logstd, const double *value_mean, const double *value_var, double value_eps,
+                 int32_t num_envs, int32_t num_actions, float *mu, float *actions, float *sigmas, float *neglogp,
+                 float *value_out, void *stream);
+
+/*
  * ABI 7 -- play_steps' experience of horizon slot `slot` before env.step (rl_games a2c_common.py
  * update_data('obses' / 'dones' / 'values' / 'actions' / 'neglogpacs' / 'mus' / 'sigmas')), one launch:
  *   b_obs[e][slot][:] = obs[e][:]            obs [N][obs_dim] f32, b_obs [N][horizon][obs_dim]
@@ -275,6 +288,15 @@ int rl_linear_fwd_g(const void *x, int32_t M, int32_t K, int32_t ldx, const void
 int rl_linear_bwd_g(const void *dy, const void *y, int32_t M, int32_t N, const void *x, int32_t K, int32_t ldx,
                     const void *w, void *dx, int32_t splits, float *wpart, float *bpart, int64_t pstride,
                     const rl_linear_groups *groups, void *stream);
+/*
+ * ABI 7 -- the rollout's act forward in f32 (rl_games play_steps: no autocast): y = act(x w^T + bias) with f32
+ * operands, products and accumulation (v_mfma_f32_32x32x2_f32; the kernel's own order of the sum, so within f32
+ * rounding of a library GEMM), act = ELU when nonzero.  Same arguments and groups as rl_linear_fwd_g with f32
+ * tensors (the weight is w [N][K] row-major, row stride K).  Requires M % 64, N % 64, K % 4, ldx % 4, ldy % 4 and
+ * 16-byte aligned x / w / y; group strides % 4.
+ */
+int rl_linear_fwd_f32_g(const float *x, int32_t M, int32_t K, int32_t ldx, const float *w, int32_t N,
+                        const float *bias, int32_t act, float *y, const rl_linear_groups *groups, void *stream);
 
 /*
  * ABI 6 -- the minibatch's policy bookkeeping (rl_policy.hip; rl_games a2c_common.py after the optimizer step:

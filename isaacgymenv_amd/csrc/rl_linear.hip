@@ -225,6 +225,122 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(const _Float16* __restrict
   });
 }
 
+// ---------------------------------------------------------------- NT in f32: the rollout's act forward
+// rl_games play_steps runs the act forward in f32 (no autocast).  C[m][c] = act(sum_r A[m][r] Bt[c][r] + bias[c])
+// with f32 operands on v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulation; the order of the sum is this
+// kernel's, so the result agrees with a library f32 GEMM to f32 rounding), bias and ELU in the epilogue.  64 x 64
+// tiles, 4 waves in 2 x 2, one 32 x 32 MFMA tile each; the reduction in stages of 32 through double-buffered LDS
+// (row stride 36 floats).  A lane reads 4 consecutive k of its row (one 16-B LDS read per operand) and feeds them
+// to 4 MFMAs: in MFMA s, half h of the wave carries k = 8 ks + 4 h + s -- the A and Bt fragments use the same map,
+// so every k is summed exactly once.  The output tile goes out through LDS as whole 256-B row segments.
+typedef float f4 __attribute__((ext_vector_type(4)));
+constexpr int kF32Step = 32, kF32Ld = kF32Step + 4;
+
+__device__ __forceinline__ f4 load4f(const float* __restrict__ p, int valid) {
+  if (valid >= 4) return *reinterpret_cast<const f4*>(p);
+  f4 v;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = j < valid ? p[j] : 0.f;
+  return v;
+}
+
+template <bool ACT>
+__global__ __launch_bounds__(kThreads) void k_gemm_nt_f32(const float* __restrict__ A, int lda,
+                                                          const float* __restrict__ Bt, int ldb,
+                                                          const float* __restrict__ bias, float* __restrict__ C,
+                                                          int ldc, int R, int64_t gA, int64_t gB, int64_t gBias,
+                                                          int64_t gC, int MT, int NT) {
+  constexpr int BM = 64, BN = 64, KS = kF32Step, LD = kF32Ld, CPR = KS / 4;
+  constexpr int CA = BM * KS / 4 / kThreads, CB = BN * KS / 4 / kThreads;  // 16-B chunks per thread (2, 2)
+  int gi, mt, nt;
+  tile_of(MT, NT, gi, mt, nt);
+  {
+    const int64_t g = gi;
+    A += g * gA;
+    Bt += g * gB;
+    if (bias) bias += g * gBias;
+    C += g * gC;
+  }
+  __shared__ float sA[2][BM * LD];
+  __shared__ float sB[2][BN * LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = mt * BM, c0 = nt * BN;
+  const int r = lane & 31, hh = lane >> 5;
+  f16v acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+  float bcol[4][4];  // this lane's output columns c0 + 32 wn + 8 g + 4 hh + e
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bcol[g][e] = bias ? bias[c0 + wn * 32 + 8 * g + 4 * hh + e] : 0.f;
+  f4 ra[CA], rb[CB];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int c = tid + i * kThreads, row = c / CPR, kc = (c % CPR) * 4;
+      ra[i] = load4f(A + (size_t)(m0 + row) * lda + k0 + kc, R - (k0 + kc));
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const int c = tid + i * kThreads, row = c / CPR, kc = (c % CPR) * 4;
+      rb[i] = load4f(Bt + (size_t)(c0 + row) * ldb + k0 + kc, R - (k0 + kc));
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int c = tid + i * kThreads, row = c / CPR, kc = (c % CPR) * 4;
+      *reinterpret_cast<f4*>(&sA[buf][row * LD + kc]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const int c = tid + i * kThreads, row = c / CPR, kc = (c % CPR) * 4;
+      *reinterpret_cast<f4*>(&sB[buf][row * LD + kc]) = rb[i];
+    }
+  };
+  const int steps = (R + KS - 1) / KS;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int s = 0; s < steps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < steps) gload((s + 1) * KS);
+#pragma unroll
+    for (int ks = 0; ks < KS / 8; ++ks) {
+      const f4 fa = *reinterpret_cast<const f4*>(&sA[buf][(wm * 32 + r) * LD + ks * 8 + 4 * hh]);
+      const f4 fb = *reinterpret_cast<const f4*>(&sB[buf][(wn * 32 + r) * LD + ks * 8 + 4 * hh]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fb[q], fa[q], acc, 0, 0, 0);
+    }
+    if (s + 1 < steps) lstore(buf ^ 1);
+    __syncthreads();
+  }
+  // epilogue: registers 4g .. 4g+3 are columns 32 wn + 8 g + 4 hh + (0..3) of tile row 32 wm + r
+  constexpr int SLD = BN + 4;
+  static_assert(BM * SLD <= 2 * BM * LD, "the output stage fits the A buffers");
+  float* stage = &sA[0][0];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    f4 ov;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float z = acc[4 * g + e] + bcol[g][e];
+      if constexpr (ACT) z = elu_f(z);
+      ov[e] = z;
+    }
+    *reinterpret_cast<f4*>(stage + (wm * 32 + r) * SLD + wn * 32 + 8 * g + 4 * hh) = ov;
+  }
+  __syncthreads();
+  constexpr int OPR = BN / 4, IT = BM * OPR / kThreads;  // 16 chunks per row, 4 per thread
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int c = tid + it * kThreads, row = c / OPR, cc = (c % OPR) * 4;
+    *reinterpret_cast<f4*>(C + (size_t)(m0 + row) * ldc + c0 + cc) = *reinterpret_cast<const f4*>(stage + row * SLD + cc);
+  }
+}
+
 // ---------------------------------------------------------------- TN: weight / bias gradient partials
 // part[s][n][k] = sum_{m in block s} dZ[m][n] X[m][k] with dZ = dY * elu'(Y) (dY, Y [M][N], X [M][K]);
 // bpart[s][n] = sum_{m in block s} dZ[m][n] (written by the blocks of k-tile 0); consecutive blocks wstride /
@@ -535,6 +651,27 @@ extern "C" int rl_linear_fwd_g(const void* x, int32_t M, int32_t K, int32_t ldx,
     else hipLaunchKernelGGL((k_gemm_nt<64, 128, false>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, ldy, K, gx, gw, gb, gy, MT, NT);
   }
   return launch_fail("rl_linear_fwd");
+}
+
+extern "C" int rl_linear_fwd_f32_g(const float* x, int32_t M, int32_t K, int32_t ldx, const float* w, int32_t N,
+                                   const float* bias, int32_t act, float* y, const rl_linear_groups* grp,
+                                   void* stream) {
+  if (!x || !w || !y || M <= 0 || K <= 0 || N <= 0) return rl_set_error("rl_linear_fwd_f32: null pointer or empty shape");
+  const int G = grp ? grp->groups : 1;
+  const int ldy = grp && grp->ldy ? grp->ldy : N;
+  if (G < 1 || G > 65535 || ldy < N || ldy % 4) return rl_set_error("rl_linear_fwd_f32: bad groups or output row stride");
+  auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (M % 64 || N % 64 || ldx % 4 || K % 4 || ldx < K || !a16(x) || !a16(w) || !a16(y) || (bias && (N % 4)))
+    return rl_set_error("rl_linear_fwd_f32: M % 64, N % 64, K % 4, ldx % 4 and 16-byte aligned x / w / y required");
+  const int64_t gx = grp ? grp->x_gstride : 0, gw = grp ? grp->w_gstride : 0, gb = grp ? grp->b_gstride : 0,
+                gy = grp ? grp->y_gstride : 0;
+  if (G > 1 && ((gx | gw | gy) % 4 != 0)) return rl_set_error("rl_linear_fwd_f32: group strides must be % 4");
+  const int MT = M / 64, NT = N / 64;
+  const dim3 g(MT * NT * G);
+  hipStream_t st = (hipStream_t)stream;
+  if (act) hipLaunchKernelGGL(k_gemm_nt_f32<true>, g, dim3(kThreads), 0, st, x, ldx, w, K, bias, y, ldy, K, gx, gw, gb, gy, MT, NT);
+  else hipLaunchKernelGGL(k_gemm_nt_f32<false>, g, dim3(kThreads), 0, st, x, ldx, w, K, bias, y, ldy, K, gx, gw, gb, gy, MT, NT);
+  return launch_fail("rl_linear_fwd_f32");
 }
 
 extern "C" int rl_linear_fwd(const void* x, int32_t M, int32_t K, int32_t ldx, const void* w, int32_t N,

@@ -228,3 +228,102 @@ extern "C" int rl_policy_head(const float* mu, const float* noise, const float* 
     }
     return 0;
 }
+
+// ---------------------------------------------------------------- act forward heads + head (ABI 7)
+// The two Linear heads on the MLP outputs (mu = a W_mu^T + b_mu, value = c w_v^T + b_v; network.py
+// ActorCriticNetwork.forward) and then rl_policy_head's statements, in one launch: 16 rows per
+// workgroup, their hidden rows and the head weights staged in LDS (row strides padded by one float so
+// the lanes of a dot product fall on different banks), one lane per (row, output) dot product as a
+// sequential f32 FMA chain over H (the library GEMM's order differs: within f32 rounding of it).
+namespace {
+
+constexpr int kHeadRows = 16;
+
+__global__ __launch_bounds__(256) void k_act_heads(const float* __restrict__ ha, int lda, const float* __restrict__ hc,
+                                                   int ldc, int H, const float* __restrict__ w_mu,
+                                                   const float* __restrict__ b_mu, const float* __restrict__ w_v,
+                                                   const float* __restrict__ b_v, const float* __restrict__ noise,
+                                                   const float* __restrict__ logstd, const double* __restrict__ vmean,
+                                                   const double* __restrict__ vvar, float veps, int N, int A,
+                                                   float nlp_const, float* __restrict__ mu_out,
+                                                   float* __restrict__ actions, float* __restrict__ sigmas,
+                                                   float* __restrict__ neglogp, float* __restrict__ value_out) {
+    extern __shared__ float sm[];
+    const int SH = 2 * H + 1, SW = H + 1, O = A + 1;
+    float* sh = sm;                     // [kHeadRows][SH]: actor hidden | critic hidden
+    float* sw = sh + kHeadRows * SH;    // [O][SW]: the A mu rows, then the value row
+    float* so = sw + O * SW;            // [kHeadRows][O]: mu | value
+    const int r0 = blockIdx.x * kHeadRows;
+    const int nr = min(kHeadRows, N - r0);
+    for (int i = threadIdx.x; i < nr * 2 * H; i += blockDim.x) {
+        const int r = i / (2 * H), k = i - r * 2 * H;
+        sh[r * SH + k] = k < H ? ha[(size_t)(r0 + r) * lda + k] : hc[(size_t)(r0 + r) * ldc + (k - H)];
+    }
+    for (int i = threadIdx.x; i < O * H; i += blockDim.x) {
+        const int o = i / H, k = i - o * H;
+        sw[o * SW + k] = o < A ? w_mu[(size_t)o * H + k] : w_v[k];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < nr * O; t += blockDim.x) {
+        const int r = t / O, o = t - r * O;
+        const float* h = sh + r * SH + (o < A ? 0 : H);
+        const float* w = sw + o * SW;
+        float acc = 0.f;
+        for (int k = 0; k < H; ++k) acc = fmaf(h[k], w[k], acc);
+        so[r * O + o] = acc + (o < A ? b_mu[o] : b_v[0]);
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < nr) {
+        const int r = threadIdx.x, i = r0 + r;
+        float sq = 0.f, sls = 0.f;
+        for (int a = 0; a < A; ++a) {  // rl_policy_head's statements, in its order
+            const size_t k = (size_t)i * A + a;
+            const float ls = logstd[a];
+            const float sg = expf(ls);
+            const float m = so[r * O + a];
+            const float x = noise[k] * sg + m;
+            mu_out[k] = m;
+            actions[k] = x;
+            sigmas[k] = sg;
+            const float z = (x - m) / sg;
+            sq += z * z;
+            sls += ls;
+        }
+        neglogp[i] = 0.5f * sq + nlp_const + sls;
+        float v = so[r * O + A];
+        if (vmean) {
+            v = fminf(fmaxf(v, -5.f), 5.f);
+            v = sqrtf((float)vvar[0] + veps) * v + (float)vmean[0];
+        }
+        value_out[i] = v;
+    }
+}
+
+}  // namespace
+
+extern "C" int rl_act_heads(const float* hidden_actor, int32_t ld_actor, const float* hidden_critic, int32_t ld_critic,
+                            int32_t H, const float* w_mu, const float* b_mu, const float* w_v, const float* b_v,
+                            const float* noise, const float* logstd, const double* value_mean, const double* value_var,
+                            double value_eps, int32_t num_envs, int32_t num_actions, float* mu, float* actions,
+                            float* sigmas, float* neglogp, float* value_out, void* stream) {
+    if (num_envs <= 0 || num_actions <= 0 || H <= 0 || ld_actor < H || ld_critic < H)
+        return rl_set_error("rl_act_heads: bad sizes");
+    if (!hidden_actor || !hidden_critic || !w_mu || !b_mu || !w_v || !b_v || !noise || !logstd || !mu || !actions ||
+        !sigmas || !neglogp || !value_out || (!value_mean) != (!value_var))
+        return rl_set_error("rl_act_heads: null pointer");
+    const size_t lds = sizeof(float) * ((size_t)kHeadRows * (2 * H + 1) + (size_t)(num_actions + 1) * (H + 1) +
+                                        (size_t)kHeadRows * (num_actions + 1));
+    if (lds > 64 * 1024) return rl_set_error("rl_act_heads: H / num_actions too large for the LDS stage");
+    const double c = 0.5 * 1.8378770664093453 * num_actions;  // as rl_policy_head
+    hipLaunchKernelGGL(k_act_heads, dim3((num_envs + kHeadRows - 1) / kHeadRows), dim3(256), lds, (hipStream_t)stream,
+                       hidden_actor, (int)ld_actor, hidden_critic, (int)ld_critic, (int)H, w_mu, b_mu, w_v, b_v, noise,
+                       logstd, value_mean, value_var, (float)value_eps, (int)num_envs, (int)num_actions, (float)c, mu,
+                       actions, sigmas, neglogp, value_out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        char msg[256];
+        snprintf(msg, sizeof(msg), "rl_act_heads: launch failed: %s", hipGetErrorString(e));
+        return rl_set_error(msg) + 1;
+    }
+    return 0;
+}

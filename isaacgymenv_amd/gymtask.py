@@ -384,6 +384,7 @@ class AnymalTailKernels:
         self._draws = None
         self._ep_keys = ["rew_" + name for name in self.TERMS]
         self._terrain_level = None
+        self._pending_extras = None  # (episode buffer, terrain) of a reset whose extras are not built yet
         self._b = None
         self._bound = None
         # (struct field, task attribute) of the buffers whose storage the kernels use
@@ -539,7 +540,7 @@ class AnymalTailKernels:
         t.extras["episode"]["terrain_level"] = self._terrain_level
         self._keep = (ids, pos_offset, vel, cx, cy, ch)
 
-    def reset_flagged(self, k: int, rand_unit=None):
+    def reset_flagged(self, k: int, rand_unit=None, defer_extras: bool = False):
         """reset_idx for the k envs the last post_a flagged, in one kernel (plane and trimesh terrain).
 
         Draws u ~ U[0,1) with ``rand_unit(shape, device)`` in the reference's order and shapes
@@ -594,14 +595,27 @@ class AnymalTailKernels:
                                              float(t.max_episode_length_s), self.reset_scratch.data_ptr(),
                                              self._stream()), "gt_anymal_reset_flagged")
         t._set_reset_state(ids)
+        self._keep = (u, ids)
+        # extras["episode"] (fresh 0-d tensors per reset, as the reference's torch.mean results): with
+        # defer_extras the caller builds it with finish_reset() once the next launches are queued
+        self._pending_extras = (ep, tr is not None)
+        if not defer_extras:
+            self.finish_reset()
+
+    def finish_reset(self):
+        """extras["episode"] of the last reset_flagged(defer_extras=True); a no-op when none is pending."""
+        pend, self._pending_extras = self._pending_extras, None
+        if pend is None:
+            return
+        ep, has_terrain = pend
+        t = self.task
         t.extras["episode"] = dict(zip(self._ep_keys, ep[:len(self.TERMS)].unbind()))
-        if tr is not None:
+        if has_terrain:
             t.extras["episode"]["terrain_level"] = ep[len(self.TERMS)]
         else:
             if self._terrain_level is None:
                 self._terrain_level = torch.mean(t.terrain_levels.float())
             t.extras["episode"]["terrain_level"] = self._terrain_level
-        self._keep = (u, ids)
 
     def _terrain_reset(self):
         """gt_anymal_terrain_reset over the task's curriculum tensors (rebuilt when the task rebinds one)."""

@@ -556,10 +556,14 @@ class Sim:
     def set_state(self, kind: str, src, idx=None, n: int = 0):
         import torch
         L, s = _lib.lib(), self.stream()
-        src = src.to(self.sim_device, dtype=torch.float32).contiguous()
+        dev = self.sim_device
+        # (the per-reset call: tensors already on the sim's device, typed and contiguous skip the conversions)
+        if not (src.dtype == torch.float32 and src.device == dev and src.is_contiguous()):
+            src = src.to(dev, dtype=torch.float32).contiguous()
         idx_ptr = None
         if idx is not None:
-            idx = idx.to(self.sim_device, dtype=torch.int32).contiguous()
+            if not (idx.dtype == torch.int32 and idx.device == dev and idx.is_contiguous()):
+                idx = idx.to(dev, dtype=torch.int32).contiguous()
             n = int(n) if n else idx.numel()
             idx_ptr = idx.data_ptr()
             if n == 0:

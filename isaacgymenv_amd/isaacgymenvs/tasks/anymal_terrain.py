@@ -467,8 +467,9 @@ class AnymalTerrain(VecTask):
                 k = kern.last_reset_count
                 if snap is not None:
                     kern.rng_restore(snap)
-                kern.reset_flagged(k, torch_rand_unit)  # reset_idx without nonzero / host sync
+                kern.reset_flagged(k, torch_rand_unit, defer_extras=True)  # reset_idx without nonzero / host sync
                 kern.observe()
+                kern.finish_reset()  # extras["episode"], built while the GPU runs the observation kernel
             return
         self.progress_buf += 1
         self.randomize_buf += 1

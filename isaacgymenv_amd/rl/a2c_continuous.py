@@ -288,6 +288,8 @@ class A2CAgent:
         # after env.step on the GPU: one fused kernel instead of the static copies + post graph
         self._fused_post = on_gpu
         self._pre_ok = None  # rl_rollout_pre fits the experience layouts (decided on first use)
+        self._post_checked = False  # rl_rollout_post has checked the agent's own output buffers
+        self._t_rew_rows, self._t_val_rows = self.t_rewards.unbind(0), self.t_values.unbind(0)  # per-slot views
         # minibatch loss + gradient as one HIP pass for the fixed-sigma models (every in-scope train
         # config); a learned-sigma head keeps the torch statement of the loss
         net = self.model.a2c_network
@@ -398,9 +400,10 @@ class A2CAgent:
         cfg = self.cfg
         boot = cfg.value_bootstrap and time_outs is not None
         gae.rollout_post(rewards, dones, time_outs if boot else None, values if boot else None,
-                         cfg.reward_shift, cfg.reward_scale, cfg.gamma, self.dones, self.t_rewards[n],
+                         cfg.reward_shift, cfg.reward_scale, cfg.gamma, self.dones, self._t_rew_rows[n],
                          self.current_rewards, self.current_lengths, self.game_rewards.state,
-                         self.game_lengths.state, cfg.games_to_track)
+                         self.game_lengths.state, cfg.games_to_track, outputs_checked=self._post_checked)
+        self._post_checked = True
 
     def _store_pre_fused(self, n, obs, res) -> bool:
         """_store_pre as one HIP kernel (libgymrl rl_rollout_pre); False when the layouts do not fit it."""
@@ -441,7 +444,7 @@ class A2CAgent:
             self.obs, rewards, dones, infos = self.env.step(actions)
             self._has_timeouts = "time_outs" in infos
             if self._fused_post:
-                pending = (n, self.t_values[n], rewards, dones, infos.get("time_outs"))
+                pending = (n, self._t_val_rows[n], rewards, dones, infos.get("time_outs"))
                 continue
             self._s_rew.copy_(rewards)
             self._s_dones.copy_(dones)

@@ -19,7 +19,8 @@ EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accu
                     "rl_linear_fwd", "rl_linear_transpose", "rl_linear_bwd", "rl_policy_head", "rl_linear_fwd_g",
                     "rl_linear_bwd_g", "rl_kl_partials_size", "rl_policy_kl", "rl_adaptive_lr",
                     "rl_ppo_heads_partials_size", "rl_ppo_heads_loss", "rl_ppo_heads_loss_backward",
-                    "rl_splitk_accum_multi", "rl_policy_kl_step", "rl_opt_step_h", "rl_rms_normalize_h", "rl_rollout_pre"]
+                    "rl_splitk_accum_multi", "rl_policy_kl_step", "rl_opt_step_h", "rl_rms_normalize_h", "rl_rollout_pre",
+                    "rl_linear_fwd_f32_g", "rl_act_heads"]
 _lib = None
 
 
@@ -85,6 +86,8 @@ def lib():
             getattr(L, f).restype = C.c_int
         L.rl_linear_fwd_g.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int32, vp, C.c_int32, vp,
                                       C.POINTER(LinearGroups), vp]
+        L.rl_linear_fwd_f32_g.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int32, vp, C.c_int32, vp,
+                                          C.POINTER(LinearGroups), vp]
         L.rl_linear_bwd_g.argtypes = [vp, vp, C.c_int32, C.c_int32, vp, C.c_int32, C.c_int32, vp, vp, C.c_int32, vp,
                                       vp, C.c_int64, C.POINTER(LinearGroups), vp]
         L.rl_ppo_heads_partials_size.restype = C.c_int
@@ -121,6 +124,9 @@ def lib():
         L.rl_rollout_post.restype = C.c_int
         L.rl_rollout_post.argtypes = [vp, vp, C.c_int32, vp, C.c_int32, vp, C.c_double, C.c_double, C.c_double,
                                       C.c_int32, vp, vp, vp, vp, vp, vp, C.c_int32, vp]
+        L.rl_act_heads.restype = C.c_int
+        L.rl_act_heads.argtypes = [vp, C.c_int32, vp, C.c_int32, C.c_int32, vp, vp, vp, vp, vp, vp, vp, vp, C.c_double,
+                                   C.c_int32, C.c_int32, vp, vp, vp, vp, vp, vp]
         L.rl_rollout_pre.restype = C.c_int
         L.rl_rollout_pre.argtypes = [vp, C.c_int32, vp, vp, C.c_int32, vp, vp, vp, vp, C.c_int32, C.c_int32, C.c_int32,
                                      C.c_int32, vp, vp, vp, vp, vp, vp, vp, vp]
@@ -251,25 +257,30 @@ def rollout_pre_applies(obs, dones, values, actions, neglogp, mu, sigma, b_obs, 
 
 def rollout_post(rewards, dones, time_outs, values, reward_shift: float, reward_scale: float, gamma: float,
                  dones_out, rewards_out, current_rewards, current_lengths, meter_rewards, meter_lengths,
-                 games_to_track: int) -> None:
+                 games_to_track: int, outputs_checked: bool = False) -> None:
     """rl_games play_steps after env.step as one kernel (include/gymrl.h rl_rollout_post).
     rewards f32 [N]; dones / time_outs bool, uint8 or int64 [N] (time_outs None: no value bootstrap);
     values f32 [N] or [N, 1] or None; dones_out u8 [N]; rewards_out, current_* f32 [N];
-    meter_* f32 [2] = (mean, current_size)."""
+    meter_* f32 [2] = (mean, current_size).  outputs_checked: the caller's own buffers (dones_out ..
+    meter_lengths) passed these checks before and are unchanged -- only the env's tensors are checked
+    (the per-step call of the rollout loop)."""
     N = rewards.shape[0]
     dev = rewards.device
     if dones.dtype not in _FLAG_BYTES:
         dones = dones.to(torch.uint8)
     if time_outs is not None and time_outs.dtype not in _FLAG_BYTES:
         time_outs = time_outs.to(torch.uint8)
-    for t in (rewards, dones, dones_out, rewards_out, current_rewards, current_lengths, meter_rewards, meter_lengths,
-              time_outs, values):
+    ins = (rewards, dones, time_outs, values)
+    for t in ins if outputs_checked else ins + (dones_out, rewards_out, current_rewards, current_lengths,
+                                                 meter_rewards, meter_lengths):
         if t is not None:
             assert t.is_cuda and t.device == dev and t.is_contiguous()
-    assert rewards.dtype == rewards_out.dtype == current_rewards.dtype == current_lengths.dtype == torch.float32
-    assert dones_out.dtype == torch.uint8 and dones.numel() == N and dones_out.numel() == N
-    assert rewards_out.numel() == N and current_rewards.numel() == N and current_lengths.numel() == N
-    assert meter_rewards.numel() == 2 and meter_lengths.numel() == 2
+    assert rewards.dtype == torch.float32 and dones.numel() == N
+    if not outputs_checked:
+        assert rewards_out.dtype == current_rewards.dtype == current_lengths.dtype == torch.float32
+        assert dones_out.dtype == torch.uint8 and dones_out.numel() == N
+        assert rewards_out.numel() == N and current_rewards.numel() == N and current_lengths.numel() == N
+        assert meter_rewards.numel() == 2 and meter_lengths.numel() == 2
     assert (time_outs is None) == (values is None), "value bootstrap needs both time_outs and values"
     if values is not None:
         assert values.dtype == torch.float32 and values.numel() == N and time_outs.numel() == N
@@ -468,6 +479,43 @@ def policy_head(mu, noise, logstd, value, value_rms=None):
     return actions, sigmas, neglogp, vout
 
 
+def act_heads_applies(a_out, c_out, w_mu, b_mu, w_v, b_v, logstd) -> bool:
+    """The layouts rl_act_heads takes: f32 rows on one GPU, unit column stride, one value output."""
+    ts = (a_out, c_out, w_mu, b_mu, w_v, b_v, logstd)
+    if not all(isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32 and t.device == a_out.device
+               for t in ts):
+        return False
+    H = a_out.shape[1] if a_out.dim() == 2 else -1
+    A = w_mu.shape[0]
+    return (c_out.dim() == 2 and c_out.shape == a_out.shape and a_out.stride(1) == 1 and c_out.stride(1) == 1
+            and w_mu.shape == (A, H) and w_mu.is_contiguous() and b_mu.numel() == A and w_v.numel() == H
+            and w_v.is_contiguous() and b_v.numel() == 1 and logstd.numel() == A and logstd.is_contiguous()
+            and 4 * (16 * (2 * H + 1) + (A + 1) * (H + 1) + 16 * (A + 1)) <= 64 * 1024)
+
+
+def act_heads(a_out, c_out, w_mu, b_mu, w_v, b_v, noise, logstd, value_rms=None):
+    """Act-forward heads + head (include/gymrl.h rl_act_heads): returns (mu [N, A], actions [N, A], sigmas [N, A],
+    neglogp [N], values [N, 1]); the caller checked act_heads_applies.  noise [N, A] = torch's normal_ draws."""
+    N, H = a_out.shape
+    A = w_mu.shape[0]
+    dev = a_out.device
+    mu, actions, sigmas = (torch.empty(N, A, dtype=torch.float32, device=dev) for _ in range(3))
+    neglogp = torch.empty(N, dtype=torch.float32, device=dev)
+    vout = torch.empty(N, 1, dtype=torch.float32, device=dev)
+    vm = vv = None
+    eps = 0.0
+    if value_rms is not None:
+        assert value_rms.running_mean.numel() == 1
+        vm, vv, eps = value_rms.running_mean.data_ptr(), value_rms.running_var.data_ptr(), value_rms.epsilon
+    rc = lib().rl_act_heads(a_out.data_ptr(), a_out.stride(0), c_out.data_ptr(), c_out.stride(0), H, w_mu.data_ptr(),
+                            b_mu.data_ptr(), w_v.data_ptr(), b_v.data_ptr(), noise.data_ptr(), logstd.data_ptr(), vm, vv,
+                            float(eps), N, A, mu.data_ptr(), actions.data_ptr(), sigmas.data_ptr(), neglogp.data_ptr(),
+                            vout.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"rl_act_heads failed: {lib().rl_last_error().decode()}")
+    return mu, actions, sigmas, neglogp, vout
+
+
 def opt_step(param, grad, exp_avg, exp_avg_sq, step, lr, scale, growth_tracker, hyper: OptHyper, partials) -> None:
     """The minibatch optimizer step on flat f32 buffers (include/gymrl.h rl_opt_step): unscale, found-inf,
     norm clip, Adam, GradScaler update; scale / growth_tracker None = no loss scaling."""
@@ -521,6 +569,16 @@ def linear_fwd_grouped(x, ldx: int, K: int, w_half, N: int, b_half, act: bool, y
     _check(lib().rl_linear_fwd_g(x.data_ptr(), M, K, ldx, w_half.data_ptr(), N,
                                  b_half.data_ptr() if b_half is not None else None, int(act), y.data_ptr(), C.byref(g),
                                  torch.cuda.current_stream().cuda_stream), "rl_linear_fwd_g")
+
+
+def linear_fwd_f32(x, ldx: int, K: int, w, N: int, b, act: bool, y, ldy: int, M: int, groups: int = 1,
+                   x_gstride: int = 0, w_gstride: int = 0, b_gstride: int = 0, y_gstride: int = 0):
+    """rl_linear_fwd_f32_g: y = act(x w^T + b) in f32 on the matrix cores, `groups` equal-shaped layers in one launch
+    (tensors are base pointers of group 0; strides in elements, include/gymrl.h)."""
+    g = LinearGroups(groups, ldy, 0, 0, x_gstride, w_gstride, b_gstride, y_gstride, 0, 0, 0)
+    _check(lib().rl_linear_fwd_f32_g(x.data_ptr(), M, K, ldx, w.data_ptr(), N, b.data_ptr() if b is not None else None,
+                                     int(act), y.data_ptr(), C.byref(g), torch.cuda.current_stream().cuda_stream),
+           "rl_linear_fwd_f32_g")
 
 
 def linear_bwd_grouped(dy, y, ldy: int, y_gstride: int, M: int, N: int, x, ldx: int, x_gstride: int, K: int, w,

@@ -225,11 +225,26 @@ class GroupedMLPSpec:
                                       flat_param[o + G * N * K:o + G * (N * K + N)].view(G, N)))
 
     def act_forward(self, x):
-        """The G MLPs in f32 without autograd (the rollout's act forward, rl_games play_steps: no autocast): layer 0
-        one library GEMM over the stacked weights, the later layers one batched GEMM, one ELU per layer for all G
-        networks.  Returns the G hidden outputs."""
+        """The G MLPs in f32 without autograd (the rollout's act forward, rl_games play_steps: no autocast).  On the
+        matrix-core path (rl_linear_fwd_f32_g, include/gymrl.h ABI 7) each layer of all G networks is ONE launch with
+        the bias and ELU in its epilogue: layer 0 over the stacked [G*N][K] weight, the later layers grouped, the
+        activations [M][G*N] (group g in columns g*N ..).  Otherwise layer 0 is one library GEMM over the stacked
+        weights and the later layers one batched GEMM, with one ELU pass per layer.  Returns the G hidden outputs."""
         import torch.nn.functional as F
         G, M = self.G, x.shape[0]
+        if self._mfma_f32_applies(x):
+            w0, b0 = self.layers32[0]
+            n0, k0 = w0.shape[1], w0.shape[2]
+            y = torch.empty(M, G * n0, dtype=torch.float32, device=x.device)
+            gae.linear_fwd_f32(x, x.stride(0), k0, w0, G * n0, b0, True, y, G * n0, M)
+            for w, b in self.layers32[1:]:
+                n, k = w.shape[1], w.shape[2]
+                z = torch.empty(M, G * n, dtype=torch.float32, device=x.device)
+                gae.linear_fwd_f32(y, G * k, k, w, n, b, True, z, G * n, M, groups=G, x_gstride=k, w_gstride=n * k,
+                                   b_gstride=n, y_gstride=n)
+                y = z
+            n = self.layers32[-1][0].shape[1]
+            return tuple(y[:, g * n:(g + 1) * n] for g in range(G))
         w0, b0 = self.layers32[0]
         y = torch.addmm(b0.reshape(-1), x, w0.reshape(-1, w0.shape[2]).t())
         F.elu(y, inplace=True)
@@ -238,6 +253,18 @@ class GroupedMLPSpec:
             y = torch.baddbmm(b.unsqueeze(1), y, w.transpose(1, 2))
             F.elu(y, inplace=True)
         return tuple(y[g] for g in range(G))
+
+    def _mfma_f32_applies(self, x) -> bool:
+        """The shapes and alignments rl_linear_fwd_f32_g takes (rows % 64, widths % 64, 16-byte rows)."""
+        if not USE_MFMA_LAYERS or x.shape[0] % 64 or x.stride(1) != 1 or x.stride(0) % 4 or x.data_ptr() % 16:
+            return False
+        k_in = x.shape[1]
+        for w, b in self.layers32:
+            n, k = w.shape[1], w.shape[2]
+            if n % 64 or k % 4 or k != k_in or w.data_ptr() % 16 or not (w.is_contiguous() and b.is_contiguous()):
+                return False
+            k_in = n
+        return True
 
     def act_applies(self, x) -> bool:
         return (bool(self.layers32) and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2
@@ -464,11 +491,19 @@ class ModelA2CContinuousLogStd(nn.Module):
             # act forward on the device: the network, torch's normal_ draws, then one kernel for the head
             obs = self.norm_obs(raw)
             a_out, c_out = net.hidden(obs)
+            vms = self.value_mean_std if self.normalize_value else None
+            heads = (a_out, c_out, net.mu.weight, net.mu.bias, net.value.weight, net.value.bias, net.sigma)
+            if USE_MFMA_LAYERS and net.value.out_features == 1 and gae.act_heads_applies(*heads):
+                # both heads and the head in one launch (rl_act_heads); the normal_ draws are the same
+                # [N, A] call the torch statement makes after mu, so the RNG stream is unchanged
+                noise = torch.empty(a_out.shape[0], net.mu.out_features, dtype=torch.float32,
+                                    device=a_out.device).normal_(0.0, 1.0)
+                mu, actions, sigmas, neglogp, values = gae.act_heads(*heads[:6], noise, net.sigma.detach(), vms)
+                return {"neglogpacs": neglogp, "values": values, "actions": actions, "mus": mu, "sigmas": sigmas}
             value = net.value(c_out).contiguous()
             mu = net.mu(a_out).contiguous()
             noise = torch.empty_like(mu).normal_(0.0, 1.0)
-            actions, sigmas, neglogp, values = gae.policy_head(
-                mu, noise, net.sigma.detach(), value, self.value_mean_std if self.normalize_value else None)
+            actions, sigmas, neglogp, values = gae.policy_head(mu, noise, net.sigma.detach(), value, vms)
             return {"neglogpacs": neglogp, "values": values, "actions": actions, "mus": mu, "sigmas": sigmas}
         obs = self.norm_obs(raw)
         mu, logstd, value = self.a2c_network(obs)

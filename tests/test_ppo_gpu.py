@@ -411,8 +411,10 @@ def test_policy_head_kernel_matches_torch_act_forward():
         act = torch.empty_like(mu).normal_(0.0, 1.0).mul_(sigma).add_(mu)
         nlp = model.neglogp(act, mu, sigma, logstd)
         val = model.denorm_value(value)
-    assert torch.equal(fused["actions"], act) and torch.equal(fused["sigmas"], sigma)
-    assert torch.equal(fused["values"], val) and torch.equal(fused["mus"], mu)
+    # the heads are rl_act_heads' FMA chains, the torch statement's a library GEMM: f32 rounding apart
+    assert torch.equal(fused["sigmas"], sigma)
+    for k, ref in (("mus", mu), ("actions", act), ("values", val)):
+        torch.testing.assert_close(fused[k], ref, rtol=1e-5, atol=2e-6, msg=k)
     torch.testing.assert_close(fused["neglogpacs"], nlp, rtol=1e-5, atol=1e-5)
 
 
@@ -770,6 +772,66 @@ def test_grouped_mlp_matches_separate_networks_bit_for_bit(monkeypatch):
         assert torch.equal(outs[True][2][n], g), n
 
 
+@pytest.mark.parametrize("vnorm", [True, False])
+def test_act_heads_kernel(vnorm):
+    """rl_act_heads: the two heads exact on small-integer data (every FMA exact: equal to the float64
+    product whatever the order), on strided hidden rows (the grouped act forward's [N][2H] layout, critic
+    columns second); the head statements bit-identical to rl_policy_head given the same mu and value."""
+    from isaacgymenv_amd.rl import gae
+    from isaacgymenv_amd.rl.running_mean_std import RunningMeanStd
+    gen = torch.Generator().manual_seed(9)
+    N, H, A = 4096 - 37, 128, 12
+    ri = lambda lo, hi, *shape: torch.randint(lo, hi, shape, generator=gen).float()  # noqa: E731
+    hid = ri(-4, 5, N, 2 * H).cuda()
+    a_out, c_out = hid[:, :H], hid[:, H:]
+    w_mu, b_mu, w_v, b_v = ri(-3, 4, A, H).cuda(), ri(-8, 9, A).cuda(), ri(-3, 4, 1, H).cuda(), ri(-8, 9, 1).cuda()
+    logstd = (torch.randn(A, generator=gen) * 0.3).cuda()
+    noise = torch.randn(N, A, generator=gen).cuda()
+    vms = None
+    if vnorm:
+        vms = RunningMeanStd((1,)).cuda()
+        vms.running_mean.fill_(0.25)
+        vms.running_var.fill_(4.0)
+    assert gae.act_heads_applies(a_out, c_out, w_mu, b_mu, w_v, b_v, logstd)
+    mu, actions, sigmas, neglogp, values = gae.act_heads(a_out, c_out, w_mu, b_mu, w_v, b_v, noise, logstd, vms)
+    want_mu = a_out.cpu().double() @ w_mu.cpu().double().t() + b_mu.cpu().double()
+    want_v = c_out.cpu().double() @ w_v.cpu().double().t() + b_v.cpu().double()
+    assert torch.equal(mu.cpu().double(), want_mu)
+    ref = gae.policy_head(mu, noise, logstd, want_v.float().cuda().contiguous(), vms)
+    for got, exp in zip((actions, sigmas, neglogp, values), ref):
+        assert torch.equal(got, exp)
+
+
+def test_linear_f32_kernel_exact_on_integers_and_elu():
+    """rl_linear_fwd_f32_g (the rollout's f32 act-forward layer): with small-integer data every product and partial
+    sum is exact in f32, so the kernel equals the float64 product bit for bit whatever its summation order -- this
+    pins the MFMA operand maps, the K tail (188 = 5 x 32 + 28), the grouping strides and the bias; with random data
+    the ELU epilogue agrees with torch's f32 addmm + elu to f32 rounding."""
+    from isaacgymenv_amd.rl import gae
+    import torch.nn.functional as F
+    gen = torch.Generator().manual_seed(5)
+    M, K0, N0, N1, G = 256, 188, 128, 64, 2
+    ri = lambda lo, hi, *shape: torch.randint(lo, hi, shape, generator=gen).float()  # noqa: E731
+    x, w0, b0 = ri(-4, 5, M, K0), ri(-4, 5, G, N0, K0), ri(-8, 9, G, N0)
+    w1, b1 = ri(-3, 4, G, N1, N0), ri(-8, 9, G, N1)
+    xd, w0d, b0d, w1d, b1d = (t.cuda() for t in (x, w0, b0, w1, b1))
+    y0 = torch.empty(M, G * N0, device="cuda")
+    gae.linear_fwd_f32(xd, K0, K0, w0d, G * N0, b0d, False, y0, G * N0, M)
+    want0 = (x.double() @ w0.reshape(G * N0, K0).double().t() + b0.reshape(-1).double())
+    assert torch.equal(y0.cpu().double(), want0)
+    y1 = torch.empty(M, G * N1, device="cuda")
+    gae.linear_fwd_f32(y0, G * N0, N0, w1d, N1, b1d, False, y1, G * N1, M, groups=G, x_gstride=N0,
+                       w_gstride=N1 * N0, b_gstride=N1, y_gstride=N1)
+    for g in range(G):
+        want1 = want0[:, g * N0:(g + 1) * N0] @ w1[g].double().t() + b1[g].double()
+        assert torch.equal(y1[:, g * N1:(g + 1) * N1].cpu().double(), want1), g
+    xr = torch.randn(M, K0, generator=gen).cuda()
+    wr, br = (torch.randn(G * N0, K0, generator=gen) * 0.1).cuda(), torch.randn(G * N0, generator=gen).cuda()
+    ye = torch.empty(M, G * N0, device="cuda")
+    gae.linear_fwd_f32(xr, K0, K0, wr, G * N0, br, True, ye, G * N0, M)
+    torch.testing.assert_close(ye, F.elu(torch.addmm(br, xr, wr.t())), rtol=1e-5, atol=1e-5)
+
+
 def test_grouped_act_forward_matches_separate_networks():
     """The rollout's act forward (f32, no autograd, no autocast) under the grouped layout: layer 0 one addmm over the
     stacked actor / critic weights, later layers one baddbmm (GroupedMLPSpec.act_forward) against each torch MLP on
@@ -787,7 +849,7 @@ def test_grouped_act_forward_matches_separate_networks():
     _flat_net(net, head + [p_ for p_ in net.parameters() if id(p_) not in ids], True)
     x = torch.randn(4096, 188, device="cuda")
     with torch.no_grad():
-        assert net.grouped.act_applies(x)
+        assert net.grouped.act_applies(x) and net.grouped._mfma_f32_applies(x)
         a_g, c_g = net.hidden(x)
         a_r, c_r = base.actor_mlp(x), base.critic_mlp(x)
         mu_g, logstd_g, v_g = net(x)
