@@ -190,7 +190,7 @@ int rl_rollout_post(const float *rewards, const void *dones, int32_t dones_bytes
  * c w_v^T + b_v (w_v [H], b_v [1]) from the actor / critic MLP outputs a, c (rows of H f32, row strides
  * ld_actor / ld_critic), then rl_policy_head's statements on them (noise [N][A] = torch's normal_ draws,
  * logstd [A]; value unnormalised when value_mean / value_var are given).  Outputs mu, actions, sigmas
- * [N][A], neglogp [N], value_out [N].  Each head output is a sequential f32 FMA chain over H.
+ * [N][A], neglogp [N], value_out [N].  Each head output: four f32 FMA chains over k mod 4, added pairwise.
  */
 int rl_act_heads(const float *hidden_actor, int32_t ld_actor, const float *hidden_critic, int32_t ld_critic,
                  int32_t H, const float *w_mu, const float *b_mu, const float *w_v, const float *b_v, const float *noise,

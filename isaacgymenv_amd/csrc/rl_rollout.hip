@@ -234,7 +234,8 @@ extern "C" int rl_policy_head(const float* mu, const float* noise, const float* 
 // ActorCriticNetwork.forward) and then rl_policy_head's statements, in one launch: 16 rows per
 // workgroup, their hidden rows and the head weights staged in LDS (row strides padded by one float so
 // the lanes of a dot product fall on different banks), one lane per (row, output) dot product as a
-// sequential f32 FMA chain over H (the library GEMM's order differs: within f32 rounding of it).
+// f32 FMA chains over H, four interleaved (k mod 4) and added pairwise (the library GEMM's order differs:
+// within f32 rounding of it).
 namespace {
 
 constexpr int kHeadRows = 16;
@@ -268,9 +269,15 @@ __global__ __launch_bounds__(256) void k_act_heads(const float* __restrict__ ha,
         const int r = t / O, o = t - r * O;
         const float* h = sh + r * SH + (o < A ? 0 : H);
         const float* w = sw + o * SW;
-        float acc = 0.f;
-        for (int k = 0; k < H; ++k) acc = fmaf(h[k], w[k], acc);
-        so[r * O + o] = acc + (o < A ? b_mu[o] : b_v[0]);
+        // four interleaved FMA chains (k mod 4), added pairwise: a quarter of the dependent latency
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        int k = 0;
+        for (; k + 4 <= H; k += 4) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[q] = fmaf(h[k + q], w[k + q], acc[q]);
+        }
+        for (; k < H; ++k) acc[k & 3] = fmaf(h[k], w[k], acc[k & 3]);
+        so[r * O + o] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + (o < A ? b_mu[o] : b_v[0]);
     }
     __syncthreads();
     if ((int)threadIdx.x < nr) {

@@ -277,6 +277,7 @@ class A2CAgent:
         # graphs only with HIP graph packet capture off (isaacgymenv_amd/__init__.py)
         self.use_graphs = on_gpu and use_graphs and isaacgymenv_amd.GRAPHS_SAFE
         self._act_graph = None
+        self._g_noise = None
         self._mb_graphs = None
         # rollout bookkeeping around env.step, one (pre, post) graph pair per horizon slot once captured;
         # env outputs are copied into these static buffers first (both paths, same arithmetic)
@@ -349,6 +350,8 @@ class A2CAgent:
         obs = self._obs(obs)
         if self._act_graph is not None:
             self._g_obs.copy_(obs)
+            if self._g_noise is not None:  # the act forward's normal_ draws, outside the graph
+                self._g_noise.normal_(0.0, 1.0)
             self._act_graph.replay()
             return self._g_res
         self.model.eval()
@@ -670,10 +673,16 @@ class A2CAgent:
         torch.cuda.synchronize(self.device)
         self.model.eval()
         self._g_obs = torch.zeros(self.num_actors, self.obs_dim, dtype=torch.float32, device=self.device)
+        # the sampling noise as a static input drawn before each replay (same normal_ call, same RNG stream):
+        # a graph without an RNG node skips torch's two per-replay seed / offset fills
+        self._g_noise = torch.zeros(self.num_actors, self.actions_num, dtype=torch.float32, device=self.device)
+        self.model.used_input_noise = False
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, pool=torch.cuda.graph_pool_handle()):
             with torch.no_grad():
-                self._g_res = self.model({"is_train": False, "obs": self._g_obs})
+                self._g_res = self.model({"is_train": False, "obs": self._g_obs, "noise": self._g_noise})
+        if not self.model.used_input_noise:  # the torch statement drew inside the graph
+            self._g_noise = None
         self._act_graph = g
         # rollout bookkeeping per horizon slot (reads the act graph's static obs / outputs)
         spool = torch.cuda.graph_pool_handle()

@@ -449,6 +449,8 @@ class ActorCriticNetwork(nn.Module):
 class ModelA2CContinuousLogStd(nn.Module):
     """Input/value normalisation around the network; the act / train forward of rl_games."""
 
+    used_input_noise = False  # set when the act forward took input_dict["noise"] instead of drawing
+
     def __init__(self, net: ActorCriticNetwork, obs_dim: int, normalize_input: bool = True,
                  normalize_value: bool = True, value_size: int = 1):
         super().__init__()
@@ -495,9 +497,15 @@ class ModelA2CContinuousLogStd(nn.Module):
             heads = (a_out, c_out, net.mu.weight, net.mu.bias, net.value.weight, net.value.bias, net.sigma)
             if USE_MFMA_LAYERS and net.value.out_features == 1 and gae.act_heads_applies(*heads):
                 # both heads and the head in one launch (rl_act_heads); the normal_ draws are the same
-                # [N, A] call the torch statement makes after mu, so the RNG stream is unchanged
-                noise = torch.empty(a_out.shape[0], net.mu.out_features, dtype=torch.float32,
-                                    device=a_out.device).normal_(0.0, 1.0)
+                # [N, A] call the torch statement makes after mu, so the RNG stream is unchanged.  A caller
+                # may pass them drawn already (input_dict["noise"], the act graph's static buffer: the
+                # graph then holds no RNG node)
+                noise = input_dict.get("noise")
+                shape = (a_out.shape[0], net.mu.out_features)
+                if noise is not None and noise.shape == shape and noise.dtype == torch.float32 and noise.is_contiguous():
+                    self.used_input_noise = True
+                else:
+                    noise = torch.empty(shape, dtype=torch.float32, device=a_out.device).normal_(0.0, 1.0)
                 mu, actions, sigmas, neglogp, values = gae.act_heads(*heads[:6], noise, net.sigma.detach(), vms)
                 return {"neglogpacs": neglogp, "values": values, "actions": actions, "mus": mu, "sigmas": sigmas}
             value = net.value(c_out).contiguous()

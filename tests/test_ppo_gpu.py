@@ -107,6 +107,25 @@ def test_graph_replay_equals_eager_updates():
     assert abs(sg["lr"] - se["lr"]) <= 1e-9 + 1e-6 * se["lr"]
 
 
+def test_act_graph_replay_equals_eager_forward():
+    """The captured act forward (sampling noise drawn outside the graph into its static input) returns, from the
+    same generator state, exactly the eager forward's outputs, and leaves the generator where the eager one does."""
+    agent = _agent("AnymalTerrain", 1024, minibatch_size=8192)
+    agent.train_epoch()  # eager epoch, then the graphs are captured
+    assert agent._act_graph is not None and agent._g_noise is not None
+    obs = agent.obs["obs"].clone()
+    torch.manual_seed(5)
+    got = {k: v.clone() for k, v in agent.get_action_values(obs).items()}
+    off_graph = torch.cuda.default_generators[0].get_offset()
+    torch.manual_seed(5)
+    agent.model.eval()
+    with torch.no_grad():
+        ref = agent.model({"is_train": False, "obs": obs})
+    assert torch.cuda.default_generators[0].get_offset() == off_graph
+    for k in ("actions", "mus", "sigmas", "values", "neglogpacs"):
+        assert torch.equal(got[k], ref[k]), k
+
+
 def test_graph_replayed_backward_is_replay_invariant():
     """A captured minibatch forward+backward gives the eager gradient on every replay (with HIP
     graph packet capture on, the first hidden-layer bias gradient drifted from a later replay on;
