@@ -572,6 +572,24 @@ class Sim:
         _lib.check(fn(self.handle, src.data_ptr(), idx_ptr, n, s), f"set {kind}")
         self._hold = (src, idx)  # keep alive until the launch consumed them (stream ordered)
 
+    def set_root_and_dof(self, root, dof, idx, n: int = 0):
+        """set_state("root", root, idx, n) then set_state("dof", dof, idx, n), one host call (a reset's pair)."""
+        import torch
+        L, s = _lib.lib(), self.stream()
+        dev = self.sim_device
+        if not (root.dtype == torch.float32 and root.device == dev and root.is_contiguous()):
+            root = root.to(dev, dtype=torch.float32).contiguous()
+        if not (dof.dtype == torch.float32 and dof.device == dev and dof.is_contiguous()):
+            dof = dof.to(dev, dtype=torch.float32).contiguous()
+        if not (idx.dtype == torch.int32 and idx.device == dev and idx.is_contiguous()):
+            idx = idx.to(dev, dtype=torch.int32).contiguous()
+        n = int(n) if n else idx.numel()
+        if n == 0:
+            return
+        _lib.check(L.gs_sim_set_root(self.handle, root.data_ptr(), idx.data_ptr(), n, s), "set root")
+        _lib.check(L.gs_sim_set_dof(self.handle, dof.data_ptr(), idx.data_ptr(), n, s), "set dof")
+        self._hold = (root, dof, idx)
+
     def simulate(self):
         L = _lib.lib()
         if self.drives_dirty:
@@ -885,6 +903,17 @@ class Gym:
 
     def set_actor_root_state_tensor(self, sim: Sim, t: GymTensor) -> bool:
         sim.set_state("root", t.tensor)
+        return True
+
+    def amd_set_root_and_dof_state_indexed(self, sim: Sim, root: GymTensor, dof: GymTensor, idx: GymTensor,
+                                           n: int) -> bool:
+        """set_actor_root_state_tensor_indexed + set_dof_state_tensor_indexed with the same indices, in one host
+        call (the reset's pair, anymal_terrain.py:401-408): the same two launches, less Python per reset."""
+        both = getattr(sim, "set_root_and_dof", None)
+        if both is None:  # a sim object with only the per-kind setter (test doubles)
+            return (self.set_actor_root_state_tensor_indexed(sim, root, idx, n)
+                    and self.set_dof_state_tensor_indexed(sim, dof, idx, n))
+        both(root.tensor, dof.tensor, idx.tensor, n)
         return True
 
     def set_actor_root_state_tensor_indexed(self, sim: Sim, t: GymTensor, idx: GymTensor, n: int) -> bool:
