@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "gymrl.h"
 
@@ -229,12 +230,11 @@ __global__ __launch_bounds__(kThreads) void k_gemm_nt(const _Float16* __restrict
 // rl_games play_steps runs the act forward in f32 (no autocast).  C[m][c] = act(sum_r A[m][r] Bt[c][r] + bias[c])
 // with f32 operands on v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulation; the order of the sum is this
 // kernel's, so the result agrees with a library f32 GEMM to f32 rounding), bias and ELU in the epilogue.  64 x 64
-// tiles, 4 waves in 2 x 2, one 32 x 32 MFMA tile each; the reduction in stages of 32 through double-buffered LDS
-// (row stride 36 floats).  A lane reads 4 consecutive k of its row (one 16-B LDS read per operand) and feeds them
+// tiles, 4 waves in 2 x 2, one 32 x 32 MFMA tile each; the reduction in stages of KS = 32 or 64 through
+// double-buffered LDS (row stride KS + 4 floats: the 16-B fragment reads of 16 rows hit disjoint banks).  A lane reads 4 consecutive k of its row (one 16-B LDS read per operand) and feeds them
 // to 4 MFMAs: in MFMA s, half h of the wave carries k = 8 ks + 4 h + s -- the A and Bt fragments use the same map,
 // so every k is summed exactly once.  The output tile goes out through LDS as whole 256-B row segments.
 typedef float f4 __attribute__((ext_vector_type(4)));
-constexpr int kF32Step = 32, kF32Ld = kF32Step + 4;
 
 __device__ __forceinline__ f4 load4f(const float* __restrict__ p, int valid) {
   if (valid >= 4) return *reinterpret_cast<const f4*>(p);
@@ -244,13 +244,13 @@ __device__ __forceinline__ f4 load4f(const float* __restrict__ p, int valid) {
   return v;
 }
 
-template <bool ACT>
+template <bool ACT, int KS>
 __global__ __launch_bounds__(kThreads) void k_gemm_nt_f32(const float* __restrict__ A, int lda,
                                                           const float* __restrict__ Bt, int ldb,
                                                           const float* __restrict__ bias, float* __restrict__ C,
                                                           int ldc, int R, int64_t gA, int64_t gB, int64_t gBias,
                                                           int64_t gC, int MT, int NT) {
-  constexpr int BM = 64, BN = 64, KS = kF32Step, LD = kF32Ld, CPR = KS / 4;
+  constexpr int BM = 64, BN = 64, LD = KS + 4, CPR = KS / 4;
   constexpr int CA = BM * KS / 4 / kThreads, CB = BN * KS / 4 / kThreads;  // 16-B chunks per thread (2, 2)
   int gi, mt, nt;
   tile_of(MT, NT, gi, mt, nt);
@@ -669,8 +669,17 @@ extern "C" int rl_linear_fwd_f32_g(const float* x, int32_t M, int32_t K, int32_t
   const int MT = M / 64, NT = N / 64;
   const dim3 g(MT * NT * G);
   hipStream_t st = (hipStream_t)stream;
-  if (act) hipLaunchKernelGGL(k_gemm_nt_f32<true>, g, dim3(kThreads), 0, st, x, ldx, w, K, bias, y, ldy, K, gx, gw, gb, gy, MT, NT);
-  else hipLaunchKernelGGL(k_gemm_nt_f32<false>, g, dim3(kThreads), 0, st, x, ldx, w, K, bias, y, ldy, K, gx, gw, gb, gy, MT, NT);
+  // K stage: 64 (two MFMA kilocycles per wave per stage against the next stage's loads; 70 KB of LDS, two
+  // workgroups per CU) when the grid has at most two workgroups per CU, else 32 (37 KB, four per CU)
+  int ks = (int64_t)MT * NT * G <= 512 ? 64 : 32;
+  if (const char* e = getenv("RL_F32_KSTEP")) ks = atoi(e) == 64 ? 64 : 32;  // A/B switch (tools/probes)
+  if (ks == 64) {
+    if (act) hipLaunchKernelGGL((k_gemm_nt_f32<true, 64>), g, dim3(kThreads), 0, st, x, ldx, w, K, bias, y, ldy, K, gx, gw, gb, gy, MT, NT);
+    else hipLaunchKernelGGL((k_gemm_nt_f32<false, 64>), g, dim3(kThreads), 0, st, x, ldx, w, K, bias, y, ldy, K, gx, gw, gb, gy, MT, NT);
+  } else {
+    if (act) hipLaunchKernelGGL((k_gemm_nt_f32<true, 32>), g, dim3(kThreads), 0, st, x, ldx, w, K, bias, y, ldy, K, gx, gw, gb, gy, MT, NT);
+    else hipLaunchKernelGGL((k_gemm_nt_f32<false, 32>), g, dim3(kThreads), 0, st, x, ldx, w, K, bias, y, ldy, K, gx, gw, gb, gy, MT, NT);
+  }
   return launch_fail("rl_linear_fwd_f32");
 }
 
