@@ -821,13 +821,15 @@ def test_act_heads_kernel(vnorm):
         assert torch.equal(got, exp)
 
 
-def test_linear_f32_kernel_exact_on_integers_and_elu():
+@pytest.mark.parametrize("kstep", ["32", "64"])
+def test_linear_f32_kernel_exact_on_integers_and_elu(kstep, monkeypatch):
     """rl_linear_fwd_f32_g (the rollout's f32 act-forward layer): with small-integer data every product and partial
     sum is exact in f32, so the kernel equals the float64 product bit for bit whatever its summation order -- this
     pins the MFMA operand maps, the K tail (188 = 5 x 32 + 28), the grouping strides and the bias; with random data
-    the ELU epilogue agrees with torch's f32 addmm + elu to f32 rounding."""
+    the ELU epilogue agrees with torch's f32 addmm + elu to f32 rounding.  Both K-stage widths (RL_F32_KSTEP)."""
     from isaacgymenv_amd.rl import gae
     import torch.nn.functional as F
+    monkeypatch.setenv("RL_F32_KSTEP", kstep)
     gen = torch.Generator().manual_seed(5)
     M, K0, N0, N1, G = 256, 188, 128, 64, 2
     ri = lambda lo, hi, *shape: torch.randint(lo, hi, shape, generator=gen).float()  # noqa: E731
