@@ -242,6 +242,12 @@ class VecTask(Env):
         fused_out, self._fused_outputs = self._fused_outputs, None
         if fused_out is not None:
             self.timeout_buf, obs = fused_out
+            if self._rl_on_sim_device():  # .to(rl_device) returns the tensor itself: skip the device parse
+                self.extras["time_outs"] = self.timeout_buf
+                self.obs_dict["obs"] = obs
+                if self.num_states > 0:
+                    self.obs_dict["states"] = self.get_state()
+                return self.obs_dict, self.rew_buf, self.reset_buf, self.extras
             self.extras["time_outs"] = self.timeout_buf.to(self.rl_device)
             self.obs_dict["obs"] = obs.to(self.rl_device)
         else:
@@ -254,6 +260,14 @@ class VecTask(Env):
         if self.num_states > 0:
             self.obs_dict["states"] = self.get_state()
         return self.obs_dict, self.rew_buf.to(self.rl_device), self.reset_buf.to(self.rl_device), self.extras
+
+    _rl_same_device = None
+
+    def _rl_on_sim_device(self) -> bool:
+        """rl_device names the tensors' own device (then every .to(rl_device) of step() is the identity)."""
+        if self._rl_same_device is None:
+            self._rl_same_device = torch.device(self.rl_device) == self.rew_buf.device == self.reset_buf.device
+        return self._rl_same_device
 
     def zero_actions(self) -> torch.Tensor:
         return torch.zeros([self.num_envs, self.num_actions], dtype=torch.float32, device=self.rl_device)
