@@ -80,6 +80,17 @@ __device__ __forceinline__ void quad_sum3(float* u) {
   u[1] = t1 + b1;
   u[2] = t2 + b2;
 }
+// four interleaved quad sums (a contact's three rows + its TGS displacement term): the same bits as quad_sum
+// of each, one DPP latency for all four
+__device__ __forceinline__ void quad_sum4(float* u) {
+  const float a0 = qperm<0xB1>(u[0]), a1 = qperm<0xB1>(u[1]), a2 = qperm<0xB1>(u[2]), a3 = qperm<0xB1>(u[3]);
+  const float t0 = u[0] + a0, t1 = u[1] + a1, t2 = u[2] + a2, t3 = u[3] + a3;
+  const float b0 = qperm<0x4E>(t0), b1 = qperm<0x4E>(t1), b2 = qperm<0x4E>(t2), b3 = qperm<0x4E>(t3);
+  u[0] = t0 + b0;
+  u[1] = t1 + b1;
+  u[2] = t2 + b2;
+  u[3] = t3 + b3;
+}
 // broadcast lane L of the quad to all four lanes; L is a constant after unrolling, the switch folds
 __device__ __forceinline__ float bcast(float x, int L) {
   switch (L) {
@@ -372,8 +383,40 @@ __device__ __forceinline__ float base_jac(const float* xc, int ax, int k) {
   return (ax == k - 3) ? 1.f : 0.f;
 }
 
+// An index the compiler cannot see through: the kernels' final stores recompute their addresses from it instead
+// of keeping the load addresses (64-bit, one pair of VGPRs per state row) live across the whole launch -- in the
+// round-5 kernel those pairs were what spilled to scratch (184 B per lane, written back once per launch)
+__device__ __forceinline__ int opaque_index(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 // Per-team shape table for the self-collision prepass: [(kShW * sh + f) * TPW + team] (TPW teams per workgroup)
 constexpr int kTeamsPerBlock = kTeamBlock / 4;
+
+// every self-collision pair of the topology has a closed form (pair kinds 0 sphere-sphere, 1 sphere-capsule,
+// 2 capsule-capsule, gs_pairs.h self_pair): the team narrowphase forms them in the lanes that found them; a
+// topology with a GJK pair (box, cylinder, hull) runs the replicated gs_pairs.h narrowphase instead
+template <class T>
+__host__ __device__ constexpr bool team_closed_form() {
+  for (int q = 0; q < T::NPAIR; ++q)
+    if (T::pair_k[q] > 2) return false;
+  return true;
+}
+// the team narrowphase's staging: per lane its kTeamLC(T) contacts of smallest pair order (kTeamSt floats each:
+// x (3), n (3), separation, shapes a, b) at [f + kTeamSt * slot][64 lanes], then the team's first NPK in pair order
+// at [f + kTeamSt * rank][TPW teams].  Each lane keeping its NPK smallest keys is exact: every contact among the
+// team's first NPK is among its own lane's first NPK.
+constexpr int kTeamSt = 9;
+template <class T>
+__host__ __device__ constexpr int team_lc() { return T::NPK > 0 ? T::NPK : 1; }
+// floats of the workgroup's shape / staging table (shared with the TERR query list)
+template <class T>
+__host__ __device__ constexpr int shw_size() {
+  const int pose = kShW * T::NS * kTeamsPerBlock;
+  const int stage = team_lc<T>() * kTeamSt * 64 + T::NPK * kTeamSt * kTeamsPerBlock;
+  return T::NPK == 0 ? 1 : (team_closed_form<T>() ? (stage > pose ? stage : pose) : pose);
+}
 
 // Self-collision prepass of a team: every lane publishes its chain's shapes' bounding-sphere
 // centres (lane 0 also the root's), the lanes split the pair list for the broadphase; a wave with a near pair
@@ -617,7 +660,9 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
   };
   // every pair site of the lane, in a fixed order: f(segment a, radius, half length, capsule?, shape, segment b, ...,
   // the pair's bit); the root shapes' and the neighbour chains' segments are formed here
-  auto visit = [&](auto&& f) {
+  // (lcv: the lane's chain; the narrowphase passes it through opaque_index so its pair bits and keys are formed
+  // there, not hoisted to the kernel's start and kept live across the launch)
+  auto visit = [&](int lcv, auto&& f) {
 #pragma unroll
     for (int sr = 0; sr < RSH; ++sr) {
       const float* rt = sct + ShapeTab<T>::ROOT + 8 * sr;
@@ -630,15 +675,15 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
       for (int j = 0; j < SPC; ++j)
         if (team_pair<T>(sr, RSH + j))
           f(r0, r1, rr, rhl, T::shkind[sr] == 1, sr, p0[j], p1[j], rad[j], hl[j], T::shkind[RSH + j] == 1,
-            RSH + lc * SPC + j, team_pair_bit<T>(lc, sr, -1, 0, j));
+            RSH + lcv * SPC + j, team_pair_bit<T>(lcv, sr, -1, 0, j));
     }
 #pragma unroll
     for (int j = 0; j < SPC; ++j)
 #pragma unroll
       for (int j2 = j + 1; j2 < SPC; ++j2)
         if (team_pair<T>(RSH + j, RSH + j2))
-          f(p0[j], p1[j], rad[j], hl[j], T::shkind[RSH + j] == 1, RSH + lc * SPC + j, p0[j2], p1[j2], rad[j2], hl[j2],
-            T::shkind[RSH + j2] == 1, RSH + lc * SPC + j2, team_pair_bit<T>(lc, 0, j, 0, j2));
+          f(p0[j], p1[j], rad[j], hl[j], T::shkind[RSH + j] == 1, RSH + lcv * SPC + j, p0[j2], p1[j2], rad[j2], hl[j2],
+            T::shkind[RSH + j2] == 1, RSH + lcv * SPC + j2, team_pair_bit<T>(lcv, 0, j, 0, j2));
     // chains lc + 1 (every lane) and lc + 2 (lanes 0 and 1): each inter-chain pair exactly once
 #pragma unroll
     for (int dl = 1; dl <= 2; ++dl) {
@@ -651,24 +696,28 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
           q1[j][g] = dl == 1 ? qperm<0x39>(p1[j][g]) : qperm<0x4E>(p1[j][g]);
         }
       }
-      if (dl == 1 || lc < 2) {
-        const int lo = (lc + dl) & 3;
+      if (dl == 1 || lcv < 2) {
+        const int lo = (lcv + dl) & 3;
 #pragma unroll
         for (int j = 0; j < SPC; ++j)
 #pragma unroll
           for (int j2 = 0; j2 < SPC; ++j2)
             if (team_pair<T>(RSH + j, RSH + SPC + j2))
-              f(p0[j], p1[j], rad[j], hl[j], T::shkind[RSH + j] == 1, RSH + lc * SPC + j, q0[j2], q1[j2], rad[j2],
-                hl[j2], T::shkind[RSH + j2] == 1, RSH + lo * SPC + j2, team_pair_bit<T>(lc, 0, j, dl, j2));
+              f(p0[j], p1[j], rad[j], hl[j], T::shkind[RSH + j] == 1, RSH + lcv * SPC + j, q0[j2], q1[j2], rad[j2],
+                hl[j2], T::shkind[RSH + j2] == 1, RSH + lo * SPC + j2, team_pair_bit<T>(lcv, 0, j, dl, j2));
       }
     }
   };
-  visit(test);
+  visit(lc, test);
   if (__ballot(near != 0ull) == 0ull) return 0;  // wave-uniform: no team of the wave has a pair within reach
 #ifdef GS_PHASE_PROFILE
   if ((threadIdx.x & 63) == 0) atomicAdd(&gs_phase_cycles[12], 1ull);  // substeps a wave runs the narrowphase
   const long long np_t0 = clock64();
 #endif
+  if constexpr (!team_closed_form<T>()) {
+    // GJK pairs: the replicated narrowphase (every pair kind of gs_pairs.h self_pair)
+    return team_narrow_replicated<T>(M, P, mu_g, N, e, lc, R0, R, X, near, shw_tab, sct, pool);
+  } else {
   // ---- narrowphase (round 5).  Each near pair's contacts are formed by the lane whose broadphase found it, from
   // the segments it holds in registers -- the closed-form sphere / capsule rules of gs_pairs.h self_pair (the
   // pair's a = the lower shape index, n from b to a, up to 2 contacts for a parallel capsule overlap), so the
@@ -676,18 +725,21 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
   // by (pair, contact) through DPP, keeps the first NPK in pair order (self_contacts' cap) and every lane of the
   // team copies them into its pool column.  Before, every lane of the team published its shapes' full poses
   // and re-ran the whole narrowphase of the team's near pairs (10.5 k cycles per wave-substep entered: the slow
-  // waves' tail).  A lane with more than kLC contacts (not seen in the pool study) takes the
-  // replicated path below for the whole wave.
-  constexpr int kLC = 2, kSt = 9;  // contacts per lane; floats per staged contact: x (3) n (3) sep, shapes a, b
+  // waves' tail).  Round 6: each lane keeps the kLC = NPK contacts of smallest pair order it finds
+  // (exact for the team's first NPK, team_lc), so no lane ever falls back to the replicated narrowphase.
+  constexpr int kLC = team_lc<T>(), kSt = kTeamSt;
+  constexpr int kNone = 0x7fffffff;
   const int wl = threadIdx.x & 63;
   const int team = threadIdx.x >> 2;
   float* lslot = shw_tab + wl;                        // [f + kSt * slot][64 lanes]
   float* tstg = shw_tab + kLC * kSt * 64 + team;      // [f + kSt * rank][TPW teams]
-  static_assert(kLC * kSt * 64 + T::NPK * kSt * TPW <= kShW * T::NS * TPW, "contact staging fits the pose table");
+  static_assert(kLC * kSt * 64 + T::NPK * kSt * TPW <= shw_size<T>(), "contact staging fits the table");
   __syncthreads();  // an earlier user of the table (the TERR query list, a previous substep) is done with it
   const float coff = P.contact_offset;
-  int cnt = 0, key0 = 0x7fffffff, key1 = 0x7fffffff;
-  bool over = false;
+  int cnt = 0;  // the lane's contacts (all of them: the team's count caps at NPK)
+  int key[kLC];
+#pragma unroll
+  for (int i = 0; i < kLC; ++i) key[i] = kNone;
   auto narrow = [&](const float* a0_, const float* a1_, float ra_, float, bool sa, int ia, const float* b0_,
                     const float* b1_, float rb_, float, bool sb, int ib, unsigned long long bit) {
     if (!(near & bit)) return;
@@ -770,8 +822,20 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
       }
       const float sep = dist - ra - rb;
       if (!(sep < coff)) continue;
-      if (cnt < kLC) {
-        float* o = lslot + kSt * cnt * 64;
+      // the slot: the next free one, else the one holding the largest key when this key is smaller
+      const int kn = 2 * q + c;
+      int slot = cnt < kLC ? cnt : -1;
+      if (cnt >= kLC) {
+        int m = 0, km = key[0];
+#pragma unroll
+        for (int i = 1; i < kLC; ++i) {
+          m = key[i] > km ? i : m;
+          km = key[i] > km ? key[i] : km;
+        }
+        slot = kn < km ? m : -1;
+      }
+      if (slot >= 0) {
+        float* o = lslot + kSt * slot * 64;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           o[k * 64] = 0.5f * ((pa[c][k] - ra * nn[k]) + (pb[c][k] + rb * nn[k]));
@@ -780,47 +844,49 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
         o[6 * 64] = sep;
         o[7 * 64] = __int_as_float(sha);
         o[8 * 64] = __int_as_float(shb);
-        const int key = 2 * q + c;
-        if (cnt == 0) key0 = key; else key1 = key;
-      } else {
-        over = true;
+#pragma unroll
+        for (int i = 0; i < kLC; ++i) key[i] = i == slot ? kn : key[i];
       }
       ++cnt;
     }
   };
-  visit(narrow);
+  visit(opaque_index(lc), narrow);
 #ifdef GS_PHASE_PROFILE
   if ((threadIdx.x & 63) == 0) atomicAdd(&gs_phase_cycles[14], (unsigned long long)(clock64() - np_t0));
 #endif
   int cnt_team = 0;
-  if (__ballot(over) == 0ull) {
-    // the team's contacts in pair order: each contact's rank among the team's (at most 4 x kLC) keys
-    constexpr int kNone = 0x7fffffff;
-    int r0 = 0, r1 = 0;
-    auto tally = [&](int k) {
-      r0 += k < key0;
-      r1 += k < key1;
-      cnt_team += k != kNone;
+  {
+    // the team's contacts in pair order: each staged contact's rank among the team's staged keys (the smaller
+    // keys of the team's first NPK are all staged, so the rank is the contact's place in the whole pair order)
+    int rk[kLC];
+#pragma unroll
+    for (int i = 0; i < kLC; ++i) rk[i] = 0;
+    auto tally = [&](const int (&ks)[kLC]) {
+#pragma unroll
+      for (int j = 0; j < kLC; ++j)
+#pragma unroll
+        for (int i = 0; i < kLC; ++i) rk[i] += ks[j] < key[i];
     };
-    tally(key0); tally(key1);
+    tally(key);
     {
-      const int a = qperm_i<0x39>(key0), b = qperm_i<0x39>(key1);
-      tally(a); tally(b);
+      int ks[kLC];
+#pragma unroll
+      for (int j = 0; j < kLC; ++j) ks[j] = qperm_i<0x39>(key[j]);
+      tally(ks);
+#pragma unroll
+      for (int j = 0; j < kLC; ++j) ks[j] = qperm_i<0x4E>(key[j]);
+      tally(ks);
+#pragma unroll
+      for (int j = 0; j < kLC; ++j) ks[j] = qperm_i<0x93>(key[j]);
+      tally(ks);
     }
-    {
-      const int a = qperm_i<0x4E>(key0), b = qperm_i<0x4E>(key1);
-      tally(a); tally(b);
-    }
-    {
-      const int a = qperm_i<0x93>(key0), b = qperm_i<0x93>(key1);
-      tally(a); tally(b);
-    }
+    cnt_team = cnt + qperm_i<0xB1>(cnt);
+    cnt_team += qperm_i<0x4E>(cnt_team);
 #pragma unroll
     for (int i = 0; i < kLC; ++i) {
-      const int rk = i == 0 ? r0 : r1;
-      if (i < cnt && rk < T::NPK) {
+      if (i < cnt && rk[i] < T::NPK) {
         const float* src = lslot + kSt * i * 64;
-        float* dst = tstg + kSt * rk * TPW;
+        float* dst = tstg + kSt * rk[i] * TPW;
 #pragma unroll
         for (int f = 0; f < kSt; ++f) dst[f * TPW] = src[f * 64];
       }
@@ -856,8 +922,6 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
         o[kPoolLB * RW] = (float)(blb & 255);
       }
     }
-  } else {
-    cnt_team = team_narrow_replicated<T>(M, P, mu_g, N, e, lc, R0, R, X, near, shw_tab, sct, pool);
   }
 #ifdef GS_PHASE_PROFILE
   {
@@ -871,6 +935,7 @@ __device__ __forceinline__ int team_self_contacts(const DevModel* __restrict__ M
   }
 #endif
   return cnt_team;
+  }  // closed-form pairs
 }
 
 // TERR (trimesh terrain): a candidate sphere at x (relative to the root origin p) against the
@@ -892,7 +957,7 @@ __device__ __forceinline__ float terrain_candidate(const DevParams& P, const flo
   return dist;
 }
 
-template <class T, bool TERR>
+template <class T, bool TERR, bool TGS>
 __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, const float* __restrict__ mdl,
                                              const DevParams& P, TeamState<T>& s, const float* tau,
                                              const float* __restrict__ mu_t, int N, int e, int lc,
@@ -1097,12 +1162,13 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
   bool act[CC];
   float sep[CC], cmu[CC];
   float cnrm[TERR ? CC : 1][3];  // TERR: each chain candidate's contact normal (the force outputs)
+  // (a) body poses and joint axes; (b) the self-collision prepass, which needs only the poses -- run here, before
+  // the chain's velocities, accelerations, inertias and forces are live, so its narrowphase spills nothing; (c)
+  // the rest of the forward pass and the contact candidates
 #pragma unroll
   for (int k = 0; k < CL; ++k) {
     const float* Rp = k == 0 ? R0 : R[k - 1];
     const float* Xp = k == 0 ? X0 : X[k - 1];
-    const float* Vp = k == 0 ? nub : V[k - 1];
-    const float* Ap = k == 0 ? A0 : A[k - 1];
     const float* bp = cm + (k * C::BODY) * LN;
     float jR[9], jt[3], ax[3];
 #pragma unroll
@@ -1133,6 +1199,20 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       S[k][0] = S[k][1] = S[k][2] = 0.f;
       S[k][3] = aw[0]; S[k][4] = aw[1]; S[k][5] = aw[2];
     }
+  }
+  GS_PROF(0)  // root + chain poses
+  // ================= self-collision prepass (rare narrowphase; the pool rows are built with the contact records)
+  int npc = 0;
+  float* pool = rows_own + RS::POOL * RW;
+  if constexpr (T::NPK > 0) {
+    if (P.self_collide) npc = team_self_contacts<T>(M, cm, P, mu_t, kTeamsPerBlock, 0, lc, R0, R, X, shw_tab, sct, pool);
+  }
+  GS_PROF(11)  // self-collision prepass
+#pragma unroll
+  for (int k = 0; k < CL; ++k) {
+    const float* Vp = k == 0 ? nub : V[k - 1];
+    const float* Ap = k == 0 ? A0 : A[k - 1];
+    const float* bp = cm + (k * C::BODY) * LN;
     const float qd = s.qd[k];
     float c6[6];
 #pragma unroll
@@ -1227,14 +1307,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     }
   }
 
-  GS_PROF(0)  // root + chain forward pass + contact Jacobians
-  // ================= self-collision prepass (rare narrowphase; the pool rows are built with the contact records)
-  int npc = 0;
-  float* pool = rows_own + RS::POOL * RW;
-  if constexpr (T::NPK > 0) {
-    if (P.self_collide) npc = team_self_contacts<T>(M, cm, P, mu_t, kTeamsPerBlock, 0, lc, R0, R, X, shw_tab, sct, pool);
-  }
-  GS_PROF(11)  // self-collision prepass
+  GS_PROF(0)  // chain forward pass + contact Jacobians
   // ================= chain backward pass: composite inertia / force, bias, chain rows of M
   float Mcc[CL][CL], Mcb[CL][6], biasc[CL];
 #pragma unroll
@@ -1693,35 +1766,45 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
   // aC); its target: a gap closes within the sub-step (-s / hs), a penetration is pushed out at -s / h (capped),
   // over the whole step; the velocity iterations target the gap left after the sub-steps; the positions integrate
   // the sub-steps' mean velocity.  PGS (0): the split-impulse targets precomputed in the records.
-  const bool tgs = P.tgs != 0;
+  // (TGS is a template parameter: the PGS kernels carry none of its state, and its target is branch-free)
+  constexpr bool tgs = TGS;
   const float hs = tgs ? h / (float)P.pos_iters : h, inv_hs = 1.f / hs;
-  float aA = 0.f, aA2 = 0.f, aC[NCH];
+  [[maybe_unused]] float aA = 0.f, aA2 = 0.f, aC[NCH];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) aC[c] = 0.f;
-  auto tgs_tdi = [&](float sc, float su, bool pos, float di0) {
-    const float sep = fmaf(hs, su, sc);
-    const float t = sep >= 0.f ? -sep * (pos ? inv_hs : inv_h) : (pos ? fminf(-sep * inv_h, P.max_depen_vel) : 0.f);
-    return t * di0;
-  };
   for (int it = 0; it < iters; ++it) {
     const int tsel = it < P.pos_iters ? RS::C_TP : RS::C_TV;
     const int rsel = it < P.pos_iters ? RS::R_TP : RS::R_TV;
     const bool pos = it < P.pos_iters;
     const float na = (float)(it < P.pos_iters ? it : P.pos_iters);  // sub-steps done
+    // the TGS target of a row at separation sep (wave-uniform factors): a gap closes at -sep / hs in a position
+    // sub-step, at -sep / h in a velocity iteration; a penetration is pushed out at -sep / h capped at
+    // max_depenetration_velocity in a position sub-step, not at all in a velocity iteration (the cap 0)
+    const float kgap = pos ? inv_hs : inv_h, cap = pos ? P.max_depen_vel : 0.f;
+    auto tgs_tdi = [&](float sc, float su, float di0) {
+      const float sep = fmaf(hs, su, sc);
+      const float t = sep >= 0.f ? -sep * kgap : fminf(-sep * inv_h, cap);
+      return t * di0;
+    };
 #pragma unroll
     for (int j = 0; j < RC; ++j) {
       if (ract[j]) {
         const float* rec = rows_own + RS::root(j) * RW;
         const float* recl = rec + 4 * lc * RW;
-        float z[12], u[3];
+        float z[12], u[4];
 #pragma unroll
         for (int i = 0; i < 12; ++i) z[i] = recl[((i >> 2) * RS::RZROW + (i & 3)) * RW];
 #pragma unroll
         for (int rr = 0; rr < 3; ++rr) u[rr] = fmaf(z[4 * rr], wA, fmaf(z[4 * rr + 1], wA2, z[4 * rr + 3]));
-        quad_sum3(u);
-        float tdi = rec[rsel * RW];
-        if (tgs) tdi = tgs_tdi(rec[RS::R_SEP * RW], quad_sum(fmaf(z[0], aA, fmaf(z[1], aA2, na * z[3]))), pos,
-                               rec[RS::R_DI * RW]);
+        float tdi;
+        if constexpr (tgs) {
+          u[3] = fmaf(z[0], aA, fmaf(z[1], aA2, na * z[3]));
+          quad_sum4(u);
+          tdi = tgs_tdi(rec[RS::R_SEP * RW], u[3], rec[RS::R_DI * RW]);
+        } else {
+          quad_sum3(u);
+          tdi = rec[rsel * RW];
+        }
         float dl0, dl1, dl2;
         contact_block(u[0], u[1], u[2], rec[RS::R_DI * RW], rec[(RS::R_DI + 1) * RW], rec[(RS::R_DI + 2) * RW],
                       rec[RS::R_G * RW], rec[(RS::R_G + 1) * RW], rec[(RS::R_G + 2) * RW], tdi,
@@ -1765,14 +1848,18 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       if (__ballot(a_o) != 0ull) GS_PROF_COUNT(8, 1)  // chain contacts the wave executes
 #endif
       if (a_o) {
-        float u[3];
+        float u[4];
 #pragma unroll
         for (int rr = 0; rr < 3; ++rr)  // the w terms last (they carry the Gauss-Seidel chain)
           u[rr] = fmaf(z[4 * rr], wA, fmaf(z[4 * rr + 1], wA2, fmaf(z[4 * rr + 2], wC[cc], z[4 * rr + 3])));
-        quad_sum3(u);
         float tdi = k8[6];
-        if (tgs)
-          tdi = tgs_tdi(k8[6], quad_sum(fmaf(z[0], aA, fmaf(z[1], aA2, fmaf(z[2], aC[cc], na * z[3])))), pos, k8[0]);
+        if constexpr (tgs) {
+          u[3] = fmaf(z[0], aA, fmaf(z[1], aA2, fmaf(z[2], aC[cc], na * z[3])));
+          quad_sum4(u);
+          tdi = tgs_tdi(k8[6], u[3], k8[0]);
+        } else {
+          quad_sum3(u);
+        }
         float dl0, dl1, dl2;
         contact_block(u[0], u[1], u[2], k8[0], k8[1], k8[2], k8[3], k8[4], k8[5], tdi, k8[7], lamc[cc][j], dl0,
                       dl1, dl2);
@@ -1794,19 +1881,22 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
           ana = c == ca ? aC[c] : ana;
           anb = c == cb ? aC[c] : anb;
         }
-        float z[15], u[3];
+        float z[15], u[4];
 #pragma unroll
         for (int i = 0; i < 15; ++i) z[i] = o[(RS::P_Z + i) * RW];
 #pragma unroll
         for (int rr = 0; rr < 3; ++rr)
           u[rr] = fmaf(z[5 * rr], wA, fmaf(z[5 * rr + 1], wA2, fmaf(z[5 * rr + 2], wa, fmaf(z[5 * rr + 3], wb, z[5 * rr + 4]))));
-        quad_sum3(u);
         float lam[3] = {o[kPoolLam * RW], o[(kPoolLam + 1) * RW], o[(kPoolLam + 2) * RW]};
-        float tdi = o[psel * RW];
-        if (tgs)
-          tdi = tgs_tdi(o[kPoolSep * RW],
-                        quad_sum(fmaf(z[0], aA, fmaf(z[1], aA2, fmaf(z[2], ana, fmaf(z[3], anb, na * z[4]))))), pos,
-                        o[RS::P_DI * RW]);
+        float tdi;
+        if constexpr (tgs) {
+          u[3] = fmaf(z[0], aA, fmaf(z[1], aA2, fmaf(z[2], ana, fmaf(z[3], anb, na * z[4]))));
+          quad_sum4(u);
+          tdi = tgs_tdi(o[kPoolSep * RW], u[3], o[RS::P_DI * RW]);
+        } else {
+          quad_sum3(u);
+          tdi = o[psel * RW];
+        }
         float dl0, dl1, dl2;
         contact_block(u[0], u[1], u[2], o[RS::P_DI * RW], o[(RS::P_DI + 1) * RW], o[(RS::P_DI + 2) * RW],
                       o[RS::P_G * RW], o[(RS::P_G + 1) * RW], o[(RS::P_G + 2) * RW], tdi, o[kPoolMu * RW], lam,
@@ -1833,7 +1923,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       for (int c = 0; c < NCH; ++c) aC[c] += wC[c];
     }
     if (it == P.pos_iters - 1) {
-      if (tgs) {  // positions integrate the sub-steps' mean velocity (w space is linear)
+      if constexpr (tgs) {  // positions integrate the sub-steps' mean velocity (w space is linear)
         const float inv_n = 1.f / (float)P.pos_iters;
         float mC[NCH];
 #pragma unroll
@@ -1908,6 +1998,8 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     s.qd[k] = nunc[k];
   }
   if (collect) {
+    // (output addresses formed here: opaque_index)
+    e = opaque_index(e);
 #pragma unroll
     for (int k = 0; k < CL; ++k) {
       float f0 = 0.f, f1 = 0.f, f2 = 0.f;
@@ -2017,13 +2109,13 @@ __device__ __forceinline__ int xcd_block(int b, int G) {
   return x * per + (x < rem ? x : rem) + q;
 }
 
-template <class T, bool TERR>
+template <class T, bool TERR, bool TGS>
 __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel* __restrict__ M, DevParams P,
                                                                  SimBuffers B, const float* __restrict__ tau_aos) {
   constexpr int LN = T::T_LANES, CL = T::T_CL, ND = T::ND;
   __shared__ float mdl[CM<T>::NP * LN];
   __shared__ float rows[RowSlots<T>::TOTAL * RW];
-  __shared__ float shw_tab[T::NPK > 0 ? kShW * T::NS * kTeamsPerBlock : 1];
+  __shared__ float shw_tab[shw_size<T>()];
   __shared__ float sct[ShapeTab<T>::SIZE];
   // the team's shape friction (constant over the launch), read by the contact records and the self-contact pool
   // from LDS instead of device memory every substep: [shape][team]
@@ -2048,19 +2140,19 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel*
   GS_PROF_DECL
   for (int sstep = 0; sstep < P.substeps; ++sstep) {
     const bool last = (sstep == P.substeps - 1) && P.collect;
-    substep_team<T, TERR>(M, mdl, P, s, tau, mu_t, N, e, lc, own, team, B.cf, last, nullptr, shw_tab, sct GS_PROF_ARGS);
+    substep_team<T, TERR, TGS>(M, mdl, P, s, tau, mu_t, N, e, lc, own, team, B.cf, last, nullptr, shw_tab, sct GS_PROF_ARGS);
   }
-  team_store<T>(B.state, N, e, lc, s);
+  team_store<T>(B.state, N, opaque_index(e), opaque_index(lc), s);
   GS_PROF_FLUSH
 }
 
-template <class T, bool TERR>
+template <class T, bool TERR, bool TGS>
 __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* __restrict__ M, DevParams P,
                                                                 SimBuffers B, PdDev A) {
   constexpr int LN = T::T_LANES, CL = T::T_CL, ND = T::ND, NB = T::NB;
   __shared__ float mdl[CM<T>::NP * LN];
   __shared__ float rows[RowSlots<T>::TOTAL * RW];
-  __shared__ float shw_tab[T::NPK > 0 ? kShW * T::NS * kTeamsPerBlock : 1];
+  __shared__ float shw_tab[shw_size<T>()];
   __shared__ float sct[ShapeTab<T>::SIZE];
   // the team's shape friction (constant over the launch), read by the contact records and the self-contact pool
   // from LDS instead of device memory every substep: [shape][team]
@@ -2083,11 +2175,13 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
   const int sub = P.substeps;
   const int n_pd = A.decimation * sub;
   const int total = (A.decimation + A.extra) * sub;
-  const size_t d0 = (size_t)e * ND + lc * CL;  // this lane's first dof in the AoS tensors
+  // this lane's first dof in the AoS tensors (formed where each use needs it, opaque_index)
+  auto dof0 = [&]() { return (size_t)opaque_index(e) * ND + lc * CL; };
   GS_PROF_DECL
   for (int it = 0; it < total; ++it) {
     if (it < n_pd && (it % sub) == 0) {
       const bool first = it == 0;
+      const size_t d0 = dof0();
 #pragma unroll
       for (int k = 0; k < CL; ++k) {
         const float qj = first ? A.dof_state_in[(d0 + k) * 2 + 0] : s.q[k];
@@ -2099,8 +2193,9 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
     const bool last = ((it % sub) == sub - 1) && P.collect;
     GS_PROF(6)  // PD torque
     float* cf_aos = (it == total - 1) ? A.cf_out : nullptr;
-    substep_team<T, TERR>(M, mdl, P, s, tau, mu_t, N, e, lc, own, team, B.cf, last, cf_aos, shw_tab, sct GS_PROF_ARGS);
+    substep_team<T, TERR, TGS>(M, mdl, P, s, tau, mu_t, N, e, lc, own, team, B.cf, last, cf_aos, shw_tab, sct GS_PROF_ARGS);
     if (it == n_pd - 1 && A.dof_out) {
+      const size_t d0 = dof0();
 #pragma unroll
       for (int k = 0; k < CL; ++k) {
         A.dof_out[(d0 + k) * 2 + 0] = s.q[k];
@@ -2108,7 +2203,8 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
       }
     }
   }
-  team_store<T>(B.state, N, e, lc, s);
+  team_store<T>(B.state, N, opaque_index(e), opaque_index(lc), s);
+  const size_t d0 = dof0();
 #pragma unroll
   for (int k = 0; k < CL; ++k) A.torques_out[d0 + k] = tau[k];
   if (A.actions_copy) {
@@ -2137,10 +2233,15 @@ hipError_t launch_sim_team(const DevModel* M, const DevParams& P, const SimBuffe
     static_assert(T::NR == T::NB, "the lane team reports contact forces per body (no kept fixed-joint links)");
     const long lanes = (long)B.N * T::T_LANES;
     const int blocks = (int)((lanes + kTeamBlock - 1) / kTeamBlock);
-    if (P.has_terrain)  // trimesh terrain: mesh queries by the candidates' owner lanes
-      hipLaunchKernelGGL((k_simulate_team<T, true>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, tau);
+    // trimesh terrain: mesh queries by the candidates' owner lanes; TGS / PGS
+    if (P.has_terrain && P.tgs)
+      hipLaunchKernelGGL((k_simulate_team<T, true, true>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, tau);
+    else if (P.has_terrain)
+      hipLaunchKernelGGL((k_simulate_team<T, true, false>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, tau);
+    else if (P.tgs)
+      hipLaunchKernelGGL((k_simulate_team<T, false, true>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, tau);
     else
-      hipLaunchKernelGGL((k_simulate_team<T, false>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, tau);
+      hipLaunchKernelGGL((k_simulate_team<T, false, false>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, tau);
     return hipGetLastError();
   } else {
     return hipErrorInvalidConfiguration;
@@ -2151,10 +2252,14 @@ hipError_t launch_pd_team(const DevModel* M, const DevParams& P, const SimBuffer
   if constexpr (T::HAS_TEAM) {
     const long lanes = (long)B.N * T::T_LANES;
     const int blocks = (int)((lanes + kTeamBlock - 1) / kTeamBlock);
-    if (P.has_terrain)
-      hipLaunchKernelGGL((k_pd_step_team<T, true>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, A);
+    if (P.has_terrain && P.tgs)
+      hipLaunchKernelGGL((k_pd_step_team<T, true, true>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, A);
+    else if (P.has_terrain)
+      hipLaunchKernelGGL((k_pd_step_team<T, true, false>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, A);
+    else if (P.tgs)
+      hipLaunchKernelGGL((k_pd_step_team<T, false, true>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, A);
     else
-      hipLaunchKernelGGL((k_pd_step_team<T, false>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, A);
+      hipLaunchKernelGGL((k_pd_step_team<T, false, false>), dim3(blocks), dim3(kTeamBlock), 0, st, M, P, B, A);
     return hipGetLastError();
   } else {
     return hipErrorInvalidConfiguration;

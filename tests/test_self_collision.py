@@ -24,16 +24,17 @@ from oracle.oracle import OracleSim
 from tests import helpers as H
 
 
-def crossed_leg_states(n, seed=3):
-    """ANYmal states with wide joint perturbations, first `n` of them that have self-contacts (oracle)."""
+def crossed_leg_states(n, seed=3, min_contacts=1, spread=1.2, pool=40):
+    """ANYmal states with wide joint perturbations, first `n` of them that have at least `min_contacts`
+    self-contacts (oracle)."""
     art, flat = H.anymal()
-    m = 40 * n
+    m = pool * n
     rng = np.random.RandomState(seed)
     root, dof, tau, mu = H.anymal_states(m, seed=seed)
-    dof[:, :, 0] += rng.uniform(-1.2, 1.2, (m, 12))
+    dof[:, :, 0] += rng.uniform(-spread, spread, (m, 12))
     o = OracleSim(flat, H.ANYMAL_PARAMS)
     c, cnt = o.self_contacts(root, dof, mu)
-    idx = np.nonzero(cnt)[0][:n]
+    idx = np.nonzero(cnt >= min_contacts)[0][:n]
     assert len(idx) == n
     return root[idx].copy(), dof[idx].copy(), tau[idx].copy(), mu[idx].copy()
 
@@ -161,9 +162,9 @@ def test_hull_face_on_ground_contacts_at_its_corners(tmp_path):
     assert len(sel) == 4 and {tuple(np.round(hv[i], 6)) for i in sel} == bottom
 
 
-def _sim_vs_oracle(host, variant=0, n=48, steps=1):
+def _sim_vs_oracle(host, variant=0, n=48, steps=1, states=None):
     art, flat = H.anymal()
-    root, dof, tau, mu = crossed_leg_states(n)
+    root, dof, tau, mu = states if states is not None else crossed_leg_states(n)
     gym, sim = H.make_gpu_sim("anymal", n, H.ANYMAL_PARAMS, host=host)
     if variant:
         assert sim.kernel_variant == variant, sim.kernel_variant
@@ -211,6 +212,16 @@ def test_lane_kernel_self_contacts_match_oracle():
 @pytest.mark.gpu
 def test_team_kernel_self_contacts_match_oracle():
     _sim_vs_oracle(host=False, variant=2)
+
+
+@pytest.mark.gpu
+def test_team_kernel_full_self_contact_pools_match_oracle():
+    """States whose pool is full (the oracle keeps NPK = 4 contacts in pair order and drops later ones): the
+    team narrowphase keeps each lane's NPK contacts of smallest pair order (round 6, gs_team.hip team_lc), so a
+    lane that finds more than two contacts -- which took the replicated narrowphase before -- still yields the
+    oracle's pool."""
+    states = crossed_leg_states(32, seed=5, min_contacts=4, spread=1.8, pool=200)
+    _sim_vs_oracle(host=False, variant=2, n=32, states=states)
 
 
 def _pool_vs_oracle(pools, flat, root, dof, mu, what):
