@@ -70,7 +70,7 @@ struct DevParams {
   int substeps;
   float g[3];
   int pos_iters, vel_iters;
-  int tgs;               // physx.solver_type 1: TGS position sub-steps (lane-team kernel only)
+  int tgs;               // physx.solver_type 1: TGS position sub-steps (every kernel form and the host backend)
   float contact_offset, rest_offset, max_depen_vel;
   float ground_mu;       // ground plane friction (0.5*(mu_shape + mu_ground) is the pair friction)
   int has_ground;

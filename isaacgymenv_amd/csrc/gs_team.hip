@@ -71,6 +71,19 @@ __device__ __forceinline__ float quad_sum(float x) {
   x = x + qperm<0xB1>(x);  // quad_perm(1,0,3,2)
   return x + qperm<0x4E>(x);  // quad_perm(2,3,0,1)
 }
+// packed f32 pairs (v_pk_fma_f32 on gfx950; a broadcast operand is op_sel_hi, not a move)
+typedef float f2 __attribute__((ext_vector_type(2)));
+#ifndef GS_TEAM_PK
+#define GS_TEAM_PK 0  // 1: v_pk_fma_f32 for the row-0/1 partials -- measured slower (r06d: 0.1101 vs 0.1059 ms)
+#endif
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) {
+#if GS_TEAM_PK
+  return __builtin_elementwise_fma(a, b, c);
+#else
+  return f2{fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y)};
+#endif
+}
+
 // three independent quad sums, interleaved so no DPP read waits on the VALU write before it
 __device__ __forceinline__ void quad_sum3(float* u) {
   const float a0 = qperm<0xB1>(u[0]), a1 = qperm<0xB1>(u[1]), a2 = qperm<0xB1>(u[2]);
@@ -145,14 +158,17 @@ constexpr int RW = kTeamBlock + 1;
 template <class T>
 struct RowSlots {
   static constexpr int CL = T::T_CL;
-  // A Z row's 9 components (base 6 | chain 3) plus c = J nu_f in PGS-owner order, four consecutive
-  // slots per lane (two paired LDS loads; the four lanes of a team hit four different banks):
+  // A Z row's 9 components (base 6 | chain 3) plus c = J nu_f in PGS-owner order, four slots per lane:
   // lane l < 3 owns base 2l, base 2l+1 and chain component l (slot 4l+3 a zero pad), lane 3 holds
-  // only c (slot 15), so every lane's partial of u = c + Z w is the same three FMAs.
+  // only c (slot 15), so every lane's partial of u = c + Z w is the same three FMAs.  Rows 0 and 1 are
+  // stored interleaved (zs): a slot's row-0 and row-1 values are adjacent, one paired LDS load lands them
+  // in a register pair, and the two rows' partials are three v_pk_fma_f32 (round 6).
   static constexpr int ZROW = 16;
   static constexpr int RZROW = 16;
   static constexpr int CSLOT = 15;
   __device__ static constexpr int zslot(int comp) { return comp < 6 ? 4 * (comp >> 1) + (comp & 1) : 4 * (comp - 6) + 2; }
+  // offset of row rr's slot s inside a record's Z block
+  __device__ static constexpr int zs(int rr, int s) { return rr < 2 ? 2 * s + rr : 2 * ZROW + s; }
   // (C_SEP / R_SEP: the row's separation at the substep's start, for TGS's per-sub-step targets)
   static constexpr int C_DI = 3 * ZROW, C_G = C_DI + 3, C_TP = C_G + 3, C_TV = C_TP + 1,
                        C_MU = C_TV + 1, C_ACT = C_MU + 1, C_SEP = C_ACT + 1, PER_CONTACT = C_SEP + 1;
@@ -169,7 +185,6 @@ struct RowSlots {
   static constexpr int POOL = CHAIN + ROOT;
   static constexpr int TOTAL = POOL + PER_POOL * T::NPK;
   __device__ static constexpr int chain(int j) { return j * PER_CONTACT; }
-  __device__ static constexpr int chain_row(int j, int rr) { return j * PER_CONTACT + rr * ZROW; }
   __device__ static constexpr int root(int j) { return CHAIN + j * PER_ROOT; }
 };
 
@@ -389,6 +404,13 @@ __device__ __forceinline__ float base_jac(const float* xc, int ax, int k) {
 __device__ __forceinline__ int opaque_index(int x) {
   asm volatile("" : "+v"(x));
   return x;
+}
+
+// floats per lane of the sweeps' LDS stash (substep_team stash_io): the base block's L factors, 1/sqrt(D) and free
+// velocity, then per chain dof its Mcb row, Mcc row, 1/sqrt(D) and free velocity
+template <class T>
+__host__ __device__ constexpr int team_stash_size() {
+  return 15 + 6 + 6 + T::T_CL * (6 + 2) + T::T_CL * (T::T_CL - 1) / 2;
 }
 
 // Per-team shape table for the self-collision prepass: [(kShW * sh + f) * TPW + team] (TPW teams per workgroup)
@@ -964,7 +986,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
                                              float* __restrict__ rows_own, const float* __restrict__ rows_team,
                                              float* __restrict__ cf_soa, bool collect,
                                              float* __restrict__ cf_aos, float* __restrict__ shw_tab,
-                                             const float* __restrict__ sct GS_PROF_PARAM) {
+                                             const float* __restrict__ sct, float* __restrict__ stash GS_PROF_PARAM) {
   constexpr int CL = T::T_CL, CC = T::T_CC, RC = T::T_RC, NCH = T::T_NCH, LN = T::T_LANES;
   static_assert(NCH == LN && LN == 4, "lane teams are DPP quads with one chain per lane");
   using C = CM<T>;
@@ -1264,16 +1286,16 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
               const float* d = dir[rr];
               float xd[3];  // the row's angular part: d.(w x xc) = w.(xc x d)
               cross3(xc, d, xd);
-              float* row = rows_own + RS::chain_row(j, rr) * RW;
+              float* row = rows_own + RS::chain(j) * RW;
 #pragma unroll
-              for (int b = 0; b < 6; ++b) row[RS::zslot(b) * RW] = b < 3 ? xd[b] : d[b - 3];
+              for (int b = 0; b < 6; ++b) row[RS::zs(rr, RS::zslot(b)) * RW] = b < 3 ? xd[b] : d[b - 3];
 #pragma unroll
               for (int kk = 0; kk < CL; ++kk) {
                 float v = 0.f;
                 if (kk <= k)
                   v = S[kk][3] * d[0] + S[kk][4] * d[1] + S[kk][5] * d[2] + S[kk][0] * xd[0] + S[kk][1] * xd[1] +
                       S[kk][2] * xd[2];
-                row[RS::zslot(6 + kk) * RW] = v;
+                row[RS::zs(rr, RS::zslot(6 + kk)) * RW] = v;
               }
             }
           }
@@ -1287,9 +1309,9 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
 #pragma unroll
           for (int rr = 0; rr < 3; ++rr) {
             const int ax3 = (rr == 0) ? 2 : (rr == 1 ? 0 : 1);
-            float* row = rows_own + RS::chain_row(j, rr) * RW;
+            float* row = rows_own + RS::chain(j) * RW;
 #pragma unroll
-            for (int b = 0; b < 6; ++b) row[RS::zslot(b) * RW] = base_jac(xc, ax3, b);
+            for (int b = 0; b < 6; ++b) row[RS::zs(rr, RS::zslot(b)) * RW] = base_jac(xc, ax3, b);
 #pragma unroll
             for (int kk = 0; kk < CL; ++kk) {
               float v = 0.f;
@@ -1298,7 +1320,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
                 cross3(S[kk], xc, tt);
                 v = S[kk][3 + ax3] + tt[ax3];
               }
-              row[RS::zslot(6 + kk) * RW] = v;
+              row[RS::zs(rr, RS::zslot(6 + kk)) * RW] = v;
             }
           }
         }
@@ -1476,13 +1498,14 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       float zr[3][6 + CL], dir[3];
 #pragma unroll
       for (int rr = 0; rr < 3; ++rr) {
-        float* row = rows_own + RS::chain_row(j, rr) * RW;
+        float* row = rows_own + RS::chain(j) * RW;
+        auto Z = [&](int sl) -> float& { return row[RS::zs(rr, sl) * RW]; };
         float zb[6], zc[CL];
         float cj = 0.f;
 #pragma unroll
-        for (int b = 0; b < 6; ++b) { zb[b] = row[RS::zslot(b) * RW]; cj += zb[b] * nufb[b]; }
+        for (int b = 0; b < 6; ++b) { zb[b] = Z(RS::zslot(b)); cj += zb[b] * nufb[b]; }
 #pragma unroll
-        for (int k = 0; k < CL; ++k) { zc[k] = row[RS::zslot(6 + k) * RW]; if (k <= kb) cj += zc[k] * nufc[k]; }
+        for (int k = 0; k < CL; ++k) { zc[k] = Z(RS::zslot(6 + k)); if (k <= kb) cj += zc[k] * nufc[k]; }
         // leaf -> root: chain nodes kb..0 then base 5..0
 #pragma unroll
         for (int kk = 0; kk < CL; ++kk) {
@@ -1505,23 +1528,23 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         for (int b = 0; b < 6; ++b) {
           zb[b] *= sDb[b];
           d += zb[b] * zb[b];
-          row[RS::zslot(b) * RW] = zb[b];
+          Z(RS::zslot(b)) = zb[b];
           zr[rr][b] = zb[b];
         }
 #pragma unroll
         for (int k = 0; k < CL; ++k) {
           const float z = k <= kb ? zc[k] * sDc[k] : 0.f;
           d += z * z;
-          row[RS::zslot(6 + k) * RW] = z;
+          Z(RS::zslot(6 + k)) = z;
           zr[rr][6 + k] = z;
         }
-        row[3 * RW] = 0.f;  // pads: lanes 0-2 add no constant, lane 3 owns no component
-        row[7 * RW] = 0.f;
-        row[11 * RW] = 0.f;
-        row[12 * RW] = 0.f;
-        row[13 * RW] = 0.f;
-        row[14 * RW] = 0.f;
-        row[RS::CSLOT * RW] = cj;
+        Z(3) = 0.f;  // pads: lanes 0-2 add no constant, lane 3 owns no component
+        Z(7) = 0.f;
+        Z(11) = 0.f;
+        Z(12) = 0.f;
+        Z(13) = 0.f;
+        Z(14) = 0.f;
+        Z(RS::CSLOT) = cj;
         dir[rr] = d > 0.f ? __builtin_amdgcn_rcpf(d) : 0.f;  // (d == 0: a row the chain cannot move along)
         rec[(RS::C_DI + rr) * RW] = dir[rr];
       }
@@ -1593,19 +1616,19 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
         for (int b = 0; b < 6; ++b) {
           zb[b] *= sDb[b];
           d += zb[b] * zb[b];
-          rec[(rr * RS::RZROW + RS::zslot(b)) * RW] = zb[b];
+          rec[RS::zs(rr, RS::zslot(b)) * RW] = zb[b];
           zr[rr][b] = zb[b];
         }
-        float* rz = rec + rr * RS::RZROW * RW;
+        auto Z = [&](int sl) -> float& { return rec[RS::zs(rr, sl) * RW]; };
 #pragma unroll
         for (int k = 0; k < 3; ++k) {  // no chain components; pads as in the chain records
-          rz[(4 * k + 2) * RW] = 0.f;
-          rz[(4 * k + 3) * RW] = 0.f;
+          Z(4 * k + 2) = 0.f;
+          Z(4 * k + 3) = 0.f;
         }
-        rz[12 * RW] = 0.f;
-        rz[13 * RW] = 0.f;
-        rz[14 * RW] = 0.f;
-        rz[RS::CSLOT * RW] = cj;
+        Z(12) = 0.f;
+        Z(13) = 0.f;
+        Z(14) = 0.f;
+        Z(RS::CSLOT) = cj;
         dir[rr] = d > 0.f ? __builtin_amdgcn_rcpf(d) : 0.f;  // (d == 0: a row the chain cannot move along)
         rec[(RS::R_DI + rr) * RW] = dir[rr];
       }
@@ -1741,6 +1764,33 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
   __syncthreads();
 
   GS_PROF(3)  // contact records
+  // The factorisation and the free velocity are read again only after the sweeps (back-substitution): they wait
+  // in the lane's LDS stash meanwhile, so the sweeps have their registers (the records of all contacts in flight,
+  // register pairs for the packed row partials) -- round 6; they spilled to scratch otherwise
+  auto stash_io = [&](bool save) {
+    int q = 0;
+    auto io = [&](float& v) {
+      if (save) stash[q * kTeamBlock] = v; else v = stash[q * kTeamBlock];
+      ++q;
+    };
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+#pragma unroll
+      for (int b = 0; b < k; ++b) io(Mbb[k][b]);
+      io(sDb[k]);
+      io(nufb[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < CL; ++k) {
+#pragma unroll
+      for (int b = 0; b < 6; ++b) io(Mcb[k][b]);
+#pragma unroll
+      for (int j = 0; j < k; ++j) io(Mcc[k][j]);
+      io(sDc[k]);
+      io(nufc[k]);
+    }
+  };
+  stash_io(true);
   // ================= projected Gauss-Seidel, global contact order: root candidates, chain 0, 1, ...
   // The 9 velocity components a chain contact row touches (base 6 | its chain's 3) are spread over
   // the team: lane l < 3 owns base 2l, base 2l+1 and chain component l (RowSlots).  Each lane forms
@@ -1790,12 +1840,15 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     for (int j = 0; j < RC; ++j) {
       if (ract[j]) {
         const float* rec = rows_own + RS::root(j) * RW;
-        const float* recl = rec + 4 * lc * RW;
         float z[12], u[4];
 #pragma unroll
-        for (int i = 0; i < 12; ++i) z[i] = recl[((i >> 2) * RS::RZROW + (i & 3)) * RW];
-#pragma unroll
-        for (int rr = 0; rr < 3; ++rr) u[rr] = fmaf(z[4 * rr], wA, fmaf(z[4 * rr + 1], wA2, z[4 * rr + 3]));
+        for (int i = 0; i < 12; ++i) z[i] = rec[RS::zs(i >> 2, 4 * lc + (i & 3)) * RW];
+        {
+          const f2 u01 = pk_fma(f2{z[0], z[4]}, f2{wA, wA}, pk_fma(f2{z[1], z[5]}, f2{wA2, wA2}, f2{z[3], z[7]}));
+          u[0] = u01.x;
+          u[1] = u01.y;
+        }
+        u[2] = fmaf(z[8], wA, fmaf(z[9], wA2, z[11]));
         float tdi;
         if constexpr (tgs) {
           u[3] = fmaf(z[0], aA, fmaf(z[1], aA2, na * z[3]));
@@ -1820,10 +1873,9 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     auto fetch = [&](int n) {
       const int cc = n / CC, j = n - (n / CC) * CC;
       const float* rec = rows_team + cc + RS::chain(j) * RW;
-      const float* recl = rec + 4 * lc * RW;
       nact = rec[RS::C_ACT * RW];
 #pragma unroll
-      for (int i = 0; i < 12; ++i) nz[i] = recl[((i >> 2) * RS::ZROW + (i & 3)) * RW];
+      for (int i = 0; i < 12; ++i) nz[i] = rec[RS::zs(i >> 2, 4 * lc + (i & 3)) * RW];
 #pragma unroll
       for (int i = 0; i < 6; ++i) nk[i] = rec[(RS::C_DI + i) * RW];
       nk[6] = rec[(tgs ? RS::C_SEP : tsel) * RW];
@@ -1842,6 +1894,9 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
       // (the scheduler hoists all 12 records' loads to the top of the sweep and parks them in AGPRs;
       // measured faster than keeping the prefetch one contact deep with a scheduling fence:
       // 0.0886 vs 0.0915 ms per launch, profiles/r02o_experiments_team_pgs.txt)
+#ifdef GS_PGS_FENCE
+      __builtin_amdgcn_sched_barrier(0);  // (A/B: keep the prefetch one contact deep)
+#endif
       if (n + 1 < NCH * CC) fetch(n + 1);
       const bool a_o = act_n != 0.f;
 #ifdef GS_PHASE_PROFILE
@@ -1849,9 +1904,14 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
 #endif
       if (a_o) {
         float u[4];
-#pragma unroll
-        for (int rr = 0; rr < 3; ++rr)  // the w terms last (they carry the Gauss-Seidel chain)
-          u[rr] = fmaf(z[4 * rr], wA, fmaf(z[4 * rr + 1], wA2, fmaf(z[4 * rr + 2], wC[cc], z[4 * rr + 3])));
+        {  // the w terms last (they carry the Gauss-Seidel chain); rows 0 and 1 as register pairs
+          const f2 u01 = pk_fma(f2{z[0], z[4]}, f2{wA, wA},
+                                pk_fma(f2{z[1], z[5]}, f2{wA2, wA2}, pk_fma(f2{z[2], z[6]}, f2{wC[cc], wC[cc]},
+                                                                         f2{z[3], z[7]})));
+          u[0] = u01.x;
+          u[1] = u01.y;
+        }
+        u[2] = fmaf(z[8], wA, fmaf(z[9], wA2, fmaf(z[10], wC[cc], z[11])));
         float tdi = k8[6];
         if constexpr (tgs) {
           u[3] = fmaf(z[0], aA, fmaf(z[1], aA2, fmaf(z[2], aC[cc], na * z[3])));
@@ -1943,6 +2003,7 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     for (int k = 0; k < CL; ++k) wcp[k] = wc[k];
   }
   __syncthreads();  // the next substep rewrites the records other lanes just read
+  stash_io(false);
 
   GS_PROF(4)  // PGS
   // ================= dnu = L^-1 D^-1/2 w (base first, then the chain)
@@ -2120,6 +2181,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel*
   // the team's shape friction (constant over the launch), read by the contact records and the self-contact pool
   // from LDS instead of device memory every substep: [shape][team]
   __shared__ float mu_tab[T::NS * kTeamsPerBlock];
+  __shared__ float stash_tab[team_stash_size<T>() * kTeamBlock];
   stage_chain_model<T>(M, mdl);
   stage_shape_consts<T>(M, sct);
   const int lc = threadIdx.x & (LN - 1);
@@ -2140,7 +2202,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_simulate_team(const DevModel*
   GS_PROF_DECL
   for (int sstep = 0; sstep < P.substeps; ++sstep) {
     const bool last = (sstep == P.substeps - 1) && P.collect;
-    substep_team<T, TERR, TGS>(M, mdl, P, s, tau, mu_t, N, e, lc, own, team, B.cf, last, nullptr, shw_tab, sct GS_PROF_ARGS);
+    substep_team<T, TERR, TGS>(M, mdl, P, s, tau, mu_t, N, e, lc, own, team, B.cf, last, nullptr, shw_tab, sct, stash_tab + threadIdx.x GS_PROF_ARGS);
   }
   team_store<T>(B.state, N, opaque_index(e), opaque_index(lc), s);
   GS_PROF_FLUSH
@@ -2157,6 +2219,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
   // the team's shape friction (constant over the launch), read by the contact records and the self-contact pool
   // from LDS instead of device memory every substep: [shape][team]
   __shared__ float mu_tab[T::NS * kTeamsPerBlock];
+  __shared__ float stash_tab[team_stash_size<T>() * kTeamBlock];
   stage_chain_model<T>(M, mdl);
   stage_shape_consts<T>(M, sct);
   const int lc = threadIdx.x & (LN - 1);
@@ -2193,7 +2256,7 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
     const bool last = ((it % sub) == sub - 1) && P.collect;
     GS_PROF(6)  // PD torque
     float* cf_aos = (it == total - 1) ? A.cf_out : nullptr;
-    substep_team<T, TERR, TGS>(M, mdl, P, s, tau, mu_t, N, e, lc, own, team, B.cf, last, cf_aos, shw_tab, sct GS_PROF_ARGS);
+    substep_team<T, TERR, TGS>(M, mdl, P, s, tau, mu_t, N, e, lc, own, team, B.cf, last, cf_aos, shw_tab, sct, stash_tab + threadIdx.x GS_PROF_ARGS);
     if (it == n_pd - 1 && A.dof_out) {
       const size_t d0 = dof0();
 #pragma unroll

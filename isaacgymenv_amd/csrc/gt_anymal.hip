@@ -16,6 +16,11 @@
 #include "../../include/gymtask.h"
 #include "torch_philox.h"
 
+// k_reset_flagged's episode-sum hand-off depends on gfx950's L2-served agent-scope atomics (see there)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "gt_anymal.hip targets gfx950 only (the k_reset_flagged hand-off ordering is gfx950's)"
+#endif
+
 namespace {
 thread_local std::string g_err;
 
@@ -477,6 +482,10 @@ __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_any
   // each wave waits for its own stores before ONE lane adds to the unsharded counter, and the wave
   // whose add returned last loads.  No __threadfence(): two of those per wave (~3.5 us each) were
   // most of this kernel's time.
+  // The ordering this hand-off relies on is gfx950's (agent-scope relaxed atomics are served by L2, the one
+  // coherence point of the agent; vmcnt(0) retires this wave's stores there before its counter add; the last
+  // wave's loads read L2): under the scoped C++ model a release on the add and an acquire in the last wave would be
+  // needed, at the cost of the cache write-back / invalidate above.  The build is gfx950-only (the #error below).
   // slot NT (terrain): the wave's sum of terrain levels after the update, for mean(terrain_levels)
   constexpr int NT = GT_ANYMAL_NUM_TERMS + 1;
 #pragma unroll

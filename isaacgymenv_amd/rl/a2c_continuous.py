@@ -299,7 +299,12 @@ class A2CAgent:
         # (gae.policy_kl / gae.adaptive_lr, rl_policy.hip) instead of ~14 torch ones
         self._fused_kl = self._fused_loss and self._opt_lr is not None
         # ... and with the grouped actor / critic layout the heads join the loss pass (network.stacked_hidden)
-        self._fused_heads = self._fused_loss and net.grouped is not None and self.mixed_precision
+        # (only where its kernels tile the shapes: every minibatch a multiple of 128 rows -- GroupedMLPSpec.applies --
+        # and a last hidden width rl_ppo_heads_loss takes; elsewhere the grouped MLPs + PpoLossFn path runs, decided
+        # here because the fused path normalises the input (a running-moments update) before it could fall back)
+        self._fused_heads = (self._fused_loss and net.grouped is not None and self.mixed_precision
+                             and self.cfg.minibatch_size % 128 == 0
+                             and net.mu.in_features in network_mod.HEADS_HIDDEN_SIZES)
         # that path writes every parameter's gradient exactly once (MLP layers, heads, sigma): no zeroing needed
         covered = (sum(p.numel() for p in net.grouped.params) + net.mu.weight.numel() + net.mu.bias.numel()
                    + net.value.weight.numel() + net.value.bias.numel() + net.sigma.numel()) if self._fused_heads else -1

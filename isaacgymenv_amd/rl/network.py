@@ -28,6 +28,8 @@ _ACT = {"elu": nn.ELU, "relu": nn.ReLU, "tanh": nn.Tanh, "selu": nn.SELU, "None"
 # cores as libgymrl's rl_linear_* kernels (csrc/rl_linear.hip): bias and ELU fused into the GEMM epilogue, ELU's
 # backward fused into the dX / dW GEMMs' operand loads.  Off: the torch Linear / ELU statements above.
 USE_MFMA_LAYERS = os.environ.get("IGE_MFMA_LAYERS", "1") != "0"  # (an A/B switch for the bench)
+# last hidden widths the fused heads + loss kernel takes (rl_ppo_loss.hip heads_check)
+HEADS_HIDDEN_SIZES = (32, 64, 128, 256)
 SPLIT_K = 16
 SPLIT_K_MIN_ROWS = 4096
 
@@ -434,6 +436,8 @@ class ActorCriticNetwork(nn.Module):
                 or self.sigma.grad is None or mu.in_features % 2):
             return None
         H = mu.in_features
+        if H not in HEADS_HIDDEN_SIZES:
+            return None
         heads = gae.HeadsSpec(0, H, H, mu.half_weight, mu.half_bias, val.half_weight, val.half_bias, mu.weight.grad,
                               mu.bias.grad, val.weight.grad, val.bias.grad, self.sigma.grad, store=True)
         return _GroupedMLPFn.apply(obs, self.grouped, True, *self.grouped.params), heads

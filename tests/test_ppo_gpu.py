@@ -1104,3 +1104,31 @@ def test_rms_normalize_half_output_is_the_rounded_f32_output():
     assert y1.dtype == torch.float16 and torch.equal(y1, y0.half())
     for a, b in zip(m0, m1):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("over", [{"units": [512, 512], "minibatch_size": 3072}, {"minibatch_size": 192}])
+def test_learner_outside_the_fused_heads_shapes_trains(over):
+    """the fused heads + loss pass only where its kernels tile the shapes (minibatch rows a multiple of
+    128, last hidden width 32 / 64 / 128 / 256); a [512, 512] MLP or a 192-row minibatch takes the grouped MLPs +
+    PpoLossFn path instead of failing at the first minibatch."""
+    agent = _agent("AnymalTerrain", 512, **over)
+    assert not agent._fused_heads
+    agent.env_reset()
+    for _ in range(2):
+        agent.train_epoch()
+    torch.cuda.synchronize()
+    assert torch.isfinite(agent.flat_param).all()
+
+
+def test_fused_heads_minibatch_writes_every_gradient():
+    """the fused heads path never zeroes the flat gradient (every element has exactly one writer,
+    A2CAgent._grad_store_covers_all): poison the buffer with NaN before one minibatch and check that every element
+    is overwritten."""
+    agent = _agent("AnymalTerrain", 512, minibatch_size=3072)
+    assert agent._fused_heads and agent._grad_store_covers_all
+    agent.env_reset()
+    agent.train_epoch()  # a real dataset in the buffers
+    agent.flat_grad.fill_(float("nan"))
+    agent._mb_forward_backward(0)
+    torch.cuda.synchronize()
+    assert torch.isfinite(agent.flat_grad).all(), int((~torch.isfinite(agent.flat_grad)).sum())
