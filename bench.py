@@ -309,17 +309,42 @@ def main():
         print(json.dumps(line), file=out, flush=True)
 
 
-def _main():
-    args = parse()
+def dist_setup(backend: str = "nccl"):
+    """One process per GPU (torch.distributed.run sets RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*): joins the
+    process group when WORLD_SIZE > 1 -- "nccl" is RCCL over xGMI on the box; the CPU tests pass "gloo" -- and
+    returns (world, rank, local_rank).  The env shards (num_envs per rank) are independent: the only collectives
+    are the timed region's barrier / max-over-ranks and the PPO leg's gradient all-reduce."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+    return world, rank, local_rank
+
+
+def collective_info(world: int, ppo) -> dict:
+    """What the N-rank run exchanges: the backend and world size of the process group, and the
+    PPO learner's one flat-gradient all-reduce per minibatch (2,094,692 B for AnymalTerrainPPO's network)."""
+    import torch.distributed as dist
+    on = world > 1 and dist.is_initialized()
+    return {"backend": (("rccl" if dist.get_backend() == "nccl" else dist.get_backend()) if on else None),
+            "world_size": dist.get_world_size() if on else 1,
+            "env_data_path": "none (num_envs shards per rank, no exchange; barrier + max-over-ranks time only)",
+            "ppo_allreduce_bytes_per_minibatch": (ppo or {}).get("allreduce_bytes_per_minibatch")}
+
+
+def _main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world, rank, local_rank = dist_setup()
     device = f"cuda:{local_rank}"
 
     import isaacgymenvs
@@ -441,6 +466,7 @@ def _main():
             "cpu_baseline": cpu,
             "ppo": ppo,
             "other_configs": others,
+            "collective": collective_info(world, ppo),
         }
     else:
         line = None

@@ -1930,46 +1930,73 @@ __device__ __forceinline__ void substep_team(const DevModel* __restrict__ Min, c
     }
     if constexpr (T::NPK > 0) {
       const int psel = it < P.pos_iters ? RS::P_TP : RS::P_TV;
-      for (int p = 0; p < npc; ++p) {
-        float* o = pool + RS::PER_POOL * p * RW;
-        const int ca = (int)o[RS::P_CA * RW], cb = (int)o[RS::P_CB * RW];
-        float wa = 0.f, wb = 0.f, ana = 0.f, anb = 0.f;
+      // unrolled over the pool's NPK slots with the next entry's record loaded ahead (as the chain contacts);
+      // the wave runs as many entries as its fullest team has (npc is per team)
+      float pz[15], pk[11];  // Z components | lam (3), 1/G_rr (3), couplings (3), target (TGS: separation), mu
+      int pca = 0, pcb = 0;
+      auto pfetch = [&](int p) {
+        const float* o = pool + RS::PER_POOL * p * RW;
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          wa = c == ca ? wC[c] : wa;
-          wb = c == cb ? wC[c] : wb;
-          ana = c == ca ? aC[c] : ana;
-          anb = c == cb ? aC[c] : anb;
+        for (int i = 0; i < 15; ++i) pz[i] = o[(RS::P_Z + i) * RW];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          pk[i] = o[(kPoolLam + i) * RW];
+          pk[3 + i] = o[(RS::P_DI + i) * RW];
+          pk[6 + i] = o[(RS::P_G + i) * RW];
         }
-        float z[15], u[4];
+        pk[9] = o[(tgs ? (int)kPoolSep : psel) * RW];
+        pk[10] = o[kPoolMu * RW];
+        pca = (int)o[RS::P_CA * RW];
+        pcb = (int)o[RS::P_CB * RW];
+      };
+      const unsigned long long any_pool = __ballot(npc > 0);
+      if (any_pool) pfetch(0);
 #pragma unroll
-        for (int i = 0; i < 15; ++i) z[i] = o[(RS::P_Z + i) * RW];
+      for (int p = 0; p < T::NPK; ++p) {
+        if (__ballot(p < npc) == 0ull) break;
+        float z[15], k11[11];
 #pragma unroll
-        for (int rr = 0; rr < 3; ++rr)
-          u[rr] = fmaf(z[5 * rr], wA, fmaf(z[5 * rr + 1], wA2, fmaf(z[5 * rr + 2], wa, fmaf(z[5 * rr + 3], wb, z[5 * rr + 4]))));
-        float lam[3] = {o[kPoolLam * RW], o[(kPoolLam + 1) * RW], o[(kPoolLam + 2) * RW]};
-        float tdi;
-        if constexpr (tgs) {
-          u[3] = fmaf(z[0], aA, fmaf(z[1], aA2, fmaf(z[2], ana, fmaf(z[3], anb, na * z[4]))));
-          quad_sum4(u);
-          tdi = tgs_tdi(o[kPoolSep * RW], u[3], o[RS::P_DI * RW]);
-        } else {
-          quad_sum3(u);
-          tdi = o[psel * RW];
+        for (int i = 0; i < 15; ++i) z[i] = pz[i];
+#pragma unroll
+        for (int i = 0; i < 11; ++i) k11[i] = pk[i];
+        const int ca = pca, cb = pcb;
+        if (p + 1 < T::NPK) pfetch(p + 1);
+        if (p < npc) {
+          float wa = 0.f, wb = 0.f, ana = 0.f, anb = 0.f;
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) {
+            wa = c == ca ? wC[c] : wa;
+            wb = c == cb ? wC[c] : wb;
+            ana = c == ca ? aC[c] : ana;
+            anb = c == cb ? aC[c] : anb;
+          }
+          float u[4];
+#pragma unroll
+          for (int rr = 0; rr < 3; ++rr)
+            u[rr] = fmaf(z[5 * rr], wA, fmaf(z[5 * rr + 1], wA2, fmaf(z[5 * rr + 2], wa, fmaf(z[5 * rr + 3], wb, z[5 * rr + 4]))));
+          float lam[3] = {k11[0], k11[1], k11[2]};
+          float tdi = k11[9];
+          if constexpr (tgs) {
+            u[3] = fmaf(z[0], aA, fmaf(z[1], aA2, fmaf(z[2], ana, fmaf(z[3], anb, na * z[4]))));
+            quad_sum4(u);
+            tdi = tgs_tdi(k11[9], u[3], k11[3]);
+          } else {
+            quad_sum3(u);
+          }
+          float dl0, dl1, dl2;
+          contact_block(u[0], u[1], u[2], k11[3], k11[4], k11[5], k11[6], k11[7], k11[8], tdi, k11[10], lam, dl0, dl1,
+                        dl2);
+          float* o = pool + RS::PER_POOL * p * RW;
+          o[kPoolLam * RW] = lam[0];
+          o[(kPoolLam + 1) * RW] = lam[1];
+          o[(kPoolLam + 2) * RW] = lam[2];
+          wA = fmaf(z[10], dl2, fmaf(z[5], dl1, fmaf(z[0], dl0, wA)));
+          wA2 = fmaf(z[11], dl2, fmaf(z[6], dl1, fmaf(z[1], dl0, wA2)));
+          const float da = fmaf(z[12], dl2, fmaf(z[7], dl1, z[2] * dl0));
+          const float db = fmaf(z[13], dl2, fmaf(z[8], dl1, z[3] * dl0));
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) wC[c] += (c == ca ? da : 0.f) + (c == cb ? db : 0.f);
         }
-        float dl0, dl1, dl2;
-        contact_block(u[0], u[1], u[2], o[RS::P_DI * RW], o[(RS::P_DI + 1) * RW], o[(RS::P_DI + 2) * RW],
-                      o[RS::P_G * RW], o[(RS::P_G + 1) * RW], o[(RS::P_G + 2) * RW], tdi, o[kPoolMu * RW], lam,
-                      dl0, dl1, dl2);
-        o[kPoolLam * RW] = lam[0];
-        o[(kPoolLam + 1) * RW] = lam[1];
-        o[(kPoolLam + 2) * RW] = lam[2];
-        wA = fmaf(z[10], dl2, fmaf(z[5], dl1, fmaf(z[0], dl0, wA)));
-        wA2 = fmaf(z[11], dl2, fmaf(z[6], dl1, fmaf(z[1], dl0, wA2)));
-        const float da = fmaf(z[12], dl2, fmaf(z[7], dl1, z[2] * dl0));
-        const float db = fmaf(z[13], dl2, fmaf(z[8], dl1, z[3] * dl0));
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) wC[c] += (c == ca ? da : 0.f) + (c == cb ? db : 0.f);
       }
     }
 #ifdef GS_PHASE_PROFILE

@@ -9,6 +9,7 @@ import ctypes as C
 import os
 
 import torch
+from isaacgymenv_amd._stream import raw_stream
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libgymtask.so")
 
@@ -227,7 +228,7 @@ class AntTailKernel:
         r.initial_dof_pos, r.initial_root_states = t.initial_dof_pos.data_ptr(), t.initial_root_states.data_ptr()
         r.dof_state, r.progress_buf, r.env_ids_out = t.dof_state.data_ptr(), t.progress_buf.data_ptr(), \
             self.env_ids.data_ptr()
-        stream = torch.cuda.current_stream(t.root_states.device).cuda_stream
+        stream = raw_stream(t.root_states.device)
         _check(lib().gt_ant_reset_flagged(C.byref(self.p), C.byref(self._buffers()), k, C.byref(r),
                                           C.c_void_p(stream)), "gt_ant_reset_flagged")
         ids = self.env_ids[:k]
@@ -258,7 +259,7 @@ class AntTailKernel:
         t = self.env
         self._seq += 1
         b = self._buffers()
-        stream = torch.cuda.current_stream(t.root_states.device).cuda_stream
+        stream = raw_stream(t.root_states.device)
         _check(lib().gt_ant_post_physics(C.byref(self.p), C.byref(b), C.c_void_p(stream)), "gt_ant_post_physics")
         self._launched = True
 
@@ -293,7 +294,7 @@ class HoundControlKernel:
     def __call__(self, actions, torques_out):
         import torch
         env = self.env
-        stream = torch.cuda.current_stream(actions.device).cuda_stream
+        stream = raw_stream(actions.device)
         _check(lib().gt_hound_control(C.byref(self.p), actions.data_ptr(), env.dof_state.data_ptr(),
                                       self.leg_default.data_ptr(), env._mm_full.data_ptr(), env._jac_full.data_ptr(),
                                       env._rigid_body_state.data_ptr(), torques_out.data_ptr(),
@@ -452,7 +453,7 @@ class AnymalTailKernels:
         return b
 
     def _stream(self):
-        return torch.cuda.current_stream(self.task.device).cuda_stream
+        return raw_stream(self.task.device)
 
     def post_a(self):
         t = self.task

@@ -33,6 +33,8 @@ from . import _assets
 from ._assets import build_articulation, load_raw, mat_to_quat_xyzw, quat_xyzw_to_mat
 from ._model import flatten
 from . import _lib
+from isaacgymenv_amd._stream import raw_stream
+
 
 class PhysicsDeviationWarning(UserWarning):
     """A requested PhysX feature the MI355X solver does not reproduce (DESIGN.md sections 3 and 6)."""
@@ -362,7 +364,7 @@ class Sim:
         if self.host:
             return None  # host backend: every call completes before it returns
         import torch
-        return torch.cuda.current_stream(self.sim_device).cuda_stream
+        return raw_stream(self.sim_device)
 
     # -------- prepare: allocate + bind tensors, initial state
     def prepare(self):

@@ -12,6 +12,7 @@ import ctypes as C
 import os
 
 import torch
+from isaacgymenv_amd._stream import raw_stream
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib", "libgymrl.so")
 EXPORTED_SYMBOLS = ["rl_abi_version", "rl_last_error", "rl_gae", "rl_splitk_accum", "rl_colsum_accum", "rl_rollout_post",
@@ -171,7 +172,7 @@ def discount_values(rewards, values, dones, last_values, last_dones, gamma: floa
     returns = torch.empty(N * H, dtype=torch.float32, device=rewards.device)
     advs = torch.empty_like(returns)
     vals = torch.empty_like(returns)
-    stream = torch.cuda.current_stream(rewards.device).cuda_stream
+    stream = raw_stream(rewards.device)
     rc = lib().rl_gae(rewards.data_ptr(), values.data_ptr(), dones.data_ptr(), last_values.data_ptr(),
                       last_dones.data_ptr(), H, N, float(gamma), float(tau), returns.data_ptr(), advs.data_ptr(),
                       vals.data_ptr(), stream)
@@ -187,7 +188,7 @@ def splitk_accum(parts: torch.Tensor, grad: torch.Tensor) -> None:
     assert parts.is_cuda and grad.is_cuda and parts.device == grad.device
     assert parts.is_contiguous() and grad.is_contiguous() and grad.dtype == torch.float32
     assert parts.dtype in (torch.float16, torch.float32) and parts[0].numel() == grad.numel()
-    stream = torch.cuda.current_stream(grad.device).cuda_stream
+    stream = raw_stream(grad.device)
     rc = lib().rl_splitk_accum(parts.data_ptr(), parts.shape[0], grad.numel(), int(parts.dtype == torch.float16),
                                grad.data_ptr(), stream)
     if rc != 0:
@@ -210,7 +211,7 @@ def colsum_accum(g: torch.Tensor, grad: torch.Tensor) -> None:
     ws = _COLSUM_WORK.get(g.device)
     if ws is None:
         ws = _COLSUM_WORK[g.device] = torch.empty(256 * 2048, dtype=torch.float32, device=g.device)
-    stream = torch.cuda.current_stream(g.device).cuda_stream
+    stream = raw_stream(g.device)
     rc = lib().rl_colsum_accum(g.data_ptr(), g.shape[0], g.shape[1], int(g.dtype == torch.float16), grad.data_ptr(),
                                ws.data_ptr(), stream)
     if rc != 0:
@@ -228,7 +229,7 @@ def rollout_pre(n: int, obs, dones, values, actions, neglogp, mu, sigma, b_obs, 
     once (rollout_pre_applies); this is the per-step call."""
     N, O = obs.shape
     H, A = b_obs.shape[1], actions.shape[1]
-    stream = torch.cuda.current_stream(obs.device).cuda_stream
+    stream = raw_stream(obs.device)
     rc = lib().rl_rollout_pre(obs.data_ptr(), O, dones.data_ptr(), values.data_ptr(), values.stride(0),
                               actions.data_ptr(), neglogp.data_ptr(), mu.data_ptr(), sigma.data_ptr(), N, A, H, int(n),
                               b_obs.data_ptr(), t_dones.data_ptr(), t_values.data_ptr(), b_actions.data_ptr(),
@@ -284,7 +285,7 @@ def rollout_post(rewards, dones, time_outs, values, reward_shift: float, reward_
     assert (time_outs is None) == (values is None), "value bootstrap needs both time_outs and values"
     if values is not None:
         assert values.dtype == torch.float32 and values.numel() == N and time_outs.numel() == N
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    stream = raw_stream(dev)
     ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
     rc = lib().rl_rollout_post(rewards.data_ptr(), dones.data_ptr(), _FLAG_BYTES[dones.dtype], ptr(time_outs),
                                _FLAG_BYTES[time_outs.dtype] if time_outs is not None else 0, ptr(values),
@@ -319,7 +320,7 @@ class PpoLossFn(torch.autograd.Function):
         loss = torch.empty((), dtype=f32, device=dev)
         stats = torch.empty(4, dtype=f32, device=dev)
         dls = torch.empty(A, dtype=f32, device=dev)
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = raw_stream(dev)
         rc = lib().rl_ppo_loss(mu.data_ptr(), int(mu.dtype == torch.float16), values.data_ptr(),
                                int(values.dtype == torch.float16), logstd.data_ptr(), actions.data_ptr(),
                                old_neglogp.data_ptr(), advantages.data_ptr(), old_values.data_ptr(), returns.data_ptr(),
@@ -343,7 +344,7 @@ class PpoLossFn(torch.autograd.Function):
         dmu_out = torch.empty(B, A, dtype=mu_dt, device=dev)
         dv_out = torch.empty(v_shape, dtype=v_dt, device=dev)
         dls_out = torch.empty(A, dtype=torch.float32, device=dev)
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = raw_stream(dev)
         rc = lib().rl_ppo_loss_backward(g.data_ptr(), dmu.data_ptr(), dv.data_ptr(), dls.data_ptr(), B, A,
                                         dmu_out.data_ptr(), int(mu_dt == torch.float16), dv_out.data_ptr(),
                                         int(v_dt == torch.float16), dls_out.data_ptr(), stream)
@@ -397,7 +398,7 @@ class PpoHeadsLossFn(torch.autograd.Function):
         loss = torch.empty((), dtype=f32, device=dev)
         stats = torch.empty(4, dtype=f32, device=dev)
         dls = torch.empty(A, dtype=f32, device=dev)
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = raw_stream(dev)
         _check(lib().rl_ppo_heads_loss(hidden.data_ptr(), hidden.stride(0), heads.actor_col, heads.critic_col, H,
                                        heads.w_mu.data_ptr(), heads.b_mu.data_ptr(), heads.w_v.data_ptr(),
                                        heads.b_v.data_ptr(), logstd.data_ptr(), actions.data_ptr(),
@@ -426,7 +427,7 @@ class PpoHeadsLossFn(torch.autograd.Function):
                                                 hd.hidden, hd.w_mu.data_ptr(), hd.w_v.data_ptr(), B, A, dh.data_ptr(),
                                                 part.data_ptr(), hd.gw_mu.data_ptr(), hd.gb_mu.data_ptr(),
                                                 hd.gw_v.data_ptr(), hd.gb_v.data_ptr(), hd.g_logstd.data_ptr(),
-                                                int(hd.store), torch.cuda.current_stream(hidden.device).cuda_stream),
+                                                int(hd.store), raw_stream(hidden.device)),
                "rl_ppo_heads_loss_backward")
         return (dh,) + (None,) * 12
 
@@ -446,7 +447,7 @@ def rms_normalize(x, running_mean, running_var, count, epsilon: float, update: b
     N, Cc = x.shape
     y = torch.empty_like(x, dtype=torch.float16 if out_half else torch.float32)
     part = torch.empty(((N + 63) // 64) * Cc * 2, dtype=torch.float32, device=x.device) if update else None
-    stream = torch.cuda.current_stream(x.device).cuda_stream
+    stream = raw_stream(x.device)
     fn = lib().rl_rms_normalize_h if out_half else lib().rl_rms_normalize
     rc = fn(x.data_ptr(), N, Cc, running_mean.data_ptr(), running_var.data_ptr(),
                                 count.data_ptr(), float(epsilon), int(bool(update)),
@@ -471,7 +472,7 @@ def policy_head(mu, noise, logstd, value, value_rms=None):
     if value_rms is not None:
         assert value_rms.running_mean.numel() == 1
         vm, vv, eps = value_rms.running_mean.data_ptr(), value_rms.running_var.data_ptr(), value_rms.epsilon
-    stream = torch.cuda.current_stream(mu.device).cuda_stream
+    stream = raw_stream(mu.device)
     rc = lib().rl_policy_head(mu.data_ptr(), noise.data_ptr(), logstd.data_ptr(), value.data_ptr(), vm, vv, float(eps),
                               N, A, actions.data_ptr(), sigmas.data_ptr(), neglogp.data_ptr(), vout.data_ptr(), stream)
     if rc != 0:
@@ -510,7 +511,7 @@ def act_heads(a_out, c_out, w_mu, b_mu, w_v, b_v, noise, logstd, value_rms=None)
     rc = lib().rl_act_heads(a_out.data_ptr(), a_out.stride(0), c_out.data_ptr(), c_out.stride(0), H, w_mu.data_ptr(),
                             b_mu.data_ptr(), w_v.data_ptr(), b_v.data_ptr(), noise.data_ptr(), logstd.data_ptr(), vm, vv,
                             float(eps), N, A, mu.data_ptr(), actions.data_ptr(), sigmas.data_ptr(), neglogp.data_ptr(),
-                            vout.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+                            vout.data_ptr(), raw_stream(dev))
     if rc != 0:
         raise RuntimeError(f"rl_act_heads failed: {lib().rl_last_error().decode()}")
     return mu, actions, sigmas, neglogp, vout
@@ -523,7 +524,7 @@ def opt_step(param, grad, exp_avg, exp_avg_sq, step, lr, scale, growth_tracker, 
                            param.numel(), step.data_ptr(), lr.data_ptr(),
                            scale.data_ptr() if scale is not None else None,
                            growth_tracker.data_ptr() if growth_tracker is not None else None, C.byref(hyper),
-                           partials.data_ptr(), torch.cuda.current_stream().cuda_stream)
+                           partials.data_ptr(), raw_stream())
     if rc != 0:
         raise RuntimeError(f"rl_opt_step failed: {lib().rl_last_error().decode()}")
 
@@ -539,12 +540,12 @@ def linear_fwd(x, w_half, b_half, act: bool, out):
     N = w_half.shape[0]
     _check(lib().rl_linear_fwd(x.data_ptr(), M, K, x.stride(0), w_half.data_ptr(), N,
                                b_half.data_ptr() if b_half is not None else None, int(act), out.data_ptr(),
-                               torch.cuda.current_stream().cuda_stream), "rl_linear_fwd")
+                               raw_stream()), "rl_linear_fwd")
 
 
 def linear_transpose(w_half, out):
     N, K = w_half.shape
-    _check(lib().rl_linear_transpose(w_half.data_ptr(), N, K, out.data_ptr(), torch.cuda.current_stream().cuda_stream),
+    _check(lib().rl_linear_transpose(w_half.data_ptr(), N, K, out.data_ptr(), raw_stream()),
            "rl_linear_transpose")
 
 
@@ -558,7 +559,7 @@ def linear_bwd(dy, y, x, w, dx, splits: int, wpart, bpart, pstride: int = 0):
                                w.data_ptr() if w is not None else None, dx.data_ptr() if dx is not None else None,
                                splits, wpart.data_ptr() if wpart is not None else None,
                                bpart.data_ptr() if bpart is not None else None, int(pstride),
-                               torch.cuda.current_stream().cuda_stream), "rl_linear_bwd")
+                               raw_stream()), "rl_linear_bwd")
 
 
 def linear_fwd_grouped(x, ldx: int, K: int, w_half, N: int, b_half, act: bool, y, ldy: int, groups: int, x_gstride: int,
@@ -568,7 +569,7 @@ def linear_fwd_grouped(x, ldx: int, K: int, w_half, N: int, b_half, act: bool, y
     g = LinearGroups(groups, ldy, 0, 0, x_gstride, w_gstride, b_gstride, y_gstride, 0, 0, 0)
     _check(lib().rl_linear_fwd_g(x.data_ptr(), M, K, ldx, w_half.data_ptr(), N,
                                  b_half.data_ptr() if b_half is not None else None, int(act), y.data_ptr(), C.byref(g),
-                                 torch.cuda.current_stream().cuda_stream), "rl_linear_fwd_g")
+                                 raw_stream()), "rl_linear_fwd_g")
 
 
 def linear_fwd_f32(x, ldx: int, K: int, w, N: int, b, act: bool, y, ldy: int, M: int, groups: int = 1,
@@ -577,7 +578,7 @@ def linear_fwd_f32(x, ldx: int, K: int, w, N: int, b, act: bool, y, ldy: int, M:
     (tensors are base pointers of group 0; strides in elements, include/gymrl.h)."""
     g = LinearGroups(groups, ldy, 0, 0, x_gstride, w_gstride, b_gstride, y_gstride, 0, 0, 0)
     _check(lib().rl_linear_fwd_f32_g(x.data_ptr(), M, K, ldx, w.data_ptr(), N, b.data_ptr() if b is not None else None,
-                                     int(act), y.data_ptr(), C.byref(g), torch.cuda.current_stream().cuda_stream),
+                                     int(act), y.data_ptr(), C.byref(g), raw_stream()),
            "rl_linear_fwd_f32_g")
 
 
@@ -590,7 +591,7 @@ def linear_bwd_grouped(dy, y, ldy: int, y_gstride: int, M: int, N: int, x, ldx: 
                                  w.data_ptr() if w is not None else None, dx.data_ptr() if dx is not None else None,
                                  splits, wpart.data_ptr() if wpart is not None else None,
                                  bpart.data_ptr() if bpart is not None else None, int(pstride), C.byref(g),
-                                 torch.cuda.current_stream().cuda_stream), "rl_linear_bwd_g")
+                                 raw_stream()), "rl_linear_bwd_g")
 
 
 def policy_kl(mu_new, sigma_row, mu_old, sigma_old, kl_out, partials, write_back: bool = True,
@@ -604,7 +605,7 @@ def policy_kl(mu_new, sigma_row, mu_old, sigma_old, kl_out, partials, write_back
     assert mu_new.is_contiguous() and mu_old.is_contiguous() and sigma_old.is_contiguous()
     assert mu_old.dtype == torch.float32 and sigma_old.dtype == torch.float32 and sigma_row.dtype == torch.float32
     stride = 0 if sigma_row.dim() == 1 else sigma_row.stride(0)
-    stream = torch.cuda.current_stream().cuda_stream
+    stream = raw_stream()
     half = int(mu_new.dtype == torch.float16)
     if lr_step is None:
         _check(lib().rl_policy_kl(mu_new.data_ptr(), half, sigma_row.data_ptr(), stride, int(sigma_is_log),
@@ -626,7 +627,7 @@ def adaptive_lr(kl, inv_world: float, adaptive: bool, kl_threshold: float, lr, o
     ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
     _check(lib().rl_adaptive_lr(kl.data_ptr(), float(inv_world), int(adaptive), float(kl_threshold), ptr(lr),
                                 ptr(opt_lr), ptr(stats), ptr(a_loss), ptr(c_loss), ptr(entropy),
-                                torch.cuda.current_stream().cuda_stream), "rl_adaptive_lr")
+                                raw_stream()), "rl_adaptive_lr")
 
 
 def splitk_accum_multi(jobs, store: bool = False) -> None:
@@ -638,7 +639,7 @@ def splitk_accum_multi(jobs, store: bool = False) -> None:
         assert parts.dtype in (torch.float16, torch.float32) and parts[0].numel() == grad.numel()
         arr[k] = SplitkJob(parts.data_ptr(), grad.data_ptr(), grad.numel(), parts.shape[0],
                            int(parts.dtype == torch.float16))
-    _check(lib().rl_splitk_accum_multi(arr, len(jobs), int(store), torch.cuda.current_stream().cuda_stream),
+    _check(lib().rl_splitk_accum_multi(arr, len(jobs), int(store), raw_stream()),
            "rl_splitk_accum_multi")
 
 
@@ -650,4 +651,4 @@ def opt_step_h(param, param_half, grad, exp_avg, exp_avg_sq, step, lr, scale, gr
                                exp_avg_sq.data_ptr(), param.numel(), step.data_ptr(), lr.data_ptr(),
                                scale.data_ptr() if scale is not None else None,
                                growth_tracker.data_ptr() if growth_tracker is not None else None, C.byref(hyper),
-                               partials.data_ptr(), torch.cuda.current_stream().cuda_stream), "rl_opt_step_h")
+                               partials.data_ptr(), raw_stream()), "rl_opt_step_h")
