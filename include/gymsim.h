@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 7
+#define GS_ABI_VERSION 8
 
 typedef struct gs_sim gs_sim;
 
@@ -242,6 +242,15 @@ int gs_sim_set_dof_drives(gs_sim *sim, const int32_t *mode, const double *stiffn
  * set_dof_velocity_target_tensor, useful_hound.py:622-627), read by every later simulate / pd_step;
  * NULL = zero targets. */
 int gs_sim_bind_dof_targets(gs_sim *sim, const float *pos_targets, const float *vel_targets);
+/* Per-actor dof properties (ABI 8): gym.set_actor_dof_properties called actor by actor with differing values
+ * (anymal_terrain.py:283, useful_hound.py:422 call it per actor; Isaac Gym keeps the properties per actor).
+ * Caller-owned table [6][nd][N] float32 on the sim's device (host memory for the host backend): drive
+ * stiffness (DOF_MODE_POS, else 0), drive damping (DOF_MODE_POS / VEL, else 0), effort (<= 0 unlimited), lower,
+ * upper (lower >= upper: no limit), velocity (<= 0 unlimited) -- read by every later simulate / pd_step in
+ * place of the asset's values (gs_sim_set_model, gs_sim_set_dof_drives).  any_drive / any_limits: some env has
+ * a drive gain / a limit.  NULL unbinds (the asset's values again).  A sim with a table runs the
+ * one-env-per-lane kernel; kernel_variant 2 (lane team forced) fails. */
+int gs_sim_bind_dof_properties_env(gs_sim *sim, const float *table, int any_drive, int any_limits);
 
 /* Self-collision (ABI 5): gym.create_actor with collision filter 0 (anymal_terrain.py:282,
  * useful_hound.py:421) makes Isaac Gym collide an actor's shapes with each other except on links joined

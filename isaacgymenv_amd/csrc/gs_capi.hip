@@ -74,6 +74,9 @@ struct gs_sim {
   launch_pd_fn model_pd_fn = nullptr;
   int model_variant = 0;
   bool team_pairs = false;  // the lane-team kernel solves self-contacts (gs_team.hip)
+  // the asset-wide (uniform) drive / limit flags; a bound per-actor property table overrides them in dp
+  int uni_any_drive = 0, uni_any_limits = 0;
+  int env_any_drive = 0, env_any_limits = 0;
   DevModel* d_model = nullptr;
   DevModel h_model{};             // host copy (sensors are added after set_model)
   DevLinks* d_links = nullptr;    // link kinematics tables (gs_kinematics.hip)
@@ -559,6 +562,7 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   s->h_model = h;
   s->h_links = hl;
   s->dp.any_limits = any_lim;
+  s->uni_any_limits = any_lim;
   s->parent.assign(m->parent, m->parent + m->num_bodies);
   s->sim_fn = sim_fn;
   s->pd_fn = pd_fn;
@@ -776,6 +780,26 @@ int gs_sim_set_force_sensors(gs_sim* s, int n, const int32_t* bodies) {
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_set_force_sensors hipMemcpy");
 }
 
+// The kernel form for the sim's current features: the one gs_sim_set_model selected, or the one-env-per-lane
+// kernel where the lane team lacks a feature in use (joint drives, a per-actor dof property table)
+static int kernel_select(gs_sim* s, const char* who) {
+  launch_sim_fn sim_fn = s->model_sim_fn;
+  launch_pd_fn pd_fn = s->model_pd_fn;
+  int variant = s->model_variant;
+  const bool lane = s->dp.any_drive || s->dp.dof_env || (s->dp.self_collide && !s->team_pairs);
+  if (lane && variant == 2) {
+    if (s->params.kernel_variant == 2)
+      return fail("%s: the lane-team kernel (kernel_variant 2) has no joint drives or per-actor dof properties", who);
+    sim_fn = s->topo->sim;
+    pd_fn = s->topo->pd;
+    variant = 1;
+  }
+  s->sim_fn = sim_fn;
+  s->pd_fn = pd_fn;
+  s->variant = variant;
+  return 0;
+}
+
 int gs_sim_set_dof_drives(gs_sim* s, const int32_t* mode, const double* stiffness, const double* damping) {
   if (!s || !s->topo) return fail("gs_sim_set_dof_drives: model not set");
   if (s->nd > 0 && (!mode || !stiffness || !damping)) return fail("gs_sim_set_dof_drives: null argument");
@@ -792,16 +816,8 @@ int gs_sim_set_dof_drives(gs_sim* s, const int32_t* mode, const double* stiffnes
   }
   // the lane-team kernel has no drive terms: drives run the one-env-per-lane kernel; the kernel
   // gs_sim_set_model selected comes back once every gain is zero again
-  launch_sim_fn sim_fn = s->model_sim_fn;
-  launch_pd_fn pd_fn = s->model_pd_fn;
-  int variant = s->model_variant;
-  if (any && variant == 2) {
-    if (s->params.kernel_variant == 2)
-      return fail("gs_sim_set_dof_drives: the lane-team kernel (kernel_variant 2) has no joint drives");
-    sim_fn = s->topo->sim;
-    pd_fn = s->topo->pd;
-    variant = 1;
-  }
+  if (any && s->model_variant == 2 && s->params.kernel_variant == 2)
+    return fail("gs_sim_set_dof_drives: the lane-team kernel (kernel_variant 2) has no joint drives");
   if (!s->host) {
     // the physics kernels read d_model: the blocking upload must not overtake a launch still queued on
     // a caller's (non-blocking) stream, so the device drains first (cold path: dof property changes)
@@ -811,11 +827,9 @@ int gs_sim_set_dof_drives(gs_sim* s, const int32_t* mode, const double* stiffnes
     if (e != hipSuccess) return hip_fail(e, "gs_sim_set_dof_drives hipMemcpy");
   }
   s->h_model = h;
-  s->dp.any_drive = any;
-  s->sim_fn = sim_fn;
-  s->pd_fn = pd_fn;
-  s->variant = variant;
-  return 0;
+  s->uni_any_drive = any;
+  s->dp.any_drive = s->dp.dof_env ? s->env_any_drive : any;
+  return kernel_select(s, "gs_sim_set_dof_drives");
 }
 
 int gs_sim_set_self_collision(gs_sim* s, int enable) {
@@ -838,6 +852,24 @@ int gs_sim_bind_dof_targets(gs_sim* s, const float* pos_targets, const float* ve
   s->dp.ptgt = pos_targets;
   s->dp.vtgt = vel_targets;
   return 0;
+}
+
+int gs_sim_bind_dof_properties_env(gs_sim* s, const float* table, int any_drive, int any_limits) {
+  if (ready(s, "gs_sim_bind_dof_properties_env")) return -1;
+  if (table) {
+    s->dp.dof_env = table;
+    s->dp.dof_env_n = s->N;
+    s->env_any_drive = any_drive != 0;
+    s->env_any_limits = any_limits != 0;
+    s->dp.any_drive = s->env_any_drive;
+    s->dp.any_limits = s->env_any_limits;
+  } else {
+    s->dp.dof_env = nullptr;
+    s->dp.dof_env_n = 0;
+    s->dp.any_drive = s->uni_any_drive;
+    s->dp.any_limits = s->uni_any_limits;
+  }
+  return kernel_select(s, "gs_sim_bind_dof_properties_env");
 }
 
 int gs_sim_bind_force_sensors(gs_sim* s, float* soa) {

@@ -83,7 +83,13 @@ struct DevParams {
   int self_collide;      // filter-0 actors: self-collision pairs
   const float* ptgt;     // [N][nd] dof position targets or null (= 0)
   const float* vtgt;     // [N][nd] dof velocity targets or null (= 0)
+  // per-actor dof properties (set_actor_dof_properties actor by actor; gs_sim_set_dof_properties_env):
+  // [GS_DOFP_FIELDS][nd][N] -- drive stiffness, drive damping (after the drive-mode rule), effort, lower, upper
+  // (lower >= upper: no limit), velocity limit; null = the model's per-asset values
+  const float* dof_env;
+  int dof_env_n;         // the table's env stride (N)
 };
+#define GS_DOFP_FIELDS 6
 
 // SoA state: field f of env e at state[f*N + e]
 //   0..2 root pos, 3..6 quat xyzw, 7..9 root ORIGIN lin vel, 10..12 ang vel,

@@ -310,6 +310,10 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
 #pragma unroll
   for (int j = 0; j < T::ND; ++j) nu[NB6 + j] = s.qd[j];
 
+  // per-actor dof property f of dof j (GS_DOFP_FIELDS order), else the asset's value mv
+  auto dofp = [&](int f, int j, float mv) -> float {
+    return P.dof_env ? P.dof_env[((size_t)f * ND + j) * P.dof_env_n + e] : mv;
+  };
   // joint drives: the drive force estimate kp (q* - q - h qd) + kd (qd* - qd) of each dof;
   // within the dof's effort limit the drive is implicit ((h kd + h^2 kp) on M's diagonal), a saturated drive
   // applies the clamped force explicitly (PhysX: the drive's max force is the dof's effort property)
@@ -320,8 +324,8 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
     for (int j = 0; j < ND; ++j) {
       const float pt = P.ptgt ? P.ptgt[(size_t)e * ND + j] : 0.f;
       const float vt = P.vtgt ? P.vtgt[(size_t)e * ND + j] : 0.f;
-      const float f = M->dkp[j] * (pt - s.q[j] - h * s.qd[j]) + M->dkd[j] * (vt - s.qd[j]);
-      const float ef = M->effort[j];
+      const float f = dofp(0, j, M->dkp[j]) * (pt - s.q[j] - h * s.qd[j]) + dofp(1, j, M->dkd[j]) * (vt - s.qd[j]);
+      const float ef = dofp(2, j, M->effort[j]);
       dimpl[j] = !(ef > 0.f) || fabsf(f) <= ef;
       dforce[j] = dimpl[j] ? f : clampf(f, -ef, ef);
     }
@@ -598,7 +602,8 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
             float F[6];
             spi_mul(Ic[a], S[a], F);
             Mm[ga][ga] = dot6(S[a], F) + M->armature[T::bdof[a]];
-            if (P.any_drive && dimpl[T::bdof[a]]) Mm[ga][ga] += h * (M->dkd[T::bdof[a]] + h * M->dkp[T::bdof[a]]);
+            if (P.any_drive && dimpl[T::bdof[a]])
+              Mm[ga][ga] += h * (dofp(1, T::bdof[a], M->dkd[T::bdof[a]]) + h * dofp(0, T::bdof[a], M->dkp[T::bdof[a]]));
 #pragma unroll
             for (int k = 0; k < T::MAXDEP; ++k) {
               if (k < T::depth[ga]) {
@@ -639,8 +644,9 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
   for (int j = 0; j < ND; ++j) {
     lsgn[j] = 0.f;
     lsep[j] = 0.f;
-    if (P.any_limits && M->has_lim[j]) {
-      const float lo = s.q[j] - M->lower[j], hi = M->upper[j] - s.q[j];
+    const float lwr = dofp(3, j, M->lower[j]), upr = dofp(4, j, M->upper[j]);
+    if (P.any_limits && (P.dof_env ? lwr < upr : M->has_lim[j] != 0)) {
+      const float lo = s.q[j] - lwr, hi = upr - s.q[j];
       if (lo < P.limit_margin || hi < P.limit_margin) {
         lsgn[j] = lo <= hi ? 1.f : -1.f;
         lsep[j] = lo <= hi ? lo : hi;
@@ -684,7 +690,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
 #pragma unroll
     for (int j = 0; j < T::ND; ++j) {
       float t = tau[j];
-      const float ef = M->effort[j];
+      const float ef = dofp(2, j, M->effort[j]);
       if (ef > 0.f) t = clampf(t, -ef, ef);
       r[NB6 + j] = t - bias[NB6 + j];
       if (P.any_drive) r[NB6 + j] += dforce[j];
@@ -997,7 +1003,7 @@ GS_HD void substep(const DevModel* __restrict__ Min, const DevParams& P, EnvStat
   // ---------------- joint velocity limits
 #pragma unroll
   for (int j = 0; j < T::ND; ++j) {
-    const float vm = M->vmax[j];
+    const float vm = dofp(5, j, M->vmax[j]);
     if (vm > 0.f) {
       nun[NB6 + j] = clampf(nun[NB6 + j], -vm, vm);
       nupos[NB6 + j] = clampf(nupos[NB6 + j], -vm, vm);

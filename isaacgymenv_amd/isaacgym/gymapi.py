@@ -450,36 +450,76 @@ class Sim:
         for kind in ("rigid_body", "jacobian", "mass_matrix"):  # acquired before prepare_sim
             self.refresh(kind)
 
+    def _effective_dof_props(self, p):
+        """(kp, kd, effort, lower, upper, velocity) float64 [nd] of one actor's dof properties as the solver reads
+        them: stiffness only where driveMode is POS, damping where it is POS or VEL (EFFORT / NONE dofs ignore
+        both, as gs_sim_set_dof_drives does); a dof without limits has lower = upper = 0."""
+        mode = p["driveMode"].astype(np.int32)
+        pos, vel = mode == int(DOF_MODE_POS), mode == int(DOF_MODE_VEL)
+        lim = p["hasLimits"].astype(bool) & (p["upper"].astype(np.float64) > p["lower"].astype(np.float64))
+        return (np.where(pos, p["stiffness"].astype(np.float64), 0.0),
+                np.where(pos | vel, p["damping"].astype(np.float64), 0.0),
+                p["effort"].astype(np.float64),
+                np.where(lim, p["lower"].astype(np.float64), 0.0),
+                np.where(lim, p["upper"].astype(np.float64), 0.0),
+                p["velocity"].astype(np.float64))
+
+    def _asset_dof_props(self):
+        """The asset's values the model was built with (gs_sim_set_model), in _effective_dof_props' layout."""
+        flat = self.asset.flat
+        nd = int(flat["nd"])
+        lim = np.asarray(flat["has_limits"], dtype=bool)[:nd] & (np.asarray(flat["upper"])[:nd] > np.asarray(flat["lower"])[:nd])
+        return (np.asarray(flat["effort"], dtype=np.float64)[:nd],
+                np.where(lim, np.asarray(flat["lower"], dtype=np.float64)[:nd], 0.0),
+                np.where(lim, np.asarray(flat["upper"], dtype=np.float64)[:nd], 0.0),
+                np.asarray(flat["vmax"], dtype=np.float64)[:nd])
+
     def drive_tables(self):
-        """(mode int32 [nd], stiffness [nd], damping [nd]) of the actors' dof properties.  Isaac Gym keeps
-        drive gains per actor; this simulator holds one set per sim (the in-scope tasks give every actor
-        the same properties), so actors whose EFFECTIVE drive gains differ are refused: stiffness counts
-        only where driveMode is POS, damping where it is POS or VEL (EFFORT / NONE dofs ignore both, as
-        gs_sim_set_dof_drives does)."""
-        first = None
-        for e in self.envs:
-            for a in e.actors:
-                p = a.dof_props
-                mode = p["driveMode"].astype(np.int32)
-                pos, vel = mode == int(DOF_MODE_POS), mode == int(DOF_MODE_VEL)
-                t = (mode, p["stiffness"].astype(np.float64), p["damping"].astype(np.float64))
-                eff = (np.where(pos, t[1], 0.0), np.where(pos | vel, t[2], 0.0))
-                if first is None:
-                    first, first_eff = t, eff
-                elif not all(np.array_equal(x, y) for x, y in zip(first_eff, eff)):
-                    raise NotImplementedError("joint drives: actors with different driveMode / stiffness / damping "
-                                              "(one drive setting per sim, DESIGN.md section 6)")
-        return first
+        """(mode int32 [nd], stiffness [nd], damping [nd]) of the first actor's dof properties: the asset-wide
+        drive setting (gs_sim_set_dof_drives).  Actors whose properties differ get the per-actor table on top
+        (dof_property_table)."""
+        p = self.envs[0].actors[0].dof_props
+        return (p["driveMode"].astype(np.int32), p["stiffness"].astype(np.float64), p["damping"].astype(np.float64))
+
+    def dof_property_table(self):
+        """[GS_DOFP_FIELDS = 6][nd][N] float32 of the actors' properties (gymsim.h gs_sim_bind_dof_properties_env),
+        or None when every actor's effective drive gains equal the first actor's and its effort, limits and
+        velocity limit the asset's (the uniform path: the asset model + gs_sim_set_dof_drives).  Isaac Gym keeps
+        dof properties per actor (set_actor_dof_properties, anymal_terrain.py:283, useful_hound.py:422)."""
+        props = [self._effective_dof_props(e.actors[0].dof_props) for e in self.envs]
+        asset = self._asset_dof_props()
+        first = props[0]
+        uniform = all(all(np.array_equal(x, y) for x, y in zip(first[:2], q[:2])) for q in props[1:]) and \
+            all(np.array_equal(np.float32(x), np.float32(y)) for q in props for x, y in zip(q[2:], asset))
+        if uniform:
+            return None
+        tab = np.stack([np.stack(q, axis=0) for q in props], axis=-1).astype(np.float32)  # [6][nd][N]
+        return np.ascontiguousarray(tab)
 
     def apply_drives(self):
-        """Upload the drive gains (gs_sim_set_dof_drives); called at prepare_sim and whenever dof
-        properties change afterwards (set_actor_dof_properties)."""
+        """Upload the drive gains (gs_sim_set_dof_drives) and, where actors differ, the per-actor property table
+        (gs_sim_bind_dof_properties_env); called at prepare_sim and whenever dof properties change afterwards
+        (set_actor_dof_properties)."""
+        import torch
         self.drives_dirty = False
         mode, kp, kd = self.drive_tables()
         mode, kp, kd = (np.ascontiguousarray(x) for x in (mode, kp, kd))
-        _lib.check(_lib.lib().gs_sim_set_dof_drives(self.handle, mode.ctypes.data, kp.ctypes.data, kd.ctypes.data),
+        L = _lib.lib()
+        _lib.check(L.gs_sim_set_dof_drives(self.handle, mode.ctypes.data, kp.ctypes.data, kd.ctypes.data),
                    "gs_sim_set_dof_drives")
-        self.kernel_variant = _lib.lib().gs_sim_kernel_variant(self.handle)
+        tab = self.dof_property_table()
+        if tab is None:
+            self.dof_env_table = None
+            _lib.check(L.gs_sim_bind_dof_properties_env(self.handle, None, 0, 0), "gs_sim_bind_dof_properties_env")
+        else:
+            any_drive = int(bool(np.any(tab[0] > 0) or np.any(tab[1] > 0)))
+            any_limits = int(bool(np.any(tab[3] < tab[4])))
+            if not self.host:
+                torch.cuda.synchronize(self.sim_device)  # (a launch still queued may read the previous table)
+            self.dof_env_table = torch.from_numpy(tab).to(self.sim_device)
+            _lib.check(L.gs_sim_bind_dof_properties_env(self.handle, self.dof_env_table.data_ptr(), any_drive,
+                                                        any_limits), "gs_sim_bind_dof_properties_env")
+        self.kernel_variant = L.gs_sim_kernel_variant(self.handle)
 
     def set_targets(self, kind: str, src, idx=None, n: int = 0):
         """Copy (or scatter, for the listed actor indices) a [N*nd] target tensor into the bound buffer."""

@@ -29,7 +29,7 @@ class OModel(C.Structure):
                                   "hverts", "shv0", "shv1")] + [
         ("npair", C.c_int32), ("pair_a", C.c_void_p), ("pair_b", C.c_void_p), ("pair_kind", C.c_void_p),
         ("npool", C.c_int32), ("self_collide", C.c_int32), ("pverts", C.c_void_p), ("shp0", C.c_void_p),
-        ("shp1", C.c_void_p)]
+        ("shp1", C.c_void_p), ("pool_policy", C.c_int32)]
 
 
 class OParams(C.Structure):
@@ -77,12 +77,13 @@ class OracleSim:
     """Holds the model arrays alive and steps numpy state in place."""
 
     def __init__(self, flat: dict, params: dict, real_bits: int = 64, sensor_bodies=(), terrain=None, drives=None,
-                 self_collide=None):
+                 self_collide=None, pool_policy: int = 0):
         """terrain: optional dict(vertices float32 [rows*cols, 3] world coordinates, rows, cols, x0, y0,
         hs, friction) -- the heightfield-grid mesh of gym.add_triangle_mesh.
         drives: optional (kp [nd], kd [nd]) joint-drive gains.
         self_collide: the actor's collision filter is 0 (self-collision pairs); None follows
-        flat["self_collide"] (absent: off)."""
+        flat["self_collide"] (absent: off).
+        pool_policy: 0 the product's self-contact rules; see OModel.pool_policy."""
         self.flat = flat
         self.real = np.float64 if real_bits == 64 else np.float32
         self.lib = _lib(real_bits)
@@ -110,6 +111,9 @@ class OracleSim:
         m.npair = int(flat["npair"])
         m.npool = int(flat["npool"])
         m.self_collide = int(bool(flat.get("self_collide", 0) if self_collide is None else self_collide))
+        # DESIGN.md 3.12's self-contact departures as switches (tools/pool_policy_study.py): bit 0 overlapping cores
+        # make a contact, bit 1 no MIN_RESPONSE bound; 0 = the product's rules
+        m.pool_policy = int(pool_policy)
         sb = np.ascontiguousarray(list(sensor_bodies) or [0], dtype=np.int32)
         keep["sens_body"] = sb
         m.nsens = len(sensor_bodies)

@@ -103,6 +103,10 @@ typedef struct {
     int32_t self_collide;       /* filter-0 actor: self-collision pairs enabled */
     const double *pverts;       /* [npv][4] a hull's self-collision core vertices (subset of hverts) */
     const int32_t *shp0, *shp1; /* [ns] their range */
+    /* the self-contact departures of DESIGN.md 3.12 as switches, for tools/pool_policy_study.py (0 = the
+     * product's rules): bit 0 overlapping cores make a contact (centres' direction, depth = both margins)
+     * instead of none; bit 1 every self-contact row responds (no MIN_RESPONSE bound).  The pool cap is npool. */
+    int32_t pool_policy;
 } OModel;
 
 typedef struct {
@@ -775,7 +779,11 @@ static int self_contacts(const OModel *m, const OParams *p, real R[][9], real P[
             } else {
                 for (int k = 0; k < 3; ++k) nn[k] /= dist;
             }
-            if (deep) { ++g_pair_stats[5]; continue; } /* overlapping cores: no contact */
+            if (deep) {
+                ++g_pair_stats[5];
+                if (!(m->pool_policy & 1)) continue; /* overlapping cores: no contact */
+                dist = 0;
+            }
             const real sep = dist - ra - rb;
             if (!(sep < off)) continue;
             PairContact *o = &out[n++];
@@ -1119,6 +1127,7 @@ static void env_substep(const OModel *m, const OParams *p, real h,
     PairContact pc[MAXPOOL];
     int npc = 0;
     real PJ[3 * MAXPOOL * MAXV], PW[3 * MAXPOOL * MAXV], PD[3 * MAXPOOL];
+    const real min_resp = (m->pool_policy & 2) ? (real)0 : (real)MIN_RESPONSE; /* (pool_policy bit 1: study) */
     if (m->self_collide && m->npair > 0 && m->npool > 0) {
         npc = self_contacts(m, p, R, P, mu_shape, pc);
         for (int a = 0; a < npc; ++a) {
@@ -1234,11 +1243,11 @@ static void env_substep(const OModel *m, const OParams *p, real h,
                     if (s >= 0) target = -s / hd;
                     else if (pos_phase) { target = -s / hpush; if (target > (real)p->max_depen_vel) target = (real)p->max_depen_vel; }
                     else target = 0;
-                    ln = PD[r] > MIN_RESPONSE ? plam[r] + (target - u) / PD[r] : plam[r];
+                    ln = PD[r] > min_resp ? plam[r] + (target - u) / PD[r] : plam[r];
                     if (ln < 0) ln = 0;
                 } else {
                     const real lim = pc[a].mu * plam[3 * a];
-                    ln = PD[r] > MIN_RESPONSE ? plam[r] - u / PD[r] : plam[r];
+                    ln = PD[r] > min_resp ? plam[r] - u / PD[r] : plam[r];
                     if (ln > lim) ln = lim;
                     if (ln < -lim) ln = -lim;
                 }

@@ -11,7 +11,8 @@ closed and absent).
 
 CPU tests (host backend, no GPU): host vs oracle with random targets (Cartpole, fixed base; Hound,
 floating base with ground contacts), a drive holds a pendulum at its target, indexed targets
-scatter by actor, drive settings that differ between actors are refused.
+scatter by actor, per-actor dof properties (drive gains, efforts, velocity and joint limits) against the
+oracle run env by env.
 GPU tests: the one-env-per-lane kernel vs the oracle, and a drive on ANYmal moves the sim off the
 lane-team kernel.
 """
@@ -167,13 +168,140 @@ def test_indexed_targets_scatter_by_actor():
     assert torch.equal(got, want)
 
 
-def test_different_drive_gains_per_actor_are_refused():
-    gym, sim = H.make_host_sim("cartpole", 2, H.CARTPOLE_PARAMS, drives=CARTPOLE_DRIVES)
-    props = gym.get_actor_dof_properties(sim.envs[1], 0)
-    props["stiffness"][0] = 123.0
-    gym.set_actor_dof_properties(sim.envs[1], 0, props)
-    with pytest.raises(NotImplementedError):
+def _random_actor_props(gym, sim, rng, modes=(DOF_MODE_POS, DOF_MODE_VEL, DOF_MODE_EFFORT), limit_p=0.5,
+                        effort=(20.0, 400.0), kp=(50.0, 600.0), kd=(1.0, 30.0), vel=(2.0, 30.0), lim=(0.05, 0.6)):
+    """Every actor its own dof properties (set_actor_dof_properties actor by actor, as anymal_terrain.py:283 /
+    useful_hound.py:422 call it): random drive modes, gains, efforts, velocity limits and joint limits.  Returns
+    the per-env effective values (kp, kd, effort, lower, upper, has_limits, velocity) [N][nd]."""
+    out = {k: [] for k in ("kp", "kd", "effort", "lower", "upper", "has", "vel")}
+    for e in sim.envs:
+        p = gym.get_actor_dof_properties(e, 0)
+        nd = len(p)
+        mode = rng.choice(modes, nd).astype(np.int32)
+        p["driveMode"] = mode
+        p["stiffness"] = rng.uniform(*kp, nd)
+        p["damping"] = rng.uniform(*kd, nd)
+        p["effort"] = rng.uniform(*effort, nd)
+        p["velocity"] = rng.uniform(*vel, nd)
+        has = rng.rand(nd) < limit_p
+        p["hasLimits"] = has
+        p["lower"] = np.where(has, -rng.uniform(*lim, nd), -3.4028235e38)
+        p["upper"] = np.where(has, rng.uniform(*lim, nd), 3.4028235e38)
+        gym.set_actor_dof_properties(e, 0, p)
+        pos, vel_m = mode == DOF_MODE_POS, mode == DOF_MODE_VEL
+        out["kp"].append(np.where(pos, p["stiffness"], 0.0).astype(np.float32).astype(np.float64))
+        out["kd"].append(np.where(pos | vel_m, p["damping"], 0.0).astype(np.float32).astype(np.float64))
+        for k, f in (("effort", "effort"), ("lower", "lower"), ("upper", "upper"), ("vel", "velocity")):
+            out[k].append(p[f].astype(np.float32).astype(np.float64))
+        out["has"].append(has.astype(np.int32))
+    return {k: np.stack(v) for k, v in out.items()}
+
+
+def _oracle_per_env(flat, params, props, root, dof, tau, mu, ptgt, vtgt, steps=1, bits=64, idx=None):
+    """The oracle run env by env, each with its actor's dof properties in the model (effort, velocity limit,
+    joint limits) and drive gains."""
+    idx = np.arange(root.shape[0]) if idx is None else idx
+    rs, ds = [], []
+    for k, e in enumerate(idx):
+        fe = dict(flat)
+        fe["effort"] = props["effort"][e].copy()
+        fe["vmax"] = props["vel"][e].copy()
+        fe["has_limits"] = props["has"][e].copy()
+        fe["lower"] = np.where(props["has"][e] > 0, props["lower"][e], 0.0)
+        fe["upper"] = np.where(props["has"][e] > 0, props["upper"][e], 0.0)
+        r, d, _, _ = H.oracle_run(fe, params, root[k:k + 1], dof[k:k + 1], tau[k:k + 1], mu[k:k + 1], bits, steps,
+                                  drives=(props["kp"][e], props["kd"][e]), pos_targets=ptgt[k:k + 1],
+                                  vel_targets=vtgt[k:k + 1])
+        rs.append(r)
+        ds.append(d)
+    return np.concatenate(rs), np.concatenate(ds)
+
+
+def _per_actor_cartpole(host):
+    n, steps = 48, 10
+    art, flat = H.cartpole()
+    root, dof, tau, mu, ptgt, vtgt = _cartpole_case(n, seed=21)
+    gym, sim = H.make_gpu_sim("cartpole", n, H.CARTPOLE_PARAMS, host=host)
+    props = _random_actor_props(gym, sim, np.random.RandomState(5))
+    gym2, sim, (g_root, g_dof) = _run_sim_on(gym, sim, root, dof, tau, mu, ptgt, vtgt, steps, host)
+    assert sim.dof_env_table is not None and (host or sim.kernel_variant == 1)
+    o_root, o_dof = _oracle_per_env(flat, H.CARTPOLE_PARAMS, props, root, dof, tau, mu, ptgt, vtgt, steps)
+    np.testing.assert_allclose(g_dof, o_dof, atol=2e-4, rtol=1e-3)
+    # the per-actor values are in effect: the first actor's values for every env end elsewhere
+    same = {k: np.repeat(v[:1], n, axis=0) for k, v in props.items()}
+    f_root, f_dof = _oracle_per_env(flat, H.CARTPOLE_PARAMS, same, root, dof, tau, mu, ptgt, vtgt, steps)
+    assert np.abs(f_dof - o_dof).max() > 1e-2
+
+
+def _run_sim_on(gym, sim, root, dof, tau, mu, ptgt, vtgt, steps, host):
+    H.load_state_into(sim, root, dof, mu)
+    dev = sim.state.device
+    sim.dof_force.copy_(torch.from_numpy(tau.astype(np.float32).reshape(-1)).to(dev))
+    from isaacgymenv_amd.isaacgym import gymtorch
+    gym.set_dof_position_target_tensor(sim, gymtorch.unwrap_tensor(torch.from_numpy(ptgt.astype(np.float32)).to(dev)))
+    gym.set_dof_velocity_target_tensor(sim, gymtorch.unwrap_tensor(torch.from_numpy(vtgt.astype(np.float32)).to(dev)))
+    for _ in range(steps):
         gym.simulate(sim)
+    if not host:
+        torch.cuda.synchronize()
+    return gym, sim, H.read_state(sim, dof.shape[1])
+
+
+def _per_actor_anymal(host):
+    """Floating base with ground contacts: ANYmal, every actor its own drive gains, efforts, velocity and joint
+    limits (the one-env-per-lane kernel / the host backend) against the oracle env by env."""
+    n = 64
+    art, flat = H.anymal()
+    root, dof, tau, mu = H.anymal_states(n, seed=12)
+    rng = np.random.RandomState(8)
+    gym, sim = H.make_gpu_sim("anymal", n, H.ANYMAL_PARAMS, host=host)
+    props = _random_actor_props(gym, sim, rng, effort=(30.0, 120.0), kp=(20.0, 200.0), kd=(0.5, 6.0))
+    ptgt = dof[:, :, 0] + rng.uniform(-0.3, 0.3, (n, 12))
+    vtgt = rng.uniform(-1.0, 1.0, (n, 12))
+    gym, sim, (g_root, g_dof) = _run_sim_on(gym, sim, root, dof, tau, mu, ptgt, vtgt, 1, host)
+    assert host or sim.kernel_variant == 1
+    o_root, o_dof = _oracle_per_env(flat, H.ANYMAL_PARAMS, props, root, dof, tau, mu, ptgt, vtgt)
+
+    def rerun(idx, rng_, bits):
+        r, d = H.perturbed(root, dof, idx, rng_)
+        return H.state_fields(*_oracle_per_env(flat, H.ANYMAL_PARAMS, props, r, d, tau[idx], mu[idx], ptgt[idx],
+                                               vtgt[idx], 1, bits, idx=idx))
+    H.assert_close_or_explained(H.state_fields(g_root, g_dof), H.state_fields(o_root, o_dof), rerun,
+                                max_env_frac=0.05, what=f"anymal per-actor dof properties {'host' if host else 'gpu'} "
+                                                        f"vs oracle")
+
+
+def test_per_actor_dof_properties_host_match_oracle():
+    """actors with differing drive gains, efforts and limits are no longer refused; the host
+    backend reads them from the per-actor table (gymsim.h gs_sim_bind_dof_properties_env) and matches the oracle
+    run env by env with each actor's values."""
+    _per_actor_cartpole(host=True)
+
+
+def test_per_actor_dof_properties_anymal_host_match_oracle():
+    _per_actor_anymal(host=True)
+
+
+@pytest.mark.gpu
+def test_per_actor_dof_properties_gpu_match_oracle():
+    _per_actor_cartpole(host=False)
+
+
+@pytest.mark.gpu
+def test_per_actor_dof_properties_anymal_gpu_match_oracle():
+    _per_actor_anymal(host=False)
+
+
+def test_uniform_dof_properties_keep_the_asset_path():
+    """Actors with the same properties as the asset bind no table (the lane-team kernel stays selectable)."""
+    gym, sim = H.make_host_sim("cartpole", 3, H.CARTPOLE_PARAMS, drives=CARTPOLE_DRIVES)
+    gym.simulate(sim)
+    assert sim.dof_env_table is None
+    props = gym.get_actor_dof_properties(sim.envs[2], 0)
+    props["effort"][1] = 7.0
+    gym.set_actor_dof_properties(sim.envs[2], 0, props)
+    gym.simulate(sim)
+    assert sim.dof_env_table is not None and float(sim.dof_env_table[2, 1, 2]) == 7.0
 
 
 def test_gains_of_undriven_dofs_may_differ_between_actors():
