@@ -120,7 +120,7 @@ typedef struct gs_sim_params {
     double bounce_threshold_velocity;   /* accepted, restitution is 0 in every in-scope task */
     double max_depenetration_velocity;
     int32_t contact_collection;         /* 0 never, 1 last substep (2 treated as 1)        */
-    int32_t kernel_variant;             /* 0 auto, 1 one env per lane, 2 lane team (4 lanes/env) */
+    int32_t kernel_variant;             /* 0 auto, 1 one env per lane, 2 lane team (4 lanes/env), 4 runtime-sized (ABI 8) */
     double joint_limit_margin;          /* a limit row is active within this distance of the limit */
     int32_t num_threads;                /* ABI 3, host backend: physx.num_threads (cfg/config.yaml:30)
                                            solver threads including the caller; <= 1 = caller only */
@@ -257,8 +257,11 @@ int gs_sim_bind_dof_properties_env(gs_sim *sim, const float *table, int any_driv
  * by a joint.  enable = 1 turns the model's pairs on (every actor of the sim must agree). */
 int gs_sim_set_self_collision(gs_sim *sim, int enable);
 
-/* Physics kernel selected by gs_sim_set_model: 1 one env per lane, 2 lane team, 3 host backend;
- * -1 on error. */
+/* Physics kernel selected by gs_sim_set_model: 1 one env per lane, 2 lane team, 3 host backend, 4 the
+ * runtime-sized kernel (ABI 8: a topology with no compiled kernel -- any tree of revolute / prismatic joints with
+ * plane contacts of sphere / capsule / cylinder / box candidates, joint limits, drives, per-actor dof properties;
+ * one wave per env, dense joint-space rows; hull candidates, self-collision, terrain meshes and force sensors
+ * need a compiled topology and are refused); -1 on error. */
 int gs_sim_kernel_variant(gs_sim *sim);
 
 /* Kernel time of the last gs_sim_pd_step / gs_sim_simulate launch measured with

@@ -19,7 +19,7 @@ ARCH = os.environ.get("GS_OFFLOAD_ARCH", "gfx950")
 
 LIBS = {
     "libgymsim.so": ["gs_physics.hip", "gs_phys_inst.hip", "gs_team.hip", "gs_kinematics.hip", "gs_host.hip",
-                     "gs_capi.hip"],
+                     "gs_generic.hip", "gs_capi.hip"],
     "libgymtask.so": ["gt_anymal.hip", "gt_hound.hip", "gt_ant.hip"],
     "libgymrl.so": ["rl_gae.hip", "rl_grad.hip", "rl_rollout.hip", "rl_ppo_loss.hip", "rl_rms.hip", "rl_adam.hip", "rl_linear.hip",
                    "rl_policy.hip"],

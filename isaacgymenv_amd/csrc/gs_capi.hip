@@ -76,6 +76,10 @@ struct gs_sim {
   bool team_pairs = false;  // the lane-team kernel solves self-contacts (gs_team.hip)
   // the asset-wide (uniform) drive / limit flags; a bound per-actor property table overrides them in dp
   int uni_any_drive = 0, uni_any_limits = 0;
+  // the runtime-sized kernel (gs_generic.hip, kernel_variant 4): the topology entry it stands in for and its
+  // candidate tables on the device
+  TopoEntry gen_entry{};
+  GenTopo* d_gen = nullptr;
   int env_any_drive = 0, env_any_limits = 0;
   DevModel* d_model = nullptr;
   DevModel h_model{};             // host copy (sensors are added after set_model)
@@ -176,6 +180,7 @@ void gs_sim_destroy(gs_sim* s) {
   if (s->d_tblk) (void)hipFree(s->d_tblk);
   if (s->d_tsq4) (void)hipFree(s->d_tsq4);
   if (s->d_rows) (void)hipFree(s->d_rows);
+  if (s->d_gen) (void)hipFree(s->d_gen);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   delete s;
@@ -367,23 +372,43 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   for (int c = 0; c < m->num_candidates; ++c)
     if (m->cand_link[c] < 0 || m->cand_link[c] >= m->num_links) return fail("gs_sim_set_model: cand_link out of range");
   const TopoEntry* t = find_topology(m);
-  if (!t)
-    return fail("gs_sim_set_model: no compiled kernel for topology %s (add it to tools/gen_topologies.py)",
-                signature(m).c_str());
-  if (m->num_pairs > 0 && m->pair_pool != t->npk)
+  // A topology with no compiled kernel runs the runtime-sized kernel (gs_generic.hip, kernel_variant 4) on the GPU:
+  // any tree of revolute / prismatic joints with plane contacts of point candidates (spheres, capsule / cylinder
+  // ends, box corners), joint limits and drives.  Hull candidates, self-collision, terrain meshes and force
+  // sensors need a compiled topology (tools/gen_topologies.py) and are refused where they are set up.
+  // (kernel_variant 4 asks for it on a compiled topology too: the cross-check of the two solver forms)
+  const bool generic = !t || (s->params.kernel_variant == 4 && !s->host);
+  if (generic) {
+    if (s->host)
+      return fail("gs_sim_set_model: the runtime-sized kernel is a GPU kernel and no host solver is compiled for "
+                  "this topology (add it with tools/gen_topologies.py): %s", signature(m).c_str());
+    if (s->params.kernel_variant == 1 || s->params.kernel_variant == 2)
+      return fail("gs_sim_set_model: kernel_variant 1 / 2 requested but topology %s is not compiled (the runtime-"
+                  "sized kernel is variant 4)", signature(m).c_str());
+    for (int c = 0; c < m->num_candidates; ++c)
+      if (m->cand_dyn && m->cand_dyn[c] >= 0)
+        return fail("gs_sim_set_model: topology %s has convex-hull candidates: the runtime-sized kernel has no hull "
+                    "ground manifold (compile the topology with tools/gen_topologies.py)", signature(m).c_str());
+    if (s->dp.has_terrain)
+      return fail("gs_sim_set_model: topology %s with a terrain mesh: the runtime-sized kernel has plane contacts only "
+                  "(compile the topology with tools/gen_topologies.py)", signature(m).c_str());
+    if (m->num_dofs + 6 > GS_MAXD + 6 || (m->num_candidates > 0 && !m->cand_shape))
+      return fail("gs_sim_set_model: runtime-sized kernel tables missing for %s", signature(m).c_str());
+  }
+  if (!generic && m->num_pairs > 0 && m->pair_pool != t->npk)
     return fail("gs_sim_set_model: self-contact pool differs from the compiled topology's %s",
                 std::to_string(t->npk).c_str());
-  for (int c = 0; c < m->num_candidates; ++c)
+  for (int c = 0; c < m->num_candidates && !generic; ++c)
     if (m->cand_dyn && m->cand_dyn[c] != t->cdyn[c])
       return fail("gs_sim_set_model: hull slots differ from the compiled topology (tools/gen_topologies.py)");
   // the kernels unroll the self-collision pairs and shape kinds at compile time
-  if (m->num_pairs > 0 && m->num_pairs != t->npair)
+  if (!generic && m->num_pairs > 0 && m->num_pairs != t->npair)
     return fail("gs_sim_set_model: self-collision pair count differs from the compiled topology's %s",
                 std::to_string(t->npair).c_str());
-  for (int q = 0; q < m->num_pairs; ++q)
+  for (int q = 0; q < m->num_pairs && !generic; ++q)
     if (m->pair_a[q] != t->pair_a[q] || m->pair_b[q] != t->pair_b[q] || m->pair_kind[q] != t->pair_k[q])
       return fail("gs_sim_set_model: self-collision pairs differ from the compiled topology (tools/gen_topologies.py)");
-  for (int sh = 0; sh < m->num_shapes; ++sh)
+  for (int sh = 0; sh < m->num_shapes && !generic; ++sh)
     if (m->shape_kind && m->shape_kind[sh] != t->shkind[sh])
       return fail("gs_sim_set_model: shape kinds differ from the compiled topology (tools/gen_topologies.py)");
   // Everything is built into locals first and committed at the end, so a failure leaves the sim as
@@ -521,6 +546,32 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   launch_pd_fn pd_fn = nullptr;
   const HostTopoEntry* htopo = nullptr;
   int variant = 0;
+  GenTopo hg;
+  std::memset(&hg, 0, sizeof(hg));
+  if (generic) {
+    hg.nc = m->num_candidates;
+    for (int c = 0; c < m->num_candidates; ++c) {
+      hg.cbody[c] = m->cand_body[c];
+      hg.cshape[c] = m->cand_shape[c];
+      hg.clink[c] = m->cand_link[c];
+      if (hg.cbody[c] < 0 || hg.cbody[c] >= m->num_bodies || hg.cshape[c] < 0 || hg.cshape[c] >= m->num_shapes)
+        return fail("gs_sim_set_model: candidate %s tables out of range", std::to_string(c).c_str());
+    }
+    TopoEntry& g = s->gen_entry;
+    g = TopoEntry{};
+    g.sig = "runtime";
+    g.name = "runtime-sized (gs_generic.hip)";
+    g.sim = launch_sim_generic;
+    g.pd = launch_pd_generic;
+    g.dbg_pool = nullptr;
+    g.nb = m->num_bodies; g.nd = m->num_dofs; g.nc = m->num_candidates; g.ns = m->num_shapes;
+    g.sens = 0;
+    g.row_floats = (int)generic_ws_floats(m->num_candidates, m->num_dofs, m->fixed_base);
+    g.row_lanes = 1;
+    g.npk = 0;
+    g.npair = 0;
+    t = &g;
+  }
   if (s->host) {
     for (int i = 0; i < g_num_host_topologies; ++i)
       if (std::strcmp(g_host_topologies[i].sig, t->sig) == 0) htopo = &g_host_topologies[i];
@@ -536,7 +587,11 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
     if (te && any_lim) te = nullptr;
     if (want == 2 && !te)
       return fail("gs_sim_set_model: no lane-team kernel for this topology / joint limits");
-    if (te && want != 1) {
+    if (generic) {
+      sim_fn = launch_sim_generic;
+      pd_fn = launch_pd_generic;
+      variant = 4;
+    } else if (te && want != 1) {
       sim_fn = te->sim;
       pd_fn = te->pd;
       variant = 2;
@@ -556,6 +611,8 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
     s->d_links = dl;
     if (e == hipSuccess) e = hipMemcpy(dm, &h, sizeof(DevModel), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(dl, &hl, sizeof(DevLinks), hipMemcpyHostToDevice);
+    if (e == hipSuccess && generic && !s->d_gen) e = hipMalloc(&s->d_gen, sizeof(GenTopo));
+    if (e == hipSuccess && generic) e = hipMemcpy(s->d_gen, &hg, sizeof(GenTopo), hipMemcpyHostToDevice);
     if (e != hipSuccess) return hip_fail(e, "gs_sim_set_model upload");
   }
   // commit
@@ -579,6 +636,10 @@ int gs_sim_set_model(gs_sim* s, const gs_model_desc* m) {
   s->nc = m->num_candidates;
   s->ns = m->num_shapes;
   s->topo = t;
+  s->dp.gen = generic ? s->d_gen : nullptr;
+  s->dp.gen_links = generic ? s->d_links : nullptr;
+  s->dp.gen_nd = m->num_dofs;
+  s->dp.gen_nr = m->num_links;
   return 0;
 }
 
@@ -596,7 +657,9 @@ static SimBuffers buffers(gs_sim* s) { return SimBuffers{s->state, s->mu, s->cf,
 
 // floats of contact-row tiles the selected GPU kernel needs for N envs (0: its rows live in LDS)
 static size_t rows_needed(const gs_sim* s) {
-  if (s->host || !s->topo || s->variant != 1 || s->dp.has_terrain || s->topo->row_floats <= 0 || s->N <= 0) return 0;
+  if (s->host || !s->topo || (s->variant != 1 && s->variant != 4) || (s->variant == 1 && s->dp.has_terrain) ||
+      s->topo->row_floats <= 0 || s->N <= 0)
+    return 0;
   const size_t lanes = (size_t)s->topo->row_lanes;
   return ((size_t)s->N + lanes - 1) / lanes * lanes * (size_t)s->topo->row_floats;
 }
@@ -760,6 +823,8 @@ int gs_sim_set_force_sensors(gs_sim* s, int n, const int32_t* bodies) {
   if (n < 0 || n > GS_MAXS || (n > 0 && !bodies)) return fail("gs_sim_set_force_sensors: at most 8 sensors");
   if (n > 0 && s->variant == 2)
     return fail("gs_sim_set_force_sensors: the lane-team kernel has no force sensors (use kernel_variant 1)");
+  if (n > 0 && s->variant == 4)
+    return fail("gs_sim_set_force_sensors: the runtime-sized kernel has no force sensors (compile the topology)");
   if (n > 0 && !s->topo->sens)
     return fail("gs_sim_set_force_sensors: topology %s is compiled without force sensors (sensors flag in "
                 "tools/gen_topologies.py MODELS)", s->topo->name);
@@ -787,7 +852,7 @@ static int kernel_select(gs_sim* s, const char* who) {
   launch_pd_fn pd_fn = s->model_pd_fn;
   int variant = s->model_variant;
   const bool lane = s->dp.any_drive || s->dp.dof_env || (s->dp.self_collide && !s->team_pairs);
-  if (lane && variant == 2) {
+  if (lane && variant == 2) {  // (the runtime-sized kernel, variant 4, has drives and per-actor properties)
     if (s->params.kernel_variant == 2)
       return fail("%s: the lane-team kernel (kernel_variant 2) has no joint drives or per-actor dof properties", who);
     sim_fn = s->topo->sim;
@@ -836,6 +901,9 @@ int gs_sim_set_self_collision(gs_sim* s, int enable) {
   if (!s || !s->topo) return fail("gs_sim_set_self_collision: model not set");
   if (enable && s->h_model.np > 0 && s->topo->npk <= 0)
     return fail("gs_sim_set_self_collision: the compiled topology has no self-contact pool");
+  if (enable && s->h_model.np > 0 && s->variant == 4)
+    return fail("gs_sim_set_self_collision: the runtime-sized kernel has no self-collision (compile the topology "
+                "with tools/gen_topologies.py, or create the actors with collision filter 1)");
   s->dp.self_collide = enable && s->h_model.np > 0;
   if (s->dp.self_collide && s->variant == 2 && !s->team_pairs) {  // this lane-team build has no pair rows
     if (s->params.kernel_variant == 2)

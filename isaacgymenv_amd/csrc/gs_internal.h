@@ -88,6 +88,10 @@ struct DevParams {
   // (lower >= upper: no limit), velocity limit; null = the model's per-asset values
   const float* dof_env;
   int dof_env_n;         // the table's env stride (N)
+  // the runtime-sized kernel (gs_generic.hip, kernel_variant 4): its tree and candidate tables; null otherwise
+  const struct GenTopo* gen;
+  const struct DevLinks* gen_links;
+  int gen_nd, gen_nr;
 };
 #define GS_DOFP_FIELDS 6
 
@@ -101,6 +105,12 @@ struct SimBuffers {
   int N;
   float* sens;           // [6*nsens][N] force-sensor readings or null
   float* rows;           // contact-row tiles of the GLOBAL-row kernels (LaneCfg::GLOBAL), else null
+};
+
+// Candidate tables of the runtime-sized kernel (the compiled kernels have them as Topo_* constants)
+struct GenTopo {
+  int nc;
+  int cbody[GS_MAXC], cshape[GS_MAXC], clink[GS_MAXC];
 };
 
 struct PdDev {
@@ -179,6 +189,14 @@ hipError_t launch_set_root(float* state, int N, int nd, const float* com0, const
                            int n_idx, hipStream_t s);
 hipError_t launch_set_dof(float* state, int N, int nd, const float* src, const int* idx, int n_idx,
                           hipStream_t s);
+// the runtime-sized kernel (gs_generic.hip): workspace SimBuffers::rows = generic_ws_floats per env
+hipError_t launch_sim_generic(const DevModel* M, const DevParams& P, const SimBuffers& B, const float* tau,
+                              hipStream_t st);
+hipError_t launch_pd_generic(const DevModel* M, const DevParams& P, const SimBuffers& B, const PdDev& A,
+                             hipStream_t st);
+inline size_t generic_ws_floats(int nc, int nd, int fixed_base) {
+  return (size_t)2 * (3 * nc + nd) * ((fixed_base ? 0 : 6) + nd);
+}
 
 // ---------------------------------------------------------------- host backend (gs_host.hip)
 // The sim_device=cpu pipeline: the same solver on host buffers, envs spread over a thread pool.

@@ -741,6 +741,9 @@ PACKED_INDEX = {
     "cartpole.urdf": "cartpole.model.json",
     "Hound.urdf": "hound.model.json",
     "nv_ant.xml": "nv_ant.model.json",
+    # (keyed by the last two path components where a file name is shared: hound.py loads urdf/Hound_new/Hound.urdf,
+    # useful_hound.py urdf/UsefulHound/urdf/Hound.urdf)
+    "Hound_new/Hound.urdf": "hound_new.model.json",
 }
 
 
@@ -752,7 +755,9 @@ def load_raw(root: str, filename: str) -> RawModel:
     if os.path.isfile(path) and path.endswith(".xml"):
         from . import _mjcf
         return _mjcf.parse_mjcf(path)
-    if base in PACKED_INDEX:
-        with open(os.path.join(PACKED_DIR, PACKED_INDEX[base])) as f:
-            return RawModel.from_json(json.load(f))
+    key2 = "/".join(filename.replace(os.sep, "/").split("/")[-2:])
+    for key in (key2, base):
+        if key in PACKED_INDEX:
+            with open(os.path.join(PACKED_DIR, PACKED_INDEX[key])) as f:
+                return RawModel.from_json(json.load(f))
     raise FileNotFoundError(f"asset not found: {path} (and no packed model named {base})")

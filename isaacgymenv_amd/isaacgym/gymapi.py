@@ -337,7 +337,8 @@ class Sim:
         p.max_depenetration_velocity = float(px.max_depenetration_velocity)
         p.contact_collection = int(px.contact_collection)
         # GS_PHYSICS_KERNEL=auto|lane|team selects the physics kernel form
-        p.kernel_variant = {"auto": 0, "lane": 1, "team": 2}[os.environ.get("GS_PHYSICS_KERNEL", "auto")]
+        # (generic: the runtime-sized kernel even where a compiled topology exists -- gymsim.h kernel_variant 4)
+        p.kernel_variant = {"auto": 0, "lane": 1, "team": 2, "generic": 4}[os.environ.get("GS_PHYSICS_KERNEL", "auto")]
         # a joint-limit row is generated within this distance of a limit (rad / m)
         p.joint_limit_margin = JOINT_LIMIT_MARGIN
         # PhysX CPU worker threads (cfg/config.yaml:30 num_threads: 4); 0 = the calling thread only
@@ -1049,7 +1050,8 @@ class Gym:
         _lib.check(_lib.lib().gs_sim_enable_timing(sim.handle, int(enable)), "gs_sim_enable_timing")
 
     def amd_kernel_variant(self, sim: Sim) -> int:
-        """1: one env per lane, 2: lane team (4 lanes per env); see gs_sim_kernel_variant."""
+        """1: one env per lane, 2: lane team (4 lanes per env), 3 host backend, 4 runtime-sized (any topology); see
+        gs_sim_kernel_variant."""
         return int(_lib.lib().gs_sim_kernel_variant(sim.handle))
 
     def amd_last_kernel_ms(self, sim: Sim) -> float:

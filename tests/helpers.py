@@ -41,7 +41,12 @@ HOUND_PARAMS = dict(dt=0.005, substeps=1, gravity=[0.0, 0.0, -9.81], pos_iters=4
 # (anymal_terrain.py:282) and UsefulHound (useful_hound.py:421), 1 for Ant (ant.py:190) and Cartpole
 # (cartpole.py:107).  flatten() results of these helpers carry it as flat["self_collide"], which the
 # oracle (OracleSim) and make_gpu_sim follow.
-SELF_COLLIDE = {"anymal": 1, "hound": 1, "ant": 0, "cartpole": 0}
+SELF_COLLIDE = {"anymal": 1, "hound": 1, "ant": 0, "cartpole": 0, "hound_new": 0}
+# hound.py:170-181 (the fork's own quadruped, assets/urdf/Hound_new/Hound.urdf; collision filter 1, :208) and
+# cfg/task/Hound.yaml:31-32,53 (position drives 85 / 2, fixed joints kept): no compiled topology -- the
+# runtime-sized kernel (gs_generic.hip) runs it
+HOUND_NEW_OPTS = dict(HOUND_OPTS, collapse_fixed_joints=False)
+HOUND_NEW_DRIVES = (np.full(12, 1, dtype=np.int32), np.full(12, 85.0), np.full(12, 2.0))
 
 
 def load_art(name, opts):
@@ -75,6 +80,37 @@ def hound():
     flat = flatten(art)
     flat["self_collide"] = SELF_COLLIDE["hound"]
     return art, flat
+
+
+def hound_new():
+    art = load_art("hound_new.model.json", HOUND_NEW_OPTS)
+    flat = flatten(art)
+    flat["self_collide"] = SELF_COLLIDE["hound_new"]
+    return art, flat
+
+
+def hound_new_states(n, seed=0, spread=1.0):
+    """Random Hound_new states: standing near Hound.yaml's 0.62 m (feet on, above or into the ground), tilted,
+    moving, joints within their limits."""
+    rng = np.random.RandomState(seed)
+    art, flat = hound_new()
+    root = np.zeros((n, 13))
+    root[:, 0:2] = rng.uniform(-2, 2, (n, 2))
+    root[:, 2] = rng.uniform(0.35, 0.65, n)
+    axis = rng.normal(size=(n, 3))
+    axis /= np.linalg.norm(axis, axis=1, keepdims=True)
+    ang = rng.uniform(0, 0.3 * spread, n)
+    root[:, 3:6] = axis * np.sin(ang / 2)[:, None]
+    root[:, 6] = np.cos(ang / 2)
+    root[:, 7:10] = rng.normal(0, 0.3 * spread, (n, 3))
+    root[:, 10:13] = rng.normal(0, 0.5 * spread, (n, 3))
+    dof = np.zeros((n, 12, 2))
+    leg = np.tile([0.0, 0.6, -1.2], 4)
+    dof[:, :, 0] = leg + rng.uniform(-0.4, 0.4, (n, 12)) * spread
+    dof[:, :, 1] = rng.normal(0, 1.0 * spread, (n, 12))
+    tau = rng.uniform(-60, 60, (n, 12))
+    mu = np.repeat(rng.uniform(0.5, 1.25, (n, 1)), flat["ns"], axis=1)
+    return root, dof, tau, mu
 
 
 def hound_states(n, seed=0, spread=1.0):
@@ -203,6 +239,11 @@ def make_gpu_sim(kind: str, n: int, params: dict, terrain=None, host: bool = Fal
             setattr(opts, k, v)
         opts.default_dof_drive_mode = gymapi.DOF_MODE_EFFORT
         asset = gym.load_asset(sim, "/nonexistent", "urdf/UsefulHound/urdf/Hound.urdf", opts)
+    elif kind == "hound_new":
+        for k, v in HOUND_NEW_OPTS.items():
+            setattr(opts, k, v)
+        opts.default_dof_drive_mode = gymapi.DOF_MODE_NONE  # hound.py:171
+        asset = gym.load_asset(sim, "/nonexistent", "urdf/Hound_new/Hound.urdf", opts)
     else:
         opts.fix_base_link = True
         asset = gym.load_asset(sim, "/nonexistent", "urdf/cartpole.urdf", opts)
@@ -211,7 +252,7 @@ def make_gpu_sim(kind: str, n: int, params: dict, terrain=None, host: bool = Fal
     for i in range(n):
         env = gym.create_env(sim, gymapi.Vec3(-1, -1, 0), gymapi.Vec3(1, 1, 1), 8)
         pose = gymapi.Transform()
-        pose.p = gymapi.Vec3(0, 0, {"anymal": 0.62, "ant": 0.44, "hound": 0.55}.get(kind, 2.0))
+        pose.p = gymapi.Vec3(0, 0, {"anymal": 0.62, "ant": 0.44, "hound": 0.55, "hound_new": 0.62}.get(kind, 2.0))
         a = gym.create_actor(env, asset, pose, kind, i, 0 if (SELF_COLLIDE[kind] if self_collide is None else self_collide)
                              else 1, 0)
         if drives is not None:

@@ -24,6 +24,8 @@ SOURCES = {
     "cartpole.model.json": "urdf/cartpole.urdf",
     "hound.model.json": "urdf/UsefulHound/urdf/Hound.urdf",
     "nv_ant.model.json": "mjcf/nv_ant.xml",
+    # the fork's own quadruped (hound.py:168-183): no compiled topology, the runtime-sized kernel runs it
+    "hound_new.model.json": "urdf/Hound_new/Hound.urdf",
 }
 
 
