@@ -78,6 +78,8 @@ def parse():
     ap.add_argument("--kernel-launches", type=int, default=50, help="launches timed for the roofline figure")
     ap.add_argument("--other-steps", type=int, default=100,
                     help="timed steps of each other BASELINE config (Ant, trimesh AnymalTerrain, UsefulHound); 0 = skip")
+    ap.add_argument("--others", default="Ant,AnymalTerrain,UsefulHound",
+                    help="comma list of the other configs to time (A/B runs of one of them)")
     ap.add_argument("--ppo-epochs", type=int, default=5,
                     help="timed PPO epochs (AnymalTerrainPPO.yaml: horizon 24 x envs samples each); 0 = skip")
     ap.add_argument("--physx-solver-type", type=int, default=None,
@@ -408,6 +410,8 @@ def _main():
     if args.other_steps > 0:
         del env
         for task, desc, ov, with_ppo in OTHER_CONFIGS:
+            if task not in args.others.split(","):
+                continue
             others.append(other_config_leg(task, desc, ov, args.num_envs, args.other_steps, 20, device, rank, world,
                                            ppo_epochs=min(args.ppo_epochs, 2) if with_ppo else 0))
 

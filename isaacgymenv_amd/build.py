@@ -83,7 +83,7 @@ def _deps_newer(out: str, deps) -> bool:
     return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True, prof: bool = False) -> None:
+def build(force: bool = False, verbose: bool = True, prof: bool = False, variant=None) -> None:
     """Compile every stale library.  Each source is its own hipcc job (objects under _lib/obj/<lib>/,
     all jobs of all libraries in parallel: the physics sources dominate and compile independently),
     then each library is linked from its objects."""
@@ -92,7 +92,12 @@ def build(force: bool = False, verbose: bool = True, prof: bool = False) -> None
     cc = hipcc()
     inc = ["-I", os.path.join(os.path.dirname(HERE), "include"), "-I", CSRC]
     compile_jobs, link_jobs = [], []
-    for lib, srcs in (dict(LIBS, **PROF_LIBS) if prof else LIBS).items():
+    libs = dict(LIBS, **PROF_LIBS) if prof else LIBS
+    if variant:  # (name, defines): an A/B build libgymsim_<name>.so with extra -D flags, never loaded by default
+        vname, vdefs = variant
+        libs = {f"libgymsim_{vname}.so": LIBS["libgymsim.so"]}
+        EXTRA_FLAGS[f"libgymsim_{vname}.so"] = SIM_FLAGS + [f"-D{d}" for d in vdefs]
+    for lib, srcs in libs.items():
         if not all(os.path.exists(os.path.join(CSRC, s)) for s in srcs):
             raise RuntimeError(f"missing sources for {lib}: {srcs}")
         out = os.path.join(LIBDIR, lib)
@@ -139,4 +144,9 @@ def build(force: bool = False, verbose: bool = True, prof: bool = False) -> None
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, prof="--prof" in sys.argv)
+    # python -m isaacgymenv_amd.build [--force] [--prof] [--variant NAME DEFINE ...]
+    var = None
+    if "--variant" in sys.argv:
+        k = sys.argv.index("--variant")
+        var = (sys.argv[k + 1], [d for d in sys.argv[k + 2:] if not d.startswith("--")])
+    build(force="--force" in sys.argv, prof="--prof" in sys.argv, variant=var)

@@ -99,6 +99,7 @@ struct gs_sim {
   uint4* d_tcells = nullptr;
   float* d_tblk = nullptr;        // highest cell top per TERRAIN_BLK x TERRAIN_BLK block of cells
   float* d_tsq4 = nullptr;        // highest cell top of the 4 x 4 cells starting at each cell
+  float4* d_trec = nullptr;       // cell records: vertices + face normals (gs_terrain.h TERRAIN_REC)
   float* d_rows = nullptr;        // contact-row tiles of the GLOBAL-row kernels (TopoEntry::row_floats)
   size_t rows_cap = 0;            // floats allocated
   // host backend (device < 0)
@@ -110,6 +111,7 @@ struct gs_sim {
   std::vector<uint4> h_tcells;
   std::vector<float> h_tblk;
   std::vector<float> h_tsq4;
+  std::vector<float4> h_trec;
   double host_ms = -1.0;          // wall time of the last simulate / pd_step (timing enabled)
   const DevModel* model() const { return host ? &h_model : d_model; }
   const DevLinks* links() const { return host ? &h_links : d_links; }
@@ -179,6 +181,7 @@ void gs_sim_destroy(gs_sim* s) {
   if (s->d_tcells) (void)hipFree(s->d_tcells);
   if (s->d_tblk) (void)hipFree(s->d_tblk);
   if (s->d_tsq4) (void)hipFree(s->d_tsq4);
+  if (s->d_trec) (void)hipFree(s->d_trec);
   if (s->d_rows) (void)hipFree(s->d_rows);
   if (s->d_gen) (void)hipFree(s->d_gen);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -307,12 +310,42 @@ int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_verti
       for (int64_t d = 0; d < 4 && i + d < cr; ++d) m = std::max(m, h4[(size_t)((i + d) * cc + j)]);
       hq[(size_t)(i * cc + j)] = m;
     }
+  // cell records (gs_terrain.h TERRAIN_REC): the four vertices, the unit normals of the cell's triangles
+  // (v00, v11, v01) and (v00, v10, v11) in double from the float vertices; degenerate or downward-facing: (0, 0, -1)
+  std::vector<float4> hr((size_t)(cr * cc * TERRAIN_REC));
+  for (int64_t i = 0; i < cr; ++i)
+    for (int64_t j = 0; j < cc; ++j) {
+      const float4 q00 = hv[i * cols + j], q01 = hv[i * cols + j + 1], q10 = hv[(i + 1) * cols + j],
+                   q11 = hv[(i + 1) * cols + j + 1];
+      auto normal = [](const float4& a, const float4& b, const float4& c, float* nf) {
+        const double e1[3] = {(double)b.x - a.x, (double)b.y - a.y, (double)b.z - a.z};
+        const double e2[3] = {(double)c.x - a.x, (double)c.y - a.y, (double)c.z - a.z};
+        const double x[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+        const double l2 = x[0] * x[0] + x[1] * x[1] + x[2] * x[2];
+        nf[0] = 0.f; nf[1] = 0.f; nf[2] = -1.f;
+        if (!(l2 > 1e-14)) return;
+        const double il = 1.0 / std::sqrt(l2);
+        if (x[2] * il < (double)TERRAIN_DOWN_NZ) return;
+        for (int k = 0; k < 3; ++k) nf[k] = (float)(x[k] * il);
+      };
+      float n0[3], n1[3];
+      normal(q00, q11, q01, n0);
+      normal(q00, q10, q11, n1);
+      float4* r = &hr[(size_t)((i * cc + j) * TERRAIN_REC)];
+      r[0] = make_float4(q00.x, q00.y, q00.z, n0[0]);
+      r[1] = make_float4(q01.x, q01.y, q01.z, n0[1]);
+      r[2] = make_float4(q10.x, q10.y, q10.z, n0[2]);
+      r[3] = make_float4(q11.x, q11.y, q11.z, n1[0]);
+      r[4] = make_float4(n1[1], n1[2], 0.f, 0.f);
+    }
   TerrainDev& T = s->dp.terr;
   if (s->host) {
     s->h_tverts = std::move(hv);
     s->h_tcells = std::move(hc);
     s->h_tblk = std::move(hb);
     s->h_tsq4 = std::move(hq);
+    s->h_trec = std::move(hr);
+    T.rec = s->h_trec.data();
     T.v = s->h_tverts.data();
     T.cell = s->h_tcells.data();
     T.blk = s->h_tblk.data();
@@ -322,6 +355,7 @@ int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_verti
     uint4* dc = nullptr;
     float* db = nullptr;
     float* dq = nullptr;
+    float4* dr = nullptr;
     hipError_t e = hipSetDevice(s->device);
     if (e == hipSuccess) e = hipMalloc(&dv, hv.size() * sizeof(float4));
     if (e == hipSuccess) e = hipMalloc(&dc, hc.size() * sizeof(uint4));
@@ -331,7 +365,10 @@ int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_verti
     if (e == hipSuccess) e = hipMemcpy(dc, hc.data(), hc.size() * sizeof(uint4), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(db, hb.data(), hb.size() * sizeof(float), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(dq, hq.data(), hq.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&dr, hr.size() * sizeof(float4));
+    if (e == hipSuccess) e = hipMemcpy(dr, hr.data(), hr.size() * sizeof(float4), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
+      if (dr) (void)hipFree(dr);
       if (dv) (void)hipFree(dv);
       if (dc) (void)hipFree(dc);
       if (db) (void)hipFree(db);
@@ -342,6 +379,8 @@ int gs_sim_add_triangle_mesh(gs_sim* s, const float* vertices, int64_t num_verti
     s->d_tcells = dc;
     s->d_tblk = db;
     s->d_tsq4 = dq;
+    s->d_trec = dr;
+    T.rec = s->d_trec;
     T.v = s->d_tverts;
     T.cell = s->d_tcells;
     T.blk = s->d_tblk;

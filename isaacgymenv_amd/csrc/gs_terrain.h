@@ -46,10 +46,21 @@ struct TerrainDev {
                        // z = bottom height (float bits), w = footprint extents (TCELL_EXT_*)
   const float* blk;    // [ceil((rows-1)/TERRAIN_BLK)][bcols]: the highest top of each block of cells
   const float* sq4;    // [(rows-1)*(cols-1)]: the highest top of the 4 x 4 cells starting at each cell (clipped)
+  const float4* rec;   // [(rows-1)*(cols-1)][TERRAIN_REC]: each cell's vertices and its two face normals (below)
   int rows, cols, bcols;
   float x0, y0, hs, inv_hs;
   float mu;            // static friction of the mesh
 };
+
+// Cell record (GS_TERR_PLANES): a cell's two triangles tested from one batch of five 16-byte
+// loads, with no normal reconstruction.  rec[0..3] = v00, v01, v10, v11 (xyz), their w = n0.x, n0.y, n0.z, n1.x;
+// rec[4] = (n1.y, n1.z, 0, 0); n0 / n1 = unit face normals of triangles (v00, v11, v01) / (v00, v10, v11), computed
+// on the host in double from the float vertices; a degenerate (|e1 x e2|^2 <= 1e-14) or downward-facing
+// (n_z < TERRAIN_DOWN_NZ) triangle is stored as n = (0, 0, -1), which the face test rejects.
+#define TERRAIN_REC 5
+#ifndef GS_TERR_PLANES
+#define GS_TERR_PLANES 1
+#endif
 
 // footprint flags of a cell: its triangles reach one cell further towards -x, +x, -y, +y
 #define TCELL_XLO 1u
@@ -152,6 +163,38 @@ GS_HD void triangle(const float* p, float r, float thr, const float4& A, const f
   }
 }
 
+// one triangle given its unit face normal from the cell record (triangle()'s statements past the normal)
+GS_HD void triangle_n(const float* p, float r, float thr, const float4& A, const float4& B, const float4& C,
+                      const float* nf, float& bkey, float& best, float* n) {
+  if (nf[2] < TERRAIN_DOWN_NZ) return;  // inverted or degenerate (flagged on the host)
+  const float a[3] = {A.x, A.y, A.z}, b[3] = {B.x, B.y, B.z}, c[3] = {C.x, C.y, C.z};
+  const float ap[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
+  const float sd = dot3(nf, ap);
+  if (sd > thr || sd < -(r + TERRAIN_BACK)) return;
+  float q[3];
+  const bool face = closest_on_triangle(p, a, b, c, q);
+  if (face) {
+    const float key = fabsf(sd);
+    if (key < bkey) { bkey = key; best = sd - r; n[0] = nf[0]; n[1] = nf[1]; n[2] = nf[2]; }
+    return;
+  }
+  if (sd < 0.f) return;
+  const float d[3] = {p[0] - q[0], p[1] - q[1], p[2] - q[2]};
+  const float dd = dot3(d, d);
+  if (dd > thr * thr) return;
+  const float dist = sqrtf(dd);
+  if (dist < bkey) {
+    bkey = dist;
+    best = dist - r;
+    if (dist > 1e-7f) {
+      const float id = 1.f / dist;
+      n[0] = d[0] * id; n[1] = d[1] * id; n[2] = d[2] * id;
+    } else {
+      n[0] = nf[0]; n[1] = nf[1]; n[2] = nf[2];
+    }
+  }
+}
+
 // false when no cell around sphere (p, r) can hold a surface within thr: the range of cells within the horizontal
 // reach is empty, or the sphere's lowest reach lies above the highest cell top of the range (from the 4 x 4
 // square maxima; ranges wider than 8 cells from the 8 x 8 block summary).  sphere_contact starts with exactly this test; the lane team runs it alone first to hand only
@@ -205,7 +248,8 @@ GS_HD bool sphere_contact_scan(const TerrainDev& T, const float* p, float r, flo
   float best = 3.0e38f, bkey = 3.0e38f;
   const float zlo = p[2] - thr;
   const float pad = 1e-4f * T.hs;
-  // one cell given its info word: the culling tests, then its two triangles (vertices loaded here unless given)
+  // one cell given its info word: the culling tests, then its two triangles (vertices loaded here unless given:
+  // the cell record's TERRAIN_REC float4 with GS_TERR_PLANES, else the four vertices)
   auto cell = [&](int i, int j, const uint4& cinfo, const float4* pre = nullptr) {
     const float top = gs_bits_float(cinfo.x);
     if (zlo > top) return;
@@ -218,18 +262,32 @@ GS_HD bool sphere_contact_scan(const TerrainDev& T, const float* p, float r, flo
     const float dy = fmaxf(fmaxf(by0 - pad - p[1], p[1] - by1 - pad), 0.f);
     const float dz = fmaxf(fmaxf(gs_bits_float(cinfo.z) - pad - p[2], p[2] - top - pad), 0.f);
     if (dx * dx + dy * dy + dz * dz >= bkey * bkey) return;
+#if GS_TERR_PLANES
+    const float4* rc = T.rec + ((size_t)i * (T.cols - 1) + j) * TERRAIN_REC;
+    const float4 v00 = pre ? pre[0] : rc[0], v01 = pre ? pre[1] : rc[1], v10 = pre ? pre[2] : rc[2],
+                 v11 = pre ? pre[3] : rc[3], x4 = pre ? pre[4] : rc[4];
+    const float n0[3] = {v00.w, v01.w, v10.w}, n1[3] = {v11.w, x4.x, x4.y};
+    triangle_n(p, r, thr, v00, v11, v01, n0, bkey, best, n);
+    triangle_n(p, r, thr, v00, v10, v11, n1, bkey, best, n);
+#else
     const size_t v0 = (size_t)i * T.cols + j;
     const float4 v00 = pre ? pre[0] : T.v[v0], v01 = pre ? pre[1] : T.v[v0 + 1];
     const float4 v10 = pre ? pre[2] : T.v[v0 + T.cols], v11 = pre ? pre[3] : T.v[v0 + T.cols + 1];
     triangle(p, r, thr, v00, v11, v01, bkey, best, n);
     triangle(p, r, thr, v00, v10, v11, bkey, best, n);
+#endif
   };
   const int ic = (int)floorf(gx), jc = (int)floorf(gy);
   const bool centre = ic >= 0 && ic <= T.rows - 2 && jc >= 0 && jc <= T.cols - 2;
   if (centre) {  // the centre cell's word and vertices in one batch (it is nearly always tested)
-    const size_t v0 = (size_t)ic * T.cols + jc;
     const uint4 cw = T.cell[(size_t)ic * (T.cols - 1) + jc];
+#if GS_TERR_PLANES
+    const float4* rc = T.rec + ((size_t)ic * (T.cols - 1) + jc) * TERRAIN_REC;
+    const float4 pre[TERRAIN_REC] = {rc[0], rc[1], rc[2], rc[3], rc[4]};
+#else
+    const size_t v0 = (size_t)ic * T.cols + jc;
     const float4 pre[4] = {T.v[v0], T.v[v0 + 1], T.v[v0 + T.cols], T.v[v0 + T.cols + 1]};
+#endif
     cell(ic, jc, cw, pre);
   }
   // (2) the rest in (i, j) order.  Before loading a cell's word, its widest possible footprint (one cell further

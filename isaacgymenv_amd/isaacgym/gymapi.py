@@ -323,6 +323,7 @@ class Sim:
         self.prepared = False
         self.drives_dirty = False
         self.handle = None
+        self._pd_args, self._pd_key = None, None  # Gym.amd_pd_decimation_step's cached argument struct
         px = params.physx
         p = _lib.GsSimParams()
         p.dt = params.dt
@@ -1031,16 +1032,21 @@ class Gym:
         """Fused ``for i in decimation: PD torque; simulate; refresh dof`` + ``extra_simulates`` more
         simulates, + the root/contact refreshes of post_physics_step, in ONE kernel launch."""
         L = _lib.lib()
-        a = _lib.GsPdArgs()
         assert sim.gpu_pipeline or sim.host, "the fused step needs the GPU pipeline or the host backend"
+        # the argument struct is kept per sim and rebuilt only when a fixed field changes (a step changes the two
+        # action pointers only): ~2 us of ctypes field stores off the host path before the launch
+        key = (default_pos.data_ptr(), kp, kd, action_scale, torque_limit, decimation, extra_simulates,
+               torques_out.data_ptr(), sim.dof_tensor.data_ptr(), sim.root_tensor.data_ptr() if write_root else None,
+               sim.contact_tensor.data_ptr() if write_contacts else None)
+        a = sim._pd_args
+        if a is None or sim._pd_key != key:
+            a = _lib.GsPdArgs()
+            a.default_pos = key[0]
+            a.kp, a.kd, a.action_scale, a.torque_limit = kp, kd, action_scale, torque_limit
+            a.decimation, a.extra_simulates = int(decimation), int(extra_simulates)
+            a.torques_out, a.dof_state_out, a.root_state_out, a.contact_out = key[7:]
+            sim._pd_args, sim._pd_key = a, key
         a.actions = actions.data_ptr()
-        a.default_pos = default_pos.data_ptr()
-        a.kp, a.kd, a.action_scale, a.torque_limit = kp, kd, action_scale, torque_limit
-        a.decimation, a.extra_simulates = int(decimation), int(extra_simulates)
-        a.torques_out = torques_out.data_ptr()
-        a.dof_state_out = sim.dof_tensor.data_ptr()
-        a.root_state_out = sim.root_tensor.data_ptr() if write_root else None
-        a.contact_out = sim.contact_tensor.data_ptr() if write_contacts else None
         a.actions_copy_out = actions_copy_out.data_ptr() if actions_copy_out is not None else None
         if sim.drives_dirty:
             sim.apply_drives()

@@ -23,11 +23,21 @@ KEEP = ("k_pd_step", "k_simulate", "k_post_", "k_reset", "k_kinematics", "k_houn
 
 
 def short(name: str) -> str:
-    m = re.search(r"(k_\w+|soa_rw|aos_dof_rw|aos13_write|stream_copy|\w*gae\w*)(<[^>]*>|I[0-9]+\w+?E)?", name)
+    if name.startswith("_Z"):  # mangled: ...14k_pd_step_teamI13Topo_anymal_cLb1ELb0EE...
+        m = re.search(r"\d(k_[a-z0-9_]+?)(?:I\d|E|v)", name)
+        t = re.search(r"Topo_([a-z0-9_]+?)(?=[A-Z])", name)
+    else:
+        m = re.search(r"(k_\w+|soa_rw|aos_dof_rw|aos13_write|stream_copy|\w*gae\w*)(<[^>]*>)?", name)
+        t = re.search(r"Topo_(\w+?)[,> ]", name)
     base = m.group(1) if m else name[:60]
-    t = re.search(r"Topo_(\w+?)[,>E ]", name)
-    terr = ", true" in name or "Lb1E" in name
-    return base + (f"<{t.group(1)}{', terr' if terr else ''}>" if t else "")
+    if not t:
+        return base
+    # the template's bool arguments in order (demangled ", true" / mangled "Lb1E"): k_pd_step_team<T, TERR, TGS>
+    # is "k_pd_step_team<anymal_c,0,1>" for the headline (plane, TGS)
+    tail = name[t.end() - 1:]
+    bits = re.findall(r"(?:, (true|false))|(?:Lb([01])E)", tail.split("(")[0] if "<" in name else tail)
+    flags = "".join(("1" if a == "true" or b == "1" else "0") for a, b in bits)
+    return base + f"<{t.group(1)}{',' + ','.join(flags) if flags else ''}>"
 
 
 def main():

@@ -16,7 +16,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "k_pd_step_team<anymal_c>"
+KERNEL = "k_pd_step_team<anymal_c,0,1>"  # <T, TERR, TGS>: the headline (plane, TGS)
 
 
 def main():
