@@ -429,17 +429,24 @@ class AnymalTerrain(VecTask):
     def fused_physics_step(self, actions):
         """pre_physics_step + VecTask's simulate loop + post_physics_step's refreshes, one kernel."""
         if actions.device == self.torques.device and actions.dtype == torch.float32 and actions.is_contiguous():
-            # self.actions = actions.clone() (anymal_terrain.py:442), written by the physics kernel
-            self.actions = torch.empty_like(actions)
+            # self.actions = actions.clone() (anymal_terrain.py:442), written by the physics kernel into a fresh
+            # tensor; the next step's is allocated right after this launch, off the host path before it
+            nxt = self._next_actions
+            if nxt is None or nxt.shape != actions.shape:
+                nxt = torch.empty_like(actions)
+            self.actions = nxt
             self.gym.amd_pd_decimation_step(self.sim, actions, self._default_pos_row(), float(self.Kp),
                                             float(self.Kd), float(self.action_scale), 80.0, self.decimation,
-                                            self.control_freq_inv, self.torques, actions_copy_out=self.actions)
+                                            self.control_freq_inv, self.torques, actions_copy_out=nxt)
+            self._next_actions = torch.empty_like(actions)
         else:
             self.actions = actions.clone().to(self.device)
             self.gym.amd_pd_decimation_step(self.sim, self.actions, self._default_pos_row(), float(self.Kp),
                                             float(self.Kd), float(self.action_scale), 80.0, self.decimation,
                                             self.control_freq_inv, self.torques)
         self._fused_refreshed = True
+
+    _next_actions = None
 
     def _default_pos_row(self):
         if getattr(self, "_default_row", None) is None:
