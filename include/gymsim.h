@@ -41,11 +41,13 @@
 
 #include <stdint.h>
 
+#include "gymtask.h"  /* gs_pd_args.tail_*: the AnymalTerrain tail structs */
+
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define GS_ABI_VERSION 8
+#define GS_ABI_VERSION 9
 
 typedef struct gs_sim gs_sim;
 
@@ -153,10 +155,25 @@ typedef struct gs_pd_args {
     float *contact_out;          /* [N*nb][3] or NULL            */
     float *actions_copy_out;     /* [N][nd] or NULL: receives `actions` (the task's
                                     `self.actions = actions.clone()`, anymal_terrain.py:442) */
+    /* ABI 9: the AnymalTerrain post_physics_step part A (include/gymtask.h gt_anymal_post_physics_a:
+     * anymal_terrain.py:458-475 minus the push) run by the physics kernel's last phase on the outputs it
+     * just wrote -- counters, base-frame quantities, heading command, termination, reward, episode sums,
+     * the reset mask and the {count, seq} publication -- instead of a separate launch; both NULL: none
+     * (the caller launches gt_anymal_post_physics_a).  Only where gs_sim_pd_tail_supported() is 1, with
+     * post_a's vector rows (num_dofs % 4 == 0; torques, actions, last_actions, last_dof_vel and dof_state
+     * 16-byte aligned) and buffers.torques / actions / root_states / contact_forces / dof_state being
+     * this call's torques_out / actions_copy_out / root_state_out / contact_out / dof_state_out.  The
+     * structs are read during the call (they may change afterwards). */
+    const gt_anymal_params *tail_params;
+    const gt_anymal_buffers *tail_buffers;
 } gs_pd_args;
 
 int gs_abi_version(void);
 const char *gs_last_error(void);
+
+/* 1 when gs_sim_pd_step can run the AnymalTerrain tail in its physics kernel (gs_pd_args.tail_*): the
+ * lane-team kernel on the GPU (gs_sim_kernel_variant 2); 0 otherwise. */
+int gs_sim_pd_tail_supported(const gs_sim *sim);
 
 /* 1 if libgymsim was compiled with a specialised kernel for this topology. */
 int gs_topology_supported(const gs_model_desc *model);

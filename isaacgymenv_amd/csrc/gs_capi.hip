@@ -776,6 +776,35 @@ int gs_sim_pd_step(gs_sim* s, const gs_pd_args* a, void* stream) {
   d.root_out = a->root_state_out;
   d.cf_out = a->contact_out;
   d.actions_copy = a->actions_copy_out;
+  d.tail_on = 0;
+  if (a->tail_params || a->tail_buffers) {
+    // the AnymalTerrain tail in the team kernel's last phase (gymsim.h ABI 9): the checks gt_anymal_post_physics_a
+    // makes, post_a's vector rows, and the buffers the kernel has just written being the tail's inputs
+    const gt_anymal_params* tp = a->tail_params;
+    const gt_anymal_buffers* tb = a->tail_buffers;
+    auto aligned = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
+    if (!gs_sim_pd_tail_supported(s)) return fail("gs_sim_pd_step: this sim's kernel has no fused tail");
+    if (!tp || !tb || tb->hound || tp->num_envs != s->N || tp->num_dofs != s->nd || tp->num_dofs % 4 != 0 ||
+        tp->num_bodies != s->nr || tp->num_feet > 4 || tp->num_knees > 4 || tp->num_feet < 0 || tp->num_knees < 0 ||
+        tp->base_index < 0 || tp->base_index >= s->nr || !tb->reset_count || !tb->reset_masks || !tb->reset_buf ||
+        !tb->timeout_buf || !tb->rew_buf || !tb->episode_sums || !tb->base_lin_vel || !tb->base_ang_vel ||
+        !tb->projected_gravity || !tb->progress_buf || !tb->randomize_buf || !tb->commands || !tb->feet_air_time ||
+        !tb->last_actions || !tb->last_dof_vel)
+      return fail("gs_sim_pd_step: invalid tail parameters / buffers");
+    for (int k = 0; k < tp->num_feet; ++k)
+      if (tp->feet_idx[k] < 0 || tp->feet_idx[k] >= s->nr) return fail("gs_sim_pd_step: tail foot index");
+    for (int k = 0; k < tp->num_knees; ++k)
+      if (tp->knee_idx[k] < 0 || tp->knee_idx[k] >= s->nr) return fail("gs_sim_pd_step: tail knee index");
+    if (tb->torques != a->torques_out || tb->actions != a->actions_copy_out || tb->root_states != a->root_state_out ||
+        tb->contact_forces != a->contact_out || tb->dof_state != a->dof_state_out)
+      return fail("gs_sim_pd_step: the tail must read this call's outputs");
+    if (!aligned(tb->torques) || !aligned(tb->actions) || !aligned(tb->last_actions) || !aligned(tb->last_dof_vel) ||
+        !aligned(tb->dof_state))
+      return fail("gs_sim_pd_step: the tail's dof rows must be 16-byte aligned");
+    d.tail_on = 1;
+    d.tail_p = *tp;
+    d.tail_b = *tb;
+  }
   if (s->host) {
     const auto t0 = host_clock::now();
     s->htopo->pd(&s->h_model, s->dp, buffers(s), d, s->pool);
@@ -1022,6 +1051,10 @@ int gs_debug_self_contacts(gs_sim* s, int mode, float* out, int* count, void* st
 }
 
 int gs_sim_kernel_variant(gs_sim* s) { return s ? s->variant : -1; }
+
+int gs_sim_pd_tail_supported(const gs_sim* s) {
+  return s && !s->host && s->topo && s->variant == 2 && team_fused_tail_available() ? 1 : 0;
+}
 
 int gs_sim_enable_timing(gs_sim* s, int enable) {
   if (!s) return fail("gs_sim_enable_timing: null sim");

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include "gs_terrain.h"
+#include "../../include/gymtask.h"
 
 #define GS_MAXB 32   // bodies per articulation
 #define GS_MAXD 32   // dofs per articulation
@@ -124,7 +125,13 @@ struct PdDev {
   float* root_out;           // [N][13]   or null
   float* cf_out;             // [N*nr][3] or null
   float* actions_copy;       // [N][nd]   or null
+  // the AnymalTerrain tail (gymsim.h gs_pd_args.tail_*, gt_anymal_tail.h) run by the team kernel's last phase
+  int tail_on;
+  gt_anymal_params tail_p;
+  gt_anymal_buffers tail_b;
 };
+
+bool team_fused_tail_available();  // gs_team.hip: the lane-team kernel can run PdDev's tail
 
 typedef hipError_t (*launch_sim_fn)(const DevModel*, const DevParams&, const SimBuffers&, const float* tau,
                                     hipStream_t);

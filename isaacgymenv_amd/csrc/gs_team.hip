@@ -21,6 +21,7 @@
 #include "gs_topologies.h"
 #include "gs_math.h"
 #include "gs_pairs.h"
+#include "gt_anymal_tail.h"
 
 // Phase profiler (profiling build only, -DGS_PHASE_PROFILE -> libgymsim_prof.so): per-wave
 // s_memtime deltas per solver phase, summed over waves into gs_phase_cycles (gs_capi.hip).
@@ -2310,11 +2311,39 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
     o[7] = v[0]; o[8] = v[1]; o[9] = v[2];
     o[10] = s.w[0]; o[11] = s.w[1]; o[12] = s.w[2];
   }
+  if (kTeamsPerBlock == 16 && A.tail_on) {
+    // The AnymalTerrain tail (gymsim.h gs_pd_args.tail_*; gt_anymal_tail.h, the source of libgymtask's k_post_a)
+    // on the outputs this wave has just stored (root, contacts, dofs, torques, the actions copy): lane 0 of each
+    // team runs its env, so the separate post_a launch and its wait behind this kernel go away.  The wave's 16
+    // done bits are its 16-bit slice of the 64-env reset-mask word k_reset_flagged ranks; the wave that completes
+    // the grid publishes the count.
+    __syncthreads();  // (one wave per workgroup) this wave's global stores are visible to its own loads
+    const bool reset = lc == 0 && (ND == 12 ? gt_tail::post_a_env<true, false, (ND == 12 ? 12 : 0)>(
+                                                  A.tail_p, A.tail_b, gt_anymal_hound{}, e)
+                                            : gt_tail::post_a_env<true, false>(A.tail_p, A.tail_b, gt_anymal_hound{}, e));
+    const unsigned long long m = __ballot(reset);
+    unsigned m16 = 0;
+#pragma unroll
+    for (int i = 0; i < kTeamsPerBlock; ++i) m16 |= (unsigned)((m >> (LN * i)) & 1ull) << i;
+    const int e0 = e - (int)(threadIdx.x / LN);  // the wave's first env (16-aligned)
+    const unsigned long long live = __ballot(true);
+    if ((int)(threadIdx.x & 63) == __ffsll((long long)live) - 1) {
+      uint16_t* slices = reinterpret_cast<uint16_t*>(A.tail_b.reset_masks);
+      slices[e0 / kTeamsPerBlock] = (uint16_t)m16;
+      // the last wave also clears the slices of its mask word past the last env
+      if (e0 + kTeamsPerBlock >= N)
+        for (int q = e0 / kTeamsPerBlock + 1; q % 4 != 0; ++q) slices[q] = 0;
+      gt_tail::publish_count(A.tail_b, (unsigned)__popc(m16), gridDim.x);
+    }
+  }
   GS_PROF(7)  // outputs
   GS_PROF_FLUSH
 }
 
 }  // namespace
+
+// the fused tail writes 16-env slices of the reset-mask words (one wave of 16 teams per workgroup)
+bool team_fused_tail_available() { return kTeamsPerBlock == 16; }
 
 template <class T>
 hipError_t launch_sim_team(const DevModel* M, const DevParams& P, const SimBuffers& B, const float* tau,

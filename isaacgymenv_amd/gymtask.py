@@ -467,6 +467,34 @@ class AnymalTailKernels:
         _check(lib().gt_anymal_post_physics_a(self.p, b, self._stream()), "gt_anymal_post_physics_a")
         t.reset_buf = self.reset_bool  # check_termination makes reset_buf a bool tensor (anymal_terrain.py:295)
 
+    def tail_for_launch(self):
+        """post_a run by the fused physics launch instead of its own (gymsim ABI 9, gs_pd_args.tail_*): the
+        (params, buffers) structs for amd_pd_decimation_step, with the next sequence number the count is
+        published under; None where the lane team cannot run it (then call post_a after the launch).  Call after
+        the step's actions copy is bound to the task (task.actions) and before the launch."""
+        t = self.task
+        ok = self._tail_ok
+        if ok is None:
+            # off by default (GS_FUSED_TAIL=1 turns it on): measured no faster than the separate launch -- the
+            # physics kernel grew by what post_a took (0.1106 -> 0.1185 ms, 30.0 vs 29.8 M env-steps/s,
+            # profiles/r06i_fused_tail_ab.txt): the tail's cost is its own dependent chain, not the launch
+            ok = self._tail_ok = (os.environ.get("GS_FUSED_TAIL", "0") == "1" and not self.hound and self.nd % 4 == 0
+                                  and t.gym.amd_pd_tail_supported(t.sim))
+        if not ok or not (t.torques.is_contiguous() and t.actions.is_contiguous()):
+            return None
+        b = self._buffers()
+        if any(x % 16 for x in (b.torques, b.actions, b.last_actions, b.last_dof_vel, b.dof_state)):
+            return None
+        self._seq = (self._seq + 1) & 0x7FFFFFFF
+        b.seq = self._seq
+        return self.p, b
+
+    def after_fused_tail(self):
+        """The host side of post_a once the fused launch ran it (check_termination's bool reset_buf)."""
+        self.task.reset_buf = self.reset_bool
+
+    _tail_ok = None
+
     def num_resets(self) -> int:
         """Envs the last post_a flagged for reset, read back through the stream (synchronising)."""
         return int(self.reset_count[2].item())

@@ -46,10 +46,15 @@ class GsPdArgs(C.Structure):
     _fields_ = [("actions", C.c_void_p), ("default_pos", C.c_void_p), ("kp", C.c_float), ("kd", C.c_float),
                 ("action_scale", C.c_float), ("torque_limit", C.c_float), ("decimation", C.c_int32),
                 ("extra_simulates", C.c_int32), ("torques_out", C.c_void_p), ("dof_state_out", C.c_void_p),
-                ("root_state_out", C.c_void_p), ("contact_out", C.c_void_p), ("actions_copy_out", C.c_void_p)]
+                ("root_state_out", C.c_void_p), ("contact_out", C.c_void_p), ("actions_copy_out", C.c_void_p),
+                # ABI 9: the AnymalTerrain tail (gymtask.h gt_anymal_params / gt_anymal_buffers) or NULL
+                ("tail_params", C.c_void_p), ("tail_buffers", C.c_void_p)]
 
 
 _lib = None
+
+
+GS_ABI = 9  # include/gymsim.h GS_ABI_VERSION this binding's structs follow
 
 
 def lib():
@@ -59,6 +64,10 @@ def lib():
             raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m isaacgymenv_amd.build` "
                                "(hipcc, gfx950). There is no CPU fallback.")
         L = C.CDLL(LIB_PATH)
+        L.gs_abi_version.restype = C.c_int
+        if L.gs_abi_version() != GS_ABI:
+            raise RuntimeError(f"{LIB_PATH} has gymsim ABI {L.gs_abi_version()}, this binding needs {GS_ABI}: "
+                               "rebuild it with `python -m isaacgymenv_amd.build`")
         vp, i, f, d = C.c_void_p, C.c_int, C.c_float, C.c_double
         sig = {
             "gs_abi_version": (i, []),
@@ -88,6 +97,7 @@ def lib():
             "gs_sim_set_dof_drives": (i, [vp, vp, vp, vp]),
             "gs_sim_bind_dof_targets": (i, [vp, vp, vp]),
             "gs_sim_bind_dof_properties_env": (i, [vp, vp, i, i]),
+            "gs_sim_pd_tail_supported": (i, [vp]),
             "gs_sim_set_self_collision": (i, [vp, i]),
             "gs_sim_refresh_force_sensor": (i, [vp, vp, vp]),
             "gs_sim_add_triangle_mesh": (i, [vp, vp, C.c_int64, vp, C.c_int64, vp, d, d, d]),
@@ -115,7 +125,7 @@ EXPORTED_SYMBOLS = [
     "gs_sim_set_force_sensors", "gs_sim_bind_force_sensors", "gs_sim_refresh_force_sensor",
     "gs_sim_add_triangle_mesh", "gs_debug_terrain_query", "gs_sim_refresh_rigid_body", "gs_sim_refresh_jacobian",
     "gs_sim_refresh_mass_matrix", "gs_sim_set_dof_drives", "gs_sim_bind_dof_targets", "gs_sim_set_self_collision",
-    "gs_debug_self_contacts", "gs_sim_bind_dof_properties_env",
+    "gs_debug_self_contacts", "gs_sim_bind_dof_properties_env", "gs_sim_pd_tail_supported",
 ]
 
 

@@ -1028,9 +1028,12 @@ class Gym:
     # ---- MI355X extensions (not part of the Isaac Gym API)
     def amd_pd_decimation_step(self, sim: Sim, actions, default_pos, kp: float, kd: float, action_scale: float,
                                torque_limit: float, decimation: int, extra_simulates: int, torques_out,
-                               write_root: bool = True, write_contacts: bool = True, actions_copy_out=None):
+                               write_root: bool = True, write_contacts: bool = True, actions_copy_out=None,
+                               tail=None):
         """Fused ``for i in decimation: PD torque; simulate; refresh dof`` + ``extra_simulates`` more
-        simulates, + the root/contact refreshes of post_physics_step, in ONE kernel launch."""
+        simulates, + the root/contact refreshes of post_physics_step, in ONE kernel launch.  ``tail``: the
+        AnymalTerrain post_physics_step part A run in the same launch, as (gt_anymal_params, gt_anymal_buffers)
+        ctypes structs (gymtask.AnymalTailKernel.tail_for_launch; only where amd_pd_tail_supported)."""
         L = _lib.lib()
         assert sim.gpu_pipeline or sim.host, "the fused step needs the GPU pipeline or the host backend"
         # the argument struct is kept per sim and rebuilt only when a fixed field changes (a step changes the two
@@ -1048,9 +1051,17 @@ class Gym:
             sim._pd_args, sim._pd_key = a, key
         a.actions = actions.data_ptr()
         a.actions_copy_out = actions_copy_out.data_ptr() if actions_copy_out is not None else None
+        if tail is None:
+            a.tail_params = a.tail_buffers = None
+        else:
+            a.tail_params, a.tail_buffers = C.addressof(tail[0]), C.addressof(tail[1])
         if sim.drives_dirty:
             sim.apply_drives()
         _lib.check(L.gs_sim_pd_step(sim.handle, a, sim.stream()), "gs_sim_pd_step")
+
+    def amd_pd_tail_supported(self, sim: Sim) -> bool:
+        """The fused step's kernel can run the AnymalTerrain tail (gs_sim_pd_tail_supported: the lane team)."""
+        return bool(_lib.lib().gs_sim_pd_tail_supported(sim.handle))
 
     def amd_enable_kernel_timing(self, sim: Sim, enable: bool = True):
         _lib.check(_lib.lib().gs_sim_enable_timing(sim.handle, int(enable)), "gs_sim_enable_timing")

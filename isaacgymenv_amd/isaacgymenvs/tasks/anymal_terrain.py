@@ -435,18 +435,29 @@ class AnymalTerrain(VecTask):
             if nxt is None or nxt.shape != actions.shape:
                 nxt = torch.empty_like(actions)
             self.actions = nxt
+            # post_physics_step's part A (gymtask post_a) in the same launch, except on a push step (the push
+            # changes root_states before post_a reads them, anymal_terrain.py:458-460)
+            tail = None
+            kern = self._kernels
+            if kern is not None and (self.common_step_counter + 1) % self.push_interval != 0:
+                tail = kern.tail_for_launch()
             self.gym.amd_pd_decimation_step(self.sim, actions, self._default_pos_row(), float(self.Kp),
                                             float(self.Kd), float(self.action_scale), 80.0, self.decimation,
-                                            self.control_freq_inv, self.torques, actions_copy_out=nxt)
+                                            self.control_freq_inv, self.torques, actions_copy_out=nxt, tail=tail)
+            self._tail_fused = tail is not None
+            self.fused_tail_steps += int(tail is not None)
             self._next_actions = torch.empty_like(actions)
         else:
             self.actions = actions.clone().to(self.device)
             self.gym.amd_pd_decimation_step(self.sim, self.actions, self._default_pos_row(), float(self.Kp),
                                             float(self.Kd), float(self.action_scale), 80.0, self.decimation,
                                             self.control_freq_inv, self.torques)
+            self._tail_fused = False
         self._fused_refreshed = True
 
     _next_actions = None
+    _tail_fused = False
+    fused_tail_steps = 0  # steps whose post_a ran inside the physics launch (a counter for tests / probes)
 
     def _default_pos_row(self):
         if getattr(self, "_default_row", None) is None:
@@ -464,7 +475,11 @@ class AnymalTerrain(VecTask):
             if push:
                 self.push_robots()
             kern = self._kernels
-            kern.post_a()  # counters, base quantities, heading command, termination, reward
+            if self._tail_fused:  # post_a ran in the physics launch (fused_physics_step)
+                kern.after_fused_tail()
+            else:
+                kern.post_a()  # counters, base quantities, heading command, termination, reward
+            self._tail_fused = False
             # Optimistic: most steps reset nobody, so draw the noise and build the observations before
             # the host knows the count.  On a reset step, roll the RNG back and redo both after
             # reset_idx: the draws, their order and the results are the reference's either way.

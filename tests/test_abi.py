@@ -48,7 +48,7 @@ def test_abi_version_and_topology_query():
     from isaacgymenv_amd.isaacgym import _lib
     from tests import helpers as H
     L = _lib.lib()
-    assert L.gs_abi_version() == 8
+    assert L.gs_abi_version() == 9
     for make in (H.anymal, H.cartpole, H.hound):
         art, flat = make()
         d, keep = _lib.model_desc(flat)

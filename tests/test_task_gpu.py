@@ -171,6 +171,56 @@ def test_kernel_tail_equals_torch_tail_across_resets(terrain, monkeypatch):
     assert n_reset_steps >= 2
 
 
+@pytest.mark.parametrize("terrain", ["plane", "trimesh"])
+def test_fused_tail_in_physics_launch_is_bit_identical_to_post_a(terrain, monkeypatch):
+    """post_a run by the lane-team physics kernel's last phase (gymsim ABI 9, gs_pd_args.tail_*) against the
+    separate k_post_a launch, from the same state over 12 steps of 5-step episodes with a push step inside the
+    window (that step falls back to the separate launch): every output bit-identical -- the same source
+    (gt_anymal_tail.h) compiled without FMA contraction in both libraries."""
+    n = 256
+    over = {"task.env.learn.episodeLength_s": 0.1}
+    if terrain == "trimesh":
+        over.update(TRIMESH)
+    monkeypatch.setenv("GS_FUSED_TAIL", "1")
+    env = _make("AnymalTerrain", n, monkeypatch, **over)
+    assert env.gym.amd_pd_tail_supported(env.sim)
+    gen = torch.Generator(device="cuda:0").manual_seed(11)
+    acts = [2 * torch.rand((n, 12), device="cuda:0", generator=gen) - 1 for _ in range(12)]
+    env.step(acts[0])
+    env.common_step_counter = env.push_interval - 6  # the 6th step below pushes
+    snap = _snapshot(env)
+    kernels = env._kernels
+    out, fused_steps = {}, {}
+    for mode in ("fused", "separate"):
+        _restore(env, snap)
+        kernels._tail_ok = None if mode == "fused" else False
+        env.extras.pop("episode", None)
+        res, n0 = [], env.fused_tail_steps
+        for a in acts:
+            obs, rew, reset, extras = env.step(a)
+            ep = extras.get("episode")
+            res.append([obs["obs"].clone(), rew.clone(), reset.clone(), extras["time_outs"].clone(),
+                        None if ep is None else torch.stack([torch.as_tensor(v, device="cuda:0").float()
+                                                             for v in ep.values()]),
+                        env.root_states.clone(), env.progress_buf.clone(), env.commands.clone(),
+                        env.feet_air_time.clone(), torch.stack([v.clone() for v in env.episode_sums.values()]),
+                        env.base_lin_vel.clone(), env.projected_gravity.clone(), kernels.reset_masks.clone()])
+            env.extras.pop("episode", None)
+        out[mode] = res
+        fused_steps[mode] = env.fused_tail_steps - n0
+    kernels._tail_ok = None
+    # every step but the push step ran post_a in the physics launch; the separate mode never did
+    assert fused_steps == {"fused": len(acts) - 1, "separate": 0}, fused_steps
+    n_reset_steps = 0
+    for t, (a, b) in enumerate(zip(out["fused"], out["separate"])):
+        n_reset_steps += int(bool(a[2].any()))
+        for k, (x, y) in enumerate(zip(a, b)):
+            assert (x is None) == (y is None), (t, k)
+            if x is not None:
+                assert torch.equal(x, y), f"step {t} output {k}"
+    assert n_reset_steps >= 2
+
+
 def test_anymal_full_episode(monkeypatch):
     n = 512
     env = _make("AnymalTerrain", n, monkeypatch)
