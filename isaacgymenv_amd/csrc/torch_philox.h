@@ -44,12 +44,29 @@ __device__ __forceinline__ uint4 philox10(uint4 c, uint32_t k0, uint32_t k1) {
 }
 
 // element i of torch.rand(n) drawn from plan d (d.numel == n)
+#ifndef GT_PHILOX_WIDE
+#define GT_PHILOX_WIDE 0  // 1: always the 64-bit index math (A/B builds)
+#endif
+
 __device__ __forceinline__ float rand_at(const gt_torch_rand_plan& d, uint64_t i) {
   const uint64_t T = d.threads;
-  const uint64_t it = i / (4 * T);
-  const uint64_t r = i - it * 4 * T;
-  const uint32_t ii = (uint32_t)(r / T);
-  const uint64_t idx = r - (uint64_t)ii * T;
+  uint64_t it, idx;
+  uint32_t ii;
+  if (!GT_PHILOX_WIDE && (i >> 32) == 0 && (T >> 30) == 0) {
+    // the same integer quotients in 32 bits (a 64-bit division is a long software sequence on the GPU; the
+    // observation draws of a 4096-env step are ~770 k elements)
+    const uint32_t i32 = (uint32_t)i, T32 = (uint32_t)T;
+    const uint32_t it32 = i32 / (4u * T32);
+    const uint32_t r = i32 - it32 * (4u * T32);
+    ii = r / T32;
+    it = it32;
+    idx = r - ii * T32;
+  } else {
+    it = i / (4 * T);
+    const uint64_t r = i - it * 4 * T;
+    ii = (uint32_t)(r / T);
+    idx = r - (uint64_t)ii * T;
+  }
   const uint64_t ctr = d.offset / 4 + it;
   const uint4 v = philox10(uint4{(uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)idx, (uint32_t)(idx >> 32)},
                            (uint32_t)d.seed, (uint32_t)(d.seed >> 32));

@@ -11,7 +11,9 @@ import os
 import torch
 from isaacgymenv_amd._stream import raw_stream
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libgymtask.so")
+# GT_LIBGYMTASK names another build of the library in _lib/ (A/B runs)
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                        os.path.basename(os.environ.get("GT_LIBGYMTASK", "libgymtask.so")))
 
 
 class GtTorchRandPlan(C.Structure):

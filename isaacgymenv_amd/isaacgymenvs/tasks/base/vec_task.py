@@ -24,6 +24,7 @@ which replaces the three torch ops of vec_task.py:393-402.
 from __future__ import annotations
 
 import abc
+import math
 import os
 import sys
 import time
@@ -223,7 +224,7 @@ class VecTask(Env):
                                                    Dict[str, Any]]:
         if self.dr_randomizations.get("actions", None):
             actions = self.dr_randomizations["actions"]["noise_lambda"](actions)
-        if np.isinf(self.clip_actions):
+        if math.isinf(self.clip_actions):  # (a Python float: math.isinf, ~1 us cheaper per step than np.isinf)
             action_tensor = actions  # clamp(+-inf) is an identity copy; pre_physics_step clones anyway
         else:
             action_tensor = torch.clamp(actions, -self.clip_actions, self.clip_actions)
