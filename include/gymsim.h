@@ -232,6 +232,10 @@ int gs_sim_refresh_mass_matrix(gs_sim *sim, float *mass_matrix, void *stream);
  * anymal_terrain.py:401-407, 439 */
 int gs_sim_set_root(gs_sim *sim, const float *root_state, const int32_t *idx, int n_idx, void *stream);
 int gs_sim_set_dof(gs_sim *sim, const float *dof_state, const int32_t *idx, int n_idx, void *stream);
+/* ABI 9: gs_sim_set_root + gs_sim_set_dof with the same indices in ONE launch (a reset's pair,
+ * set_actor_root_state_tensor_indexed + set_dof_state_tensor_indexed, anymal_terrain.py:401-408). */
+int gs_sim_set_root_and_dof(gs_sim *sim, const float *root, const float *dof, const int32_t *idx, int n_idx,
+                            void *stream);
 
 /* Fused decimation step, see gs_pd_args. */
 int gs_sim_pd_step(gs_sim *sim, const gs_pd_args *args, void *stream);

@@ -885,6 +885,20 @@ int gs_sim_set_dof(gs_sim* s, const float* src, const int32_t* idx, int n_idx, v
   return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_set_dof");
 }
 
+int gs_sim_set_root_and_dof(gs_sim* s, const float* root, const float* dof, const int32_t* idx, int n_idx,
+                            void* stream) {
+  if (ready(s, "gs_sim_set_root_and_dof")) return -1;
+  if (!root || !dof || !idx || n_idx < 0) return fail("gs_sim_set_root_and_dof: root, dof and idx required");
+  if (s->host) {
+    host_set_root(s->state, s->N, &s->h_model.root_com[0], root, idx, n_idx);
+    host_set_dof(s->state, s->N, s->nd, dof, idx, n_idx);
+    return 0;
+  }
+  hipError_t e = launch_set_root_dof(s->state, s->N, s->nd, &s->d_model->root_com[0], root, dof, idx, n_idx,
+                                     (hipStream_t)stream);
+  return e == hipSuccess ? 0 : hip_fail(e, "gs_sim_set_root_and_dof");
+}
+
 int gs_sim_set_force_sensors(gs_sim* s, int n, const int32_t* bodies) {
   if (!s || !s->topo) return fail("gs_sim_set_force_sensors: model not set");
   if (s->state) return fail("gs_sim_set_force_sensors: call before gs_sim_prepare");

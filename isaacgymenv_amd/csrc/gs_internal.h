@@ -194,6 +194,8 @@ hipError_t launch_kinematics(const DevModel* M, const DevLinks* L, const float* 
 hipError_t launch_refresh_sensor(const float* soa, int N, int ns, float* out, hipStream_t s);
 hipError_t launch_set_root(float* state, int N, int nd, const float* com0, const float* src, const int* idx,
                            int n_idx, hipStream_t s);
+hipError_t launch_set_root_dof(float* state, int N, int nd, const float* com0, const float* root, const float* dof,
+                               const int* idx, int n, hipStream_t s);
 hipError_t launch_set_dof(float* state, int N, int nd, const float* src, const int* idx, int n_idx,
                           hipStream_t s);
 // the runtime-sized kernel (gs_generic.hip): workspace SimBuffers::rows = generic_ws_floats per env

@@ -77,6 +77,25 @@ __global__ void k_set_dof(float* __restrict__ st, int N, int nd, const float* __
   st[(13 + nd + j) * N + e] = src[((size_t)e * nd + j) * 2 + 1];
 }
 
+// a reset's two indexed sets in one launch: threads [0, n nd) the dofs (as k_set_dof), [n nd, n nd + n) the roots
+__global__ void k_set_root_dof(float* __restrict__ st, int N, int nd, const float* __restrict__ com0,
+                               const float* __restrict__ root, const float* __restrict__ dof,
+                               const int* __restrict__ idx, int n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nt = n * nd;
+  if (t < nt) {
+    const int r = t / nd, j = t - r * nd;
+    const int e = idx[r];
+    if (e < 0 || e >= N) return;
+    st[(13 + j) * N + e] = dof[((size_t)e * nd + j) * 2 + 0];
+    st[(13 + nd + j) * N + e] = dof[((size_t)e * nd + j) * 2 + 1];
+  } else if (t < nt + n) {
+    const int e = idx[t - nt];
+    if (e < 0 || e >= N) return;
+    set_root_env(st, N, com0, root, e);
+  }
+}
+
 __global__ void k_terrain_query(TerrainDev T, float offset, const float* __restrict__ c, const float* __restrict__ r,
                                 int n, float* __restrict__ out) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -123,6 +142,13 @@ hipError_t launch_set_root(float* state, int N, int nd, const float* com0, const
   const int n = idx ? n_idx : N;
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_set_root, dim3(nblk(n, 256)), dim3(256), 0, s, state, N, com0, src, idx, n);
+  return hipGetLastError();
+}
+hipError_t launch_set_root_dof(float* state, int N, int nd, const float* com0, const float* root, const float* dof,
+                               const int* idx, int n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_set_root_dof, dim3(nblk((long)n * (nd + 1), 256)), dim3(256), 0, s, state, N, nd, com0, root, dof,
+                     idx, n);
   return hipGetLastError();
 }
 hipError_t launch_set_dof(float* state, int N, int nd, const float* src, const int* idx, int n_idx, hipStream_t s) {

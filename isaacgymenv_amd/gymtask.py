@@ -425,12 +425,14 @@ class AnymalTailKernels:
                "feet_air_time", "progress_buf", "randomize_buf", "rew_buf", "base_lin_vel", "base_ang_vel",
                "projected_gravity", "obs_buf")
 
-    def _buffers(self):
-        """The gt_anymal_buffers struct; rebuilt only if the task rebound a buffer (cheap on the hot path)."""
+    def _buffers(self, check: bool = True):
+        """The gt_anymal_buffers struct; rebuilt only if the task rebound a buffer (cheap on the hot path).
+        check=False skips the rebinding check (the later launches of one step's tail, after post_a checked)."""
         t = self.task
-        cur = tuple(getattr(t, attr) for _, attr in self._stable)
         b = self._b
-        if b is None or any(x is not y for x, y in zip(cur, self._bound)):
+        if b is None or check:
+            cur = tuple(getattr(t, attr) for _, attr in self._stable)
+        if b is None or (check and any(x is not y for x, y in zip(cur, self._bound))):
             b = GtAnymalBuffers()
             for (name, attr), v in zip(self._stable, cur):
                 assert v.is_contiguous() and v.device.type == "cuda", attr
@@ -622,7 +624,7 @@ class AnymalTailKernels:
                 h.u_arm = extra.pop(0).data_ptr()
         ids = torch.empty(k, dtype=torch.int32, device=dev)
         ep = torch.empty(len(self.TERMS) + 1, dtype=torch.float32, device=dev)
-        _check(lib().gt_anymal_reset_flagged(self.p, self._buffers(), k, d, tr, ids.data_ptr(), ep.data_ptr(),
+        _check(lib().gt_anymal_reset_flagged(self.p, self._buffers(check=False), k, d, tr, ids.data_ptr(), ep.data_ptr(),
                                              float(t.max_episode_length_s), self.reset_scratch.data_ptr(),
                                              self._stream()), "gt_anymal_reset_flagged")
         t._set_reset_state(ids)
@@ -669,7 +671,7 @@ class AnymalTailKernels:
     def post_b(self, noise, noise_plan=None):
         """Observations (+noise), history buffers, and VecTask's time_outs / clamped obs (vec_task.py:393-402)."""
         t = self.task
-        b = self._buffers()
+        b = self._buffers(check=False)
         fuse_outputs = not t.dr_randomizations.get("observations", None)
         if fuse_outputs:
             obs = torch.empty_like(t.obs_buf)

@@ -98,6 +98,7 @@ def lib():
             "gs_sim_bind_dof_targets": (i, [vp, vp, vp]),
             "gs_sim_bind_dof_properties_env": (i, [vp, vp, i, i]),
             "gs_sim_pd_tail_supported": (i, [vp]),
+            "gs_sim_set_root_and_dof": (i, [vp, vp, vp, vp, i, vp]),
             "gs_sim_set_self_collision": (i, [vp, i]),
             "gs_sim_refresh_force_sensor": (i, [vp, vp, vp]),
             "gs_sim_add_triangle_mesh": (i, [vp, vp, C.c_int64, vp, C.c_int64, vp, d, d, d]),
@@ -125,7 +126,7 @@ EXPORTED_SYMBOLS = [
     "gs_sim_set_force_sensors", "gs_sim_bind_force_sensors", "gs_sim_refresh_force_sensor",
     "gs_sim_add_triangle_mesh", "gs_debug_terrain_query", "gs_sim_refresh_rigid_body", "gs_sim_refresh_jacobian",
     "gs_sim_refresh_mass_matrix", "gs_sim_set_dof_drives", "gs_sim_bind_dof_targets", "gs_sim_set_self_collision",
-    "gs_debug_self_contacts", "gs_sim_bind_dof_properties_env", "gs_sim_pd_tail_supported",
+    "gs_debug_self_contacts", "gs_sim_bind_dof_properties_env", "gs_sim_pd_tail_supported", "gs_sim_set_root_and_dof",
 ]
 
 

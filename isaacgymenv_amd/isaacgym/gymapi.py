@@ -630,8 +630,8 @@ class Sim:
         n = int(n) if n else idx.numel()
         if n == 0:
             return
-        _lib.check(L.gs_sim_set_root(self.handle, root.data_ptr(), idx.data_ptr(), n, s), "set root")
-        _lib.check(L.gs_sim_set_dof(self.handle, dof.data_ptr(), idx.data_ptr(), n, s), "set dof")
+        _lib.check(L.gs_sim_set_root_and_dof(self.handle, root.data_ptr(), dof.data_ptr(), idx.data_ptr(), n, s),
+                   "set root and dof")
         self._hold = (root, dof, idx)
 
     def simulate(self):
