@@ -498,6 +498,7 @@ class AnymalTailKernels:
         self.task.reset_buf = self.reset_bool
 
     _tail_ok = None
+    _ids_buf = None
 
     def num_resets(self) -> int:
         """Envs the last post_a flagged for reset, read back through the stream (synchronising)."""
@@ -622,7 +623,12 @@ class AnymalTailKernels:
                 tr.u_root_xy = extra.pop(0).data_ptr()
             if h is not None:
                 h.u_arm = extra.pop(0).data_ptr()
-        ids = torch.empty(k, dtype=torch.int32, device=dev)
+        # the flagged env ids: a prefix of one persistent buffer (stream order keeps the previous reset's readers
+        # ahead of this write); extras["episode"] gets a fresh buffer per reset, as the reference's torch.mean
+        ids_buf = self._ids_buf
+        if ids_buf is None or ids_buf.numel() < t.num_envs:
+            ids_buf = self._ids_buf = torch.empty(t.num_envs, dtype=torch.int32, device=dev)
+        ids = ids_buf[:k]
         ep = torch.empty(len(self.TERMS) + 1, dtype=torch.float32, device=dev)
         _check(lib().gt_anymal_reset_flagged(self.p, self._buffers(check=False), k, d, tr, ids.data_ptr(), ep.data_ptr(),
                                              float(t.max_episode_length_s), self.reset_scratch.data_ptr(),

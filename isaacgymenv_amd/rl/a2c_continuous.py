@@ -447,8 +447,9 @@ class A2CAgent:
                 else:
                     self._store_pre(n, obs, res)
             actions = res["actions"]
-            if cfg.clip_actions:
-                actions = torch.clamp(actions, -1.0, 1.0)  # action space is [-1, 1]: rescale is identity
+            if cfg.clip_actions:  # action space is [-1, 1]: rescale is identity
+                clipped = res.get("actions_clipped")  # (the act graph's static clamp output)
+                actions = clipped if clipped is not None else torch.clamp(actions, -1.0, 1.0)
             self.obs, rewards, dones, infos = self.env.step(actions)
             self._has_timeouts = "time_outs" in infos
             if self._fused_post:
@@ -686,6 +687,8 @@ class A2CAgent:
         with torch.cuda.graph(g, pool=torch.cuda.graph_pool_handle()):
             with torch.no_grad():
                 self._g_res = self.model({"is_train": False, "obs": self._g_obs, "noise": self._g_noise})
+                if self.cfg.clip_actions:  # play_steps' clamp, replayed with the forward (one host launch less)
+                    self._g_res["actions_clipped"] = torch.clamp(self._g_res["actions"], -1.0, 1.0)
         if not self.model.used_input_noise:  # the torch statement drew inside the graph
             self._g_noise = None
         self._act_graph = g
