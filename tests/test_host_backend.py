@@ -492,3 +492,25 @@ def test_host_tgs_matches_oracle_tgs_and_warns_nothing():
 
         H.assert_close_or_explained(H.state_fields(g_root, g_dof), H.state_fields(o_root, o_dof), rerun,
                                     what=f"host TGS one simulate vs the oracle's TGS ({kind}, {n} random states)")
+
+
+def test_set_root_and_dof_in_one_call_equals_the_two_indexed_sets():
+    """gs_sim_set_root_and_dof (ABI 9: a reset's root and dof indexed sets in one call / one launch) writes the same
+    sim state as gs_sim_set_root then gs_sim_set_dof with the same indices (host backend; the GPU form runs in every
+    fused reset of tests/test_task_gpu.py)."""
+    import torch
+    art, flat = H.anymal()
+    n = 16
+    rng = np.random.RandomState(4)
+    sims = [H.make_host_sim("anymal", n, H.ANYMAL_PARAMS)[1] for _ in range(2)]
+    root = torch.from_numpy(rng.normal(size=(n, 13)).astype(np.float32))
+    root[:, 3:7] /= root[:, 3:7].norm(dim=1, keepdim=True)
+    dof = torch.from_numpy(rng.normal(size=(n * 12, 2)).astype(np.float32))
+    idx = torch.tensor([1, 4, 5, 11, 15], dtype=torch.int32)
+    sims[0].set_root_and_dof(root, dof, idx, len(idx))
+    sims[1].set_state("root", root, idx, len(idx))
+    sims[1].set_state("dof", dof, idx, len(idx))
+    assert torch.equal(sims[0].state, sims[1].state)
+    untouched = [e for e in range(n) if e not in idx.tolist()]
+    fresh = H.make_host_sim("anymal", n, H.ANYMAL_PARAMS)[1].state
+    assert torch.equal(sims[0].state[:, untouched], fresh[:, untouched])
