@@ -172,7 +172,7 @@ int gs_abi_version(void);
 const char *gs_last_error(void);
 
 /* 1 when gs_sim_pd_step can run the AnymalTerrain tail in its physics kernel (gs_pd_args.tail_*): the
- * lane-team kernel on the GPU (gs_sim_kernel_variant 2); 0 otherwise. */
+ * lane-team kernel on the GPU (gs_sim_kernel_variant 2) of a plane scene; 0 otherwise. */
 int gs_sim_pd_tail_supported(const gs_sim *sim);
 
 /* 1 if libgymsim was compiled with a specialised kernel for this topology. */

@@ -1067,7 +1067,7 @@ int gs_debug_self_contacts(gs_sim* s, int mode, float* out, int* count, void* st
 int gs_sim_kernel_variant(gs_sim* s) { return s ? s->variant : -1; }
 
 int gs_sim_pd_tail_supported(const gs_sim* s) {
-  return s && !s->host && s->topo && s->variant == 2 && team_fused_tail_available() ? 1 : 0;
+  return s && !s->host && s->topo && s->variant == 2 && !s->dp.has_terrain && team_fused_tail_available() ? 1 : 0;
 }
 
 int gs_sim_enable_timing(gs_sim* s, int enable) {

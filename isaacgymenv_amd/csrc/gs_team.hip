@@ -2311,7 +2311,8 @@ __global__ __launch_bounds__(kTeamBlock, 1) void k_pd_step_team(const DevModel* 
     o[7] = v[0]; o[8] = v[1]; o[9] = v[2];
     o[10] = s.w[0]; o[11] = s.w[1]; o[12] = s.w[2];
   }
-  if (kTeamsPerBlock == 16 && A.tail_on) {
+  if constexpr (!TERR) if (kTeamsPerBlock == 16 && A.tail_on) {  // (plane kernels only: the TERR form is at its
+                                                                    // register limit, the tail cost it 12 B scratch)
     // The AnymalTerrain tail (gymsim.h gs_pd_args.tail_*; gt_anymal_tail.h, the source of libgymtask's k_post_a)
     // on the outputs this wave has just stored (root, contacts, dofs, torques, the actions copy): lane 0 of each
     // team runs its env, so the separate post_a launch and its wait behind this kernel go away.  The wave's 16

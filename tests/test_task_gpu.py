@@ -171,7 +171,7 @@ def test_kernel_tail_equals_torch_tail_across_resets(terrain, monkeypatch):
     assert n_reset_steps >= 2
 
 
-@pytest.mark.parametrize("terrain", ["plane", "trimesh"])
+@pytest.mark.parametrize("terrain", ["plane"])  # (the TERR kernels carry no tail: gs_sim_pd_tail_supported 0)
 def test_fused_tail_in_physics_launch_is_bit_identical_to_post_a(terrain, monkeypatch):
     """post_a run by the lane-team physics kernel's last phase (gymsim ABI 9, gs_pd_args.tail_*) against the
     separate k_post_a launch, from the same state over 12 steps of 5-step episodes with a push step inside the
