@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define GT_ABI_VERSION 4
+#define GT_ABI_VERSION 5
 #define GT_ANYMAL_NUM_TERMS 13  /* lin_vel_xy lin_vel_z ang_vel_z ang_vel_xy orient torques joint_acc
                                    base_height air_time collision stumble action_rate hip */
 
@@ -178,6 +178,23 @@ int gt_anymal_reset_flagged(const gt_anymal_params *p, const gt_anymal_buffers *
                             const gt_anymal_reset_draws *draws, const struct gt_anymal_terrain_reset *terrain,
                             int32_t *env_ids_out, float *episode_out, float episode_length_s, void *scratch,
                             void *stream);
+
+/* ABI 5: a reset step's whole host sequence after post_a's count (anymal_terrain.py:458-485 with k > 0, plane,
+ * AnymalTerrain): the reset draws' plans (torch.rand of k*nd, k*nd, k, k, k in the reference's order), the
+ * gt_anymal_reset_flagged launch, the root / dof indexed sets through `set_state` (e.g. gymsim's
+ * gs_sim_set_root_and_dof with ctx = the gs_sim), then gt_anymal_post_physics_b with the observation noise plan
+ * (add_noise) -- one host call instead of the Python between them.  seed / *offset: the
+ * device generator's seed and Philox offset before the draws (the caller's rolled-back offset); *offset returns
+ * the offset after them, as torch would leave it.  grid_cap = CUs * maxThreadsPerCU / 256 (the plans' thread
+ * counts, see gt_torch_rand_plan).  draws: the affine maps (its u_* / plan_* are written here).  b->obs_out /
+ * time_outs / clip_obs as for post_physics_b.  UsefulHound (b->hound) and the trimesh reset are refused. */
+typedef int (*gt_set_state_fn)(void *ctx, const float *root_states, const float *dof_state, const int32_t *idx,
+                               int n, void *stream);
+int gt_anymal_reset_observe(const gt_anymal_params *p, const gt_anymal_buffers *b, int k, gt_anymal_reset_draws *draws,
+                            int32_t *env_ids_out, float *episode_out, float episode_length_s, void *scratch,
+                            uint64_t seed, uint64_t *offset, uint32_t grid_cap, int add_noise,
+                            gt_set_state_fn set_state, void *set_state_ctx, const float *root_states,
+                            const float *dof_state, void *stream);
 
 /* Pinned, device-mapped, coherent host memory for host_count (hipHostMalloc). */
 int gt_host_alloc(uint64_t bytes, void **host_ptr, void **device_ptr);

@@ -543,6 +543,45 @@ int gt_anymal_reset_flagged(const gt_anymal_params* p, const gt_anymal_buffers* 
   return e == hipSuccess ? 0 : fail("gt_anymal_reset_flagged", e);
 }
 
+int gt_anymal_reset_observe(const gt_anymal_params* p, const gt_anymal_buffers* b, int k, gt_anymal_reset_draws* d,
+                            int32_t* env_ids_out, float* episode_out, float episode_length_s, void* scratch,
+                            uint64_t seed, uint64_t* offset, uint32_t grid_cap, int add_noise, gt_set_state_fn set_state,
+                            void* set_state_ctx, const float* root_states, const float* dof_state, void* stream) {
+  if (check_params(p, b)) return -1;
+  if (b->hound || !d || !offset || grid_cap == 0 || !set_state || !root_states || !dof_state || k <= 0 ||
+      k > p->num_envs) {
+    g_err = "gt_anymal_reset_observe: invalid arguments (AnymalTerrain plane resets, k > 0)";
+    return -1;
+  }
+  // torch.rand(n) plans on the generator stream (gymtask.TorchRandPlanner.plan_many's arithmetic)
+  uint64_t off = *offset;
+  auto plan = [&](uint64_t n) {
+    const uint64_t blocks = (n + 255) / 256;
+    const uint32_t threads = (uint32_t)(256 * (blocks < grid_cap ? blocks : grid_cap));
+    const gt_torch_rand_plan pl{seed, off, threads, (uint32_t)n};
+    off += ((n - 1) / (4 * (uint64_t)threads) + 1) * 4;
+    return pl;
+  };
+  const uint64_t kn = (uint64_t)k * p->num_dofs;
+  d->u_pos = d->u_vel = d->u_cmd_x = d->u_cmd_y = d->u_cmd_h = nullptr;
+  d->plan_pos = plan(kn);
+  d->plan_vel = plan(kn);
+  d->plan_cmd_x = plan((uint64_t)k);
+  d->plan_cmd_y = plan((uint64_t)k);
+  d->plan_cmd_h = plan((uint64_t)k);
+  if (gt_anymal_reset_flagged(p, b, k, d, nullptr, env_ids_out, episode_out, episode_length_s, scratch, stream))
+    return -1;
+  if (set_state(set_state_ctx, root_states, dof_state, env_ids_out, k, stream)) {
+    g_err = "gt_anymal_reset_observe: the set_state callback failed";
+    return -1;
+  }
+  gt_torch_rand_plan noise{};
+  if (add_noise) noise = plan((uint64_t)p->num_envs * p->num_obs);
+  if (gt_anymal_post_physics_b(p, b, nullptr, add_noise ? &noise : nullptr, stream)) return -1;
+  *offset = off;
+  return 0;
+}
+
 int gt_measure_heights(const int16_t* samples, int rows, int cols, float border, float hs, float vs,
                        const float* root_states, const float* points, int num_envs, int num_points, float* heights,
                        void* stream) {

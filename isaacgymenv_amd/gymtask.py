@@ -130,6 +130,13 @@ class GtAntResetArgs(C.Structure):
 _lib = None
 
 
+def _anymal_set_reset_state():
+    """AnymalTerrain._set_reset_state (the one-call root + dof indexed set that gt_anymal_reset_observe replaces by
+    its C callback); a task that overrides it keeps the Python sequence."""
+    from isaacgymenv_amd.isaacgymenvs.tasks.anymal_terrain import AnymalTerrain
+    return AnymalTerrain._set_reset_state
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -153,7 +160,10 @@ def lib():
                                                 vp],
                            "gt_ant_post_physics": [C.POINTER(GtAntParams), C.POINTER(GtAntBuffers), vp],
                            "gt_ant_reset_flagged": [C.POINTER(GtAntParams), C.POINTER(GtAntBuffers), i,
-                                                    C.POINTER(GtAntResetArgs), vp]}.items():
+                                                    C.POINTER(GtAntResetArgs), vp],
+                           "gt_anymal_reset_observe": [P, B, i, C.POINTER(GtAnymalResetDraws), vp, vp, C.c_float, vp,
+                                                       C.c_uint64, C.POINTER(C.c_uint64), C.c_uint32, i, vp, vp, vp,
+                                                       vp, vp]}.items():
             fn = getattr(L, name)
             fn.restype = C.c_int
             fn.argtypes = args
@@ -166,7 +176,7 @@ def lib():
 EXPORTED_SYMBOLS = ["gt_abi_version", "gt_last_error", "gt_anymal_post_physics_a", "gt_anymal_reset",
                     "gt_anymal_post_physics_b", "gt_anymal_reset_flagged", "gt_torch_rand", "gt_host_alloc",
                     "gt_host_free", "gt_wait_host_seq", "gt_measure_heights", "gt_hound_control",
-                    "gt_ant_post_physics", "gt_ant_reset_flagged"]
+                    "gt_ant_post_physics", "gt_ant_reset_flagged", "gt_anymal_reset_observe"]
 
 
 class AntTailKernel:
@@ -640,6 +650,55 @@ class AnymalTailKernels:
         self._pending_extras = (ep, tr is not None)
         if not defer_extras:
             self.finish_reset()
+
+    def reset_observe_applies(self) -> bool:
+        """The reset step's sequence can be one C call (gt_anymal_reset_observe): plane AnymalTerrain, in-kernel
+        draws, fused observation outputs, and a sim whose indexed sets libgymsim does itself."""
+        t = self.task
+        return (self.inkernel_rng and not self.hound and not t.custom_origins and getattr(t, "_heights_dev", None) is None
+                and not t.dr_randomizations.get("observations", None) and hasattr(t.sim, "handle")
+                and type(t)._set_reset_state is _anymal_set_reset_state())
+
+    def reset_observe(self, k: int):
+        """reset_flagged(k) + observe() of a reset step in one host call (gymtask ABI 5, gt_anymal_reset_observe:
+        the reset draws' plans, k_reset_flagged, gymsim's one-launch root / dof indexed sets through a C callback,
+        k_post_b with the noise plan); the generator ends where the Python sequence leaves it.  extras["episode"] is
+        left pending for finish_reset()."""
+        t = self.task
+        dev = t.device
+        d = self._draws
+        if d is None:
+            d = self._draws = GtAnymalResetDraws()
+            for name, (lo, hi) in (("pos", (0.5, 1.5)), ("vel", (-0.1, 0.1)), ("cmd_x", t.command_x_range),
+                                   ("cmd_y", t.command_y_range), ("cmd_h", t.command_yaw_range)):
+                setattr(d, name + "_range", float(hi - lo))
+                setattr(d, name + "_lower", float(lo))
+        ids_buf = self._ids_buf
+        if ids_buf is None or ids_buf.numel() < t.num_envs:
+            ids_buf = self._ids_buf = torch.empty(t.num_envs, dtype=torch.int32, device=dev)
+        ids = ids_buf[:k]
+        ep = torch.empty(len(self.TERMS) + 1, dtype=torch.float32, device=dev)
+        obs = torch.empty_like(t.obs_buf)
+        time_outs = torch.empty(t.num_envs, dtype=torch.bool, device=dev)
+        b = self._buffers(check=False)
+        b.obs_out, b.time_outs, b.clip_obs = obs.data_ptr(), time_outs.data_ptr(), float(t.clip_obs)
+        cb = self._set_state_cb
+        if cb is None:
+            from isaacgymenv_amd.isaacgym import _lib as gs
+            cb = self._set_state_cb = C.cast(gs.lib().gs_sim_set_root_and_dof, C.c_void_p).value
+        g = self.planner.gen
+        off = C.c_uint64(g.get_offset())
+        _check(lib().gt_anymal_reset_observe(self.p, b, k, d, ids.data_ptr(), ep.data_ptr(),
+                                             float(t.max_episode_length_s), self.reset_scratch.data_ptr(),
+                                             g.initial_seed(), C.byref(off), self.planner.grid_cap, int(bool(t.add_noise)),
+                                             cb, t.sim.handle, t.root_states.data_ptr(), t.dof_state.data_ptr(),
+                                             self._stream()), "gt_anymal_reset_observe")
+        g.set_offset(off.value)
+        t._fused_outputs = (time_outs, obs)
+        self._keep = (ids, ep)
+        self._pending_extras = (ep, False)
+
+    _set_state_cb = None
 
     def finish_reset(self):
         """extras["episode"] of the last reset_flagged(defer_extras=True); a no-op when none is pending."""

@@ -489,8 +489,11 @@ class AnymalTerrain(VecTask):
                 k = kern.last_reset_count
                 if snap is not None:
                     kern.rng_restore(snap)
-                kern.reset_flagged(k, torch_rand_unit, defer_extras=True)  # reset_idx without nonzero / host sync
-                kern.observe()
+                if kern.reset_observe_applies():  # the two below as one host call (gymtask ABI 5)
+                    kern.reset_observe(k)
+                else:
+                    kern.reset_flagged(k, torch_rand_unit, defer_extras=True)  # reset_idx without nonzero / host sync
+                    kern.observe()
                 kern.finish_reset()  # extras["episode"], built while the GPU runs the observation kernel
             return
         self.progress_buf += 1
