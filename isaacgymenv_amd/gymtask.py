@@ -653,7 +653,19 @@ class AnymalTailKernels:
 
     def reset_observe_applies(self) -> bool:
         """The reset step's sequence can be one C call (gt_anymal_reset_observe): plane AnymalTerrain, in-kernel
-        draws, fused observation outputs, and a sim whose indexed sets libgymsim does itself."""
+        draws, fused observation outputs, and a sim whose indexed sets libgymsim does itself.  (The task-level
+        conditions are fixed after construction and cached; inkernel_rng and the observation DR are re-read.)"""
+        t = self.task
+        if not self.inkernel_rng or t.dr_randomizations.get("observations", None):
+            return False
+        ok = self._ro_ok
+        if ok is None:
+            ok = self._ro_ok = self._reset_observe_static()
+        return ok
+
+    _ro_ok = None
+
+    def _reset_observe_static(self) -> bool:
         t = self.task
         return (self.inkernel_rng and not self.hound and not t.custom_origins and getattr(t, "_heights_dev", None) is None
                 and not t.dr_randomizations.get("observations", None) and hasattr(t.sim, "handle")
@@ -677,9 +689,12 @@ class AnymalTailKernels:
         if ids_buf is None or ids_buf.numel() < t.num_envs:
             ids_buf = self._ids_buf = torch.empty(t.num_envs, dtype=torch.int32, device=dev)
         ids = ids_buf[:k]
-        ep = torch.empty(len(self.TERMS) + 1, dtype=torch.float32, device=dev)
-        obs = torch.empty_like(t.obs_buf)
-        time_outs = torch.empty(t.num_envs, dtype=torch.bool, device=dev)
+        # fresh outputs (extras["episode"], the observations, time_outs): allocated after the previous reset's call,
+        # off the host path between the count and this one
+        nxt = self._ro_next
+        if nxt is None or nxt[1].shape != t.obs_buf.shape:
+            nxt = self._ro_alloc()
+        ep, obs, time_outs = nxt
         b = self._buffers(check=False)
         b.obs_out, b.time_outs, b.clip_obs = obs.data_ptr(), time_outs.data_ptr(), float(t.clip_obs)
         cb = self._set_state_cb
@@ -697,8 +712,15 @@ class AnymalTailKernels:
         t._fused_outputs = (time_outs, obs)
         self._keep = (ids, ep)
         self._pending_extras = (ep, False)
+        self._ro_next = self._ro_alloc()
+
+    def _ro_alloc(self):
+        t = self.task
+        return (torch.empty(len(self.TERMS) + 1, dtype=torch.float32, device=t.device), torch.empty_like(t.obs_buf),
+                torch.empty(t.num_envs, dtype=torch.bool, device=t.device))
 
     _set_state_cb = None
+    _ro_next = None
 
     def finish_reset(self):
         """extras["episode"] of the last reset_flagged(defer_extras=True); a no-op when none is pending."""
