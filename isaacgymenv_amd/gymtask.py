@@ -130,6 +130,91 @@ class GtAntResetArgs(C.Structure):
 _lib = None
 
 
+class EpisodeExtras(dict):
+    """extras["episode"] of a fused reset (anymal_terrain.py:416-421): {"rew_<term>": 0-d tensor, ...,
+    "terrain_level": 0-d tensor}, the same keys, order and values as the dict of fresh torch.mean results the
+    reference builds -- held as the reset's own fresh device buffer and split into its 0-d tensors when first read
+    (splitting 14 views costs ~10-20 us of host time on every reset step, and a learner that never reads the meters,
+    like the PPO rollout, never pays it).  Every read path of a dict materialises first, the C-level ones included
+    (dict(x) / {**x} / copy go through the overridden __iter__ / keys)."""
+
+    __slots__ = ("_src",)
+
+    def __init__(self, keys, ep, terrain_level=None):
+        super().__init__()
+        self._src = (keys, ep, terrain_level)
+
+    def _m(self):
+        src = self._src
+        if src is not None:
+            self._src = None
+            keys, ep, lvl = src
+            n = len(keys)
+            dict.update(self, zip(keys, ep[:n].unbind()))
+            dict.__setitem__(self, "terrain_level", ep[n] if lvl is None else lvl)
+        return self
+
+    def __getitem__(self, k):
+        return dict.__getitem__(self._m(), k)
+
+    def __iter__(self):
+        return dict.__iter__(self._m())
+
+    def __len__(self):
+        return dict.__len__(self._m())
+
+    def __contains__(self, k):
+        return dict.__contains__(self._m(), k)
+
+    def __repr__(self):
+        return dict.__repr__(self._m())
+
+    def __eq__(self, other):
+        return dict.__eq__(self._m(), other)
+
+    def __reduce__(self):
+        return (dict, (dict(self._m().items()),))
+
+    def get(self, k, default=None):
+        return dict.get(self._m(), k, default)
+
+    def keys(self):
+        return dict.keys(self._m())
+
+    def values(self):
+        return dict.values(self._m())
+
+    def items(self):
+        return dict.items(self._m())
+
+    def copy(self):
+        return dict(self._m().items())
+
+    def pop(self, *a):
+        return dict.pop(self._m(), *a)
+
+    def popitem(self):
+        return dict.popitem(self._m())
+
+    def setdefault(self, *a):
+        return dict.setdefault(self._m(), *a)
+
+    def update(self, *a, **k):
+        return dict.update(self._m(), *a, **k)
+
+    def __setitem__(self, k, v):
+        dict.__setitem__(self._m(), k, v)
+
+    def __delitem__(self, k):
+        dict.__delitem__(self._m(), k)
+
+    def clear(self):
+        self._src = None
+        dict.clear(self)
+
+    __hash__ = None
+
+
 def _anymal_set_reset_state():
     """AnymalTerrain._set_reset_state (the one-call root + dof indexed set that gt_anymal_reset_observe replaces by
     its C callback); a task that overrides it keeps the Python sequence."""
@@ -729,13 +814,13 @@ class AnymalTailKernels:
             return
         ep, has_terrain = pend
         t = self.task
-        t.extras["episode"] = dict(zip(self._ep_keys, ep[:len(self.TERMS)].unbind()))
         if has_terrain:
-            t.extras["episode"]["terrain_level"] = ep[len(self.TERMS)]
+            last = None
         else:
             if self._terrain_level is None:
                 self._terrain_level = torch.mean(t.terrain_levels.float())
-            t.extras["episode"]["terrain_level"] = self._terrain_level
+            last = self._terrain_level
+        t.extras["episode"] = EpisodeExtras(self._ep_keys, ep, last)
 
     def _terrain_reset(self):
         """gt_anymal_terrain_reset over the task's curriculum tensors (rebuilt when the task rebinds one)."""
