@@ -196,6 +196,16 @@ int gt_anymal_reset_observe(const gt_anymal_params *p, const gt_anymal_buffers *
                             gt_set_state_fn set_state, void *set_state_ctx, const float *root_states,
                             const float *dof_state, void *stream);
 
+/* ABI 5: gt_wait_host_seq, then -- when the count is > 0 -- gt_anymal_reset_observe with it, so the reset's first
+ * launch follows the count with no caller code in between; *count receives the count either way (*offset is only
+ * advanced when it is > 0). */
+int gt_anymal_wait_reset_observe(const int32_t *words, int32_t seq, int32_t timeout_ms, int32_t *count,
+                                 const gt_anymal_params *p, const gt_anymal_buffers *b, gt_anymal_reset_draws *draws,
+                                 int32_t *env_ids_out, float *episode_out, float episode_length_s, void *scratch,
+                                 uint64_t seed, uint64_t *offset, uint32_t grid_cap, int add_noise,
+                                 gt_set_state_fn set_state, void *set_state_ctx, const float *root_states,
+                                 const float *dof_state, void *stream);
+
 /* Pinned, device-mapped, coherent host memory for host_count (hipHostMalloc). */
 int gt_host_alloc(uint64_t bytes, void **host_ptr, void **device_ptr);
 int gt_host_free(void *host_ptr);

@@ -662,4 +662,16 @@ int gt_wait_host_seq(const int32_t* words, int32_t seq, int32_t timeout_ms, int3
   }
 }
 
+int gt_anymal_wait_reset_observe(const int32_t* words, int32_t seq, int32_t timeout_ms, int32_t* count,
+                                 const gt_anymal_params* p, const gt_anymal_buffers* b, gt_anymal_reset_draws* d,
+                                 int32_t* env_ids_out, float* episode_out, float episode_length_s, void* scratch,
+                                 uint64_t seed, uint64_t* offset, uint32_t grid_cap, int add_noise,
+                                 gt_set_state_fn set_state, void* set_state_ctx, const float* root_states,
+                                 const float* dof_state, void* stream) {
+  if (!count || gt_wait_host_seq(words, seq, timeout_ms, count)) return -1;
+  if (*count <= 0) return 0;
+  return gt_anymal_reset_observe(p, b, *count, d, env_ids_out, episode_out, episode_length_s, scratch, seed, offset,
+                                 grid_cap, add_noise, set_state, set_state_ctx, root_states, dof_state, stream);
+}
+
 }  // extern "C"

@@ -248,7 +248,11 @@ def lib():
                                                     C.POINTER(GtAntResetArgs), vp],
                            "gt_anymal_reset_observe": [P, B, i, C.POINTER(GtAnymalResetDraws), vp, vp, C.c_float, vp,
                                                        C.c_uint64, C.POINTER(C.c_uint64), C.c_uint32, i, vp, vp, vp,
-                                                       vp, vp]}.items():
+                                                       vp, vp],
+                           "gt_anymal_wait_reset_observe": [vp, C.c_int32, C.c_int32, C.POINTER(C.c_int32), P, B,
+                                                            C.POINTER(GtAnymalResetDraws), vp, vp, C.c_float, vp,
+                                                            C.c_uint64, C.POINTER(C.c_uint64), C.c_uint32, i, vp, vp,
+                                                            vp, vp, vp]}.items():
             fn = getattr(L, name)
             fn.restype = C.c_int
             fn.argtypes = args
@@ -261,7 +265,8 @@ def lib():
 EXPORTED_SYMBOLS = ["gt_abi_version", "gt_last_error", "gt_anymal_post_physics_a", "gt_anymal_reset",
                     "gt_anymal_post_physics_b", "gt_anymal_reset_flagged", "gt_torch_rand", "gt_host_alloc",
                     "gt_host_free", "gt_wait_host_seq", "gt_measure_heights", "gt_hound_control",
-                    "gt_ant_post_physics", "gt_ant_reset_flagged", "gt_anymal_reset_observe"]
+                    "gt_ant_post_physics", "gt_ant_reset_flagged", "gt_anymal_reset_observe",
+                    "gt_anymal_wait_reset_observe"]
 
 
 class AntTailKernel:
@@ -761,8 +766,29 @@ class AnymalTailKernels:
         the reset draws' plans, k_reset_flagged, gymsim's one-launch root / dof indexed sets through a C callback,
         k_post_b with the noise plan); the generator ends where the Python sequence leaves it.  extras["episode"] is
         left pending for finish_reset()."""
+        args, off, outs = self._ro_prepare()
+        _check(lib().gt_anymal_reset_observe(self.p, args[0], k, *args[1:]), "gt_anymal_reset_observe")
+        self._ro_done(off, outs)
+
+    def wait_reset_observe(self, snap) -> int:
+        """wait_reset_count() and, when the count is > 0, reset_observe(count) in the same C call (the reset's first
+        launch follows the count with no Python in between).  snap: rng_snapshot() taken before the optimistic
+        observation (None: the generator has not moved since).  Returns the count; a reset's extras["episode"] is
+        left pending for finish_reset()."""
+        # the reset draws start where the optimistic noise did (the rolled-back offset); with no reset the generator
+        # stays after the optimistic draws
+        args, off, outs = self._ro_prepare(None if snap is None else snap[0])
+        cnt = self._count_out
+        rc = lib().gt_anymal_wait_reset_observe(self._host_words, self._seq, self.WAIT_TIMEOUT_MS, C.byref(cnt),
+                                                self.p, *args)
+        _check(rc, "gt_anymal_wait_reset_observe")
+        k = self.last_reset_count = int(cnt.value)
+        if k > 0:
+            self._ro_done(off, outs)
+        return k
+
+    def _ro_prepare(self, start_offset=None):
         t = self.task
-        dev = t.device
         d = self._draws
         if d is None:
             d = self._draws = GtAnymalResetDraws()
@@ -772,13 +798,12 @@ class AnymalTailKernels:
                 setattr(d, name + "_lower", float(lo))
         ids_buf = self._ids_buf
         if ids_buf is None or ids_buf.numel() < t.num_envs:
-            ids_buf = self._ids_buf = torch.empty(t.num_envs, dtype=torch.int32, device=dev)
-        ids = ids_buf[:k]
+            ids_buf = self._ids_buf = torch.empty(t.num_envs, dtype=torch.int32, device=t.device)
         # fresh outputs (extras["episode"], the observations, time_outs): allocated after the previous reset's call,
         # off the host path between the count and this one
         nxt = self._ro_next
         if nxt is None or nxt[1].shape != t.obs_buf.shape:
-            nxt = self._ro_alloc()
+            nxt = self._ro_next = self._ro_alloc()
         ep, obs, time_outs = nxt
         b = self._buffers(check=False)
         b.obs_out, b.time_outs, b.clip_obs = obs.data_ptr(), time_outs.data_ptr(), float(t.clip_obs)
@@ -787,15 +812,19 @@ class AnymalTailKernels:
             from isaacgymenv_amd.isaacgym import _lib as gs
             cb = self._set_state_cb = C.cast(gs.lib().gs_sim_set_root_and_dof, C.c_void_p).value
         g = self.planner.gen
-        off = C.c_uint64(g.get_offset())
-        _check(lib().gt_anymal_reset_observe(self.p, b, k, d, ids.data_ptr(), ep.data_ptr(),
-                                             float(t.max_episode_length_s), self.reset_scratch.data_ptr(),
-                                             g.initial_seed(), C.byref(off), self.planner.grid_cap, int(bool(t.add_noise)),
-                                             cb, t.sim.handle, t.root_states.data_ptr(), t.dof_state.data_ptr(),
-                                             self._stream()), "gt_anymal_reset_observe")
-        g.set_offset(off.value)
+        off = C.c_uint64(g.get_offset() if start_offset is None else start_offset)
+        args = (b, self._draws, ids_buf.data_ptr(), ep.data_ptr(), float(t.max_episode_length_s),
+                self.reset_scratch.data_ptr(), g.initial_seed(), C.byref(off), self.planner.grid_cap,
+                int(bool(t.add_noise)), cb, t.sim.handle, t.root_states.data_ptr(), t.dof_state.data_ptr(),
+                self._stream())
+        return args, off, nxt
+
+    def _ro_done(self, off, outs):
+        t = self.task
+        ep, obs, time_outs = outs
+        self.planner.gen.set_offset(off.value)
         t._fused_outputs = (time_outs, obs)
-        self._keep = (ids, ep)
+        self._keep = (self._ids_buf, ep)
         self._pending_extras = (ep, False)
         self._ro_next = self._ro_alloc()
 

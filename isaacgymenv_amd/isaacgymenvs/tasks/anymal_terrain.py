@@ -485,15 +485,17 @@ class AnymalTerrain(VecTask):
             # reset_idx: the draws, their order and the results are the reference's either way.
             snap = kern.rng_snapshot() if self.add_noise else None
             kern.observe()
+            if kern.reset_observe_applies():
+                # the count, and on a reset step the whole reset + observation sequence, in one C call
+                if kern.wait_reset_observe(snap) > 0:
+                    kern.finish_reset()
+                return
             if kern.wait_reset_count() > 0:
                 k = kern.last_reset_count
                 if snap is not None:
                     kern.rng_restore(snap)
-                if kern.reset_observe_applies():  # the two below as one host call (gymtask ABI 5)
-                    kern.reset_observe(k)
-                else:
-                    kern.reset_flagged(k, torch_rand_unit, defer_extras=True)  # reset_idx without nonzero / host sync
-                    kern.observe()
+                kern.reset_flagged(k, torch_rand_unit, defer_extras=True)  # reset_idx without nonzero / host sync
+                kern.observe()
                 kern.finish_reset()  # extras["episode"], built while the GPU runs the observation kernel
             return
         self.progress_buf += 1
