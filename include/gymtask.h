@@ -94,6 +94,8 @@ typedef struct gt_anymal_buffers {
     const float *measured_heights; /* [N][140] terrain heights under the probes
                                     (gt_measure_heights), or NULL: plane terrain, heights 0 */
     const struct gt_anymal_hound *hound; /* NULL for AnymalTerrain; UsefulHound's differences (ABI 3) */
+    float *obs_mirror;           /* ABI 5: [N][num_obs] or NULL: a second copy of what obs_out receives (a
+                                    learner's static act-forward input: no copy launch per step); needs obs_out */
 } gt_anymal_buffers;
 
 /* UsefulHound (reference tasks/useful_hound.py) runs the same tail with these differences

