@@ -112,11 +112,14 @@ class Linear(nn.Linear):
         return super().forward(x)
 
 
+_SPLITK_WG = int(os.environ.get("RL_SPLITK_WG", "256"))  # (A/B switch: the workgroup target below)
+
+
 def _splits(M: int, tiles: int) -> int:
     """Row blocks of the weight-gradient partials: enough workgroups for the 256 CUs (>= 256 with the layer's
     128 x 128 output tiles), each block a multiple of 128 rows."""
     s = 1
-    while s * tiles < 256 and M % (2 * s * 128) == 0:
+    while s * tiles < _SPLITK_WG and M % (2 * s * 128) == 0:
         s *= 2
     return s
 
