@@ -112,12 +112,16 @@ class Linear(nn.Linear):
         return super().forward(x)
 
 
-_SPLITK_WG = int(os.environ.get("RL_SPLITK_WG", "256"))  # (A/B switch: the workgroup target below)
+# the target below (RL_SPLITK_WG, an A/B switch): 128 measured best for AnymalTerrainPPO's grouped layers, whose
+# launches run the actor and critic groups side by side (2 x 128 workgroups): update 10.45-10.52 ms per epoch at
+# 256, 9.81-9.96 at 128, 11.4 at 64 and 512 (fewer row blocks: fewer f32 partials to write and finish; too few:
+# idle CUs) -- profiles/r06x_splitk_sweep.txt
+_SPLITK_WG = int(os.environ.get("RL_SPLITK_WG", "128"))
 
 
 def _splits(M: int, tiles: int) -> int:
-    """Row blocks of the weight-gradient partials: enough workgroups for the 256 CUs (>= 256 with the layer's
-    128 x 128 output tiles), each block a multiple of 128 rows."""
+    """Row blocks of the weight-gradient partials: enough workgroups to cover the CUs with the layer's 128 x 128
+    output tiles (_SPLITK_WG per group), each block a multiple of 128 rows."""
     s = 1
     while s * tiles < _SPLITK_WG and M % (2 * s * 128) == 0:
         s *= 2
