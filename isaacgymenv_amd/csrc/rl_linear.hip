@@ -21,6 +21,8 @@
 // (tests/test_ppo_gpu.py test_linear_kernels_exact_on_integers pins them with exact integer data.)
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -639,7 +641,9 @@ extern "C" int rl_linear_fwd_g(const void* x, int32_t M, int32_t K, int32_t ldx,
   const auto* B = static_cast<const _Float16*>(bias);
   auto* Y = static_cast<_Float16*>(y);
   // 128 x 128 tiles when that still gives >= 256 workgroups (over all groups), else 64-row tiles
-  if ((M / 128) * (N / 128) * G >= 256 && M % 128 == 0) {
+  // (RL_NT_WG: that workgroup threshold, an A/B switch)
+  static const int nt_wg = getenv("RL_NT_WG") ? atoi(getenv("RL_NT_WG")) : 256;
+  if ((M / 128) * (N / 128) * G >= nt_wg && M % 128 == 0) {
     const int MT = M / 128, NT = N / 128;
     const dim3 g(MT * NT * G);
     if (act) hipLaunchKernelGGL((k_gemm_nt<128, 128, true>), g, dim3(kThreads), 0, st, X, ldx, W, K, B, Y, ldy, K, gx, gw, gb, gy, MT, NT);
@@ -721,7 +725,8 @@ extern "C" int rl_linear_bwd_g(const void* dy, const void* y, int32_t M, int32_t
       return rl_set_error("rl_linear_bwd: dX needs W, 8-byte aligned rows and K % 128");
     const auto* Wp = static_cast<const _Float16*>(w);
     auto* DX = static_cast<_Float16*>(dx);
-    if ((M / 128) * (K / 128) * G >= 256)
+    static const int nn_wg = getenv("RL_NN_WG") ? atoi(getenv("RL_NN_WG")) : 256;  // (A/B switch)
+    if ((M / 128) * (K / 128) * G >= nn_wg)
       hipLaunchKernelGGL((k_gemm_nn<128>), dim3((M / 128) * (K / 128) * G), dim3(kThreads), 0, st, DY, Yv, N, ldy, Wp,
                          K, DX, lddx, gy, gw, gdx, M / 128, K / 128);
     else
