@@ -61,6 +61,9 @@ struct TerrainDev {
 #ifndef GS_TERR_PLANES
 #define GS_TERR_PLANES 1
 #endif
+#ifndef GS_TERR_ROWBATCH
+#define GS_TERR_ROWBATCH 8  // cell words of a row loaded together in the scan (A/B builds: 4, 16)
+#endif
 
 // footprint flags of a cell: its triangles reach one cell further towards -x, +x, -y, +y
 #define TCELL_XLO 1u
@@ -296,7 +299,7 @@ GS_HD bool sphere_contact_scan(const TerrainDev& T, const float* p, float r, flo
   //     words are loaded together before any is tested (one load latency per row, not one per cell).
   const float marg = pad + 0.01f * T.hs;
   const float kscale = 1.f + 1e-5f;  // the key test on the widest footprint, safely on the skipping side
-  constexpr int kRowBatch = 8;
+  constexpr int kRowBatch = GS_TERR_ROWBATCH;
   for (int i = i0; i <= i1; ++i) {
     const float cx0 = T.x0 + (float)i * T.hs;
     const float wx0 = cx0 - T.hs - marg, wx1 = cx0 + 2.f * T.hs + marg;
