@@ -153,7 +153,10 @@ __device__ __forceinline__ void pair_records(const DevModel* __restrict__ M, con
 // several waves per SIMD to hide the narrowphase's load latency, which the solver kernel (512 VGPR, scratch,
 // 3 waves per CU) cannot.  Two waves per SIMD (<= 256 VGPR): unbounded, the 4 publishing lanes' link poses (the
 // forward kinematics of shape_world) took the kernel to 383 VGPR + AGPR, one wave per SIMD.
-constexpr int kPairEnvs = 2;
+#ifndef GS_PAIR_ENVS
+#define GS_PAIR_ENVS 2  // (A/B builds: 1)
+#endif
+constexpr int kPairEnvs = GS_PAIR_ENVS;
 template <class T>
 __global__ __launch_bounds__(kTerrWave, 2) void k_pair_records(const DevModel* __restrict__ M, DevParams P, SimBuffers B) {
   __shared__ float shw[kShW * T::NS * kPairEnvs];
