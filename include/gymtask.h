@@ -198,6 +198,13 @@ int gt_anymal_reset_observe(const gt_anymal_params *p, const gt_anymal_buffers *
                             gt_set_state_fn set_state, void *set_state_ctx, const float *root_states,
                             const float *dof_state, void *stream);
 
+/* ABI 5: gt_anymal_post_physics_a + gt_anymal_post_physics_b (noise_plan or none) in one launch, for
+ * AnymalTerrain on the plane (num_dofs 12, no measured heights, post_a's 16-byte aligned dof rows): each
+ * workgroup runs part A for its 16 envs, then their observations; the count and the reset masks are published
+ * exactly as post_physics_a publishes them. */
+int gt_anymal_post_physics_ab(const gt_anymal_params *p, const gt_anymal_buffers *b,
+                              const gt_torch_rand_plan *noise_plan, void *stream);
+
 /* ABI 5: gt_wait_host_seq, then -- when the count is > 0 -- gt_anymal_reset_observe with it, so the reset's first
  * launch follows the count with no caller code in between; *count receives the count either way (*offset is only
  * advanced when it is > 0). */

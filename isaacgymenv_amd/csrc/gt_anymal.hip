@@ -295,12 +295,10 @@ __global__ void __launch_bounds__(64) k_reset_flagged(gt_anymal_params p, gt_any
 // Each lane selects its source address and scale first and then issues ONE load, so the
 // ragged segments of the obs row do not serialise into one memory round trip per segment.
 template <int NOISE, bool HOUND>  // NOISE: 0 none, 1 drawn buffer, 2 in-kernel torch.rand stream
-__global__ void __launch_bounds__(256) k_post_b(gt_anymal_params p, gt_anymal_buffers b, gt_anymal_hound h,
-                                                const float* __restrict__ noise, gt_torch_rand_plan plan) {
-  const int e = blockIdx.x;
-  const int k = threadIdx.x;
+__device__ __forceinline__ void post_b_elem(const gt_anymal_params& p, const gt_anymal_buffers& b,
+                                            const gt_anymal_hound& h, const float* __restrict__ noise,
+                                            const gt_torch_rand_plan& plan, const int e, const int k) {
   const int no = p.num_obs;
-  if (k >= no) return;
   const int nd = p.num_dofs;
   const int na = HOUND ? h.num_actions : nd;    // actions width, dof_state row width
   const int ne = HOUND ? 10 : 0;                // end-effector position, quaternion, arm command
@@ -362,6 +360,47 @@ __global__ void __launch_bounds__(256) k_post_b(gt_anymal_params p, gt_anymal_bu
   if (k == 0 && b.time_outs) b.time_outs[e] = (prog >= p.max_episode_length - 1) && (rst != 0);
   if (k < na) b.last_actions[(size_t)e * na + k] = la;
   if (k < nd) b.last_dof_vel[(size_t)e * nd + k] = lq;
+}
+
+template <int NOISE, bool HOUND>
+__global__ void __launch_bounds__(256) k_post_b(gt_anymal_params p, gt_anymal_buffers b, gt_anymal_hound h,
+                                                const float* __restrict__ noise, gt_torch_rand_plan plan) {
+  const int k = threadIdx.x;
+  if (k < p.num_obs) post_b_elem<NOISE, HOUND>(p, b, h, noise, plan, blockIdx.x, k);
+}
+
+// post_a + post_b in one launch (gt_anymal_post_physics_ab; AnymalTerrain, 12 dofs, plane): a workgroup of 256
+// lanes takes 16 envs; lanes 0-15 run post_a_env for them (the same source as k_post_a), publish their 16 done bits
+// as a slice of the 64-env mask word and join the grid's count, then -- after a workgroup barrier, so post_a's
+// stores of these envs are visible -- all 256 lanes run the 16 x num_obs observation elements (k_post_b's body).
+// Each workgroup moves on to its observations as soon as its own envs' part A is done, without a launch boundary
+// and without waiting for the rest of the grid.
+constexpr int kAbEnvs = 16;
+// (called, not inlined, in k_post_ab's element loop: inlining it there crashes this compiler's loop passes)
+template <int NOISE>
+__device__ __attribute__((noinline)) void post_b_elem_call(const gt_anymal_params& p, const gt_anymal_buffers& b,
+                                                           const float* __restrict__ noise,
+                                                           const gt_torch_rand_plan& plan, const int e, const int k) {
+  post_b_elem<NOISE, false>(p, b, gt_anymal_hound{}, noise, plan, e, k);
+}
+template <int NOISE>
+__global__ void __launch_bounds__(256) k_post_ab(gt_anymal_params p, gt_anymal_buffers b,
+                                                 const float* __restrict__ noise, gt_torch_rand_plan plan) {
+  const gt_anymal_hound h{};
+  const int tid = threadIdx.x, e0 = blockIdx.x * kAbEnvs, N = p.num_envs;
+  bool reset = false;
+  if (tid < kAbEnvs && e0 + tid < N) reset = post_a_env<true, false, 12>(p, b, h, e0 + tid);
+  const unsigned long long m = __ballot(reset);  // (wave 0: lanes 0-15 hold the envs)
+  if (tid == 0) {
+    uint16_t* slices = reinterpret_cast<uint16_t*>(b.reset_masks);
+    slices[e0 / kAbEnvs] = (uint16_t)(m & 0xffffull);
+    if (e0 + kAbEnvs >= N)  // the last workgroup clears its mask word's slices past the last env
+      for (int q = e0 / kAbEnvs + 1; q % 4 != 0; ++q) slices[q] = 0;
+    publish_count(b, (unsigned)__popcll(m & 0xffffull), gridDim.x);
+  }
+  __syncthreads();
+  const int no = p.num_obs, ne = (N - e0 < kAbEnvs ? N - e0 : kAbEnvs);
+  for (int i = tid; i < ne * no; i += blockDim.x) post_b_elem_call<NOISE>(p, b, noise, plan, e0 + i / no, i % no);
 }
 
 // get_heights, one lane per (env, probe).  The statement order follows the reference's torch
@@ -485,6 +524,29 @@ int gt_anymal_reset(const gt_anymal_params* p, const gt_anymal_buffers* b, const
                      cmd_x, cmd_y, cmd_heading);
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail("gt_anymal_reset", e);
+}
+
+int gt_anymal_post_physics_ab(const gt_anymal_params* p, const gt_anymal_buffers* b,
+                              const gt_torch_rand_plan* noise_plan, void* stream) {
+  if (check_params(p, b)) return -1;
+  auto aligned = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
+  if (b->hound || p->num_dofs != 12 || !b->reset_count || !b->reset_masks || b->measured_heights ||
+      !aligned(b->torques) || !aligned(b->actions) || !aligned(b->last_actions) || !aligned(b->last_dof_vel) ||
+      !aligned(b->dof_state)) {
+    g_err = "gt_anymal_post_physics_ab: AnymalTerrain plane, 12 dofs, 16-byte aligned dof rows, reset_count and "
+            "reset_masks required";
+    return -1;
+  }
+  if (noise_plan && ((uint64_t)noise_plan->numel != (uint64_t)p->num_envs * p->num_obs || noise_plan->threads == 0)) {
+    g_err = "gt_anymal_post_physics_ab: noise plan does not cover obs_buf";
+    return -1;
+  }
+  const dim3 g((p->num_envs + kAbEnvs - 1) / kAbEnvs), bl(256);
+  const gt_torch_rand_plan pl = noise_plan ? *noise_plan : gt_torch_rand_plan{};
+  if (noise_plan) hipLaunchKernelGGL((k_post_ab<2>), g, bl, 0, (hipStream_t)stream, *p, *b, nullptr, pl);
+  else hipLaunchKernelGGL((k_post_ab<0>), g, bl, 0, (hipStream_t)stream, *p, *b, nullptr, pl);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : fail("gt_anymal_post_physics_ab", e);
 }
 
 int gt_anymal_post_physics_b(const gt_anymal_params* p, const gt_anymal_buffers* b, const float* noise,

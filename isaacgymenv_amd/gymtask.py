@@ -233,6 +233,7 @@ def lib():
         for name, args in {"gt_anymal_post_physics_a": [P, B, vp],
                            "gt_anymal_reset": [P, B, vp, i, vp, vp, vp, vp, vp, vp, vp],
                            "gt_anymal_post_physics_b": [P, B, vp, C.POINTER(GtTorchRandPlan), vp],
+                           "gt_anymal_post_physics_ab": [P, B, C.POINTER(GtTorchRandPlan), vp],
                            "gt_torch_rand": [C.POINTER(GtTorchRandPlan), vp, vp],
                            "gt_anymal_reset_flagged": [P, B, i, C.POINTER(GtAnymalResetDraws),
                                                        C.POINTER(GtAnymalTerrainReset), vp, vp, C.c_float, vp, vp],
@@ -265,7 +266,7 @@ def lib():
 EXPORTED_SYMBOLS = ["gt_abi_version", "gt_last_error", "gt_anymal_post_physics_a", "gt_anymal_reset",
                     "gt_anymal_post_physics_b", "gt_anymal_reset_flagged", "gt_torch_rand", "gt_host_alloc",
                     "gt_host_free", "gt_wait_host_seq", "gt_measure_heights", "gt_hound_control",
-                    "gt_ant_post_physics", "gt_ant_reset_flagged", "gt_anymal_reset_observe",
+                    "gt_ant_post_physics", "gt_ant_reset_flagged", "gt_anymal_reset_observe", "gt_anymal_post_physics_ab",
                     "gt_anymal_wait_reset_observe"]
 
 
@@ -599,6 +600,42 @@ class AnymalTailKernels:
 
     _tail_ok = None
     _ids_buf = None
+
+    def post_ab_applies(self) -> bool:
+        """post_a and the (optimistic) observations can be one launch (gt_anymal_post_physics_ab): AnymalTerrain on
+        the plane, 12 dofs, in-kernel noise draws (or none), fused observation outputs, post_a's vector rows.
+        GT_POST_AB=0 keeps the two launches (A/B runs)."""
+        ok = self._ab_ok
+        if ok is None:
+            t = self.task
+            ok = self._ab_ok = (os.environ.get("GT_POST_AB", "1") != "0" and not self.hound and self.nd == 12
+                                and getattr(t, "_heights_dev", None) is None)
+        t = self.task
+        return (ok and (self.inkernel_rng or not t.add_noise) and not t.dr_randomizations.get("observations", None)
+                and t.torques.is_contiguous() and t.actions.is_contiguous())
+
+    _ab_ok = None
+
+    def post_ab(self):
+        """post_a() + observe() as one launch (gymtask ABI 5): the counters, termination, reward, the reset count
+        and masks, then the observations with their noise, time_outs and the clamped copy."""
+        t = self.task
+        b = self._buffers()
+        if any(x % 16 for x in (b.torques, b.actions, b.last_actions, b.last_dof_vel, b.dof_state)):
+            self.post_a()
+            self.observe()
+            return
+        self._seq = (self._seq + 1) & 0x7FFFFFFF
+        b.seq = self._seq
+        plan = self.planner.plan(t.obs_buf.numel()) if t.add_noise else None
+        obs = torch.empty_like(t.obs_buf)
+        time_outs = torch.empty(t.num_envs, dtype=torch.bool, device=t.device)
+        b.obs_out, b.time_outs, b.clip_obs = obs.data_ptr(), time_outs.data_ptr(), float(t.clip_obs)
+        b.obs_mirror = self._mirror_ptr
+        _check(lib().gt_anymal_post_physics_ab(self.p, b, plan, self._stream()), "gt_anymal_post_physics_ab")
+        t.reset_buf = self.reset_bool
+        t._fused_outputs = (time_outs, obs)
+        t._obs_mirrored = obs if self._mirror_ptr else None
 
     def num_resets(self) -> int:
         """Envs the last post_a flagged for reset, read back through the stream (synchronising)."""

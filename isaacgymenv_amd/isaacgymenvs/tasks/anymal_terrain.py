@@ -486,16 +486,21 @@ class AnymalTerrain(VecTask):
             if push:
                 self.push_robots()
             kern = self._kernels
-            if self._tail_fused:  # post_a ran in the physics launch (fused_physics_step)
-                kern.after_fused_tail()
-            else:
-                kern.post_a()  # counters, base quantities, heading command, termination, reward
-            self._tail_fused = False
             # Optimistic: most steps reset nobody, so draw the noise and build the observations before
             # the host knows the count.  On a reset step, roll the RNG back and redo both after
             # reset_idx: the draws, their order and the results are the reference's either way.
-            snap = kern.rng_snapshot() if self.add_noise else None
-            kern.observe()
+            if self._tail_fused:  # post_a ran in the physics launch (fused_physics_step)
+                kern.after_fused_tail()
+                snap = kern.rng_snapshot() if self.add_noise else None
+                kern.observe()
+            elif kern.post_ab_applies():  # post_a + the observations in one launch (gymtask ABI 5)
+                snap = kern.rng_snapshot() if self.add_noise else None
+                kern.post_ab()
+            else:
+                kern.post_a()  # counters, base quantities, heading command, termination, reward
+                snap = kern.rng_snapshot() if self.add_noise else None
+                kern.observe()
+            self._tail_fused = False
             if kern.reset_observe_applies():
                 # the count, and on a reset step the whole reset + observation sequence, in one C call
                 if kern.wait_reset_observe(snap) > 0:

@@ -338,3 +338,45 @@ def test_obs_mirror_holds_every_returned_observation(monkeypatch):
     env.amd_set_obs_mirror(None)
     obs, _, _, _ = env.step(torch.zeros((n, 12), device="cuda:0"))
     assert env._obs_mirrored is None
+
+
+def test_post_ab_launch_is_bit_identical_to_post_a_then_post_b(monkeypatch):
+    """gt_anymal_post_physics_ab (post_a and the optimistic observations in one launch, 16 envs per workgroup)
+    against the separate k_post_a + k_post_b launches from the same state, over 12 steps of 5-step episodes with a
+    push step: every output bit-identical (the same sources, gt_anymal_tail.h and k_post_b's element body)."""
+    n = 256
+    env = _make("AnymalTerrain", n, monkeypatch, **{"task.env.learn.episodeLength_s": 0.1})
+    gen = torch.Generator(device="cuda:0").manual_seed(21)
+    acts = [2 * torch.rand((n, 12), device="cuda:0", generator=gen) - 1 for _ in range(12)]
+    env.step(acts[0])
+    env.common_step_counter = env.push_interval - 6
+    snap = _snapshot(env)
+    kernels = env._kernels
+    out = {}
+    for mode in ("ab", "separate"):
+        _restore(env, snap)
+        kernels._ab_ok = None if mode == "ab" else False
+        assert kernels.post_ab_applies() == (mode == "ab")
+        env.extras.pop("episode", None)
+        res = []
+        for a in acts:
+            obs, rew, reset, extras = env.step(a)
+            ep = extras.get("episode")
+            res.append([obs["obs"].clone(), rew.clone(), reset.clone(), extras["time_outs"].clone(),
+                        None if ep is None else torch.stack([torch.as_tensor(v, device="cuda:0").float()
+                                                             for v in ep.values()]),
+                        env.root_states.clone(), env.progress_buf.clone(), env.commands.clone(),
+                        env.feet_air_time.clone(), torch.stack([v.clone() for v in env.episode_sums.values()]),
+                        env.last_actions.clone(), env.last_dof_vel.clone(), kernels.reset_masks.clone(),
+                        kernels.reset_count.clone()])
+            env.extras.pop("episode", None)
+        out[mode] = res
+    kernels._ab_ok = None
+    n_reset_steps = 0
+    for t, (a, b) in enumerate(zip(out["ab"], out["separate"])):
+        n_reset_steps += int(bool(a[2].any()))
+        for k, (x, y) in enumerate(zip(a, b)):
+            assert (x is None) == (y is None), (t, k)
+            if x is not None:
+                assert torch.equal(x, y), f"step {t} output {k}"
+    assert n_reset_steps >= 2
