@@ -604,11 +604,13 @@ class AnymalTailKernels:
     def post_ab_applies(self) -> bool:
         """post_a and the (optimistic) observations can be one launch (gt_anymal_post_physics_ab): AnymalTerrain on
         the plane, 12 dofs, in-kernel noise draws (or none), fused observation outputs, post_a's vector rows.
-        GT_POST_AB=0 keeps the two launches (A/B runs)."""
+        Opt-in (GT_POST_AB=1): measured slower than the two launches -- 0.170 vs 0.131 ms per headline step
+        (profiles/r06zd_post_ab_ab.txt): the element loop must call k_post_b's body out of line (inlining it in a
+        loop crashes this compiler), and the call's by-reference structs cost ~570 B of scratch per lane."""
         ok = self._ab_ok
         if ok is None:
             t = self.task
-            ok = self._ab_ok = (os.environ.get("GT_POST_AB", "1") != "0" and not self.hound and self.nd == 12
+            ok = self._ab_ok = (os.environ.get("GT_POST_AB", "0") == "1" and not self.hound and self.nd == 12
                                 and getattr(t, "_heights_dev", None) is None)
         t = self.task
         return (ok and (self.inkernel_rng or not t.add_noise) and not t.dr_randomizations.get("observations", None)

@@ -345,6 +345,7 @@ def test_post_ab_launch_is_bit_identical_to_post_a_then_post_b(monkeypatch):
     against the separate k_post_a + k_post_b launches from the same state, over 12 steps of 5-step episodes with a
     push step: every output bit-identical (the same sources, gt_anymal_tail.h and k_post_b's element body)."""
     n = 256
+    monkeypatch.setenv("GT_POST_AB", "1")  # (opt-in: measured slower, gymtask.post_ab_applies)
     env = _make("AnymalTerrain", n, monkeypatch, **{"task.env.learn.episodeLength_s": 0.1})
     gen = torch.Generator(device="cuda:0").manual_seed(21)
     acts = [2 * torch.rand((n, 12), device="cuda:0", generator=gen) - 1 for _ in range(12)]
